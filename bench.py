@@ -1,0 +1,231 @@
+"""bench.py -- end-to-end calculate_VDP throughput on MI355X (BASELINE.json metric).
+
+One step = the whole Vent_Analysis.calculate_VDP hot path (N4 with SimpleITK defaults -> sorted
+masked list -> numpy-order mean anchor -> threshold + 3x3 median + border -> 99th-pct linear
+binning -> k-means -> SNR -> scalars, plus the cohort histogram) over one batch of synthetic
+128x128x24 studies already resident in HBM.  N GPUs = N processes (torchrun), each with its own
+batch (weak scaling, no data-path collective); the cohort histogram is all-reduced over RCCL once
+per step when N > 1.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 256]
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+METRIC = "volumes/sec end-to-end VDP, 128×128×24 Xe volume, 1 GPU and 8-GPU batch"
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+
+
+# ------------------------------------------------------------------------------------------------
+# CPU baseline: the oracle (numpy VDP chain + C N4 restatement) on a bounded sample, spawn pool
+# ------------------------------------------------------------------------------------------------
+def _cpu_one(args):
+    R, C, Z, seed = args
+    from oracle import native, vdp_oracle as O
+    from vent_analysis_amd.synth import synth_volume
+    X, M = synth_volume(R, C, Z, seed)
+    t = time.perf_counter()
+    n4, _, _ = native.n4(X, M)
+    O.calculate_vdp(n4, M, (1.5, 1.5, 10.0), HP=X)
+    return time.perf_counter() - t
+
+
+def cpu_baseline(R, C, Z, seconds=15.0, procs=16):
+    import multiprocessing as mp
+    from oracle import native
+    native.build()
+    procs = max(1, min(procs, os.cpu_count() or 1))
+    ctx = mp.get_context("spawn")
+    done = 0
+    busy = 0.0
+    with ctx.Pool(procs) as pool:
+        pool.map(_cpu_one, [(R, C, Z, 1000 + i) for i in range(procs)])   # warm imports
+        t0 = time.perf_counter()
+        seed = 0
+        while time.perf_counter() - t0 < seconds:
+            ts = pool.map(_cpu_one, [(R, C, Z, seed + i) for i in range(procs)])
+            seed += procs
+            done += len(ts)
+            busy += sum(ts)
+        wall = time.perf_counter() - t0
+    return {"value": done / wall, "unit": "volumes/s", "cores": procs, "kind": "port",
+            "sample": f"{done} synthetic {R}x{C}x{Z} volumes (oracle/n4_oracle.c N4 + "
+                      f"oracle/vdp_oracle.py chain), {procs} processes, {wall:.1f} s wall, "
+                      f"{busy / max(done, 1):.3f} s per volume per core"}
+
+
+# ------------------------------------------------------------------------------------------------
+# algorithmic bytes per kernel class (DESIGN.md "Roofline accounting")
+# ------------------------------------------------------------------------------------------------
+def algorithmic_bytes(name, hp, mk, res, R, C, Z):
+    """Total algorithmic HBM bytes moved by all launches of kernel class ``name`` in one step."""
+    V = R * C * Z
+    B = hp.shape[0]
+    m = mk.reshape(B, R, C * Z)
+    nz = m != 0
+    vm = nz.sum(axis=(1, 2)).astype(np.float64)                 # masked voxels
+    has = nz.any(axis=1)
+    lo = np.where(has, nz.argmax(axis=1), 0)
+    hi = np.where(has, R - 1 - nz[:, ::-1, :].argmax(axis=1), -1)
+    vr = np.maximum(hi - lo + 1, 0).sum(axis=1).astype(np.float64)   # voxels in column ranges
+    iters = np.array([sum(r.n4_iters[:4]) for r in res], np.float64)
+    if name == "n4_eval":        # read mask (range) + L0 + B_old, write B_new   at masked voxels
+        return float(np.sum(iters * (vr + 12.0 * vm)))
+    if name == "n4_fit":         # read mask (range) + L0 + B                    at masked voxels
+        return float(np.sum(iters * (vr + 8.0 * vm)))
+    if name == "n4_hist":
+        return float(np.sum(iters * (vr + 8.0 * vm)))
+    if name == "n4_final":       # read I, write N4HPvent                        every voxel
+        return float(B * 8.0 * V)
+    if name == "classify":       # read N4 + mask, write defect, border, LB      every voxel
+        return float(B * 8.0 * V)
+    if name == "sort":           # 4 LSD passes: read keys twice, write once     masked voxels
+        return float(np.sum(4 * 12.0 * vm))
+    if name == "gather":
+        return float(np.sum(vr * 5.0 + 4.0 * vm))
+    if name == "snr":
+        return float(B * 5.0 * V)
+    if name == "mask_stats":
+        return float(B * 1.0 * V)
+    return 0.0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--batch", type=int, default=256, help="volumes per GPU")
+    ap.add_argument("--shape", type=int, nargs=3, default=(128, 128, 24))
+    ap.add_argument("--no-n4", action="store_true", help="VDP chain only (N4 := identity)")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-profile", action="store_true", help="no HIP events in the timed region")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    R, C, Z = args.shape
+    nb = args.batch
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(R, C, Z, seconds=args.cpu_seconds)   # before any GPU initialisation
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    from vent_analysis_amd import _lib
+    from vent_analysis_amd.synth import synth_batch
+
+    hp, mk = synth_batch(R, C, Z, nb, base_seed=1000 * rank, unique=16)
+    Bt = _lib.Batch(R, C, Z, nb, device=local)
+    Bt.upload(hp, mk)
+    if world > 1:
+        uid = [_lib.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        _lib.comm_init(world, rank, uid[0], device=local)
+    vox = (1.5, 1.5, 10.0)
+    opts = Bt.options(do_n4=not args.no_n4, vox=vox, do_cohort=True,
+                      profile=not args.no_profile)
+    warm = Bt.options(do_n4=not args.no_n4, vox=vox, do_cohort=True, profile=False)
+
+    def step(o):
+        Bt.run(o)
+        if world > 1:
+            Bt.cohort_allreduce()
+        Bt.sync()
+
+    try:
+        import torch
+        sync_dev = torch.cuda.synchronize if torch.cuda.is_available() else (lambda: None)
+    except Exception:   # torch is plumbing only; the library syncs its own stream
+        sync_dev = lambda: None  # noqa: E731
+
+    for _ in range(args.warmup):
+        step(warm)
+    if dist:
+        dist.barrier()
+    sync_dev()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(opts)
+    sync_dev()
+    if dist:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        import torch
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    _, _, _, _, res = Bt.download(n4=False, maps=False)
+    kernels = {}
+    if not args.no_profile:
+        for name in _lib.lib().vh_batch_kernel_names().decode().split(";"):
+            ms, n, _ = Bt.kernel_time(name)
+            if n:
+                kernels[name] = {"ms_total": ms, "launches": n,
+                                 "alg_bytes": algorithmic_bytes(name, hp, mk, res, R, C, Z) * args.steps}
+    roof = None
+    if kernels:
+        dom = max(kernels, key=lambda k: kernels[k]["ms_total"])
+        k = kernels[dom]
+        avg_ms = k["ms_total"] / k["launches"]
+        bpl = k["alg_bytes"] / k["launches"]
+        ach = bpl / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+        roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                "avg_launch_us": round(avg_ms * 1e3, 2), "alg_bytes_per_launch": bpl,
+                "kernel_ms_per_step": {n: round(v["ms_total"] / args.steps, 3)
+                                       for n, v in sorted(kernels.items(),
+                                                          key=lambda kv: -kv[1]["ms_total"])}}
+    its = np.array([list(r.n4_iters[:4]) for r in res])
+    total = world * nb * args.steps
+    line = {
+        "metric": METRIC,
+        "value": round(total / dt, 2),
+        "unit": "volumes/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic",
+        "config": {"workload": f"batch of {nb} synthetic {R}x{C}x{Z} Xe volumes per GPU, "
+                               "end-to-end calculate_VDP: N4 (SimpleITK defaults 4x50 it) + "
+                               "mean-anchored + linear-binning + k-means VDP + defect border + "
+                               "SNR + cohort histogram" + (" (N4 skipped)" if args.no_n4 else ""),
+                   "volumes_per_gpu": nb, "shape": [R, C, Z],
+                   "parallelism": f"dp{world}",
+                   "n4_iterations_mean": float(its.sum(axis=1).mean()) if its.size else 0.0},
+        "roofline": roof,
+        "cpu_baseline": cpu,
+    }
+    if rank == 0:
+        print(json.dumps(line))
+    Bt.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,151 @@
+/* vent_hip.h -- C-ABI of libventhip.so, the MI355X (gfx950) implementation of the Vent_Analysis
+ * voxel hot path (N4 -> mean-anchored / linear-binning / k-means VDP -> defect morphology -> CI).
+ *
+ * Plain C types only (no torch, no HIP types).  Every function returns an int status (VH_OK = 0)
+ * and never throws across the boundary; vh_last_error() gives the message of the last failure on
+ * a context.  Host buffers are caller-allocated and C-contiguous in numpy's (rows, cols, slices)
+ * order (slice axis fastest, as Vent_Analysis.openSingleDICOM produces, Vent_Analysis.py:179);
+ * device buffers are owned by the library.  A context is bound to one GPU and one HIP stream and
+ * is re-entrant per context (one context per thread/GPU).
+ *
+ * Reference interface each entry point replaces (file:line in thomenr/Vent_Analysis):
+ *   vh_n4        Vent_Analysis.N4_bias_correction            Vent_Analysis.py:316-334
+ *   vh_snr       Vent_Analysis.calculate_SNR                 Vent_Analysis.py:337-357
+ *   vh_border    Vent_Analysis.calculateBorder               Vent_Analysis.py:225-231
+ *   vh_vdp       Vent_Analysis.calculate_VDP (post-N4 part)  Vent_Analysis.py:239-263
+ *   vh_ci        CI.calculate_CI + Vent_Analysis.calculate_CI CI.py:107-145, Vent_Analysis.py:265-271
+ *   vh_batch_*   the same pipeline over a device-resident batch of studies (build-defined)
+ *   vh_comm_*    cohort histogram all-reduce over RCCL (build-defined, BASELINE config 4)
+ */
+#ifndef VENT_HIP_H
+#define VENT_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VH_ABI_VERSION 1
+
+/* status codes */
+#define VH_OK 0
+#define VH_ERR_ARG 1          /* bad argument (maps to ValueError/TypeError in the shim) */
+#define VH_ERR_HIP 2          /* HIP runtime failure */
+#define VH_ERR_NOMEM 3        /* device allocation failed */
+#define VH_ERR_MAXRADIUS 4    /* CI: sphere reached the table's last radius (CI.py:101-103, ValueError) */
+#define VH_ERR_EMPTY 5        /* empty mask / defect list (Vent_Analysis.py:270 IndexError) */
+#define VH_ERR_RCCL 6         /* RCCL failure */
+#define VH_ERR_NODEV 7        /* no GPU visible */
+
+typedef struct vh_ctx vh_ctx;
+typedef struct vh_batch vh_batch;
+
+/* N4 parameters; vh_n4_default_params() fills the SimpleITK 2.3.1 defaults the reference runs with
+ * (Vent_Analysis.py:330: no setter is called).  ncp is given per numpy axis (rows, cols, slices). */
+typedef struct {
+    int32_t n_levels;        /* 4  = len(MaximumNumberOfIterations) */
+    int32_t max_iters[8];    /* 50, 50, 50, 50 */
+    float conv_threshold;    /* 0.001 */
+    int32_t ncp[3];          /* 4, 4, 4 control points per axis at level 0 */
+    int32_t spline_order;    /* 3 (only 3 supported) */
+    int32_t n_bins;          /* 200 histogram bins (<= 256) */
+    float wiener_noise;      /* 0.01 */
+    float fwhm;              /* 0.15 bias-field FWHM */
+} vh_n4_params;
+
+/* Per-volume scalars of calculate_VDP / calculate_CI (metadata keys of Vent_Analysis.py:78-103). */
+typedef struct {
+    double vdp;              /* metadata['VDP']        100*sum(defect)/sum(mask)            :251 */
+    double vdp_lb;           /* metadata['VDP_lb']     100*count(LB in {1,2})/sum(mask)     :257 */
+    double vdp_km;           /* metadata['VDP_km']     build-defined 1-D k-means (k=4)       :259-261 */
+    double defect_volume;    /* metadata['DefectVolume'] litres                              :252 */
+    double lung_volume;      /* metadata['LungVolume']   litres                              :166 */
+    double km_centres[4];
+    double snr;              /* metadata['SNR'] (double accumulation; the shim casts to HPvent's
+                                float dtype like numpy)                                      :241 */
+    float mean_anchor;       /* np.mean(sorted masked N4) (float32, numpy reduction order)  :246 */
+    float p99;               /* sorted[int(0.99 n)]                                          :255 */
+    int64_t n_mask;          /* voxels with mask > 0 */
+    int64_t n_defect;
+    int64_t n_lb12;
+    int64_t n_km0;
+    int32_t n4_iters[8];     /* N4 iterations executed per level (0 when N4 skipped) */
+    float n4_conv[8];        /* last convergence measure per level */
+} vh_vdp_result;
+
+/* Options for vh_batch_run. */
+typedef struct {
+    int32_t do_n4;           /* 1: N4 on HPvent (calculate_VDP);  0: N4 := identity (HPvent) */
+    vh_n4_params n4;
+    float thresh;            /* mean-anchored threshold (calculate_VDP thresh=0.6) */
+    int32_t do_snr;
+    int32_t do_kmeans;
+    int32_t do_cohort;       /* accumulate the cohort histogram (1024 u64 bins, [0,1.5) of p99-normalised masked N4) */
+    int32_t profile;         /* 1: time kernel classes with HIP events (vh_batch_kernel_time) */
+    double vox[3];           /* voxel size (mm) for the volume scalars */
+} vh_run_opts;
+
+#define VH_COHORT_BINS 1024
+
+/* ---- library / context ---------------------------------------------------------------------- */
+int vh_abi_version(void);
+const char *vh_status_string(int status);
+int vh_device_count(int *n);
+void vh_n4_default_params(vh_n4_params *p);
+void vh_default_run_opts(vh_run_opts *o);
+int vh_create(int device, vh_ctx **out);
+int vh_destroy(vh_ctx *ctx);
+const char *vh_last_error(const vh_ctx *ctx);
+int vh_synchronize(vh_ctx *ctx);
+
+/* ---- host-buffer entry points (one call = upload, compute, download) --------------------------
+ * hp: float32, mask: uint8 0/1, shapes [batch][R][C][Z]. */
+int vh_n4(vh_ctx *ctx, const float *hp, const uint8_t *mask, int64_t R, int64_t C, int64_t Z,
+          int64_t batch, const vh_n4_params *prm, float *out, int32_t *iters /* [batch][n_levels] */,
+          float *conv /* [batch][n_levels], nullable */);
+int vh_border(vh_ctx *ctx, const uint8_t *a, int64_t R, int64_t C, int64_t Z, int64_t batch,
+              uint8_t *border);
+int vh_snr(vh_ctx *ctx, const float *hp, const uint8_t *mask, int64_t R, int64_t C, int64_t Z,
+           int64_t batch, double *snr);
+/* calculate_VDP after N4.  hp may be NULL (no SNR).  Outputs: defect / defect_border / lb uint8
+ * volumes (any may be NULL), res[batch]. */
+int vh_vdp(vh_ctx *ctx, const float *hp, const float *n4, const uint8_t *mask, int64_t R,
+           int64_t C, int64_t Z, int64_t batch, float thresh, const double vox[3],
+           uint8_t *defect, uint8_t *defect_border, uint8_t *lb, vh_vdp_result *res);
+/* Cluster index map.  The sphere table comes from the host (reference-identical rows; see
+ * vent_analysis_amd/sphere.py): offs int16 [rows][3] (dx,dy,dz), dup uint8 [rows], bounds int32
+ * [nb] prefix lengths, radii float64 [nb] (= r[b-1]).  Outputs: ci_array float64 volume,
+ * ci_scalar[batch] (95th-percentile CV, Vent_Analysis.py:268-270), shell int32 volume (nullable). */
+int vh_ci(vh_ctx *ctx, const uint8_t *defect, int64_t R, int64_t C, int64_t Z, int64_t batch,
+          const int16_t *offs, const uint8_t *dup, int64_t rows, const int32_t *bounds,
+          const double *radii, int64_t nb, double minvox, double *ci_array, double *ci_scalar,
+          int32_t *shell);
+
+/* ---- device-resident batch pipeline ---------------------------------------------------------- */
+int vh_batch_create(vh_ctx *ctx, int64_t R, int64_t C, int64_t Z, int64_t batch, vh_batch **out);
+int vh_batch_destroy(vh_batch *b);
+int vh_batch_upload(vh_batch *b, const float *hp, const uint8_t *mask);
+int vh_batch_run(vh_batch *b, const vh_run_opts *opts);      /* enqueue; returns before the GPU ends */
+int vh_batch_sync(vh_batch *b);
+int vh_batch_download(vh_batch *b, float *n4, uint8_t *defect, uint8_t *defect_border, uint8_t *lb,
+                      vh_vdp_result *res /* [batch] */);
+int vh_batch_cohort_hist(vh_batch *b, uint64_t *hist /* [VH_COHORT_BINS] */);
+/* Kernel-class timing from HIP events on the context stream (opts.profile = 1).  name is one of
+ * the classes listed by vh_batch_kernel_names (';'-separated). */
+const char *vh_batch_kernel_names(void);
+int vh_batch_kernel_time(vh_batch *b, const char *name, double *total_ms, int64_t *launches,
+                         double *bytes_per_launch);
+
+/* ---- multi-GPU (RCCL over xGMI) -------------------------------------------------------------- */
+#define VH_COMM_ID_BYTES 128
+int vh_comm_unique_id(uint8_t id[VH_COMM_ID_BYTES]);
+int vh_comm_init(vh_ctx *ctx, int nranks, int rank, const uint8_t id[VH_COMM_ID_BYTES]);
+/* Sum the batch's device cohort histogram over all ranks of the context's communicator. */
+int vh_batch_cohort_allreduce(vh_batch *b);
+int vh_comm_destroy(vh_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VENT_HIP_H */

@@ -1,0 +1,208 @@
+"""GPU parity tests (MI355X): the HIP path through the C-ABI against the reference goldens and the
+CPU oracle.  Tolerances: masks / indices / counts bit-exact; VDP scalars exact (they are ratios of
+exact counts); SNR rel 1e-5; N4 rel 1e-5 (north_star), identical iteration counts."""
+import numpy as np
+import pytest
+
+from conftest import load_case, golden_files
+from oracle import native, vdp_oracle as O
+from vent_analysis_amd import _lib
+from vent_analysis_amd.sphere import compact_table, sphere_pix
+from vent_analysis_amd.synth import synth_volume, synth_batch
+
+pytestmark = pytest.mark.gpu
+
+GOLD = golden_files()
+
+
+def rel(a, b):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    return float(np.max(np.abs(a - b) / np.maximum(np.abs(b), 1e-30)))
+
+
+def test_library_runs_on_gpu():
+    assert _lib.device_count() >= 1
+    c = _lib.context(0)
+    assert c.h
+
+
+@pytest.mark.parametrize("path", GOLD, ids=lambda p: p.split("/")[-1])
+def test_vdp_chain_vs_reference(path):
+    X, M, vox, exp, _ = load_case(path)
+    d, bo, lb, res = _lib.vdp(X, M.astype(np.uint8), vox, hp=X)   # N4 = identity, as the goldens
+    r = res[0]
+    assert np.array_equal(d[0], exp["defect"])
+    assert np.array_equal(bo[0] == 1, exp["defect_border"])
+    assert np.array_equal(lb[0], exp["lb"])
+    assert np.float32(r.mean_anchor) == exp["mean_anchor"]
+    assert np.float32(r.p99) == exp["p99"]
+    assert 100 * np.float64(r.n_defect) / np.sum(M) == exp["VDP"]
+    assert 100 * np.float64(r.n_lb12) / np.sum(M) == exp["VDP_lb"]
+    assert r.n_defect * np.prod(np.divide(vox, 10)) / 1000 == exp["DefectVolume"]
+    assert r.defect_volume == pytest.approx(exp["DefectVolume"], rel=1e-15)
+    assert r.lung_volume == pytest.approx(exp["LungVolume"], rel=1e-15)
+    assert rel(np.float32(r.snr), exp["SNR"]) < 1e-5
+
+
+@pytest.mark.parametrize("path", GOLD, ids=lambda p: p.split("/")[-1])
+def test_mask_border_vs_reference(path):
+    X, M, vox, exp, _ = load_case(path)
+    assert np.array_equal(_lib.border(M.astype(np.uint8))[0], exp["mask_border"])
+
+
+def test_snr_vs_reference():
+    for path in GOLD:
+        X, M, vox, exp, _ = load_case(path)
+        s = _lib.snr(X, M.astype(np.uint8))[0]
+        assert rel(np.float32(s), exp["SNR"]) < 1e-5, path
+
+
+@pytest.mark.parametrize("path", [p for p in GOLD if "ci_values" in np.load(p)],
+                         ids=lambda p: p.split("/")[-1])
+def test_ci_vs_reference(path):
+    X, M, vox, exp, _ = load_case(path)
+    d = exp["defect"]
+    table = compact_table(sphere_pix(vox, 50), d.shape)
+    ci, sc, shell = _lib.ci(d, table, float(np.min(vox)))
+    assert np.array_equal(ci[0][d > 0], exp["ci_values"])
+    assert np.all(ci[0][d == 0] == 0)
+    assert sc[0] == exp["CI"]
+
+
+@pytest.mark.parametrize("shape,seed", [((40, 36, 9), 1), ((70, 90, 12), 2), ((130, 104, 8), 3)])
+def test_ci_vs_oracle_random_blobs(shape, seed):
+    """Edge-touching and small arrays (s0 or s1 <= 100 exercises the duplicate-offset uniquing of
+    np.intersect1d)."""
+    rng = np.random.default_rng(seed)
+    i, j, k = np.meshgrid(*[np.arange(s) for s in shape], indexing="ij")
+    d = np.zeros(shape, bool)
+    for _ in range(7):
+        c = [rng.uniform(-0.1, 1.1) * s for s in shape]
+        r = rng.uniform(3, 12)
+        d |= (i - c[0]) ** 2 + (j - c[1]) ** 2 + ((k - c[2]) * 3) ** 2 <= r * r
+    d &= rng.random(shape) > 0.15
+    vox = (1.5, 1.5, 10.0)
+    table = compact_table(sphere_pix(vox, 50), shape)
+    ref, _ = native.ci(d, table, vox)
+    ci, sc, _ = _lib.ci(d, table, 1.5)
+    assert np.array_equal(ci[0], ref)
+    assert sc[0] == O.ci_scalar(ref[d])
+
+
+def test_ci_errors():
+    """Empty defect map -> IndexError (Vent_Analysis.py:270 / CI.py:118); a sphere that never drops
+    below 50 % defect before the table's last radius -> ValueError (CI.py:101-103).  A radius-10
+    table keeps offsets unaliased in a 40x40x24 all-defect volume, so interior voxels never stop."""
+    table = compact_table(sphere_pix((1.5, 1.5, 10.0), 10), (40, 40, 24))
+    with pytest.raises(IndexError):
+        _lib.ci(np.zeros((40, 40, 24), np.uint8), table, 1.5)
+    with pytest.raises(ValueError):
+        _lib.ci(np.ones((40, 40, 24), np.uint8), table, 1.5)
+    with pytest.raises(ValueError):
+        native.ci(np.ones((40, 40, 24), np.uint8), table, (1.5, 1.5, 10.0))
+
+
+@pytest.mark.parametrize("shape,seed", [((64, 64, 16), 0), ((128, 128, 24), 0), ((96, 112, 20), 5)])
+def test_n4_vs_oracle(shape, seed):
+    X, M = synth_volume(*shape, seed)
+    ref, its_ref, conv_ref = native.n4(X, M)
+    out, its, conv = _lib.n4(X, M.astype(np.uint8))
+    assert list(its[0]) == list(its_ref)
+    assert np.all((its[0] >= 1) & (its[0] <= 50))
+    assert rel(out[0], ref) < 1e-5
+    assert np.allclose(conv[0], conv_ref, rtol=1e-4)
+
+
+def test_batch_pipeline_end_to_end():
+    """Full calculate_VDP on a batch (N4 on device -> VDP chain), per-volume against the oracle
+    applied to the GPU's N4 output (chain bit-exact) and the oracle N4 (tolerance)."""
+    hp, mk = synth_batch(128, 128, 24, 3, base_seed=10)
+    vox = (1.5, 1.5, 10.0)
+    B = _lib.Batch(128, 128, 24, 3)
+    B.upload(hp, mk)
+    B.run(B.options(do_n4=True, vox=vox, do_cohort=True))
+    n4, d, bo, lb, res = B.download(n4=True)
+    for b in range(3):
+        ref_n4, its_ref, _ = native.n4(hp[b], mk[b])
+        assert list(res[b].n4_iters[:4]) == list(its_ref)
+        assert rel(n4[b], ref_n4) < 1e-5
+        o = O.calculate_vdp(n4[b], mk[b].astype(np.float64), vox, HP=hp[b])
+        assert np.array_equal(d[b], o["defectArray"])
+        assert np.array_equal(bo[b] == 1, o["defectBorder"])
+        assert np.array_equal(lb[b], o["defectArrayLB"])
+        assert res[b].vdp == o["VDP"]
+        assert res[b].vdp_lb == o["VDP_lb"]
+        assert res[b].n_km0 * 100 / mk[b].sum() == pytest.approx(o["VDP_km"], abs=0)
+        assert rel(np.float32(res[b].snr), o["SNR"]) < 1e-5
+    # cohort histogram = sum of per-volume float32 histograms
+    h = B.cohort_hist()
+    exp = np.zeros(_lib.COHORT_BINS, np.uint64)
+    for b in range(3):
+        nv = (n4[b] / np.float32(res[b].p99)).astype(np.float32)[mk[b] > 0]
+        sel = (nv >= 0) & (nv < np.float32(1.5))
+        bi = np.minimum((nv[sel] * np.float32(_lib.COHORT_BINS / 1.5)).astype(np.int64), 1023)
+        exp += np.bincount(bi, minlength=_lib.COHORT_BINS).astype(np.uint64)
+    assert np.array_equal(h, exp)
+    B.close()
+
+
+def test_batch_equals_single():
+    hp, mk = synth_batch(64, 64, 16, 4, base_seed=3)
+    B = _lib.Batch(64, 64, 16, 4)
+    B.upload(hp, mk)
+    B.run(B.options(do_n4=True, vox=(2, 2, 11.5)))
+    n4, d, _, lb, res = B.download(n4=True)
+    B.close()
+    for b in range(4):
+        out, its, _ = _lib.n4(hp[b], mk[b])
+        assert np.array_equal(out[0], n4[b])
+        assert list(its[0]) == list(res[b].n4_iters[:4])
+
+
+def test_kmeans_vs_oracle():
+    for seed in range(3):
+        X, M = synth_volume(96, 96, 20, seed)
+        _, _, _, res = _lib.vdp(X, M.astype(np.uint8), (1.5, 1.5, 10.0))
+        sig = np.sort(X[M > 0])
+        counts, centres, _ = O.kmeans_1d_sorted(sig)
+        assert res[0].n_km0 == counts[0]
+        assert np.allclose(list(res[0].km_centres), centres, rtol=1e-12)
+
+
+def test_class_shim_matches_reference_goldens():
+    from vent_analysis_amd import Vent_Analysis
+    for path in GOLD:
+        X, M, vox, exp, name = load_case(path)
+        v = Vent_Analysis(xenon_array=X, mask_array=M, vox=vox)
+        assert np.array_equal(v.mask_border, exp["mask_border"])
+        v.N4_bias_correction = lambda H, Mk: H.astype(np.float32)   # as the goldens were made
+        v.calculate_VDP()
+        assert v.defectArray.dtype == np.float64 and v.defectArrayLB.dtype == np.float64
+        assert np.array_equal(v.defectArray, exp["defect"])
+        assert np.array_equal(v.defectBorder, exp["defect_border"])
+        assert np.array_equal(v.defectArrayLB, exp["lb"])
+        assert v.metadata["VDP"] == exp["VDP"]
+        assert v.metadata["VDP_lb"] == exp["VDP_lb"]
+        assert v.metadata["DefectVolume"] == exp["DefectVolume"]
+        assert v.metadata["LungVolume"] == exp["LungVolume"]
+        assert isinstance(v.metadata["SNR"], np.float32)
+        assert rel(v.metadata["SNR"], exp["SNR"]) < 1e-5
+        if "CI" in exp:
+            v.calculate_CI()
+            assert v.metadata["CI"] == exp["CI"]
+            assert np.array_equal(v.CIarray[exp["defect"] > 0], exp["ci_values"])
+
+
+def test_class_full_pipeline_with_n4():
+    from vent_analysis_amd import Vent_Analysis
+    X, M = synth_volume(128, 128, 24, 0)
+    v = Vent_Analysis(xenon_array=X, mask_array=M, vox=(1.5, 1.5, 10.0))
+    v.calculate_VDP()
+    ref, its, _ = native.n4(X, M)
+    assert v.N4HPvent.dtype == np.float32
+    assert rel(v.N4HPvent, ref) < 1e-5
+    o = O.calculate_vdp(v.N4HPvent, M, (1.5, 1.5, 10.0), HP=X)
+    assert v.metadata["VDP"] == o["VDP"]
+    n4b = v.N4_bias_correction(X, M)
+    assert np.array_equal(n4b, v.N4HPvent)

@@ -1,0 +1,305 @@
+"""Vent_Analysis -- drop-in for the reference class (Vent_Analysis.py:26-577), GPU hot path.
+
+Keeps the constructor keywords, method names, attribute names/dtypes and metadata keys the GUI
+reads (Vent_Analysis.py:724-781, 839-1004), so it can replace ``from Vent_Analysis import
+Vent_Analysis``.  The voxel work -- N4, SNR, the mean-anchored / linear-binning / k-means VDP
+chain, defect/mask borders and the cluster index -- runs in libventhip.so on an MI355X
+(include/vent_hip.h).  Host code only moves arrays, casts dtypes and fills the metadata dict.
+There is no CPU fallback: a missing library raises ImportError on first use.
+
+Additions (backward compatible): a ``vox=`` constructor keyword (the reference's array-only
+constructor crashes at Vent_Analysis.py:166 because vox is '' -- pass vox to avoid it) and
+``metadata['VDP_km']`` is now filled (the reference leaves it '', :259-261; build-defined k-means).
+"""
+from __future__ import annotations
+
+import os
+import pickle
+
+import numpy as np
+
+from . import CI
+from . import _lib
+
+__all__ = ["Vent_Analysis"]
+
+
+def _binary_u8(A, what):
+    a = np.asarray(A)
+    if a.dtype == np.uint8 and a.max(initial=0) <= 1:
+        return np.ascontiguousarray(a)
+    u8 = (a != 0).astype(np.uint8)
+    if not np.array_equal(u8, a):
+        raise ValueError(f"{what} must be binary (0/1); the GPU path implements the reference's "
+                         "behaviour for binary masks only")
+    return u8
+
+
+class Vent_Analysis:
+    """Complete VDP analysis: N4 bias correction, normalisation, defect maps, VDPs, CI.
+    See the reference docstring (Vent_Analysis.py:27-57) for the attribute list."""
+
+    def __init__(self, xenon_path=None, mask_path=None, proton_path=None, xenon_array=None,
+                 mask_array=None, proton_array=None, pickle_dict=None, pickle_path=None,
+                 vox=None, device=0):
+        self.version = '241007_vent'
+        self.device = device
+        self.proton = ''
+        self.N4HPvent = ''
+        self.defectArray = ''
+        self.CIarray = ''
+        self.vox = ''
+        self.ds = ''
+        self.twix = ''
+        self.raw_k = ''
+        self.raw_HPvent = ''
+        self.metadata = {'fileName': '', 'PatientName': '', 'PatientAge': '',
+                         'PatientBirthDate': '', 'PatientSex': '', 'Disease': '', 'StudyDate': '',
+                         'SeriesTime': '', 'DE': '', 'SNR': '', 'VDP': '', 'VDP_lb': '',
+                         'VDP_km': '', 'LungVolume': '', 'DefectVolume': '', 'CI': '',
+                         'FEV1': '', 'FVC': '', 'visit': '', 'IRB': '', 'treatment': '',
+                         'analysisUser': '', 'notes': ''}
+
+        if xenon_array is not None:
+            print(f'\033[34mXenon array provided: {xenon_array.shape}\033[37m')
+            self.HPvent = xenon_array
+        if xenon_path is not None:
+            try:
+                print('\033[34mXenon DICOM path provided. Opening DICOM...\033[37m')
+                self.ds, self.HPvent = self.openSingleDICOM(xenon_path)
+            except Exception:
+                print('\033[31mOpening Xenon DICOM failed...\033[37m')
+            try:
+                print('\033[34mPulling Xenon DICOM Header\033[37m')
+                self.pullDICOMHeader()
+            except Exception:
+                print('\033[31mPulling Xenon DICOM Header failed...\033[37m')
+        if mask_array is not None:
+            print(f'\033[34mMask array provided: {mask_array.shape}\033[37m')
+            self.mask = mask_array
+            self.mask_border = self.calculateBorder(self.mask)
+        if mask_path is not None:
+            try:
+                print('\033[34mLoading Mask and calculating border\033[37m')
+                _, self.mask = self.openDICOMfolder(mask_path)
+                self.mask_border = self.calculateBorder(self.mask)
+            except Exception:
+                print('\033[31mLoading Mask and calculating border failed...\033[37m')
+        if proton_array is not None:
+            print(f'\033[34mProton array provided: {proton_array.shape}\033[37m')
+            self.proton = proton_array
+        if proton_path is not None:
+            try:
+                print('\033[34mProton DICOM Path provided. Opening...\033[37m')
+                self.proton_ds, self.proton = self.openSingleDICOM(proton_path)
+            except Exception:
+                print('\033[31mOpening Proton DICOM failed...\033[37m')
+        if pickle_path is not None:
+            print(f'\033[34mPickle path provided: {pickle_path}. Loading...\033[37m')
+            try:
+                with open(pickle_path, 'rb') as file:
+                    pickle_dict = pickle.load(file)   # the user's own study pickle (:153-155)
+                print('\033[32mPickle file successfully loaded.\033[37m')
+            except Exception:
+                print('\033[31mOpening Pickle from path and building arrays failed...\033[37m')
+        if pickle_dict is not None:
+            self.unPickleMe(pickle_dict)
+        if vox is not None:
+            self.vox = [float(v) for v in vox]
+        self.metadata['LungVolume'] = np.sum(self.mask == 1) * np.prod(np.divide(self.vox, 10)) / 1000
+
+    # ---- DICOM ingest (next row; needs pydicom, absent in this image) --------
+    def openSingleDICOM(self, dicom_path):
+        import pydicom as dicom   # noqa: F401  (raises ImportError here like any missing module)
+        ds = dicom.dcmread(dicom_path)
+        arr = np.transpose(ds.pixel_array, (1, 2, 0))
+        print(f'\033[32mI opened a DICOM of shape {arr.shape}\033[37m')
+        return ds, arr
+
+    def openDICOMfolder(self, maskFolder):
+        import pydicom as dicom
+        files = [f for f in sorted(os.listdir(maskFolder)) if f.endswith('.dcm')]
+        ds = dicom.dcmread(os.path.join(maskFolder, files[0]))
+        mask = np.zeros((ds.pixel_array.shape[0], ds.pixel_array.shape[1], len(files)))
+        for k, f in enumerate(files):
+            ds = dicom.dcmread(os.path.join(maskFolder, f))
+            mask[:, :, k] = ds.pixel_array
+        print(f'\033[32mI built a mask of shape {mask.shape}\033[37m')
+        return ds, mask
+
+    def pullDICOMHeader(self):
+        for elem in ['PatientName', 'PatientAge', 'PatientBirthDate', 'PatientSize',
+                     'PatientWeight', 'PatientSex', 'StudyDate', 'StudyTime', 'SeriesTime']:
+            try:
+                self.metadata[elem] = self.ds[elem].value
+            except Exception:
+                self.metadata[elem] = ''
+        for k in range(100):
+            try:
+                self.vox = self.ds[0x5200, 0x9230][k]['PixelMeasuresSequence'][0].PixelSpacing
+                break
+            except Exception:
+                pass
+        self.vox = [float(self.vox[0]), float(self.vox[1]), float(self.ds.SpacingBetweenSlices)]
+        self.metadata['LungVolume'] = np.sum(self.mask == 1) * np.prod(np.divide(self.vox, 10)) / 1000
+
+    # ---- hot path ---------------------------------------------------------------------------
+    def calculateBorder(self, A):
+        """Vent_Analysis.py:225-231 on the GPU: per slice, np.gradient != 0 along rows or cols.
+        Returns float64 0/1.  Equality is all that matters, so any array with <= 256 distinct
+        values is exact (values are replaced by their rank)."""
+        a = np.asarray(A)
+        if a.dtype == np.bool_ or (a.size and a.min() >= 0 and a.max() <= 1 and np.all(a == np.round(a))):
+            u8 = np.ascontiguousarray(a, dtype=np.uint8)
+        else:
+            uniq, inv = np.unique(a, return_inverse=True)
+            if uniq.size > 256:
+                raise ValueError("calculateBorder: more than 256 distinct values")
+            u8 = inv.reshape(a.shape).astype(np.uint8)
+        return _lib.border(u8, device=self.device)[0].astype(np.float64)
+
+    def normalize(self, x):
+        if (np.max(x) - np.min(x)) == 0:
+            return x
+        return (x - np.min(x)) / (np.max(x) - np.min(x))
+
+    def _n4_overridden(self):
+        return 'N4_bias_correction' in self.__dict__
+
+    def calculate_VDP(self, thresh=0.6):
+        """Vent_Analysis.py:239-263 as one GPU pipeline: SNR, N4, sorted masked list -> numpy-order
+        mean anchor, threshold + 3x3 median + border, 99th-pct linear binning, k-means, volumes."""
+        mask_u8 = _binary_u8(self.mask, 'mask')
+        hp = np.asarray(self.HPvent)
+        vox = np.asarray(self.vox, dtype=np.float64)
+        if self._n4_overridden():
+            # a caller-supplied N4 (e.g. identity): GPU chain on its output
+            self.metadata['SNR'] = self.calculate_SNR(self.HPvent, self.mask)
+            self.N4HPvent = self.N4_bias_correction(self.HPvent, self.mask)
+            d, bo, lb, res = _lib.vdp(self.N4HPvent, mask_u8, vox, hp=None, thresh=thresh,
+                                      device=self.device)
+        else:
+            B = _lib.Batch(*hp.shape, 1, device=self.device)
+            try:
+                B.upload(hp.astype(np.float32)[None], mask_u8[None])
+                B.run(B.options(do_n4=True, thresh=thresh, vox=vox))
+                n4, d, bo, lb, res = B.download(n4=True)
+            finally:
+                B.close()
+            self.N4HPvent = n4[0]
+            self.metadata['SNR'] = self._snr_dtype(res[0].snr, hp)
+        r = res[0]
+        self.defectArray = d[0].astype(np.float64)
+        self.defectBorder = bo[0] == 1
+        self.metadata['VDP'] = 100 * np.float64(r.n_defect) / np.sum(self.mask)
+        self.metadata['DefectVolume'] = r.n_defect * np.prod(np.divide(self.vox, 10)) / 1000
+        self.defectArrayLB = lb[0].astype(np.float64) * np.asarray(self.mask)
+        self.metadata['VDP_lb'] = 100 * np.float64(r.n_lb12) / np.sum(self.mask)
+        self.metadata['VDP_km'] = 100 * np.float64(r.n_km0) / np.sum(self.mask)
+        self.n4_iterations = list(r.n4_iters)[:4]
+        print('\033[32mcalculate_VDP ran successfully\033[37m')
+
+    @staticmethod
+    def _snr_dtype(v, A):
+        dt = np.asarray(A).dtype
+        if dt == np.float32 or dt == np.float16:
+            return np.float32(v)
+        return np.float64(v)
+
+    def calculate_CI(self):
+        """Vent_Analysis.py:265-271: CIarray + 95th-percentile CI, one GPU pass."""
+        self.CIarray, ci = CI.calculate_CI_with_index(self.defectArray, self.vox, device=self.device)
+        self.metadata['CI'] = ci
+        print(f"Calculated CI: {self.metadata['CI']}")
+
+    def N4_bias_correction(self, HPvent, mask):
+        """Vent_Analysis.py:316-334: N4 with the SimpleITK 2.3.1 defaults, on the GPU.
+        Returns float32 like sitk.GetArrayFromImage."""
+        m = (np.asarray(mask) == 1).astype(np.uint8)
+        out, its, _ = _lib.n4(np.asarray(HPvent, dtype=np.float32), m, device=self.device)
+        self.n4_iterations = list(its[0])
+        return out[0]
+
+    def calculate_SNR(self, A, FOVbuffer=20, manualNoise=False):
+        """Vent_Analysis.py:337-357 on the GPU (noise box from self.mask, FOVbuffer forced to 20
+        like the reference).  Returns A's float dtype (float32 for float32 input)."""
+        if manualNoise:
+            raise UnboundLocalError("cannot access local variable 'noise' (manualNoise branch is "
+                                    "empty in the reference, Vent_Analysis.py:353-355)")
+        m = _binary_u8(self.mask, 'mask')
+        v = _lib.snr(np.asarray(A, dtype=np.float32), m, device=self.device)[0]
+        return self._snr_dtype(v, A)
+
+    # ---- persistence / export helpers (format compat, not voxel compute) ---------------------
+    def build4DdataArray(self):
+        """Vent_Analysis.py:292-313: Proton, HPvent, mask, N4HPvent, defectArray, CIarray."""
+        dataArray = np.zeros(tuple(self.HPvent.shape) + (6,), dtype=np.float32)
+        dataArray[:, :, :, 1] = self.HPvent
+        dataArray[:, :, :, 2] = self.mask
+        for ch, name in ((0, 'proton'), (3, 'N4HPvent'), (4, 'defectArray'), (5, 'CIarray')):
+            try:
+                dataArray[:, :, :, ch] = getattr(self, name)
+            except Exception:
+                print(f'\033[33m{name} does not exist and was not added to 4D array\033[37m')
+        return dataArray
+
+    def cropToData(self, A, border=0, borderSlices=False):
+        """Vent_Analysis.py:430-456."""
+        slices = [x for x in range(A.shape[2]) if np.sum(A[:, :, x]) > 0]
+        rows = [x for x in range(A.shape[0]) if np.sum(A[x, :, :]) > 0]
+        cols = [x for x in range(A.shape[1]) if np.sum(A[:, x, :]) > 0]
+        if borderSlices:
+            s0, s1 = max(slices[0] - border, 0), min(slices[-1] + border + 1, A.shape[2])
+        else:
+            s0, s1 = max(slices[0], 0), min(slices[-1] + 1, A.shape[2])
+        r0, r1 = max(rows[0] - border, 0), min(rows[-1] + border + 1, A.shape[0])
+        c0, c1 = max(cols[0] - border, 0), min(cols[-1] + border + 1, A.shape[1])
+        return (A[r0:r1, c0:c1, s0:s1], list(range(r0, r1)), list(range(c0, c1)),
+                list(range(s0, s1)))
+
+    def pickleMe(self, pickle_path='C:/PIRL/data/VentPickle.pkl'):
+        """Vent_Analysis.py:542-553: every picklable attribute into one dict."""
+        d = {}
+        for attr in vars(self):
+            try:
+                pickle.dumps(getattr(self, attr))
+                d[attr] = getattr(self, attr)
+            except (pickle.PicklingError, AttributeError, TypeError):
+                print(f"\033[31mSkipping non-picklable attribute: {attr}\033[37m")
+        with open(pickle_path, 'wb') as f:
+            pickle.dump(d, f)
+        print(f'\033[32mPickled dictionary saved to {pickle_path}\033[37m')
+
+    def unPickleMe(self, pickle_dict):
+        for attr, value in pickle_dict.items():
+            setattr(self, attr, value)
+
+    def exportNifti(self, *a, **k):
+        raise NotImplementedError("NIfTI export (Vent_Analysis.py:273-290) is outside the GPU hot "
+                                  "path (SURVEY §8f); use build4DdataArray() with nibabel")
+
+    def exportDICOM(self, *a, **k):
+        raise NotImplementedError("defect-overlay DICOM export (Vent_Analysis.py:381-428) is a "
+                                  "next row (SURVEY §8f rank 3)")
+
+    def screenShot(self, *a, **k):
+        raise NotImplementedError("montage rendering (Vent_Analysis.py:458-520) is a next row "
+                                  "(SURVEY §8f rank 3)")
+
+    def process_RAW(self, *a, **k):
+        raise NotImplementedError("TWIX recon (Vent_Analysis.py:522-540) is disabled in the "
+                                  "reference GUI (SURVEY §8f rank 4)")
+
+    def __repr__(self):
+        s = f'\033[35mVent_Analysis\033[37m class object version \033[94m{self.version}\033[37m\n'
+        for attr, value in vars(self).items():
+            if isinstance(value, np.ndarray):
+                s += f'\033[32m {attr}: \033[36m{value.shape} \033[37m\n'
+            elif isinstance(value, dict):
+                for a2, v2 in value.items():
+                    s += f'   \033[32m {a2}: \033[36m{v2} \033[37m\n'
+            elif isinstance(value, str) and value == '':
+                s += f'\033[31m {attr}: \033[37m\n'
+            else:
+                s += f'\033[32m {attr}: \033[36m{type(value)} \033[37m\n'
+        return s

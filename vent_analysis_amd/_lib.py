@@ -1,0 +1,356 @@
+"""ctypes binding of libventhip.so (include/vent_hip.h).
+
+The library is built in-tree (``python __graft_entry__.py`` / ``make -C vent_analysis_amd/csrc``)
+and MUST be present: there is no CPU fallback.  Every status code is mapped to the Python
+exception the reference raises at the same point (SURVEY.md §8b "Errors").
+"""
+from __future__ import annotations
+
+import ctypes as ct
+import os
+import threading
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libventhip.so")
+
+VH_OK, VH_ERR_ARG, VH_ERR_HIP, VH_ERR_NOMEM, VH_ERR_MAXRADIUS, VH_ERR_EMPTY, VH_ERR_RCCL, \
+    VH_ERR_NODEV = range(8)
+COHORT_BINS = 1024
+COMM_ID_BYTES = 128
+
+
+class N4Params(ct.Structure):
+    _fields_ = [("n_levels", ct.c_int32), ("max_iters", ct.c_int32 * 8),
+                ("conv_threshold", ct.c_float), ("ncp", ct.c_int32 * 3),
+                ("spline_order", ct.c_int32), ("n_bins", ct.c_int32),
+                ("wiener_noise", ct.c_float), ("fwhm", ct.c_float)]
+
+
+class VdpResult(ct.Structure):
+    _fields_ = [("vdp", ct.c_double), ("vdp_lb", ct.c_double), ("vdp_km", ct.c_double),
+                ("defect_volume", ct.c_double), ("lung_volume", ct.c_double),
+                ("km_centres", ct.c_double * 4), ("snr", ct.c_double),
+                ("mean_anchor", ct.c_float), ("p99", ct.c_float),
+                ("n_mask", ct.c_int64), ("n_defect", ct.c_int64), ("n_lb12", ct.c_int64),
+                ("n_km0", ct.c_int64), ("n4_iters", ct.c_int32 * 8), ("n4_conv", ct.c_float * 8)]
+
+
+class RunOpts(ct.Structure):
+    _fields_ = [("do_n4", ct.c_int32), ("n4", N4Params), ("thresh", ct.c_float),
+                ("do_snr", ct.c_int32), ("do_kmeans", ct.c_int32), ("do_cohort", ct.c_int32),
+                ("profile", ct.c_int32), ("vox", ct.c_double * 3)]
+
+
+class VentHipError(RuntimeError):
+    pass
+
+
+_P = ct.c_void_p
+_I64 = ct.c_int64
+_SIGS = {
+    "vh_abi_version": ([], ct.c_int),
+    "vh_status_string": ([ct.c_int], ct.c_char_p),
+    "vh_device_count": ([ct.POINTER(ct.c_int)], ct.c_int),
+    "vh_n4_default_params": ([ct.POINTER(N4Params)], None),
+    "vh_default_run_opts": ([ct.POINTER(RunOpts)], None),
+    "vh_create": ([ct.c_int, ct.POINTER(_P)], ct.c_int),
+    "vh_destroy": ([_P], ct.c_int),
+    "vh_last_error": ([_P], ct.c_char_p),
+    "vh_synchronize": ([_P], ct.c_int),
+    "vh_n4": ([_P, _P, _P, _I64, _I64, _I64, _I64, ct.POINTER(N4Params), _P, _P, _P], ct.c_int),
+    "vh_border": ([_P, _P, _I64, _I64, _I64, _I64, _P], ct.c_int),
+    "vh_snr": ([_P, _P, _P, _I64, _I64, _I64, _I64, _P], ct.c_int),
+    "vh_vdp": ([_P, _P, _P, _P, _I64, _I64, _I64, _I64, ct.c_float, _P, _P, _P, _P, _P], ct.c_int),
+    "vh_ci": ([_P, _P, _I64, _I64, _I64, _I64, _P, _P, _I64, _P, _P, _I64, ct.c_double, _P, _P,
+               _P], ct.c_int),
+    "vh_batch_create": ([_P, _I64, _I64, _I64, _I64, ct.POINTER(_P)], ct.c_int),
+    "vh_batch_destroy": ([_P], ct.c_int),
+    "vh_batch_upload": ([_P, _P, _P], ct.c_int),
+    "vh_batch_run": ([_P, ct.POINTER(RunOpts)], ct.c_int),
+    "vh_batch_sync": ([_P], ct.c_int),
+    "vh_batch_download": ([_P, _P, _P, _P, _P, _P], ct.c_int),
+    "vh_batch_cohort_hist": ([_P, _P], ct.c_int),
+    "vh_batch_kernel_names": ([], ct.c_char_p),
+    "vh_batch_kernel_time": ([_P, ct.c_char_p, ct.POINTER(ct.c_double), ct.POINTER(ct.c_int64),
+                              ct.POINTER(ct.c_double)], ct.c_int),
+    "vh_comm_unique_id": ([_P], ct.c_int),
+    "vh_comm_init": ([_P, ct.c_int, ct.c_int, _P], ct.c_int),
+    "vh_batch_cohort_allreduce": ([_P], ct.c_int),
+    "vh_comm_destroy": ([_P], ct.c_int),
+}
+EXPORTED = tuple(_SIGS)
+
+_lib = None
+_lock = threading.RLock()
+
+
+def lib():
+    """Load libventhip.so; fails loudly when the HIP extension has not been built."""
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                if not os.path.exists(LIB_PATH):
+                    raise ImportError(f"{LIB_PATH} is missing: build it with "
+                                      "`python __graft_entry__.py build` (no CPU fallback exists)")
+                L = ct.CDLL(LIB_PATH)
+                for name, (args, res) in _SIGS.items():
+                    f = getattr(L, name)
+                    f.argtypes = args
+                    f.restype = res
+                _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return None if a is None else ct.c_void_p(a.ctypes.data)
+
+
+class Context:
+    """One device + one HIP stream (vh_ctx)."""
+
+    def __init__(self, device: int = 0):
+        self.L = lib()
+        h = _P()
+        rc = self.L.vh_create(int(device), ct.byref(h))
+        if rc != VH_OK:
+            raise VentHipError(f"vh_create(device={device}) failed: "
+                               f"{self.L.vh_status_string(rc).decode()}")
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.vh_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def check(self, rc: int, where: str):
+        if rc == VH_OK:
+            return
+        msg = (self.L.vh_last_error(self.h) or b"").decode() if self.h else ""
+        text = f"{where}: {self.L.vh_status_string(rc).decode()}: {msg}"
+        if rc == VH_ERR_MAXRADIUS:
+            raise ValueError(text)
+        if rc == VH_ERR_EMPTY:
+            raise IndexError(text)
+        if rc == VH_ERR_ARG:
+            raise ValueError(text)
+        if rc == VH_ERR_NOMEM:
+            raise MemoryError(text)
+        raise VentHipError(text)
+
+
+_ctx = {}
+
+
+def context(device: int = 0) -> Context:
+    c = _ctx.get(device)
+    if c is None:
+        with _lock:
+            c = _ctx.get(device)
+            if c is None:
+                c = Context(device)
+                _ctx[device] = c
+    return c
+
+
+def device_count() -> int:
+    n = ct.c_int(0)
+    lib().vh_device_count(ct.byref(n))
+    return n.value
+
+
+def n4_params(max_iters=(50, 50, 50, 50), conv_threshold=0.001, ncp=(4, 4, 4), n_bins=200,
+              wiener_noise=0.01, fwhm=0.15) -> N4Params:
+    p = N4Params()
+    lib().vh_n4_default_params(ct.byref(p))
+    p.n_levels = len(max_iters)
+    for i in range(8):
+        p.max_iters[i] = max_iters[i] if i < len(max_iters) else 0
+    p.conv_threshold = conv_threshold
+    for i in range(3):
+        p.ncp[i] = ncp[i]
+    p.n_bins = n_bins
+    p.wiener_noise = wiener_noise
+    p.fwhm = fwhm
+    return p
+
+
+def as_batch(a, dtype):
+    """(R,C,Z) or (B,R,C,Z) -> contiguous (B,R,C,Z) of dtype (DICOM arrays are transposed views,
+    Vent_Analysis.py:179, so a contiguous copy is made when needed)."""
+    a = np.asarray(a)
+    if a.ndim == 3:
+        a = a[None]
+    if a.ndim != 4:
+        raise ValueError(f"expected a 3-D volume or a 4-D batch, got shape {a.shape}")
+    return np.ascontiguousarray(a, dtype=dtype)
+
+
+# ---- thin wrappers over the host-buffer entry points -------------------------------------------
+def n4(hp, mask, device=0, **kw):
+    c = context(device)
+    h = as_batch(hp, np.float32)
+    m = as_batch(mask, np.uint8)
+    if h.shape != m.shape:
+        raise ValueError("HPvent and mask shapes differ")
+    B, R, C, Z = h.shape
+    p = n4_params(**kw)
+    out = np.empty_like(h)
+    its = np.zeros((B, p.n_levels), np.int32)
+    conv = np.zeros((B, p.n_levels), np.float32)
+    c.check(c.L.vh_n4(c.h, _ptr(h), _ptr(m), R, C, Z, B, ct.byref(p), _ptr(out), _ptr(its),
+                      _ptr(conv)), "vh_n4")
+    return out, its, conv
+
+
+def border(a, device=0):
+    c = context(device)
+    x = as_batch(a, np.uint8)
+    B, R, C, Z = x.shape
+    out = np.empty_like(x)
+    c.check(c.L.vh_border(c.h, _ptr(x), R, C, Z, B, _ptr(out)), "vh_border")
+    return out
+
+
+def snr(hp, mask, device=0):
+    c = context(device)
+    h = as_batch(hp, np.float32)
+    m = as_batch(mask, np.uint8)
+    B, R, C, Z = h.shape
+    out = np.zeros(B, np.float64)
+    c.check(c.L.vh_snr(c.h, _ptr(h), _ptr(m), R, C, Z, B, _ptr(out)), "vh_snr")
+    return out
+
+
+def vdp(n4v, mask, vox, hp=None, thresh=0.6, device=0):
+    c = context(device)
+    n = as_batch(n4v, np.float32)
+    m = as_batch(mask, np.uint8)
+    h = None if hp is None else as_batch(hp, np.float32)
+    B, R, C, Z = n.shape
+    defect = np.empty((B, R, C, Z), np.uint8)
+    bord = np.empty_like(defect)
+    lb = np.empty_like(defect)
+    res = (VdpResult * B)()
+    vx = np.ascontiguousarray(vox, dtype=np.float64)
+    c.check(c.L.vh_vdp(c.h, _ptr(h), _ptr(n), _ptr(m), R, C, Z, B, ct.c_float(thresh), _ptr(vx),
+                       _ptr(defect), _ptr(bord), _ptr(lb), ct.cast(res, ct.c_void_p)), "vh_vdp")
+    return defect, bord, lb, list(res)
+
+
+def ci(defect, table, minvox, device=0):
+    """table: vent_analysis_amd.sphere.SphereTable for this shape.  Returns (ci f64, scalar[B],
+    shell int32)."""
+    c = context(device)
+    d = as_batch(np.asarray(defect) != 0, np.uint8)
+    B, R, C, Z = d.shape
+    out = np.empty((B, R, C, Z), np.float64)
+    shell = np.empty((B, R, C, Z), np.int32)
+    sc = np.zeros(B, np.float64)
+    c.check(c.L.vh_ci(c.h, _ptr(d), R, C, Z, B, _ptr(table.offsets), _ptr(table.dup), table.rows,
+                      _ptr(table.bounds), _ptr(table.radii), table.bounds.shape[0],
+                      ct.c_double(minvox), _ptr(out), _ptr(sc), _ptr(shell)), "vh_ci")
+    return out, sc, shell
+
+
+class Batch:
+    """Device-resident batch of studies (vh_batch): upload once, run the whole pipeline on the
+    GPU, download results.  Used by bench.py and for cohort processing."""
+
+    def __init__(self, R, C, Z, n, device=0):
+        self.ctx = context(device)
+        self.L = self.ctx.L
+        self.shape = (int(n), int(R), int(C), int(Z))
+        h = _P()
+        self.ctx.check(self.L.vh_batch_create(self.ctx.h, R, C, Z, n, ct.byref(h)),
+                       "vh_batch_create")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.vh_batch_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def upload(self, hp, mask):
+        h = np.ascontiguousarray(hp, dtype=np.float32)
+        m = np.ascontiguousarray(mask, dtype=np.uint8)
+        if h.shape != self.shape or m.shape != self.shape:
+            raise ValueError(f"batch expects {self.shape}")
+        self.ctx.check(self.L.vh_batch_upload(self.h, _ptr(h), _ptr(m)), "vh_batch_upload")
+
+    @staticmethod
+    def options(do_n4=True, thresh=0.6, do_snr=True, do_kmeans=True, do_cohort=False,
+                profile=False, vox=(1.0, 1.0, 1.0), **n4kw) -> RunOpts:
+        o = RunOpts()
+        lib().vh_default_run_opts(ct.byref(o))
+        o.do_n4 = int(bool(do_n4))
+        o.n4 = n4_params(**n4kw)
+        o.thresh = thresh
+        o.do_snr = int(bool(do_snr))
+        o.do_kmeans = int(bool(do_kmeans))
+        o.do_cohort = int(bool(do_cohort))
+        o.profile = int(bool(profile))
+        for i in range(3):
+            o.vox[i] = float(vox[i])
+        return o
+
+    def run(self, opts: RunOpts):
+        self.ctx.check(self.L.vh_batch_run(self.h, ct.byref(opts)), "vh_batch_run")
+
+    def sync(self):
+        self.ctx.check(self.L.vh_batch_sync(self.h), "vh_batch_sync")
+
+    def download(self, n4=False, maps=True):
+        B = self.shape[0]
+        out_n4 = np.empty(self.shape, np.float32) if n4 else None
+        d = np.empty(self.shape, np.uint8) if maps else None
+        bo = np.empty(self.shape, np.uint8) if maps else None
+        lb = np.empty(self.shape, np.uint8) if maps else None
+        res = (VdpResult * B)()
+        self.ctx.check(self.L.vh_batch_download(self.h, _ptr(out_n4), _ptr(d), _ptr(bo), _ptr(lb),
+                                                ct.cast(res, ct.c_void_p)), "vh_batch_download")
+        return out_n4, d, bo, lb, list(res)
+
+    def cohort_hist(self):
+        h = np.zeros(COHORT_BINS, np.uint64)
+        self.ctx.check(self.L.vh_batch_cohort_hist(self.h, _ptr(h)), "vh_batch_cohort_hist")
+        return h
+
+    def cohort_allreduce(self):
+        self.ctx.check(self.L.vh_batch_cohort_allreduce(self.h), "vh_batch_cohort_allreduce")
+
+    def kernel_time(self, name):
+        ms, n, by = ct.c_double(0), ct.c_int64(0), ct.c_double(0)
+        self.ctx.check(self.L.vh_batch_kernel_time(self.h, name.encode(), ct.byref(ms),
+                                                   ct.byref(n), ct.byref(by)),
+                       "vh_batch_kernel_time")
+        return ms.value, n.value, by.value
+
+
+def comm_unique_id() -> bytes:
+    buf = np.zeros(COMM_ID_BYTES, np.uint8)
+    rc = lib().vh_comm_unique_id(_ptr(buf))
+    if rc != VH_OK:
+        raise VentHipError("ncclGetUniqueId failed")
+    return buf.tobytes()
+
+
+def comm_init(nranks: int, rank: int, uid: bytes, device=0):
+    c = context(device)
+    buf = np.frombuffer(uid, np.uint8).copy()
+    c.check(c.L.vh_comm_init(c.h, nranks, rank, _ptr(buf)), "vh_comm_init")

@@ -1,0 +1,581 @@
+// api.hip -- the extern "C" boundary of libventhip.so (include/vent_hip.h).
+// Contexts own a HIP stream on one device; batches own the device buffers of nb studies.
+// No exception crosses the ABI: every entry point maps failures to a status code and keeps the
+// message for vh_last_error().
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <stdexcept>
+
+#include "vh_internal.h"
+
+// ---------------------------------------------------------------------------------------------
+// timing
+// ---------------------------------------------------------------------------------------------
+ScopedKTimer::ScopedKTimer(vh_batch *bb, const char *name, double bytes) : b(bb), t(nullptr) {
+    if (!b->profile) return;
+    t = &b->timers[name];
+    if (bytes > 0) t->bytes_per_launch = bytes;
+    hipEvent_t e0;
+    HIP_TRY(hipEventCreate(&e0));
+    HIP_TRY(hipEventCreate(&e1));
+    HIP_TRY(hipEventRecord(e0, b->ctx->stream));
+    t->ev.push_back(e0);
+}
+ScopedKTimer::~ScopedKTimer() {
+    if (!t) return;
+    (void)hipEventRecord(e1, b->ctx->stream);
+    t->ev.push_back(e1);
+}
+
+static void clear_timers(vh_batch *b) {
+    for (auto &kv : b->timers)
+        for (auto e : kv.second.ev) (void)hipEventDestroy(e);
+    b->timers.clear();
+}
+
+static void resolve_timers(vh_batch *b) {
+    for (auto &kv : b->timers) {
+        KTimer &t = kv.second;
+        for (size_t i = 0; i + 1 < t.ev.size(); i += 2) {
+            float ms = 0.f;
+            HIP_TRY(hipEventSynchronize(t.ev[i + 1]));
+            HIP_TRY(hipEventElapsedTime(&ms, t.ev[i], t.ev[i + 1]));
+            t.total_ms += ms;
+            t.launches += 1;
+            (void)hipEventDestroy(t.ev[i]);
+            (void)hipEventDestroy(t.ev[i + 1]);
+        }
+        t.ev.clear();
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
+// helpers
+// ---------------------------------------------------------------------------------------------
+static int fail(vh_ctx *c, int code, const std::string &msg) {
+    if (c) c->last_error = msg;
+    return code;
+}
+
+#define API_TRY(ctx, ...)                                                                    \
+    try {                                                                                    \
+        __VA_ARGS__                                                                          \
+    } catch (const VhError &e) {                                                             \
+        return fail(ctx, e.code, e.msg);                                                     \
+    } catch (const std::bad_alloc &) {                                                       \
+        return fail(ctx, VH_ERR_NOMEM, "host allocation failed");                            \
+    } catch (const std::exception &e) {                                                      \
+        return fail(ctx, VH_ERR_HIP, e.what());                                              \
+    } catch (...) {                                                                          \
+        return fail(ctx, VH_ERR_HIP, "unknown error");                                       \
+    }                                                                                        \
+    return VH_OK;
+
+template <typename T>
+static void dalloc(T **p, size_t n) {
+    HIP_TRY(hipMalloc((void **)p, sizeof(T) * (n ? n : 1)));
+}
+template <typename T>
+static void dfree(T *&p) {
+    if (p) (void)hipFree((void *)p);
+    p = nullptr;
+}
+
+static void check_dims(int64_t R, int64_t C, int64_t Z, int64_t batch) {
+    if (R < 2 || C < 2 || Z < 1 || batch < 1)
+        throw VhError{VH_ERR_ARG, "dims must be R>=2, C>=2, Z>=1, batch>=1"};
+    if (R * C * Z >= (int64_t)1 << 31)
+        throw VhError{VH_ERR_ARG, "a volume must have < 2^31 voxels"};
+    if (R > 65535 || C * Z > ((int64_t)1 << 31))
+        throw VhError{VH_ERR_ARG, "volume dims out of range"};
+}
+
+static void batch_free(vh_batch *b) {
+    if (!b) return;
+    clear_timers(b);
+    dfree(b->d_hp); dfree(b->d_mask); dfree(b->d_n4);
+    dfree(b->d_defect); dfree(b->d_border); dfree(b->d_lb);
+    dfree(b->d_colrange); dfree(b->d_colcount); dfree(b->d_colstart);
+    dfree(b->d_rowany); dfree(b->d_colany); dfree(b->d_sliceany);
+    dfree(b->d_sc); dfree(b->d_part); dfree(b->d_keys0); dfree(b->d_keys1); dfree(b->d_tilecnt);
+    dfree(b->d_cohort);
+    dfree(b->d_L0); dfree(b->d_B); dfree(b->d_lat); dfree(b->d_E);
+    dfree(b->d_Q1); dfree(b->d_Q2); dfree(b->d_P1); dfree(b->d_num); dfree(b->d_den);
+    dfree(b->d_hist); dfree(b->d_st); dfree(b->d_nactive); dfree(b->d_tabs); dfree(b->d_twiddle);
+    dfree(b->d_bitmap); dfree(b->d_ci_list); dfree(b->d_ci_shell); dfree(b->d_ci_hist);
+    delete b;
+}
+
+static vh_batch *batch_new(vh_ctx *ctx, int64_t R, int64_t C, int64_t Z, int64_t nb) {
+    check_dims(R, C, Z, nb);
+    HIP_TRY(hipSetDevice(ctx->device));
+    vh_batch *b = new vh_batch;
+    b->ctx = ctx;
+    b->R = R; b->C = C; b->Z = Z; b->nb = nb;
+    b->V = R * C * Z;
+    b->CZ = C * Z;
+    b->max_tiles = (b->V + VH_SORT_TILE - 1) / VH_SORT_TILE;
+    const size_t NV = (size_t)nb * b->V;
+    try {
+        dalloc(&b->d_hp, NV);
+        dalloc(&b->d_mask, NV);
+        dalloc(&b->d_n4, NV);
+        dalloc(&b->d_defect, NV);
+        dalloc(&b->d_border, NV);
+        dalloc(&b->d_lb, NV);
+        dalloc(&b->d_colrange, (size_t)nb * b->CZ * 2);
+        dalloc(&b->d_colcount, (size_t)nb * b->CZ);
+        dalloc(&b->d_colstart, (size_t)nb * b->CZ);
+        dalloc(&b->d_rowany, (size_t)nb * R);
+        dalloc(&b->d_colany, (size_t)nb * C);
+        dalloc(&b->d_sliceany, (size_t)nb * Z);
+        dalloc(&b->d_sc, (size_t)nb);
+        b->part_blocks = (b->CZ + VH_TPB - 1) / VH_TPB;
+        const int64_t max_chunks = (b->V + 8191) / 8192;
+        dalloc(&b->d_part, (size_t)nb * std::max<int64_t>(b->part_blocks * 4, max_chunks));
+        dalloc(&b->d_keys0, NV);
+        dalloc(&b->d_keys1, NV);
+        dalloc(&b->d_tilecnt, (size_t)nb * 256 * b->max_tiles);
+        dalloc(&b->d_cohort, (size_t)VH_COHORT_BINS);
+        HIP_TRY(hipMemset(b->d_cohort, 0, sizeof(uint64_t) * VH_COHORT_BINS));
+    } catch (...) {
+        batch_free(b);
+        throw;
+    }
+    return b;
+}
+
+static void batch_upload(vh_batch *b, const float *hp, const uint8_t *mask) {
+    hipStream_t st = b->ctx->stream;
+    const size_t NV = (size_t)b->nb * b->V;
+    if (hp) HIP_TRY(hipMemcpyAsync(b->d_hp, hp, sizeof(float) * NV, hipMemcpyHostToDevice, st));
+    if (mask) HIP_TRY(hipMemcpyAsync(b->d_mask, mask, NV, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipStreamSynchronize(st));
+}
+
+// n4_src: 0 = run N4 from d_hp, 1 = identity (d_hp), 2 = caller-uploaded d_n4
+static void batch_run(vh_batch *b, const vh_run_opts &o, int n4_src) {
+    HIP_TRY(hipSetDevice(b->ctx->device));
+    clear_timers(b);
+    b->profile = o.profile != 0;
+    b->opts = o;
+    hipStream_t st = b->ctx->stream;
+    if (o.do_n4) {
+        if (o.n4.n_levels < 1 || o.n4.n_levels > VH_MAX_LEVELS || o.n4.spline_order != 3 ||
+            o.n4.n_bins < 2 || o.n4.n_bins > VH_MAX_BINS || o.n4.ncp[0] < 4 || o.n4.ncp[1] < 4 ||
+            o.n4.ncp[2] < 4 || b->Z < 2)
+            throw VhError{VH_ERR_ARG, "unsupported N4 parameters (spline order 3, bins <= 256, ncp >= 4, Z >= 2)"};
+        int tot = 0;
+        for (int l = 0; l < o.n4.n_levels; ++l) {
+            if (o.n4.max_iters[l] < 1) throw VhError{VH_ERR_ARG, "max_iters must be >= 1"};
+            tot += o.n4.max_iters[l];
+        }
+        if (tot > 8 * 1024 - 1) throw VhError{VH_ERR_ARG, "too many N4 iterations"};
+    }
+    vh_launch_mask_stats(b);
+    if (o.do_cohort) HIP_TRY(hipMemsetAsync(b->d_cohort, 0, sizeof(uint64_t) * VH_COHORT_BINS, st));
+    const float *n4 = b->d_hp;
+    if (o.do_n4) {
+        vh_launch_n4(b, o.n4);
+        n4 = b->d_n4;
+    } else if (n4_src == 2) {
+        n4 = b->d_n4;
+    }
+    vh_launch_vdp_chain(b, n4, o);
+    b->have_result = true;
+}
+
+static void fill_results(vh_batch *b, vh_vdp_result *res) {
+    std::vector<VolScalars> sc(b->nb);
+    HIP_TRY(hipMemcpy(sc.data(), b->d_sc, sizeof(VolScalars) * b->nb, hipMemcpyDeviceToHost));
+    std::vector<N4State> st;
+    if (b->opts.do_n4) {
+        st.resize(b->nb);
+        HIP_TRY(hipMemcpy(st.data(), b->d_st, sizeof(N4State) * b->nb, hipMemcpyDeviceToHost));
+    }
+    const double *vox = b->opts.vox;
+    // np.prod(np.divide(vox, 10)): sequential multiply (Vent_Analysis.py:166, 252)
+    const double pv = ((vox[0] / 10.0) * (vox[1] / 10.0)) * (vox[2] / 10.0);
+    for (int64_t i = 0; i < b->nb; ++i) {
+        vh_vdp_result &r = res[i];
+        memset(&r, 0, sizeof r);
+        const VolScalars &s = sc[i];
+        const double nm = (double)s.n_mask;
+        r.n_mask = s.n_mask;
+        r.n_defect = s.n_defect;
+        r.n_lb12 = s.n_lb12;
+        r.n_km0 = s.n_km0;
+        r.vdp = (100.0 * (double)s.n_defect) / nm;
+        r.vdp_lb = (100.0 * (double)s.n_lb12) / nm;
+        r.vdp_km = b->opts.do_kmeans ? (100.0 * (double)s.n_km0) / nm : 0.0;
+        r.defect_volume = (double)s.n_defect * pv / 1000.0;
+        r.lung_volume = (double)s.n_mask1 * pv / 1000.0;
+        for (int j = 0; j < 4; ++j) r.km_centres[j] = s.km_c[j];
+        r.snr = b->opts.do_snr ? s.snr : 0.0;
+        r.mean_anchor = s.mean_anchor;
+        r.p99 = s.p99;
+        if (b->opts.do_n4)
+            for (int l = 0; l < b->opts.n4.n_levels; ++l) {
+                r.n4_iters[l] = st[i].iters_level[l];
+                r.n4_conv[l] = st[i].conv_level[l];
+            }
+    }
+}
+
+static void batch_download(vh_batch *b, float *n4, uint8_t *defect, uint8_t *border, uint8_t *lb,
+                           vh_vdp_result *res) {
+    hipStream_t st = b->ctx->stream;
+    HIP_TRY(hipStreamSynchronize(st));
+    const size_t NV = (size_t)b->nb * b->V;
+    if (n4) HIP_TRY(hipMemcpy(n4, b->opts.do_n4 ? b->d_n4 : b->d_hp, sizeof(float) * NV, hipMemcpyDeviceToHost));
+    if (defect) HIP_TRY(hipMemcpy(defect, b->d_defect, NV, hipMemcpyDeviceToHost));
+    if (border) HIP_TRY(hipMemcpy(border, b->d_border, NV, hipMemcpyDeviceToHost));
+    if (lb) HIP_TRY(hipMemcpy(lb, b->d_lb, NV, hipMemcpyDeviceToHost));
+    if (res) fill_results(b, res);
+}
+
+// a cached scratch batch per context for the host-buffer entry points
+struct CtxScratch {
+    vh_batch *b = nullptr;
+};
+static std::map<vh_ctx *, CtxScratch> g_scratch;
+
+static vh_batch *scratch_batch(vh_ctx *ctx, int64_t R, int64_t C, int64_t Z, int64_t nb) {
+    CtxScratch &s = g_scratch[ctx];
+    if (s.b && s.b->R == R && s.b->C == C && s.b->Z == Z && s.b->nb == nb) return s.b;
+    if (s.b) batch_free(s.b);
+    s.b = nullptr;
+    s.b = batch_new(ctx, R, C, Z, nb);
+    return s.b;
+}
+
+// ---------------------------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------------------------
+extern "C" {
+
+int vh_abi_version(void) { return VH_ABI_VERSION; }
+
+const char *vh_status_string(int s) {
+    switch (s) {
+        case VH_OK: return "ok";
+        case VH_ERR_ARG: return "invalid argument";
+        case VH_ERR_HIP: return "HIP runtime error";
+        case VH_ERR_NOMEM: return "out of device memory";
+        case VH_ERR_MAXRADIUS: return "cluster index: maximum radius reached";
+        case VH_ERR_EMPTY: return "empty mask or defect list";
+        case VH_ERR_RCCL: return "RCCL error";
+        case VH_ERR_NODEV: return "no GPU device";
+        default: return "unknown status";
+    }
+}
+
+int vh_device_count(int *n) {
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    *n = e == hipSuccess ? c : 0;
+    return VH_OK;
+}
+
+void vh_n4_default_params(vh_n4_params *p) {
+    memset(p, 0, sizeof *p);
+    p->n_levels = 4;
+    for (int i = 0; i < 4; ++i) p->max_iters[i] = 50;
+    p->conv_threshold = 0.001f;
+    p->ncp[0] = p->ncp[1] = p->ncp[2] = 4;
+    p->spline_order = 3;
+    p->n_bins = 200;
+    p->wiener_noise = 0.01f;
+    p->fwhm = 0.15f;
+}
+
+void vh_default_run_opts(vh_run_opts *o) {
+    memset(o, 0, sizeof *o);
+    o->do_n4 = 1;
+    vh_n4_default_params(&o->n4);
+    o->thresh = 0.6f;
+    o->do_snr = 1;
+    o->do_kmeans = 1;
+    o->do_cohort = 0;
+    o->profile = 0;
+    o->vox[0] = o->vox[1] = o->vox[2] = 1.0;
+}
+
+int vh_create(int device, vh_ctx **out) {
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+        return VH_ERR_NODEV;
+    if (device < 0 || device >= n) return VH_ERR_ARG;
+    vh_ctx *c = new vh_ctx;
+    c->device = device;
+    API_TRY(c, {
+        HIP_TRY(hipSetDevice(device));
+        HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+        HIP_TRY(hipHostMalloc((void **)&c->h_pinned, sizeof(int32_t) * 1024));
+        *out = c;
+    })
+}
+
+int vh_destroy(vh_ctx *ctx) {
+    if (!ctx) return VH_OK;
+    (void)hipSetDevice(ctx->device);
+    auto it = g_scratch.find(ctx);
+    if (it != g_scratch.end()) {
+        batch_free(it->second.b);
+        g_scratch.erase(it);
+    }
+    if (ctx->comm) ncclCommDestroy((ncclComm_t)ctx->comm);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
+    delete ctx;
+    return VH_OK;
+}
+
+const char *vh_last_error(const vh_ctx *ctx) { return ctx ? ctx->last_error.c_str() : ""; }
+
+int vh_synchronize(vh_ctx *ctx) {
+    API_TRY(ctx, { HIP_TRY(hipStreamSynchronize(ctx->stream)); })
+}
+
+int vh_n4(vh_ctx *ctx, const float *hp, const uint8_t *mask, int64_t R, int64_t C, int64_t Z,
+          int64_t batch, const vh_n4_params *prm, float *out, int32_t *iters, float *conv) {
+    API_TRY(ctx, {
+        if (!hp || !mask || !out || !prm) throw VhError{VH_ERR_ARG, "null buffer"};
+        vh_batch *b = scratch_batch(ctx, R, C, Z, batch);
+        batch_upload(b, hp, mask);
+        vh_run_opts o;
+        vh_default_run_opts(&o);
+        o.n4 = *prm;
+        o.do_n4 = 1;
+        clear_timers(b);
+        b->profile = false;
+        b->opts = o;
+        HIP_TRY(hipSetDevice(ctx->device));
+        vh_launch_mask_stats(b);
+        vh_launch_n4(b, o.n4);
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        HIP_TRY(hipMemcpy(out, b->d_n4, sizeof(float) * batch * b->V, hipMemcpyDeviceToHost));
+        std::vector<N4State> st(batch);
+        HIP_TRY(hipMemcpy(st.data(), b->d_st, sizeof(N4State) * batch, hipMemcpyDeviceToHost));
+        for (int64_t i = 0; i < batch; ++i)
+            for (int l = 0; l < prm->n_levels; ++l) {
+                if (iters) iters[i * prm->n_levels + l] = st[i].iters_level[l];
+                if (conv) conv[i * prm->n_levels + l] = st[i].conv_level[l];
+            }
+        std::vector<VolScalars> sc(batch);
+        HIP_TRY(hipMemcpy(sc.data(), b->d_sc, sizeof(VolScalars) * batch, hipMemcpyDeviceToHost));
+        for (int64_t i = 0; i < batch; ++i)
+            if (sc[i].n_mask1 < 2) throw VhError{VH_ERR_EMPTY, "N4 needs at least 2 voxels with mask == 1"};
+    })
+}
+
+int vh_border(vh_ctx *ctx, const uint8_t *a, int64_t R, int64_t C, int64_t Z, int64_t batch,
+              uint8_t *border) {
+    API_TRY(ctx, {
+        if (!a || !border) throw VhError{VH_ERR_ARG, "null buffer"};
+        vh_batch *b = scratch_batch(ctx, R, C, Z, batch);
+        HIP_TRY(hipSetDevice(ctx->device));
+        b->profile = false;
+        const size_t NV = (size_t)batch * b->V;
+        HIP_TRY(hipMemcpyAsync(b->d_defect, a, NV, hipMemcpyHostToDevice, ctx->stream));
+        vh_launch_border(b, b->d_defect, b->d_border);
+        HIP_TRY(hipMemcpyAsync(border, b->d_border, NV, hipMemcpyDeviceToHost, ctx->stream));
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+    })
+}
+
+int vh_snr(vh_ctx *ctx, const float *hp, const uint8_t *mask, int64_t R, int64_t C, int64_t Z,
+           int64_t batch, double *snr) {
+    API_TRY(ctx, {
+        if (!hp || !mask || !snr) throw VhError{VH_ERR_ARG, "null buffer"};
+        vh_batch *b = scratch_batch(ctx, R, C, Z, batch);
+        batch_upload(b, hp, mask);
+        HIP_TRY(hipSetDevice(ctx->device));
+        b->profile = false;
+        vh_launch_mask_stats(b);
+        vh_launch_snr(b);
+        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        std::vector<VolScalars> sc(batch);
+        HIP_TRY(hipMemcpy(sc.data(), b->d_sc, sizeof(VolScalars) * batch, hipMemcpyDeviceToHost));
+        for (int64_t i = 0; i < batch; ++i) {
+            if (!sc[i].snr_ok) throw VhError{VH_ERR_ARG, "calculate_SNR: no masked column > 0 (numpy min of an empty array)"};
+            snr[i] = sc[i].snr;
+        }
+    })
+}
+
+int vh_vdp(vh_ctx *ctx, const float *hp, const float *n4, const uint8_t *mask, int64_t R,
+           int64_t C, int64_t Z, int64_t batch, float thresh, const double vox[3],
+           uint8_t *defect, uint8_t *defect_border, uint8_t *lb, vh_vdp_result *res) {
+    API_TRY(ctx, {
+        if (!n4 || !mask || !res || !vox) throw VhError{VH_ERR_ARG, "null buffer"};
+        vh_batch *b = scratch_batch(ctx, R, C, Z, batch);
+        const size_t NV = (size_t)batch * b->V;
+        HIP_TRY(hipMemcpyAsync(b->d_n4, n4, sizeof(float) * NV, hipMemcpyHostToDevice, ctx->stream));
+        batch_upload(b, hp, mask);
+        vh_run_opts o;
+        vh_default_run_opts(&o);
+        o.do_n4 = 0;
+        o.do_snr = hp != nullptr;
+        o.thresh = thresh;
+        for (int i = 0; i < 3; ++i) o.vox[i] = vox[i];
+        batch_run(b, o, 2);
+        batch_download(b, nullptr, defect, defect_border, lb, res);
+        std::vector<VolScalars> sc(batch);
+        HIP_TRY(hipMemcpy(sc.data(), b->d_sc, sizeof(VolScalars) * batch, hipMemcpyDeviceToHost));
+        for (int64_t i = 0; i < batch; ++i) {
+            if (sc[i].n_mask <= 0) throw VhError{VH_ERR_EMPTY, "empty mask"};
+            if (hp && !sc[i].snr_ok) throw VhError{VH_ERR_ARG, "calculate_SNR: no masked column > 0"};
+        }
+    })
+}
+
+int vh_ci(vh_ctx *ctx, const uint8_t *defect, int64_t R, int64_t C, int64_t Z, int64_t batch,
+          const int16_t *offs, const uint8_t *dup, int64_t rows, const int32_t *bounds,
+          const double *radii, int64_t nb, double minvox, double *ci_array, double *ci_scalar,
+          int32_t *shell) {
+    API_TRY(ctx, {
+        if (!defect || !offs || !dup || !bounds || !radii || rows < 1 || nb < 1)
+            throw VhError{VH_ERR_ARG, "null buffer / empty table"};
+        for (int64_t q = 0; q < nb; ++q)
+            if (bounds[q] < 1 || bounds[q] > rows || (q && bounds[q] <= bounds[q - 1]))
+                throw VhError{VH_ERR_ARG, "sphere table bounds must be increasing in [1, rows]"};
+        vh_batch *b = scratch_batch(ctx, R, C, Z, batch);
+        HIP_TRY(hipSetDevice(ctx->device));
+        b->profile = false;
+        const size_t NV = (size_t)batch * b->V;
+        HIP_TRY(hipMemcpyAsync(b->d_defect, defect, NV, hipMemcpyHostToDevice, ctx->stream));
+        double *d_ci = nullptr;
+        if (ci_array) HIP_TRY(hipMalloc(&d_ci, sizeof(double) * NV));
+        try {
+            vh_ci_run(b, offs, dup, rows, bounds, radii, nb, minvox, d_ci);
+            if (ci_array) HIP_TRY(hipMemcpy(ci_array, d_ci, sizeof(double) * NV, hipMemcpyDeviceToHost));
+            if (shell) HIP_TRY(hipMemcpy(shell, b->d_ci_shell, sizeof(int32_t) * NV, hipMemcpyDeviceToHost));
+        } catch (...) {
+            if (d_ci) (void)hipFree(d_ci);
+            throw;
+        }
+        if (d_ci) HIP_TRY(hipFree(d_ci));
+        std::vector<VolScalars> sc(batch);
+        HIP_TRY(hipMemcpy(sc.data(), b->d_sc, sizeof(VolScalars) * batch, hipMemcpyDeviceToHost));
+        for (int64_t i = 0; i < batch; ++i) {
+            if (ci_scalar) ci_scalar[i] = sc[i].ci_scalar;
+            if (sc[i].ci_status == VH_ERR_MAXRADIUS)
+                throw VhError{VH_ERR_MAXRADIUS, "--MAX RADIUS REACHED-- (CI.py:101-103)"};
+            if (sc[i].ci_status == VH_ERR_EMPTY)
+                throw VhError{VH_ERR_EMPTY, "no defect voxels (Vent_Analysis.py:270 IndexError)"};
+        }
+    })
+}
+
+int vh_batch_create(vh_ctx *ctx, int64_t R, int64_t C, int64_t Z, int64_t batch, vh_batch **out) {
+    *out = nullptr;
+    API_TRY(ctx, { *out = batch_new(ctx, R, C, Z, batch); })
+}
+
+int vh_batch_destroy(vh_batch *b) {
+    if (b) {
+        (void)hipSetDevice(b->ctx->device);
+        (void)hipStreamSynchronize(b->ctx->stream);
+        batch_free(b);
+    }
+    return VH_OK;
+}
+
+int vh_batch_upload(vh_batch *b, const float *hp, const uint8_t *mask) {
+    API_TRY(b->ctx, {
+        HIP_TRY(hipSetDevice(b->ctx->device));
+        batch_upload(b, hp, mask);
+    })
+}
+
+int vh_batch_run(vh_batch *b, const vh_run_opts *opts) {
+    API_TRY(b->ctx, {
+        if (!opts) throw VhError{VH_ERR_ARG, "null options"};
+        batch_run(b, *opts, opts->do_n4 ? 0 : 1);
+    })
+}
+
+int vh_batch_sync(vh_batch *b) {
+    API_TRY(b->ctx, { HIP_TRY(hipStreamSynchronize(b->ctx->stream)); })
+}
+
+int vh_batch_download(vh_batch *b, float *n4, uint8_t *defect, uint8_t *defect_border, uint8_t *lb,
+                      vh_vdp_result *res) {
+    API_TRY(b->ctx, {
+        if (!b->have_result) throw VhError{VH_ERR_ARG, "vh_batch_run has not been called"};
+        batch_download(b, n4, defect, defect_border, lb, res);
+    })
+}
+
+int vh_batch_cohort_hist(vh_batch *b, uint64_t *hist) {
+    API_TRY(b->ctx, {
+        HIP_TRY(hipStreamSynchronize(b->ctx->stream));
+        HIP_TRY(hipMemcpy(hist, b->d_cohort, sizeof(uint64_t) * VH_COHORT_BINS, hipMemcpyDeviceToHost));
+    })
+}
+
+const char *vh_batch_kernel_names(void) {
+    return "mask_stats;gather;sort;classify;kmeans;snr;border;n4_init;n4_den;n4_hist;n4_fit;"
+           "n4_contract;n4_eval;n4_final;ci_walk";
+}
+
+int vh_batch_kernel_time(vh_batch *b, const char *name, double *total_ms, int64_t *launches,
+                         double *bytes_per_launch) {
+    API_TRY(b->ctx, {
+        resolve_timers(b);
+        auto it = b->timers.find(name);
+        if (it == b->timers.end()) {
+            *total_ms = 0; *launches = 0;
+            if (bytes_per_launch) *bytes_per_launch = 0;
+        } else {
+            *total_ms = it->second.total_ms;
+            *launches = it->second.launches;
+            if (bytes_per_launch) *bytes_per_launch = it->second.bytes_per_launch;
+        }
+    })
+}
+
+int vh_comm_unique_id(uint8_t id[VH_COMM_ID_BYTES]) {
+    static_assert(sizeof(ncclUniqueId) <= VH_COMM_ID_BYTES, "nccl id size");
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return VH_ERR_RCCL;
+    memcpy(id, &u, sizeof u);
+    return VH_OK;
+}
+
+int vh_comm_init(vh_ctx *ctx, int nranks, int rank, const uint8_t id[VH_COMM_ID_BYTES]) {
+    API_TRY(ctx, {
+        HIP_TRY(hipSetDevice(ctx->device));
+        ncclUniqueId u;
+        memcpy(&u, id, sizeof u);
+        ncclComm_t comm;
+        ncclResult_t r = ncclCommInitRank(&comm, nranks, u, rank);
+        if (r != ncclSuccess) throw VhError{VH_ERR_RCCL, std::string("ncclCommInitRank: ") + ncclGetErrorString(r)};
+        ctx->comm = comm;
+        ctx->nranks = nranks;
+        ctx->rank = rank;
+    })
+}
+
+int vh_batch_cohort_allreduce(vh_batch *b) {
+    API_TRY(b->ctx, {
+        vh_ctx *c = b->ctx;
+        if (!c->comm) throw VhError{VH_ERR_ARG, "vh_comm_init has not been called"};
+        ncclResult_t r = ncclAllReduce(b->d_cohort, b->d_cohort, VH_COHORT_BINS, ncclUint64, ncclSum,
+                                       (ncclComm_t)c->comm, c->stream);
+        if (r != ncclSuccess) throw VhError{VH_ERR_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r)};
+    })
+}
+
+int vh_comm_destroy(vh_ctx *ctx) {
+    if (ctx && ctx->comm) {
+        ncclCommDestroy((ncclComm_t)ctx->comm);
+        ctx->comm = nullptr;
+    }
+    return VH_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,184 @@
+// ci.hip -- cluster-index map on gfx950 (CI.calculate_CI, CI.py:107-145, and the 95th-percentile
+// tail of Vent_Analysis.calculate_CI, Vent_Analysis.py:265-271).
+//
+// One lane per defect voxel.  The lanes of a wave walk the sphere table in LOCKSTEP (row index is
+// wave-uniform, so the table's row offset is one broadcast load per row for the whole wave), each
+// lane testing one bit of the volume's defect bitmap per row.  At every shell boundary b the lane
+// stops at the first b with 2*hits < b (C = hits/b < 0.5, CI.py:97) and records the shell.
+// Semantics restated in oracle/ci_oracle.c: the bitmap is indexed by the
+// Fortran-order linear index L = (i+dx) + (j+dy) s0 + (k+dz) s0 s1 (px2vec, CI.py:65-68), so
+// out-of-range rows/cols alias into neighbouring columns/slices and only 0 <= L < N is required;
+// table rows whose linear offset repeats an earlier row never count (np.intersect1d uniques).
+#include <climits>
+
+#include "vh_internal.h"
+
+#define CI_SENTINEL INT32_MIN
+
+__global__ void k_ci_bitmap(const uint8_t *__restrict__ defect, int64_t s0, int64_t s1,
+                            int64_t s2, int64_t V, int64_t words, uint32_t *bits,
+                            int32_t *list, unsigned long long *count) {
+    const int64_t b = blockIdx.y;
+    __shared__ unsigned long long s_cnt, s_base;
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+    const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    bool d = false;
+    unsigned long long my = 0;
+    if (v < V) {
+        d = defect[b * V + v] != 0;
+        if (d) {
+            const int64_t i = v / (s1 * s2), j = (v / s2) % s1, k = v % s2;
+            const int64_t L = i + j * s0 + k * s0 * s1;
+            atomicOr(&bits[b * words + (L >> 5)], 1u << (L & 31));
+            my = atomicAdd(&s_cnt, 1ull);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) s_base = s_cnt ? atomicAdd(&count[b], s_cnt) : 0ull;
+    __syncthreads();
+    if (d) list[b * V + (int64_t)(s_base + my)] = (int32_t)v;
+}
+
+__global__ void __launch_bounds__(VH_TPB) k_ci_walk(const uint32_t *__restrict__ bits,
+                                                   const int32_t *__restrict__ list,
+                                                   const unsigned long long *count,
+                                                   const int32_t *__restrict__ offL,
+                                                   const int32_t *__restrict__ bounds, int64_t nbs,
+                                                   int64_t s0, int64_t s1, int64_t s2, int64_t V,
+                                                   int64_t words, int32_t *shell_of,
+                                                   uint32_t *hist, int32_t *status) {
+    const int64_t b = blockIdx.y;
+    const int64_t n = (int64_t)count[b];
+    const int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if ((int64_t)blockIdx.x * blockDim.x >= n) return;   // block-uniform exit
+    const bool valid = idx < n;
+    int64_t base = 0;
+    int32_t v = 0;
+    if (valid) {
+        v = list[b * V + idx];
+        const int64_t i = v / (s1 * s2), j = (v / s2) % s1, k = v % s2;
+        base = i + j * s0 + k * s0 * s1;
+    }
+    const int64_t N = s0 * s1 * s2;
+    const uint32_t *bm = bits + b * words;
+    bool done = !valid;
+    int32_t qstop = -1;
+    int64_t hits = 0;
+    int64_t row = 0;
+    for (int64_t q = 0; q < nbs; ++q) {
+        if (__all(done)) break;
+        const int64_t bq = bounds[q];
+        for (; row < bq; ++row) {
+            const int32_t off = offL[row];
+            if (!done && off != CI_SENTINEL) {
+                const int64_t L = base + off;
+                if (L >= 0 && L < N) hits += (bm[L >> 5] >> (L & 31)) & 1u;
+            }
+        }
+        if (!done && 2 * hits < bq) {
+            done = true;
+            qstop = (int32_t)q;
+        }
+    }
+    if (valid) {
+        shell_of[b * V + v] = qstop;
+        if (qstop >= 0) atomicAdd(&hist[b * nbs + qstop], 1u);
+        else atomicExch(&status[b], 1);
+    }
+}
+
+__global__ void k_ci_finish(const uint32_t *hist, const unsigned long long *count,
+                            const double *radii, int64_t nbs, double minvox, int64_t nb,
+                            const int32_t *status, VolScalars *sc) {
+    const int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    const int64_t D = (int64_t)count[b];
+    sc[b].n_ci = D;
+    sc[b].ci_status = status[b] ? VH_ERR_MAXRADIUS : (D == 0 ? VH_ERR_EMPTY : VH_OK);
+    sc[b].ci_scalar = 0.0;
+    if (status[b] || D == 0) return;
+    const int64_t i95 = (int64_t)(0.95 * (double)D);
+    int64_t cum = 0;
+    for (int64_t q = 0; q < nbs; ++q) {
+        cum += hist[b * nbs + q];
+        if (cum > i95) { sc[b].ci_scalar = radii[q] * minvox; return; }
+    }
+}
+
+__global__ void k_ci_scatter(const int32_t *shell_of, const uint8_t *defect, const double *radii,
+                             double minvox, int64_t V, double *ci) {
+    const int64_t b = blockIdx.y;
+    const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (v >= V) return;
+    double r = 0.0;
+    if (defect[b * V + v]) {
+        const int32_t q = shell_of[b * V + v];
+        r = q >= 0 ? radii[q] * minvox : 0.0;
+    }
+    ci[b * V + v] = r;
+}
+
+// host: offs/dup/bounds/radii are host arrays; results stay on device (d_ci_shell, d_sc) and the
+// float64 CI map goes to ci_dev (caller-provided device buffer, nb*V doubles).
+void vh_ci_run(vh_batch *b, const int16_t *offs, const uint8_t *dup, int64_t rows,
+               const int32_t *bounds, const double *radii, int64_t nbs, double minvox,
+               double *d_ci) {
+    hipStream_t st = b->ctx->stream;
+    const int64_t words = (b->V + 31) / 32;
+    // px2vec strides (CI.py:65-68): s0 = R (rows), s1 = C (cols): L = i + j R + k R C
+    std::vector<int32_t> offL(rows);
+    for (int64_t r = 0; r < rows; ++r)
+        offL[r] = dup[r] ? CI_SENTINEL
+                         : (int32_t)(offs[3 * r] + (int64_t)offs[3 * r + 1] * b->R +
+                                     (int64_t)offs[3 * r + 2] * b->R * b->C);
+    int32_t *d_offL = nullptr, *d_bounds = nullptr, *d_status = nullptr;
+    double *d_radii = nullptr;
+    unsigned long long *d_count = nullptr;
+    HIP_TRY(hipMalloc(&d_offL, sizeof(int32_t) * rows));
+    HIP_TRY(hipMalloc(&d_bounds, sizeof(int32_t) * nbs));
+    HIP_TRY(hipMalloc(&d_radii, sizeof(double) * nbs));
+    HIP_TRY(hipMalloc(&d_status, sizeof(int32_t) * b->nb));
+    HIP_TRY(hipMalloc(&d_count, sizeof(unsigned long long) * b->nb));
+    if (!b->d_bitmap) {
+        HIP_TRY(hipMalloc(&b->d_bitmap, sizeof(uint32_t) * b->nb * words));
+        HIP_TRY(hipMalloc(&b->d_ci_list, sizeof(int32_t) * b->nb * b->V));
+        HIP_TRY(hipMalloc(&b->d_ci_shell, sizeof(int32_t) * b->nb * b->V));
+    }
+    if (nbs > b->ci_nb_cap) {
+        if (b->d_ci_hist) HIP_TRY(hipFree(b->d_ci_hist));
+        HIP_TRY(hipMalloc(&b->d_ci_hist, sizeof(uint32_t) * b->nb * nbs));
+        b->ci_nb_cap = nbs;
+    }
+    HIP_TRY(hipMemcpyAsync(d_offL, offL.data(), sizeof(int32_t) * rows, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(d_bounds, bounds, sizeof(int32_t) * nbs, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(d_radii, radii, sizeof(double) * nbs, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemsetAsync(d_status, 0, sizeof(int32_t) * b->nb, st));
+    HIP_TRY(hipMemsetAsync(d_count, 0, sizeof(unsigned long long) * b->nb, st));
+    HIP_TRY(hipMemsetAsync(b->d_bitmap, 0, sizeof(uint32_t) * b->nb * words, st));
+    HIP_TRY(hipMemsetAsync(b->d_ci_hist, 0, sizeof(uint32_t) * b->nb * nbs, st));
+    const dim3 vg((unsigned)((b->V + VH_TPB - 1) / VH_TPB), (unsigned)b->nb);
+    k_ci_bitmap<<<vg, VH_TPB, 0, st>>>(b->d_defect, b->R, b->C, b->Z, b->V, words, b->d_bitmap,
+                                       b->d_ci_list, d_count);
+    VH_CHECK_LAUNCH();
+    {
+        ScopedKTimer tm(b, "ci_walk", 0.0);
+        k_ci_walk<<<vg, VH_TPB, 0, st>>>(b->d_bitmap, b->d_ci_list, d_count, d_offL, d_bounds, nbs,
+                                         b->R, b->C, b->Z, b->V, words, b->d_ci_shell,
+                                         b->d_ci_hist, d_status);
+        VH_CHECK_LAUNCH();
+    }
+    k_ci_finish<<<(unsigned)((b->nb + 63) / 64), 64, 0, st>>>(b->d_ci_hist, d_count, d_radii, nbs,
+                                                              minvox, b->nb, d_status, b->d_sc);
+    VH_CHECK_LAUNCH();
+    if (d_ci) {
+        k_ci_scatter<<<vg, VH_TPB, 0, st>>>(b->d_ci_shell, b->d_defect, d_radii, minvox, b->V, d_ci);
+        VH_CHECK_LAUNCH();
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(hipFree(d_offL));
+    HIP_TRY(hipFree(d_bounds));
+    HIP_TRY(hipFree(d_radii));
+    HIP_TRY(hipFree(d_status));
+    HIP_TRY(hipFree(d_count));
+}

@@ -1,0 +1,710 @@
+// vdp.hip -- post-N4 VDP chain on gfx950 (Vent_Analysis.calculate_VDP, Vent_Analysis.py:239-263),
+// calculateBorder (:225-231) and calculate_SNR (:337-357), over a batch of volumes.
+//
+// Layout: volume b at [b][R][C][Z] (numpy C order, slice axis fastest).  A "column" is one
+// (col, slice) pair; column sweeps put one thread per column and walk the rows, so consecutive
+// lanes touch consecutive bytes for every row (coalesced).
+#include <climits>
+
+#include "vh_internal.h"
+
+// =============================================================================================
+// mask statistics (once per batch): per-column masked row range + count, row/col/slice "any"
+// flags for calculate_SNR's box (Vent_Analysis.py:344-347), masked counts, first mask==1 voxel.
+// =============================================================================================
+__global__ void k_init_scalars(VolScalars *sc, int64_t nb) {
+    int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    VolScalars s{};
+    s.first_masked = INT64_MAX;
+    sc[b] = s;
+}
+
+__global__ void __launch_bounds__(VH_TPB) k_mask_stats(const uint8_t *__restrict__ mask, int64_t R,
+                                                      int64_t C, int64_t Z, int64_t V,
+                                                      int32_t *colrange, int32_t *colcount,
+                                                      uint8_t *rowany, uint8_t *colany,
+                                                      uint8_t *sliceany, VolScalars *sc) {
+    extern __shared__ uint8_t s_row[];   // [R]
+    __shared__ unsigned long long s_n, s_n1, s_first;
+    const int64_t b = blockIdx.y;
+    const int64_t CZ = C * Z;
+    const int64_t col = blockIdx.x * (int64_t)VH_TPB + threadIdx.x;
+    for (int64_t x = threadIdx.x; x < R; x += VH_TPB) s_row[x] = 0;
+    if (threadIdx.x == 0) { s_n = 0; s_n1 = 0; s_first = ULLONG_MAX; }
+    __syncthreads();
+    unsigned long long n = 0, n1 = 0, first = ULLONG_MAX;
+    if (col < CZ) {
+        const uint8_t *m = mask + b * V + col;
+        int32_t lo = (int32_t)R, hi = -1;
+        for (int64_t x = 0; x < R; ++x) {
+            const uint8_t v = m[x * CZ];
+            if (v) {
+                ++n;
+                if (lo == (int32_t)R) lo = (int32_t)x;
+                hi = (int32_t)x;
+                s_row[x] = 1;
+                if (v == 1) {
+                    ++n1;
+                    const unsigned long long idx = (unsigned long long)(x * CZ + col);
+                    if (idx < first) first = idx;
+                }
+            }
+        }
+        colrange[(b * CZ + col) * 2] = lo;
+        colrange[(b * CZ + col) * 2 + 1] = hi;
+        colcount[b * CZ + col] = (int32_t)n;
+        if (n) {
+            colany[b * C + col / Z] = 1;
+            sliceany[b * Z + col % Z] = 1;
+        }
+    }
+    if (n) atomicAdd(&s_n, n);
+    if (n1) atomicAdd(&s_n1, n1);
+    if (first != ULLONG_MAX) atomicMin(&s_first, first);
+    __syncthreads();
+    for (int64_t x = threadIdx.x; x < R; x += VH_TPB)
+        if (s_row[x]) rowany[b * R + x] = 1;
+    if (threadIdx.x == 0) {
+        if (s_n) atomicAdd((unsigned long long *)&sc[b].n_mask, s_n);
+        if (s_n1) atomicAdd((unsigned long long *)&sc[b].n_mask1, s_n1);
+        if (s_first != ULLONG_MAX) atomicMin((unsigned long long *)&sc[b].first_masked, s_first);
+    }
+}
+
+// exclusive prefix of the per-column masked counts (compaction offsets for the sort keys) and
+// the SNR box parameters.  One block per volume.
+__global__ void __launch_bounds__(VH_TPB) k_mask_finish(const int32_t *colcount, int64_t *colstart,
+                                                       const uint8_t *rowany, const uint8_t *colany,
+                                                       const uint8_t *sliceany, int64_t R,
+                                                       int64_t C, int64_t Z, VolScalars *sc) {
+    __shared__ int64_t s_part[VH_TPB];
+    __shared__ int32_t s_cmin, s_cmax, s_rowe, s_slie;
+    const int64_t b = blockIdx.x;
+    const int64_t CZ = C * Z;
+    const int t = threadIdx.x;
+    const int64_t per = (CZ + VH_TPB - 1) / VH_TPB;
+    const int64_t s = t * per, e = s + per < CZ ? s + per : CZ;
+    int64_t acc = 0;
+    for (int64_t i = s; i < e; ++i) acc += colcount[b * CZ + i];
+    s_part[t] = acc;
+    if (t == 0) { s_cmin = INT_MAX; s_cmax = 0; s_rowe = 0; s_slie = 0; }
+    __syncthreads();
+    if (t == 0) {
+        int64_t run = 0;
+        for (int i = 0; i < VH_TPB; ++i) { int64_t v = s_part[i]; s_part[i] = run; run += v; }
+    }
+    __syncthreads();
+    int64_t run = s_part[t];
+    for (int64_t i = s; i < e; ++i) { colstart[b * CZ + i] = run; run += colcount[b * CZ + i]; }
+    for (int64_t c = t; c < C; c += VH_TPB)
+        if (colany[b * C + c]) {
+            if (c > 0) atomicMin(&s_cmin, (int32_t)c);
+            atomicMax(&s_cmax, (int32_t)c);
+        }
+    for (int64_t r = t; r < R; r += VH_TPB)
+        if (!rowany[b * R + r]) s_rowe = 1;
+    for (int64_t z = t; z < Z; z += VH_TPB)
+        if (!sliceany[b * Z + z]) s_slie = 1;
+    __syncthreads();
+    if (t == 0) {
+        sc[b].cmin = s_cmin;
+        sc[b].cmax = s_cmax;
+        sc[b].any_row_empty = s_rowe;
+        sc[b].any_slice_empty = s_slie;
+        sc[b].snr_ok = s_cmin != INT_MAX;
+    }
+}
+
+void vh_launch_mask_stats(vh_batch *b) {
+    hipStream_t st = b->ctx->stream;
+    HIP_TRY(hipMemsetAsync(b->d_rowany, 0, b->nb * b->R, st));
+    HIP_TRY(hipMemsetAsync(b->d_colany, 0, b->nb * b->C, st));
+    HIP_TRY(hipMemsetAsync(b->d_sliceany, 0, b->nb * b->Z, st));
+    k_init_scalars<<<(unsigned)((b->nb + 255) / 256), 256, 0, st>>>(b->d_sc, b->nb);
+    VH_CHECK_LAUNCH();
+    {
+        ScopedKTimer tm(b, "mask_stats", (double)b->V);
+        k_mask_stats<<<col_grid(b), VH_TPB, (size_t)b->R, st>>>(
+            b->d_mask, b->R, b->C, b->Z, b->V, b->d_colrange, b->d_colcount, b->d_rowany,
+            b->d_colany, b->d_sliceany, b->d_sc);
+        VH_CHECK_LAUNCH();
+    }
+    k_mask_finish<<<(unsigned)b->nb, VH_TPB, 0, st>>>(b->d_colcount, b->d_colstart, b->d_rowany,
+                                                      b->d_colany, b->d_sliceany, b->R, b->C,
+                                                      b->Z, b->d_sc);
+    VH_CHECK_LAUNCH();
+}
+
+// =============================================================================================
+// masked gather -> sortable uint32 keys, compacted column by column (order is irrelevant: sorted
+// next; only the multiset matters, Vent_Analysis.py:245).
+// =============================================================================================
+__global__ void __launch_bounds__(VH_TPB) k_gather(const float *__restrict__ n4,
+                                                  const uint8_t *__restrict__ mask,
+                                                  const int32_t *colrange, const int64_t *colstart,
+                                                  int64_t CZ, int64_t V, uint32_t *keys) {
+    const int64_t b = blockIdx.y;
+    const int64_t col = blockIdx.x * (int64_t)VH_TPB + threadIdx.x;
+    if (col >= CZ) return;
+    const int32_t lo = colrange[(b * CZ + col) * 2], hi = colrange[(b * CZ + col) * 2 + 1];
+    int64_t pos = b * V + colstart[b * CZ + col];
+    const float *p = n4 + b * V + col;
+    const uint8_t *m = mask + b * V + col;
+    for (int64_t x = lo; x <= hi; ++x)
+        if (m[x * CZ]) keys[pos++] = f2key(p[x * CZ]);
+}
+
+// =============================================================================================
+// segmented LSD radix sort (4 x 8-bit digits), one segment per volume, tiles of 4096 keys.
+//   up:   per-tile digit counts                    tilecnt[b][digit][tile]
+//   scan: per-volume exclusive scan (digit-major)  -> scatter base of (digit, tile)
+//   down: stable in-tile ranks by wave ballots (8 ballots build the same-digit peer mask), then
+//         scatter.  Stable => LSD correct.
+// =============================================================================================
+__global__ void __launch_bounds__(VH_TPB) k_sort_up(const uint32_t *__restrict__ keys,
+                                                   const VolScalars *sc, int64_t V,
+                                                   int64_t max_tiles, int shift,
+                                                   uint32_t *tilecnt) {
+    __shared__ uint32_t h[256];
+    const int64_t b = blockIdx.y, t = blockIdx.x;
+    const int64_t n = sc[b].n_mask;
+    const int64_t s = t * VH_SORT_TILE;
+    if (s >= n) return;
+    h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t *k = keys + b * V;
+    for (int i = 0; i < VH_SORT_KPT; ++i) {
+        const int64_t idx = s + i * VH_TPB + threadIdx.x;
+        if (idx < n) atomicAdd(&h[(k[idx] >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    tilecnt[(b * 256 + threadIdx.x) * max_tiles + t] = h[threadIdx.x];
+}
+
+__global__ void __launch_bounds__(VH_TPB) k_sort_scan(uint32_t *tilecnt, const VolScalars *sc,
+                                                     int64_t max_tiles) {
+    __shared__ uint32_t s_row[256];
+    const int64_t b = blockIdx.x;
+    const int64_t n = sc[b].n_mask;
+    const int64_t nt = (n + VH_SORT_TILE - 1) / VH_SORT_TILE;
+    uint32_t *row = tilecnt + (b * 256 + threadIdx.x) * max_tiles;
+    uint32_t sum = 0;
+    for (int64_t t = 0; t < nt; ++t) sum += row[t];
+    s_row[threadIdx.x] = sum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (int d = 0; d < 256; ++d) { uint32_t v = s_row[d]; s_row[d] = run; run += v; }
+    }
+    __syncthreads();
+    uint32_t run = s_row[threadIdx.x];
+    for (int64_t t = 0; t < nt; ++t) { uint32_t v = row[t]; row[t] = run; run += v; }
+}
+
+__global__ void __launch_bounds__(VH_TPB) k_sort_down(const uint32_t *__restrict__ kin,
+                                                     uint32_t *__restrict__ kout,
+                                                     const uint32_t *__restrict__ tilecnt,
+                                                     const VolScalars *sc, int64_t V,
+                                                     int64_t max_tiles, int shift) {
+    __shared__ uint32_t s_wc[4][256];
+    const int64_t b = blockIdx.y, t = blockIdx.x;
+    const int64_t n = sc[b].n_mask;
+    const int64_t s = t * VH_SORT_TILE;
+    if (s >= n) return;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int d = lane; d < 256; d += 64) s_wc[w][d] = 0;
+    __syncthreads();
+    const uint32_t *k = kin + b * V;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    uint32_t key[VH_SORT_KPT];
+    uint32_t rank[VH_SORT_KPT];
+#pragma unroll
+    for (int r = 0; r < VH_SORT_KPT; ++r) {
+        const int64_t idx = s + (int64_t)w * (VH_SORT_KPT * 64) + r * 64 + lane;
+        const bool valid = idx < n;
+        const uint32_t kk = valid ? k[idx] : 0u;
+        const uint32_t d = (kk >> shift) & 255u;
+        uint64_t peers = __ballot(valid);
+#pragma unroll
+        for (int bit = 0; bit < 8; ++bit) {
+            const uint64_t bb = __ballot(valid && ((d >> bit) & 1u));
+            peers &= ((d >> bit) & 1u) ? bb : ~bb;
+        }
+        const uint32_t below = (uint32_t)__popcll(peers & lt);
+        const uint32_t base = valid ? s_wc[w][d] : 0u;
+        __builtin_amdgcn_wave_barrier();
+        if (valid && below == 0) s_wc[w][d] = base + (uint32_t)__popcll(peers);
+        __builtin_amdgcn_wave_barrier();
+        key[r] = kk;
+        rank[r] = valid ? base + below : 0xffffffffu;
+    }
+    __syncthreads();
+    uint32_t *o = kout + b * V;
+#pragma unroll
+    for (int r = 0; r < VH_SORT_KPT; ++r) {
+        if (rank[r] == 0xffffffffu) continue;
+        const uint32_t d = (key[r] >> shift) & 255u;
+        uint32_t pos = tilecnt[(b * 256 + d) * max_tiles + t] + rank[r];
+        for (int ww = 0; ww < w; ++ww) pos += s_wc[ww][d];
+        o[pos] = key[r];
+    }
+}
+
+// =============================================================================================
+// mean anchor (Vent_Analysis.py:246): np.mean of the sorted float32 list is
+//   float32( float64( serial float32 sum over 8192-chunks of numpy pairwise_sum(chunk) ) / n ).
+// One thread per chunk evaluates numpy's pairwise recursion exactly (explicit stack), then one
+// thread per volume adds the chunk sums in order.  p99 (Vent_Analysis.py:255) is the order
+// statistic sorted[int(n * 0.99)].
+// =============================================================================================
+__device__ float pw_leaf(const uint32_t *a, int64_t n) {
+    if (n < 8) {
+        float res = 0.0f;
+        for (int64_t i = 0; i < n; ++i) res = res + key2f(a[i]);
+        return res;
+    }
+    float r0 = key2f(a[0]), r1 = key2f(a[1]), r2 = key2f(a[2]), r3 = key2f(a[3]);
+    float r4 = key2f(a[4]), r5 = key2f(a[5]), r6 = key2f(a[6]), r7 = key2f(a[7]);
+    int64_t i = 8;
+    const int64_t lim = n - (n % 8);
+    for (; i < lim; i += 8) {
+        r0 = r0 + key2f(a[i + 0]); r1 = r1 + key2f(a[i + 1]);
+        r2 = r2 + key2f(a[i + 2]); r3 = r3 + key2f(a[i + 3]);
+        r4 = r4 + key2f(a[i + 4]); r5 = r5 + key2f(a[i + 5]);
+        r6 = r6 + key2f(a[i + 6]); r7 = r7 + key2f(a[i + 7]);
+    }
+    float res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
+    for (; i < n; ++i) res = res + key2f(a[i]);
+    return res;
+}
+
+__device__ float pw_sum(const uint32_t *a, int64_t n) {
+    // iterative post-order walk of numpy's pairwise_sum recursion (depth <= 8 for n <= 8192)
+    int64_t st_s[12], st_n[12];
+    float st_left[12];
+    int st_stage[12];
+    int sp = 0;
+    st_s[0] = 0; st_n[0] = n; st_stage[0] = 0;
+    for (;;) {
+        if (st_n[sp] <= 128) {
+            float ret = pw_leaf(a + st_s[sp], st_n[sp]);
+            for (;;) {
+                if (sp == 0) return ret;
+                --sp;
+                const int64_t n2 = (st_n[sp] / 2) - ((st_n[sp] / 2) % 8);
+                if (st_stage[sp] == 1) {
+                    st_left[sp] = ret;
+                    st_stage[sp] = 2;
+                    ++sp;
+                    st_s[sp] = st_s[sp - 1] + n2;
+                    st_n[sp] = st_n[sp - 1] - n2;
+                    st_stage[sp] = 0;
+                    break;
+                }
+                ret = st_left[sp] + ret;   // stage 2: left + right
+            }
+        } else {
+            const int64_t n2 = (st_n[sp] / 2) - ((st_n[sp] / 2) % 8);
+            st_stage[sp] = 1;
+            ++sp;
+            st_s[sp] = st_s[sp - 1];
+            st_n[sp] = n2;
+            st_stage[sp] = 0;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(VH_TPB) k_chunk_sums(const uint32_t *__restrict__ keys,
+                                                      const VolScalars *sc, int64_t V,
+                                                      int64_t max_chunks, float *chunk) {
+    const int64_t b = blockIdx.y;
+    const int64_t c = blockIdx.x * (int64_t)VH_TPB + threadIdx.x;
+    const int64_t n = sc[b].n_mask;
+    const int64_t s = c * 8192;
+    if (s >= n) return;
+    const int64_t m = n - s < 8192 ? n - s : 8192;
+    chunk[b * max_chunks + c] = pw_sum(keys + b * V + s, m);
+}
+
+__global__ void k_mean_p99(const uint32_t *__restrict__ keys, const float *chunk,
+                           int64_t max_chunks, int64_t V, int64_t nb, VolScalars *sc) {
+    const int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    const int64_t n = sc[b].n_mask;
+    if (n <= 0) {
+        sc[b].mean_anchor = __int_as_float(0x7fc00000);
+        sc[b].p99 = __int_as_float(0x7fc00000);
+        return;
+    }
+    float S = 0.0f;
+    const int64_t nc = (n + 8191) / 8192;
+    for (int64_t c = 0; c < nc; ++c) S = S + chunk[b * max_chunks + c];
+    sc[b].mean_anchor = (float)((double)S / (double)n);
+    const int64_t i99 = (int64_t)((double)n * 0.99);
+    sc[b].p99 = key2f(keys[b * V + i99]);
+}
+
+// =============================================================================================
+// fused classify tile kernel: mean-anchored threshold (:249) -> 3x3 zero-padded median on the
+// binary map (scipy medfilt2d, :248-249) -> np.gradient border of the defect map (:250) ->
+// linear-binning classes (:256) -> counts (:251,257) (+ optional cohort histogram).
+// Tile = TX rows x TY cols x TZ slices; raw map staged in LDS with a 2-voxel in-plane halo,
+// defect map with a 1-voxel halo.
+// =============================================================================================
+#define CL_TX 8
+#define CL_TY 16
+#define CL_TZMAX 32
+
+__device__ __forceinline__ uint8_t lb_class(float nv) {
+    // (x<=.16)*1 + (.16<x<=.34)*2 + ... + (x>.88)*6, float32 edges; NaN -> 0
+    if (nv <= 0.16f) return 1;
+    if (nv <= 0.34f) return 2;
+    if (nv <= 0.52f) return 3;
+    if (nv <= 0.7f) return 4;
+    if (nv <= 0.88f) return 5;
+    if (nv > 0.88f) return 6;
+    return 0;
+}
+
+template <bool CLASSIFY>
+__global__ void __launch_bounds__(VH_TPB) k_tile(const float *__restrict__ n4,
+                                                const uint8_t *__restrict__ mask,
+                                                const uint8_t *__restrict__ in_bin,
+                                                const VolScalars *__restrict__ sc, float thresh,
+                                                int64_t R, int64_t C, int64_t Z, int64_t V,
+                                                int tz, uint8_t *defect, uint8_t *border,
+                                                uint8_t *lb, unsigned long long *cnt_out,
+                                                uint64_t *cohort, int do_cohort) {
+    extern __shared__ uint8_t lds[];
+    const int64_t b = blockIdx.y;
+    const int64_t ntx = (R + CL_TX - 1) / CL_TX, nty = (C + CL_TY - 1) / CL_TY;
+    int64_t bid = blockIdx.x;
+    const int64_t tix = bid % ntx; bid /= ntx;
+    const int64_t tiy = bid % nty; bid /= nty;
+    const int64_t x0 = tix * CL_TX, y0 = tiy * CL_TY, z0 = bid * tz;
+    const int tzn = (int)(Z - z0 < tz ? Z - z0 : tz);
+    const int EX = CL_TX + 4, EY = CL_TY + 4, DX = CL_TX + 2, DY = CL_TY + 2;
+    uint8_t *raw = lds;                         // [EX][EY][tzn]
+    uint8_t *def = lds + EX * EY * tz;          // [DX][DY][tzn]
+    const float *p4 = CLASSIFY ? n4 + b * V : nullptr;
+    const uint8_t *pm = mask + b * V;
+    float m = 0.0f, p99 = 0.0f;
+    if (CLASSIFY) { m = sc[b].mean_anchor; p99 = sc[b].p99; }
+    if (CLASSIFY) {
+        for (int e = threadIdx.x; e < EX * EY * tzn; e += VH_TPB) {
+            const int ex = e / (EY * tzn), r = e % (EY * tzn), ey = r / tzn, ez = r % tzn;
+            const int64_t x = x0 - 2 + ex, y = y0 - 2 + ey, z = z0 + ez;
+            uint8_t v = 0;
+            if (x >= 0 && x < R && y >= 0 && y < C) {
+                const int64_t i = (x * C + y) * Z + z;
+                if (pm[i]) v = (p4[i] / m) < thresh;   // IEEE f32 division, float32(thresh)
+            }
+            raw[e] = v;
+        }
+        __syncthreads();
+        for (int e = threadIdx.x; e < DX * DY * tzn; e += VH_TPB) {
+            const int dx = e / (DY * tzn), r = e % (DY * tzn), dy = r / tzn, dz = r % tzn;
+            int cnt = 0;
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) cnt += raw[((dx + i) * EY + (dy + j)) * tzn + dz];
+            def[e] = cnt >= 5;
+        }
+    } else {
+        // border of an arbitrary binary volume: stage it as the "defect" map directly
+        const uint8_t *pin = in_bin + b * V;
+        for (int e = threadIdx.x; e < DX * DY * tzn; e += VH_TPB) {
+            const int dx = e / (DY * tzn), r = e % (DY * tzn), dy = r / tzn, dz = r % tzn;
+            const int64_t x = x0 - 1 + dx, y = y0 - 1 + dy, z = z0 + dz;
+            uint8_t v = 0;
+            if (x >= 0 && x < R && y >= 0 && y < C) v = pin[(x * C + y) * Z + z];
+            def[e] = v;
+        }
+    }
+    __syncthreads();
+    unsigned long long n_def = 0, n_lb12 = 0;
+    for (int e = threadIdx.x; e < CL_TX * CL_TY * tzn; e += VH_TPB) {
+        const int ix = e / (CL_TY * tzn), r = e % (CL_TY * tzn), iy = r / tzn, iz = r % tzn;
+        const int64_t x = x0 + ix, y = y0 + iy, z = z0 + iz;
+        if (x >= R || y >= C) continue;
+        const int dx = ix + 1, dy = iy + 1;
+#define DEF(a, c) def[((a) * DY + (c)) * tzn + iz]
+        const uint8_t d = DEF(dx, dy);
+        bool gx, gy;
+        if (x == 0) gx = DEF(dx + 1, dy) != d;
+        else if (x == R - 1) gx = d != DEF(dx - 1, dy);
+        else gx = DEF(dx + 1, dy) != DEF(dx - 1, dy);
+        if (y == 0) gy = DEF(dx, dy + 1) != d;
+        else if (y == C - 1) gy = d != DEF(dx, dy - 1);
+        else gy = DEF(dx, dy + 1) != DEF(dx, dy - 1);
+#undef DEF
+        const int64_t i = b * V + (x * C + y) * Z + z;
+        border[i] = gx || gy;
+        if (CLASSIFY) {
+            defect[i] = d;
+            n_def += d;
+            uint8_t cls = 0;
+            const uint8_t mk = pm[(x * C + y) * Z + z];
+            if (mk) {
+                const float nv = p4[(x * C + y) * Z + z] / p99;
+                cls = lb_class(nv);
+                if (do_cohort && nv >= 0.0f && nv < 1.5f) {
+                    int bi = (int)(nv * ((float)VH_COHORT_BINS / 1.5f));
+                    bi = bi > VH_COHORT_BINS - 1 ? VH_COHORT_BINS - 1 : bi;
+                    atomicAdd((unsigned long long *)&cohort[bi], 1ull);
+                }
+            }
+            lb[i] = cls;
+            n_lb12 += (cls == 1 || cls == 2);
+        }
+    }
+    if (CLASSIFY) {
+        // wave reduce, one atomic per wave
+        for (int off = 32; off > 0; off >>= 1) {
+            n_def += __shfl_down(n_def, off, 64);
+            n_lb12 += __shfl_down(n_lb12, off, 64);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            if (n_def) atomicAdd(&cnt_out[b * 2 + 0], n_def);
+            if (n_lb12) atomicAdd(&cnt_out[b * 2 + 1], n_lb12);
+        }
+    }
+}
+
+__global__ void k_counts_to_scalars(const unsigned long long *cnt, int64_t nb, VolScalars *sc) {
+    int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    sc[b].n_defect = (int64_t)cnt[b * 2];
+    sc[b].n_lb12 = (int64_t)cnt[b * 2 + 1];
+}
+
+static void tile_geometry(const vh_batch *b, int &tz, dim3 &grid, size_t &lds) {
+    tz = (int)(b->Z < CL_TZMAX ? b->Z : CL_TZMAX);
+    const int64_t ntx = (b->R + CL_TX - 1) / CL_TX, nty = (b->C + CL_TY - 1) / CL_TY;
+    const int64_t ntz = (b->Z + tz - 1) / tz;
+    grid = dim3((unsigned)(ntx * nty * ntz), (unsigned)b->nb, 1);
+    lds = (size_t)(CL_TX + 4) * (CL_TY + 4) * tz + (size_t)(CL_TX + 2) * (CL_TY + 2) * tz;
+}
+
+void vh_launch_border(vh_batch *b, const uint8_t *d_in, uint8_t *d_out) {
+    int tz; dim3 grid; size_t lds;
+    tile_geometry(b, tz, grid, lds);
+    ScopedKTimer tm(b, "border", 2.0 * (double)b->V);
+    k_tile<false><<<grid, VH_TPB, lds, b->ctx->stream>>>(nullptr, b->d_mask, d_in, b->d_sc, 0.f,
+                                                         b->R, b->C, b->Z, b->V, tz, nullptr,
+                                                         d_out, nullptr, nullptr, nullptr, 0);
+    VH_CHECK_LAUNCH();
+}
+
+// =============================================================================================
+// k-means VDP (build-defined): 1-D Lloyd, k = 4, on the sorted masked N4
+// values; centres start at sorted[floor(n (2j+1) / 2k)]; a value joins the nearest centre (ties
+// to the lower); iterate until the partition is stable (<= 300).  One block per volume.
+// =============================================================================================
+#define KM_K 4
+__global__ void __launch_bounds__(VH_TPB) k_kmeans(const uint32_t *__restrict__ keys,
+                                                  int64_t V, VolScalars *sc) {
+    __shared__ double s_c[KM_K];
+    __shared__ int64_t s_cut[KM_K + 1], s_new[KM_K + 1];
+    __shared__ double s_part[KM_K][VH_TPB];
+    __shared__ int s_done;
+    const int64_t b = blockIdx.x;
+    const int64_t n = sc[b].n_mask;
+    const uint32_t *k = keys + b * V;
+    const int t = threadIdx.x;
+    if (n <= 0) return;
+    if (t < KM_K) s_c[t] = (double)key2f(k[(n * (2 * t + 1)) / (2 * KM_K)]);
+    if (t == 0) { s_cut[0] = -1; s_done = 0; }
+    __syncthreads();
+    const int64_t per = (n + VH_TPB - 1) / VH_TPB;
+    const int64_t cs = t * per, ce = cs + per < n ? cs + per : n;
+    int it = 0;
+    for (it = 1; it <= 300; ++it) {
+        if (t < KM_K - 1) {
+            // first index whose value is strictly closer to c[t+1] than to c[t]
+            const double clo = s_c[t], chi = s_c[t + 1];
+            int64_t lo = 0, hi = n;
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) >> 1;
+                const double x = (double)key2f(k[mid]);
+                if (fabs(x - chi) < fabs(x - clo)) hi = mid; else lo = mid + 1;
+            }
+            s_new[t + 1] = lo;
+        }
+        __syncthreads();
+        if (t == 0) {
+            s_new[0] = 0;
+            s_new[KM_K] = n;
+            for (int j = 2; j < KM_K; ++j)
+                if (s_new[j] < s_new[j - 1]) s_new[j] = s_new[j - 1];
+            bool same = true;
+            for (int j = 0; j <= KM_K; ++j) same = same && s_new[j] == s_cut[j];
+            s_done = same;
+            for (int j = 0; j <= KM_K; ++j) s_cut[j] = s_new[j];
+        }
+        __syncthreads();
+        if (s_done) break;
+        double acc[KM_K] = {0.0, 0.0, 0.0, 0.0};
+        for (int64_t i = cs; i < ce; ++i) {
+            const double x = (double)key2f(k[i]);
+            int j = 0;
+            while (j < KM_K - 1 && i >= s_cut[j + 1]) ++j;
+            acc[j] += x;
+        }
+        for (int j = 0; j < KM_K; ++j) s_part[j][t] = acc[j];
+        __syncthreads();
+        if (t < KM_K) {
+            double s = 0.0;
+            for (int i = 0; i < VH_TPB; ++i) s += s_part[t][i];
+            const int64_t cnt = s_cut[t + 1] - s_cut[t];
+            if (cnt > 0) s_c[t] = s / (double)cnt;
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        sc[b].n_km0 = s_cut[1] - s_cut[0];
+        sc[b].km_iters = it;
+        for (int j = 0; j < KM_K; ++j) sc[b].km_c[j] = s_c[j];
+    }
+}
+
+// =============================================================================================
+// SNR (Vent_Analysis.py:337-357): signal = A[mask>0]; noise = A outside the ix_(rr, cc, ss) box and
+// outside the first/last 20 rows.  Per-block double partials (fixed order), then a finish kernel.
+// =============================================================================================
+__global__ void __launch_bounds__(VH_TPB) k_snr(const float *__restrict__ hp,
+                                               const uint8_t *__restrict__ mask,
+                                               const uint8_t *rowany, const uint8_t *sliceany,
+                                               const VolScalars *sc, int64_t R, int64_t C,
+                                               int64_t Z, int64_t V, int64_t nparts,
+                                               double *part) {
+    // column sweep: one thread per (col, slice), rows walked in order
+    __shared__ double s_red[4][VH_TPB / 64];
+    const int64_t b = blockIdx.y;
+    const int64_t CZ = C * Z;
+    const int64_t col = blockIdx.x * (int64_t)VH_TPB + threadIdx.x;
+    const VolScalars s = sc[b];
+    double ssig = 0.0, sn = 0.0, sn2 = 0.0, nn = 0.0;
+    const int64_t FOV = 20;
+    if (col < CZ) {
+        const int64_t y = col / Z, z = col % Z;
+        const bool cin = y >= s.cmin && y < s.cmax;
+        const bool sin_ = sliceany[b * Z + z] || (z == 0 && s.any_slice_empty);
+        const float *a = hp + b * V + col;
+        const uint8_t *m = mask + b * V + col;
+        for (int64_t x = 0; x < R; ++x) {
+            const float v = a[x * CZ];
+            if (m[x * CZ]) ssig += (double)v;
+            if (x < FOV || x >= R - FOV) continue;
+            const bool rin = rowany[b * R + x] || (x == 0 && s.any_row_empty);
+            if (!(rin && cin && sin_)) { sn += (double)v; sn2 += (double)v * (double)v; nn += 1.0; }
+        }
+    }
+    double v[4] = {ssig, sn, sn2, nn};
+    for (int q = 0; q < 4; ++q) {
+        double x = v[q];
+        for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
+        if ((threadIdx.x & 63) == 0) s_red[q][threadIdx.x >> 6] = x;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        double x = 0.0;
+        for (int w = 0; w < VH_TPB / 64; ++w) x += s_red[threadIdx.x][w];
+        part[(b * nparts + blockIdx.x) * 4 + threadIdx.x] = x;
+    }
+}
+
+__global__ void k_snr_finish(const double *part, int64_t nparts, int64_t nb, VolScalars *sc) {
+    const int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (b >= nb) return;
+    double a[4] = {0, 0, 0, 0};
+    for (int64_t p = 0; p < nparts; ++p)
+        for (int q = 0; q < 4; ++q) a[q] += part[(b * nparts + p) * 4 + q];
+    const double nsig = (double)sc[b].n_mask;
+    if (!sc[b].snr_ok || a[3] <= 0.0 || nsig <= 0.0) {
+        sc[b].snr = __longlong_as_double(0x7ff8000000000000ll);
+        return;
+    }
+    // (mean(signal) - mean(noise)) / std(noise), ddof 0, double accumulation
+    const double ms = a[0] / nsig;
+    const double mn = a[1] / a[3];
+    double var = a[2] / a[3] - mn * mn;
+    if (var < 0.0) var = 0.0;
+    sc[b].snr = (ms - mn) / sqrt(var);
+}
+
+void vh_launch_snr(vh_batch *b) {
+    hipStream_t st = b->ctx->stream;
+    const int64_t nparts = (b->CZ + VH_TPB - 1) / VH_TPB;
+    ScopedKTimer tm(b, "snr", 5.0 * (double)b->V);
+    k_snr<<<col_grid(b), VH_TPB, 0, st>>>(
+        b->d_hp, b->d_mask, b->d_rowany, b->d_sliceany, b->d_sc, b->R, b->C, b->Z, b->V, nparts,
+        b->d_part);
+    VH_CHECK_LAUNCH();
+    k_snr_finish<<<(unsigned)((b->nb + 63) / 64), 64, 0, st>>>(b->d_part, nparts, b->nb, b->d_sc);
+    VH_CHECK_LAUNCH();
+}
+
+// =============================================================================================
+// the chain
+// =============================================================================================
+void vh_launch_vdp_chain(vh_batch *b, const float *d_n4, const vh_run_opts &o) {
+    hipStream_t st = b->ctx->stream;
+    const int64_t CZ = b->CZ;
+    {
+        ScopedKTimer tm(b, "gather", 5.0 * (double)b->V);
+        k_gather<<<col_grid(b), VH_TPB, 0, st>>>(d_n4, b->d_mask, b->d_colrange, b->d_colstart,
+                                                 CZ, b->V, b->d_keys0);
+        VH_CHECK_LAUNCH();
+    }
+    {
+        ScopedKTimer tm(b, "sort", 0.0);
+        uint32_t *kin = b->d_keys0, *kout = b->d_keys1;
+        const dim3 tg((unsigned)b->max_tiles, (unsigned)b->nb);
+        for (int pass = 0; pass < 4; ++pass) {
+            const int shift = 8 * pass;
+            k_sort_up<<<tg, VH_TPB, 0, st>>>(kin, b->d_sc, b->V, b->max_tiles, shift, b->d_tilecnt);
+            VH_CHECK_LAUNCH();
+            k_sort_scan<<<(unsigned)b->nb, VH_TPB, 0, st>>>(b->d_tilecnt, b->d_sc, b->max_tiles);
+            VH_CHECK_LAUNCH();
+            k_sort_down<<<tg, VH_TPB, 0, st>>>(kin, kout, b->d_tilecnt, b->d_sc, b->V,
+                                               b->max_tiles, shift);
+            VH_CHECK_LAUNCH();
+            uint32_t *t = kin; kin = kout; kout = t;
+        }
+    }
+    {
+        const int64_t max_chunks = (b->V + 8191) / 8192;
+        float *chunk = reinterpret_cast<float *>(b->d_part);   // part holds >= nb*max_chunks floats
+        k_chunk_sums<<<dim3((unsigned)((max_chunks + VH_TPB - 1) / VH_TPB), (unsigned)b->nb),
+                       VH_TPB, 0, st>>>(b->d_keys0, b->d_sc, b->V, max_chunks, chunk);
+        VH_CHECK_LAUNCH();
+        k_mean_p99<<<(unsigned)((b->nb + 63) / 64), 64, 0, st>>>(b->d_keys0, chunk, max_chunks,
+                                                                  b->V, b->nb, b->d_sc);
+        VH_CHECK_LAUNCH();
+    }
+    {
+        unsigned long long *cnt = reinterpret_cast<unsigned long long *>(b->d_tilecnt);
+        HIP_TRY(hipMemsetAsync(cnt, 0, sizeof(unsigned long long) * 2 * b->nb, st));
+        int tz; dim3 grid; size_t lds;
+        tile_geometry(b, tz, grid, lds);
+        {
+            ScopedKTimer tm(b, "classify", 8.0 * (double)b->V);
+            k_tile<true><<<grid, VH_TPB, lds, st>>>(d_n4, b->d_mask, nullptr, b->d_sc, o.thresh,
+                                                    b->R, b->C, b->Z, b->V, tz, b->d_defect,
+                                                    b->d_border, b->d_lb, cnt, b->d_cohort,
+                                                    o.do_cohort);
+            VH_CHECK_LAUNCH();
+        }
+        k_counts_to_scalars<<<(unsigned)((b->nb + 63) / 64), 64, 0, st>>>(cnt, b->nb, b->d_sc);
+        VH_CHECK_LAUNCH();
+    }
+    if (o.do_kmeans) {
+        ScopedKTimer tm(b, "kmeans", 0.0);
+        k_kmeans<<<(unsigned)b->nb, VH_TPB, 0, st>>>(b->d_keys0, b->V, b->d_sc);
+        VH_CHECK_LAUNCH();
+    }
+    if (o.do_snr) vh_launch_snr(b);
+}

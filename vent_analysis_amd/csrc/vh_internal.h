@@ -1,0 +1,181 @@
+// Internal declarations shared by the libventhip translation units (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/vent_hip.h"
+
+#define VH_TPB 256          // threads per block for streaming kernels (4 waves of 64)
+#define VH_WAVE 64
+#define VH_SORT_TILE 4096   // keys per radix-sort tile (256 threads x 16 keys)
+#define VH_SORT_KPT 16
+#define VH_MAX_LEVELS 8
+#define VH_FFT_P 512
+#define VH_MAX_BINS 256
+
+struct VhError {
+    int code;
+    std::string msg;
+};
+
+#define HIP_TRY(expr)                                                                       \
+    do {                                                                                    \
+        hipError_t _e = (expr);                                                             \
+        if (_e != hipSuccess)                                                               \
+            throw VhError{_e == hipErrorOutOfMemory ? VH_ERR_NOMEM : VH_ERR_HIP,            \
+                          std::string(#expr) + ": " + hipGetErrorString(_e)};               \
+    } while (0)
+
+#define VH_CHECK_LAUNCH() HIP_TRY(hipGetLastError())
+
+// Per-volume device scalars (one record per study).
+struct VolScalars {
+    int64_t n_mask;          // mask != 0
+    int64_t n_mask1;         // mask == 1 (N4 label, LungVolume)
+    int64_t first_masked;    // raster index of the first mask==1 voxel (N4 bin-range quirk)
+    int64_t n_defect;
+    int64_t n_lb12;
+    int64_t n_km0;
+    float mean_anchor;
+    float p99;
+    double snr;
+    int32_t km_iters;
+    int32_t pad0;
+    double km_c[4];
+    int32_t cmin, cmax;      // SNR column box [cmin, cmax)
+    int32_t any_row_empty, any_slice_empty;
+    int32_t snr_ok;          // 0 when the reference would raise (no masked column > 0)
+    int32_t ci_status;       // VH_OK / VH_ERR_MAXRADIUS
+    int64_t n_ci;            // defect voxels for CI
+    double ci_scalar;
+};
+
+// Per-volume N4 iteration state.
+struct N4State {
+    float bin_min, bin_max, slope;
+    int32_t active;          // 1 while the current level is still iterating
+    int32_t iters;           // iterations executed in the current level
+    int32_t need_exact_min;  // bin-range quirk: first masked pixel is the strict minimum
+    uint32_t umax_key, umin_key;  // sortable keys: max over all masked, min over all but first
+    float u_first;
+    double conv;
+    int32_t iters_level[VH_MAX_LEVELS];
+    float conv_level[VH_MAX_LEVELS];
+};
+
+// Per-axis, per-level B-spline tables (host-built, identical to oracle/n4_oracle.c).
+struct AxisTab {
+    int32_t n, ncp;
+    std::vector<int32_t> base;
+    std::vector<float> w;      // [n][4]
+    std::vector<double> sw2;   // [n]
+};
+
+struct KTimer {
+    std::vector<hipEvent_t> ev;   // pairs (start, stop)
+    double bytes_per_launch = 0;
+    double total_ms = 0;
+    int64_t launches = 0;
+};
+
+struct vh_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string last_error;
+    void *comm = nullptr;           // ncclComm_t
+    int nranks = 1, rank = 0;
+    // pinned scratch for small readbacks
+    int32_t *h_pinned = nullptr;
+};
+
+struct vh_batch {
+    vh_ctx *ctx = nullptr;
+    int64_t R = 0, C = 0, Z = 0, V = 0, nb = 0, CZ = 0;
+    int64_t max_tiles = 0;
+    // inputs / outputs
+    float *d_hp = nullptr;
+    uint8_t *d_mask = nullptr;
+    float *d_n4 = nullptr;
+    uint8_t *d_defect = nullptr, *d_border = nullptr, *d_lb = nullptr;
+    // mask statistics
+    int32_t *d_colrange = nullptr;   // [nb][CZ][2]  first/last masked row of each (col, slice) column
+    int32_t *d_colcount = nullptr;   // [nb][CZ]
+    int64_t *d_colstart = nullptr;   // [nb][CZ]     exclusive prefix of colcount
+    uint8_t *d_rowany = nullptr, *d_colany = nullptr, *d_sliceany = nullptr;
+    VolScalars *d_sc = nullptr;
+    double *d_part = nullptr;        // [nb][part_blocks][4] deterministic partial sums
+    int64_t part_blocks = 0;
+    // sort
+    uint32_t *d_keys0 = nullptr, *d_keys1 = nullptr;
+    uint32_t *d_tilecnt = nullptr;   // [nb][256][max_tiles]
+    // cohort
+    uint64_t *d_cohort = nullptr;
+    // N4 workspace
+    float *d_L0 = nullptr, *d_B = nullptr, *d_lat = nullptr, *d_E = nullptr;
+    double *d_Q1 = nullptr, *d_Q2 = nullptr, *d_P1 = nullptr, *d_num = nullptr, *d_den = nullptr;
+    uint64_t *d_hist = nullptr;
+    N4State *d_st = nullptr;
+    int32_t *d_nactive = nullptr;
+    void *d_tabs = nullptr;          // device copy of all per-level axis tables
+    int64_t lat_cap = 0, q1_cap = 0, q2_cap = 0, p1_cap = 0;
+    std::vector<size_t> tab_off;     // offsets of each (level, axis) table in d_tabs
+    vh_n4_params tab_prm{};          // parameters the tables were built for
+    bool tabs_valid = false;
+    double2 *d_twiddle = nullptr;    // FFT twiddles (host-computed)
+    // CI workspace
+    uint32_t *d_bitmap = nullptr;    // [nb][ceil(V/32)] Fortran-order defect bits
+    int32_t *d_ci_list = nullptr;    // [nb][V] defect voxel raster indices (compacted)
+    int32_t *d_ci_shell = nullptr;   // [nb][V]
+    uint32_t *d_ci_hist = nullptr;   // [nb][ci_nb]
+    int64_t ci_nb_cap = 0;
+    // timing
+    bool profile = false;
+    std::map<std::string, KTimer> timers;
+    // last run options
+    vh_run_opts opts{};
+    bool have_result = false;
+};
+
+// ---- timing helper ----------------------------------------------------------------------------
+struct ScopedKTimer {
+    vh_batch *b;
+    KTimer *t;
+    hipEvent_t e1 = nullptr;
+    ScopedKTimer(vh_batch *bb, const char *name, double bytes);
+    ~ScopedKTimer();
+};
+
+// ---- launchers (defined in vdp.hip / n4.hip / ci.hip) ---------------------------------------
+void vh_launch_mask_stats(vh_batch *b);
+void vh_launch_vdp_chain(vh_batch *b, const float *d_n4, const vh_run_opts &o);
+void vh_launch_snr(vh_batch *b);
+void vh_launch_border(vh_batch *b, const uint8_t *d_in, uint8_t *d_out);
+void vh_launch_n4(vh_batch *b, const vh_n4_params &prm);
+void vh_n4_prepare_tables(vh_batch *b, const vh_n4_params &prm);
+void vh_ci_run(vh_batch *b, const int16_t *offs, const uint8_t *dup, int64_t rows,
+               const int32_t *bounds, const double *radii, int64_t nb_shell, double minvox,
+               double *d_ci);
+void vh_ensure_n4_workspace(vh_batch *b, const vh_n4_params &prm);
+
+// ---- shared host helpers ----------------------------------------------------------------------
+void vh_axis_tables(int n, int ncp, float eps, AxisTab &t);
+float vh_bspline_eps(int max_spans);
+
+inline dim3 col_grid(const vh_batch *b) {
+    return dim3((unsigned)((b->CZ + VH_TPB - 1) / VH_TPB), (unsigned)b->nb, 1);
+}
+
+// ---- device helpers ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t f2key(float f) {
+    uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float key2f(uint32_t k) {
+    uint32_t u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
+    return __uint_as_float(u);
+}
