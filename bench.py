@@ -158,6 +158,7 @@ def main():
 
     for _ in range(args.warmup):
         step(warm)
+    Bt.reset_timers()
     if dist:
         dist.barrier()
     sync_dev()

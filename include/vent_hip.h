@@ -134,6 +134,8 @@ int vh_batch_cohort_hist(vh_batch *b, uint64_t *hist /* [VH_COHORT_BINS] */);
 /* Kernel-class timing from HIP events on the context stream (opts.profile = 1).  name is one of
  * the classes listed by vh_batch_kernel_names (';'-separated). */
 const char *vh_batch_kernel_names(void);
+/* Discard accumulated kernel timings (timings accumulate over vh_batch_run calls). */
+int vh_batch_reset_timers(vh_batch *b);
 int vh_batch_kernel_time(vh_batch *b, const char *name, double *total_ms, int64_t *launches,
                          double *bytes_per_launch);
 

@@ -1,0 +1,83 @@
+"""CPU: known-answer tests for the N4 restatement.  SimpleITK is not
+installable offline, so N4 parity with the reference is UNPINNED; these tests pin the oracle's
+behaviour to properties any correct N4 has, and the GPU is then checked against the oracle."""
+import numpy as np
+import pytest
+
+from oracle import native
+from vent_analysis_amd.synth import synth_volume
+
+
+def log_slope(img, mask, R, sel=None):
+    i = np.broadcast_to(np.arange(R)[:, None, None], img.shape)
+    sel = (mask > 0) if sel is None else sel
+    return np.polyfit(i[sel], np.log(img[sel]), 1)[0] * R
+
+
+def phantom(R=64, C=64, Z=16, seed=0, amp=0.5):
+    """Two-class piecewise-constant tissue times a smooth multiplicative bias exp(b)."""
+    rng = np.random.default_rng(seed)
+    i, j, k = np.meshgrid(np.arange(R), np.arange(C), np.arange(Z), indexing="ij")
+    mask = (((i - R / 2) / (0.4 * R)) ** 2 + ((j - C / 2) / (0.4 * C)) ** 2 +
+            ((k - Z / 2) / (0.45 * Z)) ** 2) <= 1
+    tissue = np.where((i // 8 + j // 8) % 2 == 0, 100.0, 160.0)
+    b = amp * (i / R - 0.5) + 0.3 * amp * np.sin(np.pi * j / C)
+    img = (tissue * np.exp(b) * (1 + 0.01 * rng.standard_normal(mask.shape))).astype(np.float32)
+    img[~mask] = rng.rayleigh(5, (~mask).sum()).astype(np.float32)
+    return img, mask.astype(np.uint8), b
+
+
+def test_removes_smooth_bias():
+    X, M = synth_volume(64, 64, 16, 0)
+    out, its, conv = native.n4(X, M)
+    healthy = (M > 0) & (X > 100)          # exclude the x0.2 ventilation defects
+    assert abs(log_slope(X, M, 64, healthy)) > 0.3
+    assert abs(log_slope(out, M, 64, healthy)) < 0.05 * abs(log_slope(X, M, 64, healthy))
+
+
+def test_recovers_phantom_bias_up_to_constant():
+    img, mask, b = phantom()
+    out, its, _ = native.n4(img, mask)
+    sel = mask > 0
+    est = np.log(img[sel]) - np.log(out[sel])          # estimated log bias at masked voxels
+    err = (est - est.mean()) - (b[sel] - b[sel].mean())
+    assert np.std(err) < 0.25 * np.std(b[sel])
+
+
+def test_iteration_counts_and_convergence():
+    X, M = synth_volume(64, 64, 16, 1)
+    out, its, conv = native.n4(X, M)
+    assert np.all((its >= 1) & (its <= 50))
+    for n, c in zip(its, conv):
+        assert n == 50 or c <= 0.001
+
+
+def test_max_iters_respected():
+    X, M = synth_volume(48, 48, 12, 2)
+    out, its, conv = native.n4(X, M, max_iters=(3, 2), conv_threshold=0.0)
+    assert list(its) == [3, 2]
+
+
+def test_scale_covariance():
+    """N4(k I) = k N4(I): log(kI) shifts U by log k, which shifts the histogram range and the E map
+    by the same amount, so residuals, lattice and bias are unchanged."""
+    X, M = synth_volume(64, 64, 16, 3)
+    a, ia, _ = native.n4(X, M)
+    b, ib, _ = native.n4(X * np.float32(4.0), M)
+    assert list(ia) == list(ib)
+    assert np.max(np.abs(b / 4.0 - a) / a) < 1e-4
+
+
+def test_output_outside_mask_is_bias_corrected_too():
+    X, M = synth_volume(48, 48, 12, 4)
+    out, _, _ = native.n4(X, M)
+    ratio = X / out                                   # = exp(B) everywhere
+    assert np.all(np.isfinite(ratio)) and np.all(ratio > 0)
+    assert not np.allclose(ratio[M == 0], 1.0)
+
+
+def test_deterministic():
+    X, M = synth_volume(48, 48, 12, 5)
+    a = native.n4(X, M)[0]
+    b = native.n4(X, M)[0]
+    assert np.array_equal(a, b)

@@ -73,6 +73,7 @@ _SIGS = {
     "vh_batch_download": ([_P, _P, _P, _P, _P, _P], ct.c_int),
     "vh_batch_cohort_hist": ([_P, _P], ct.c_int),
     "vh_batch_kernel_names": ([], ct.c_char_p),
+    "vh_batch_reset_timers": ([_P], ct.c_int),
     "vh_batch_kernel_time": ([_P, ct.c_char_p, ct.POINTER(ct.c_double), ct.POINTER(ct.c_int64),
                               ct.POINTER(ct.c_double)], ct.c_int),
     "vh_comm_unique_id": ([_P], ct.c_int),
@@ -333,6 +334,9 @@ class Batch:
 
     def cohort_allreduce(self):
         self.ctx.check(self.L.vh_batch_cohort_allreduce(self.h), "vh_batch_cohort_allreduce")
+
+    def reset_timers(self):
+        self.ctx.check(self.L.vh_batch_reset_timers(self.h), "vh_batch_reset_timers")
 
     def kernel_time(self, name):
         ms, n, by = ct.c_double(0), ct.c_int64(0), ct.c_double(0)

@@ -96,7 +96,7 @@ static void batch_free(vh_batch *b) {
     clear_timers(b);
     dfree(b->d_hp); dfree(b->d_mask); dfree(b->d_n4);
     dfree(b->d_defect); dfree(b->d_border); dfree(b->d_lb);
-    dfree(b->d_colrange); dfree(b->d_colcount); dfree(b->d_colstart);
+    dfree(b->d_colrange); dfree(b->d_colcount); dfree(b->d_colstart); dfree(b->d_colbits);
     dfree(b->d_rowany); dfree(b->d_colany); dfree(b->d_sliceany);
     dfree(b->d_sc); dfree(b->d_part); dfree(b->d_keys0); dfree(b->d_keys1); dfree(b->d_tilecnt);
     dfree(b->d_cohort);
@@ -126,6 +126,7 @@ static vh_batch *batch_new(vh_ctx *ctx, int64_t R, int64_t C, int64_t Z, int64_t
         dalloc(&b->d_lb, NV);
         dalloc(&b->d_colrange, (size_t)nb * b->CZ * 2);
         dalloc(&b->d_colcount, (size_t)nb * b->CZ);
+        dalloc(&b->d_colbits, (size_t)nb * ((R + 31) / 32) * b->CZ);
         dalloc(&b->d_colstart, (size_t)nb * b->CZ);
         dalloc(&b->d_rowany, (size_t)nb * R);
         dalloc(&b->d_colany, (size_t)nb * C);
@@ -157,10 +158,8 @@ static void batch_upload(vh_batch *b, const float *hp, const uint8_t *mask) {
 // n4_src: 0 = run N4 from d_hp, 1 = identity (d_hp), 2 = caller-uploaded d_n4
 static void batch_run(vh_batch *b, const vh_run_opts &o, int n4_src) {
     HIP_TRY(hipSetDevice(b->ctx->device));
-    clear_timers(b);
     b->profile = o.profile != 0;
     b->opts = o;
-    hipStream_t st = b->ctx->stream;
     if (o.do_n4) {
         if (o.n4.n_levels < 1 || o.n4.n_levels > VH_MAX_LEVELS || o.n4.spline_order != 3 ||
             o.n4.n_bins < 2 || o.n4.n_bins > VH_MAX_BINS || o.n4.ncp[0] < 4 || o.n4.ncp[1] < 4 ||
@@ -174,7 +173,6 @@ static void batch_run(vh_batch *b, const vh_run_opts &o, int n4_src) {
         if (tot > 8 * 1024 - 1) throw VhError{VH_ERR_ARG, "too many N4 iterations"};
     }
     vh_launch_mask_stats(b);
-    if (o.do_cohort) HIP_TRY(hipMemsetAsync(b->d_cohort, 0, sizeof(uint64_t) * VH_COHORT_BINS, st));
     const float *n4 = b->d_hp;
     if (o.do_n4) {
         vh_launch_n4(b, o.n4);
@@ -518,8 +516,15 @@ int vh_batch_cohort_hist(vh_batch *b, uint64_t *hist) {
 }
 
 const char *vh_batch_kernel_names(void) {
-    return "mask_stats;gather;sort;classify;kmeans;snr;border;n4_init;n4_den;n4_hist;n4_fit;"
-           "n4_contract;n4_eval;n4_final;ci_walk";
+    return "mask_stats;gather;sort;classify;cohort;kmeans;snr;border;n4_init;n4_den;n4_hist;"
+           "n4_fit;n4_contract;n4_eval;n4_final;ci_walk";
+}
+
+int vh_batch_reset_timers(vh_batch *b) {
+    API_TRY(b->ctx, {
+        HIP_TRY(hipStreamSynchronize(b->ctx->stream));
+        clear_timers(b);
+    })
 }
 
 int vh_batch_kernel_time(vh_batch *b, const char *name, double *total_ms, int64_t *launches,

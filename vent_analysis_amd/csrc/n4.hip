@@ -232,32 +232,79 @@ __global__ void k_n4_state_init(N4State *st, int64_t nb) {
     st[b] = s;
 }
 
-// L0 = log(I) at mask == 1 (non-positive -> 0), B = 0, and the first U range.
+// ---------------------------------------------------------------------------------------------
+// column-sweep scaffolding.  A lane owns one (col, slice) column; the wave walks the UNION of its
+// lanes' masked row ranges in aligned chunks of 8 rows (row index wave-uniform, so the B-spline
+// row weights are scalar loads), each lane predicating on its column's mask==1 row bitmap.  All 8
+// rows' loads of a chunk are issued before any is used (memory-level parallelism).
+// ---------------------------------------------------------------------------------------------
+#define SW_CHUNK 8
+
+struct ColSweep {
+    int64_t col;      // column index in the volume (valid iff col < CZ)
+    bool valid;
+    int wlo, whi;     // wave-uniform row range (wlo > whi: nothing to do)
+};
+
+__device__ __forceinline__ ColSweep col_sweep_begin(const int32_t *colrange, int64_t b,
+                                                    int64_t CZ, int64_t R) {
+    ColSweep s;
+    s.col = blockIdx.x * (int64_t)VH_TPB + threadIdx.x;
+    s.valid = s.col < CZ;
+    int lo = (int)R, hi = -1;
+    if (s.valid) {
+        lo = colrange[(b * CZ + s.col) * 2];
+        hi = colrange[(b * CZ + s.col) * 2 + 1];
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        lo = min(lo, __shfl_xor(lo, off, 64));
+        hi = max(hi, __shfl_xor(hi, off, 64));
+    }
+    s.wlo = __builtin_amdgcn_readfirstlane(lo);
+    s.whi = __builtin_amdgcn_readfirstlane(hi);
+    return s;
+}
+
+__device__ __forceinline__ uint32_t chunk_bits(const uint32_t *colbits, const ColSweep &s,
+                                               int64_t b, int64_t nw, int64_t CZ, int x0) {
+    if (!s.valid) return 0u;
+    const uint32_t w = colbits[(b * nw + (x0 >> 5)) * CZ + s.col];
+    return (w >> (x0 & 31)) & 0xffu;
+}
+
+// L0 = log(I) at mask == 1 (non-positive -> 0), B = 0, U = L0 and the first U range.
 __global__ void __launch_bounds__(VH_TPB) k_n4_init(const float *__restrict__ I,
-                                                   const uint8_t *__restrict__ mask,
+                                                   const uint32_t *__restrict__ colbits,
                                                    const int32_t *colrange,
-                                                   const VolScalars *sc, int64_t CZ, int64_t V,
-                                                   float *L0, float *B, N4State *st) {
+                                                   const VolScalars *sc, int64_t R, int64_t CZ,
+                                                   int64_t V, float *L0, float *B, float *U,
+                                                   N4State *st) {
     __shared__ uint32_t s_max, s_min;
     const int64_t b = blockIdx.y;
-    const int64_t col = blockIdx.x * (int64_t)VH_TPB + threadIdx.x;
     if (threadIdx.x == 0) { s_max = 0u; s_min = 0xffffffffu; }
     __syncthreads();
+    const ColSweep cs = col_sweep_begin(colrange, b, CZ, R);
+    const int64_t nw = (R + 31) >> 5;
+    const int64_t first = sc[b].first_masked;
     uint32_t kmax = 0u, kmin = 0xffffffffu;
-    if (col < CZ) {
-        const int32_t lo = colrange[(b * CZ + col) * 2], hi = colrange[(b * CZ + col) * 2 + 1];
-        const int64_t first = sc[b].first_masked;
-        for (int64_t x = lo; x <= hi; ++x) {
-            const int64_t r = x * CZ + col, v = b * V + r;
-            if (mask[v] != 1) continue;
-            const float a = I[v];
-            const float l = a > 0.0f ? (float)log((double)a) : 0.0f;
+    for (int x0 = cs.wlo & ~(SW_CHUNK - 1); x0 <= cs.whi; x0 += SW_CHUNK) {
+        const uint32_t m8 = chunk_bits(colbits, cs, b, nw, CZ, x0);
+        float a[SW_CHUNK];
+#pragma unroll
+        for (int k = 0; k < SW_CHUNK; ++k)
+            a[k] = (m8 >> k) & 1u ? I[b * V + (int64_t)(x0 + k) * CZ + cs.col] : 0.0f;
+#pragma unroll
+        for (int k = 0; k < SW_CHUNK; ++k) {
+            if (!((m8 >> k) & 1u)) continue;
+            const int64_t r = (int64_t)(x0 + k) * CZ + cs.col, v = b * V + r;
+            const float l = a[k] > 0.0f ? (float)log((double)a[k]) : 0.0f;
             L0[v] = l;
             B[v] = 0.0f;
-            const uint32_t k = f2key(l);
-            kmax = k > kmax ? k : kmax;
+            U[v] = l;
+            const uint32_t key = f2key(l);
+            kmax = key > kmax ? key : kmax;
             if (r == first) st[b].u_first = l;
-            else kmin = k < kmin ? k : kmin;
+            else kmin = key < kmin ? key : kmin;
         }
     }
     if (kmax) atomicMax(&s_max, kmax);
@@ -324,8 +371,7 @@ __global__ void k_n4_level_end(N4State *st, const double *part, int64_t nparts,
 
 // Exact ITK bin minimum when the first masked pixel is the strict minimum: min over the pixels
 // that are not running maxima in raster order (chunked prefix-max scan).  One block per volume.
-__global__ void __launch_bounds__(VH_TPB) k_n4_exact_min(const float *__restrict__ L0,
-                                                        const float *__restrict__ B,
+__global__ void __launch_bounds__(VH_TPB) k_n4_exact_min(const float *__restrict__ U,
                                                         const uint8_t *__restrict__ mask,
                                                         int64_t V, int bins, N4State *st) {
     __shared__ float s_cmax[VH_TPB];
@@ -338,7 +384,7 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_exact_min(const float *__restrict
     float cmax = -FLT_MAX;
     for (int64_t r = s0; r < e0; ++r)
         if (mask[b * V + r] == 1) {
-            const float u = L0[b * V + r] - B[b * V + r];
+            const float u = U[b * V + r];
             cmax = u > cmax ? u : cmax;
         }
     s_cmax[t] = cmax;
@@ -351,7 +397,7 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_exact_min(const float *__restrict
     float run = s_cmax[t], mn = FLT_MAX;
     for (int64_t r = s0; r < e0; ++r)
         if (mask[b * V + r] == 1) {
-            const float u = L0[b * V + r] - B[b * V + r];
+            const float u = U[b * V + r];
             if (u > run) run = u;
             else if (u < mn) mn = u;
         }
@@ -366,35 +412,61 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_exact_min(const float *__restrict
 }
 
 // Triangular Parzen histogram of U at mask == 1, unsigned 64-bit fixed point (2^-32 units).
-__global__ void __launch_bounds__(VH_TPB) k_n4_hist(const float *__restrict__ L0,
-                                                   const float *__restrict__ B,
-                                                   const uint8_t *__restrict__ mask,
-                                                   const int32_t *colrange, int64_t CZ, int64_t V,
-                                                   int bins, const N4State *st, uint64_t *hist) {
+// Neighbouring rows of a column fall in the same bin most of the time: each lane keeps a run
+// (bin, two weights) in registers and only touches LDS when the bin changes.
+__global__ void __launch_bounds__(VH_TPB) k_n4_hist(const float *__restrict__ U,
+                                                   const uint32_t *__restrict__ colbits,
+                                                   const int32_t *colrange, int64_t R,
+                                                   int64_t CZ, int64_t V, int bins,
+                                                   const N4State *st, uint64_t *hist) {
     __shared__ unsigned long long H[VH_MAX_BINS];
     const int64_t b = blockIdx.y;
     if (!st[b].active) return;
     for (int i = threadIdx.x; i < VH_MAX_BINS; i += VH_TPB) H[i] = 0ull;
     __syncthreads();
     const float bmin = st[b].bin_min, slope = st[b].slope;
-    const int64_t col = blockIdx.x * (int64_t)VH_TPB + threadIdx.x;
-    if (col < CZ) {
-        const int32_t lo = colrange[(b * CZ + col) * 2], hi = colrange[(b * CZ + col) * 2 + 1];
-        for (int64_t x = lo; x <= hi; ++x) {
-            const int64_t v = b * V + x * CZ + col;
-            if (mask[v] != 1) continue;
-            const float u = L0[v] - B[v];
-            const float cidx = (u - bmin) / slope;
+    const ColSweep cs = col_sweep_begin(colrange, b, CZ, R);
+    const int64_t nw = (R + 31) >> 5;
+    int cur = -1;
+    unsigned long long w0 = 0ull, w1 = 0ull;
+    for (int x0 = cs.wlo & ~(SW_CHUNK - 1); x0 <= cs.whi; x0 += SW_CHUNK) {
+        const uint32_t m8 = chunk_bits(colbits, cs, b, nw, CZ, x0);
+        float u[SW_CHUNK];
+#pragma unroll
+        for (int k = 0; k < SW_CHUNK; ++k)
+            u[k] = (m8 >> k) & 1u ? U[b * V + (int64_t)(x0 + k) * CZ + cs.col] : 0.0f;
+#pragma unroll
+        for (int k = 0; k < SW_CHUNK; ++k) {
+            if (!((m8 >> k) & 1u)) continue;
+            const float cidx = (u[k] - bmin) / slope;
             if (!(cidx >= 0.0f) || !(cidx < (float)bins)) continue;
             const int idx = (int)floorf(cidx);
             const float o = cidx - (float)idx;
+            unsigned long long a0, a1 = 0ull;
             if (o == 0.0f) {
-                atomicAdd(&H[idx], 1ull << 32);
+                a0 = 1ull << 32;
             } else if (idx < bins - 1) {
-                atomicAdd(&H[idx], (unsigned long long)((double)(1.0f - o) * 4294967296.0));
-                atomicAdd(&H[idx + 1], (unsigned long long)((double)o * 4294967296.0));
+                a0 = (unsigned long long)((double)(1.0f - o) * 4294967296.0);
+                a1 = (unsigned long long)((double)o * 4294967296.0);
+            } else {
+                continue;
             }
+            if (idx != cur) {
+                if (cur >= 0) {
+                    if (w0) atomicAdd(&H[cur], w0);
+                    if (w1) atomicAdd(&H[cur + 1], w1);
+                }
+                cur = idx;
+                w0 = 0ull;
+                w1 = 0ull;
+            }
+            w0 += a0;
+            w1 += a1;
         }
+    }
+    if (cur >= 0) {
+        if (w0) atomicAdd(&H[cur], w0);
+        if (w1) atomicAdd(&H[cur + 1], w1);
     }
     __syncthreads();
     for (int i = threadIdx.x; i < bins; i += VH_TPB)
@@ -500,12 +572,12 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_emap(const uint64_t *hist, const 
 
 // Sliding-window row contraction.  MODE 0: numerator  Q1[i][col] = sum_x wx(x,i)^3 q(x,col),
 // q = (U - sharpen(U)) / sum w^2;  MODE 1: denominator Q1[i][col] = sum_x wx(x,i)^2 [mask==1].
+// The window start wb = base(x) is wave-uniform (x is), so the window logic never diverges.
 template <int MODE>
-__global__ void __launch_bounds__(VH_TPB) k_n4_fitsweep(const float *__restrict__ L0,
-                                                       const float *__restrict__ B,
-                                                       const uint8_t *__restrict__ mask,
-                                                       const int32_t *colrange, int64_t C,
-                                                       int64_t Z, int64_t V, int bins,
+__global__ void __launch_bounds__(VH_TPB) k_n4_fitsweep(const float *__restrict__ U,
+                                                       const uint32_t *__restrict__ colbits,
+                                                       const int32_t *colrange, int64_t R,
+                                                       int64_t C, int64_t Z, int64_t V, int bins,
                                                        const N4State *st, const float *E,
                                                        DevLevel lv, double *Q1) {
     __shared__ float sE[VH_MAX_BINS];
@@ -516,59 +588,81 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_fitsweep(const float *__restrict_
         for (int i = threadIdx.x; i < bins; i += VH_TPB) sE[i] = E[b * VH_MAX_BINS + i];
         __syncthreads();
     }
-    const int64_t col = blockIdx.x * (int64_t)VH_TPB + threadIdx.x;
-    if (col >= CZ) return;
+    const ColSweep cs = col_sweep_begin(colrange, b, CZ, R);
     const DevAxis ax = lv.ax[0];
     const int ncx = ax.ncp;
-    double *q1 = Q1 + (b * ncx) * CZ + col;
-    const int32_t lo = colrange[(b * CZ + col) * 2], hi = colrange[(b * CZ + col) * 2 + 1];
-    if (hi < lo) {
-        for (int i = 0; i < ncx; ++i) q1[i * CZ] = 0.0;
+    double *q1 = Q1 + (b * ncx) * CZ + cs.col;
+    const int64_t nw = (R + 31) >> 5;
+    if (cs.wlo > cs.whi) {
+        if (cs.valid)
+            for (int i = 0; i < ncx; ++i) q1[i * CZ] = 0.0;
         return;
     }
-    const int64_t y = col / Z, z = col % Z;
-    double syz = 0.0;
     float bmin = 0.0f, slope = 1.0f;
     if (MODE == 0) {
         bmin = st[b].bin_min;
         slope = st[b].slope;
     }
-    const double sy = lv.ax[1].sw2[y], sz = lv.ax[2].sw2[z];
+    double syz = 1.0;
+    if (cs.valid) syz = lv.ax[1].sw2[cs.col / Z] * lv.ax[2].sw2[cs.col % Z];
     (void)syz;
-    int wb = ax.base[lo];
-    for (int i = 0; i < wb; ++i) q1[i * CZ] = 0.0;
+    const int xs = cs.wlo & ~(SW_CHUNK - 1);
+    int wb = ax.base[xs];
+    if (cs.valid)
+        for (int i = 0; i < wb; ++i) q1[i * CZ] = 0.0;
     double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-    for (int64_t x = lo; x <= hi; ++x) {
-        const int bx = ax.base[x];
-        while (wb < bx) {
-            q1[wb * CZ] = a0;
-            a0 = a1; a1 = a2; a2 = a3; a3 = 0.0;
-            ++wb;
-        }
-        const int64_t v = b * V + x * CZ + col;
-        if (mask[v] != 1) continue;
-        const float4 w = *reinterpret_cast<const float4 *>(ax.w + 4 * x);
-        const double w0 = w.x, w1 = w.y, w2 = w.z, w3 = w.w;
+    for (int x0 = xs; x0 <= cs.whi; x0 += SW_CHUNK) {
+        const uint32_t m8 = chunk_bits(colbits, cs, b, nw, CZ, x0);
+        float u[SW_CHUNK];
         if (MODE == 0) {
-            const float u = L0[v] - B[v];
-            const float r = u - sharpen_value(u, bmin, slope, sE, bins);
-            const double q = (double)r / (ax.sw2[x] * sy * sz);
-            a0 += w0 * w0 * w0 * q;
-            a1 += w1 * w1 * w1 * q;
-            a2 += w2 * w2 * w2 * q;
-            a3 += w3 * w3 * w3 * q;
-        } else {
-            a0 += w0 * w0;
-            a1 += w1 * w1;
-            a2 += w2 * w2;
-            a3 += w3 * w3;
+#pragma unroll
+            for (int k = 0; k < SW_CHUNK; ++k)
+                u[k] = (m8 >> k) & 1u ? U[b * V + (int64_t)(x0 + k) * CZ + cs.col] : 0.0f;
+        }
+#pragma unroll
+        for (int k = 0; k < SW_CHUNK; ++k) {
+            const int x = x0 + k;
+            if (x >= R) break;
+            const int bx = ax.base[x];
+            while (wb < bx) {
+                if (cs.valid) q1[wb * CZ] = a0;
+                a0 = a1; a1 = a2; a2 = a3; a3 = 0.0;
+                ++wb;
+            }
+            if (!((m8 >> k) & 1u)) continue;
+            const float4 w = *reinterpret_cast<const float4 *>(ax.w + 4 * x);
+            const double w0 = w.x, w1 = w.y, w2 = w.z, w3 = w.w;
+            if (MODE == 0) {
+                const float r = u[k] - sharpen_value(u[k], bmin, slope, sE, bins);
+                const double q = (double)r / (ax.sw2[x] * syz);
+                a0 += w0 * w0 * w0 * q;
+                a1 += w1 * w1 * w1 * q;
+                a2 += w2 * w2 * w2 * q;
+                a3 += w3 * w3 * w3 * q;
+            } else {
+                a0 += w0 * w0;
+                a1 += w1 * w1;
+                a2 += w2 * w2;
+                a3 += w3 * w3;
+            }
         }
     }
+    if (!cs.valid) return;
     q1[wb * CZ] = a0;
     if (wb + 1 < ncx) q1[(wb + 1) * CZ] = a1;
     if (wb + 2 < ncx) q1[(wb + 2) * CZ] = a2;
     if (wb + 3 < ncx) q1[(wb + 3) * CZ] = a3;
     for (int i = wb + 4; i < ncx; ++i) q1[i * CZ] = 0.0;
+}
+
+// first index i in [0, n) with base[i] >= v (base is non-decreasing), n if none
+__device__ __forceinline__ int64_t first_ge(const int32_t *base, int64_t n, int v) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (base[mid] >= v) hi = mid; else lo = mid + 1;
+    }
+    return lo;
 }
 
 // Contract the col and slice axes of Q1 (one block per volume).  MODE 1 -> den.  MODE 0 -> num,
@@ -589,9 +683,9 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_contract(const double *Q1, double
     for (int64_t e = threadIdx.x; e < (int64_t)ncx * ncy * Z; e += VH_TPB) {
         const int64_t i = e / (ncy * Z), j = (e / Z) % ncy, z = e % Z;
         double acc = 0.0;
-        for (int64_t y = 0; y < C; ++y) {
+        const int64_t y0 = first_ge(ay.base, C, (int)j - 3), y1 = first_ge(ay.base, C, (int)j + 1);
+        for (int64_t y = y0; y < y1; ++y) {
             const int k = (int)j - ay.base[y];
-            if (k < 0 || k > 3) continue;
             const double w = ay.w[4 * y + k];
             const double wp = MODE == 0 ? w * w * w : w * w;
             acc += wp * q1[i * CZ + y * Z + z];
@@ -604,9 +698,9 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_contract(const double *Q1, double
     for (int64_t e = threadIdx.x; e < (int64_t)ncx * ncy * ncz; e += VH_TPB) {
         const int64_t ij = e / ncz, k = e % ncz;
         double acc = 0.0;
-        for (int64_t z = 0; z < Z; ++z) {
+        const int64_t z0 = first_ge(az.base, Z, (int)k - 3), z1 = first_ge(az.base, Z, (int)k + 1);
+        for (int64_t z = z0; z < z1; ++z) {
             const int c = (int)k - az.base[z];
-            if (c < 0 || c > 3) continue;
             const double w = az.w[4 * z + c];
             const double wp = MODE == 0 ? w * w * w : w * w;
             acc += wp * q2[ij * Z + z];
@@ -640,11 +734,12 @@ __device__ __forceinline__ double col_T(const double *p1, int i, int ncy, int64_
     return (double)wy.x * r[0] + (double)wy.y * r[Z] + (double)wy.z * r[2 * Z] + (double)wy.w * r[3 * Z];
 }
 
-// Evaluate the new field at masked voxels, convergence partials, U range for the next iteration.
+// Evaluate the new field at masked voxels, convergence partials, U = L0 - B and its range for the
+// next iteration.
 __global__ void __launch_bounds__(VH_TPB) k_n4_eval(const float *__restrict__ L0, float *B,
-                                                   const uint8_t *__restrict__ mask,
+                                                   float *U, const uint32_t *__restrict__ colbits,
                                                    const int32_t *colrange, const VolScalars *sc,
-                                                   int64_t C, int64_t Z, int64_t V,
+                                                   int64_t R, int64_t C, int64_t Z, int64_t V,
                                                    int64_t q2_cap, const double *P1,
                                                    DevLevel lv, N4State *st, int64_t nparts,
                                                    double *part) {
@@ -654,43 +749,56 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_eval(const float *__restrict__ L0
     if (!st[b].active) return;
     if (threadIdx.x == 0) { s_max = 0u; s_min = 0xffffffffu; }
     const int64_t CZ = C * Z;
-    const int64_t col = blockIdx.x * (int64_t)VH_TPB + threadIdx.x;
+    const ColSweep cs = col_sweep_begin(colrange, b, CZ, R);
+    const int64_t nw = (R + 31) >> 5;
     double sd = 0.0, sd2 = 0.0;
     uint32_t kmax = 0u, kmin = 0xffffffffu;
-    if (col < CZ) {
-        const int32_t lo = colrange[(b * CZ + col) * 2], hi = colrange[(b * CZ + col) * 2 + 1];
-        if (lo <= hi) {
-            const int64_t y = col / Z, z = col % Z;
-            const int ncy = lv.ax[1].ncp;
-            const int by = lv.ax[1].base[y];
-            const float4 wy = *reinterpret_cast<const float4 *>(lv.ax[1].w + 4 * y);
-            const double *p1 = P1 + b * q2_cap;
-            const DevAxis ax = lv.ax[0];
-            const int64_t first = sc[b].first_masked;
-            int wb = ax.base[lo];
-            double t0 = col_T(p1, wb, ncy, Z, by, wy, z), t1 = col_T(p1, wb + 1, ncy, Z, by, wy, z);
-            double t2 = col_T(p1, wb + 2, ncy, Z, by, wy, z), t3 = col_T(p1, wb + 3, ncy, Z, by, wy, z);
-            for (int64_t x = lo; x <= hi; ++x) {
-                const int64_t r = x * CZ + col, v = b * V + r;
-                if (mask[v] != 1) continue;
+    if (cs.wlo <= cs.whi) {
+        const int64_t y = cs.valid ? cs.col / Z : 0, z = cs.valid ? cs.col % Z : 0;
+        const int ncy = lv.ax[1].ncp;
+        const int by = lv.ax[1].base[y];
+        const float4 wy = *reinterpret_cast<const float4 *>(lv.ax[1].w + 4 * y);
+        const double *p1 = P1 + b * q2_cap;
+        const DevAxis ax = lv.ax[0];
+        const int64_t first = sc[b].first_masked;
+        const int xs = cs.wlo & ~(SW_CHUNK - 1);
+        int wb = ax.base[xs];
+        double t0 = col_T(p1, wb, ncy, Z, by, wy, z), t1 = col_T(p1, wb + 1, ncy, Z, by, wy, z);
+        double t2 = col_T(p1, wb + 2, ncy, Z, by, wy, z), t3 = col_T(p1, wb + 3, ncy, Z, by, wy, z);
+        for (int x0 = xs; x0 <= cs.whi; x0 += SW_CHUNK) {
+            const uint32_t m8 = chunk_bits(colbits, cs, b, nw, CZ, x0);
+            float l0[SW_CHUNK], bo[SW_CHUNK];
+#pragma unroll
+            for (int k = 0; k < SW_CHUNK; ++k) {
+                const bool on = (m8 >> k) & 1u;
+                const int64_t v = b * V + (int64_t)(x0 + k) * CZ + cs.col;
+                l0[k] = on ? L0[v] : 0.0f;
+                bo[k] = on ? B[v] : 0.0f;
+            }
+#pragma unroll
+            for (int k = 0; k < SW_CHUNK; ++k) {
+                const int x = x0 + k;
+                if (x >= R) break;
                 const int bx = ax.base[x];
                 while (wb < bx) {
                     ++wb;
                     t0 = t1; t1 = t2; t2 = t3;
                     t3 = col_T(p1, wb + 3, ncy, Z, by, wy, z);
                 }
+                if (!((m8 >> k) & 1u)) continue;
                 const float4 w = *reinterpret_cast<const float4 *>(ax.w + 4 * x);
                 const float bn = (float)((double)w.x * t0 + (double)w.y * t1 + (double)w.z * t2 + (double)w.w * t3);
-                const float bo = B[v];
-                const double d = exp((double)bo - (double)bn) - 1.0;
+                const double d = exp((double)bo[k] - (double)bn) - 1.0;
                 sd += d;
                 sd2 += d * d;
+                const int64_t r = (int64_t)x * CZ + cs.col, v = b * V + r;
                 B[v] = bn;
-                const float u = L0[v] - bn;
-                const uint32_t k = f2key(u);
-                kmax = k > kmax ? k : kmax;
+                const float u = l0[k] - bn;
+                U[v] = u;
+                const uint32_t key = f2key(u);
+                kmax = key > kmax ? key : kmax;
                 if (r == first) st[b].u_first = u;
-                else kmin = k < kmin ? k : kmin;
+                else kmin = key < kmin ? key : kmin;
             }
         }
     }
@@ -784,6 +892,7 @@ void vh_launch_n4(vh_batch *b, const vh_n4_params &prm) {
     const int bins = prm.n_bins;
     const double masked_bytes = (double)b->V;   // refined per kernel below
     (void)masked_bytes;
+    float *U = b->d_n4;   // U = L0 - B lives in the output buffer until k_n4_final overwrites it
     HIP_TRY(hipMemsetAsync(b->d_lat, 0, sizeof(float) * b->nb * b->lat_cap, st));
     k_n4_state_init<<<(unsigned)((b->nb + 255) / 256), 256, 0, st>>>(b->d_st, b->nb);
     VH_CHECK_LAUNCH();
@@ -792,8 +901,8 @@ void vh_launch_n4(vh_batch *b, const vh_n4_params &prm) {
     HIP_TRY(hipMemsetAsync(b->d_nactive, 0, sizeof(int32_t) * (total_iters + 1), st));
     {
         ScopedKTimer tm(b, "n4_init", 0.0);
-        k_n4_init<<<cg, VH_TPB, 0, st>>>(b->d_hp, b->d_mask, b->d_colrange, b->d_sc, b->CZ, b->V,
-                                         b->d_L0, b->d_B, b->d_st);
+        k_n4_init<<<cg, VH_TPB, 0, st>>>(b->d_hp, b->d_colbits, b->d_colrange, b->d_sc, b->R,
+                                         b->CZ, b->V, b->d_L0, b->d_B, U, b->d_st);
         VH_CHECK_LAUNCH();
     }
     const int LOOK = 3;
@@ -804,8 +913,8 @@ void vh_launch_n4(vh_batch *b, const vh_n4_params &prm) {
         const DevLevel lv = dev_level(b, prm, L);
         {
             ScopedKTimer tm(b, "n4_den", 0.0);
-            k_n4_fitsweep<1><<<cg, VH_TPB, 0, st>>>(b->d_L0, b->d_B, b->d_mask, b->d_colrange,
-                                                    b->C, b->Z, b->V, bins, b->d_st, b->d_E, lv,
+            k_n4_fitsweep<1><<<cg, VH_TPB, 0, st>>>(U, b->d_colbits, b->d_colrange, b->R, b->C,
+                                                    b->Z, b->V, bins, b->d_st, b->d_E, lv,
                                                     b->d_Q1);
             VH_CHECK_LAUNCH();
             k_n4_contract<1><<<(unsigned)b->nb, VH_TPB, 0, st>>>(
@@ -825,12 +934,12 @@ void vh_launch_n4(vh_batch *b, const vh_n4_params &prm) {
             HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
             HIP_TRY(hipEventRecord(ev, st));
             evs.push_back(ev);
-            k_n4_exact_min<<<(unsigned)b->nb, VH_TPB, 0, st>>>(b->d_L0, b->d_B, b->d_mask, b->V,
-                                                               bins, b->d_st);
+            k_n4_exact_min<<<(unsigned)b->nb, VH_TPB, 0, st>>>(U, b->d_mask, b->V, bins,
+                                                               b->d_st);
             VH_CHECK_LAUNCH();
             {
                 ScopedKTimer tm(b, "n4_hist", 0.0);
-                k_n4_hist<<<cg, VH_TPB, 0, st>>>(b->d_L0, b->d_B, b->d_mask, b->d_colrange, b->CZ,
+                k_n4_hist<<<cg, VH_TPB, 0, st>>>(U, b->d_colbits, b->d_colrange, b->R, b->CZ,
                                                  b->V, bins, b->d_st, b->d_hist);
                 VH_CHECK_LAUNCH();
             }
@@ -839,9 +948,9 @@ void vh_launch_n4(vh_batch *b, const vh_n4_params &prm) {
             VH_CHECK_LAUNCH();
             {
                 ScopedKTimer tm(b, "n4_fit", 0.0);
-                k_n4_fitsweep<0><<<cg, VH_TPB, 0, st>>>(b->d_L0, b->d_B, b->d_mask,
-                                                        b->d_colrange, b->C, b->Z, b->V, bins,
-                                                        b->d_st, b->d_E, lv, b->d_Q1);
+                k_n4_fitsweep<0><<<cg, VH_TPB, 0, st>>>(U, b->d_colbits, b->d_colrange, b->R,
+                                                        b->C, b->Z, b->V, bins, b->d_st, b->d_E,
+                                                        lv, b->d_Q1);
                 VH_CHECK_LAUNCH();
             }
             {
@@ -853,9 +962,10 @@ void vh_launch_n4(vh_batch *b, const vh_n4_params &prm) {
             }
             {
                 ScopedKTimer tm(b, "n4_eval", 0.0);
-                k_n4_eval<<<cg, VH_TPB, 0, st>>>(b->d_L0, b->d_B, b->d_mask, b->d_colrange,
-                                                 b->d_sc, b->C, b->Z, b->V, b->q2_cap, b->d_P1,
-                                                 lv, b->d_st, nparts, b->d_part);
+                k_n4_eval<<<cg, VH_TPB, 0, st>>>(b->d_L0, b->d_B, U, b->d_colbits,
+                                                 b->d_colrange, b->d_sc, b->R, b->C, b->Z, b->V,
+                                                 b->q2_cap, b->d_P1, lv, b->d_st, nparts,
+                                                 b->d_part);
                 VH_CHECK_LAUNCH();
             }
             const int k = (int)evs.size() - 1 - LOOK;

@@ -23,8 +23,9 @@ __global__ void k_init_scalars(VolScalars *sc, int64_t nb) {
 __global__ void __launch_bounds__(VH_TPB) k_mask_stats(const uint8_t *__restrict__ mask, int64_t R,
                                                       int64_t C, int64_t Z, int64_t V,
                                                       int32_t *colrange, int32_t *colcount,
-                                                      uint8_t *rowany, uint8_t *colany,
-                                                      uint8_t *sliceany, VolScalars *sc) {
+                                                      uint32_t *colbits, uint8_t *rowany,
+                                                      uint8_t *colany, uint8_t *sliceany,
+                                                      VolScalars *sc) {
     extern __shared__ uint8_t s_row[];   // [R]
     __shared__ unsigned long long s_n, s_n1, s_first;
     const int64_t b = blockIdx.y;
@@ -36,9 +37,17 @@ __global__ void __launch_bounds__(VH_TPB) k_mask_stats(const uint8_t *__restrict
     unsigned long long n = 0, n1 = 0, first = ULLONG_MAX;
     if (col < CZ) {
         const uint8_t *m = mask + b * V + col;
+        const int64_t nw = (R + 31) >> 5;
+        uint32_t *cb = colbits + (b * nw) * CZ + col;   // bit x&31 of word x>>5: mask == 1
+        uint32_t word = 0u;
         int32_t lo = (int32_t)R, hi = -1;
         for (int64_t x = 0; x < R; ++x) {
             const uint8_t v = m[x * CZ];
+            if (v == 1) word |= 1u << (x & 31);
+            if ((x & 31) == 31 || x == R - 1) {
+                cb[(x >> 5) * CZ] = word;
+                word = 0u;
+            }
             if (v) {
                 ++n;
                 if (lo == (int32_t)R) lo = (int32_t)x;
@@ -126,8 +135,8 @@ void vh_launch_mask_stats(vh_batch *b) {
     {
         ScopedKTimer tm(b, "mask_stats", (double)b->V);
         k_mask_stats<<<col_grid(b), VH_TPB, (size_t)b->R, st>>>(
-            b->d_mask, b->R, b->C, b->Z, b->V, b->d_colrange, b->d_colcount, b->d_rowany,
-            b->d_colany, b->d_sliceany, b->d_sc);
+            b->d_mask, b->R, b->C, b->Z, b->V, b->d_colrange, b->d_colcount, b->d_colbits,
+            b->d_rowany, b->d_colany, b->d_sliceany, b->d_sc);
         VH_CHECK_LAUNCH();
     }
     k_mask_finish<<<(unsigned)b->nb, VH_TPB, 0, st>>>(b->d_colcount, b->d_colstart, b->d_rowany,
@@ -374,8 +383,7 @@ __global__ void __launch_bounds__(VH_TPB) k_tile(const float *__restrict__ n4,
                                                 const VolScalars *__restrict__ sc, float thresh,
                                                 int64_t R, int64_t C, int64_t Z, int64_t V,
                                                 int tz, uint8_t *defect, uint8_t *border,
-                                                uint8_t *lb, unsigned long long *cnt_out,
-                                                uint64_t *cohort, int do_cohort) {
+                                                uint8_t *lb, unsigned long long *cnt_out) {
     extern __shared__ uint8_t lds[];
     const int64_t b = blockIdx.y;
     const int64_t ntx = (R + CL_TX - 1) / CL_TX, nty = (C + CL_TY - 1) / CL_TY;
@@ -450,11 +458,6 @@ __global__ void __launch_bounds__(VH_TPB) k_tile(const float *__restrict__ n4,
             if (mk) {
                 const float nv = p4[(x * C + y) * Z + z] / p99;
                 cls = lb_class(nv);
-                if (do_cohort && nv >= 0.0f && nv < 1.5f) {
-                    int bi = (int)(nv * ((float)VH_COHORT_BINS / 1.5f));
-                    bi = bi > VH_COHORT_BINS - 1 ? VH_COHORT_BINS - 1 : bi;
-                    atomicAdd((unsigned long long *)&cohort[bi], 1ull);
-                }
             }
             lb[i] = cls;
             n_lb12 += (cls == 1 || cls == 2);
@@ -494,7 +497,7 @@ void vh_launch_border(vh_batch *b, const uint8_t *d_in, uint8_t *d_out) {
     ScopedKTimer tm(b, "border", 2.0 * (double)b->V);
     k_tile<false><<<grid, VH_TPB, lds, b->ctx->stream>>>(nullptr, b->d_mask, d_in, b->d_sc, 0.f,
                                                          b->R, b->C, b->Z, b->V, tz, nullptr,
-                                                         d_out, nullptr, nullptr, nullptr, 0);
+                                                         d_out, nullptr, nullptr);
     VH_CHECK_LAUNCH();
 }
 
@@ -506,8 +509,13 @@ void vh_launch_border(vh_batch *b, const uint8_t *d_in, uint8_t *d_out) {
 #define KM_K 4
 __global__ void __launch_bounds__(VH_TPB) k_kmeans(const uint32_t *__restrict__ keys,
                                                   int64_t V, VolScalars *sc) {
+    // Chunk t = [t*per, (t+1)*per) of the sorted values.  A cluster sum is sum_t p_t in t order,
+    // p_t = sequential sum over chunk t intersected with the cluster: a fully covered chunk uses
+    // its precomputed total (the same sequential sum), so an iteration only loops over the <= 2
+    // chunks cut by each boundary.
     __shared__ double s_c[KM_K];
     __shared__ int64_t s_cut[KM_K + 1], s_new[KM_K + 1];
+    __shared__ double s_tot[VH_TPB];
     __shared__ double s_part[KM_K][VH_TPB];
     __shared__ int s_done;
     const int64_t b = blockIdx.x;
@@ -517,9 +525,14 @@ __global__ void __launch_bounds__(VH_TPB) k_kmeans(const uint32_t *__restrict__ 
     if (n <= 0) return;
     if (t < KM_K) s_c[t] = (double)key2f(k[(n * (2 * t + 1)) / (2 * KM_K)]);
     if (t == 0) { s_cut[0] = -1; s_done = 0; }
-    __syncthreads();
     const int64_t per = (n + VH_TPB - 1) / VH_TPB;
-    const int64_t cs = t * per, ce = cs + per < n ? cs + per : n;
+    const int64_t cs = t * per < n ? t * per : n, ce = cs + per < n ? cs + per : n;
+    {
+        double tot = 0.0;
+        for (int64_t i = cs; i < ce; ++i) tot += (double)key2f(k[i]);
+        s_tot[t] = tot;
+    }
+    __syncthreads();
     int it = 0;
     for (it = 1; it <= 300; ++it) {
         if (t < KM_K - 1) {
@@ -546,14 +559,17 @@ __global__ void __launch_bounds__(VH_TPB) k_kmeans(const uint32_t *__restrict__ 
         }
         __syncthreads();
         if (s_done) break;
-        double acc[KM_K] = {0.0, 0.0, 0.0, 0.0};
-        for (int64_t i = cs; i < ce; ++i) {
-            const double x = (double)key2f(k[i]);
-            int j = 0;
-            while (j < KM_K - 1 && i >= s_cut[j + 1]) ++j;
-            acc[j] += x;
+        for (int j = 0; j < KM_K; ++j) {
+            const int64_t a = s_cut[j], e = s_cut[j + 1];
+            double p = 0.0;
+            if (cs >= a && ce <= e) {
+                p = s_tot[t];
+            } else {
+                const int64_t lo = cs > a ? cs : a, hi = ce < e ? ce : e;
+                for (int64_t i = lo; i < hi; ++i) p += (double)key2f(k[i]);
+            }
+            s_part[j][t] = p;
         }
-        for (int j = 0; j < KM_K; ++j) s_part[j][t] = acc[j];
         __syncthreads();
         if (t < KM_K) {
             double s = 0.0;
@@ -568,6 +584,55 @@ __global__ void __launch_bounds__(VH_TPB) k_kmeans(const uint32_t *__restrict__ 
         sc[b].km_iters = it;
         for (int j = 0; j < KM_K; ++j) sc[b].km_c[j] = s_c[j];
     }
+}
+
+// =============================================================================================
+// cohort histogram (build-defined, BASELINE config 4): 1024 bins over [0, 1.5) of the
+// p99-normalised masked N4 values, bin = int(nv * (1024 / 1.5f)).  Computed from the sorted keys
+// (bins are monotone in the value, so each thread's contiguous chunk produces runs of equal bins:
+// one LDS atomic per run), per-volume rows, then a fixed-order sum over volumes (no float or
+// global atomics: deterministic).
+// =============================================================================================
+__global__ void __launch_bounds__(VH_TPB) k_cohort_vol(const uint32_t *__restrict__ keys,
+                                                      const VolScalars *sc, int64_t V,
+                                                      uint32_t *rows) {
+    __shared__ uint32_t h[VH_COHORT_BINS];
+    const int64_t b = blockIdx.x;
+    for (int i = threadIdx.x; i < VH_COHORT_BINS; i += VH_TPB) h[i] = 0u;
+    __syncthreads();
+    const int64_t n = sc[b].n_mask;
+    const float p99 = sc[b].p99;
+    const int64_t per = (n + VH_TPB - 1) / VH_TPB;
+    const int64_t cs = threadIdx.x * per < n ? threadIdx.x * per : n;
+    const int64_t ce = cs + per < n ? cs + per : n;
+    const uint32_t *k = keys + b * V;
+    int cur = -1;
+    uint32_t run = 0;
+    for (int64_t i = cs; i < ce; ++i) {
+        const float nv = key2f(k[i]) / p99;
+        int bi = -1;
+        if (nv >= 0.0f && nv < 1.5f) {
+            bi = (int)(nv * ((float)VH_COHORT_BINS / 1.5f));
+            bi = bi > VH_COHORT_BINS - 1 ? VH_COHORT_BINS - 1 : bi;
+        }
+        if (bi != cur) {
+            if (cur >= 0 && run) atomicAdd(&h[cur], run);
+            cur = bi;
+            run = 0;
+        }
+        run += (bi >= 0);
+    }
+    if (cur >= 0 && run) atomicAdd(&h[cur], run);
+    __syncthreads();
+    for (int i = threadIdx.x; i < VH_COHORT_BINS; i += VH_TPB) rows[b * VH_COHORT_BINS + i] = h[i];
+}
+
+__global__ void k_cohort_sum(const uint32_t *rows, int64_t nb, uint64_t *cohort) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= VH_COHORT_BINS) return;
+    uint64_t s = 0;
+    for (int64_t b = 0; b < nb; ++b) s += rows[b * VH_COHORT_BINS + i];
+    cohort[i] = s;
 }
 
 // =============================================================================================
@@ -694,11 +759,18 @@ void vh_launch_vdp_chain(vh_batch *b, const float *d_n4, const vh_run_opts &o) {
             ScopedKTimer tm(b, "classify", 8.0 * (double)b->V);
             k_tile<true><<<grid, VH_TPB, lds, st>>>(d_n4, b->d_mask, nullptr, b->d_sc, o.thresh,
                                                     b->R, b->C, b->Z, b->V, tz, b->d_defect,
-                                                    b->d_border, b->d_lb, cnt, b->d_cohort,
-                                                    o.do_cohort);
+                                                    b->d_border, b->d_lb, cnt);
             VH_CHECK_LAUNCH();
         }
         k_counts_to_scalars<<<(unsigned)((b->nb + 63) / 64), 64, 0, st>>>(cnt, b->nb, b->d_sc);
+        VH_CHECK_LAUNCH();
+    }
+    if (o.do_cohort) {
+        ScopedKTimer tm(b, "cohort", 0.0);
+        uint32_t *rows = b->d_tilecnt;   // free after the sort: nb*256*max_tiles >= nb*1024 u32
+        k_cohort_vol<<<(unsigned)b->nb, VH_TPB, 0, st>>>(b->d_keys0, b->d_sc, b->V, rows);
+        VH_CHECK_LAUNCH();
+        k_cohort_sum<<<VH_COHORT_BINS / 256, 256, 0, st>>>(rows, b->nb, b->d_cohort);
         VH_CHECK_LAUNCH();
     }
     if (o.do_kmeans) {

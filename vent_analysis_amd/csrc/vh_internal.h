@@ -105,6 +105,7 @@ struct vh_batch {
     // mask statistics
     int32_t *d_colrange = nullptr;   // [nb][CZ][2]  first/last masked row of each (col, slice) column
     int32_t *d_colcount = nullptr;   // [nb][CZ]
+    uint32_t *d_colbits = nullptr;   // [nb][ceil(R/32)][CZ]  row bitmap of mask == 1 per column
     int64_t *d_colstart = nullptr;   // [nb][CZ]     exclusive prefix of colcount
     uint8_t *d_rowany = nullptr, *d_colany = nullptr, *d_sliceany = nullptr;
     VolScalars *d_sc = nullptr;
