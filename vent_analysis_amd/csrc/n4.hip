@@ -26,11 +26,27 @@ struct DevAxis {
     const int32_t *base;
     const float *w;
     const double *sw2;
+    const double *isw2;   // 1 / sw2
     int32_t n, ncp;
 };
 struct DevLevel {
     DevAxis ax[3];
 };
+
+struct FitTile {
+    int yb, zb;        // tile extent
+    int nty, ntz;      // tiles per volume along cols / slices
+};
+
+__host__ __device__ inline FitTile fit_tile(int64_t C, int64_t Z) {
+    FitTile t;
+    t.zb = (int)(Z < VH_TPB ? Z : VH_TPB);
+    t.yb = VH_TPB / t.zb;
+    if (t.yb > C) t.yb = (int)C;
+    t.nty = (int)((C + t.yb - 1) / t.yb);
+    t.ntz = (int)((Z + t.zb - 1) / t.zb);
+    return t;
+}
 
 #define LN2 0.69314718055994530942
 #define PI_D 3.14159265358979323846
@@ -92,7 +108,7 @@ void vh_n4_prepare_tables(vh_batch *b, const vh_n4_params &prm) {
     if (b->tabs_valid && same_params(b->tab_prm, prm)) return;
     const int64_t dims[3] = {b->R, b->C, b->Z};
     std::vector<uint8_t> blob;
-    b->tab_off.assign((size_t)prm.n_levels * 3 * 3, 0);
+    b->tab_off.assign((size_t)prm.n_levels * 3 * 4, 0);
     auto push = [&](const void *p, size_t bytes) {
         size_t off = (blob.size() + 15) & ~(size_t)15;
         blob.resize(off + bytes);
@@ -106,9 +122,12 @@ void vh_n4_prepare_tables(vh_batch *b, const vh_n4_params &prm) {
         for (int a = 0; a < 3; ++a) {
             AxisTab t;
             vh_axis_tables((int)dims[a], level_ncp(prm, L, a), eps, t);
-            b->tab_off[(L * 3 + a) * 3 + 0] = push(t.base.data(), t.base.size() * 4);
-            b->tab_off[(L * 3 + a) * 3 + 1] = push(t.w.data(), t.w.size() * 4);
-            b->tab_off[(L * 3 + a) * 3 + 2] = push(t.sw2.data(), t.sw2.size() * 8);
+            std::vector<double> inv(t.sw2.size());
+            for (size_t i = 0; i < inv.size(); ++i) inv[i] = 1.0 / t.sw2[i];
+            b->tab_off[(L * 3 + a) * 4 + 0] = push(t.base.data(), t.base.size() * 4);
+            b->tab_off[(L * 3 + a) * 4 + 1] = push(t.w.data(), t.w.size() * 4);
+            b->tab_off[(L * 3 + a) * 4 + 2] = push(t.sw2.data(), t.sw2.size() * 8);
+            b->tab_off[(L * 3 + a) * 4 + 3] = push(inv.data(), inv.size() * 8);
         }
     }
     if (b->d_tabs) HIP_TRY(hipFree(b->d_tabs));
@@ -135,9 +154,10 @@ static DevLevel dev_level(const vh_batch *b, const vh_n4_params &prm, int L) {
     const int64_t dims[3] = {b->R, b->C, b->Z};
     const uint8_t *base = (const uint8_t *)b->d_tabs;
     for (int a = 0; a < 3; ++a) {
-        lv.ax[a].base = (const int32_t *)(base + b->tab_off[(L * 3 + a) * 3 + 0]);
-        lv.ax[a].w = (const float *)(base + b->tab_off[(L * 3 + a) * 3 + 1]);
-        lv.ax[a].sw2 = (const double *)(base + b->tab_off[(L * 3 + a) * 3 + 2]);
+        lv.ax[a].base = (const int32_t *)(base + b->tab_off[(L * 3 + a) * 4 + 0]);
+        lv.ax[a].w = (const float *)(base + b->tab_off[(L * 3 + a) * 4 + 1]);
+        lv.ax[a].sw2 = (const double *)(base + b->tab_off[(L * 3 + a) * 4 + 2]);
+        lv.ax[a].isw2 = (const double *)(base + b->tab_off[(L * 3 + a) * 4 + 3]);
         lv.ax[a].n = (int32_t)dims[a];
         lv.ax[a].ncp = level_ncp(prm, L, a);
     }
@@ -148,7 +168,6 @@ void vh_ensure_n4_workspace(vh_batch *b, const vh_n4_params &prm) {
     const int L = prm.n_levels - 1;
     const int64_t cx = level_ncp(prm, L, 0), cy = level_ncp(prm, L, 1), cz = level_ncp(prm, L, 2);
     const int64_t lat = cx * cy * cz;
-    const int64_t q1 = cx * b->CZ;
     const int64_t q2 = cx * cy * b->Z;
     if (b->d_L0 == nullptr) {
         HIP_TRY(hipMalloc(&b->d_L0, sizeof(float) * b->nb * b->V));
@@ -167,15 +186,16 @@ void vh_ensure_n4_workspace(vh_batch *b, const vh_n4_params &prm) {
         HIP_TRY(hipMalloc(&b->d_den, sizeof(double) * b->nb * lat));
         b->lat_cap = lat;
     }
-    if (q1 > b->q1_cap) {
-        if (b->d_Q1) HIP_TRY(hipFree(b->d_Q1));
-        HIP_TRY(hipMalloc(&b->d_Q1, sizeof(double) * b->nb * q1));
-        b->q1_cap = q1;
+    if (cx > 64) throw VhError{VH_ERR_ARG, "N4 lattice too fine: > 64 control points along rows"};
+    const FitTile ft = fit_tile(b->C, b->Z);
+    const int64_t fp = (int64_t)ft.nty * ft.ntz * lat;   // per-volume tile slabs
+    if (fp > b->q1_cap) {
+        if (b->d_fitpart) HIP_TRY(hipFree(b->d_fitpart));
+        HIP_TRY(hipMalloc(&b->d_fitpart, sizeof(double) * b->nb * fp));
+        b->q1_cap = fp;
     }
     if (q2 > b->q2_cap) {
-        if (b->d_Q2) HIP_TRY(hipFree(b->d_Q2));
         if (b->d_P1) HIP_TRY(hipFree(b->d_P1));
-        HIP_TRY(hipMalloc(&b->d_Q2, sizeof(double) * b->nb * q2));
         HIP_TRY(hipMalloc(&b->d_P1, sizeof(double) * b->nb * q2));
         b->q2_cap = q2;
     }
@@ -570,140 +590,168 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_emap(const uint64_t *hist, const 
     }
 }
 
-// Sliding-window row contraction.  MODE 0: numerator  Q1[i][col] = sum_x wx(x,i)^3 q(x,col),
-// q = (U - sharpen(U)) / sum w^2;  MODE 1: denominator Q1[i][col] = sum_x wx(x,i)^2 [mask==1].
-// The window start wb = base(x) is wave-uniform (x is), so the window logic never diverges.
+// ---------------------------------------------------------------------------------------------
+// Fit sweep with in-block contraction.  A block owns a tile of YB cols x ZB slices (YB*ZB <= 256
+// columns, one per thread); after the row sweep (same sliding window as k_n4_fitsweep) every
+// thread holds Q1[i] of its column in LDS, and the block contracts its tile over cols and slices:
+//   Pn[i][j][k] = sum_{y in tile} sum_{z in tile} wy(y,j)^p wz(z,k)^p Q1[i][y][z]
+// for the lattice rows j / slices k its tile touches.  Only that small slab goes to HBM; the
+// contract kernel adds the slabs of a volume's tiles in tile order (deterministic).
+// p = 3 (MODE 0, numerator) or 2 (MODE 1, denominator).
+// ---------------------------------------------------------------------------------------------
 template <int MODE>
-__global__ void __launch_bounds__(VH_TPB) k_n4_fitsweep(const float *__restrict__ U,
+__global__ void __launch_bounds__(VH_TPB) k_n4_fitblock(const float *__restrict__ U,
                                                        const uint32_t *__restrict__ colbits,
                                                        const int32_t *colrange, int64_t R,
                                                        int64_t C, int64_t Z, int64_t V, int bins,
                                                        const N4State *st, const float *E,
-                                                       DevLevel lv, double *Q1) {
+                                                       DevLevel lv, int64_t slab, double *part) {
+    extern __shared__ __attribute__((aligned(16))) double sQ1[];   // [ncx][VH_TPB]
     __shared__ float sE[VH_MAX_BINS];
     const int64_t b = blockIdx.y;
-    const int64_t CZ = C * Z;
-    if (MODE == 0) {
-        if (!st[b].active) return;
-        for (int i = threadIdx.x; i < bins; i += VH_TPB) sE[i] = E[b * VH_MAX_BINS + i];
-        __syncthreads();
-    }
-    const ColSweep cs = col_sweep_begin(colrange, b, CZ, R);
-    const DevAxis ax = lv.ax[0];
-    const int ncx = ax.ncp;
-    double *q1 = Q1 + (b * ncx) * CZ + cs.col;
-    const int64_t nw = (R + 31) >> 5;
-    if (cs.wlo > cs.whi) {
-        if (cs.valid)
-            for (int i = 0; i < ncx; ++i) q1[i * CZ] = 0.0;
-        return;
-    }
-    float bmin = 0.0f, slope = 1.0f;
-    if (MODE == 0) {
-        bmin = st[b].bin_min;
-        slope = st[b].slope;
-    }
-    double syz = 1.0;
-    if (cs.valid) syz = lv.ax[1].sw2[cs.col / Z] * lv.ax[2].sw2[cs.col % Z];
-    (void)syz;
-    const int xs = cs.wlo & ~(SW_CHUNK - 1);
-    int wb = ax.base[xs];
-    if (cs.valid)
-        for (int i = 0; i < wb; ++i) q1[i * CZ] = 0.0;
-    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-    for (int x0 = xs; x0 <= cs.whi; x0 += SW_CHUNK) {
-        const uint32_t m8 = chunk_bits(colbits, cs, b, nw, CZ, x0);
-        float u[SW_CHUNK];
-        if (MODE == 0) {
-#pragma unroll
-            for (int k = 0; k < SW_CHUNK; ++k)
-                u[k] = (m8 >> k) & 1u ? U[b * V + (int64_t)(x0 + k) * CZ + cs.col] : 0.0f;
-        }
-#pragma unroll
-        for (int k = 0; k < SW_CHUNK; ++k) {
-            const int x = x0 + k;
-            if (x >= R) break;
-            const int bx = ax.base[x];
-            while (wb < bx) {
-                if (cs.valid) q1[wb * CZ] = a0;
-                a0 = a1; a1 = a2; a2 = a3; a3 = 0.0;
-                ++wb;
-            }
-            if (!((m8 >> k) & 1u)) continue;
-            const float4 w = *reinterpret_cast<const float4 *>(ax.w + 4 * x);
-            const double w0 = w.x, w1 = w.y, w2 = w.z, w3 = w.w;
-            if (MODE == 0) {
-                const float r = u[k] - sharpen_value(u[k], bmin, slope, sE, bins);
-                const double q = (double)r / (ax.sw2[x] * syz);
-                a0 += w0 * w0 * w0 * q;
-                a1 += w1 * w1 * w1 * q;
-                a2 += w2 * w2 * w2 * q;
-                a3 += w3 * w3 * w3 * q;
-            } else {
-                a0 += w0 * w0;
-                a1 += w1 * w1;
-                a2 += w2 * w2;
-                a3 += w3 * w3;
-            }
-        }
-    }
-    if (!cs.valid) return;
-    q1[wb * CZ] = a0;
-    if (wb + 1 < ncx) q1[(wb + 1) * CZ] = a1;
-    if (wb + 2 < ncx) q1[(wb + 2) * CZ] = a2;
-    if (wb + 3 < ncx) q1[(wb + 3) * CZ] = a3;
-    for (int i = wb + 4; i < ncx; ++i) q1[i * CZ] = 0.0;
-}
-
-// first index i in [0, n) with base[i] >= v (base is non-decreasing), n if none
-__device__ __forceinline__ int64_t first_ge(const int32_t *base, int64_t n, int v) {
-    int64_t lo = 0, hi = n;
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (base[mid] >= v) hi = mid; else lo = mid + 1;
-    }
-    return lo;
-}
-
-// Contract the col and slice axes of Q1 (one block per volume).  MODE 1 -> den.  MODE 0 -> num,
-// phi = num/den, lattice += phi, then P1[i][j][z] = sum_k wz(z,k) lat[i][j][k] for the eval sweep.
-template <int MODE>
-__global__ void __launch_bounds__(VH_TPB) k_n4_contract(const double *Q1, double *Q2, float *lat,
-                                                       double *den, double *P1, int64_t C,
-                                                       int64_t Z, int64_t lat_cap,
-                                                       int64_t q2_cap, const N4State *st,
-                                                       DevLevel lv) {
-    const int64_t b = blockIdx.x;
     if (MODE == 0 && !st[b].active) return;
-    const int ncx = lv.ax[0].ncp, ncy = lv.ax[1].ncp, ncz = lv.ax[2].ncp;
+    const FitTile ft = fit_tile(C, Z);
+    const int tile = blockIdx.x;
+    const int ty0 = (tile / ft.ntz) * ft.yb, tz0 = (tile % ft.ntz) * ft.zb;
+    const int ny = (int)(C - ty0 < ft.yb ? C - ty0 : ft.yb);
+    const int nz = (int)(Z - tz0 < ft.zb ? Z - tz0 : ft.zb);
+    const int tid = threadIdx.x;
+    const int ly = tid / ft.zb, lz = tid % ft.zb;
+    const bool mine = ly < ny && lz < nz;
     const int64_t CZ = C * Z;
-    const DevAxis ay = lv.ax[1], az = lv.ax[2];
-    const double *q1 = Q1 + (b * ncx) * CZ;
-    double *q2 = Q2 + b * q2_cap;
-    for (int64_t e = threadIdx.x; e < (int64_t)ncx * ncy * Z; e += VH_TPB) {
-        const int64_t i = e / (ncy * Z), j = (e / Z) % ncy, z = e % Z;
-        double acc = 0.0;
-        const int64_t y0 = first_ge(ay.base, C, (int)j - 3), y1 = first_ge(ay.base, C, (int)j + 1);
-        for (int64_t y = y0; y < y1; ++y) {
-            const int k = (int)j - ay.base[y];
-            const double w = ay.w[4 * y + k];
-            const double wp = MODE == 0 ? w * w * w : w * w;
-            acc += wp * q1[i * CZ + y * Z + z];
+    const DevAxis ax = lv.ax[0], ay = lv.ax[1], az = lv.ax[2];
+    const int ncx = ax.ncp;
+    for (int i = 0; i < ncx; ++i) sQ1[i * VH_TPB + tid] = 0.0;
+    if (MODE == 0)
+        for (int i = tid; i < bins; i += VH_TPB) sE[i] = E[b * VH_MAX_BINS + i];
+    // ---- row sweep of this thread's column (wave-uniform chunked rows) ----
+    ColSweep cs;
+    cs.col = (int64_t)(ty0 + ly) * Z + (tz0 + lz);
+    cs.valid = mine;
+    {
+        int lo = (int)R, hi = -1;
+        if (mine) {
+            lo = colrange[(b * CZ + cs.col) * 2];
+            hi = colrange[(b * CZ + cs.col) * 2 + 1];
         }
-        q2[e] = acc;
+        for (int off = 32; off > 0; off >>= 1) {
+            lo = min(lo, __shfl_xor(lo, off, 64));
+            hi = max(hi, __shfl_xor(hi, off, 64));
+        }
+        cs.wlo = __builtin_amdgcn_readfirstlane(lo);
+        cs.whi = __builtin_amdgcn_readfirstlane(hi);
     }
     __syncthreads();
+    if (cs.wlo <= cs.whi) {
+        const int64_t nw = (R + 31) >> 5;
+        float bmin = 0.0f, slope = 1.0f;
+        if (MODE == 0) {
+            bmin = st[b].bin_min;
+            slope = st[b].slope;
+        }
+        double isyz = 1.0;
+        if (mine) isyz = ay.isw2[ty0 + ly] * az.isw2[tz0 + lz];
+        const int xs = cs.wlo & ~(SW_CHUNK - 1);
+        int wb = ax.base[xs];
+        double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+        for (int x0 = xs; x0 <= cs.whi; x0 += SW_CHUNK) {
+            const uint32_t m8 = chunk_bits(colbits, cs, b, nw, CZ, x0);
+            float u[SW_CHUNK];
+            if (MODE == 0) {
+#pragma unroll
+                for (int k = 0; k < SW_CHUNK; ++k)
+                    u[k] = (m8 >> k) & 1u ? U[b * V + (int64_t)(x0 + k) * CZ + cs.col] : 0.0f;
+            }
+#pragma unroll
+            for (int k = 0; k < SW_CHUNK; ++k) {
+                const int x = x0 + k;
+                if (x >= R) break;
+                const int bx = ax.base[x];
+                while (wb < bx) {
+                    sQ1[wb * VH_TPB + tid] = a0;
+                    a0 = a1; a1 = a2; a2 = a3; a3 = 0.0;
+                    ++wb;
+                }
+                if (!((m8 >> k) & 1u)) continue;
+                const float4 w = *reinterpret_cast<const float4 *>(ax.w + 4 * x);
+                const double w0 = w.x, w1 = w.y, w2 = w.z, w3 = w.w;
+                if (MODE == 0) {
+                    const float r = u[k] - sharpen_value(u[k], bmin, slope, sE, bins);
+                    const double q = ((double)r * ax.isw2[x]) * isyz;
+                    a0 += (w0 * w0 * w0) * q;
+                    a1 += (w1 * w1 * w1) * q;
+                    a2 += (w2 * w2 * w2) * q;
+                    a3 += (w3 * w3 * w3) * q;
+                } else {
+                    a0 += w0 * w0;
+                    a1 += w1 * w1;
+                    a2 += w2 * w2;
+                    a3 += w3 * w3;
+                }
+            }
+        }
+        sQ1[wb * VH_TPB + tid] = a0;
+        if (wb + 1 < ncx) sQ1[(wb + 1) * VH_TPB + tid] = a1;
+        if (wb + 2 < ncx) sQ1[(wb + 2) * VH_TPB + tid] = a2;
+        if (wb + 3 < ncx) sQ1[(wb + 3) * VH_TPB + tid] = a3;
+    }
+    __syncthreads();
+    // ---- contract the tile over cols and slices ----
+    const int jlo = ay.base[ty0], jhi = ay.base[ty0 + ny - 1] + 3;
+    const int klo = az.base[tz0], khi = az.base[tz0 + nz - 1] + 3;
+    const int JT = jhi - jlo + 1, KT = khi - klo + 1;
+    double *out = part + (b * (int64_t)(ft.nty * ft.ntz) + tile) * slab;
+    for (int e = tid; e < ncx * JT * KT; e += VH_TPB) {
+        const int i = e / (JT * KT), jj = (e / KT) % JT, kk = e % KT;
+        const int j = jlo + jj, kq = klo + kk;
+        double acc = 0.0;
+        for (int yy = 0; yy < ny; ++yy) {
+            const int cy = j - ay.base[ty0 + yy];
+            if (cy < 0 || cy > 3) continue;
+            const double wyv = ay.w[4 * (ty0 + yy) + cy];
+            const double wyp = MODE == 0 ? wyv * wyv * wyv : wyv * wyv;
+            double accz = 0.0;
+            for (int zz = 0; zz < nz; ++zz) {
+                const int cz = kq - az.base[tz0 + zz];
+                if (cz < 0 || cz > 3) continue;
+                const double wzv = az.w[4 * (tz0 + zz) + cz];
+                const double wzp = MODE == 0 ? wzv * wzv * wzv : wzv * wzv;
+                accz += wzp * sQ1[i * VH_TPB + yy * ft.zb + zz];
+            }
+            acc += wyp * accz;
+        }
+        out[e] = acc;
+    }
+}
+
+// Sum the tile slabs of each volume (tile order), then MODE 1: den; MODE 0: phi = num/den,
+// lattice += phi, P1[i][j][z] = sum_k wz(z,k) lat[i][j][k] for the eval sweep.  One block/volume.
+template <int MODE>
+__global__ void __launch_bounds__(VH_TPB) k_n4_tilesum(const double *part, int64_t slab,
+                                                      float *lat, double *den, double *P1,
+                                                      int64_t C, int64_t Z, int64_t lat_cap,
+                                                      int64_t q2_cap, const N4State *st,
+                                                      DevLevel lv) {
+    const int64_t b = blockIdx.x;
+    if (MODE == 0 && !st[b].active) return;
+    const FitTile ft = fit_tile(C, Z);
+    const int ntiles = ft.nty * ft.ntz;
+    const DevAxis ay = lv.ax[1], az = lv.ax[2];
+    const int ncx = lv.ax[0].ncp, ncy = ay.ncp, ncz = az.ncp;
     float *L = lat + b * lat_cap;
     double *D = den + b * lat_cap;
-    for (int64_t e = threadIdx.x; e < (int64_t)ncx * ncy * ncz; e += VH_TPB) {
-        const int64_t ij = e / ncz, k = e % ncz;
+    for (int e = threadIdx.x; e < ncx * ncy * ncz; e += VH_TPB) {
+        const int i = e / (ncy * ncz), j = (e / ncz) % ncy, kq = e % ncz;
         double acc = 0.0;
-        const int64_t z0 = first_ge(az.base, Z, (int)k - 3), z1 = first_ge(az.base, Z, (int)k + 1);
-        for (int64_t z = z0; z < z1; ++z) {
-            const int c = (int)k - az.base[z];
-            const double w = az.w[4 * z + c];
-            const double wp = MODE == 0 ? w * w * w : w * w;
-            acc += wp * q2[ij * Z + z];
+        for (int tile = 0; tile < ntiles; ++tile) {
+            const int ty0 = (tile / ft.ntz) * ft.yb, tz0 = (tile % ft.ntz) * ft.zb;
+            const int ny = (int)(C - ty0 < ft.yb ? C - ty0 : ft.yb);
+            const int nz = (int)(Z - tz0 < ft.zb ? Z - tz0 : ft.zb);
+            const int jlo = ay.base[ty0], jhi = ay.base[ty0 + ny - 1] + 3;
+            const int klo = az.base[tz0], khi = az.base[tz0 + nz - 1] + 3;
+            if (j < jlo || j > jhi || kq < klo || kq > khi) continue;
+            const int JT = jhi - jlo + 1, KT = khi - klo + 1;
+            acc += part[(b * (int64_t)ntiles + tile) * slab + (i * JT + (j - jlo)) * KT + (kq - klo)];
         }
         if (MODE == 1) {
             D[e] = acc;
@@ -763,8 +811,9 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_eval(const float *__restrict__ L0
         const int64_t first = sc[b].first_masked;
         const int xs = cs.wlo & ~(SW_CHUNK - 1);
         int wb = ax.base[xs];
-        double t0 = col_T(p1, wb, ncy, Z, by, wy, z), t1 = col_T(p1, wb + 1, ncy, Z, by, wy, z);
-        double t2 = col_T(p1, wb + 2, ncy, Z, by, wy, z), t3 = col_T(p1, wb + 3, ncy, Z, by, wy, z);
+        // window of T(i), i = wb..wb+3 (double contraction, float value like the lattice)
+        float t0 = (float)col_T(p1, wb, ncy, Z, by, wy, z), t1 = (float)col_T(p1, wb + 1, ncy, Z, by, wy, z);
+        float t2 = (float)col_T(p1, wb + 2, ncy, Z, by, wy, z), t3 = (float)col_T(p1, wb + 3, ncy, Z, by, wy, z);
         for (int x0 = xs; x0 <= cs.whi; x0 += SW_CHUNK) {
             const uint32_t m8 = chunk_bits(colbits, cs, b, nw, CZ, x0);
             float l0[SW_CHUNK], bo[SW_CHUNK];
@@ -783,12 +832,12 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_eval(const float *__restrict__ L0
                 while (wb < bx) {
                     ++wb;
                     t0 = t1; t1 = t2; t2 = t3;
-                    t3 = col_T(p1, wb + 3, ncy, Z, by, wy, z);
+                    t3 = (float)col_T(p1, wb + 3, ncy, Z, by, wy, z);
                 }
                 if (!((m8 >> k) & 1u)) continue;
                 const float4 w = *reinterpret_cast<const float4 *>(ax.w + 4 * x);
-                const float bn = (float)((double)w.x * t0 + (double)w.y * t1 + (double)w.z * t2 + (double)w.w * t3);
-                const double d = exp((double)bo[k] - (double)bn) - 1.0;
+                const float bn = ((w.x * t0 + w.y * t1) + w.z * t2) + w.w * t3;
+                const double d = (double)expm1f(bo[k] - bn);   // p - 1, p = exp(B_old - B_new)
                 sd += d;
                 sd2 += d * d;
                 const int64_t r = (int64_t)x * CZ + cs.col, v = b * V + r;
@@ -911,15 +960,18 @@ void vh_launch_n4(vh_batch *b, const vh_n4_params &prm) {
     int gi = 0;   // global iteration slot
     for (int L = 0; L < prm.n_levels; ++L) {
         const DevLevel lv = dev_level(b, prm, L);
+        const FitTile ftile = fit_tile(b->C, b->Z);
+        const dim3 fg((unsigned)(ftile.nty * ftile.ntz), (unsigned)b->nb);
+        const size_t fit_lds = sizeof(double) * (size_t)lv.ax[0].ncp * VH_TPB;
         {
             ScopedKTimer tm(b, "n4_den", 0.0);
-            k_n4_fitsweep<1><<<cg, VH_TPB, 0, st>>>(U, b->d_colbits, b->d_colrange, b->R, b->C,
-                                                    b->Z, b->V, bins, b->d_st, b->d_E, lv,
-                                                    b->d_Q1);
+            k_n4_fitblock<1><<<fg, VH_TPB, fit_lds, st>>>(U, b->d_colbits, b->d_colrange, b->R,
+                                                          b->C, b->Z, b->V, bins, b->d_st, b->d_E,
+                                                          lv, b->lat_cap, b->d_fitpart);
             VH_CHECK_LAUNCH();
-            k_n4_contract<1><<<(unsigned)b->nb, VH_TPB, 0, st>>>(
-                b->d_Q1, b->d_Q2, b->d_lat, b->d_den, b->d_P1, b->C, b->Z, b->lat_cap, b->q2_cap,
-                b->d_st, lv);
+            k_n4_tilesum<1><<<(unsigned)b->nb, VH_TPB, 0, st>>>(b->d_fitpart, b->lat_cap, b->d_lat,
+                                                                b->d_den, b->d_P1, b->C, b->Z,
+                                                                b->lat_cap, b->q2_cap, b->d_st, lv);
             VH_CHECK_LAUNCH();
         }
         const int level_start = (int)evs.size();
@@ -948,15 +1000,16 @@ void vh_launch_n4(vh_batch *b, const vh_n4_params &prm) {
             VH_CHECK_LAUNCH();
             {
                 ScopedKTimer tm(b, "n4_fit", 0.0);
-                k_n4_fitsweep<0><<<cg, VH_TPB, 0, st>>>(U, b->d_colbits, b->d_colrange, b->R,
-                                                        b->C, b->Z, b->V, bins, b->d_st, b->d_E,
-                                                        lv, b->d_Q1);
+                k_n4_fitblock<0><<<fg, VH_TPB, fit_lds, st>>>(U, b->d_colbits, b->d_colrange,
+                                                              b->R, b->C, b->Z, b->V, bins,
+                                                              b->d_st, b->d_E, lv, b->lat_cap,
+                                                              b->d_fitpart);
                 VH_CHECK_LAUNCH();
             }
             {
                 ScopedKTimer tm(b, "n4_contract", 0.0);
-                k_n4_contract<0><<<(unsigned)b->nb, VH_TPB, 0, st>>>(
-                    b->d_Q1, b->d_Q2, b->d_lat, b->d_den, b->d_P1, b->C, b->Z, b->lat_cap,
+                k_n4_tilesum<0><<<(unsigned)b->nb, VH_TPB, 0, st>>>(
+                    b->d_fitpart, b->lat_cap, b->d_lat, b->d_den, b->d_P1, b->C, b->Z, b->lat_cap,
                     b->q2_cap, b->d_st, lv);
                 VH_CHECK_LAUNCH();
             }

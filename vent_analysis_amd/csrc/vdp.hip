@@ -160,8 +160,17 @@ __global__ void __launch_bounds__(VH_TPB) k_gather(const float *__restrict__ n4,
     int64_t pos = b * V + colstart[b * CZ + col];
     const float *p = n4 + b * V + col;
     const uint8_t *m = mask + b * V + col;
-    for (int64_t x = lo; x <= hi; ++x)
-        if (m[x * CZ]) keys[pos++] = f2key(p[x * CZ]);
+    for (int64_t x0 = lo; x0 <= hi; x0 += 8) {   // 8 rows of loads in flight
+        uint8_t mk[8];
+        float v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) mk[k] = x0 + k <= hi ? m[(x0 + k) * CZ] : 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = mk[k] ? p[(x0 + k) * CZ] : 0.0f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if (mk[k]) keys[pos++] = f2key(v[k]);
+    }
 }
 
 // =============================================================================================
@@ -507,44 +516,89 @@ void vh_launch_border(vh_batch *b, const uint8_t *d_in, uint8_t *d_out) {
 // to the lower); iterate until the partition is stable (<= 300).  One block per volume.
 // =============================================================================================
 #define KM_K 4
+#define KM_TILE 1024
+#define KM_LDS_TILES 4096
+
+// wave-cooperative sum of sorted values k[i], i in tile t intersected with [a, e): lane l adds
+// elements t*1024 + j*64 + l for j = 0..15 in order, then a fixed shuffle tree (deterministic)
+__device__ __forceinline__ double km_tile_sum(const uint32_t *k, int64_t t, int64_t a, int64_t e) {
+    const int lane = threadIdx.x & 63;
+    double acc = 0.0;
+    float v[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int64_t i = t * KM_TILE + j * 64 + lane;
+        v[j] = (i >= a && i < e) ? key2f(k[i]) : 0.0f;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) acc += (double)v[j];
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
+    return __shfl(acc, 0, 64);
+}
+
+// first index in [0, n) whose value is strictly closer to chi than to clo (values sorted, so the
+// predicate is monotone): 64-ary search, one probe per lane per round
+__device__ __forceinline__ int64_t km_boundary(const uint32_t *k, int64_t n, double clo, double chi) {
+    const int lane = threadIdx.x & 63;
+    int64_t lo = 0, hi = n;   // answer in [lo, hi]
+    while (hi - lo > 64) {
+        const int64_t span = hi - lo;
+        const int64_t p = lo + (span * (lane + 1)) / 65;
+        const double x = (double)key2f(k[p]);
+        const bool pr = fabs(x - chi) < fabs(x - clo);
+        const uint64_t m = __ballot(pr);
+        if (m == 0ull) {
+            lo = lo + (span * 64) / 65 + 1;
+        } else {
+            const int f = __ffsll((long long)m) - 1;        // first lane with predicate true
+            const int64_t pf = lo + (span * (f + 1)) / 65;
+            const int64_t pprev = f == 0 ? lo - 1 : lo + (span * f) / 65;
+            lo = pprev + 1;
+            hi = pf;
+        }
+    }
+    const int64_t p = lo + lane;
+    bool pr = true;
+    if (p < hi) {
+        const double x = (double)key2f(k[p]);
+        pr = fabs(x - chi) < fabs(x - clo);
+    }
+    const uint64_t m = __ballot(pr);
+    return lo + (__ffsll((long long)m) - 1);
+}
+
+// One block (4 waves) per volume.  Cluster sums: head partial tile + whole-tile sums + tail
+// partial tile, in tile order (deterministic).
 __global__ void __launch_bounds__(VH_TPB) k_kmeans(const uint32_t *__restrict__ keys,
-                                                  int64_t V, VolScalars *sc) {
-    // Chunk t = [t*per, (t+1)*per) of the sorted values.  A cluster sum is sum_t p_t in t order,
-    // p_t = sequential sum over chunk t intersected with the cluster: a fully covered chunk uses
-    // its precomputed total (the same sequential sum), so an iteration only loops over the <= 2
-    // chunks cut by each boundary.
+                                                  int64_t V, double *tile_scratch,
+                                                  int64_t max_ktiles, VolScalars *sc) {
+    __shared__ double s_tiles[KM_LDS_TILES];
     __shared__ double s_c[KM_K];
     __shared__ int64_t s_cut[KM_K + 1], s_new[KM_K + 1];
-    __shared__ double s_tot[VH_TPB];
-    __shared__ double s_part[KM_K][VH_TPB];
     __shared__ int s_done;
     const int64_t b = blockIdx.x;
     const int64_t n = sc[b].n_mask;
-    const uint32_t *k = keys + b * V;
-    const int t = threadIdx.x;
     if (n <= 0) return;
+    const uint32_t *k = keys + b * V;
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    const int64_t nt = (n + KM_TILE - 1) / KM_TILE;
+    double *gt = tile_scratch + b * max_ktiles;
+    const bool in_lds = nt <= KM_LDS_TILES;
+    for (int64_t tt = w; tt < nt; tt += VH_TPB / 64) {
+        const double ts = km_tile_sum(k, tt, 0, n);
+        if (lane == 0) {
+            if (in_lds) s_tiles[tt] = ts;
+            else gt[tt] = ts;
+        }
+    }
     if (t < KM_K) s_c[t] = (double)key2f(k[(n * (2 * t + 1)) / (2 * KM_K)]);
     if (t == 0) { s_cut[0] = -1; s_done = 0; }
-    const int64_t per = (n + VH_TPB - 1) / VH_TPB;
-    const int64_t cs = t * per < n ? t * per : n, ce = cs + per < n ? cs + per : n;
-    {
-        double tot = 0.0;
-        for (int64_t i = cs; i < ce; ++i) tot += (double)key2f(k[i]);
-        s_tot[t] = tot;
-    }
     __syncthreads();
     int it = 0;
     for (it = 1; it <= 300; ++it) {
-        if (t < KM_K - 1) {
-            // first index whose value is strictly closer to c[t+1] than to c[t]
-            const double clo = s_c[t], chi = s_c[t + 1];
-            int64_t lo = 0, hi = n;
-            while (lo < hi) {
-                const int64_t mid = (lo + hi) >> 1;
-                const double x = (double)key2f(k[mid]);
-                if (fabs(x - chi) < fabs(x - clo)) hi = mid; else lo = mid + 1;
-            }
-            s_new[t + 1] = lo;
+        if (w < KM_K - 1) {
+            const int64_t c = km_boundary(k, n, s_c[w], s_c[w + 1]);
+            if (lane == 0) s_new[w + 1] = c;
         }
         __syncthreads();
         if (t == 0) {
@@ -559,23 +613,19 @@ __global__ void __launch_bounds__(VH_TPB) k_kmeans(const uint32_t *__restrict__ 
         }
         __syncthreads();
         if (s_done) break;
-        for (int j = 0; j < KM_K; ++j) {
-            const int64_t a = s_cut[j], e = s_cut[j + 1];
-            double p = 0.0;
-            if (cs >= a && ce <= e) {
-                p = s_tot[t];
-            } else {
-                const int64_t lo = cs > a ? cs : a, hi = ce < e ? ce : e;
-                for (int64_t i = lo; i < hi; ++i) p += (double)key2f(k[i]);
+        {   // wave w updates centre w
+            const int64_t a = s_cut[w], e = s_cut[w + 1];
+            if (e > a) {
+                const int64_t ta = a / KM_TILE, te = (e - 1) / KM_TILE;
+                const double head = km_tile_sum(k, ta, a, e);
+                const double tail = te != ta ? km_tile_sum(k, te, a, e) : 0.0;
+                if (lane == 0) {
+                    double sum = head;
+                    for (int64_t tt = ta + 1; tt < te; ++tt) sum += in_lds ? s_tiles[tt] : gt[tt];
+                    if (te != ta) sum += tail;
+                    s_c[w] = sum / (double)(e - a);
+                }
             }
-            s_part[j][t] = p;
-        }
-        __syncthreads();
-        if (t < KM_K) {
-            double s = 0.0;
-            for (int i = 0; i < VH_TPB; ++i) s += s_part[t][i];
-            const int64_t cnt = s_cut[t + 1] - s_cut[t];
-            if (cnt > 0) s_c[t] = s / (double)cnt;
         }
         __syncthreads();
     }
@@ -775,7 +825,9 @@ void vh_launch_vdp_chain(vh_batch *b, const float *d_n4, const vh_run_opts &o) {
     }
     if (o.do_kmeans) {
         ScopedKTimer tm(b, "kmeans", 0.0);
-        k_kmeans<<<(unsigned)b->nb, VH_TPB, 0, st>>>(b->d_keys0, b->V, b->d_sc);
+        const int64_t max_ktiles = (b->V + KM_TILE - 1) / KM_TILE;
+        double *scratch = reinterpret_cast<double *>(b->d_keys1);   // free after the sort (4V >= 8V/1024 B)
+        k_kmeans<<<(unsigned)b->nb, VH_TPB, 0, st>>>(b->d_keys0, b->V, scratch, max_ktiles, b->d_sc);
         VH_CHECK_LAUNCH();
     }
     if (o.do_snr) vh_launch_snr(b);

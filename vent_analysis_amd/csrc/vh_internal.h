@@ -118,12 +118,13 @@ struct vh_batch {
     uint64_t *d_cohort = nullptr;
     // N4 workspace
     float *d_L0 = nullptr, *d_B = nullptr, *d_lat = nullptr, *d_E = nullptr;
-    double *d_Q1 = nullptr, *d_Q2 = nullptr, *d_P1 = nullptr, *d_num = nullptr, *d_den = nullptr;
+    double *d_fitpart = nullptr;     // [nb][tiles][lattice] per-tile contracted fit slabs
+    double *d_P1 = nullptr, *d_num = nullptr, *d_den = nullptr;
     uint64_t *d_hist = nullptr;
     N4State *d_st = nullptr;
     int32_t *d_nactive = nullptr;
     void *d_tabs = nullptr;          // device copy of all per-level axis tables
-    int64_t lat_cap = 0, q1_cap = 0, q2_cap = 0, p1_cap = 0;
+    int64_t lat_cap = 0, q1_cap = 0, q2_cap = 0;
     std::vector<size_t> tab_off;     // offsets of each (level, axis) table in d_tabs
     vh_n4_params tab_prm{};          // parameters the tables were built for
     bool tabs_valid = false;
