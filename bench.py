@@ -112,6 +112,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="no HIP events in the timed region")
+    ap.add_argument("--subbatch", type=int, default=0, help="volumes per N4 sub-batch (0: all)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -141,8 +142,9 @@ def main():
         _lib.comm_init(world, rank, uid[0], device=local)
     vox = (1.5, 1.5, 10.0)
     opts = Bt.options(do_n4=not args.no_n4, vox=vox, do_cohort=True,
-                      profile=not args.no_profile)
-    warm = Bt.options(do_n4=not args.no_n4, vox=vox, do_cohort=True, profile=False)
+                      profile=not args.no_profile, n4_subbatch=args.subbatch)
+    warm = Bt.options(do_n4=not args.no_n4, vox=vox, do_cohort=True, profile=False,
+                      n4_subbatch=args.subbatch)
 
     def step(o):
         Bt.run(o)
@@ -216,7 +218,7 @@ def main():
                                "mean-anchored + linear-binning + k-means VDP + defect border + "
                                "SNR + cohort histogram" + (" (N4 skipped)" if args.no_n4 else ""),
                    "volumes_per_gpu": nb, "shape": [R, C, Z],
-                   "parallelism": f"dp{world}",
+                   "parallelism": f"dp{world}", "n4_subbatch": args.subbatch or nb,
                    "n4_iterations_mean": float(its.sum(axis=1).mean()) if its.size else 0.0},
         "roofline": roof,
         "cpu_baseline": cpu,

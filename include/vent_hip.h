@@ -84,6 +84,9 @@ typedef struct {
     int32_t do_cohort;       /* accumulate the cohort histogram (1024 u64 bins, [0,1.5) of p99-normalised masked N4) */
     int32_t profile;         /* 1: time kernel classes with HIP events (vh_batch_kernel_time) */
     double vox[3];           /* voxel size (mm) for the volume scalars */
+    int32_t n4_subbatch;     /* volumes per N4 sub-batch (0 = whole batch); smaller sub-batches
+                                keep an iteration's working set in the 256 MiB Infinity Cache */
+    int32_t pad0;
 } vh_run_opts;
 
 #define VH_COHORT_BINS 1024

@@ -40,7 +40,8 @@ class VdpResult(ct.Structure):
 class RunOpts(ct.Structure):
     _fields_ = [("do_n4", ct.c_int32), ("n4", N4Params), ("thresh", ct.c_float),
                 ("do_snr", ct.c_int32), ("do_kmeans", ct.c_int32), ("do_cohort", ct.c_int32),
-                ("profile", ct.c_int32), ("vox", ct.c_double * 3)]
+                ("profile", ct.c_int32), ("vox", ct.c_double * 3), ("n4_subbatch", ct.c_int32),
+                ("pad0", ct.c_int32)]
 
 
 class VentHipError(RuntimeError):
@@ -296,7 +297,7 @@ class Batch:
 
     @staticmethod
     def options(do_n4=True, thresh=0.6, do_snr=True, do_kmeans=True, do_cohort=False,
-                profile=False, vox=(1.0, 1.0, 1.0), **n4kw) -> RunOpts:
+                profile=False, vox=(1.0, 1.0, 1.0), n4_subbatch=0, **n4kw) -> RunOpts:
         o = RunOpts()
         lib().vh_default_run_opts(ct.byref(o))
         o.do_n4 = int(bool(do_n4))
@@ -308,6 +309,7 @@ class Batch:
         o.profile = int(bool(profile))
         for i in range(3):
             o.vox[i] = float(vox[i])
+        o.n4_subbatch = int(n4_subbatch)
         return o
 
     def run(self, opts: RunOpts):

@@ -101,7 +101,7 @@ static void batch_free(vh_batch *b) {
     dfree(b->d_sc); dfree(b->d_part); dfree(b->d_keys0); dfree(b->d_keys1); dfree(b->d_tilecnt);
     dfree(b->d_cohort);
     dfree(b->d_L0); dfree(b->d_B); dfree(b->d_lat); dfree(b->d_E);
-    dfree(b->d_fitpart); dfree(b->d_P1); dfree(b->d_num); dfree(b->d_den);
+    dfree(b->d_fitpart); dfree(b->d_rowstart); dfree(b->d_P1); dfree(b->d_num); dfree(b->d_den); dfree(b->d_T);
     dfree(b->d_hist); dfree(b->d_st); dfree(b->d_nactive); dfree(b->d_tabs); dfree(b->d_twiddle);
     dfree(b->d_bitmap); dfree(b->d_ci_list); dfree(b->d_ci_shell); dfree(b->d_ci_hist);
     delete b;
@@ -134,7 +134,9 @@ static vh_batch *batch_new(vh_ctx *ctx, int64_t R, int64_t C, int64_t Z, int64_t
         dalloc(&b->d_sc, (size_t)nb);
         b->part_blocks = (b->CZ + VH_TPB - 1) / VH_TPB;
         const int64_t max_chunks = (b->V + 8191) / 8192;
-        dalloc(&b->d_part, (size_t)nb * std::max<int64_t>(b->part_blocks * 4, max_chunks));
+        const int64_t eval_slots = ((b->CZ + 63) / 64) * ((R + 15) / 16);   // n4 eval partial slots
+        dalloc(&b->d_part, (size_t)nb * std::max<int64_t>(std::max<int64_t>(b->part_blocks * 4, max_chunks),
+                                                         eval_slots * 2));
         dalloc(&b->d_keys0, NV);
         dalloc(&b->d_keys1, NV);
         dalloc(&b->d_tilecnt, (size_t)nb * 256 * b->max_tiles);
@@ -160,6 +162,7 @@ static void batch_run(vh_batch *b, const vh_run_opts &o, int n4_src) {
     HIP_TRY(hipSetDevice(b->ctx->device));
     b->profile = o.profile != 0;
     b->opts = o;
+    b->n4_subbatch = o.n4_subbatch;
     if (o.do_n4) {
         if (o.n4.n_levels < 1 || o.n4.n_levels > VH_MAX_LEVELS || o.n4.spline_order != 3 ||
             o.n4.n_bins < 2 || o.n4.n_bins > VH_MAX_BINS || o.n4.ncp[0] < 4 || o.n4.ncp[1] < 4 ||

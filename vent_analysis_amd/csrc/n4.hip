@@ -16,6 +16,7 @@
 //
 // Per iteration (one launch each, all volumes of the batch in one grid; converged volumes exit):
 //   ctrl -> exact_min (rare) -> hist -> emap -> fit -> contract -> eval
+#include <algorithm>
 #include <cfloat>
 #include <climits>
 #include <cstring>
@@ -27,27 +28,20 @@ struct DevAxis {
     const float *w;
     const double *sw2;
     const double *isw2;   // 1 / sw2
+    const double *w2;     // [n][4] w^2 (double)
+    const double *w3;     // [n][4] w^3 (double)
     int32_t n, ncp;
 };
 struct DevLevel {
     DevAxis ax[3];
+    // per 64-column fit tile: {y0, y1, z0, z1} (first/last column's col and slice), then
+    // {jlo, JT, klo, KT} (lattice cols / slices the tile's slab covers)
+    const int4 *tiles;
 };
 
-struct FitTile {
-    int yb, zb;        // tile extent
-    int nty, ntz;      // tiles per volume along cols / slices
-};
 
-__host__ __device__ inline FitTile fit_tile(int64_t C, int64_t Z) {
-    FitTile t;
-    t.zb = (int)(Z < VH_TPB ? Z : VH_TPB);
-    t.yb = VH_TPB / t.zb;
-    if (t.yb > C) t.yb = (int)C;
-    t.nty = (int)((C + t.yb - 1) / t.yb);
-    t.ntz = (int)((Z + t.zb - 1) / t.zb);
-    return t;
-}
-
+#define TILE_W 64   // columns per compact tile (one wave)
+#define SEG_R 16    // rows per wave segment
 #define LN2 0.69314718055994530942
 #define PI_D 3.14159265358979323846
 
@@ -108,7 +102,8 @@ void vh_n4_prepare_tables(vh_batch *b, const vh_n4_params &prm) {
     if (b->tabs_valid && same_params(b->tab_prm, prm)) return;
     const int64_t dims[3] = {b->R, b->C, b->Z};
     std::vector<uint8_t> blob;
-    b->tab_off.assign((size_t)prm.n_levels * 3 * 4, 0);
+    b->tab_off.assign((size_t)prm.n_levels * 3 * 6, 0);
+    b->fit_pmax.assign((size_t)prm.n_levels, 4);
     auto push = [&](const void *p, size_t bytes) {
         size_t off = (blob.size() + 15) & ~(size_t)15;
         blob.resize(off + bytes);
@@ -122,13 +117,56 @@ void vh_n4_prepare_tables(vh_batch *b, const vh_n4_params &prm) {
         for (int a = 0; a < 3; ++a) {
             AxisTab t;
             vh_axis_tables((int)dims[a], level_ncp(prm, L, a), eps, t);
-            std::vector<double> inv(t.sw2.size());
+            std::vector<double> inv(t.sw2.size()), w2(t.w.size()), w3(t.w.size());
             for (size_t i = 0; i < inv.size(); ++i) inv[i] = 1.0 / t.sw2[i];
-            b->tab_off[(L * 3 + a) * 4 + 0] = push(t.base.data(), t.base.size() * 4);
-            b->tab_off[(L * 3 + a) * 4 + 1] = push(t.w.data(), t.w.size() * 4);
-            b->tab_off[(L * 3 + a) * 4 + 2] = push(t.sw2.data(), t.sw2.size() * 8);
-            b->tab_off[(L * 3 + a) * 4 + 3] = push(inv.data(), inv.size() * 8);
+            for (size_t i = 0; i < w2.size(); ++i) {
+                const double w = t.w[i];
+                w2[i] = w * w;
+                w3[i] = w * w * w;
+            }
+            b->tab_off[(L * 3 + a) * 6 + 0] = push(t.base.data(), t.base.size() * 4);
+            b->tab_off[(L * 3 + a) * 6 + 1] = push(t.w.data(), t.w.size() * 4);
+            b->tab_off[(L * 3 + a) * 6 + 2] = push(t.sw2.data(), t.sw2.size() * 8);
+            b->tab_off[(L * 3 + a) * 6 + 3] = push(inv.data(), inv.size() * 8);
+            b->tab_off[(L * 3 + a) * 6 + 4] = push(w2.data(), w2.size() * 8);
+            b->tab_off[(L * 3 + a) * 6 + 5] = push(w3.data(), w3.size() * 8);
+            if (a == 0) {   // widest control-point window of one fit row-wave (see fit_geo)
+                const int R = (int)dims[0], nseg = (R + 15) / 16, W = nseg < 16 ? nseg : 16;
+                const int RW = ((nseg + W - 1) / W) * 16;
+                int pm = 4;
+                for (int x0 = 0; x0 < R; x0 += RW) {
+                    const int x1 = std::min(R, x0 + RW) - 1;
+                    pm = std::max(pm, t.base[x1] - t.base[x0] + 4);
+                }
+                b->fit_pmax[L] = pm;
+            }
         }
+    }
+    // fit tile metadata per level (64-column tiles of the (col, slice) plane)
+    const int64_t ntiles = (b->CZ + TILE_W - 1) / TILE_W;
+    b->tile_off.assign((size_t)prm.n_levels, 0);
+    b->fit_smax.assign((size_t)prm.n_levels, 0);
+    for (int L = 0; L < prm.n_levels; ++L) {
+        const float eps = vh_bspline_eps(std::max({level_ncp(prm, L, 0), level_ncp(prm, L, 1),
+                                                   level_ncp(prm, L, 2)}) - 3);
+        AxisTab ty, tz;
+        vh_axis_tables((int)b->C, level_ncp(prm, L, 1), eps, ty);
+        vh_axis_tables((int)b->Z, level_ncp(prm, L, 2), eps, tz);
+        std::vector<int32_t> meta(8 * (size_t)ntiles);
+        int smax = 0;
+        for (int64_t t = 0; t < ntiles; ++t) {
+            const int64_t c0 = t * TILE_W, c1 = std::min(c0 + TILE_W, b->CZ) - 1;
+            const int y0 = (int)(c0 / b->Z), y1 = (int)(c1 / b->Z);
+            const int z0 = (int)(c0 % b->Z), z1 = (int)(c1 % b->Z);
+            const int zlo = y0 == y1 ? z0 : 0, zhi = y0 == y1 ? z1 : (int)b->Z - 1;
+            const int jlo = ty.base[y0], JT = ty.base[y1] + 4 - jlo;
+            const int klo = tz.base[zlo], KT = tz.base[zhi] + 4 - klo;
+            const int32_t m[8] = {y0, y1, z0, z1, jlo, JT, klo, KT};
+            std::memcpy(&meta[8 * t], m, sizeof(m));
+            smax = std::max(smax, level_ncp(prm, L, 0) * (y1 - y0 + 1) * KT);
+        }
+        b->tile_off[L] = push(meta.data(), meta.size() * 4);
+        b->fit_smax[L] = smax;
     }
     if (b->d_tabs) HIP_TRY(hipFree(b->d_tabs));
     b->d_tabs = nullptr;
@@ -154,13 +192,16 @@ static DevLevel dev_level(const vh_batch *b, const vh_n4_params &prm, int L) {
     const int64_t dims[3] = {b->R, b->C, b->Z};
     const uint8_t *base = (const uint8_t *)b->d_tabs;
     for (int a = 0; a < 3; ++a) {
-        lv.ax[a].base = (const int32_t *)(base + b->tab_off[(L * 3 + a) * 4 + 0]);
-        lv.ax[a].w = (const float *)(base + b->tab_off[(L * 3 + a) * 4 + 1]);
-        lv.ax[a].sw2 = (const double *)(base + b->tab_off[(L * 3 + a) * 4 + 2]);
-        lv.ax[a].isw2 = (const double *)(base + b->tab_off[(L * 3 + a) * 4 + 3]);
+        lv.ax[a].base = (const int32_t *)(base + b->tab_off[(L * 3 + a) * 6 + 0]);
+        lv.ax[a].w = (const float *)(base + b->tab_off[(L * 3 + a) * 6 + 1]);
+        lv.ax[a].sw2 = (const double *)(base + b->tab_off[(L * 3 + a) * 6 + 2]);
+        lv.ax[a].isw2 = (const double *)(base + b->tab_off[(L * 3 + a) * 6 + 3]);
+        lv.ax[a].w2 = (const double *)(base + b->tab_off[(L * 3 + a) * 6 + 4]);
+        lv.ax[a].w3 = (const double *)(base + b->tab_off[(L * 3 + a) * 6 + 5]);
         lv.ax[a].n = (int32_t)dims[a];
         lv.ax[a].ncp = level_ncp(prm, L, a);
     }
+    lv.tiles = (const int4 *)(base + b->tile_off[L]);
     return lv;
 }
 
@@ -187,12 +228,22 @@ void vh_ensure_n4_workspace(vh_batch *b, const vh_n4_params &prm) {
         b->lat_cap = lat;
     }
     if (cx > 64) throw VhError{VH_ERR_ARG, "N4 lattice too fine: > 64 control points along rows"};
-    const FitTile ft = fit_tile(b->C, b->Z);
-    const int64_t fp = (int64_t)ft.nty * ft.ntz * lat;   // per-volume tile slabs
+    const int64_t ntiles = (b->CZ + TILE_W - 1) / TILE_W;
+    if (b->d_rowstart == nullptr || b->n4_tiles != ntiles) {
+        if (b->d_rowstart) HIP_TRY(hipFree(b->d_rowstart));
+        HIP_TRY(hipMalloc(&b->d_rowstart, sizeof(int32_t) * b->nb * ntiles * b->R));
+        b->n4_tiles = ntiles;
+    }
+    const int64_t fp = ntiles * lat;   // per-volume tile slabs
     if (fp > b->q1_cap) {
         if (b->d_fitpart) HIP_TRY(hipFree(b->d_fitpart));
         HIP_TRY(hipMalloc(&b->d_fitpart, sizeof(double) * b->nb * fp));
         b->q1_cap = fp;
+    }
+    if (cx * b->CZ > b->t_cap) {
+        if (b->d_T) HIP_TRY(hipFree(b->d_T));
+        HIP_TRY(hipMalloc(&b->d_T, sizeof(float) * b->nb * cx * b->CZ));
+        b->t_cap = cx * b->CZ;
     }
     if (q2 > b->q2_cap) {
         if (b->d_P1) HIP_TRY(hipFree(b->d_P1));
@@ -225,13 +276,22 @@ __device__ __forceinline__ T block_sum_fixed(T v, T *s_red) {
     return r;
 }
 
+// Convergence measure from the eval partials, reduced by one wave in a fixed order (lane l sums
+// slots l, l+64, ...; then a shuffle tree): deterministic.  Returns the value in every lane.
 __device__ __forceinline__ double conv_from_parts(const double *part, int64_t nparts, int64_t b,
                                                   double N) {
+    const int lane = threadIdx.x & 63;
     double sd = 0.0, sd2 = 0.0;
-    for (int64_t p = 0; p < nparts; ++p) {
+    for (int64_t p = lane; p < nparts; p += 64) {
         sd += part[(b * nparts + p) * 2];
         sd2 += part[(b * nparts + p) * 2 + 1];
     }
+    for (int off = 32; off > 0; off >>= 1) {
+        sd += __shfl_down(sd, off, 64);
+        sd2 += __shfl_down(sd2, off, 64);
+    }
+    sd = __shfl(sd, 0, 64);
+    sd2 = __shfl(sd2, 0, 64);
     // CoV of p = exp(B_old - B_new) over masked voxels, with d = p - 1 (no cancellation)
     const double mu = 1.0 + sd / N;
     double var = (sd2 - sd * sd / N) / (N - 1.0);
@@ -253,103 +313,158 @@ __global__ void k_n4_state_init(N4State *st, int64_t nb) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// column-sweep scaffolding.  A lane owns one (col, slice) column; the wave walks the UNION of its
-// lanes' masked row ranges in aligned chunks of 8 rows (row index wave-uniform, so the B-spline
-// row weights are scalar loads), each lane predicating on its column's mask==1 row bitmap.  All 8
-// rows' loads of a chunk are issued before any is used (memory-level parallelism).
+// Compact N4 state.  The mask==1 voxels of a volume are stored in "tile-row" order: column tiles
+// of 64 consecutive (col, slice) columns -- one wave, one lane per column -- then rows, then the
+// set lanes of that row in lane order.  rs[b][tile][x] is the start of (tile, row x); a lane's
+// slot is rs + mbcnt(ballot(its bit)).  A wave processes one tile x 16-row segment: 16 coalesced
+// loads per array in flight, only masked bytes move, one memory round trip per wave.
 // ---------------------------------------------------------------------------------------------
-#define SW_CHUNK 8
+#define VH_OOB 0x80000000u
 
-struct ColSweep {
-    int64_t col;      // column index in the volume (valid iff col < CZ)
-    bool valid;
-    int wlo, whi;     // wave-uniform row range (wlo > whi: nothing to do)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t vol_rsrc(const float *base, int64_t V) {
+    return __builtin_amdgcn_make_buffer_rsrc((void *)base, 0, (int)(V * 4), 0x00020000);
+}
+__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, 0, 0));
+}
+__device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, uint32_t voff, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)voff, 0, 0);
+}
+__device__ __forceinline__ int lanes_below(uint64_t m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+struct Seg {
+    int64_t col;      // this lane's column
+    int tile, x0;     // wave-uniform tile and first row
+    uint32_t m;       // this lane's mask==1 bits for rows x0..x0+15
+    uint32_t off[SEG_R];   // byte offsets into the volume's compact arrays (VH_OOB when unset)
 };
 
-__device__ __forceinline__ ColSweep col_sweep_begin(const int32_t *colrange, int64_t b,
-                                                    int64_t CZ, int64_t R) {
-    ColSweep s;
-    s.col = blockIdx.x * (int64_t)VH_TPB + threadIdx.x;
-    s.valid = s.col < CZ;
-    int lo = (int)R, hi = -1;
-    if (s.valid) {
-        lo = colrange[(b * CZ + s.col) * 2];
-        hi = colrange[(b * CZ + s.col) * 2 + 1];
-    }
-    for (int off = 32; off > 0; off >>= 1) {
-        lo = min(lo, __shfl_xor(lo, off, 64));
-        hi = max(hi, __shfl_xor(hi, off, 64));
-    }
-    s.wlo = __builtin_amdgcn_readfirstlane(lo);
-    s.whi = __builtin_amdgcn_readfirstlane(hi);
-    return s;
-}
-
-__device__ __forceinline__ uint32_t chunk_bits(const uint32_t *colbits, const ColSweep &s,
-                                               int64_t b, int64_t nw, int64_t CZ, int x0) {
-    if (!s.valid) return 0u;
-    const uint32_t w = colbits[(b * nw + (x0 >> 5)) * CZ + s.col];
-    return (w >> (x0 & 31)) & 0xffu;
-}
-
-// L0 = log(I) at mask == 1 (non-positive -> 0), B = 0, U = L0 and the first U range.
-__global__ void __launch_bounds__(VH_TPB) k_n4_init(const float *__restrict__ I,
-                                                   const uint32_t *__restrict__ colbits,
-                                                   const int32_t *colrange,
-                                                   const VolScalars *sc, int64_t R, int64_t CZ,
-                                                   int64_t V, float *L0, float *B, float *U,
-                                                   N4State *st) {
-    __shared__ uint32_t s_max, s_min;
-    const int64_t b = blockIdx.y;
-    if (threadIdx.x == 0) { s_max = 0u; s_min = 0xffffffffu; }
-    __syncthreads();
-    const ColSweep cs = col_sweep_begin(colrange, b, CZ, R);
+// one wave = (tile, 16-row segment); x0 multiple of 16 so the bits sit in one 32-row word
+__device__ __forceinline__ void seg_begin(Seg &s, const uint32_t *colbits, const int32_t *rs,
+                                          int64_t b, int64_t R, int64_t CZ, int64_t ntiles,
+                                          int tile, int x0) {
+    const int lane = threadIdx.x & 63;
     const int64_t nw = (R + 31) >> 5;
-    const int64_t first = sc[b].first_masked;
-    uint32_t kmax = 0u, kmin = 0xffffffffu;
-    for (int x0 = cs.wlo & ~(SW_CHUNK - 1); x0 <= cs.whi; x0 += SW_CHUNK) {
-        const uint32_t m8 = chunk_bits(colbits, cs, b, nw, CZ, x0);
-        float a[SW_CHUNK];
+    s.tile = tile;
+    s.x0 = x0;
+    s.col = (int64_t)tile * TILE_W + lane;
+    s.m = 0u;
+    if (s.col < CZ && x0 < R) s.m = (colbits[(b * nw + (x0 >> 5)) * CZ + s.col] >> (x0 & 31)) & 0xffffu;
+    const int32_t *r = rs + (b * ntiles + tile) * R;
 #pragma unroll
-        for (int k = 0; k < SW_CHUNK; ++k)
-            a[k] = (m8 >> k) & 1u ? I[b * V + (int64_t)(x0 + k) * CZ + cs.col] : 0.0f;
-#pragma unroll
-        for (int k = 0; k < SW_CHUNK; ++k) {
-            if (!((m8 >> k) & 1u)) continue;
-            const int64_t r = (int64_t)(x0 + k) * CZ + cs.col, v = b * V + r;
-            const float l = a[k] > 0.0f ? (float)log((double)a[k]) : 0.0f;
-            L0[v] = l;
-            B[v] = 0.0f;
-            U[v] = l;
-            const uint32_t key = f2key(l);
-            kmax = key > kmax ? key : kmax;
-            if (r == first) st[b].u_first = l;
-            else kmin = key < kmin ? key : kmin;
+    for (int k = 0; k < SEG_R; ++k) {
+        const bool on = (s.m >> k) & 1u;
+        const uint64_t bal = __ballot(on);
+        const int32_t rk = x0 + k < R ? r[x0 + k] : 0;   // wave-uniform guard: ragged last segment
+        s.off[k] = on ? (uint32_t)((rk + lanes_below(bal)) * 4) : VH_OOB;
+    }
+}
+
+// per (volume, tile, row): number of mask==1 lanes (pass 1 of the compact offsets)
+__global__ void __launch_bounds__(64) k_n4_rowcount(const uint32_t *colbits, int64_t R,
+                                                   int64_t CZ, int64_t ntiles, int32_t *rs) {
+    const int64_t b = blockIdx.y;
+    const int tile = blockIdx.x;
+    const int64_t col = (int64_t)tile * TILE_W + threadIdx.x;
+    const int64_t nw = (R + 31) >> 5;
+    int32_t *out = rs + (b * ntiles + tile) * R;
+    for (int64_t w = 0; w < nw; ++w) {
+        const uint32_t bits = col < CZ ? colbits[(b * nw + w) * CZ + col] : 0u;
+        for (int k = 0; k < 32 && w * 32 + k < R; ++k) {
+            const uint64_t bal = __ballot((bits >> k) & 1u);
+            if (threadIdx.x == 0) out[w * 32 + k] = __popcll(bal);
         }
     }
-    if (kmax) atomicMax(&s_max, kmax);
-    if (kmin != 0xffffffffu) atomicMin(&s_min, kmin);
+}
+
+// pass 2: exclusive scan over (tile, row) in tile-major order, one block per volume
+__global__ void __launch_bounds__(VH_TPB) k_n4_rowscan(int32_t *rs, int64_t n) {
+    __shared__ int64_t s_part[VH_TPB];
+    const int64_t b = blockIdx.x;
+    int32_t *a = rs + b * n;
+    const int t = threadIdx.x;
+    const int64_t per = (n + VH_TPB - 1) / VH_TPB;
+    const int64_t s0 = t * per < n ? t * per : n, e0 = s0 + per < n ? s0 + per : n;
+    int64_t acc = 0;
+    for (int64_t i = s0; i < e0; ++i) acc += a[i];
+    s_part[t] = acc;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        if (s_max) atomicMax(&st[b].umax_key, s_max);
-        if (s_min != 0xffffffffu) atomicMin(&st[b].umin_key, s_min);
+    if (t == 0) {
+        int64_t run = 0;
+        for (int i = 0; i < VH_TPB; ++i) { const int64_t v = s_part[i]; s_part[i] = run; run += v; }
+    }
+    __syncthreads();
+    int64_t run = s_part[t];
+    for (int64_t i = s0; i < e0; ++i) { const int32_t v = a[i]; a[i] = (int32_t)run; run += v; }
+}
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+    for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off, 64));
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+    for (int off = 32; off > 0; off >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, off, 64));
+    return v;
+}
+
+// L0 = log(I) at mask == 1 (non-positive -> 0), B = 0, U = L0 (compact) and the first U range.
+// grid (ceil(tiles/4), segments, volumes), 4 waves = 4 tiles per block.
+__global__ void __launch_bounds__(VH_TPB) k_n4_init(const float *__restrict__ I,
+                                                   const uint32_t *__restrict__ colbits,
+                                                   const int32_t *rs, const VolScalars *sc,
+                                                   int64_t R, int64_t CZ, int64_t V, int64_t ntiles,
+                                                   float *L0, float *B, float *U, N4State *st,
+                                                   int64_t vol0) {
+    const int64_t b = vol0 + blockIdx.z;
+    const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (tile >= ntiles) return;
+    Seg s;
+    seg_begin(s, colbits, rs, b, R, CZ, ntiles, tile, blockIdx.y * SEG_R);
+    const __amdgpu_buffer_rsrc_t rL = vol_rsrc(L0 + b * V, V), rB = vol_rsrc(B + b * V, V),
+                                 rU = vol_rsrc(U + b * V, V);
+    const int64_t first = sc[b].first_masked;
+    uint32_t kmax = 0u, kmin = 0xffffffffu;
+#pragma unroll
+    for (int k = 0; k < SEG_R; ++k) {
+        if (!((s.m >> k) & 1u)) continue;
+        const int64_t r = (int64_t)(s.x0 + k) * CZ + s.col;
+        const float a = I[b * V + r];
+        const float l = a > 0.0f ? (float)log((double)a) : 0.0f;
+        bstore(rL, s.off[k], l);
+        bstore(rB, s.off[k], 0.0f);
+        bstore(rU, s.off[k], l);
+        const uint32_t key = f2key(l);
+        kmax = key > kmax ? key : kmax;
+        if (r == first) st[b].u_first = l;
+        else kmin = key < kmin ? key : kmin;
+    }
+    kmax = wave_max_u32(kmax);
+    kmin = wave_min_u32(kmin);
+    if ((threadIdx.x & 63) == 0) {
+        if (kmax) atomicMax(&st[b].umax_key, kmax);
+        if (kmin != 0xffffffffu) atomicMin(&st[b].umin_key, kmin);
     }
 }
 
 // Iteration control: convergence of the previous iteration, the while-condition of ITK's loop,
 // bin range (common case of the else-if quirk), histogram reset.
-__global__ void k_n4_ctrl(N4State *st, const double *part, int64_t nparts, const VolScalars *sc,
-                          int level, int it, float thresh, int bins, int64_t nb,
-                          uint64_t *hist, int32_t *nactive) {
-    const int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (b >= nb) return;
+__global__ void __launch_bounds__(64) k_n4_ctrl(N4State *st, const double *part, int64_t nparts,
+                                               const VolScalars *sc, int level, int it,
+                                               float thresh, int bins, int64_t vol0,
+                                               int32_t *nactive) {
+    const int64_t b = vol0 + blockIdx.x;
     N4State &s = st[b];
+    const bool was_active = s.active;
+    double conv = 0.0;
+    if (it > 0 && was_active) conv = conv_from_parts(part, nparts, b, (double)sc[b].n_mask1);
+    if (threadIdx.x != 0) return;
     if (it == 0) {
         s.active = 1;
         s.iters = 0;
         s.conv = INFINITY;
-    } else if (s.active) {
-        const double conv = conv_from_parts(part, nparts, b, (double)sc[b].n_mask1);
+    } else if (was_active) {
         s.conv = conv;
         if (!(conv > (double)thresh)) {
             s.active = 0;
@@ -371,42 +486,56 @@ __global__ void k_n4_ctrl(N4State *st, const double *part, int64_t nparts, const
     }
     s.umax_key = 0u;
     s.umin_key = 0xffffffffu;
-    for (int i = 0; i < VH_MAX_BINS; ++i) hist[b * VH_MAX_BINS + i] = 0ull;
     atomicAdd(nactive, 1);
 }
 
-__global__ void k_n4_level_end(N4State *st, const double *part, int64_t nparts,
-                               const VolScalars *sc, int level, int64_t nb) {
-    const int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (b >= nb) return;
+__global__ void __launch_bounds__(64) k_n4_level_end(N4State *st, const double *part,
+                                                    int64_t nparts, const VolScalars *sc,
+                                                    int level, int64_t vol0) {
+    const int64_t b = vol0 + blockIdx.x;
     N4State &s = st[b];
-    if (s.active) {
-        const double conv = conv_from_parts(part, nparts, b, (double)sc[b].n_mask1);
-        s.conv = conv;
-        s.iters_level[level] = s.iters;
-        s.conv_level[level] = (float)conv;
-        s.active = 0;
-    }
+    if (!s.active) return;
+    const double conv = conv_from_parts(part, nparts, b, (double)sc[b].n_mask1);
+    if (threadIdx.x != 0) return;
+    s.conv = conv;
+    s.iters_level[level] = s.iters;
+    s.conv_level[level] = (float)conv;
+    s.active = 0;
 }
 
 // Exact ITK bin minimum when the first masked pixel is the strict minimum: min over the pixels
-// that are not running maxima in raster order (chunked prefix-max scan).  One block per volume.
+// that are not running maxima in raster order (chunked prefix-max scan over rows).  Rare path,
+// one block per volume; each thread walks whole rows, tracking compact offsets incrementally.
+__device__ __forceinline__ void exact_row_scan(const float *Uv, const uint32_t *colbits,
+                                               const int32_t *rs, int64_t b, int64_t R, int64_t CZ,
+                                               int64_t ntiles, int64_t x, float &run, float &mn,
+                                               bool track_min) {
+    const int64_t nw = (R + 31) >> 5;
+    int64_t off = 0;
+    for (int64_t col = 0; col < CZ; ++col) {
+        if ((col & (TILE_W - 1)) == 0) off = rs[(b * ntiles + col / TILE_W) * R + x];
+        if (!((colbits[(b * nw + (x >> 5)) * CZ + col] >> (x & 31)) & 1u)) continue;
+        const float u = Uv[off++];
+        if (u > run) run = u;
+        else if (track_min && u < mn) mn = u;
+    }
+}
+
 __global__ void __launch_bounds__(VH_TPB) k_n4_exact_min(const float *__restrict__ U,
-                                                        const uint8_t *__restrict__ mask,
-                                                        int64_t V, int bins, N4State *st) {
+                                                        const uint32_t *__restrict__ colbits,
+                                                        const int32_t *rs, int64_t R, int64_t CZ,
+                                                        int64_t V, int64_t ntiles, int bins,
+                                                        N4State *st, int64_t vol0) {
     __shared__ float s_cmax[VH_TPB];
     __shared__ float s_min[VH_TPB];
-    const int64_t b = blockIdx.x;
+    const int64_t b = vol0 + blockIdx.x;
     if (!st[b].active || !st[b].need_exact_min) return;
     const int t = threadIdx.x;
-    const int64_t per = (V + VH_TPB - 1) / VH_TPB;
-    const int64_t s0 = t * per, e0 = s0 + per < V ? s0 + per : V;
-    float cmax = -FLT_MAX;
-    for (int64_t r = s0; r < e0; ++r)
-        if (mask[b * V + r] == 1) {
-            const float u = U[b * V + r];
-            cmax = u > cmax ? u : cmax;
-        }
+    const int64_t per = (R + VH_TPB - 1) / VH_TPB;
+    const int64_t s0 = t * per < R ? t * per : R, e0 = s0 + per < R ? s0 + per : R;
+    const float *Uv = U + b * V;
+    float cmax = -FLT_MAX, dummy = FLT_MAX;
+    for (int64_t x = s0; x < e0; ++x) exact_row_scan(Uv, colbits, rs, b, R, CZ, ntiles, x, cmax, dummy, false);
     s_cmax[t] = cmax;
     __syncthreads();
     if (t == 0) {
@@ -415,12 +544,7 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_exact_min(const float *__restrict
     }
     __syncthreads();
     float run = s_cmax[t], mn = FLT_MAX;
-    for (int64_t r = s0; r < e0; ++r)
-        if (mask[b * V + r] == 1) {
-            const float u = U[b * V + r];
-            if (u > run) run = u;
-            else if (u < mn) mn = u;
-        }
+    for (int64_t x = s0; x < e0; ++x) exact_row_scan(Uv, colbits, rs, b, R, CZ, ntiles, x, run, mn, true);
     s_min[t] = mn;
     __syncthreads();
     if (t == 0) {
@@ -432,32 +556,33 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_exact_min(const float *__restrict
 }
 
 // Triangular Parzen histogram of U at mask == 1, unsigned 64-bit fixed point (2^-32 units).
-// Neighbouring rows of a column fall in the same bin most of the time: each lane keeps a run
-// (bin, two weights) in registers and only touches LDS when the bin changes.
+// Per lane a run (bin, two weights) over its 16 rows, per block an LDS histogram, then one global
+// 64-bit atomic per touched bin (integer adds: deterministic).
 __global__ void __launch_bounds__(VH_TPB) k_n4_hist(const float *__restrict__ U,
                                                    const uint32_t *__restrict__ colbits,
-                                                   const int32_t *colrange, int64_t R,
-                                                   int64_t CZ, int64_t V, int bins,
-                                                   const N4State *st, uint64_t *hist) {
+                                                   const int32_t *rs, int64_t R, int64_t CZ,
+                                                   int64_t V, int64_t ntiles, int bins,
+                                                   const N4State *st, uint64_t *hist,
+                                                   int64_t vol0) {
     __shared__ unsigned long long H[VH_MAX_BINS];
-    const int64_t b = blockIdx.y;
+    const int64_t b = vol0 + blockIdx.z;
     if (!st[b].active) return;
     for (int i = threadIdx.x; i < VH_MAX_BINS; i += VH_TPB) H[i] = 0ull;
     __syncthreads();
-    const float bmin = st[b].bin_min, slope = st[b].slope;
-    const ColSweep cs = col_sweep_begin(colrange, b, CZ, R);
-    const int64_t nw = (R + 31) >> 5;
-    int cur = -1;
-    unsigned long long w0 = 0ull, w1 = 0ull;
-    for (int x0 = cs.wlo & ~(SW_CHUNK - 1); x0 <= cs.whi; x0 += SW_CHUNK) {
-        const uint32_t m8 = chunk_bits(colbits, cs, b, nw, CZ, x0);
-        float u[SW_CHUNK];
+    const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (tile < ntiles) {
+        Seg s;
+        seg_begin(s, colbits, rs, b, R, CZ, ntiles, tile, blockIdx.y * SEG_R);
+        const __amdgpu_buffer_rsrc_t rU = vol_rsrc(U + b * V, V);
+        float u[SEG_R];
 #pragma unroll
-        for (int k = 0; k < SW_CHUNK; ++k)
-            u[k] = (m8 >> k) & 1u ? U[b * V + (int64_t)(x0 + k) * CZ + cs.col] : 0.0f;
+        for (int k = 0; k < SEG_R; ++k) u[k] = bload(rU, s.off[k]);
+        const float bmin = st[b].bin_min, slope = st[b].slope;
+        int cur = -1;
+        unsigned long long w0 = 0ull, w1 = 0ull;
 #pragma unroll
-        for (int k = 0; k < SW_CHUNK; ++k) {
-            if (!((m8 >> k) & 1u)) continue;
+        for (int k = 0; k < SEG_R; ++k) {
+            if (!((s.m >> k) & 1u)) continue;
             const float cidx = (u[k] - bmin) / slope;
             if (!(cidx >= 0.0f) || !(cidx < (float)bins)) continue;
             const int idx = (int)floorf(cidx);
@@ -483,10 +608,10 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_hist(const float *__restrict__ U,
             w0 += a0;
             w1 += a1;
         }
-    }
-    if (cur >= 0) {
-        if (w0) atomicAdd(&H[cur], w0);
-        if (w1) atomicAdd(&H[cur + 1], w1);
+        if (cur >= 0) {
+            if (w0) atomicAdd(&H[cur], w0);
+            if (w1) atomicAdd(&H[cur + 1], w1);
+        }
     }
     __syncthreads();
     for (int i = threadIdx.x; i < bins; i += VH_TPB)
@@ -525,10 +650,11 @@ __device__ __forceinline__ float expf_cr(float x) { return (float)exp((double)x)
 // E(u|v) map (Wiener deconvolution of the histogram by the bias Gaussian), one block per volume.
 __global__ void __launch_bounds__(VH_TPB) k_n4_emap(const uint64_t *hist, const double2 *tw,
                                                    int bins, float fwhm, float noise,
-                                                   const N4State *st, float *Eout) {
+                                                   const N4State *st, float *Eout, int64_t vol0,
+                                                   uint64_t *hist_rw) {
     __shared__ double2 V[VH_FFT_P], F[VH_FFT_P], U[VH_FFT_P], NUM[VH_FFT_P], DEN[VH_FFT_P],
         TMP[VH_FFT_P];
-    const int64_t b = blockIdx.x;
+    const int64_t b = vol0 + blockIdx.x;
     if (!st[b].active) return;
     const int P = VH_FFT_P, off = (P - bins) / 2;
     const int t = threadIdx.x;
@@ -536,6 +662,7 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_emap(const uint64_t *hist, const 
     for (int n = t; n < P; n += VH_TPB) {
         const int h = n - off;
         V[n] = make_double2(h >= 0 && h < bins ? (double)hist[b * VH_MAX_BINS + h] * (1.0 / 4294967296.0) : 0.0, 0.0);
+        if (h >= 0 && h < bins) hist_rw[b * VH_MAX_BINS + h] = 0ull;   // ready for the next iteration
         F[n] = make_double2(0.0, 0.0);
     }
     __syncthreads();
@@ -591,188 +718,194 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_emap(const uint64_t *hist, const 
 }
 
 // ---------------------------------------------------------------------------------------------
-// Fit sweep with in-block contraction.  A block owns a tile of YB cols x ZB slices (YB*ZB <= 256
-// columns, one per thread); after the row sweep (same sliding window as k_n4_fitsweep) every
-// thread holds Q1[i] of its column in LDS, and the block contracts its tile over cols and slices:
-//   Pn[i][j][k] = sum_{y in tile} sum_{z in tile} wy(y,j)^p wz(z,k)^p Q1[i][y][z]
-// for the lattice rows j / slices k its tile touches.  Only that small slab goes to HBM; the
-// contract kernel adds the slabs of a volume's tiles in tile order (deterministic).
-// p = 3 (MODE 0, numerator) or 2 (MODE 1, denominator).
+// Fit with in-block contraction.  Block = one 64-column tile x W row-waves (wave w owns rows
+// [w RW, (w+1) RW)); every lane runs the sliding 4-wide window of the row contraction over its
+// wave's rows, the per-wave partials are summed per column in wave order (deterministic), then
+// the block contracts its 64 columns over cols and slices:
+//   Pn[i][j][k] = sum_{(y,z) in tile} wy(y,j)^p wz(z,k)^p Q1[i][y][z],  p = 3 (num) / 2 (den)
+// Only that small slab goes to HBM; k_n4_tilesum adds a volume's slabs in tile order.
 // ---------------------------------------------------------------------------------------------
+// fit block geometry shared by host and device
+struct FitGeo {
+    int W;      // waves per block
+    int RW;     // rows per wave (multiple of SEG_R)
+    int PMAX;   // partial control points per wave
+};
+
 template <int MODE>
-__global__ void __launch_bounds__(VH_TPB) k_n4_fitblock(const float *__restrict__ U,
-                                                       const uint32_t *__restrict__ colbits,
-                                                       const int32_t *colrange, int64_t R,
-                                                       int64_t C, int64_t Z, int64_t V, int bins,
-                                                       const N4State *st, const float *E,
-                                                       DevLevel lv, int64_t slab, double *part) {
-    extern __shared__ __attribute__((aligned(16))) double sQ1[];   // [ncx][VH_TPB]
+__global__ void k_n4_fit(const float *__restrict__ U, const uint32_t *__restrict__ colbits,
+                         const int32_t *rs, int64_t R, int64_t C, int64_t Z, int64_t V,
+                         int64_t ntiles, int bins, const N4State *st, const float *E, DevLevel lv,
+                         FitGeo g, int64_t slab, double *part, int64_t vol0) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
     __shared__ float sE[VH_MAX_BINS];
-    const int64_t b = blockIdx.y;
+    const int64_t b = vol0 + blockIdx.y;
     if (MODE == 0 && !st[b].active) return;
-    const FitTile ft = fit_tile(C, Z);
     const int tile = blockIdx.x;
-    const int ty0 = (tile / ft.ntz) * ft.yb, tz0 = (tile % ft.ntz) * ft.zb;
-    const int ny = (int)(C - ty0 < ft.yb ? C - ty0 : ft.yb);
-    const int nz = (int)(Z - tz0 < ft.zb ? Z - tz0 : ft.zb);
-    const int tid = threadIdx.x;
-    const int ly = tid / ft.zb, lz = tid % ft.zb;
-    const bool mine = ly < ny && lz < nz;
-    const int64_t CZ = C * Z;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const DevAxis ax = lv.ax[0], ay = lv.ax[1], az = lv.ax[2];
     const int ncx = ax.ncp;
-    for (int i = 0; i < ncx; ++i) sQ1[i * VH_TPB + tid] = 0.0;
+    const int64_t CZ = C * Z;
+    double *sQ1 = smem;                         // [ncx][64]
+    double *sP = smem + (size_t)ncx * TILE_W;   // [W][PMAX][64]
     if (MODE == 0)
-        for (int i = tid; i < bins; i += VH_TPB) sE[i] = E[b * VH_MAX_BINS + i];
-    // ---- row sweep of this thread's column (wave-uniform chunked rows) ----
-    ColSweep cs;
-    cs.col = (int64_t)(ty0 + ly) * Z + (tz0 + lz);
-    cs.valid = mine;
-    {
-        int lo = (int)R, hi = -1;
-        if (mine) {
-            lo = colrange[(b * CZ + cs.col) * 2];
-            hi = colrange[(b * CZ + cs.col) * 2 + 1];
-        }
-        for (int off = 32; off > 0; off >>= 1) {
-            lo = min(lo, __shfl_xor(lo, off, 64));
-            hi = max(hi, __shfl_xor(hi, off, 64));
-        }
-        cs.wlo = __builtin_amdgcn_readfirstlane(lo);
-        cs.whi = __builtin_amdgcn_readfirstlane(hi);
-    }
+        for (int i = threadIdx.x; i < bins; i += blockDim.x) sE[i] = E[b * VH_MAX_BINS + i];
+    for (int i = threadIdx.x; i < g.W * g.PMAX * TILE_W; i += blockDim.x) sP[i] = 0.0;
     __syncthreads();
-    if (cs.wlo <= cs.whi) {
-        const int64_t nw = (R + 31) >> 5;
-        float bmin = 0.0f, slope = 1.0f;
-        if (MODE == 0) {
-            bmin = st[b].bin_min;
-            slope = st[b].slope;
-        }
-        double isyz = 1.0;
-        if (mine) isyz = ay.isw2[ty0 + ly] * az.isw2[tz0 + lz];
-        const int xs = cs.wlo & ~(SW_CHUNK - 1);
-        int wb = ax.base[xs];
+    // ---- row contraction of this wave's rows ----
+    const int64_t col = (int64_t)tile * TILE_W + lane;
+    const bool mine = col < CZ;
+    double isyz = 1.0;
+    if (mine) isyz = ay.isw2[col / Z] * az.isw2[col % Z];
+    float bmin = 0.0f, slope = 1.0f;
+    if (MODE == 0) {
+        bmin = st[b].bin_min;
+        slope = st[b].slope;
+    }
+    const int xw0 = w * g.RW;
+    const int xw1 = (xw0 + g.RW < R ? xw0 + g.RW : (int)R);
+    if (xw0 < xw1) {
+        const int ib0 = ax.base[xw0];
+        int wb = ib0;
         double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-        for (int x0 = xs; x0 <= cs.whi; x0 += SW_CHUNK) {
-            const uint32_t m8 = chunk_bits(colbits, cs, b, nw, CZ, x0);
-            float u[SW_CHUNK];
+        double *P = sP + (size_t)w * g.PMAX * TILE_W + lane;
+        const __amdgpu_buffer_rsrc_t rU = vol_rsrc(U + b * V, V);
+        for (int x0 = xw0; x0 < xw1; x0 += SEG_R) {
+            Seg s;
+            seg_begin(s, colbits, rs, b, R, CZ, ntiles, tile, x0);
+            float u[SEG_R];
             if (MODE == 0) {
 #pragma unroll
-                for (int k = 0; k < SW_CHUNK; ++k)
-                    u[k] = (m8 >> k) & 1u ? U[b * V + (int64_t)(x0 + k) * CZ + cs.col] : 0.0f;
+                for (int k = 0; k < SEG_R; ++k) u[k] = bload(rU, s.off[k]);
             }
 #pragma unroll
-            for (int k = 0; k < SW_CHUNK; ++k) {
+            for (int k = 0; k < SEG_R; ++k) {
                 const int x = x0 + k;
-                if (x >= R) break;
+                if (x >= xw1) break;
                 const int bx = ax.base[x];
                 while (wb < bx) {
-                    sQ1[wb * VH_TPB + tid] = a0;
+                    P[(wb - ib0) * TILE_W] = a0;
                     a0 = a1; a1 = a2; a2 = a3; a3 = 0.0;
                     ++wb;
                 }
-                if (!((m8 >> k) & 1u)) continue;
-                const float4 w = *reinterpret_cast<const float4 *>(ax.w + 4 * x);
-                const double w0 = w.x, w1 = w.y, w2 = w.z, w3 = w.w;
+                if (!((s.m >> k) & 1u)) continue;
+                const double *wp = (MODE == 0 ? ax.w3 : ax.w2) + 4 * x;   // wave-uniform row
                 if (MODE == 0) {
                     const float r = u[k] - sharpen_value(u[k], bmin, slope, sE, bins);
                     const double q = ((double)r * ax.isw2[x]) * isyz;
-                    a0 += (w0 * w0 * w0) * q;
-                    a1 += (w1 * w1 * w1) * q;
-                    a2 += (w2 * w2 * w2) * q;
-                    a3 += (w3 * w3 * w3) * q;
+                    a0 = fma(wp[0], q, a0);
+                    a1 = fma(wp[1], q, a1);
+                    a2 = fma(wp[2], q, a2);
+                    a3 = fma(wp[3], q, a3);
                 } else {
-                    a0 += w0 * w0;
-                    a1 += w1 * w1;
-                    a2 += w2 * w2;
-                    a3 += w3 * w3;
+                    a0 += wp[0];
+                    a1 += wp[1];
+                    a2 += wp[2];
+                    a3 += wp[3];
                 }
             }
         }
-        sQ1[wb * VH_TPB + tid] = a0;
-        if (wb + 1 < ncx) sQ1[(wb + 1) * VH_TPB + tid] = a1;
-        if (wb + 2 < ncx) sQ1[(wb + 2) * VH_TPB + tid] = a2;
-        if (wb + 3 < ncx) sQ1[(wb + 3) * VH_TPB + tid] = a3;
+        P[(wb - ib0) * TILE_W] = a0;
+        if (wb + 1 < ncx) P[(wb + 1 - ib0) * TILE_W] = a1;
+        if (wb + 2 < ncx) P[(wb + 2 - ib0) * TILE_W] = a2;
+        if (wb + 3 < ncx) P[(wb + 3 - ib0) * TILE_W] = a3;
     }
     __syncthreads();
-    // ---- contract the tile over cols and slices ----
-    const int jlo = ay.base[ty0], jhi = ay.base[ty0 + ny - 1] + 3;
-    const int klo = az.base[tz0], khi = az.base[tz0 + nz - 1] + 3;
-    const int JT = jhi - jlo + 1, KT = khi - klo + 1;
-    double *out = part + (b * (int64_t)(ft.nty * ft.ntz) + tile) * slab;
-    for (int e = tid; e < ncx * JT * KT; e += VH_TPB) {
-        const int i = e / (JT * KT), jj = (e / KT) % JT, kk = e % KT;
-        const int j = jlo + jj, kq = klo + kk;
+    // ---- per column: sum the wave partials in wave order ----
+    for (int e = threadIdx.x; e < ncx * TILE_W; e += blockDim.x) {
+        const int i = e / TILE_W, l = e % TILE_W;
         double acc = 0.0;
-        for (int yy = 0; yy < ny; ++yy) {
-            const int cy = j - ay.base[ty0 + yy];
+        for (int ww = 0; ww < g.W; ++ww) {
+            const int r0 = ww * g.RW;
+            if (r0 >= R) break;
+            const int ib = ax.base[r0];
+            const int o = i - ib;
+            if (o >= 0 && o < g.PMAX) acc += sP[((size_t)ww * g.PMAX + o) * TILE_W + l];
+        }
+        sQ1[e] = acc;
+    }
+    __syncthreads();
+    // ---- contract the tile's columns: over slices per tile row (stage 1), then over cols ----
+    const int4 m0 = lv.tiles[2 * tile], m1 = lv.tiles[2 * tile + 1];
+    const int y0 = m0.x, y1 = m0.y, ny = y1 - y0 + 1;
+    const int jlo = m1.x, JT = m1.y, klo = m1.z, KT = m1.w;
+    const int64_t c0 = (int64_t)tile * TILE_W;
+    const double *wzp = MODE == 0 ? az.w3 : az.w2;
+    const double *wyp = MODE == 0 ? ay.w3 : ay.w2;
+    double *sS = sP;   // [ncx][ny][KT], reuses the wave-partial space
+    for (int e = threadIdx.x; e < ncx * ny * KT; e += blockDim.x) {
+        const int i = e / (ny * KT), yy = (e / KT) % ny, k = klo + e % KT;
+        const int y = y0 + yy;
+        const int zs = y == y0 ? m0.z : 0, ze = y == y1 ? m0.w : (int)Z - 1;
+        const int lb = (int)((int64_t)y * Z - c0);   // lane of (y, z = 0)
+        double acc = 0.0;
+        for (int z = zs; z <= ze; ++z) {
+            const int cz = k - az.base[z];
+            if (cz < 0 || cz > 3) continue;
+            acc = fma(wzp[4 * z + cz], sQ1[i * TILE_W + lb + z], acc);
+        }
+        sS[e] = acc;
+    }
+    __syncthreads();
+    double *out = part + (b * ntiles + tile) * slab;
+    for (int e = threadIdx.x; e < ncx * JT * KT; e += blockDim.x) {
+        const int i = e / (JT * KT), j = jlo + (e / KT) % JT, kk = e % KT;
+        double acc = 0.0;
+        for (int y = y0; y <= y1; ++y) {
+            const int cy = j - ay.base[y];
             if (cy < 0 || cy > 3) continue;
-            const double wyv = ay.w[4 * (ty0 + yy) + cy];
-            const double wyp = MODE == 0 ? wyv * wyv * wyv : wyv * wyv;
-            double accz = 0.0;
-            for (int zz = 0; zz < nz; ++zz) {
-                const int cz = kq - az.base[tz0 + zz];
-                if (cz < 0 || cz > 3) continue;
-                const double wzv = az.w[4 * (tz0 + zz) + cz];
-                const double wzp = MODE == 0 ? wzv * wzv * wzv : wzv * wzv;
-                accz += wzp * sQ1[i * VH_TPB + yy * ft.zb + zz];
-            }
-            acc += wyp * accz;
+            acc = fma(wyp[4 * y + cy], sS[(i * ny + (y - y0)) * KT + kk], acc);
         }
         out[e] = acc;
     }
 }
 
-// Sum the tile slabs of each volume (tile order), then MODE 1: den; MODE 0: phi = num/den,
-// lattice += phi, P1[i][j][z] = sum_k wz(z,k) lat[i][j][k] for the eval sweep.  One block/volume.
+// Sum the tile slabs of each volume in tile order: MODE 1 den; MODE 0 phi = num / den and
+// lattice += phi.  grid (volumes, lattice chunks of 256).
 template <int MODE>
 __global__ void __launch_bounds__(VH_TPB) k_n4_tilesum(const double *part, int64_t slab,
-                                                      float *lat, double *den, double *P1,
-                                                      int64_t C, int64_t Z, int64_t lat_cap,
-                                                      int64_t q2_cap, const N4State *st,
-                                                      DevLevel lv) {
-    const int64_t b = blockIdx.x;
+                                                      int64_t ntiles, float *lat, double *den,
+                                                      int64_t lat_cap, const N4State *st,
+                                                      DevLevel lv, int64_t vol0) {
+    const int64_t b = vol0 + blockIdx.x;
     if (MODE == 0 && !st[b].active) return;
-    const FitTile ft = fit_tile(C, Z);
-    const int ntiles = ft.nty * ft.ntz;
-    const DevAxis ay = lv.ax[1], az = lv.ax[2];
-    const int ncx = lv.ax[0].ncp, ncy = ay.ncp, ncz = az.ncp;
-    float *L = lat + b * lat_cap;
-    double *D = den + b * lat_cap;
-    for (int e = threadIdx.x; e < ncx * ncy * ncz; e += VH_TPB) {
-        const int i = e / (ncy * ncz), j = (e / ncz) % ncy, kq = e % ncz;
-        double acc = 0.0;
-        for (int tile = 0; tile < ntiles; ++tile) {
-            const int ty0 = (tile / ft.ntz) * ft.yb, tz0 = (tile % ft.ntz) * ft.zb;
-            const int ny = (int)(C - ty0 < ft.yb ? C - ty0 : ft.yb);
-            const int nz = (int)(Z - tz0 < ft.zb ? Z - tz0 : ft.zb);
-            const int jlo = ay.base[ty0], jhi = ay.base[ty0 + ny - 1] + 3;
-            const int klo = az.base[tz0], khi = az.base[tz0 + nz - 1] + 3;
-            if (j < jlo || j > jhi || kq < klo || kq > khi) continue;
-            const int JT = jhi - jlo + 1, KT = khi - klo + 1;
-            acc += part[(b * (int64_t)ntiles + tile) * slab + (i * JT + (j - jlo)) * KT + (kq - klo)];
-        }
-        if (MODE == 1) {
-            D[e] = acc;
-        } else {
-            const double d = D[e];
-            const float phi = d != 0.0 ? (float)(acc / d) : 0.0f;
-            L[e] = L[e] + phi;
-        }
+    const int ncx = lv.ax[0].ncp, ncy = lv.ax[1].ncp, ncz = lv.ax[2].ncp;
+    const int e = blockIdx.y * VH_TPB + threadIdx.x;
+    if (e >= ncx * ncy * ncz) return;
+    const int i = e / (ncy * ncz), j = (e / ncz) % ncy, kq = e % ncz;
+    double acc = 0.0;
+    const double *pb = part + b * ntiles * slab;
+    for (int64_t tile = 0; tile < ntiles; ++tile) {
+        const int4 m = lv.tiles[2 * tile + 1];   // jlo, JT, klo, KT
+        const int jj = j - m.x, kk = kq - m.z;
+        if (jj < 0 || jj >= m.y || kk < 0 || kk >= m.w) continue;
+        acc += pb[tile * slab + (i * m.y + jj) * m.w + kk];
     }
-    if (MODE == 0) {
-        __syncthreads();
-        double *p1 = P1 + b * q2_cap;
-        for (int64_t e = threadIdx.x; e < (int64_t)ncx * ncy * Z; e += VH_TPB) {
-            const int64_t ij = e / Z, z = e % Z;
-            const int bz = az.base[z];
-            const float4 w = *reinterpret_cast<const float4 *>(az.w + 4 * z);
-            const float *l = L + ij * ncz + bz;
-            p1[e] = (double)w.x * (double)l[0] + (double)w.y * (double)l[1] +
-                    (double)w.z * (double)l[2] + (double)w.w * (double)l[3];
-        }
+    if (MODE == 1) {
+        den[b * lat_cap + e] = acc;
+    } else {
+        const double d = den[b * lat_cap + e];
+        const float phi = d != 0.0 ? (float)(acc / d) : 0.0f;
+        lat[b * lat_cap + e] += phi;
     }
+}
+
+// P1[i][j][z] = sum_k wz(z,k) lat[i][j][k] for the eval sweep.  grid (volumes, chunks of 256).
+__global__ void __launch_bounds__(VH_TPB) k_n4_P1(const float *lat, int64_t lat_cap, double *P1,
+                                                 int64_t q2_cap, int64_t Z, const N4State *st,
+                                                 DevLevel lv, int64_t vol0, int all) {
+    const int64_t b = vol0 + blockIdx.x;
+    if (!all && !st[b].active) return;
+    const DevAxis az = lv.ax[2];
+    const int ncx = lv.ax[0].ncp, ncy = lv.ax[1].ncp, ncz = az.ncp;
+    const int64_t e = blockIdx.y * (int64_t)VH_TPB + threadIdx.x;
+    if (e >= (int64_t)ncx * ncy * Z) return;
+    const int64_t ij = e / Z, z = e % Z;
+    const int bz = az.base[z];
+    const float4 w = *reinterpret_cast<const float4 *>(az.w + 4 * z);
+    const float *l = lat + b * lat_cap + ij * ncz + bz;
+    P1[b * q2_cap + e] = (double)w.x * (double)l[0] + (double)w.y * (double)l[1] +
+                         (double)w.z * (double)l[2] + (double)w.w * (double)l[3];
 }
 
 // T(i) = sum_j wy(y,j) P1[i][j][z] for one column
@@ -782,89 +915,100 @@ __device__ __forceinline__ double col_T(const double *p1, int i, int ncy, int64_
     return (double)wy.x * r[0] + (double)wy.y * r[Z] + (double)wy.z * r[2 * Z] + (double)wy.w * r[3 * Z];
 }
 
-// Evaluate the new field at masked voxels, convergence partials, U = L0 - B and its range for the
-// next iteration.
-__global__ void __launch_bounds__(VH_TPB) k_n4_eval(const float *__restrict__ L0, float *B,
-                                                   float *U, const uint32_t *__restrict__ colbits,
-                                                   const int32_t *colrange, const VolScalars *sc,
-                                                   int64_t R, int64_t C, int64_t Z, int64_t V,
-                                                   int64_t q2_cap, const double *P1,
-                                                   DevLevel lv, N4State *st, int64_t nparts,
-                                                   double *part) {
-    __shared__ double s_red[VH_TPB / 64];
-    __shared__ uint32_t s_max, s_min;
-    const int64_t b = blockIdx.y;
+// Per-column contraction of the lattice for the eval sweep: T[i][col] (float).
+__global__ void __launch_bounds__(VH_TPB) k_n4_T(const double *P1, int64_t q2_cap, int64_t C,
+                                                int64_t Z, DevLevel lv, const N4State *st,
+                                                float *T, int64_t tcap, int64_t vol0) {
+    const int64_t b = vol0 + blockIdx.y;
     if (!st[b].active) return;
-    if (threadIdx.x == 0) { s_max = 0u; s_min = 0xffffffffu; }
     const int64_t CZ = C * Z;
-    const ColSweep cs = col_sweep_begin(colrange, b, CZ, R);
-    const int64_t nw = (R + 31) >> 5;
-    double sd = 0.0, sd2 = 0.0;
-    uint32_t kmax = 0u, kmin = 0xffffffffu;
-    if (cs.wlo <= cs.whi) {
-        const int64_t y = cs.valid ? cs.col / Z : 0, z = cs.valid ? cs.col % Z : 0;
-        const int ncy = lv.ax[1].ncp;
-        const int by = lv.ax[1].base[y];
-        const float4 wy = *reinterpret_cast<const float4 *>(lv.ax[1].w + 4 * y);
-        const double *p1 = P1 + b * q2_cap;
-        const DevAxis ax = lv.ax[0];
-        const int64_t first = sc[b].first_masked;
-        const int xs = cs.wlo & ~(SW_CHUNK - 1);
-        int wb = ax.base[xs];
-        // window of T(i), i = wb..wb+3 (double contraction, float value like the lattice)
-        float t0 = (float)col_T(p1, wb, ncy, Z, by, wy, z), t1 = (float)col_T(p1, wb + 1, ncy, Z, by, wy, z);
-        float t2 = (float)col_T(p1, wb + 2, ncy, Z, by, wy, z), t3 = (float)col_T(p1, wb + 3, ncy, Z, by, wy, z);
-        for (int x0 = xs; x0 <= cs.whi; x0 += SW_CHUNK) {
-            const uint32_t m8 = chunk_bits(colbits, cs, b, nw, CZ, x0);
-            float l0[SW_CHUNK], bo[SW_CHUNK];
-#pragma unroll
-            for (int k = 0; k < SW_CHUNK; ++k) {
-                const bool on = (m8 >> k) & 1u;
-                const int64_t v = b * V + (int64_t)(x0 + k) * CZ + cs.col;
-                l0[k] = on ? L0[v] : 0.0f;
-                bo[k] = on ? B[v] : 0.0f;
-            }
-#pragma unroll
-            for (int k = 0; k < SW_CHUNK; ++k) {
-                const int x = x0 + k;
-                if (x >= R) break;
-                const int bx = ax.base[x];
-                while (wb < bx) {
-                    ++wb;
-                    t0 = t1; t1 = t2; t2 = t3;
-                    t3 = (float)col_T(p1, wb + 3, ncy, Z, by, wy, z);
-                }
-                if (!((m8 >> k) & 1u)) continue;
-                const float4 w = *reinterpret_cast<const float4 *>(ax.w + 4 * x);
-                const float bn = ((w.x * t0 + w.y * t1) + w.z * t2) + w.w * t3;
-                const double d = (double)expm1f(bo[k] - bn);   // p - 1, p = exp(B_old - B_new)
-                sd += d;
-                sd2 += d * d;
-                const int64_t r = (int64_t)x * CZ + cs.col, v = b * V + r;
-                B[v] = bn;
-                const float u = l0[k] - bn;
-                U[v] = u;
-                const uint32_t key = f2key(u);
-                kmax = key > kmax ? key : kmax;
-                if (r == first) st[b].u_first = u;
-                else kmin = key < kmin ? key : kmin;
-            }
-        }
-    }
-    __syncthreads();
-    if (kmax) atomicMax(&s_max, kmax);
-    if (kmin != 0xffffffffu) atomicMin(&s_min, kmin);
-    const double tsd = block_sum_fixed(sd, s_red);
-    __syncthreads();
-    const double tsd2 = block_sum_fixed(sd2, s_red);
-    if (threadIdx.x == 0) {
-        part[(b * nparts + blockIdx.x) * 2] = tsd;
-        part[(b * nparts + blockIdx.x) * 2 + 1] = tsd2;
-        if (s_max) atomicMax(&st[b].umax_key, s_max);
-        if (s_min != 0xffffffffu) atomicMin(&st[b].umin_key, s_min);
-    }
+    const int64_t col = blockIdx.x * (int64_t)VH_TPB + threadIdx.x;
+    if (col >= CZ) return;
+    const int64_t y = col / Z, z = col % Z;
+    const int ncy = lv.ax[1].ncp;
+    const int by = lv.ax[1].base[y];
+    const float4 wy = *reinterpret_cast<const float4 *>(lv.ax[1].w + 4 * y);
+    const double *p1 = P1 + b * q2_cap;
+    float *t = T + b * tcap + col;
+    for (int i = 0; i < lv.ax[0].ncp; ++i) t[(int64_t)i * CZ] = (float)col_T(p1, i, ncy, Z, by, wy, z);
 }
 
+// Evaluate the new field at masked voxels: B_new, U = L0 - B_new (compact, in place), the
+// convergence partial sums of exp(B_old - B_new) - 1 (one slot per wave, written without a block
+// barrier) and the U range for the next iteration.
+__global__ void __launch_bounds__(VH_TPB) k_n4_eval(const float *__restrict__ L0, float *B,
+                                                   float *U, const uint32_t *__restrict__ colbits,
+                                                   const int32_t *rs, const VolScalars *sc,
+                                                   int64_t R, int64_t CZ, int64_t V,
+                                                   int64_t ntiles, const float *T, int64_t tcap,
+                                                   DevLevel lv, N4State *st, int64_t nparts,
+                                                   double *part, int64_t vol0) {
+    const int64_t b = vol0 + blockIdx.z;
+    if (!st[b].active) return;
+    const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (tile >= ntiles) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t slot = (int64_t)blockIdx.y * ntiles + tile;
+    Seg s;
+    seg_begin(s, colbits, rs, b, R, CZ, ntiles, tile, blockIdx.y * SEG_R);
+    double sd = 0.0, sd2 = 0.0;
+    uint32_t kmax = 0u, kmin = 0xffffffffu;
+    if (__ballot(s.m != 0u)) {
+        const __amdgpu_buffer_rsrc_t rL = vol_rsrc(L0 + b * V, V), rB = vol_rsrc(B + b * V, V),
+                                     rU = vol_rsrc(U + b * V, V);
+        float la[SEG_R], ba[SEG_R];
+#pragma unroll
+        for (int k = 0; k < SEG_R; ++k) {
+            la[k] = bload(rL, s.off[k]);
+            ba[k] = bload(rB, s.off[k]);
+        }
+        const DevAxis ax = lv.ax[0];
+        const float *Tb = T + b * tcap + (s.col < CZ ? s.col : 0);
+        int wb = ax.base[s.x0 < R ? s.x0 : (int)R - 1];
+        float t0 = 0.f, t1 = 0.f, t2 = 0.f, t3 = 0.f;
+        if (s.m) {
+            t0 = Tb[(int64_t)wb * CZ]; t1 = Tb[(int64_t)(wb + 1) * CZ];
+            t2 = Tb[(int64_t)(wb + 2) * CZ]; t3 = Tb[(int64_t)(wb + 3) * CZ];
+        }
+        const int64_t first = sc[b].first_masked;
+#pragma unroll
+        for (int k = 0; k < SEG_R; ++k) {
+            const int x = s.x0 + k;
+            if (x >= R) break;
+            const int bx = ax.base[x];
+            while (wb < bx) {
+                ++wb;
+                t0 = t1; t1 = t2; t2 = t3;
+                t3 = s.m ? Tb[(int64_t)(wb + 3) * CZ] : 0.f;
+            }
+            if (!((s.m >> k) & 1u)) continue;
+            const float4 w = *reinterpret_cast<const float4 *>(ax.w + 4 * x);
+            const float bn = ((w.x * t0 + w.y * t1) + w.z * t2) + w.w * t3;
+            const float u = la[k] - bn;
+            bstore(rB, s.off[k], bn);
+            bstore(rU, s.off[k], u);
+            const double d = (double)expm1f(ba[k] - bn);   // p - 1, p = exp(B_old - B_new)
+            sd += d;
+            sd2 = fma(d, d, sd2);
+            const uint32_t key = f2key(u);
+            kmax = key > kmax ? key : kmax;
+            if ((int64_t)x * CZ + s.col == first) st[b].u_first = u;
+            else kmin = key < kmin ? key : kmin;
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        sd += __shfl_down(sd, off, 64);
+        sd2 += __shfl_down(sd2, off, 64);
+    }
+    kmax = wave_max_u32(kmax);
+    kmin = wave_min_u32(kmin);
+    if (lane == 0) {
+        part[(b * nparts + slot) * 2] = sd;
+        part[(b * nparts + slot) * 2 + 1] = sd2;
+        if (kmax) atomicMax(&st[b].umax_key, kmax);
+        if (kmin != 0xffffffffu) atomicMin(&st[b].umin_key, kmin);
+    }
+}
 // Exact cubic B-spline subdivision (spans doubled on every axis), axis by axis, one block/volume.
 __device__ void refine_axis_dev(const float *in, float *out, int d0, int d1, int d2, int axis) {
     int od[3] = {d0, d1, d2};
@@ -886,8 +1030,8 @@ __device__ void refine_axis_dev(const float *in, float *out, int d0, int d1, int
 }
 
 __global__ void __launch_bounds__(VH_TPB) k_n4_refine(float *lat, int64_t lat_cap, int64_t nb,
-                                                     int n0, int n1, int n2) {
-    const int64_t b = blockIdx.x;
+                                                     int n0, int n1, int n2, int64_t vol0) {
+    const int64_t b = vol0 + blockIdx.x;
     float *L = lat + b * lat_cap;
     float *T1 = lat + (nb + b) * lat_cap;
     float *T2 = lat + (2 * nb + b) * lat_cap;
@@ -933,110 +1077,171 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_final(const float *__restrict__ I
 // ---------------------------------------------------------------------------------------------
 // host driver
 // ---------------------------------------------------------------------------------------------
+// Fit block geometry: W row-waves of RW rows (RW a multiple of SEG_R), PMAX = most control points
+// one wave's rows touch at level L (bounds the per-wave partial window in LDS).
+static FitGeo fit_geo(const vh_batch *b, int L) {
+    FitGeo g;
+    const int R = (int)b->R;
+    const int nseg = (R + SEG_R - 1) / SEG_R;
+    int W = nseg < 16 ? nseg : 16;
+    const int segs_per_wave = (nseg + W - 1) / W;
+    g.RW = segs_per_wave * SEG_R;
+    g.W = (R + g.RW - 1) / g.RW;
+    g.PMAX = b->fit_pmax[L];
+    (void)W;
+    return g;
+}
+
+static size_t fit_lds_bytes(const FitGeo &g, int ncx, int smax) {
+    return sizeof(double) * ((size_t)ncx * TILE_W + std::max((size_t)g.W * g.PMAX * TILE_W, (size_t)smax));
+}
+
+// One sub-batch [vol0, vol0 + ns): the whole multi-level loop.
+static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int64_t ns, float *U) {
+    hipStream_t st = b->ctx->stream;
+    const int64_t ntiles = b->n4_tiles;
+    const unsigned nseg = (unsigned)((b->R + SEG_R - 1) / SEG_R);
+    const dim3 cg((unsigned)((b->CZ + VH_TPB - 1) / VH_TPB), (unsigned)ns);
+    const dim3 sg((unsigned)((ntiles + 3) / 4), nseg, (unsigned)ns);   // 4 tile-waves per block
+    const int64_t nparts = ntiles * nseg;   // eval partial slots per volume
+    const int bins = prm.n_bins;
+    const int LOOK = 3;
+    std::vector<hipEvent_t> evs;
+    int32_t *hflag = b->ctx->h_pinned;
+    int total_iters = 0;
+    for (int L = 0; L < prm.n_levels; ++L) total_iters += prm.max_iters[L];
+    HIP_TRY(hipMemsetAsync(b->d_nactive, 0, sizeof(int32_t) * (total_iters + 1), st));
+    int gi = 0;   // iteration slot within this sub-batch
+    float *cL0 = b->d_L0, *cB = b->d_B;
+    const int32_t *rs = b->d_rowstart;
+    try {
+        for (int L = 0; L < prm.n_levels; ++L) {
+            const DevLevel lv = dev_level(b, prm, L);
+            const FitGeo g = fit_geo(b, L);
+            const dim3 fg((unsigned)ntiles, (unsigned)ns);
+            const size_t fit_lds = fit_lds_bytes(g, lv.ax[0].ncp, b->fit_smax[L]);
+            const int64_t nlat = (int64_t)lv.ax[0].ncp * lv.ax[1].ncp * lv.ax[2].ncp;
+            const dim3 lg((unsigned)ns, (unsigned)((nlat + VH_TPB - 1) / VH_TPB));
+            const dim3 pg((unsigned)ns, (unsigned)((nlat / lv.ax[2].ncp * b->Z + VH_TPB - 1) / VH_TPB));
+            const unsigned fit_threads = (unsigned)(g.W * 64);
+            if (fit_lds > 64 * 1024)
+                throw VhError{VH_ERR_ARG, "N4 fit: control-point window exceeds the LDS budget"};
+            {
+                ScopedKTimer tm(b, "n4_den", 0.0);
+                k_n4_fit<1><<<fg, fit_threads, fit_lds, st>>>(U, b->d_colbits, rs, b->R, b->C, b->Z,
+                                                             b->V, ntiles, bins, b->d_st, b->d_E,
+                                                             lv, g, b->lat_cap, b->d_fitpart, vol0);
+                VH_CHECK_LAUNCH();
+                k_n4_tilesum<1><<<lg, VH_TPB, 0, st>>>(b->d_fitpart, b->lat_cap, ntiles, b->d_lat,
+                                                       b->d_den, b->lat_cap, b->d_st, lv, vol0);
+                VH_CHECK_LAUNCH();
+            }
+            const int level_start = (int)evs.size();
+            for (int it = 0; it < prm.max_iters[L]; ++it, ++gi) {
+                k_n4_ctrl<<<(unsigned)ns, 64, 0, st>>>(b->d_st, b->d_part, nparts, b->d_sc, L, it,
+                                                       prm.conv_threshold, bins, vol0,
+                                                       b->d_nactive + gi);
+                VH_CHECK_LAUNCH();
+                HIP_TRY(hipMemcpyAsync(hflag + (gi % 1024), b->d_nactive + gi, sizeof(int32_t),
+                                       hipMemcpyDeviceToHost, st));
+                hipEvent_t ev;
+                HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+                evs.push_back(ev);
+                HIP_TRY(hipEventRecord(ev, st));
+                k_n4_exact_min<<<(unsigned)ns, VH_TPB, 0, st>>>(U, b->d_colbits, rs, b->R, b->CZ,
+                                                                b->V, ntiles, bins, b->d_st, vol0);
+                VH_CHECK_LAUNCH();
+                {
+                    ScopedKTimer tm(b, "n4_hist", 0.0);
+                    k_n4_hist<<<sg, VH_TPB, 0, st>>>(U, b->d_colbits, rs, b->R, b->CZ, b->V, ntiles,
+                                                     bins, b->d_st, b->d_hist, vol0);
+                    VH_CHECK_LAUNCH();
+                }
+                k_n4_emap<<<(unsigned)ns, VH_TPB, 0, st>>>(b->d_hist, b->d_twiddle, bins, prm.fwhm,
+                                                           prm.wiener_noise, b->d_st, b->d_E,
+                                                           vol0, b->d_hist);
+                VH_CHECK_LAUNCH();
+                {
+                    ScopedKTimer tm(b, "n4_fit", 0.0);
+                    k_n4_fit<0><<<fg, fit_threads, fit_lds, st>>>(
+                        U, b->d_colbits, rs, b->R, b->C, b->Z, b->V, ntiles, bins, b->d_st,
+                        b->d_E, lv, g, b->lat_cap, b->d_fitpart, vol0);
+                    VH_CHECK_LAUNCH();
+                }
+                {
+                    ScopedKTimer tm(b, "n4_contract", 0.0);
+                    k_n4_tilesum<0><<<lg, VH_TPB, 0, st>>>(b->d_fitpart, b->lat_cap, ntiles,
+                                                           b->d_lat, b->d_den, b->lat_cap, b->d_st,
+                                                           lv, vol0);
+                    VH_CHECK_LAUNCH();
+                    k_n4_P1<<<pg, VH_TPB, 0, st>>>(b->d_lat, b->lat_cap, b->d_P1, b->q2_cap, b->Z,
+                                                   b->d_st, lv, vol0, 0);
+                    VH_CHECK_LAUNCH();
+                    k_n4_T<<<cg, VH_TPB, 0, st>>>(b->d_P1, b->q2_cap, b->C, b->Z, lv, b->d_st,
+                                                  b->d_T, b->t_cap, vol0);
+                    VH_CHECK_LAUNCH();
+                }
+                {
+                    ScopedKTimer tm(b, "n4_eval", 0.0);
+                    k_n4_eval<<<sg, VH_TPB, 0, st>>>(cL0, cB, U, b->d_colbits, rs, b->d_sc, b->R,
+                                                     b->CZ, b->V, ntiles, b->d_T, b->t_cap, lv,
+                                                     b->d_st, nparts, b->d_part, vol0);
+                    VH_CHECK_LAUNCH();
+                }
+                const int k = (int)evs.size() - 1 - LOOK;
+                if (k >= level_start) {
+                    HIP_TRY(hipEventSynchronize(evs[k]));
+                    if (hflag[(gi - LOOK) % 1024] == 0) { ++gi; break; }
+                }
+            }
+            k_n4_level_end<<<(unsigned)ns, 64, 0, st>>>(b->d_st, b->d_part, nparts, b->d_sc, L,
+                                                        vol0);
+            VH_CHECK_LAUNCH();
+            if (L < prm.n_levels - 1) {
+                k_n4_refine<<<(unsigned)ns, VH_TPB, 0, st>>>(b->d_lat, b->lat_cap, b->nb,
+                                                             lv.ax[0].ncp, lv.ax[1].ncp,
+                                                             lv.ax[2].ncp, vol0);
+                VH_CHECK_LAUNCH();
+            }
+        }
+    } catch (...) {
+        for (auto e : evs) (void)hipEventDestroy(e);
+        throw;
+    }
+    for (auto e : evs) HIP_TRY(hipEventDestroy(e));
+}
+
 void vh_launch_n4(vh_batch *b, const vh_n4_params &prm) {
     hipStream_t st = b->ctx->stream;
     vh_ensure_n4_workspace(b, prm);
     const dim3 cg = col_grid(b);
-    const int64_t nparts = cg.x;
-    const int bins = prm.n_bins;
-    const double masked_bytes = (double)b->V;   // refined per kernel below
-    (void)masked_bytes;
-    float *U = b->d_n4;   // U = L0 - B lives in the output buffer until k_n4_final overwrites it
+    const int64_t ntiles = b->n4_tiles;
+    // U = L0 - B (compact) lives in the output buffer until k_n4_final overwrites it densely
+    float *U = b->d_n4;
     HIP_TRY(hipMemsetAsync(b->d_lat, 0, sizeof(float) * b->nb * b->lat_cap, st));
+    HIP_TRY(hipMemsetAsync(b->d_hist, 0, sizeof(uint64_t) * b->nb * VH_MAX_BINS, st));
     k_n4_state_init<<<(unsigned)((b->nb + 255) / 256), 256, 0, st>>>(b->d_st, b->nb);
     VH_CHECK_LAUNCH();
-    int total_iters = 0;
-    for (int L = 0; L < prm.n_levels; ++L) total_iters += prm.max_iters[L];
-    HIP_TRY(hipMemsetAsync(b->d_nactive, 0, sizeof(int32_t) * (total_iters + 1), st));
     {
         ScopedKTimer tm(b, "n4_init", 0.0);
-        k_n4_init<<<cg, VH_TPB, 0, st>>>(b->d_hp, b->d_colbits, b->d_colrange, b->d_sc, b->R,
-                                         b->CZ, b->V, b->d_L0, b->d_B, U, b->d_st);
+        k_n4_rowcount<<<dim3((unsigned)ntiles, (unsigned)b->nb), 64, 0, st>>>(
+            b->d_colbits, b->R, b->CZ, ntiles, b->d_rowstart);
+        VH_CHECK_LAUNCH();
+        k_n4_rowscan<<<(unsigned)b->nb, VH_TPB, 0, st>>>(b->d_rowstart, ntiles * b->R);
+        VH_CHECK_LAUNCH();
+        const dim3 sg((unsigned)((ntiles + 3) / 4), (unsigned)((b->R + SEG_R - 1) / SEG_R),
+                      (unsigned)b->nb);
+        k_n4_init<<<sg, VH_TPB, 0, st>>>(b->d_hp, b->d_colbits, b->d_rowstart, b->d_sc, b->R, b->CZ,
+                                         b->V, ntiles, b->d_L0, b->d_B, U, b->d_st, 0);
         VH_CHECK_LAUNCH();
     }
-    const int LOOK = 3;
-    std::vector<hipEvent_t> evs;
-    int32_t *hflag = b->ctx->h_pinned;
-    int gi = 0;   // global iteration slot
-    for (int L = 0; L < prm.n_levels; ++L) {
-        const DevLevel lv = dev_level(b, prm, L);
-        const FitTile ftile = fit_tile(b->C, b->Z);
-        const dim3 fg((unsigned)(ftile.nty * ftile.ntz), (unsigned)b->nb);
-        const size_t fit_lds = sizeof(double) * (size_t)lv.ax[0].ncp * VH_TPB;
-        {
-            ScopedKTimer tm(b, "n4_den", 0.0);
-            k_n4_fitblock<1><<<fg, VH_TPB, fit_lds, st>>>(U, b->d_colbits, b->d_colrange, b->R,
-                                                          b->C, b->Z, b->V, bins, b->d_st, b->d_E,
-                                                          lv, b->lat_cap, b->d_fitpart);
-            VH_CHECK_LAUNCH();
-            k_n4_tilesum<1><<<(unsigned)b->nb, VH_TPB, 0, st>>>(b->d_fitpart, b->lat_cap, b->d_lat,
-                                                                b->d_den, b->d_P1, b->C, b->Z,
-                                                                b->lat_cap, b->q2_cap, b->d_st, lv);
-            VH_CHECK_LAUNCH();
-        }
-        const int level_start = (int)evs.size();
-        for (int it = 0; it < prm.max_iters[L]; ++it, ++gi) {
-            k_n4_ctrl<<<(unsigned)((b->nb + 255) / 256), 256, 0, st>>>(
-                b->d_st, b->d_part, nparts, b->d_sc, L, it, prm.conv_threshold, bins, b->nb,
-                b->d_hist, b->d_nactive + gi);
-            VH_CHECK_LAUNCH();
-            HIP_TRY(hipMemcpyAsync(hflag + (gi % 1024), b->d_nactive + gi, sizeof(int32_t),
-                                   hipMemcpyDeviceToHost, st));
-            hipEvent_t ev;
-            HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-            HIP_TRY(hipEventRecord(ev, st));
-            evs.push_back(ev);
-            k_n4_exact_min<<<(unsigned)b->nb, VH_TPB, 0, st>>>(U, b->d_mask, b->V, bins,
-                                                               b->d_st);
-            VH_CHECK_LAUNCH();
-            {
-                ScopedKTimer tm(b, "n4_hist", 0.0);
-                k_n4_hist<<<cg, VH_TPB, 0, st>>>(U, b->d_colbits, b->d_colrange, b->R, b->CZ,
-                                                 b->V, bins, b->d_st, b->d_hist);
-                VH_CHECK_LAUNCH();
-            }
-            k_n4_emap<<<(unsigned)b->nb, VH_TPB, 0, st>>>(b->d_hist, b->d_twiddle, bins, prm.fwhm,
-                                                           prm.wiener_noise, b->d_st, b->d_E);
-            VH_CHECK_LAUNCH();
-            {
-                ScopedKTimer tm(b, "n4_fit", 0.0);
-                k_n4_fitblock<0><<<fg, VH_TPB, fit_lds, st>>>(U, b->d_colbits, b->d_colrange,
-                                                              b->R, b->C, b->Z, b->V, bins,
-                                                              b->d_st, b->d_E, lv, b->lat_cap,
-                                                              b->d_fitpart);
-                VH_CHECK_LAUNCH();
-            }
-            {
-                ScopedKTimer tm(b, "n4_contract", 0.0);
-                k_n4_tilesum<0><<<(unsigned)b->nb, VH_TPB, 0, st>>>(
-                    b->d_fitpart, b->lat_cap, b->d_lat, b->d_den, b->d_P1, b->C, b->Z, b->lat_cap,
-                    b->q2_cap, b->d_st, lv);
-                VH_CHECK_LAUNCH();
-            }
-            {
-                ScopedKTimer tm(b, "n4_eval", 0.0);
-                k_n4_eval<<<cg, VH_TPB, 0, st>>>(b->d_L0, b->d_B, U, b->d_colbits,
-                                                 b->d_colrange, b->d_sc, b->R, b->C, b->Z, b->V,
-                                                 b->q2_cap, b->d_P1, lv, b->d_st, nparts,
-                                                 b->d_part);
-                VH_CHECK_LAUNCH();
-            }
-            const int k = (int)evs.size() - 1 - LOOK;
-            if (k >= level_start) {
-                HIP_TRY(hipEventSynchronize(evs[k]));
-                if (hflag[(gi - LOOK) % 1024] == 0) { ++gi; break; }
-            }
-        }
-        k_n4_level_end<<<(unsigned)((b->nb + 255) / 256), 256, 0, st>>>(b->d_st, b->d_part,
-                                                                         nparts, b->d_sc, L, b->nb);
-        VH_CHECK_LAUNCH();
-        if (L < prm.n_levels - 1) {
-            k_n4_refine<<<(unsigned)b->nb, VH_TPB, 0, st>>>(b->d_lat, b->lat_cap, b->nb,
-                                                            lv.ax[0].ncp, lv.ax[1].ncp,
-                                                            lv.ax[2].ncp);
-            VH_CHECK_LAUNCH();
-        }
+    int64_t sb = b->n4_subbatch > 0 ? b->n4_subbatch : b->nb;
+    if (const char *e = getenv("VH_N4_SUBBATCH")) {
+        const long v = atol(e);
+        if (v > 0) sb = v;
     }
+    if (sb > b->nb) sb = b->nb;
+    for (int64_t v0 = 0; v0 < b->nb; v0 += sb) n4_subbatch(b, prm, v0, std::min(sb, b->nb - v0), U);
     {
         const DevLevel lv = dev_level(b, prm, prm.n_levels - 1);
         ScopedKTimer tm(b, "n4_final", 9.0 * (double)b->V);
@@ -1044,5 +1249,4 @@ void vh_launch_n4(vh_batch *b, const vh_n4_params &prm) {
                                           b->d_P1, lv);
         VH_CHECK_LAUNCH();
     }
-    for (auto e : evs) HIP_TRY(hipEventDestroy(e));
 }

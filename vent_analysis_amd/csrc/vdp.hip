@@ -88,7 +88,7 @@ __global__ void __launch_bounds__(VH_TPB) k_mask_finish(const int32_t *colcount,
                                                        const uint8_t *sliceany, int64_t R,
                                                        int64_t C, int64_t Z, VolScalars *sc) {
     __shared__ int64_t s_part[VH_TPB];
-    __shared__ int32_t s_cmin, s_cmax, s_rowe, s_slie;
+    __shared__ int32_t s_cmin, s_cmax, s_rowe, s_slie, s_rlo, s_rhi;
     const int64_t b = blockIdx.x;
     const int64_t CZ = C * Z;
     const int t = threadIdx.x;
@@ -97,7 +97,7 @@ __global__ void __launch_bounds__(VH_TPB) k_mask_finish(const int32_t *colcount,
     int64_t acc = 0;
     for (int64_t i = s; i < e; ++i) acc += colcount[b * CZ + i];
     s_part[t] = acc;
-    if (t == 0) { s_cmin = INT_MAX; s_cmax = 0; s_rowe = 0; s_slie = 0; }
+    if (t == 0) { s_cmin = INT_MAX; s_cmax = 0; s_rowe = 0; s_slie = 0; s_rlo = INT_MAX; s_rhi = -1; }
     __syncthreads();
     if (t == 0) {
         int64_t run = 0;
@@ -111,8 +111,13 @@ __global__ void __launch_bounds__(VH_TPB) k_mask_finish(const int32_t *colcount,
             if (c > 0) atomicMin(&s_cmin, (int32_t)c);
             atomicMax(&s_cmax, (int32_t)c);
         }
-    for (int64_t r = t; r < R; r += VH_TPB)
+    for (int64_t r = t; r < R; r += VH_TPB) {
         if (!rowany[b * R + r]) s_rowe = 1;
+        else {
+            atomicMin(&s_rlo, (int32_t)r);
+            atomicMax(&s_rhi, (int32_t)r);
+        }
+    }
     for (int64_t z = t; z < Z; z += VH_TPB)
         if (!sliceany[b * Z + z]) s_slie = 1;
     __syncthreads();
@@ -122,6 +127,8 @@ __global__ void __launch_bounds__(VH_TPB) k_mask_finish(const int32_t *colcount,
         sc[b].any_row_empty = s_rowe;
         sc[b].any_slice_empty = s_slie;
         sc[b].snr_ok = s_cmin != INT_MAX;
+        sc[b].row_lo = s_rlo;
+        sc[b].row_hi = s_rhi;
     }
 }
 

@@ -51,6 +51,7 @@ struct VolScalars {
     int32_t any_row_empty, any_slice_empty;
     int32_t snr_ok;          // 0 when the reference would raise (no masked column > 0)
     int32_t ci_status;       // VH_OK / VH_ERR_MAXRADIUS
+    int32_t row_lo, row_hi;  // first / last row holding any masked voxel
     int64_t n_ci;            // defect voxels for CI
     double ci_scalar;
 };
@@ -119,7 +120,14 @@ struct vh_batch {
     // N4 workspace
     float *d_L0 = nullptr, *d_B = nullptr, *d_lat = nullptr, *d_E = nullptr;
     double *d_fitpart = nullptr;     // [nb][tiles][lattice] per-tile contracted fit slabs
+    int32_t *d_rowstart = nullptr;   // [nb][tiles][R] compact offset of each (64-column tile, row)
+    int64_t n4_tiles = 0;
+    std::vector<int> fit_pmax;       // per level: control points one fit row-wave touches
+    std::vector<int> fit_smax;       // per level: doubles of the fit's slice-contracted tile slab
+    std::vector<size_t> tile_off;    // per level: offset of the fit tile metadata in d_tabs
     double *d_P1 = nullptr, *d_num = nullptr, *d_den = nullptr;
+    float *d_T = nullptr;            // [nb][ncx][CZ] per-column lattice contraction for eval
+    int64_t t_cap = 0;
     uint64_t *d_hist = nullptr;
     N4State *d_st = nullptr;
     int32_t *d_nactive = nullptr;
@@ -135,6 +143,7 @@ struct vh_batch {
     int32_t *d_ci_shell = nullptr;   // [nb][V]
     uint32_t *d_ci_hist = nullptr;   // [nb][ci_nb]
     int64_t ci_nb_cap = 0;
+    int64_t n4_subbatch = 0;         // volumes per N4 sub-batch (0 = whole batch)
     // timing
     bool profile = false;
     std::map<std::string, KTimer> timers;
