@@ -42,6 +42,9 @@ struct DevLevel {
 
 #define TILE_W 64   // columns per compact tile (one wave)
 #define SEG_R 16    // rows per wave segment
+#define N4_CH 4096  // compact voxels per chunk (flat sweeps: 256 threads x 16)
+#define N4_VPT (N4_CH / VH_TPB)
+#define N4_FIX 68719476736.0   // 2^36: fixed-point scale of the fit's LDS row contraction
 #define LN2 0.69314718055994530942
 #define PI_D 3.14159265358979323846
 
@@ -103,7 +106,6 @@ void vh_n4_prepare_tables(vh_batch *b, const vh_n4_params &prm) {
     const int64_t dims[3] = {b->R, b->C, b->Z};
     std::vector<uint8_t> blob;
     b->tab_off.assign((size_t)prm.n_levels * 3 * 6, 0);
-    b->fit_pmax.assign((size_t)prm.n_levels, 4);
     auto push = [&](const void *p, size_t bytes) {
         size_t off = (blob.size() + 15) & ~(size_t)15;
         blob.resize(off + bytes);
@@ -130,16 +132,6 @@ void vh_n4_prepare_tables(vh_batch *b, const vh_n4_params &prm) {
             b->tab_off[(L * 3 + a) * 6 + 3] = push(inv.data(), inv.size() * 8);
             b->tab_off[(L * 3 + a) * 6 + 4] = push(w2.data(), w2.size() * 8);
             b->tab_off[(L * 3 + a) * 6 + 5] = push(w3.data(), w3.size() * 8);
-            if (a == 0) {   // widest control-point window of one fit row-wave (see fit_geo)
-                const int R = (int)dims[0], nseg = (R + 15) / 16, W = nseg < 16 ? nseg : 16;
-                const int RW = ((nseg + W - 1) / W) * 16;
-                int pm = 4;
-                for (int x0 = 0; x0 < R; x0 += RW) {
-                    const int x1 = std::min(R, x0 + RW) - 1;
-                    pm = std::max(pm, t.base[x1] - t.base[x0] + 4);
-                }
-                b->fit_pmax[L] = pm;
-            }
         }
     }
     // fit tile metadata per level (64-column tiles of the (col, slice) plane)
@@ -210,10 +202,18 @@ void vh_ensure_n4_workspace(vh_batch *b, const vh_n4_params &prm) {
     const int64_t cx = level_ncp(prm, L, 0), cy = level_ncp(prm, L, 1), cz = level_ncp(prm, L, 2);
     const int64_t lat = cx * cy * cz;
     const int64_t q2 = cx * cy * b->Z;
+    if (b->V >= (int64_t)1 << 29) throw VhError{VH_ERR_ARG, "N4: volume too large (>= 2^29 voxels)"};
     if (b->d_L0 == nullptr) {
-        HIP_TRY(hipMalloc(&b->d_L0, sizeof(float) * b->nb * b->V));
-        HIP_TRY(hipMalloc(&b->d_B, sizeof(float) * b->nb * b->V));
-        HIP_TRY(hipMalloc(&b->d_hist, sizeof(uint64_t) * b->nb * VH_MAX_BINS));
+        b->VS = (b->V + 63) & ~(int64_t)63;   // compact-array stride: 256-byte aligned volumes
+        const int64_t nch = b->nb * ((b->VS + N4_CH - 1) / N4_CH);
+        HIP_TRY(hipMalloc(&b->d_L0, sizeof(float) * b->nb * b->VS));
+        HIP_TRY(hipMalloc(&b->d_B, sizeof(float) * b->nb * b->VS));
+        HIP_TRY(hipMalloc(&b->d_U, sizeof(float) * b->nb * b->VS));
+        HIP_TRY(hipMalloc(&b->d_ridx, sizeof(int32_t) * b->nb * b->VS));
+        HIP_TRY(hipMalloc(&b->d_cp, sizeof(int32_t) * (b->nb + 1)));
+        HIP_TRY(hipMalloc(&b->d_cvol, sizeof(int32_t) * nch));
+        HIP_TRY(hipMalloc(&b->d_hpart, sizeof(uint64_t) * nch * VH_MAX_BINS));
+        HIP_TRY(hipMalloc(&b->d_cpart, sizeof(double) * 2 * nch));
         HIP_TRY(hipMalloc(&b->d_E, sizeof(float) * b->nb * VH_MAX_BINS));
         HIP_TRY(hipMalloc(&b->d_st, sizeof(N4State) * b->nb));
         HIP_TRY(hipMalloc(&b->d_nactive, sizeof(int32_t) * 8 * 1024));
@@ -276,15 +276,15 @@ __device__ __forceinline__ T block_sum_fixed(T v, T *s_red) {
     return r;
 }
 
-// Convergence measure from the eval partials, reduced by one wave in a fixed order (lane l sums
-// slots l, l+64, ...; then a shuffle tree): deterministic.  Returns the value in every lane.
-__device__ __forceinline__ double conv_from_parts(const double *part, int64_t nparts, int64_t b,
+// Convergence measure from the eval partials (one slot per chunk of the volume), reduced by one
+// wave in a fixed order (lane l sums slots l, l+64, ...; then a shuffle tree): deterministic.
+__device__ __forceinline__ double conv_from_parts(const double *part, const int32_t *cp, int64_t b,
                                                   double N) {
     const int lane = threadIdx.x & 63;
     double sd = 0.0, sd2 = 0.0;
-    for (int64_t p = lane; p < nparts; p += 64) {
-        sd += part[(b * nparts + p) * 2];
-        sd2 += part[(b * nparts + p) * 2 + 1];
+    for (int64_t p = cp[b] + lane; p < cp[b + 1]; p += 64) {
+        sd += part[p * 2];
+        sd2 += part[p * 2 + 1];
     }
     for (int off = 32; off > 0; off >>= 1) {
         sd += __shfl_down(sd, off, 64);
@@ -409,21 +409,22 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
     return v;
 }
 
-// L0 = log(I) at mask == 1 (non-positive -> 0), B = 0, U = L0 (compact) and the first U range.
-// grid (ceil(tiles/4), segments, volumes), 4 waves = 4 tiles per block.
+// L0 = log(I) at mask == 1 (non-positive -> 0), B = 0, U = L0, ridx = raster index (compact, volume
+// stride VS) and the first U range.  grid (ceil(tiles/4), segments, volumes), 4 tile-waves/block.
 __global__ void __launch_bounds__(VH_TPB) k_n4_init(const float *__restrict__ I,
                                                    const uint32_t *__restrict__ colbits,
                                                    const int32_t *rs, const VolScalars *sc,
-                                                   int64_t R, int64_t CZ, int64_t V, int64_t ntiles,
-                                                   float *L0, float *B, float *U, N4State *st,
-                                                   int64_t vol0) {
-    const int64_t b = vol0 + blockIdx.z;
+                                                   int64_t R, int64_t CZ, int64_t V, int64_t VS,
+                                                   int64_t ntiles, float *L0, float *B, float *U,
+                                                   int32_t *ridx, N4State *st) {
+    const int64_t b = blockIdx.z;
     const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (tile >= ntiles) return;
     Seg s;
     seg_begin(s, colbits, rs, b, R, CZ, ntiles, tile, blockIdx.y * SEG_R);
-    const __amdgpu_buffer_rsrc_t rL = vol_rsrc(L0 + b * V, V), rB = vol_rsrc(B + b * V, V),
-                                 rU = vol_rsrc(U + b * V, V);
+    const __amdgpu_buffer_rsrc_t rL = vol_rsrc(L0 + b * VS, VS), rB = vol_rsrc(B + b * VS, VS),
+                                 rU = vol_rsrc(U + b * VS, VS),
+                                 rR = vol_rsrc((const float *)(ridx + b * VS), VS);
     const int64_t first = sc[b].first_masked;
     uint32_t kmax = 0u, kmin = 0xffffffffu;
 #pragma unroll
@@ -435,6 +436,7 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_init(const float *__restrict__ I,
         bstore(rL, s.off[k], l);
         bstore(rB, s.off[k], 0.0f);
         bstore(rU, s.off[k], l);
+        bstore(rR, s.off[k], __int_as_float((int)r));
         const uint32_t key = f2key(l);
         kmax = key > kmax ? key : kmax;
         if (r == first) st[b].u_first = l;
@@ -448,9 +450,26 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_init(const float *__restrict__ I,
     }
 }
 
+// Chunk table: volume b's compact voxels split into chunks of N4_CH; cp = exclusive prefix of the
+// chunk counts, cvol[c] = owning volume.  One block.
+__global__ void __launch_bounds__(VH_TPB) k_n4_chunks(const VolScalars *sc, int64_t nb,
+                                                     int32_t *cp, int32_t *cvol) {
+    if (threadIdx.x == 0) {
+        int32_t run = 0;
+        for (int64_t b = 0; b < nb; ++b) {
+            cp[b] = run;
+            run += (int32_t)((sc[b].n_mask1 + N4_CH - 1) / N4_CH);
+        }
+        cp[nb] = run;
+    }
+    __syncthreads();
+    for (int64_t b = threadIdx.x; b < nb; b += VH_TPB)
+        for (int32_t c = cp[b]; c < cp[b + 1]; ++c) cvol[c] = (int32_t)b;
+}
+
 // Iteration control: convergence of the previous iteration, the while-condition of ITK's loop,
 // bin range (common case of the else-if quirk), histogram reset.
-__global__ void __launch_bounds__(64) k_n4_ctrl(N4State *st, const double *part, int64_t nparts,
+__global__ void __launch_bounds__(64) k_n4_ctrl(N4State *st, const double *part, const int32_t *cp,
                                                const VolScalars *sc, int level, int it,
                                                float thresh, int bins, int64_t vol0,
                                                int32_t *nactive) {
@@ -458,7 +477,7 @@ __global__ void __launch_bounds__(64) k_n4_ctrl(N4State *st, const double *part,
     N4State &s = st[b];
     const bool was_active = s.active;
     double conv = 0.0;
-    if (it > 0 && was_active) conv = conv_from_parts(part, nparts, b, (double)sc[b].n_mask1);
+    if (it > 0 && was_active) conv = conv_from_parts(part, cp, b, (double)sc[b].n_mask1);
     if (threadIdx.x != 0) return;
     if (it == 0) {
         s.active = 1;
@@ -490,12 +509,12 @@ __global__ void __launch_bounds__(64) k_n4_ctrl(N4State *st, const double *part,
 }
 
 __global__ void __launch_bounds__(64) k_n4_level_end(N4State *st, const double *part,
-                                                    int64_t nparts, const VolScalars *sc,
+                                                    const int32_t *cp, const VolScalars *sc,
                                                     int level, int64_t vol0) {
     const int64_t b = vol0 + blockIdx.x;
     N4State &s = st[b];
     if (!s.active) return;
-    const double conv = conv_from_parts(part, nparts, b, (double)sc[b].n_mask1);
+    const double conv = conv_from_parts(part, cp, b, (double)sc[b].n_mask1);
     if (threadIdx.x != 0) return;
     s.conv = conv;
     s.iters_level[level] = s.iters;
@@ -524,7 +543,7 @@ __device__ __forceinline__ void exact_row_scan(const float *Uv, const uint32_t *
 __global__ void __launch_bounds__(VH_TPB) k_n4_exact_min(const float *__restrict__ U,
                                                         const uint32_t *__restrict__ colbits,
                                                         const int32_t *rs, int64_t R, int64_t CZ,
-                                                        int64_t V, int64_t ntiles, int bins,
+                                                        int64_t VS, int64_t ntiles, int bins,
                                                         N4State *st, int64_t vol0) {
     __shared__ float s_cmax[VH_TPB];
     __shared__ float s_min[VH_TPB];
@@ -533,7 +552,7 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_exact_min(const float *__restrict
     const int t = threadIdx.x;
     const int64_t per = (R + VH_TPB - 1) / VH_TPB;
     const int64_t s0 = t * per < R ? t * per : R, e0 = s0 + per < R ? s0 + per : R;
-    const float *Uv = U + b * V;
+    const float *Uv = U + b * VS;
     float cmax = -FLT_MAX, dummy = FLT_MAX;
     for (int64_t x = s0; x < e0; ++x) exact_row_scan(Uv, colbits, rs, b, R, CZ, ntiles, x, cmax, dummy, false);
     s_cmax[t] = cmax;
@@ -556,66 +575,70 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_exact_min(const float *__restrict
 }
 
 // Triangular Parzen histogram of U at mask == 1, unsigned 64-bit fixed point (2^-32 units).
-// Per lane a run (bin, two weights) over its 16 rows, per block an LDS histogram, then one global
-// 64-bit atomic per touched bin (integer adds: deterministic).
-__global__ void __launch_bounds__(VH_TPB) k_n4_hist(const float *__restrict__ U,
-                                                   const uint32_t *__restrict__ colbits,
-                                                   const int32_t *rs, int64_t R, int64_t CZ,
-                                                   int64_t V, int64_t ntiles, int bins,
-                                                   const N4State *st, uint64_t *hist,
-                                                   int64_t vol0) {
+// One block per chunk of N4_CH compact voxels; a thread takes 16 consecutive voxels (neighbours in
+// a row, so a run (bin, two weights) usually covers several), LDS histogram, then the block writes
+// its partial histogram; k_n4_emap adds a volume's partials in chunk order (deterministic).
+__global__ void __launch_bounds__(VH_TPB) k_n4_hist(const float *__restrict__ U, const int32_t *cp,
+                                                   const int32_t *cvol, const VolScalars *sc,
+                                                   int64_t VS, int bins, const N4State *st,
+                                                   uint64_t *hpart, int32_t c0) {
     __shared__ unsigned long long H[VH_MAX_BINS];
-    const int64_t b = vol0 + blockIdx.z;
+    const int32_t c = c0 + blockIdx.x;
+    const int64_t b = cvol[c];
     if (!st[b].active) return;
     for (int i = threadIdx.x; i < VH_MAX_BINS; i += VH_TPB) H[i] = 0ull;
-    __syncthreads();
-    const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (tile < ntiles) {
-        Seg s;
-        seg_begin(s, colbits, rs, b, R, CZ, ntiles, tile, blockIdx.y * SEG_R);
-        const __amdgpu_buffer_rsrc_t rU = vol_rsrc(U + b * V, V);
-        float u[SEG_R];
+    const int64_t j0 = (int64_t)(c - cp[b]) * N4_CH;
+    const int64_t n = sc[b].n_mask1 - j0 < N4_CH ? sc[b].n_mask1 - j0 : N4_CH;
+    const int t0 = threadIdx.x * N4_VPT;
+    const float *src = U + b * VS + j0 + t0;
+    float u[N4_VPT];
+    if (t0 + N4_VPT <= n) {
 #pragma unroll
-        for (int k = 0; k < SEG_R; ++k) u[k] = bload(rU, s.off[k]);
-        const float bmin = st[b].bin_min, slope = st[b].slope;
-        int cur = -1;
-        unsigned long long w0 = 0ull, w1 = 0ull;
+        for (int q = 0; q < N4_VPT / 4; ++q) {
+            const float4 v = reinterpret_cast<const float4 *>(src)[q];
+            u[4 * q] = v.x; u[4 * q + 1] = v.y; u[4 * q + 2] = v.z; u[4 * q + 3] = v.w;
+        }
+    } else {
 #pragma unroll
-        for (int k = 0; k < SEG_R; ++k) {
-            if (!((s.m >> k) & 1u)) continue;
-            const float cidx = (u[k] - bmin) / slope;
-            if (!(cidx >= 0.0f) || !(cidx < (float)bins)) continue;
-            const int idx = (int)floorf(cidx);
-            const float o = cidx - (float)idx;
-            unsigned long long a0, a1 = 0ull;
-            if (o == 0.0f) {
-                a0 = 1ull << 32;
-            } else if (idx < bins - 1) {
-                a0 = (unsigned long long)((double)(1.0f - o) * 4294967296.0);
-                a1 = (unsigned long long)((double)o * 4294967296.0);
-            } else {
-                continue;
-            }
-            if (idx != cur) {
-                if (cur >= 0) {
-                    if (w0) atomicAdd(&H[cur], w0);
-                    if (w1) atomicAdd(&H[cur + 1], w1);
-                }
-                cur = idx;
-                w0 = 0ull;
-                w1 = 0ull;
-            }
-            w0 += a0;
-            w1 += a1;
-        }
-        if (cur >= 0) {
-            if (w0) atomicAdd(&H[cur], w0);
-            if (w1) atomicAdd(&H[cur + 1], w1);
-        }
+        for (int k = 0; k < N4_VPT; ++k) u[k] = t0 + k < n ? src[k] : __int_as_float(0x7fc00000);
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < bins; i += VH_TPB)
-        if (H[i]) atomicAdd((unsigned long long *)&hist[b * VH_MAX_BINS + i], H[i]);
+    const float bmin = st[b].bin_min, slope = st[b].slope;
+    int cur = -1;
+    unsigned long long w0 = 0ull, w1 = 0ull;
+#pragma unroll
+    for (int k = 0; k < N4_VPT; ++k) {
+        const float cidx = (u[k] - bmin) / slope;   // NaN (padding) fails both range tests
+        if (!(cidx >= 0.0f) || !(cidx < (float)bins)) continue;
+        const int idx = (int)floorf(cidx);
+        const float o = cidx - (float)idx;
+        unsigned long long a0, a1 = 0ull;
+        if (o == 0.0f) {
+            a0 = 1ull << 32;
+        } else if (idx < bins - 1) {
+            a0 = (unsigned long long)((double)(1.0f - o) * 4294967296.0);
+            a1 = (unsigned long long)((double)o * 4294967296.0);
+        } else {
+            continue;
+        }
+        if (idx != cur) {
+            if (cur >= 0) {
+                if (w0) atomicAdd(&H[cur], w0);
+                if (w1) atomicAdd(&H[cur + 1], w1);
+            }
+            cur = idx;
+            w0 = 0ull;
+            w1 = 0ull;
+        }
+        w0 += a0;
+        w1 += a1;
+    }
+    if (cur >= 0) {
+        if (w0) atomicAdd(&H[cur], w0);
+        if (w1) atomicAdd(&H[cur + 1], w1);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < bins; i += VH_TPB) hpart[(int64_t)c * VH_MAX_BINS + i] = H[i];
 }
 
 // 512-point radix-2 FFT in LDS, 256 threads (one butterfly each per stage); same butterfly and
@@ -648,10 +671,10 @@ __device__ void lds_fft(double2 *x, double2 *tmp, const double2 *tw, bool invers
 __device__ __forceinline__ float expf_cr(float x) { return (float)exp((double)x); }
 
 // E(u|v) map (Wiener deconvolution of the histogram by the bias Gaussian), one block per volume.
-__global__ void __launch_bounds__(VH_TPB) k_n4_emap(const uint64_t *hist, const double2 *tw,
-                                                   int bins, float fwhm, float noise,
-                                                   const N4State *st, float *Eout, int64_t vol0,
-                                                   uint64_t *hist_rw) {
+__global__ void __launch_bounds__(VH_TPB) k_n4_emap(const uint64_t *hpart, const int32_t *cp,
+                                                   const double2 *tw, int bins, float fwhm,
+                                                   float noise, const N4State *st, float *Eout,
+                                                   int64_t vol0) {
     __shared__ double2 V[VH_FFT_P], F[VH_FFT_P], U[VH_FFT_P], NUM[VH_FFT_P], DEN[VH_FFT_P],
         TMP[VH_FFT_P];
     const int64_t b = vol0 + blockIdx.x;
@@ -661,8 +684,10 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_emap(const uint64_t *hist, const 
     const float binMin = st[b].bin_min, slope = st[b].slope;
     for (int n = t; n < P; n += VH_TPB) {
         const int h = n - off;
-        V[n] = make_double2(h >= 0 && h < bins ? (double)hist[b * VH_MAX_BINS + h] * (1.0 / 4294967296.0) : 0.0, 0.0);
-        if (h >= 0 && h < bins) hist_rw[b * VH_MAX_BINS + h] = 0ull;   // ready for the next iteration
+        uint64_t hs = 0ull;   // chunk partials in chunk order (integer: exact)
+        if (h >= 0 && h < bins)
+            for (int32_t c = cp[b]; c < cp[b + 1]; ++c) hs += hpart[(int64_t)c * VH_MAX_BINS + h];
+        V[n] = make_double2((double)hs * (1.0 / 4294967296.0), 0.0);
         F[n] = make_double2(0.0, 0.0);
     }
     __syncthreads();
@@ -718,122 +743,100 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_emap(const uint64_t *hist, const 
 }
 
 // ---------------------------------------------------------------------------------------------
-// Fit with in-block contraction.  Block = one 64-column tile x W row-waves (wave w owns rows
-// [w RW, (w+1) RW)); every lane runs the sliding 4-wide window of the row contraction over its
-// wave's rows, the per-wave partials are summed per column in wave order (deterministic), then
-// the block contracts its 64 columns over cols and slices:
+// Fit with in-block contraction.  Block = one 64-column tile of one volume: its compact voxels are
+// contiguous (tile-row order), a thread takes every 256th.  Row contraction into LDS
+//   Q1[i][l] = sum_x wx(x,i)^p q(x, l)          (l = column within the tile)
+// with 64-bit fixed-point LDS atomics (2^-36 units: integer adds, so the order does not matter
+// and the result is deterministic), then the block contracts its 64 columns over slices and cols
 //   Pn[i][j][k] = sum_{(y,z) in tile} wy(y,j)^p wz(z,k)^p Q1[i][y][z],  p = 3 (num) / 2 (den)
-// Only that small slab goes to HBM; k_n4_tilesum adds a volume's slabs in tile order.
+// q = r / (sum wx^2 sum wy^2 sum wz^2) for the numerator, 1 for the denominator.  Only the small
+// slab goes to HBM; k_n4_tilesum adds a volume's slabs in tile order.
 // ---------------------------------------------------------------------------------------------
-// fit block geometry shared by host and device
-struct FitGeo {
-    int W;      // waves per block
-    int RW;     // rows per wave (multiple of SEG_R)
-    int PMAX;   // partial control points per wave
-};
+__device__ __forceinline__ int row_of(int r, int64_t CZ, double inv_cz) {
+    int x = (int)((double)r * inv_cz);
+    if ((int64_t)x * CZ > r) --x;
+    else if ((int64_t)(x + 1) * CZ <= r) ++x;
+    return x;
+}
 
 template <int MODE>
-__global__ void k_n4_fit(const float *__restrict__ U, const uint32_t *__restrict__ colbits,
-                         const int32_t *rs, int64_t R, int64_t C, int64_t Z, int64_t V,
-                         int64_t ntiles, int bins, const N4State *st, const float *E, DevLevel lv,
-                         FitGeo g, int64_t slab, double *part, int64_t vol0) {
+__global__ void __launch_bounds__(VH_TPB) k_n4_fit(const float *__restrict__ U,
+                                                  const int32_t *__restrict__ ridx,
+                                                  const int32_t *rs, const VolScalars *sc,
+                                                  int64_t R, int64_t C, int64_t Z, int64_t VS,
+                                                  int64_t ntiles, int bins, const N4State *st,
+                                                  const float *E, DevLevel lv, double inv_cz,
+                                                  int64_t slab, double *part, int64_t vol0) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     __shared__ float sE[VH_MAX_BINS];
+    __shared__ double sIyz[TILE_W];
     const int64_t b = vol0 + blockIdx.y;
     if (MODE == 0 && !st[b].active) return;
     const int tile = blockIdx.x;
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const DevAxis ax = lv.ax[0], ay = lv.ax[1], az = lv.ax[2];
     const int ncx = ax.ncp;
     const int64_t CZ = C * Z;
-    double *sQ1 = smem;                         // [ncx][64]
-    double *sP = smem + (size_t)ncx * TILE_W;   // [W][PMAX][64]
-    if (MODE == 0)
-        for (int i = threadIdx.x; i < bins; i += blockDim.x) sE[i] = E[b * VH_MAX_BINS + i];
-    for (int i = threadIdx.x; i < g.W * g.PMAX * TILE_W; i += blockDim.x) sP[i] = 0.0;
+    const int64_t c0 = (int64_t)tile * TILE_W;
+    const int4 m0 = lv.tiles[2 * tile], m1 = lv.tiles[2 * tile + 1];
+    const int jlo = m1.x, JT = m1.y, klo = m1.z, KT = m1.w;
+    double *out = part + (b * ntiles + tile) * slab;
+    const int32_t *rt = rs + (b * ntiles + tile) * R;
+    const int64_t ts = rt[0];
+    const int64_t te = tile + 1 < ntiles ? rt[R] : sc[b].n_mask1;
+    if (ts >= te) {   // no masked voxel in this tile
+        for (int e = threadIdx.x; e < ncx * JT * KT; e += VH_TPB) out[e] = 0.0;
+        return;
+    }
+    unsigned long long *sQi = reinterpret_cast<unsigned long long *>(smem);   // [ncx][64]
+    for (int e = threadIdx.x; e < ncx * TILE_W; e += VH_TPB) sQi[e] = 0ull;
+    if (MODE == 0) {
+        for (int i = threadIdx.x; i < bins; i += VH_TPB) sE[i] = E[b * VH_MAX_BINS + i];
+        if (threadIdx.x < TILE_W && c0 + threadIdx.x < CZ) {
+            const int64_t col = c0 + threadIdx.x;
+            sIyz[threadIdx.x] = ay.isw2[col / Z] * az.isw2[col % Z];
+        }
+    }
     __syncthreads();
-    // ---- row contraction of this wave's rows ----
-    const int64_t col = (int64_t)tile * TILE_W + lane;
-    const bool mine = col < CZ;
-    double isyz = 1.0;
-    if (mine) isyz = ay.isw2[col / Z] * az.isw2[col % Z];
+    // ---- row contraction: every masked voxel of the tile ----
     float bmin = 0.0f, slope = 1.0f;
     if (MODE == 0) {
         bmin = st[b].bin_min;
         slope = st[b].slope;
     }
-    const int xw0 = w * g.RW;
-    const int xw1 = (xw0 + g.RW < R ? xw0 + g.RW : (int)R);
-    if (xw0 < xw1) {
-        const int ib0 = ax.base[xw0];
-        int wb = ib0;
-        double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-        double *P = sP + (size_t)w * g.PMAX * TILE_W + lane;
-        const __amdgpu_buffer_rsrc_t rU = vol_rsrc(U + b * V, V);
-        for (int x0 = xw0; x0 < xw1; x0 += SEG_R) {
-            Seg s;
-            seg_begin(s, colbits, rs, b, R, CZ, ntiles, tile, x0);
-            float u[SEG_R];
-            if (MODE == 0) {
+    const float *Ub = U + b * VS;
+    const int32_t *Rb = ridx + b * VS;
+    for (int64_t j = ts + threadIdx.x; j < te; j += VH_TPB) {
+        const int r = Rb[j];
+        const int x = row_of(r, CZ, inv_cz);
+        const int l = (int)((int64_t)r - (int64_t)x * CZ - c0);
+        const int bx = ax.base[x];
+        const double *wp = (MODE == 0 ? ax.w3 : ax.w2) + 4 * x;
+        if (MODE == 0) {
+            const float u = Ub[j];
+            const float rr = u - sharpen_value(u, bmin, slope, sE, bins);
+            const double q = ((double)rr * ax.isw2[x]) * sIyz[l];
 #pragma unroll
-                for (int k = 0; k < SEG_R; ++k) u[k] = bload(rU, s.off[k]);
-            }
+            for (int c = 0; c < 4; ++c)
+                atomicAdd(&sQi[(bx + c) * TILE_W + l],
+                          (unsigned long long)__double2ll_rn(wp[c] * q * N4_FIX));
+        } else {
 #pragma unroll
-            for (int k = 0; k < SEG_R; ++k) {
-                const int x = x0 + k;
-                if (x >= xw1) break;
-                const int bx = ax.base[x];
-                while (wb < bx) {
-                    P[(wb - ib0) * TILE_W] = a0;
-                    a0 = a1; a1 = a2; a2 = a3; a3 = 0.0;
-                    ++wb;
-                }
-                if (!((s.m >> k) & 1u)) continue;
-                const double *wp = (MODE == 0 ? ax.w3 : ax.w2) + 4 * x;   // wave-uniform row
-                if (MODE == 0) {
-                    const float r = u[k] - sharpen_value(u[k], bmin, slope, sE, bins);
-                    const double q = ((double)r * ax.isw2[x]) * isyz;
-                    a0 = fma(wp[0], q, a0);
-                    a1 = fma(wp[1], q, a1);
-                    a2 = fma(wp[2], q, a2);
-                    a3 = fma(wp[3], q, a3);
-                } else {
-                    a0 += wp[0];
-                    a1 += wp[1];
-                    a2 += wp[2];
-                    a3 += wp[3];
-                }
-            }
+            for (int c = 0; c < 4; ++c)
+                atomicAdd(&sQi[(bx + c) * TILE_W + l],
+                          (unsigned long long)__double2ll_rn(wp[c] * N4_FIX));
         }
-        P[(wb - ib0) * TILE_W] = a0;
-        if (wb + 1 < ncx) P[(wb + 1 - ib0) * TILE_W] = a1;
-        if (wb + 2 < ncx) P[(wb + 2 - ib0) * TILE_W] = a2;
-        if (wb + 3 < ncx) P[(wb + 3 - ib0) * TILE_W] = a3;
     }
     __syncthreads();
-    // ---- per column: sum the wave partials in wave order ----
-    for (int e = threadIdx.x; e < ncx * TILE_W; e += blockDim.x) {
-        const int i = e / TILE_W, l = e % TILE_W;
-        double acc = 0.0;
-        for (int ww = 0; ww < g.W; ++ww) {
-            const int r0 = ww * g.RW;
-            if (r0 >= R) break;
-            const int ib = ax.base[r0];
-            const int o = i - ib;
-            if (o >= 0 && o < g.PMAX) acc += sP[((size_t)ww * g.PMAX + o) * TILE_W + l];
-        }
-        sQ1[e] = acc;
-    }
+    double *sQ1 = smem;   // in place: each slot converted by the thread that reads it
+    for (int e = threadIdx.x; e < ncx * TILE_W; e += VH_TPB)
+        sQ1[e] = (double)(long long)sQi[e] * (1.0 / N4_FIX);
     __syncthreads();
     // ---- contract the tile's columns: over slices per tile row (stage 1), then over cols ----
-    const int4 m0 = lv.tiles[2 * tile], m1 = lv.tiles[2 * tile + 1];
     const int y0 = m0.x, y1 = m0.y, ny = y1 - y0 + 1;
-    const int jlo = m1.x, JT = m1.y, klo = m1.z, KT = m1.w;
-    const int64_t c0 = (int64_t)tile * TILE_W;
     const double *wzp = MODE == 0 ? az.w3 : az.w2;
     const double *wyp = MODE == 0 ? ay.w3 : ay.w2;
-    double *sS = sP;   // [ncx][ny][KT], reuses the wave-partial space
-    for (int e = threadIdx.x; e < ncx * ny * KT; e += blockDim.x) {
+    double *sS = smem + (size_t)ncx * TILE_W;   // [ncx][ny][KT]
+    for (int e = threadIdx.x; e < ncx * ny * KT; e += VH_TPB) {
         const int i = e / (ny * KT), yy = (e / KT) % ny, k = klo + e % KT;
         const int y = y0 + yy;
         const int zs = y == y0 ? m0.z : 0, ze = y == y1 ? m0.w : (int)Z - 1;
@@ -847,8 +850,7 @@ __global__ void k_n4_fit(const float *__restrict__ U, const uint32_t *__restrict
         sS[e] = acc;
     }
     __syncthreads();
-    double *out = part + (b * ntiles + tile) * slab;
-    for (int e = threadIdx.x; e < ncx * JT * KT; e += blockDim.x) {
+    for (int e = threadIdx.x; e < ncx * JT * KT; e += VH_TPB) {
         const int i = e / (JT * KT), j = jlo + (e / KT) % JT, kk = e % KT;
         double acc = 0.0;
         for (int y = y0; y <= y1; ++y) {
@@ -934,65 +936,65 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_T(const double *P1, int64_t q2_ca
 }
 
 // Evaluate the new field at masked voxels: B_new, U = L0 - B_new (compact, in place), the
-// convergence partial sums of exp(B_old - B_new) - 1 (one slot per wave, written without a block
-// barrier) and the U range for the next iteration.
+// convergence partial sums of exp(B_old - B_new) - 1 (one slot per chunk, fixed-order block
+// reduction) and the U range for the next iteration.  One block per chunk, lane-consecutive voxels
+// (coalesced), 8 voxels' loads in flight per thread.
+#define EV_G 8
 __global__ void __launch_bounds__(VH_TPB) k_n4_eval(const float *__restrict__ L0, float *B,
-                                                   float *U, const uint32_t *__restrict__ colbits,
-                                                   const int32_t *rs, const VolScalars *sc,
-                                                   int64_t R, int64_t CZ, int64_t V,
-                                                   int64_t ntiles, const float *T, int64_t tcap,
-                                                   DevLevel lv, N4State *st, int64_t nparts,
-                                                   double *part, int64_t vol0) {
-    const int64_t b = vol0 + blockIdx.z;
+                                                   float *U, const int32_t *__restrict__ ridx,
+                                                   const int32_t *cp, const int32_t *cvol,
+                                                   const VolScalars *sc, int64_t CZ, int64_t VS,
+                                                   double inv_cz, const float *T, int64_t tcap,
+                                                   DevLevel lv, N4State *st, double *part,
+                                                   int32_t c0) {
+    __shared__ double s_sd[VH_TPB / 64], s_sd2[VH_TPB / 64];
+    __shared__ uint32_t s_max[VH_TPB / 64], s_min[VH_TPB / 64];
+    const int32_t c = c0 + blockIdx.x;
+    const int64_t b = cvol[c];
     if (!st[b].active) return;
-    const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (tile >= ntiles) return;
-    const int lane = threadIdx.x & 63;
-    const int64_t slot = (int64_t)blockIdx.y * ntiles + tile;
-    Seg s;
-    seg_begin(s, colbits, rs, b, R, CZ, ntiles, tile, blockIdx.y * SEG_R);
+    const int64_t j0 = (int64_t)(c - cp[b]) * N4_CH;
+    const int n = (int)(sc[b].n_mask1 - j0 < N4_CH ? sc[b].n_mask1 - j0 : N4_CH);
+    const int64_t first = sc[b].first_masked;
+    const float *Lb = L0 + b * VS + j0;
+    float *Bb = B + b * VS + j0;
+    float *Ub = U + b * VS + j0;
+    const int32_t *Rb = ridx + b * VS + j0;
+    const float *Tb = T + b * tcap;
+    const DevAxis ax = lv.ax[0];
     double sd = 0.0, sd2 = 0.0;
     uint32_t kmax = 0u, kmin = 0xffffffffu;
-    if (__ballot(s.m != 0u)) {
-        const __amdgpu_buffer_rsrc_t rL = vol_rsrc(L0 + b * V, V), rB = vol_rsrc(B + b * V, V),
-                                     rU = vol_rsrc(U + b * V, V);
-        float la[SEG_R], ba[SEG_R];
+    for (int g = 0; g < N4_VPT; g += EV_G) {
+        int rr[EV_G];
+        float la[EV_G], ba[EV_G];
 #pragma unroll
-        for (int k = 0; k < SEG_R; ++k) {
-            la[k] = bload(rL, s.off[k]);
-            ba[k] = bload(rB, s.off[k]);
+        for (int k = 0; k < EV_G; ++k) {
+            const int j = threadIdx.x + (g + k) * VH_TPB;
+            const bool ok = j < n;
+            rr[k] = ok ? Rb[j] : -1;
+            la[k] = ok ? Lb[j] : 0.0f;
+            ba[k] = ok ? Bb[j] : 0.0f;
         }
-        const DevAxis ax = lv.ax[0];
-        const float *Tb = T + b * tcap + (s.col < CZ ? s.col : 0);
-        int wb = ax.base[s.x0 < R ? s.x0 : (int)R - 1];
-        float t0 = 0.f, t1 = 0.f, t2 = 0.f, t3 = 0.f;
-        if (s.m) {
-            t0 = Tb[(int64_t)wb * CZ]; t1 = Tb[(int64_t)(wb + 1) * CZ];
-            t2 = Tb[(int64_t)(wb + 2) * CZ]; t3 = Tb[(int64_t)(wb + 3) * CZ];
-        }
-        const int64_t first = sc[b].first_masked;
 #pragma unroll
-        for (int k = 0; k < SEG_R; ++k) {
-            const int x = s.x0 + k;
-            if (x >= R) break;
+        for (int k = 0; k < EV_G; ++k) {
+            if (rr[k] < 0) continue;
+            const int j = threadIdx.x + (g + k) * VH_TPB;
+            const int r = rr[k];
+            const int x = row_of(r, CZ, inv_cz);
+            const int64_t col = (int64_t)r - (int64_t)x * CZ;
             const int bx = ax.base[x];
-            while (wb < bx) {
-                ++wb;
-                t0 = t1; t1 = t2; t2 = t3;
-                t3 = s.m ? Tb[(int64_t)(wb + 3) * CZ] : 0.f;
-            }
-            if (!((s.m >> k) & 1u)) continue;
             const float4 w = *reinterpret_cast<const float4 *>(ax.w + 4 * x);
+            const float *tp = Tb + (int64_t)bx * CZ + col;
+            const float t0 = tp[0], t1 = tp[CZ], t2 = tp[2 * CZ], t3 = tp[3 * CZ];
             const float bn = ((w.x * t0 + w.y * t1) + w.z * t2) + w.w * t3;
             const float u = la[k] - bn;
-            bstore(rB, s.off[k], bn);
-            bstore(rU, s.off[k], u);
+            Bb[j] = bn;
+            Ub[j] = u;
             const double d = (double)expm1f(ba[k] - bn);   // p - 1, p = exp(B_old - B_new)
             sd += d;
             sd2 = fma(d, d, sd2);
             const uint32_t key = f2key(u);
             kmax = key > kmax ? key : kmax;
-            if ((int64_t)x * CZ + s.col == first) st[b].u_first = u;
+            if ((int64_t)r == first) st[b].u_first = u;
             else kmin = key < kmin ? key : kmin;
         }
     }
@@ -1002,13 +1004,30 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_eval(const float *__restrict__ L0
     }
     kmax = wave_max_u32(kmax);
     kmin = wave_min_u32(kmin);
-    if (lane == 0) {
-        part[(b * nparts + slot) * 2] = sd;
-        part[(b * nparts + slot) * 2 + 1] = sd2;
-        if (kmax) atomicMax(&st[b].umax_key, kmax);
-        if (kmin != 0xffffffffu) atomicMin(&st[b].umin_key, kmin);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        s_sd[w] = sd;
+        s_sd2[w] = sd2;
+        s_max[w] = kmax;
+        s_min[w] = kmin;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double a = 0.0, a2 = 0.0;
+        uint32_t mx = 0u, mn = 0xffffffffu;
+        for (int i = 0; i < VH_TPB / 64; ++i) {
+            a += s_sd[i];
+            a2 += s_sd2[i];
+            mx = s_max[i] > mx ? s_max[i] : mx;
+            mn = s_min[i] < mn ? s_min[i] : mn;
+        }
+        part[(int64_t)c * 2] = a;
+        part[(int64_t)c * 2 + 1] = a2;
+        if (mx) atomicMax(&st[b].umax_key, mx);
+        if (mn != 0xffffffffu) atomicMin(&st[b].umin_key, mn);
     }
 }
+
 // Exact cubic B-spline subdivision (spans doubled on every axis), axis by axis, one block/volume.
 __device__ void refine_axis_dev(const float *in, float *out, int d0, int d1, int d2, int axis) {
     int od[3] = {d0, d1, d2};
@@ -1077,60 +1096,41 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_final(const float *__restrict__ I
 // ---------------------------------------------------------------------------------------------
 // host driver
 // ---------------------------------------------------------------------------------------------
-// Fit block geometry: W row-waves of RW rows (RW a multiple of SEG_R), PMAX = most control points
-// one wave's rows touch at level L (bounds the per-wave partial window in LDS).
-static FitGeo fit_geo(const vh_batch *b, int L) {
-    FitGeo g;
-    const int R = (int)b->R;
-    const int nseg = (R + SEG_R - 1) / SEG_R;
-    int W = nseg < 16 ? nseg : 16;
-    const int segs_per_wave = (nseg + W - 1) / W;
-    g.RW = segs_per_wave * SEG_R;
-    g.W = (R + g.RW - 1) / g.RW;
-    g.PMAX = b->fit_pmax[L];
-    (void)W;
-    return g;
-}
-
-static size_t fit_lds_bytes(const FitGeo &g, int ncx, int smax) {
-    return sizeof(double) * ((size_t)ncx * TILE_W + std::max((size_t)g.W * g.PMAX * TILE_W, (size_t)smax));
-}
-
-// One sub-batch [vol0, vol0 + ns): the whole multi-level loop.
-static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int64_t ns, float *U) {
+// One sub-batch [vol0, vol0 + ns): the whole multi-level loop.  Flat sweeps run over the chunk
+// range [cp[vol0], cp[vol0 + ns]); converged volumes' blocks exit at once.
+static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int64_t ns,
+                        const std::vector<int32_t> &hcp) {
     hipStream_t st = b->ctx->stream;
     const int64_t ntiles = b->n4_tiles;
-    const unsigned nseg = (unsigned)((b->R + SEG_R - 1) / SEG_R);
+    const int32_t ch0 = hcp[vol0], nch = hcp[vol0 + ns] - hcp[vol0];
     const dim3 cg((unsigned)((b->CZ + VH_TPB - 1) / VH_TPB), (unsigned)ns);
-    const dim3 sg((unsigned)((ntiles + 3) / 4), nseg, (unsigned)ns);   // 4 tile-waves per block
-    const int64_t nparts = ntiles * nseg;   // eval partial slots per volume
+    const double inv_cz = 1.0 / (double)b->CZ;
     const int bins = prm.n_bins;
     const int LOOK = 3;
+    float *U = b->d_U;
     std::vector<hipEvent_t> evs;
     int32_t *hflag = b->ctx->h_pinned;
     int total_iters = 0;
     for (int L = 0; L < prm.n_levels; ++L) total_iters += prm.max_iters[L];
     HIP_TRY(hipMemsetAsync(b->d_nactive, 0, sizeof(int32_t) * (total_iters + 1), st));
     int gi = 0;   // iteration slot within this sub-batch
-    float *cL0 = b->d_L0, *cB = b->d_B;
-    const int32_t *rs = b->d_rowstart;
     try {
         for (int L = 0; L < prm.n_levels; ++L) {
             const DevLevel lv = dev_level(b, prm, L);
-            const FitGeo g = fit_geo(b, L);
             const dim3 fg((unsigned)ntiles, (unsigned)ns);
-            const size_t fit_lds = fit_lds_bytes(g, lv.ax[0].ncp, b->fit_smax[L]);
-            const int64_t nlat = (int64_t)lv.ax[0].ncp * lv.ax[1].ncp * lv.ax[2].ncp;
+            const int ncx = lv.ax[0].ncp;
+            const size_t fit_lds = sizeof(double) * ((size_t)ncx * TILE_W + (size_t)b->fit_smax[L]);
+            if (fit_lds > 64 * 1024)
+                throw VhError{VH_ERR_ARG, "N4 fit: tile slab exceeds the LDS budget"};
+            const int64_t nlat = (int64_t)ncx * lv.ax[1].ncp * lv.ax[2].ncp;
             const dim3 lg((unsigned)ns, (unsigned)((nlat + VH_TPB - 1) / VH_TPB));
             const dim3 pg((unsigned)ns, (unsigned)((nlat / lv.ax[2].ncp * b->Z + VH_TPB - 1) / VH_TPB));
-            const unsigned fit_threads = (unsigned)(g.W * 64);
-            if (fit_lds > 64 * 1024)
-                throw VhError{VH_ERR_ARG, "N4 fit: control-point window exceeds the LDS budget"};
             {
                 ScopedKTimer tm(b, "n4_den", 0.0);
-                k_n4_fit<1><<<fg, fit_threads, fit_lds, st>>>(U, b->d_colbits, rs, b->R, b->C, b->Z,
-                                                             b->V, ntiles, bins, b->d_st, b->d_E,
-                                                             lv, g, b->lat_cap, b->d_fitpart, vol0);
+                k_n4_fit<1><<<fg, VH_TPB, fit_lds, st>>>(U, b->d_ridx, b->d_rowstart, b->d_sc, b->R,
+                                                        b->C, b->Z, b->VS, ntiles, bins, b->d_st,
+                                                        b->d_E, lv, inv_cz, b->lat_cap,
+                                                        b->d_fitpart, vol0);
                 VH_CHECK_LAUNCH();
                 k_n4_tilesum<1><<<lg, VH_TPB, 0, st>>>(b->d_fitpart, b->lat_cap, ntiles, b->d_lat,
                                                        b->d_den, b->lat_cap, b->d_st, lv, vol0);
@@ -1138,7 +1138,7 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
             }
             const int level_start = (int)evs.size();
             for (int it = 0; it < prm.max_iters[L]; ++it, ++gi) {
-                k_n4_ctrl<<<(unsigned)ns, 64, 0, st>>>(b->d_st, b->d_part, nparts, b->d_sc, L, it,
+                k_n4_ctrl<<<(unsigned)ns, 64, 0, st>>>(b->d_st, b->d_cpart, b->d_cp, b->d_sc, L, it,
                                                        prm.conv_threshold, bins, vol0,
                                                        b->d_nactive + gi);
                 VH_CHECK_LAUNCH();
@@ -1148,24 +1148,25 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
                 HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
                 evs.push_back(ev);
                 HIP_TRY(hipEventRecord(ev, st));
-                k_n4_exact_min<<<(unsigned)ns, VH_TPB, 0, st>>>(U, b->d_colbits, rs, b->R, b->CZ,
-                                                                b->V, ntiles, bins, b->d_st, vol0);
+                k_n4_exact_min<<<(unsigned)ns, VH_TPB, 0, st>>>(U, b->d_colbits, b->d_rowstart, b->R,
+                                                                b->CZ, b->VS, ntiles, bins, b->d_st,
+                                                                vol0);
                 VH_CHECK_LAUNCH();
-                {
+                if (nch > 0) {
                     ScopedKTimer tm(b, "n4_hist", 0.0);
-                    k_n4_hist<<<sg, VH_TPB, 0, st>>>(U, b->d_colbits, rs, b->R, b->CZ, b->V, ntiles,
-                                                     bins, b->d_st, b->d_hist, vol0);
+                    k_n4_hist<<<(unsigned)nch, VH_TPB, 0, st>>>(U, b->d_cp, b->d_cvol, b->d_sc, b->VS,
+                                                                bins, b->d_st, b->d_hpart, ch0);
                     VH_CHECK_LAUNCH();
                 }
-                k_n4_emap<<<(unsigned)ns, VH_TPB, 0, st>>>(b->d_hist, b->d_twiddle, bins, prm.fwhm,
-                                                           prm.wiener_noise, b->d_st, b->d_E,
-                                                           vol0, b->d_hist);
+                k_n4_emap<<<(unsigned)ns, VH_TPB, 0, st>>>(b->d_hpart, b->d_cp, b->d_twiddle, bins,
+                                                           prm.fwhm, prm.wiener_noise, b->d_st,
+                                                           b->d_E, vol0);
                 VH_CHECK_LAUNCH();
                 {
                     ScopedKTimer tm(b, "n4_fit", 0.0);
-                    k_n4_fit<0><<<fg, fit_threads, fit_lds, st>>>(
-                        U, b->d_colbits, rs, b->R, b->C, b->Z, b->V, ntiles, bins, b->d_st,
-                        b->d_E, lv, g, b->lat_cap, b->d_fitpart, vol0);
+                    k_n4_fit<0><<<fg, VH_TPB, fit_lds, st>>>(
+                        U, b->d_ridx, b->d_rowstart, b->d_sc, b->R, b->C, b->Z, b->VS, ntiles, bins,
+                        b->d_st, b->d_E, lv, inv_cz, b->lat_cap, b->d_fitpart, vol0);
                     VH_CHECK_LAUNCH();
                 }
                 {
@@ -1181,11 +1182,11 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
                                                   b->d_T, b->t_cap, vol0);
                     VH_CHECK_LAUNCH();
                 }
-                {
+                if (nch > 0) {
                     ScopedKTimer tm(b, "n4_eval", 0.0);
-                    k_n4_eval<<<sg, VH_TPB, 0, st>>>(cL0, cB, U, b->d_colbits, rs, b->d_sc, b->R,
-                                                     b->CZ, b->V, ntiles, b->d_T, b->t_cap, lv,
-                                                     b->d_st, nparts, b->d_part, vol0);
+                    k_n4_eval<<<(unsigned)nch, VH_TPB, 0, st>>>(
+                        b->d_L0, b->d_B, U, b->d_ridx, b->d_cp, b->d_cvol, b->d_sc, b->CZ, b->VS,
+                        inv_cz, b->d_T, b->t_cap, lv, b->d_st, b->d_cpart, ch0);
                     VH_CHECK_LAUNCH();
                 }
                 const int k = (int)evs.size() - 1 - LOOK;
@@ -1194,7 +1195,7 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
                     if (hflag[(gi - LOOK) % 1024] == 0) { ++gi; break; }
                 }
             }
-            k_n4_level_end<<<(unsigned)ns, 64, 0, st>>>(b->d_st, b->d_part, nparts, b->d_sc, L,
+            k_n4_level_end<<<(unsigned)ns, 64, 0, st>>>(b->d_st, b->d_cpart, b->d_cp, b->d_sc, L,
                                                         vol0);
             VH_CHECK_LAUNCH();
             if (L < prm.n_levels - 1) {
@@ -1216,12 +1217,10 @@ void vh_launch_n4(vh_batch *b, const vh_n4_params &prm) {
     vh_ensure_n4_workspace(b, prm);
     const dim3 cg = col_grid(b);
     const int64_t ntiles = b->n4_tiles;
-    // U = L0 - B (compact) lives in the output buffer until k_n4_final overwrites it densely
-    float *U = b->d_n4;
     HIP_TRY(hipMemsetAsync(b->d_lat, 0, sizeof(float) * b->nb * b->lat_cap, st));
-    HIP_TRY(hipMemsetAsync(b->d_hist, 0, sizeof(uint64_t) * b->nb * VH_MAX_BINS, st));
     k_n4_state_init<<<(unsigned)((b->nb + 255) / 256), 256, 0, st>>>(b->d_st, b->nb);
     VH_CHECK_LAUNCH();
+    std::vector<int32_t> hcp(b->nb + 1);
     {
         ScopedKTimer tm(b, "n4_init", 0.0);
         k_n4_rowcount<<<dim3((unsigned)ntiles, (unsigned)b->nb), 64, 0, st>>>(
@@ -1232,8 +1231,14 @@ void vh_launch_n4(vh_batch *b, const vh_n4_params &prm) {
         const dim3 sg((unsigned)((ntiles + 3) / 4), (unsigned)((b->R + SEG_R - 1) / SEG_R),
                       (unsigned)b->nb);
         k_n4_init<<<sg, VH_TPB, 0, st>>>(b->d_hp, b->d_colbits, b->d_rowstart, b->d_sc, b->R, b->CZ,
-                                         b->V, ntiles, b->d_L0, b->d_B, U, b->d_st, 0);
+                                         b->V, b->VS, ntiles, b->d_L0, b->d_B, b->d_U, b->d_ridx,
+                                         b->d_st);
         VH_CHECK_LAUNCH();
+        k_n4_chunks<<<1, VH_TPB, 0, st>>>(b->d_sc, b->nb, b->d_cp, b->d_cvol);
+        VH_CHECK_LAUNCH();
+        HIP_TRY(hipMemcpyAsync(hcp.data(), b->d_cp, sizeof(int32_t) * (b->nb + 1),
+                               hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
     }
     int64_t sb = b->n4_subbatch > 0 ? b->n4_subbatch : b->nb;
     if (const char *e = getenv("VH_N4_SUBBATCH")) {
@@ -1241,7 +1246,7 @@ void vh_launch_n4(vh_batch *b, const vh_n4_params &prm) {
         if (v > 0) sb = v;
     }
     if (sb > b->nb) sb = b->nb;
-    for (int64_t v0 = 0; v0 < b->nb; v0 += sb) n4_subbatch(b, prm, v0, std::min(sb, b->nb - v0), U);
+    for (int64_t v0 = 0; v0 < b->nb; v0 += sb) n4_subbatch(b, prm, v0, std::min(sb, b->nb - v0), hcp);
     {
         const DevLevel lv = dev_level(b, prm, prm.n_levels - 1);
         ScopedKTimer tm(b, "n4_final", 9.0 * (double)b->V);
@@ -1250,3 +1255,4 @@ void vh_launch_n4(vh_batch *b, const vh_n4_params &prm) {
         VH_CHECK_LAUNCH();
     }
 }
+

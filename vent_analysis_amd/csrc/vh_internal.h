@@ -121,14 +121,20 @@ struct vh_batch {
     float *d_L0 = nullptr, *d_B = nullptr, *d_lat = nullptr, *d_E = nullptr;
     double *d_fitpart = nullptr;     // [nb][tiles][lattice] per-tile contracted fit slabs
     int32_t *d_rowstart = nullptr;   // [nb][tiles][R] compact offset of each (64-column tile, row)
+    // compact N4 state: mask==1 voxels in tile-row order, volume stride VS
+    int64_t VS = 0;
+    float *d_U = nullptr;            // [nb][VS] U = L0 - B
+    int32_t *d_ridx = nullptr;       // [nb][VS] raster index of each compact voxel
+    int32_t *d_cp = nullptr;         // [nb + 1] chunk prefix (N4_CH voxels per chunk)
+    int32_t *d_cvol = nullptr;       // [chunks] owning volume
+    uint64_t *d_hpart = nullptr;     // [chunks][VH_MAX_BINS] per-chunk histograms
+    double *d_cpart = nullptr;       // [chunks][2] per-chunk convergence sums
     int64_t n4_tiles = 0;
-    std::vector<int> fit_pmax;       // per level: control points one fit row-wave touches
     std::vector<int> fit_smax;       // per level: doubles of the fit's slice-contracted tile slab
     std::vector<size_t> tile_off;    // per level: offset of the fit tile metadata in d_tabs
     double *d_P1 = nullptr, *d_num = nullptr, *d_den = nullptr;
     float *d_T = nullptr;            // [nb][ncx][CZ] per-column lattice contraction for eval
     int64_t t_cap = 0;
-    uint64_t *d_hist = nullptr;
     N4State *d_st = nullptr;
     int32_t *d_nactive = nullptr;
     void *d_tabs = nullptr;          // device copy of all per-level axis tables
