@@ -37,13 +37,17 @@ struct DevLevel {
     // per 64-column fit tile: {y0, y1, z0, z1} (first/last column's col and slice), then
     // {jlo, JT, klo, KT} (lattice cols / slices the tile's slab covers)
     const int4 *tiles;
+    const int2 *jt;   // per lattice col j: first / last tile whose slab covers j
 };
 
 
 #define TILE_W 64   // columns per compact tile (one wave)
+#define FIT_W 128   // columns per fit block (FIT_W / TILE_W compact tiles, contiguous in compact order)
+#define FIT_TPT (FIT_W / TILE_W)
 #define SEG_R 16    // rows per wave segment
 #define N4_CH 4096  // compact voxels per chunk (flat sweeps: 256 threads x 16)
 #define N4_VPT (N4_CH / VH_TPB)
+#define FIT_G 4     // fit voxels per thread with loads in flight together
 #define N4_FIX 68719476736.0   // 2^36: fixed-point scale of the fit's LDS row contraction
 #define LN2 0.69314718055994530942
 #define PI_D 3.14159265358979323846
@@ -135,8 +139,9 @@ void vh_n4_prepare_tables(vh_batch *b, const vh_n4_params &prm) {
         }
     }
     // fit tile metadata per level (64-column tiles of the (col, slice) plane)
-    const int64_t ntiles = (b->CZ + TILE_W - 1) / TILE_W;
+    const int64_t ntiles = (b->CZ + FIT_W - 1) / FIT_W;   // fit tiles
     b->tile_off.assign((size_t)prm.n_levels, 0);
+    b->jt_off.assign((size_t)prm.n_levels, 0);
     b->fit_smax.assign((size_t)prm.n_levels, 0);
     for (int L = 0; L < prm.n_levels; ++L) {
         const float eps = vh_bspline_eps(std::max({level_ncp(prm, L, 0), level_ncp(prm, L, 1),
@@ -147,7 +152,7 @@ void vh_n4_prepare_tables(vh_batch *b, const vh_n4_params &prm) {
         std::vector<int32_t> meta(8 * (size_t)ntiles);
         int smax = 0;
         for (int64_t t = 0; t < ntiles; ++t) {
-            const int64_t c0 = t * TILE_W, c1 = std::min(c0 + TILE_W, b->CZ) - 1;
+            const int64_t c0 = t * FIT_W, c1 = std::min(c0 + FIT_W, b->CZ) - 1;
             const int y0 = (int)(c0 / b->Z), y1 = (int)(c1 / b->Z);
             const int z0 = (int)(c0 % b->Z), z1 = (int)(c1 % b->Z);
             const int zlo = y0 == y1 ? z0 : 0, zhi = y0 == y1 ? z1 : (int)b->Z - 1;
@@ -157,7 +162,21 @@ void vh_n4_prepare_tables(vh_batch *b, const vh_n4_params &prm) {
             std::memcpy(&meta[8 * t], m, sizeof(m));
             smax = std::max(smax, level_ncp(prm, L, 0) * (y1 - y0 + 1) * KT);
         }
+        // lattice col j -> the contiguous range of tiles whose slab covers it
+        const int ncy = level_ncp(prm, L, 1);
+        std::vector<int32_t> jt(2 * (size_t)ncy);
+        for (int j = 0; j < ncy; ++j) {
+            int lo = (int)ntiles, hi = -1;
+            for (int64_t t = 0; t < ntiles; ++t)
+                if (j >= meta[8 * t + 4] && j < meta[8 * t + 4] + meta[8 * t + 5]) {
+                    lo = std::min(lo, (int)t);
+                    hi = std::max(hi, (int)t);
+                }
+            jt[2 * j] = lo;
+            jt[2 * j + 1] = hi;
+        }
         b->tile_off[L] = push(meta.data(), meta.size() * 4);
+        b->jt_off[L] = push(jt.data(), jt.size() * 4);
         b->fit_smax[L] = smax;
     }
     if (b->d_tabs) HIP_TRY(hipFree(b->d_tabs));
@@ -194,6 +213,7 @@ static DevLevel dev_level(const vh_batch *b, const vh_n4_params &prm, int L) {
         lv.ax[a].ncp = level_ncp(prm, L, a);
     }
     lv.tiles = (const int4 *)(base + b->tile_off[L]);
+    lv.jt = (const int2 *)(base + b->jt_off[L]);
     return lv;
 }
 
@@ -234,7 +254,7 @@ void vh_ensure_n4_workspace(vh_batch *b, const vh_n4_params &prm) {
         HIP_TRY(hipMalloc(&b->d_rowstart, sizeof(int32_t) * b->nb * ntiles * b->R));
         b->n4_tiles = ntiles;
     }
-    const int64_t fp = ntiles * lat;   // per-volume tile slabs
+    const int64_t fp = ((b->CZ + FIT_W - 1) / FIT_W) * lat;   // per-volume fit tile slabs
     if (fp > b->q1_cap) {
         if (b->d_fitpart) HIP_TRY(hipFree(b->d_fitpart));
         HIP_TRY(hipMalloc(&b->d_fitpart, sizeof(double) * b->nb * fp));
@@ -454,77 +474,32 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_init(const float *__restrict__ I,
 // chunk counts, cvol[c] = owning volume.  One block.
 __global__ void __launch_bounds__(VH_TPB) k_n4_chunks(const VolScalars *sc, int64_t nb,
                                                      int32_t *cp, int32_t *cvol) {
-    if (threadIdx.x == 0) {
+    __shared__ int32_t s_part[VH_TPB];
+    const int t = threadIdx.x;
+    const int64_t per = (nb + VH_TPB - 1) / VH_TPB;
+    const int64_t s0 = t * per < nb ? t * per : nb, e0 = s0 + per < nb ? s0 + per : nb;
+    int32_t acc = 0;
+    for (int64_t b = s0; b < e0; ++b) acc += (int32_t)((sc[b].n_mask1 + N4_CH - 1) / N4_CH);
+    s_part[t] = acc;
+    __syncthreads();
+    if (t == 0) {
         int32_t run = 0;
-        for (int64_t b = 0; b < nb; ++b) {
-            cp[b] = run;
-            run += (int32_t)((sc[b].n_mask1 + N4_CH - 1) / N4_CH);
-        }
+        for (int i = 0; i < VH_TPB; ++i) { const int32_t v = s_part[i]; s_part[i] = run; run += v; }
         cp[nb] = run;
     }
     __syncthreads();
-    for (int64_t b = threadIdx.x; b < nb; b += VH_TPB)
-        for (int32_t c = cp[b]; c < cp[b + 1]; ++c) cvol[c] = (int32_t)b;
-}
-
-// Iteration control: convergence of the previous iteration, the while-condition of ITK's loop,
-// bin range (common case of the else-if quirk), histogram reset.
-__global__ void __launch_bounds__(64) k_n4_ctrl(N4State *st, const double *part, const int32_t *cp,
-                                               const VolScalars *sc, int level, int it,
-                                               float thresh, int bins, int64_t vol0,
-                                               int32_t *nactive) {
-    const int64_t b = vol0 + blockIdx.x;
-    N4State &s = st[b];
-    const bool was_active = s.active;
-    double conv = 0.0;
-    if (it > 0 && was_active) conv = conv_from_parts(part, cp, b, (double)sc[b].n_mask1);
-    if (threadIdx.x != 0) return;
-    if (it == 0) {
-        s.active = 1;
-        s.iters = 0;
-        s.conv = INFINITY;
-    } else if (was_active) {
-        s.conv = conv;
-        if (!(conv > (double)thresh)) {
-            s.active = 0;
-            s.iters_level[level] = s.iters;
-            s.conv_level[level] = (float)conv;
-        }
+    int32_t run = s_part[t];
+    for (int64_t b = s0; b < e0; ++b) {
+        const int32_t n = (int32_t)((sc[b].n_mask1 + N4_CH - 1) / N4_CH);
+        cp[b] = run;
+        for (int32_t c = 0; c < n; ++c) cvol[run + c] = (int32_t)b;
+        run += n;
     }
-    if (!s.active) return;
-    s.iters += 1;
-    const float bmax = key2f(s.umax_key);
-    const float umin = s.umin_key == 0xffffffffu ? FLT_MAX : key2f(s.umin_key);
-    s.bin_max = bmax;
-    if (umin <= s.u_first) {
-        s.need_exact_min = 0;
-        s.bin_min = umin;
-        s.slope = (bmax - umin) / (float)(bins - 1);
-    } else {
-        s.need_exact_min = 1;   // k_n4_exact_min computes bin_min and slope
-    }
-    s.umax_key = 0u;
-    s.umin_key = 0xffffffffu;
-    atomicAdd(nactive, 1);
-}
-
-__global__ void __launch_bounds__(64) k_n4_level_end(N4State *st, const double *part,
-                                                    const int32_t *cp, const VolScalars *sc,
-                                                    int level, int64_t vol0) {
-    const int64_t b = vol0 + blockIdx.x;
-    N4State &s = st[b];
-    if (!s.active) return;
-    const double conv = conv_from_parts(part, cp, b, (double)sc[b].n_mask1);
-    if (threadIdx.x != 0) return;
-    s.conv = conv;
-    s.iters_level[level] = s.iters;
-    s.conv_level[level] = (float)conv;
-    s.active = 0;
 }
 
 // Exact ITK bin minimum when the first masked pixel is the strict minimum: min over the pixels
-// that are not running maxima in raster order (chunked prefix-max scan over rows).  Rare path,
-// one block per volume; each thread walks whole rows, tracking compact offsets incrementally.
+// that are not running maxima in raster order (chunked prefix-max scan over rows).  Rare path;
+// each thread walks whole rows, tracking compact offsets incrementally.
 __device__ __forceinline__ void exact_row_scan(const float *Uv, const uint32_t *colbits,
                                                const int32_t *rs, int64_t b, int64_t R, int64_t CZ,
                                                int64_t ntiles, int64_t x, float &run, float &mn,
@@ -540,19 +515,13 @@ __device__ __forceinline__ void exact_row_scan(const float *Uv, const uint32_t *
     }
 }
 
-__global__ void __launch_bounds__(VH_TPB) k_n4_exact_min(const float *__restrict__ U,
-                                                        const uint32_t *__restrict__ colbits,
-                                                        const int32_t *rs, int64_t R, int64_t CZ,
-                                                        int64_t VS, int64_t ntiles, int bins,
-                                                        N4State *st, int64_t vol0) {
+__device__ float exact_min_block(const float *Uv, const uint32_t *colbits, const int32_t *rs,
+                                 int64_t b, int64_t R, int64_t CZ, int64_t ntiles) {
     __shared__ float s_cmax[VH_TPB];
     __shared__ float s_min[VH_TPB];
-    const int64_t b = vol0 + blockIdx.x;
-    if (!st[b].active || !st[b].need_exact_min) return;
     const int t = threadIdx.x;
     const int64_t per = (R + VH_TPB - 1) / VH_TPB;
     const int64_t s0 = t * per < R ? t * per : R, e0 = s0 + per < R ? s0 + per : R;
-    const float *Uv = U + b * VS;
     float cmax = -FLT_MAX, dummy = FLT_MAX;
     for (int64_t x = s0; x < e0; ++x) exact_row_scan(Uv, colbits, rs, b, R, CZ, ntiles, x, cmax, dummy, false);
     s_cmax[t] = cmax;
@@ -566,12 +535,82 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_exact_min(const float *__restrict
     for (int64_t x = s0; x < e0; ++x) exact_row_scan(Uv, colbits, rs, b, R, CZ, ntiles, x, run, mn, true);
     s_min[t] = mn;
     __syncthreads();
-    if (t == 0) {
-        float m = FLT_MAX;
+    float m = FLT_MAX;
+    if (t == 0)
         for (int i = 0; i < VH_TPB; ++i) m = s_min[i] < m ? s_min[i] : m;
-        st[b].bin_min = m;
-        st[b].slope = (st[b].bin_max - m) / (float)(bins - 1);
+    return m;
+}
+
+// Iteration control: convergence of the previous iteration, the while-condition of ITK's loop,
+// bin range (the else-if quirk: common case directly, the exact raster scan when the first masked
+// pixel is the strict minimum).  One block per volume.
+__global__ void __launch_bounds__(VH_TPB) k_n4_ctrl(N4State *st, const double *part,
+                                                   const int32_t *cp, const VolScalars *sc,
+                                                   int level, int it, float thresh, int bins,
+                                                   int64_t vol0, int32_t *nactive, const float *U,
+                                                   const uint32_t *colbits, const int32_t *rs,
+                                                   int64_t R, int64_t CZ, int64_t VS,
+                                                   int64_t ntiles) {
+    __shared__ int s_exact;
+    __shared__ float s_bmax;
+    const int64_t b = vol0 + blockIdx.x;
+    const bool was_active = st[b].active;
+    double conv = 0.0;
+    if (threadIdx.x < 64 && it > 0 && was_active)
+        conv = conv_from_parts(part, cp, b, (double)sc[b].n_mask1);
+    if (threadIdx.x == 0) {
+        N4State &s = st[b];
+        s_exact = 0;
+        if (it == 0) {
+            s.active = 1;
+            s.iters = 0;
+            s.conv = INFINITY;
+        } else if (was_active) {
+            s.conv = conv;
+            if (!(conv > (double)thresh)) {
+                s.active = 0;
+                s.iters_level[level] = s.iters;
+                s.conv_level[level] = (float)conv;
+            }
+        }
+        if (s.active) {
+            s.iters += 1;
+            const float bmax = key2f(s.umax_key);
+            const float umin = s.umin_key == 0xffffffffu ? FLT_MAX : key2f(s.umin_key);
+            s.bin_max = bmax;
+            if (umin <= s.u_first) {
+                s.bin_min = umin;
+                s.slope = (bmax - umin) / (float)(bins - 1);
+            } else {
+                s_exact = 1;
+                s_bmax = bmax;
+            }
+            s.umax_key = 0u;
+            s.umin_key = 0xffffffffu;
+            atomicAdd(nactive, 1);
+        }
     }
+    __syncthreads();
+    if (!s_exact) return;
+    const float m = exact_min_block(U + b * VS, colbits, rs, b, R, CZ, ntiles);
+    if (threadIdx.x == 0) {
+        st[b].bin_min = m;
+        st[b].slope = (s_bmax - m) / (float)(bins - 1);
+    }
+}
+
+__global__ void __launch_bounds__(64) k_n4_level_end(N4State *st, const double *part,
+                                                    const int32_t *cp, const VolScalars *sc,
+                                                    int level, int64_t vol0) {
+    const int64_t b = vol0 + blockIdx.x;
+    N4State &s = st[b];
+    if (!s.active) return;
+    const double conv = conv_from_parts(part, cp, b, (double)sc[b].n_mask1);
+    if (threadIdx.x != 0) return;
+    s.conv = conv;
+    s.iters_level[level] = s.iters;
+    s.conv_level[level] = (float)conv;
+    s.active = 0;
 }
 
 // Triangular Parzen histogram of U at mask == 1, unsigned 64-bit fixed point (2^-32 units).
@@ -750,7 +789,9 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_emap(const uint64_t *hpart, const
 // and the result is deterministic), then the block contracts its 64 columns over slices and cols
 //   Pn[i][j][k] = sum_{(y,z) in tile} wy(y,j)^p wz(z,k)^p Q1[i][y][z],  p = 3 (num) / 2 (den)
 // q = r / (sum wx^2 sum wy^2 sum wz^2) for the numerator, 1 for the denominator.  Only the small
-// slab goes to HBM; k_n4_tilesum adds a volume's slabs in tile order.
+// slab goes to HBM; k_n4_tilesum adds a volume's slabs in tile order.  (A last-block-done fold
+// of that sum into this kernel needs agent-scope fences, which write back / invalidate the XCD's
+// L2 on gfx950: measured 10x slower, so the sum stays a separate launch.)
 // ---------------------------------------------------------------------------------------------
 __device__ __forceinline__ int row_of(int r, int64_t CZ, double inv_cz) {
     int x = (int)((double)r * inv_cz);
@@ -769,32 +810,41 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_fit(const float *__restrict__ U,
                                                   int64_t slab, double *part, int64_t vol0) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     __shared__ float sE[VH_MAX_BINS];
-    __shared__ double sIyz[TILE_W];
+    __shared__ double sIyz[FIT_W];
+    __shared__ double sWz[4 * FIT_W];
+    __shared__ int sBz[FIT_W];
     const int64_t b = vol0 + blockIdx.y;
     if (MODE == 0 && !st[b].active) return;
     const int tile = blockIdx.x;
     const DevAxis ax = lv.ax[0], ay = lv.ax[1], az = lv.ax[2];
     const int ncx = ax.ncp;
     const int64_t CZ = C * Z;
-    const int64_t c0 = (int64_t)tile * TILE_W;
+    const int64_t c0 = (int64_t)tile * FIT_W;
     const int4 m0 = lv.tiles[2 * tile], m1 = lv.tiles[2 * tile + 1];
     const int jlo = m1.x, JT = m1.y, klo = m1.z, KT = m1.w;
-    double *out = part + (b * ntiles + tile) * slab;
-    const int32_t *rt = rs + (b * ntiles + tile) * R;
-    const int64_t ts = rt[0];
-    const int64_t te = tile + 1 < ntiles ? rt[R] : sc[b].n_mask1;
+    const int64_t nft = (CZ + FIT_W - 1) / FIT_W;
+    double *out = part + (b * nft + tile) * slab;
+    // compact tiles FIT_TPT*tile .. +FIT_TPT-1 hold this block's voxels, contiguously
+    const int64_t ts = rs[(b * ntiles + (int64_t)tile * FIT_TPT) * R];
+    const int64_t te = (int64_t)(tile + 1) * FIT_TPT < ntiles
+                           ? rs[(b * ntiles + (int64_t)(tile + 1) * FIT_TPT) * R]
+                           : sc[b].n_mask1;
     if (ts >= te) {   // no masked voxel in this tile
         for (int e = threadIdx.x; e < ncx * JT * KT; e += VH_TPB) out[e] = 0.0;
         return;
     }
-    unsigned long long *sQi = reinterpret_cast<unsigned long long *>(smem);   // [ncx][64]
-    for (int e = threadIdx.x; e < ncx * TILE_W; e += VH_TPB) sQi[e] = 0ull;
-    if (MODE == 0) {
+    unsigned long long *sQi = reinterpret_cast<unsigned long long *>(smem);   // [ncx][FIT_W]
+    for (int e = threadIdx.x; e < ncx * FIT_W; e += VH_TPB) sQi[e] = 0ull;
+    if (MODE == 0)
         for (int i = threadIdx.x; i < bins; i += VH_TPB) sE[i] = E[b * VH_MAX_BINS + i];
-        if (threadIdx.x < TILE_W && c0 + threadIdx.x < CZ) {
-            const int64_t col = c0 + threadIdx.x;
-            sIyz[threadIdx.x] = ay.isw2[col / Z] * az.isw2[col % Z];
-        }
+    if (threadIdx.x < FIT_W && c0 + threadIdx.x < CZ) {   // per-column slice tables
+        const int64_t col = c0 + threadIdx.x;
+        const int64_t z = col % Z;
+        if (MODE == 0) sIyz[threadIdx.x] = ay.isw2[col / Z] * az.isw2[z];
+        sBz[threadIdx.x] = az.base[z];
+        const double *wz = (MODE == 0 ? az.w3 : az.w2) + 4 * z;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) sWz[4 * threadIdx.x + c] = wz[c];
     }
     __syncthreads();
     // ---- row contraction: every masked voxel of the tile ----
@@ -805,47 +855,58 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_fit(const float *__restrict__ U,
     }
     const float *Ub = U + b * VS;
     const int32_t *Rb = ridx + b * VS;
-    for (int64_t j = ts + threadIdx.x; j < te; j += VH_TPB) {
-        const int r = Rb[j];
-        const int x = row_of(r, CZ, inv_cz);
-        const int l = (int)((int64_t)r - (int64_t)x * CZ - c0);
-        const int bx = ax.base[x];
-        const double *wp = (MODE == 0 ? ax.w3 : ax.w2) + 4 * x;
-        if (MODE == 0) {
-            const float u = Ub[j];
-            const float rr = u - sharpen_value(u, bmin, slope, sE, bins);
-            const double q = ((double)rr * ax.isw2[x]) * sIyz[l];
+    for (int64_t jb = ts + threadIdx.x; jb < te; jb += FIT_G * VH_TPB) {
+        int rr[FIT_G];
+        float uu[FIT_G];
 #pragma unroll
-            for (int c = 0; c < 4; ++c)
-                atomicAdd(&sQi[(bx + c) * TILE_W + l],
-                          (unsigned long long)__double2ll_rn(wp[c] * q * N4_FIX));
-        } else {
+        for (int k = 0; k < FIT_G; ++k) {   // every load of the group in flight first
+            const int64_t j = jb + (int64_t)k * VH_TPB;
+            rr[k] = j < te ? Rb[j] : -1;
+            if (MODE == 0) uu[k] = j < te ? Ub[j] : 0.0f;
+        }
 #pragma unroll
-            for (int c = 0; c < 4; ++c)
-                atomicAdd(&sQi[(bx + c) * TILE_W + l],
-                          (unsigned long long)__double2ll_rn(wp[c] * N4_FIX));
+        for (int k = 0; k < FIT_G; ++k) {
+            const int r = rr[k];
+            if (r < 0) continue;
+            const int x = row_of(r, CZ, inv_cz);
+            const int l = (int)((int64_t)r - (int64_t)x * CZ - c0);
+            const int bx = ax.base[x];
+            const double *wp = (MODE == 0 ? ax.w3 : ax.w2) + 4 * x;
+            if (MODE == 0) {
+                const float u = uu[k];
+                const float rv = u - sharpen_value(u, bmin, slope, sE, bins);
+                const double q = ((double)rv * ax.isw2[x]) * sIyz[l];
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    atomicAdd(&sQi[(bx + c) * FIT_W + l],
+                              (unsigned long long)__double2ll_rn(wp[c] * q * N4_FIX));
+            } else {
+#pragma unroll
+                for (int c = 0; c < 4; ++c)
+                    atomicAdd(&sQi[(bx + c) * FIT_W + l],
+                              (unsigned long long)__double2ll_rn(wp[c] * N4_FIX));
+            }
         }
     }
     __syncthreads();
     double *sQ1 = smem;   // in place: each slot converted by the thread that reads it
-    for (int e = threadIdx.x; e < ncx * TILE_W; e += VH_TPB)
+    for (int e = threadIdx.x; e < ncx * FIT_W; e += VH_TPB)
         sQ1[e] = (double)(long long)sQi[e] * (1.0 / N4_FIX);
     __syncthreads();
     // ---- contract the tile's columns: over slices per tile row (stage 1), then over cols ----
     const int y0 = m0.x, y1 = m0.y, ny = y1 - y0 + 1;
-    const double *wzp = MODE == 0 ? az.w3 : az.w2;
     const double *wyp = MODE == 0 ? ay.w3 : ay.w2;
-    double *sS = smem + (size_t)ncx * TILE_W;   // [ncx][ny][KT]
+    double *sS = smem + (size_t)ncx * FIT_W;   // [ncx][ny][KT]
     for (int e = threadIdx.x; e < ncx * ny * KT; e += VH_TPB) {
         const int i = e / (ny * KT), yy = (e / KT) % ny, k = klo + e % KT;
         const int y = y0 + yy;
         const int zs = y == y0 ? m0.z : 0, ze = y == y1 ? m0.w : (int)Z - 1;
         const int lb = (int)((int64_t)y * Z - c0);   // lane of (y, z = 0)
         double acc = 0.0;
-        for (int z = zs; z <= ze; ++z) {
-            const int cz = k - az.base[z];
+        for (int l = lb + zs; l <= lb + ze; ++l) {
+            const int cz = k - sBz[l];
             if (cz < 0 || cz > 3) continue;
-            acc = fma(wzp[4 * z + cz], sQ1[i * TILE_W + lb + z], acc);
+            acc = fma(sWz[4 * l + cz], sQ1[i * FIT_W + l], acc);
         }
         sS[e] = acc;
     }
@@ -863,7 +924,8 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_fit(const float *__restrict__ U,
 }
 
 // Sum the tile slabs of each volume in tile order: MODE 1 den; MODE 0 phi = num / den and
-// lattice += phi.  grid (volumes, lattice chunks of 256).
+// lattice += phi.  grid (volumes, lattice chunks of 256); a lattice col j only visits the tiles
+// whose slab covers it (lv.jt), eight slab loads in flight before the ordered sum.
 template <int MODE>
 __global__ void __launch_bounds__(VH_TPB) k_n4_tilesum(const double *part, int64_t slab,
                                                       int64_t ntiles, float *lat, double *den,
@@ -877,11 +939,20 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_tilesum(const double *part, int64
     const int i = e / (ncy * ncz), j = (e / ncz) % ncy, kq = e % ncz;
     double acc = 0.0;
     const double *pb = part + b * ntiles * slab;
-    for (int64_t tile = 0; tile < ntiles; ++tile) {
-        const int4 m = lv.tiles[2 * tile + 1];   // jlo, JT, klo, KT
-        const int jj = j - m.x, kk = kq - m.z;
-        if (jj < 0 || jj >= m.y || kk < 0 || kk >= m.w) continue;
-        acc += pb[tile * slab + (i * m.y + jj) * m.w + kk];
+    const int2 tr = lv.jt[j];
+    for (int t0 = tr.x; t0 <= tr.y; t0 += 8) {
+        double v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            v[q] = 0.0;
+            const int t = t0 + q;
+            if (t > tr.y) continue;
+            const int4 m = lv.tiles[2 * t + 1];   // jlo, JT, klo, KT
+            const int jj = j - m.x, kk = kq - m.z;
+            if (kk >= 0 && kk < m.w) v[q] = pb[(int64_t)t * slab + (i * m.y + jj) * m.w + kk];
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc += v[q];
     }
     if (MODE == 1) {
         den[b * lat_cap + e] = acc;
@@ -895,9 +966,9 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_tilesum(const double *part, int64
 // P1[i][j][z] = sum_k wz(z,k) lat[i][j][k] for the eval sweep.  grid (volumes, chunks of 256).
 __global__ void __launch_bounds__(VH_TPB) k_n4_P1(const float *lat, int64_t lat_cap, double *P1,
                                                  int64_t q2_cap, int64_t Z, const N4State *st,
-                                                 DevLevel lv, int64_t vol0, int all) {
+                                                 DevLevel lv, int64_t vol0) {
     const int64_t b = vol0 + blockIdx.x;
-    if (!all && !st[b].active) return;
+    if (!st[b].active) return;
     const DevAxis az = lv.ax[2];
     const int ncx = lv.ax[0].ncp, ncy = lv.ax[1].ncp, ncz = az.ncp;
     const int64_t e = blockIdx.y * (int64_t)VH_TPB + threadIdx.x;
@@ -1117,9 +1188,10 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
     try {
         for (int L = 0; L < prm.n_levels; ++L) {
             const DevLevel lv = dev_level(b, prm, L);
-            const dim3 fg((unsigned)ntiles, (unsigned)ns);
+            const int64_t nft = (b->CZ + FIT_W - 1) / FIT_W;
+            const dim3 fg((unsigned)nft, (unsigned)ns);
             const int ncx = lv.ax[0].ncp;
-            const size_t fit_lds = sizeof(double) * ((size_t)ncx * TILE_W + (size_t)b->fit_smax[L]);
+            const size_t fit_lds = sizeof(double) * ((size_t)ncx * FIT_W + (size_t)b->fit_smax[L]);
             if (fit_lds > 64 * 1024)
                 throw VhError{VH_ERR_ARG, "N4 fit: tile slab exceeds the LDS budget"};
             const int64_t nlat = (int64_t)ncx * lv.ax[1].ncp * lv.ax[2].ncp;
@@ -1127,20 +1199,19 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
             const dim3 pg((unsigned)ns, (unsigned)((nlat / lv.ax[2].ncp * b->Z + VH_TPB - 1) / VH_TPB));
             {
                 ScopedKTimer tm(b, "n4_den", 0.0);
-                k_n4_fit<1><<<fg, VH_TPB, fit_lds, st>>>(U, b->d_ridx, b->d_rowstart, b->d_sc, b->R,
-                                                        b->C, b->Z, b->VS, ntiles, bins, b->d_st,
-                                                        b->d_E, lv, inv_cz, b->lat_cap,
-                                                        b->d_fitpart, vol0);
+                k_n4_fit<1><<<fg, VH_TPB, fit_lds, st>>>(
+                    U, b->d_ridx, b->d_rowstart, b->d_sc, b->R, b->C, b->Z, b->VS, ntiles, bins,
+                    b->d_st, b->d_E, lv, inv_cz, b->lat_cap, b->d_fitpart, vol0);
                 VH_CHECK_LAUNCH();
-                k_n4_tilesum<1><<<lg, VH_TPB, 0, st>>>(b->d_fitpart, b->lat_cap, ntiles, b->d_lat,
+                k_n4_tilesum<1><<<lg, VH_TPB, 0, st>>>(b->d_fitpart, b->lat_cap, nft, b->d_lat,
                                                        b->d_den, b->lat_cap, b->d_st, lv, vol0);
                 VH_CHECK_LAUNCH();
             }
             const int level_start = (int)evs.size();
             for (int it = 0; it < prm.max_iters[L]; ++it, ++gi) {
-                k_n4_ctrl<<<(unsigned)ns, 64, 0, st>>>(b->d_st, b->d_cpart, b->d_cp, b->d_sc, L, it,
-                                                       prm.conv_threshold, bins, vol0,
-                                                       b->d_nactive + gi);
+                k_n4_ctrl<<<(unsigned)ns, VH_TPB, 0, st>>>(
+                    b->d_st, b->d_cpart, b->d_cp, b->d_sc, L, it, prm.conv_threshold, bins, vol0,
+                    b->d_nactive + gi, U, b->d_colbits, b->d_rowstart, b->R, b->CZ, b->VS, ntiles);
                 VH_CHECK_LAUNCH();
                 HIP_TRY(hipMemcpyAsync(hflag + (gi % 1024), b->d_nactive + gi, sizeof(int32_t),
                                        hipMemcpyDeviceToHost, st));
@@ -1148,10 +1219,6 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
                 HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
                 evs.push_back(ev);
                 HIP_TRY(hipEventRecord(ev, st));
-                k_n4_exact_min<<<(unsigned)ns, VH_TPB, 0, st>>>(U, b->d_colbits, b->d_rowstart, b->R,
-                                                                b->CZ, b->VS, ntiles, bins, b->d_st,
-                                                                vol0);
-                VH_CHECK_LAUNCH();
                 if (nch > 0) {
                     ScopedKTimer tm(b, "n4_hist", 0.0);
                     k_n4_hist<<<(unsigned)nch, VH_TPB, 0, st>>>(U, b->d_cp, b->d_cvol, b->d_sc, b->VS,
@@ -1171,12 +1238,12 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
                 }
                 {
                     ScopedKTimer tm(b, "n4_contract", 0.0);
-                    k_n4_tilesum<0><<<lg, VH_TPB, 0, st>>>(b->d_fitpart, b->lat_cap, ntiles,
+                    k_n4_tilesum<0><<<lg, VH_TPB, 0, st>>>(b->d_fitpart, b->lat_cap, nft,
                                                            b->d_lat, b->d_den, b->lat_cap, b->d_st,
                                                            lv, vol0);
                     VH_CHECK_LAUNCH();
                     k_n4_P1<<<pg, VH_TPB, 0, st>>>(b->d_lat, b->lat_cap, b->d_P1, b->q2_cap, b->Z,
-                                                   b->d_st, lv, vol0, 0);
+                                                   b->d_st, lv, vol0);
                     VH_CHECK_LAUNCH();
                     k_n4_T<<<cg, VH_TPB, 0, st>>>(b->d_P1, b->q2_cap, b->C, b->Z, lv, b->d_st,
                                                   b->d_T, b->t_cap, vol0);

@@ -132,6 +132,7 @@ struct vh_batch {
     int64_t n4_tiles = 0;
     std::vector<int> fit_smax;       // per level: doubles of the fit's slice-contracted tile slab
     std::vector<size_t> tile_off;    // per level: offset of the fit tile metadata in d_tabs
+    std::vector<size_t> jt_off;      // per level: lattice col -> tile range table in d_tabs
     double *d_P1 = nullptr, *d_num = nullptr, *d_den = nullptr;
     float *d_T = nullptr;            // [nb][ncx][CZ] per-column lattice contraction for eval
     int64_t t_cap = 0;
