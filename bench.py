@@ -69,23 +69,32 @@ def cpu_baseline(R, C, Z, seconds=15.0, procs=16):
 # algorithmic bytes per kernel class (DESIGN.md "Roofline accounting")
 # ------------------------------------------------------------------------------------------------
 def algorithmic_bytes(name, hp, mk, res, R, C, Z):
-    """Total algorithmic HBM bytes moved by all launches of kernel class ``name`` in one step."""
+    """Total algorithmic HBM bytes moved by all launches of kernel class ``name`` in one step.
+
+    N4 state is compact (mask == 1 voxels only, DESIGN.md "HBM layout"), so the per-unit figures
+    are per masked voxel and per executed iteration; a volume is only touched by an iteration's
+    sweeps while it is still iterating, so the iteration count is the volume's own."""
     V = R * C * Z
     B = hp.shape[0]
     m = mk.reshape(B, R, C * Z)
+    vm = (m == 1).sum(axis=(1, 2)).astype(np.float64)          # masked (mask == 1) voxels
     nz = m != 0
-    vm = nz.sum(axis=(1, 2)).astype(np.float64)                 # masked voxels
     has = nz.any(axis=1)
     lo = np.where(has, nz.argmax(axis=1), 0)
     hi = np.where(has, R - 1 - nz[:, ::-1, :].argmax(axis=1), -1)
     vr = np.maximum(hi - lo + 1, 0).sum(axis=1).astype(np.float64)   # voxels in column ranges
     iters = np.array([sum(r.n4_iters[:4]) for r in res], np.float64)
-    if name == "n4_eval":        # read mask (range) + L0 + B_old, write B_new   at masked voxels
-        return float(np.sum(iters * (vr + 12.0 * vm)))
-    if name == "n4_fit":         # read mask (range) + L0 + B                    at masked voxels
-        return float(np.sum(iters * (vr + 8.0 * vm)))
-    if name == "n4_hist":
-        return float(np.sum(iters * (vr + 8.0 * vm)))
+    levels = np.array([sum(1 for k in range(4) if r.n4_iters[k] > 0) for r in res], np.float64)
+    if name == "n4_eval":        # read ridx + L0 + B_old, write B_new + U
+        return float(np.sum(iters * 20.0 * vm))
+    if name == "n4_fit":         # read ridx + U
+        return float(np.sum(iters * 8.0 * vm))
+    if name == "n4_hist":        # read U
+        return float(np.sum(iters * 4.0 * vm))
+    if name == "n4_den":         # read ridx, once per level
+        return float(np.sum(levels * 4.0 * vm))
+    if name == "n4_init":        # read I at masked voxels, write L0, B, U, ridx
+        return float(np.sum(20.0 * vm))
     if name == "n4_final":       # read I, write N4HPvent                        every voxel
         return float(B * 8.0 * V)
     if name == "classify":       # read N4 + mask, write defect, border, LB      every voxel
@@ -99,6 +108,19 @@ def algorithmic_bytes(name, hp, mk, res, R, C, Z):
     if name == "mask_stats":
         return float(B * 1.0 * V)
     return 0.0
+
+
+def pmc_traffic(kernel):
+    """Per-launch HBM-side bytes of ``kernel`` from the newest committed PMC summary
+    (profiles/r*_pmc_traffic.json, written by scripts/pmc_summary.py), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(HERE, "profiles", "r*_pmc_traffic.json")))
+    if not files:
+        return None, None
+    k = json.load(open(files[-1]))["kernels"].get(kernel)
+    if not k:
+        return None, None
+    return k["traffic_bytes_per_launch"], os.path.relpath(files[-1], HERE)
 
 
 def main():
@@ -192,8 +214,10 @@ def main():
         avg_ms = k["ms_total"] / k["launches"]
         bpl = k["alg_bytes"] / k["launches"]
         ach = bpl / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
+        traffic, tsrc = pmc_traffic(dom)
         roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                "traffic": round(traffic) if traffic else None, "traffic_source": tsrc,
                 "avg_launch_us": round(avg_ms * 1e3, 2), "alg_bytes_per_launch": bpl,
                 "kernel_ms_per_step": {n: round(v["ms_total"] / args.steps, 3)
                                        for n, v in sorted(kernels.items(),

@@ -1,0 +1,52 @@
+"""Per-launch HBM-side traffic of each kernel class from rocprofv3 --pmc passes.
+
+  python scripts/pmc_summary.py OUT.json DIR [DIR ...]
+
+DIR/pmc_counter_collection.csv files from separate FETCH_SIZE / WRITE_SIZE passes
+(scripts/gpu_pmc.sh).  Both counters are in KiB.  gfx950 correction (MI355X_MICROARCH.md, HBM
+section): FETCH_SIZE reports half the bytes of wide coalesced reads, so traffic =
+2 * FETCH_SIZE + WRITE_SIZE.  Kernel names map to the library's timer classes (bench.py keys).
+"""
+import collections
+import csv
+import json
+import sys
+
+CLASSES = [("k_n4_fit<0>", "n4_fit"), ("k_n4_fit<1>", "n4_den"), ("k_n4_eval", "n4_eval"),
+           ("k_n4_hist", "n4_hist"), ("k_n4_init", "n4_init"), ("k_n4_final", "n4_final"),
+           ("k_tile<true>", "classify"), ("k_gather", "gather"), ("k_snr", "snr")]
+
+
+def klass(name):
+    for key, cls in CLASSES:
+        if key in name:
+            return cls
+    return None
+
+
+def main():
+    out, dirs = sys.argv[1], sys.argv[2:]
+    tot = collections.defaultdict(lambda: collections.defaultdict(float))
+    launches = collections.defaultdict(lambda: collections.defaultdict(set))
+    for d in dirs:
+        for r in csv.DictReader(open(f"{d}/pmc_counter_collection.csv")):
+            c = klass(r["Kernel_Name"])
+            if c is None:
+                continue
+            tot[c][r["Counter_Name"]] += float(r["Counter_Value"]) * 1024.0
+            launches[c][r["Counter_Name"]].add(r["Dispatch_Id"])
+    res = {}
+    for c, v in tot.items():
+        if "FETCH_SIZE" not in v or "WRITE_SIZE" not in v:
+            continue
+        nf, nw = len(launches[c]["FETCH_SIZE"]), len(launches[c]["WRITE_SIZE"])
+        fetch, write = v["FETCH_SIZE"] / nf, v["WRITE_SIZE"] / nw
+        res[c] = {"traffic_bytes_per_launch": 2.0 * fetch + write,
+                  "fetch_size_bytes": fetch, "write_size_bytes": write, "launches": nf}
+    json.dump({"note": "traffic = 2*FETCH_SIZE + WRITE_SIZE per launch (gfx950 FETCH_SIZE halving)",
+               "kernels": res}, open(out, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
