@@ -123,6 +123,29 @@ def pmc_traffic(kernel):
     return k["traffic_bytes_per_launch"], os.path.relpath(files[-1], HERE)
 
 
+# ------------------------------------------------------------------------------------------------
+# distributed host logic (one process per GPU; tests/test_dist_gloo.py runs it on gloo)
+# ------------------------------------------------------------------------------------------------
+def shard_seed(rank):
+    """Base seed of a rank's synthetic batch: each rank owns distinct studies (weak scaling)."""
+    return 1000 * rank
+
+
+def broadcast_uid(uid, dist):
+    """Rank 0's RCCL unique id to every rank (uid is ignored on ranks > 0)."""
+    box = [uid if dist.get_rank() == 0 else None]
+    dist.broadcast_object_list(box, src=0)
+    return box[0]
+
+
+def max_over_ranks(dt, dist):
+    """The job's step time is the slowest rank's."""
+    import torch
+    t = torch.tensor([dt], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -155,13 +178,12 @@ def main():
     from vent_analysis_amd import _lib
     from vent_analysis_amd.synth import synth_batch
 
-    hp, mk = synth_batch(R, C, Z, nb, base_seed=1000 * rank, unique=16)
+    hp, mk = synth_batch(R, C, Z, nb, base_seed=shard_seed(rank), unique=16)
     Bt = _lib.Batch(R, C, Z, nb, device=local)
     Bt.upload(hp, mk)
     if world > 1:
-        uid = [_lib.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        _lib.comm_init(world, rank, uid[0], device=local)
+        uid = broadcast_uid(_lib.comm_unique_id() if rank == 0 else None, dist)
+        _lib.comm_init(world, rank, uid, device=local)
     vox = (1.5, 1.5, 10.0)
     opts = Bt.options(do_n4=not args.no_n4, vox=vox, do_cohort=True,
                       profile=not args.no_profile, n4_subbatch=args.subbatch)
@@ -194,10 +216,7 @@ def main():
         dist.barrier()
     dt = time.perf_counter() - t0
     if dist:
-        import torch
-        t = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+        dt = max_over_ranks(dt, dist)
 
     _, _, _, _, res = Bt.download(n4=False, maps=False)
     kernels = {}

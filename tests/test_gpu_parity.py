@@ -206,3 +206,101 @@ def test_class_full_pipeline_with_n4():
     assert v.metadata["VDP"] == o["VDP"]
     n4b = v.N4_bias_correction(X, M)
     assert np.array_equal(n4b, v.N4HPvent)
+
+
+# ---- ragged / degenerate shapes and full-size properties -------------------------------------
+@pytest.mark.parametrize("shape,seed", [((37, 45, 7), 11), ((12, 70, 9), 12), ((130, 20, 3), 13)])
+def test_n4_ragged_shapes_vs_oracle(shape, seed):
+    """Rows not a multiple of the 16-row segment / 32-row bitmap word, columns not a multiple of
+    the 64-column tile or the 128-column fit tile."""
+    X, M = synth_volume(*shape, seed)
+    assert M.sum() > 10
+    ref, its_ref, _ = native.n4(X, M)
+    out, its, _ = _lib.n4(X, M.astype(np.uint8))
+    assert list(its[0]) == list(its_ref)
+    assert rel(out[0], ref) < 1e-5
+
+
+def _single_slice(R, C, seed):
+    rng = np.random.default_rng(seed)
+    i, j = np.meshgrid(np.arange(R), np.arange(C), indexing="ij")
+    m = (((i - R / 2) / (0.4 * R)) ** 2 + ((j - C / 2) / (0.3 * C)) ** 2) <= 1
+    x = (np.where(m, 150.0, 0.0) * np.exp(0.3 * i / R) + rng.rayleigh(10, m.shape))
+    x[m & (rng.random(m.shape) < 0.15)] *= 0.2
+    return x.astype(np.float32)[:, :, None], m.astype(np.float64)[:, :, None]
+
+
+@pytest.mark.parametrize("case", ["37x45x7", "50x33x1", "19x130x5", "64x200x1"])
+def test_vdp_chain_ragged_vs_oracle(case):
+    R, C, Z = (int(v) for v in case.split("x"))
+    if Z == 1:
+        X, M = _single_slice(R, C, R + C)
+    else:
+        X, M = synth_volume(R, C, Z, R + C + Z)
+    vox = (1.5, 1.5, 10.0)
+    d, bo, lb, res = _lib.vdp(X, M.astype(np.uint8), vox)
+    o = O.calculate_vdp(X, M, vox, HP=X)
+    assert np.array_equal(d[0], o["defectArray"])
+    assert np.array_equal(bo[0] == 1, o["defectBorder"])
+    assert np.array_equal(lb[0], o["defectArrayLB"])
+    assert res[0].vdp == o["VDP"] and res[0].vdp_lb == o["VDP_lb"]
+    assert np.float32(res[0].mean_anchor) == o["mean_anchor"] and np.float32(res[0].p99) == o["p99"]
+    assert np.array_equal(_lib.border(M.astype(np.uint8))[0], O.calculate_border(M))
+
+
+def test_empty_mask_volume_in_batch():
+    """A study with an empty mask must not disturb its neighbours; the class raises IndexError
+    like the reference's sorted-list indexing (Vent_Analysis.py:255)."""
+    hp, mk = synth_batch(64, 64, 16, 3, base_seed=7)
+    mk[1] = 0
+    B = _lib.Batch(64, 64, 16, 3)
+    B.upload(hp, mk)
+    B.run(B.options(do_n4=True, vox=(1.5, 1.5, 10.0)))
+    n4, d, _, _, res = B.download(n4=True)
+    B.close()
+    assert res[1].n_mask == 0 and d[1].sum() == 0
+    assert np.array_equal(n4[1], hp[1])                  # B = 0: I / exp(0)
+    for b in (0, 2):
+        out, its, _ = _lib.n4(hp[b], mk[b])
+        assert np.array_equal(out[0], n4[b])
+        assert list(its[0]) == list(res[b].n4_iters[:4])
+    from vent_analysis_amd import Vent_Analysis
+    v = Vent_Analysis(xenon_array=hp[1], mask_array=np.zeros((64, 64, 16)), vox=(1.5, 1.5, 10.0))
+    with pytest.raises(IndexError):
+        v.calculate_VDP()
+
+
+def test_full_size_batch_properties():
+    """bench configuration (256 x 128x128x24, 16 distinct studies repeated): size-independent
+    properties -- counts match the maps, defects lie in the mask, repeated studies give identical
+    results wherever they sit in the batch, a second run is identical, and the cohort histogram
+    equals the numpy histogram of the p99-normalised masked N4 values."""
+    nb = 256
+    hp, mk = synth_batch(128, 128, 24, nb, base_seed=0, unique=16)
+    B = _lib.Batch(128, 128, 24, nb)
+    B.upload(hp, mk)
+    o = B.options(do_n4=True, vox=(1.5, 1.5, 10.0), do_cohort=True)
+    B.run(o)
+    n4, d, bo, lb, res = B.download(n4=True)
+    h1 = B.cohort_hist()
+    B.run(o)
+    n4b, d2, _, lb2, res2 = B.download(n4=True)
+    B.close()
+    assert np.array_equal(n4, n4b) and np.array_equal(d, d2) and np.array_equal(lb, lb2)
+    for b in range(nb):
+        r = res[b]
+        assert r.n_defect == int(d[b].sum())
+        assert r.n_lb12 == int(((lb[b] == 1) | (lb[b] == 2)).sum())
+        assert not np.any(d[b] & (mk[b] == 0))
+        assert r.n_mask == int((mk[b] > 0).sum())
+        assert all(1 <= k <= 50 for k in r.n4_iters[:4])
+        assert r.vdp == res2[b].vdp
+        if b >= 16:
+            assert np.array_equal(n4[b], n4[b % 16]) and r.vdp == res[b % 16].vdp
+    exp = np.zeros(_lib.COHORT_BINS, np.uint64)
+    for b in range(nb):
+        nv = (n4[b] / np.float32(res[b].p99)).astype(np.float32)[mk[b] > 0]
+        sel = (nv >= 0) & (nv < np.float32(1.5))
+        bi = np.minimum((nv[sel] * np.float32(_lib.COHORT_BINS / 1.5)).astype(np.int64), 1023)
+        exp += np.bincount(bi, minlength=_lib.COHORT_BINS).astype(np.uint64)
+    assert np.array_equal(h1, exp)

@@ -186,6 +186,8 @@ class Vent_Analysis:
                 n4, d, bo, lb, res = B.download(n4=True)
             finally:
                 B.close()
+            if res[0].n_mask == 0:   # sorted([])[int(0 * 0.99)] in the reference (:245, :255)
+                raise IndexError("calculate_VDP: empty mask (list index out of range)")
             self.N4HPvent = n4[0]
             self.metadata['SNR'] = self._snr_dtype(res[0].snr, hp)
         r = res[0]
