@@ -13,7 +13,7 @@ import threading
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libventhip.so")
+LIB_PATH = os.environ.get("VH_LIB_PATH") or os.path.join(HERE, "libventhip.so")   # override: A/B builds
 
 VH_OK, VH_ERR_ARG, VH_ERR_HIP, VH_ERR_NOMEM, VH_ERR_MAXRADIUS, VH_ERR_EMPTY, VH_ERR_RCCL, \
     VH_ERR_NODEV = range(8)

@@ -30,6 +30,7 @@ struct DevAxis {
     const double *isw2;   // 1 / sw2
     const double *w2;     // [n][4] w^2 (double)
     const double *w3;     // [n][4] w^3 (double)
+    const int2 *krange;   // [ncp] first / last index whose support contains control point k
     int32_t n, ncp;
 };
 struct DevLevel {
@@ -47,7 +48,8 @@ struct DevLevel {
 #define SEG_R 16    // rows per wave segment
 #define N4_CH 4096  // compact voxels per chunk (flat sweeps: 256 threads x 16)
 #define N4_VPT (N4_CH / VH_TPB)
-#define FIT_G 4     // fit voxels per thread with loads in flight together
+#define HIST_COPIES 8   // LDS histogram copies (neighbouring lanes share bins)
+#define FIT_G 8     // fit voxels per thread with loads in flight together
 #define N4_FIX 68719476736.0   // 2^36: fixed-point scale of the fit's LDS row contraction
 #define LN2 0.69314718055994530942
 #define PI_D 3.14159265358979323846
@@ -109,7 +111,7 @@ void vh_n4_prepare_tables(vh_batch *b, const vh_n4_params &prm) {
     if (b->tabs_valid && same_params(b->tab_prm, prm)) return;
     const int64_t dims[3] = {b->R, b->C, b->Z};
     std::vector<uint8_t> blob;
-    b->tab_off.assign((size_t)prm.n_levels * 3 * 6, 0);
+    b->tab_off.assign((size_t)prm.n_levels * 3 * 7, 0);
     auto push = [&](const void *p, size_t bytes) {
         size_t off = (blob.size() + 15) & ~(size_t)15;
         blob.resize(off + bytes);
@@ -130,12 +132,25 @@ void vh_n4_prepare_tables(vh_batch *b, const vh_n4_params &prm) {
                 w2[i] = w * w;
                 w3[i] = w * w * w;
             }
-            b->tab_off[(L * 3 + a) * 6 + 0] = push(t.base.data(), t.base.size() * 4);
-            b->tab_off[(L * 3 + a) * 6 + 1] = push(t.w.data(), t.w.size() * 4);
-            b->tab_off[(L * 3 + a) * 6 + 2] = push(t.sw2.data(), t.sw2.size() * 8);
-            b->tab_off[(L * 3 + a) * 6 + 3] = push(inv.data(), inv.size() * 8);
-            b->tab_off[(L * 3 + a) * 6 + 4] = push(w2.data(), w2.size() * 8);
-            b->tab_off[(L * 3 + a) * 6 + 5] = push(w3.data(), w3.size() * 8);
+            b->tab_off[(L * 3 + a) * 7 + 0] = push(t.base.data(), t.base.size() * 4);
+            b->tab_off[(L * 3 + a) * 7 + 1] = push(t.w.data(), t.w.size() * 4);
+            b->tab_off[(L * 3 + a) * 7 + 2] = push(t.sw2.data(), t.sw2.size() * 8);
+            b->tab_off[(L * 3 + a) * 7 + 3] = push(inv.data(), inv.size() * 8);
+            b->tab_off[(L * 3 + a) * 7 + 4] = push(w2.data(), w2.size() * 8);
+            b->tab_off[(L * 3 + a) * 7 + 5] = push(w3.data(), w3.size() * 8);
+            // control point k -> the index range whose 4-wide support contains k
+            std::vector<int32_t> kr(2 * (size_t)t.ncp);
+            for (int k = 0; k < t.ncp; ++k) {
+                int lo = t.n, hi = -1;
+                for (int idx = 0; idx < t.n; ++idx)
+                    if (t.base[idx] <= k && k <= t.base[idx] + 3) {
+                        lo = std::min(lo, idx);
+                        hi = std::max(hi, idx);
+                    }
+                kr[2 * k] = lo;
+                kr[2 * k + 1] = hi;
+            }
+            b->tab_off[(L * 3 + a) * 7 + 6] = push(kr.data(), kr.size() * 4);
         }
     }
     // fit tile metadata per level (64-column tiles of the (col, slice) plane)
@@ -203,12 +218,13 @@ static DevLevel dev_level(const vh_batch *b, const vh_n4_params &prm, int L) {
     const int64_t dims[3] = {b->R, b->C, b->Z};
     const uint8_t *base = (const uint8_t *)b->d_tabs;
     for (int a = 0; a < 3; ++a) {
-        lv.ax[a].base = (const int32_t *)(base + b->tab_off[(L * 3 + a) * 6 + 0]);
-        lv.ax[a].w = (const float *)(base + b->tab_off[(L * 3 + a) * 6 + 1]);
-        lv.ax[a].sw2 = (const double *)(base + b->tab_off[(L * 3 + a) * 6 + 2]);
-        lv.ax[a].isw2 = (const double *)(base + b->tab_off[(L * 3 + a) * 6 + 3]);
-        lv.ax[a].w2 = (const double *)(base + b->tab_off[(L * 3 + a) * 6 + 4]);
-        lv.ax[a].w3 = (const double *)(base + b->tab_off[(L * 3 + a) * 6 + 5]);
+        lv.ax[a].base = (const int32_t *)(base + b->tab_off[(L * 3 + a) * 7 + 0]);
+        lv.ax[a].w = (const float *)(base + b->tab_off[(L * 3 + a) * 7 + 1]);
+        lv.ax[a].sw2 = (const double *)(base + b->tab_off[(L * 3 + a) * 7 + 2]);
+        lv.ax[a].isw2 = (const double *)(base + b->tab_off[(L * 3 + a) * 7 + 3]);
+        lv.ax[a].w2 = (const double *)(base + b->tab_off[(L * 3 + a) * 7 + 4]);
+        lv.ax[a].w3 = (const double *)(base + b->tab_off[(L * 3 + a) * 7 + 5]);
+        lv.ax[a].krange = (const int2 *)(base + b->tab_off[(L * 3 + a) * 7 + 6]);
         lv.ax[a].n = (int32_t)dims[a];
         lv.ax[a].ncp = level_ncp(prm, L, a);
     }
@@ -621,11 +637,12 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_hist(const float *__restrict__ U,
                                                    const int32_t *cvol, const VolScalars *sc,
                                                    int64_t VS, int bins, const N4State *st,
                                                    uint64_t *hpart, int32_t c0) {
-    __shared__ unsigned long long H[VH_MAX_BINS];
+    __shared__ unsigned long long Hc[HIST_COPIES * VH_MAX_BINS];   // lane & 7 picks a copy
     const int32_t c = c0 + blockIdx.x;
     const int64_t b = cvol[c];
     if (!st[b].active) return;
-    for (int i = threadIdx.x; i < VH_MAX_BINS; i += VH_TPB) H[i] = 0ull;
+    for (int i = threadIdx.x; i < HIST_COPIES * VH_MAX_BINS; i += VH_TPB) Hc[i] = 0ull;
+    unsigned long long *H = Hc + (threadIdx.x & (HIST_COPIES - 1)) * VH_MAX_BINS;
     const int64_t j0 = (int64_t)(c - cp[b]) * N4_CH;
     const int64_t n = sc[b].n_mask1 - j0 < N4_CH ? sc[b].n_mask1 - j0 : N4_CH;
     const int t0 = threadIdx.x * N4_VPT;
@@ -677,7 +694,12 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_hist(const float *__restrict__ U,
         if (w1) atomicAdd(&H[cur + 1], w1);
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < bins; i += VH_TPB) hpart[(int64_t)c * VH_MAX_BINS + i] = H[i];
+    for (int i = threadIdx.x; i < bins; i += VH_TPB) {
+        unsigned long long h = 0ull;
+#pragma unroll
+        for (int q = 0; q < HIST_COPIES; ++q) h += Hc[q * VH_MAX_BINS + i];
+        hpart[(int64_t)c * VH_MAX_BINS + i] = h;
+    }
 }
 
 // 512-point radix-2 FFT in LDS, 256 threads (one butterfly each per stage); same butterfly and
@@ -807,7 +829,9 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_fit(const float *__restrict__ U,
                                                   int64_t R, int64_t C, int64_t Z, int64_t VS,
                                                   int64_t ntiles, int bins, const N4State *st,
                                                   const float *E, DevLevel lv, double inv_cz,
-                                                  int64_t slab, double *part, int64_t vol0) {
+                                                  int smax, int64_t slab, double *part,
+                                                  int64_t vol0) {
+    // dynamic LDS: Q1 [ncx][FIT_W] | slab stage [smax] | row weights [R][4] | 1/sum w^2 [R] | base [R]
     extern __shared__ __attribute__((aligned(16))) double smem[];
     __shared__ float sE[VH_MAX_BINS];
     __shared__ double sIyz[FIT_W];
@@ -835,12 +859,22 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_fit(const float *__restrict__ U,
     }
     unsigned long long *sQi = reinterpret_cast<unsigned long long *>(smem);   // [ncx][FIT_W]
     for (int e = threadIdx.x; e < ncx * FIT_W; e += VH_TPB) sQi[e] = 0ull;
+    double *sWx = smem + (size_t)ncx * FIT_W + smax;
+    double *sIx = sWx + 4 * R;
+    int *sBx = reinterpret_cast<int *>(sIx + R);
+    for (int x = threadIdx.x; x < R; x += VH_TPB) {   // per-row tables: no global loads per voxel
+        const double *wx = (MODE == 0 ? ax.w3 : ax.w2) + 4 * x;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) sWx[4 * x + c] = wx[c];
+        sIx[x] = ax.isw2[x];
+        sBx[x] = ax.base[x];
+    }
     if (MODE == 0)
         for (int i = threadIdx.x; i < bins; i += VH_TPB) sE[i] = E[b * VH_MAX_BINS + i];
     if (threadIdx.x < FIT_W && c0 + threadIdx.x < CZ) {   // per-column slice tables
-        const int64_t col = c0 + threadIdx.x;
-        const int64_t z = col % Z;
-        if (MODE == 0) sIyz[threadIdx.x] = ay.isw2[col / Z] * az.isw2[z];
+        const int col = (int)(c0 + threadIdx.x), iz = (int)Z;
+        const int z = col % iz;
+        if (MODE == 0) sIyz[threadIdx.x] = ay.isw2[col / iz] * az.isw2[z];
         sBz[threadIdx.x] = az.base[z];
         const double *wz = (MODE == 0 ? az.w3 : az.w2) + 4 * z;
 #pragma unroll
@@ -870,12 +904,12 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_fit(const float *__restrict__ U,
             if (r < 0) continue;
             const int x = row_of(r, CZ, inv_cz);
             const int l = (int)((int64_t)r - (int64_t)x * CZ - c0);
-            const int bx = ax.base[x];
-            const double *wp = (MODE == 0 ? ax.w3 : ax.w2) + 4 * x;
+            const int bx = sBx[x];
+            const double *wp = sWx + 4 * x;
             if (MODE == 0) {
                 const float u = uu[k];
                 const float rv = u - sharpen_value(u, bmin, slope, sE, bins);
-                const double q = ((double)rv * ax.isw2[x]) * sIyz[l];
+                const double q = ((double)rv * sIx[x]) * sIyz[l];
 #pragma unroll
                 for (int c = 0; c < 4; ++c)
                     atomicAdd(&sQi[(bx + c) * FIT_W + l],
@@ -900,25 +934,22 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_fit(const float *__restrict__ U,
     for (int e = threadIdx.x; e < ncx * ny * KT; e += VH_TPB) {
         const int i = e / (ny * KT), yy = (e / KT) % ny, k = klo + e % KT;
         const int y = y0 + yy;
-        const int zs = y == y0 ? m0.z : 0, ze = y == y1 ? m0.w : (int)Z - 1;
+        const int2 zr = az.krange[k];   // slices whose support covers k
+        const int zs = max(y == y0 ? m0.z : 0, zr.x), ze = min(y == y1 ? m0.w : (int)Z - 1, zr.y);
         const int lb = (int)((int64_t)y * Z - c0);   // lane of (y, z = 0)
         double acc = 0.0;
-        for (int l = lb + zs; l <= lb + ze; ++l) {
-            const int cz = k - sBz[l];
-            if (cz < 0 || cz > 3) continue;
-            acc = fma(sWz[4 * l + cz], sQ1[i * FIT_W + l], acc);
-        }
+        for (int l = lb + zs; l <= lb + ze; ++l)
+            acc = fma(sWz[4 * l + (k - sBz[l])], sQ1[i * FIT_W + l], acc);
         sS[e] = acc;
     }
     __syncthreads();
     for (int e = threadIdx.x; e < ncx * JT * KT; e += VH_TPB) {
         const int i = e / (JT * KT), j = jlo + (e / KT) % JT, kk = e % KT;
+        const int2 yr = ay.krange[j];
+        const int ys = max(y0, yr.x), ye = min(y1, yr.y);
         double acc = 0.0;
-        for (int y = y0; y <= y1; ++y) {
-            const int cy = j - ay.base[y];
-            if (cy < 0 || cy > 3) continue;
-            acc = fma(wyp[4 * y + cy], sS[(i * ny + (y - y0)) * KT + kk], acc);
-        }
+        for (int y = ys; y <= ye; ++y)
+            acc = fma(wyp[4 * y + (j - ay.base[y])], sS[(i * ny + (y - y0)) * KT + kk], acc);
         out[e] = acc;
     }
 }
@@ -1002,27 +1033,37 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_T(const double *P1, int64_t q2_ca
     const int by = lv.ax[1].base[y];
     const float4 wy = *reinterpret_cast<const float4 *>(lv.ax[1].w + 4 * y);
     const double *p1 = P1 + b * q2_cap;
-    float *t = T + b * tcap + col;
-    for (int i = 0; i < lv.ax[0].ncp; ++i) t[(int64_t)i * CZ] = (float)col_T(p1, i, ncy, Z, by, wy, z);
+    const int ncx = lv.ax[0].ncp;
+    float *t = T + b * tcap + col * ncx;   // [col][ncx]: a voxel's 4 values are one 16-B load
+    for (int i = 0; i < ncx; ++i) t[i] = (float)col_T(p1, i, ncy, Z, by, wy, z);
 }
 
 // Evaluate the new field at masked voxels: B_new, U = L0 - B_new (compact, in place), the
 // convergence partial sums of exp(B_old - B_new) - 1 (one slot per chunk, fixed-order block
 // reduction) and the U range for the next iteration.  One block per chunk, lane-consecutive voxels
-// (coalesced), 8 voxels' loads in flight per thread.
-#define EV_G 8
+// (coalesced).  Row weights come from LDS; a voxel's four column-table values T[col][bx..bx+3]
+// are one 16-byte buffer load.  Two memory round trips per thread: (ridx, L0, B) for all 16
+// voxels, then the T loads.
 __global__ void __launch_bounds__(VH_TPB) k_n4_eval(const float *__restrict__ L0, float *B,
                                                    float *U, const int32_t *__restrict__ ridx,
                                                    const int32_t *cp, const int32_t *cvol,
-                                                   const VolScalars *sc, int64_t CZ, int64_t VS,
-                                                   double inv_cz, const float *T, int64_t tcap,
-                                                   DevLevel lv, N4State *st, double *part,
-                                                   int32_t c0) {
+                                                   const VolScalars *sc, int64_t R, int64_t CZ,
+                                                   int64_t VS, double inv_cz, const float *T,
+                                                   int64_t tcap, DevLevel lv, N4State *st,
+                                                   double *part, int32_t c0) {
+    extern __shared__ __attribute__((aligned(16))) float4 sW[];   // [R] row weights, then [R] base
     __shared__ double s_sd[VH_TPB / 64], s_sd2[VH_TPB / 64];
     __shared__ uint32_t s_max[VH_TPB / 64], s_min[VH_TPB / 64];
     const int32_t c = c0 + blockIdx.x;
     const int64_t b = cvol[c];
     if (!st[b].active) return;
+    int *sB = reinterpret_cast<int *>(sW + R);
+    const DevAxis ax = lv.ax[0];
+    const int ncx = ax.ncp;
+    for (int x = threadIdx.x; x < R; x += VH_TPB) {
+        sW[x] = *reinterpret_cast<const float4 *>(ax.w + 4 * x);
+        sB[x] = ax.base[x];
+    }
     const int64_t j0 = (int64_t)(c - cp[b]) * N4_CH;
     const int n = (int)(sc[b].n_mask1 - j0 < N4_CH ? sc[b].n_mask1 - j0 : N4_CH);
     const int64_t first = sc[b].first_masked;
@@ -1030,37 +1071,48 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_eval(const float *__restrict__ L0
     float *Bb = B + b * VS + j0;
     float *Ub = U + b * VS + j0;
     const int32_t *Rb = ridx + b * VS + j0;
-    const float *Tb = T + b * tcap;
-    const DevAxis ax = lv.ax[0];
+    const __amdgpu_buffer_rsrc_t rT = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(T + b * tcap), 0, (int)(tcap * 4), 0x00020000);
+    int rr[N4_VPT];
+    float la[N4_VPT], ba[N4_VPT];
+#pragma unroll
+    for (int k = 0; k < N4_VPT; ++k) {
+        const int j = threadIdx.x + k * VH_TPB;
+        const bool ok = j < n;
+        rr[k] = ok ? Rb[j] : -1;
+        la[k] = ok ? Lb[j] : 0.0f;
+        ba[k] = ok ? Bb[j] : 0.0f;
+    }
+    __syncthreads();
     double sd = 0.0, sd2 = 0.0;
     uint32_t kmax = 0u, kmin = 0xffffffffu;
-    for (int g = 0; g < N4_VPT; g += EV_G) {
-        int rr[EV_G];
-        float la[EV_G], ba[EV_G];
 #pragma unroll
-        for (int k = 0; k < EV_G; ++k) {
-            const int j = threadIdx.x + (g + k) * VH_TPB;
-            const bool ok = j < n;
-            rr[k] = ok ? Rb[j] : -1;
-            la[k] = ok ? Lb[j] : 0.0f;
-            ba[k] = ok ? Bb[j] : 0.0f;
+    for (int h = 0; h < N4_VPT; h += 8) {
+        float4 tv[8];
+        int xs[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int r = rr[h + k];
+            const int x = r < 0 ? 0 : row_of(r, CZ, inv_cz);
+            xs[k] = x;
+            const int64_t col = (int64_t)r - (int64_t)x * CZ;
+            const uint32_t off = r < 0 ? VH_OOB : (uint32_t)((col * ncx + sB[x]) * 4);
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rT, (int)off, 0, 0);
+            tv[k] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]),
+                                __uint_as_float(v[2]), __uint_as_float(v[3]));
         }
 #pragma unroll
-        for (int k = 0; k < EV_G; ++k) {
-            if (rr[k] < 0) continue;
-            const int j = threadIdx.x + (g + k) * VH_TPB;
-            const int r = rr[k];
-            const int x = row_of(r, CZ, inv_cz);
-            const int64_t col = (int64_t)r - (int64_t)x * CZ;
-            const int bx = ax.base[x];
-            const float4 w = *reinterpret_cast<const float4 *>(ax.w + 4 * x);
-            const float *tp = Tb + (int64_t)bx * CZ + col;
-            const float t0 = tp[0], t1 = tp[CZ], t2 = tp[2 * CZ], t3 = tp[3 * CZ];
-            const float bn = ((w.x * t0 + w.y * t1) + w.z * t2) + w.w * t3;
-            const float u = la[k] - bn;
+        for (int k = 0; k < 8; ++k) {
+            const int r = rr[h + k];
+            if (r < 0) continue;
+            const int j = threadIdx.x + (h + k) * VH_TPB;
+            const float4 w = sW[xs[k]];
+            const float4 t = tv[k];
+            const float bn = ((w.x * t.x + w.y * t.y) + w.z * t.z) + w.w * t.w;
+            const float u = la[h + k] - bn;
             Bb[j] = bn;
             Ub[j] = u;
-            const double d = (double)expm1f(ba[k] - bn);   // p - 1, p = exp(B_old - B_new)
+            const double d = (double)expm1f(ba[h + k] - bn);   // p - 1, p = exp(B_old - B_new)
             sd += d;
             sd2 = fma(d, d, sd2);
             const uint32_t key = f2key(u);
@@ -1191,7 +1243,9 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
             const int64_t nft = (b->CZ + FIT_W - 1) / FIT_W;
             const dim3 fg((unsigned)nft, (unsigned)ns);
             const int ncx = lv.ax[0].ncp;
-            const size_t fit_lds = sizeof(double) * ((size_t)ncx * FIT_W + (size_t)b->fit_smax[L]);
+            const int smax = b->fit_smax[L];
+            const size_t fit_lds = sizeof(double) * ((size_t)ncx * FIT_W + (size_t)smax + 5 * (size_t)b->R) +
+                                   sizeof(int) * (size_t)b->R;
             if (fit_lds > 64 * 1024)
                 throw VhError{VH_ERR_ARG, "N4 fit: tile slab exceeds the LDS budget"};
             const int64_t nlat = (int64_t)ncx * lv.ax[1].ncp * lv.ax[2].ncp;
@@ -1201,7 +1255,7 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
                 ScopedKTimer tm(b, "n4_den", 0.0);
                 k_n4_fit<1><<<fg, VH_TPB, fit_lds, st>>>(
                     U, b->d_ridx, b->d_rowstart, b->d_sc, b->R, b->C, b->Z, b->VS, ntiles, bins,
-                    b->d_st, b->d_E, lv, inv_cz, b->lat_cap, b->d_fitpart, vol0);
+                    b->d_st, b->d_E, lv, inv_cz, smax, b->lat_cap, b->d_fitpart, vol0);
                 VH_CHECK_LAUNCH();
                 k_n4_tilesum<1><<<lg, VH_TPB, 0, st>>>(b->d_fitpart, b->lat_cap, nft, b->d_lat,
                                                        b->d_den, b->lat_cap, b->d_st, lv, vol0);
@@ -1233,7 +1287,7 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
                     ScopedKTimer tm(b, "n4_fit", 0.0);
                     k_n4_fit<0><<<fg, VH_TPB, fit_lds, st>>>(
                         U, b->d_ridx, b->d_rowstart, b->d_sc, b->R, b->C, b->Z, b->VS, ntiles, bins,
-                        b->d_st, b->d_E, lv, inv_cz, b->lat_cap, b->d_fitpart, vol0);
+                        b->d_st, b->d_E, lv, inv_cz, smax, b->lat_cap, b->d_fitpart, vol0);
                     VH_CHECK_LAUNCH();
                 }
                 {
@@ -1251,9 +1305,9 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
                 }
                 if (nch > 0) {
                     ScopedKTimer tm(b, "n4_eval", 0.0);
-                    k_n4_eval<<<(unsigned)nch, VH_TPB, 0, st>>>(
-                        b->d_L0, b->d_B, U, b->d_ridx, b->d_cp, b->d_cvol, b->d_sc, b->CZ, b->VS,
-                        inv_cz, b->d_T, b->t_cap, lv, b->d_st, b->d_cpart, ch0);
+                    k_n4_eval<<<(unsigned)nch, VH_TPB, (size_t)b->R * 20, st>>>(
+                        b->d_L0, b->d_B, U, b->d_ridx, b->d_cp, b->d_cvol, b->d_sc, b->R, b->CZ,
+                        b->VS, inv_cz, b->d_T, b->t_cap, lv, b->d_st, b->d_cpart, ch0);
                     VH_CHECK_LAUNCH();
                 }
                 const int k = (int)evs.size() - 1 - LOOK;
