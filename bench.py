@@ -158,6 +158,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="no HIP events in the timed region")
     ap.add_argument("--subbatch", type=int, default=0, help="volumes per N4 sub-batch (0: all)")
+    ap.add_argument("--conv-threshold", type=float, default=0.001,
+                    help="N4 convergence threshold (SimpleITK default 0.001; 0 = fixed 4x50 "
+                         "iterations, for kernel A/B runs at constant work)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -186,9 +189,10 @@ def main():
         _lib.comm_init(world, rank, uid, device=local)
     vox = (1.5, 1.5, 10.0)
     opts = Bt.options(do_n4=not args.no_n4, vox=vox, do_cohort=True,
-                      profile=not args.no_profile, n4_subbatch=args.subbatch)
+                      profile=not args.no_profile, n4_subbatch=args.subbatch,
+                      conv_threshold=args.conv_threshold)
     warm = Bt.options(do_n4=not args.no_n4, vox=vox, do_cohort=True, profile=False,
-                      n4_subbatch=args.subbatch)
+                      n4_subbatch=args.subbatch, conv_threshold=args.conv_threshold)
 
     def step(o):
         Bt.run(o)
@@ -240,7 +244,9 @@ def main():
                 "avg_launch_us": round(avg_ms * 1e3, 2), "alg_bytes_per_launch": bpl,
                 "kernel_ms_per_step": {n: round(v["ms_total"] / args.steps, 3)
                                        for n, v in sorted(kernels.items(),
-                                                          key=lambda kv: -kv[1]["ms_total"])}}
+                                                          key=lambda kv: -kv[1]["ms_total"])},
+                "kernel_us_per_launch": {n: round(v["ms_total"] / v["launches"] * 1e3, 2)
+                                         for n, v in kernels.items()}}
     its = np.array([list(r.n4_iters[:4]) for r in res])
     total = world * nb * args.steps
     line = {

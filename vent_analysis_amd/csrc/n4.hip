@@ -50,7 +50,8 @@ struct DevLevel {
 #define N4_VPT (N4_CH / VH_TPB)
 #define HIST_COPIES 8   // LDS histogram copies (neighbouring lanes share bins)
 #define FIT_G 8     // fit voxels per thread with loads in flight together
-#define N4_FIX 68719476736.0   // 2^36: fixed-point scale of the fit's LDS row contraction
+#define N4_FIX 4294967296.0    // 2^32: fixed-point scale of the fit's LDS row contraction
+#define N4_MAGIC 6755399441055744.0   // 1.5 * 2^52: x + MAGIC rounds x to an integer (|x| < 2^51)
 #define LN2 0.69314718055994530942
 #define PI_D 3.14159265358979323846
 
@@ -239,6 +240,9 @@ void vh_ensure_n4_workspace(vh_batch *b, const vh_n4_params &prm) {
     const int64_t lat = cx * cy * cz;
     const int64_t q2 = cx * cy * b->Z;
     if (b->V >= (int64_t)1 << 29) throw VhError{VH_ERR_ARG, "N4: volume too large (>= 2^29 voxels)"};
+    b->rsh = 1;   // compact voxel index = (row << rsh) | column
+    while (((int64_t)1 << b->rsh) < b->CZ) ++b->rsh;
+    if (b->R >= ((int64_t)1 << (31 - b->rsh))) throw VhError{VH_ERR_ARG, "N4: rows x columns too large for the packed voxel index"};
     if (b->d_L0 == nullptr) {
         b->VS = (b->V + 63) & ~(int64_t)63;   // compact-array stride: 256-byte aligned volumes
         const int64_t nch = b->nb * ((b->VS + N4_CH - 1) / N4_CH);
@@ -445,14 +449,14 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
     return v;
 }
 
-// L0 = log(I) at mask == 1 (non-positive -> 0), B = 0, U = L0, ridx = raster index (compact, volume
-// stride VS) and the first U range.  grid (ceil(tiles/4), segments, volumes), 4 tile-waves/block.
+// L0 = log(I) at mask == 1 (non-positive -> 0), B = 0, U = L0, ridx = (row << rsh) | column
+// (compact, volume stride VS) and the first U range.  grid (ceil(tiles/4), segments, volumes), 4 tile-waves/block.
 __global__ void __launch_bounds__(VH_TPB) k_n4_init(const float *__restrict__ I,
                                                    const uint32_t *__restrict__ colbits,
                                                    const int32_t *rs, const VolScalars *sc,
                                                    int64_t R, int64_t CZ, int64_t V, int64_t VS,
                                                    int64_t ntiles, float *L0, float *B, float *U,
-                                                   int32_t *ridx, N4State *st) {
+                                                   int32_t *ridx, int rsh, N4State *st) {
     const int64_t b = blockIdx.z;
     const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (tile >= ntiles) return;
@@ -472,7 +476,7 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_init(const float *__restrict__ I,
         bstore(rL, s.off[k], l);
         bstore(rB, s.off[k], 0.0f);
         bstore(rU, s.off[k], l);
-        bstore(rR, s.off[k], __int_as_float((int)r));
+        bstore(rR, s.off[k], __int_as_float(((s.x0 + k) << rsh) | (int)s.col));
         const uint32_t key = f2key(l);
         kmax = key > kmax ? key : kmax;
         if (r == first) st[b].u_first = l;
@@ -815,11 +819,12 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_emap(const uint64_t *hpart, const
 // of that sum into this kernel needs agent-scope fences, which write back / invalidate the XCD's
 // L2 on gfx950: measured 10x slower, so the sum stays a separate launch.)
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ int row_of(int r, int64_t CZ, double inv_cz) {
-    int x = (int)((double)r * inv_cz);
-    if ((int64_t)x * CZ > r) --x;
-    else if ((int64_t)(x + 1) * CZ <= r) ++x;
-    return x;
+// round(v * 2^32) as a two's-complement integer without the slow double -> int64 conversion:
+// v * 2^32 is exact, adding 1.5 * 2^52 rounds it to nearest-even (valid while |v| < 2^19; the
+// fit's terms are bounded by |w^3 q| < 2^8 for log-intensity residuals)
+__device__ __forceinline__ unsigned long long fix_round(double v) {
+    const double t = v * N4_FIX + N4_MAGIC;
+    return (unsigned long long)(__double_as_longlong(t) - __double_as_longlong(N4_MAGIC));
 }
 
 template <int MODE>
@@ -828,7 +833,7 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_fit(const float *__restrict__ U,
                                                   const int32_t *rs, const VolScalars *sc,
                                                   int64_t R, int64_t C, int64_t Z, int64_t VS,
                                                   int64_t ntiles, int bins, const N4State *st,
-                                                  const float *E, DevLevel lv, double inv_cz,
+                                                  const float *E, DevLevel lv, int rsh,
                                                   int smax, int64_t slab, double *part,
                                                   int64_t vol0) {
     // dynamic LDS: Q1 [ncx][FIT_W] | slab stage [smax] | row weights [R][4] | 1/sum w^2 [R] | base [R]
@@ -902,8 +907,8 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_fit(const float *__restrict__ U,
         for (int k = 0; k < FIT_G; ++k) {
             const int r = rr[k];
             if (r < 0) continue;
-            const int x = row_of(r, CZ, inv_cz);
-            const int l = (int)((int64_t)r - (int64_t)x * CZ - c0);
+            const int x = r >> rsh;
+            const int l = (r & ((1 << rsh) - 1)) - (int)c0;
             const int bx = sBx[x];
             const double *wp = sWx + 4 * x;
             if (MODE == 0) {
@@ -912,13 +917,11 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_fit(const float *__restrict__ U,
                 const double q = ((double)rv * sIx[x]) * sIyz[l];
 #pragma unroll
                 for (int c = 0; c < 4; ++c)
-                    atomicAdd(&sQi[(bx + c) * FIT_W + l],
-                              (unsigned long long)__double2ll_rn(wp[c] * q * N4_FIX));
+                    atomicAdd(&sQi[(bx + c) * FIT_W + l], fix_round(wp[c] * q));
             } else {
 #pragma unroll
                 for (int c = 0; c < 4; ++c)
-                    atomicAdd(&sQi[(bx + c) * FIT_W + l],
-                              (unsigned long long)__double2ll_rn(wp[c] * N4_FIX));
+                    atomicAdd(&sQi[(bx + c) * FIT_W + l], fix_round(wp[c]));
             }
         }
     }
@@ -1048,7 +1051,7 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_eval(const float *__restrict__ L0
                                                    float *U, const int32_t *__restrict__ ridx,
                                                    const int32_t *cp, const int32_t *cvol,
                                                    const VolScalars *sc, int64_t R, int64_t CZ,
-                                                   int64_t VS, double inv_cz, const float *T,
+                                                   int64_t VS, int rsh, const float *T,
                                                    int64_t tcap, DevLevel lv, N4State *st,
                                                    double *part, int32_t c0) {
     extern __shared__ __attribute__((aligned(16))) float4 sW[];   // [R] row weights, then [R] base
@@ -1066,7 +1069,8 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_eval(const float *__restrict__ L0
     }
     const int64_t j0 = (int64_t)(c - cp[b]) * N4_CH;
     const int n = (int)(sc[b].n_mask1 - j0 < N4_CH ? sc[b].n_mask1 - j0 : N4_CH);
-    const int64_t first = sc[b].first_masked;
+    const int64_t f = sc[b].first_masked;   // packed like ridx
+    const int first = f < 0 ? -1 : (int)(((f / CZ) << rsh) | (f % CZ));
     const float *Lb = L0 + b * VS + j0;
     float *Bb = B + b * VS + j0;
     float *Ub = U + b * VS + j0;
@@ -1093,9 +1097,9 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_eval(const float *__restrict__ L0
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             const int r = rr[h + k];
-            const int x = r < 0 ? 0 : row_of(r, CZ, inv_cz);
+            const int x = r < 0 ? 0 : r >> rsh;
             xs[k] = x;
-            const int64_t col = (int64_t)r - (int64_t)x * CZ;
+            const int64_t col = r & ((1 << rsh) - 1);
             const uint32_t off = r < 0 ? VH_OOB : (uint32_t)((col * ncx + sB[x]) * 4);
             const auto v = __builtin_amdgcn_raw_buffer_load_b128(rT, (int)off, 0, 0);
             tv[k] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]),
@@ -1117,7 +1121,7 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_eval(const float *__restrict__ L0
             sd2 = fma(d, d, sd2);
             const uint32_t key = f2key(u);
             kmax = key > kmax ? key : kmax;
-            if ((int64_t)r == first) st[b].u_first = u;
+            if (r == first) st[b].u_first = u;
             else kmin = key < kmin ? key : kmin;
         }
     }
@@ -1227,7 +1231,7 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
     const int64_t ntiles = b->n4_tiles;
     const int32_t ch0 = hcp[vol0], nch = hcp[vol0 + ns] - hcp[vol0];
     const dim3 cg((unsigned)((b->CZ + VH_TPB - 1) / VH_TPB), (unsigned)ns);
-    const double inv_cz = 1.0 / (double)b->CZ;
+    const int rsh = b->rsh;
     const int bins = prm.n_bins;
     const int LOOK = 3;
     float *U = b->d_U;
@@ -1255,7 +1259,7 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
                 ScopedKTimer tm(b, "n4_den", 0.0);
                 k_n4_fit<1><<<fg, VH_TPB, fit_lds, st>>>(
                     U, b->d_ridx, b->d_rowstart, b->d_sc, b->R, b->C, b->Z, b->VS, ntiles, bins,
-                    b->d_st, b->d_E, lv, inv_cz, smax, b->lat_cap, b->d_fitpart, vol0);
+                    b->d_st, b->d_E, lv, rsh, smax, b->lat_cap, b->d_fitpart, vol0);
                 VH_CHECK_LAUNCH();
                 k_n4_tilesum<1><<<lg, VH_TPB, 0, st>>>(b->d_fitpart, b->lat_cap, nft, b->d_lat,
                                                        b->d_den, b->lat_cap, b->d_st, lv, vol0);
@@ -1287,7 +1291,7 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
                     ScopedKTimer tm(b, "n4_fit", 0.0);
                     k_n4_fit<0><<<fg, VH_TPB, fit_lds, st>>>(
                         U, b->d_ridx, b->d_rowstart, b->d_sc, b->R, b->C, b->Z, b->VS, ntiles, bins,
-                        b->d_st, b->d_E, lv, inv_cz, smax, b->lat_cap, b->d_fitpart, vol0);
+                        b->d_st, b->d_E, lv, rsh, smax, b->lat_cap, b->d_fitpart, vol0);
                     VH_CHECK_LAUNCH();
                 }
                 {
@@ -1307,7 +1311,7 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
                     ScopedKTimer tm(b, "n4_eval", 0.0);
                     k_n4_eval<<<(unsigned)nch, VH_TPB, (size_t)b->R * 20, st>>>(
                         b->d_L0, b->d_B, U, b->d_ridx, b->d_cp, b->d_cvol, b->d_sc, b->R, b->CZ,
-                        b->VS, inv_cz, b->d_T, b->t_cap, lv, b->d_st, b->d_cpart, ch0);
+                        b->VS, rsh, b->d_T, b->t_cap, lv, b->d_st, b->d_cpart, ch0);
                     VH_CHECK_LAUNCH();
                 }
                 const int k = (int)evs.size() - 1 - LOOK;
@@ -1353,7 +1357,7 @@ void vh_launch_n4(vh_batch *b, const vh_n4_params &prm) {
                       (unsigned)b->nb);
         k_n4_init<<<sg, VH_TPB, 0, st>>>(b->d_hp, b->d_colbits, b->d_rowstart, b->d_sc, b->R, b->CZ,
                                          b->V, b->VS, ntiles, b->d_L0, b->d_B, b->d_U, b->d_ridx,
-                                         b->d_st);
+                                         b->rsh, b->d_st);
         VH_CHECK_LAUNCH();
         k_n4_chunks<<<1, VH_TPB, 0, st>>>(b->d_sc, b->nb, b->d_cp, b->d_cvol);
         VH_CHECK_LAUNCH();

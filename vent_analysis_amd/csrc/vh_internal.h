@@ -123,6 +123,7 @@ struct vh_batch {
     int32_t *d_rowstart = nullptr;   // [nb][tiles][R] compact offset of each (64-column tile, row)
     // compact N4 state: mask==1 voxels in tile-row order, volume stride VS
     int64_t VS = 0;
+    int rsh = 1;                     // compact voxel index = (row << rsh) | column
     float *d_U = nullptr;            // [nb][VS] U = L0 - B
     int32_t *d_ridx = nullptr;       // [nb][VS] raster index of each compact voxel
     int32_t *d_cp = nullptr;         // [nb + 1] chunk prefix (N4_CH voxels per chunk)
