@@ -100,7 +100,7 @@ static void batch_free(vh_batch *b) {
     dfree(b->d_rowany); dfree(b->d_colany); dfree(b->d_sliceany);
     dfree(b->d_sc); dfree(b->d_part); dfree(b->d_keys0); dfree(b->d_keys1); dfree(b->d_tilecnt);
     dfree(b->d_cohort);
-    dfree(b->d_L0); dfree(b->d_B); dfree(b->d_lat); dfree(b->d_E);
+    dfree(b->d_L0); dfree(b->d_lat); dfree(b->d_E);
     dfree(b->d_fitpart); dfree(b->d_rowstart); dfree(b->d_P1); dfree(b->d_num); dfree(b->d_den); dfree(b->d_T);
     dfree(b->d_U); dfree(b->d_ridx); dfree(b->d_cp); dfree(b->d_cvol); dfree(b->d_hpart); dfree(b->d_cpart); dfree(b->d_st); dfree(b->d_nactive); dfree(b->d_tabs); dfree(b->d_twiddle);
     dfree(b->d_bitmap); dfree(b->d_ci_list); dfree(b->d_ci_shell); dfree(b->d_ci_hist);

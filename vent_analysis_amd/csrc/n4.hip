@@ -247,7 +247,6 @@ void vh_ensure_n4_workspace(vh_batch *b, const vh_n4_params &prm) {
         b->VS = (b->V + 63) & ~(int64_t)63;   // compact-array stride: 256-byte aligned volumes
         const int64_t nch = b->nb * ((b->VS + N4_CH - 1) / N4_CH);
         HIP_TRY(hipMalloc(&b->d_L0, sizeof(float) * b->nb * b->VS));
-        HIP_TRY(hipMalloc(&b->d_B, sizeof(float) * b->nb * b->VS));
         HIP_TRY(hipMalloc(&b->d_U, sizeof(float) * b->nb * b->VS));
         HIP_TRY(hipMalloc(&b->d_ridx, sizeof(int32_t) * b->nb * b->VS));
         HIP_TRY(hipMalloc(&b->d_cp, sizeof(int32_t) * (b->nb + 1)));
@@ -282,7 +281,7 @@ void vh_ensure_n4_workspace(vh_batch *b, const vh_n4_params &prm) {
     }
     if (cx * b->CZ > b->t_cap) {
         if (b->d_T) HIP_TRY(hipFree(b->d_T));
-        HIP_TRY(hipMalloc(&b->d_T, sizeof(float) * b->nb * cx * b->CZ));
+        HIP_TRY(hipMalloc(&b->d_T, sizeof(float) * 2 * b->nb * cx * b->CZ));
         b->t_cap = cx * b->CZ;
     }
     if (q2 > b->q2_cap) {
@@ -349,6 +348,7 @@ __global__ void k_n4_state_init(N4State *st, int64_t nb) {
     s.umax_key = 0u;
     s.umin_key = 0xffffffffu;
     s.active = 0;
+    s.tlast = 0;
     st[b] = s;
 }
 
@@ -449,21 +449,20 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
     return v;
 }
 
-// L0 = log(I) at mask == 1 (non-positive -> 0), B = 0, U = L0, ridx = (row << rsh) | column
+// L0 = log(I) at mask == 1 (non-positive -> 0), U = L0 (B = 0), ridx = (row << rsh) | column
 // (compact, volume stride VS) and the first U range.  grid (ceil(tiles/4), segments, volumes), 4 tile-waves/block.
 __global__ void __launch_bounds__(VH_TPB) k_n4_init(const float *__restrict__ I,
                                                    const uint32_t *__restrict__ colbits,
                                                    const int32_t *rs, const VolScalars *sc,
                                                    int64_t R, int64_t CZ, int64_t V, int64_t VS,
-                                                   int64_t ntiles, float *L0, float *B, float *U,
+                                                   int64_t ntiles, float *L0, float *U,
                                                    int32_t *ridx, int rsh, N4State *st) {
     const int64_t b = blockIdx.z;
     const int tile = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (tile >= ntiles) return;
     Seg s;
     seg_begin(s, colbits, rs, b, R, CZ, ntiles, tile, blockIdx.y * SEG_R);
-    const __amdgpu_buffer_rsrc_t rL = vol_rsrc(L0 + b * VS, VS), rB = vol_rsrc(B + b * VS, VS),
-                                 rU = vol_rsrc(U + b * VS, VS),
+    const __amdgpu_buffer_rsrc_t rL = vol_rsrc(L0 + b * VS, VS), rU = vol_rsrc(U + b * VS, VS),
                                  rR = vol_rsrc((const float *)(ridx + b * VS), VS);
     const int64_t first = sc[b].first_masked;
     uint32_t kmax = 0u, kmin = 0xffffffffu;
@@ -474,7 +473,6 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_init(const float *__restrict__ I,
         const float a = I[b * V + r];
         const float l = a > 0.0f ? (float)log((double)a) : 0.0f;
         bstore(rL, s.off[k], l);
-        bstore(rB, s.off[k], 0.0f);
         bstore(rU, s.off[k], l);
         bstore(rR, s.off[k], __int_as_float(((s.x0 + k) << rsh) | (int)s.col));
         const uint32_t key = f2key(l);
@@ -586,6 +584,7 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_ctrl(N4State *st, const double *p
             s.iters = 0;
             s.conv = INFINITY;
         } else if (was_active) {
+            s.tlast ^= 1;   // the previous iteration's eval used the other T buffer as "new"
             s.conv = conv;
             if (!(conv > (double)thresh)) {
                 s.active = 0;
@@ -627,6 +626,7 @@ __global__ void __launch_bounds__(64) k_n4_level_end(N4State *st, const double *
     if (!s.active) return;
     const double conv = conv_from_parts(part, cp, b, (double)sc[b].n_mask1);
     if (threadIdx.x != 0) return;
+    s.tlast ^= 1;
     s.conv = conv;
     s.iters_level[level] = s.iters;
     s.conv_level[level] = (float)conv;
@@ -1025,7 +1025,7 @@ __device__ __forceinline__ double col_T(const double *p1, int i, int ncy, int64_
 // Per-column contraction of the lattice for the eval sweep: T[i][col] (float).
 __global__ void __launch_bounds__(VH_TPB) k_n4_T(const double *P1, int64_t q2_cap, int64_t C,
                                                 int64_t Z, DevLevel lv, const N4State *st,
-                                                float *T, int64_t tcap, int64_t vol0) {
+                                                float *T, int64_t tbuf, int64_t tcap, int64_t vol0) {
     const int64_t b = vol0 + blockIdx.y;
     if (!st[b].active) return;
     const int64_t CZ = C * Z;
@@ -1037,86 +1037,99 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_T(const double *P1, int64_t q2_ca
     const float4 wy = *reinterpret_cast<const float4 *>(lv.ax[1].w + 4 * y);
     const double *p1 = P1 + b * q2_cap;
     const int ncx = lv.ax[0].ncp;
-    float *t = T + b * tcap + col * ncx;   // [col][ncx]: a voxel's 4 values are one 16-B load
+    float *t = T + (st[b].tlast ^ 1) * tbuf + b * tcap + col * ncx;   // [col][ncx]: one 16-B load per voxel
     for (int i = 0; i < ncx; ++i) t[i] = (float)col_T(p1, i, ncy, Z, by, wy, z);
 }
 
-// Evaluate the new field at masked voxels: B_new, U = L0 - B_new (compact, in place), the
-// convergence partial sums of exp(B_old - B_new) - 1 (one slot per chunk, fixed-order block
-// reduction) and the U range for the next iteration.  One block per chunk, lane-consecutive voxels
-// (coalesced).  Row weights come from LDS; a voxel's four column-table values T[col][bx..bx+3]
-// are one 16-byte buffer load.  Two memory round trips per thread: (ridx, L0, B) for all 16
-// voxels, then the T loads.
-__global__ void __launch_bounds__(VH_TPB) k_n4_eval(const float *__restrict__ L0, float *B,
-                                                   float *U, const int32_t *__restrict__ ridx,
+// Evaluate the new field at masked voxels: B_new and U = L0 - B_new (compact), the convergence
+// partial sums of exp(B_old - B_new) - 1 (one slot per chunk, fixed-order block reduction) and the
+// U range for the next iteration.  B is never stored: B_old is re-evaluated from the previous
+// field's column tables (the other T buffer, with that field's level tables `lvo` -- the same
+// float expression the previous eval computed, so the values are identical), which trades 8 B of
+// HBM per voxel for one more 16-byte load from the L2-resident tables.  One block per chunk,
+// lane-consecutive voxels; row weights from LDS.  bo_mode 0: B_old = 0 (first iteration).
+__global__ void __launch_bounds__(VH_TPB) k_n4_eval(const float *__restrict__ L0, float *U,
+                                                   const int32_t *__restrict__ ridx,
                                                    const int32_t *cp, const int32_t *cvol,
                                                    const VolScalars *sc, int64_t R, int64_t CZ,
                                                    int64_t VS, int rsh, const float *T,
-                                                   int64_t tcap, DevLevel lv, N4State *st,
+                                                   int64_t tbuf, int64_t tcap, DevLevel lv,
+                                                   DevLevel lvo, int bo_mode, N4State *st,
                                                    double *part, int32_t c0) {
-    extern __shared__ __attribute__((aligned(16))) float4 sW[];   // [R] row weights, then [R] base
+    extern __shared__ __attribute__((aligned(16))) float4 sW[];   // [R] new, [R] old, then bases
     __shared__ double s_sd[VH_TPB / 64], s_sd2[VH_TPB / 64];
     __shared__ uint32_t s_max[VH_TPB / 64], s_min[VH_TPB / 64];
     const int32_t c = c0 + blockIdx.x;
     const int64_t b = cvol[c];
     if (!st[b].active) return;
-    int *sB = reinterpret_cast<int *>(sW + R);
-    const DevAxis ax = lv.ax[0];
-    const int ncx = ax.ncp;
+    float4 *sWo = sW + R;
+    int *sB = reinterpret_cast<int *>(sW + 2 * R);
+    int *sBo = sB + R;
+    const int ncx = lv.ax[0].ncp, ncxo = lvo.ax[0].ncp;
     for (int x = threadIdx.x; x < R; x += VH_TPB) {
-        sW[x] = *reinterpret_cast<const float4 *>(ax.w + 4 * x);
-        sB[x] = ax.base[x];
+        sW[x] = *reinterpret_cast<const float4 *>(lv.ax[0].w + 4 * x);
+        sB[x] = lv.ax[0].base[x];
+        sWo[x] = *reinterpret_cast<const float4 *>(lvo.ax[0].w + 4 * x);
+        sBo[x] = lvo.ax[0].base[x];
     }
     const int64_t j0 = (int64_t)(c - cp[b]) * N4_CH;
     const int n = (int)(sc[b].n_mask1 - j0 < N4_CH ? sc[b].n_mask1 - j0 : N4_CH);
     const int64_t f = sc[b].first_masked;   // packed like ridx
     const int first = f < 0 ? -1 : (int)(((f / CZ) << rsh) | (f % CZ));
     const float *Lb = L0 + b * VS + j0;
-    float *Bb = B + b * VS + j0;
     float *Ub = U + b * VS + j0;
     const int32_t *Rb = ridx + b * VS + j0;
-    const __amdgpu_buffer_rsrc_t rT = __builtin_amdgcn_make_buffer_rsrc(
-        (void *)(T + b * tcap), 0, (int)(tcap * 4), 0x00020000);
+    const int tl = st[b].tlast;
+    const __amdgpu_buffer_rsrc_t rTn = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(T + (tl ^ 1) * tbuf + b * tcap), 0, (int)(tcap * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t rTo = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(T + tl * tbuf + b * tcap), 0, (int)(tcap * 4), 0x00020000);
     int rr[N4_VPT];
-    float la[N4_VPT], ba[N4_VPT];
+    float la[N4_VPT];
 #pragma unroll
     for (int k = 0; k < N4_VPT; ++k) {
         const int j = threadIdx.x + k * VH_TPB;
         const bool ok = j < n;
         rr[k] = ok ? Rb[j] : -1;
         la[k] = ok ? Lb[j] : 0.0f;
-        ba[k] = ok ? Bb[j] : 0.0f;
     }
     __syncthreads();
     double sd = 0.0, sd2 = 0.0;
     uint32_t kmax = 0u, kmin = 0xffffffffu;
+    const int cmask = (1 << rsh) - 1;
 #pragma unroll
     for (int h = 0; h < N4_VPT; h += 8) {
-        float4 tv[8];
-        int xs[8];
+        float4 tn[8], to[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             const int r = rr[h + k];
             const int x = r < 0 ? 0 : r >> rsh;
-            xs[k] = x;
-            const int64_t col = r & ((1 << rsh) - 1);
-            const uint32_t off = r < 0 ? VH_OOB : (uint32_t)((col * ncx + sB[x]) * 4);
-            const auto v = __builtin_amdgcn_raw_buffer_load_b128(rT, (int)off, 0, 0);
-            tv[k] = make_float4(__uint_as_float(v[0]), __uint_as_float(v[1]),
-                                __uint_as_float(v[2]), __uint_as_float(v[3]));
+            const int64_t col = r & cmask;
+            const uint32_t on = r < 0 ? VH_OOB : (uint32_t)((col * ncx + sB[x]) * 4);
+            const uint32_t oo = (r < 0 || !bo_mode) ? VH_OOB : (uint32_t)((col * ncxo + sBo[x]) * 4);
+            const auto vn = __builtin_amdgcn_raw_buffer_load_b128(rTn, (int)on, 0, 0);
+            const auto vo = __builtin_amdgcn_raw_buffer_load_b128(rTo, (int)oo, 0, 0);
+            tn[k] = make_float4(__uint_as_float(vn[0]), __uint_as_float(vn[1]),
+                                __uint_as_float(vn[2]), __uint_as_float(vn[3]));
+            to[k] = make_float4(__uint_as_float(vo[0]), __uint_as_float(vo[1]),
+                                __uint_as_float(vo[2]), __uint_as_float(vo[3]));
         }
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             const int r = rr[h + k];
             if (r < 0) continue;
+            const int x = r >> rsh;
             const int j = threadIdx.x + (h + k) * VH_TPB;
-            const float4 w = sW[xs[k]];
-            const float4 t = tv[k];
+            const float4 w = sW[x], t = tn[k];
             const float bn = ((w.x * t.x + w.y * t.y) + w.z * t.z) + w.w * t.w;
+            float bo = 0.0f;
+            if (bo_mode) {
+                const float4 wo = sWo[x], q = to[k];
+                bo = ((wo.x * q.x + wo.y * q.y) + wo.z * q.z) + wo.w * q.w;
+            }
             const float u = la[h + k] - bn;
-            Bb[j] = bn;
             Ub[j] = u;
-            const double d = (double)expm1f(ba[h + k] - bn);   // p - 1, p = exp(B_old - B_new)
+            const double d = (double)expm1f(bo - bn);   // p - 1, p = exp(B_old - B_new)
             sd += d;
             sd2 = fma(d, d, sd2);
             const uint32_t key = f2key(u);
@@ -1304,14 +1317,17 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
                                                    b->d_st, lv, vol0);
                     VH_CHECK_LAUNCH();
                     k_n4_T<<<cg, VH_TPB, 0, st>>>(b->d_P1, b->q2_cap, b->C, b->Z, lv, b->d_st,
-                                                  b->d_T, b->t_cap, vol0);
+                                                  b->d_T, b->nb * b->t_cap, b->t_cap, vol0);
                     VH_CHECK_LAUNCH();
                 }
                 if (nch > 0) {
                     ScopedKTimer tm(b, "n4_eval", 0.0);
-                    k_n4_eval<<<(unsigned)nch, VH_TPB, (size_t)b->R * 20, st>>>(
-                        b->d_L0, b->d_B, U, b->d_ridx, b->d_cp, b->d_cvol, b->d_sc, b->R, b->CZ,
-                        b->VS, rsh, b->d_T, b->t_cap, lv, b->d_st, b->d_cpart, ch0);
+                    const DevLevel lvo = (it == 0 && L > 0) ? dev_level(b, prm, L - 1) : lv;
+                    const int bo_mode = (it == 0 && L == 0) ? 0 : 1;
+                    k_n4_eval<<<(unsigned)nch, VH_TPB, (size_t)b->R * 40, st>>>(
+                        b->d_L0, U, b->d_ridx, b->d_cp, b->d_cvol, b->d_sc, b->R, b->CZ, b->VS, rsh,
+                        b->d_T, b->nb * b->t_cap, b->t_cap, lv, lvo, bo_mode, b->d_st, b->d_cpart,
+                        ch0);
                     VH_CHECK_LAUNCH();
                 }
                 const int k = (int)evs.size() - 1 - LOOK;
@@ -1356,7 +1372,7 @@ void vh_launch_n4(vh_batch *b, const vh_n4_params &prm) {
         const dim3 sg((unsigned)((ntiles + 3) / 4), (unsigned)((b->R + SEG_R - 1) / SEG_R),
                       (unsigned)b->nb);
         k_n4_init<<<sg, VH_TPB, 0, st>>>(b->d_hp, b->d_colbits, b->d_rowstart, b->d_sc, b->R, b->CZ,
-                                         b->V, b->VS, ntiles, b->d_L0, b->d_B, b->d_U, b->d_ridx,
+                                         b->V, b->VS, ntiles, b->d_L0, b->d_U, b->d_ridx,
                                          b->rsh, b->d_st);
         VH_CHECK_LAUNCH();
         k_n4_chunks<<<1, VH_TPB, 0, st>>>(b->d_sc, b->nb, b->d_cp, b->d_cvol);

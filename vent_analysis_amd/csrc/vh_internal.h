@@ -61,7 +61,7 @@ struct N4State {
     float bin_min, bin_max, slope;
     int32_t active;          // 1 while the current level is still iterating
     int32_t iters;           // iterations executed in the current level
-    int32_t need_exact_min;  // bin-range quirk: first masked pixel is the strict minimum
+    int32_t tlast;           // T buffer (0/1) holding the column tables of the last evaluated field
     uint32_t umax_key, umin_key;  // sortable keys: max over all masked, min over all but first
     float u_first;
     double conv;
@@ -118,7 +118,7 @@ struct vh_batch {
     // cohort
     uint64_t *d_cohort = nullptr;
     // N4 workspace
-    float *d_L0 = nullptr, *d_B = nullptr, *d_lat = nullptr, *d_E = nullptr;
+    float *d_L0 = nullptr, *d_lat = nullptr, *d_E = nullptr;
     double *d_fitpart = nullptr;     // [nb][tiles][lattice] per-tile contracted fit slabs
     int32_t *d_rowstart = nullptr;   // [nb][tiles][R] compact offset of each (64-column tile, row)
     // compact N4 state: mask==1 voxels in tile-row order, volume stride VS
@@ -135,7 +135,7 @@ struct vh_batch {
     std::vector<size_t> tile_off;    // per level: offset of the fit tile metadata in d_tabs
     std::vector<size_t> jt_off;      // per level: lattice col -> tile range table in d_tabs
     double *d_P1 = nullptr, *d_num = nullptr, *d_den = nullptr;
-    float *d_T = nullptr;            // [nb][ncx][CZ] per-column lattice contraction for eval
+    float *d_T = nullptr;            // [2][nb][CZ][ncx] per-column lattice contraction (new / previous field)
     int64_t t_cap = 0;
     N4State *d_st = nullptr;
     int32_t *d_nactive = nullptr;
