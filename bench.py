@@ -158,6 +158,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="no HIP events in the timed region")
     ap.add_argument("--subbatch", type=int, default=0, help="volumes per N4 sub-batch (0: all)")
+    ap.add_argument("--morph3d", action="store_true",
+                    help="build-defined 3-D median / border (BASELINE config 5)")
     ap.add_argument("--conv-threshold", type=float, default=0.001,
                     help="N4 convergence threshold (SimpleITK default 0.001; 0 = fixed 4x50 "
                          "iterations, for kernel A/B runs at constant work)")
@@ -190,9 +192,10 @@ def main():
     vox = (1.5, 1.5, 10.0)
     opts = Bt.options(do_n4=not args.no_n4, vox=vox, do_cohort=True,
                       profile=not args.no_profile, n4_subbatch=args.subbatch,
-                      conv_threshold=args.conv_threshold)
+                      conv_threshold=args.conv_threshold, morph3d=args.morph3d)
     warm = Bt.options(do_n4=not args.no_n4, vox=vox, do_cohort=True, profile=False,
-                      n4_subbatch=args.subbatch, conv_threshold=args.conv_threshold)
+                      n4_subbatch=args.subbatch, conv_threshold=args.conv_threshold,
+                      morph3d=args.morph3d)
 
     def step(o):
         Bt.run(o)

@@ -86,7 +86,9 @@ typedef struct {
     double vox[3];           /* voxel size (mm) for the volume scalars */
     int32_t n4_subbatch;     /* volumes per N4 sub-batch (0 = whole batch); smaller sub-batches
                                 keep an iteration's working set in the 256 MiB Infinity Cache */
-    int32_t pad0;
+    int32_t morph3d;         /* build-defined 3-D morphology (BASELINE config 5): 3x3x3 majority
+                                (>= 14 of 27, zero padded) and np.gradient != 0 along all three
+                                axes, instead of the reference's per-slice medfilt2d / 2-D border */
 } vh_run_opts;
 
 #define VH_COHORT_BINS 1024

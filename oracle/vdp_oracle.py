@@ -103,6 +103,36 @@ def medfilt3x3_binary(B: np.ndarray) -> np.ndarray:
     return (cnt >= 5).astype(np.float64)
 
 
+def medfilt3d_binary(B: np.ndarray) -> np.ndarray:
+    """Build-defined 3-D morphology (BASELINE config 5): 3x3x3 median of a 0/1 volume with zero
+    padding = 1 iff at least 14 of the 27 neighbours are 1 (scipy.ndimage.median_filter(size=3,
+    mode='constant'))."""
+    b = (np.asarray(B) != 0).astype(np.int32)
+    p = np.pad(b, 1)
+    cnt = np.zeros(b.shape, np.int32)
+    R, C, Z = b.shape
+    for dr in range(3):
+        for dc in range(3):
+            for dz in range(3):
+                cnt += p[dr:dr + R, dc:dc + C, dz:dz + Z]
+    return (cnt >= 14).astype(np.float64)
+
+
+def calculate_border3d(A: np.ndarray) -> np.ndarray:
+    """Build-defined 3-D border: np.gradient != 0 along rows, cols OR slices (one-sided at the
+    edges, as calculate_border); an axis of length 1 contributes nothing.  Returns float64 0/1."""
+    A = np.asarray(A, dtype=np.float64)
+    out = calculate_border(A) != 0
+    Z = A.shape[2]
+    if Z > 1:
+        gz = np.zeros(A.shape, bool)
+        gz[:, :, 1:Z - 1] = A[:, :, 2:] != A[:, :, :Z - 2]
+        gz[:, :, 0] = A[:, :, 1] != A[:, :, 0]
+        gz[:, :, Z - 1] = A[:, :, Z - 1] != A[:, :, Z - 2]
+        out |= gz
+    return out.astype(np.float64)
+
+
 # ------------------------------------------------------------------------------------------------
 # SNR (Vent_Analysis.py:337-357)
 # ------------------------------------------------------------------------------------------------
@@ -195,8 +225,10 @@ def kmeans_1d_sorted(s: np.ndarray, k: int = 4, max_iter: int = 300):
     return counts, c, it
 
 
-def calculate_vdp(N4: np.ndarray, mask: np.ndarray, vox, thresh: float = 0.6, HP=None):
+def calculate_vdp(N4: np.ndarray, mask: np.ndarray, vox, thresh: float = 0.6, HP=None,
+                  morph3d: bool = False):
     """Vent_Analysis.calculate_VDP after N4 (Vent_Analysis.py:245-257) + build-defined k-means.
+    morph3d: build-defined 3-D median / border instead of the per-slice ones (config 5).
 
     Returns a dict with defectArray (f64 0/1), defectBorder (bool), defectArrayLB (f64 0..6),
     VDP, DefectVolume, VDP_lb, VDP_km, SNR (if HP given), mean_anchor, p99."""
@@ -205,8 +237,12 @@ def calculate_vdp(N4: np.ndarray, mask: np.ndarray, vox, thresh: float = 0.6, HP
     m = mean_f32(sig)                                                   # :246
     mn = (N4 / m).astype(F32)
     raw = (mn < F32(thresh)) * (mask != 0)                              # :249 (binary mask)
-    defect = medfilt3x3_binary(raw)                                     # :248-249
-    border = calculate_border(defect) == 1                              # :250
+    if morph3d:
+        defect = medfilt3d_binary(raw)
+        border = calculate_border3d(defect) == 1
+    else:
+        defect = medfilt3x3_binary(raw)                                 # :248-249
+        border = calculate_border(defect) == 1                          # :250
     msum = np.sum(mask)
     out = dict(defectArray=defect, defectBorder=border, mean_anchor=m)
     out["VDP"] = 100 * np.sum(defect) / msum                            # :251

@@ -100,3 +100,24 @@ def test_snr_noise_region_quirks():
     exp[:20] = False
     exp[30:] = False
     assert np.array_equal(nm, exp)
+
+
+def test_medfilt3d_matches_scipy_ndimage():
+    from scipy.ndimage import median_filter
+    rng = np.random.default_rng(3)
+    for shape in [(6, 7, 5), (20, 17, 9), (9, 9, 1)]:
+        b = (rng.random(shape) < 0.5).astype(np.float64)
+        ref = median_filter(b, size=3, mode="constant", cval=0.0)
+        assert np.array_equal(O.medfilt3d_binary(b), ref)
+
+
+def test_border3d_matches_np_gradient():
+    rng = np.random.default_rng(4)
+    for shape in [(3, 4, 2), (12, 9, 7)]:
+        a = (rng.random(shape) < 0.4).astype(np.float64)
+        g = np.gradient(a)
+        ref = ((g[0] != 0) | (g[1] != 0) | (g[2] != 0)).astype(np.float64)
+        assert np.array_equal(O.calculate_border3d(a), ref)
+    one = np.zeros((5, 5, 1))
+    one[2, 2, 0] = 1
+    assert np.array_equal(O.calculate_border3d(one), O.calculate_border(one))

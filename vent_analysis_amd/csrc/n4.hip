@@ -1098,10 +1098,10 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_eval(const float *__restrict__ L0
     uint32_t kmax = 0u, kmin = 0xffffffffu;
     const int cmask = (1 << rsh) - 1;
 #pragma unroll
-    for (int h = 0; h < N4_VPT; h += 8) {
-        float4 tn[8], to[8];
+    for (int h = 0; h < N4_VPT; h += 4) {
+        float4 tn[4], to[4];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
+        for (int k = 0; k < 4; ++k) {
             const int r = rr[h + k];
             const int x = r < 0 ? 0 : r >> rsh;
             const int64_t col = r & cmask;
@@ -1115,7 +1115,7 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_eval(const float *__restrict__ L0
                                 __uint_as_float(vo[2]), __uint_as_float(vo[3]));
         }
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
+        for (int k = 0; k < 4; ++k) {
             const int r = rr[h + k];
             if (r < 0) continue;
             const int x = r >> rsh;

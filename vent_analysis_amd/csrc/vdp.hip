@@ -392,7 +392,7 @@ __device__ __forceinline__ uint8_t lb_class(float nv) {
     return 0;
 }
 
-template <bool CLASSIFY>
+template <bool CLASSIFY, bool M3D>
 __global__ void __launch_bounds__(VH_TPB) k_tile(const float *__restrict__ n4,
                                                 const uint8_t *__restrict__ mask,
                                                 const uint8_t *__restrict__ in_bin,
@@ -409,41 +409,54 @@ __global__ void __launch_bounds__(VH_TPB) k_tile(const float *__restrict__ n4,
     const int64_t x0 = tix * CL_TX, y0 = tiy * CL_TY, z0 = bid * tz;
     const int tzn = (int)(Z - z0 < tz ? Z - z0 : tz);
     const int EX = CL_TX + 4, EY = CL_TY + 4, DX = CL_TX + 2, DY = CL_TY + 2;
-    uint8_t *raw = lds;                         // [EX][EY][tzn]
-    uint8_t *def = lds + EX * EY * tz;          // [DX][DY][tzn]
+    // M3D (build-defined 3-D morphology): slice halo of 2 (raw) / 1 (defect) as well
+    const int EZ = M3D ? tzn + 4 : tzn, DZ = M3D ? tzn + 2 : tzn;
+    const int zr = M3D ? 2 : 0, zd = M3D ? 1 : 0;
+    uint8_t *raw = lds;                                          // [EX][EY][EZ]
+    uint8_t *def = lds + EX * EY * (M3D ? tz + 4 : tz);          // [DX][DY][DZ]
     const float *p4 = CLASSIFY ? n4 + b * V : nullptr;
     const uint8_t *pm = mask + b * V;
     float m = 0.0f, p99 = 0.0f;
     if (CLASSIFY) { m = sc[b].mean_anchor; p99 = sc[b].p99; }
     if (CLASSIFY) {
-        for (int e = threadIdx.x; e < EX * EY * tzn; e += VH_TPB) {
-            const int ex = e / (EY * tzn), r = e % (EY * tzn), ey = r / tzn, ez = r % tzn;
-            const int64_t x = x0 - 2 + ex, y = y0 - 2 + ey, z = z0 + ez;
+        for (int e = threadIdx.x; e < EX * EY * EZ; e += VH_TPB) {
+            const int ex = e / (EY * EZ), r = e % (EY * EZ), ey = r / EZ, ez = r % EZ;
+            const int64_t x = x0 - 2 + ex, y = y0 - 2 + ey, z = z0 - zr + ez;
             uint8_t v = 0;
-            if (x >= 0 && x < R && y >= 0 && y < C) {
+            if (x >= 0 && x < R && y >= 0 && y < C && z >= 0 && z < Z) {
                 const int64_t i = (x * C + y) * Z + z;
                 if (pm[i]) v = (p4[i] / m) < thresh;   // IEEE f32 division, float32(thresh)
             }
             raw[e] = v;
         }
         __syncthreads();
-        for (int e = threadIdx.x; e < DX * DY * tzn; e += VH_TPB) {
-            const int dx = e / (DY * tzn), r = e % (DY * tzn), dy = r / tzn, dz = r % tzn;
+        for (int e = threadIdx.x; e < DX * DY * DZ; e += VH_TPB) {
+            const int dx = e / (DY * DZ), r = e % (DY * DZ), dy = r / DZ, dz = r % DZ;
             int cnt = 0;
+            if (M3D) {   // 3x3x3 median of a 0/1 volume, zero padded: 1 iff >= 14 of 27
 #pragma unroll
-            for (int i = 0; i < 3; ++i)
+                for (int i = 0; i < 3; ++i)
 #pragma unroll
-                for (int j = 0; j < 3; ++j) cnt += raw[((dx + i) * EY + (dy + j)) * tzn + dz];
-            def[e] = cnt >= 5;
+                    for (int j = 0; j < 3; ++j)
+#pragma unroll
+                        for (int k = 0; k < 3; ++k) cnt += raw[((dx + i) * EY + (dy + j)) * EZ + dz + k];
+                def[e] = cnt >= 14;
+            } else {     // medfilt2d 3x3 per slice (Vent_Analysis.py:249): 1 iff >= 5 of 9
+#pragma unroll
+                for (int i = 0; i < 3; ++i)
+#pragma unroll
+                    for (int j = 0; j < 3; ++j) cnt += raw[((dx + i) * EY + (dy + j)) * EZ + dz];
+                def[e] = cnt >= 5;
+            }
         }
     } else {
         // border of an arbitrary binary volume: stage it as the "defect" map directly
         const uint8_t *pin = in_bin + b * V;
-        for (int e = threadIdx.x; e < DX * DY * tzn; e += VH_TPB) {
-            const int dx = e / (DY * tzn), r = e % (DY * tzn), dy = r / tzn, dz = r % tzn;
-            const int64_t x = x0 - 1 + dx, y = y0 - 1 + dy, z = z0 + dz;
+        for (int e = threadIdx.x; e < DX * DY * DZ; e += VH_TPB) {
+            const int dx = e / (DY * DZ), r = e % (DY * DZ), dy = r / DZ, dz = r % DZ;
+            const int64_t x = x0 - 1 + dx, y = y0 - 1 + dy, z = z0 - zd + dz;
             uint8_t v = 0;
-            if (x >= 0 && x < R && y >= 0 && y < C) v = pin[(x * C + y) * Z + z];
+            if (x >= 0 && x < R && y >= 0 && y < C && z >= 0 && z < Z) v = pin[(x * C + y) * Z + z];
             def[e] = v;
         }
     }
@@ -453,19 +466,24 @@ __global__ void __launch_bounds__(VH_TPB) k_tile(const float *__restrict__ n4,
         const int ix = e / (CL_TY * tzn), r = e % (CL_TY * tzn), iy = r / tzn, iz = r % tzn;
         const int64_t x = x0 + ix, y = y0 + iy, z = z0 + iz;
         if (x >= R || y >= C) continue;
-        const int dx = ix + 1, dy = iy + 1;
-#define DEF(a, c) def[((a) * DY + (c)) * tzn + iz]
-        const uint8_t d = DEF(dx, dy);
-        bool gx, gy;
-        if (x == 0) gx = DEF(dx + 1, dy) != d;
-        else if (x == R - 1) gx = d != DEF(dx - 1, dy);
-        else gx = DEF(dx + 1, dy) != DEF(dx - 1, dy);
-        if (y == 0) gy = DEF(dx, dy + 1) != d;
-        else if (y == C - 1) gy = d != DEF(dx, dy - 1);
-        else gy = DEF(dx, dy + 1) != DEF(dx, dy - 1);
+        const int dx = ix + 1, dy = iy + 1, dz = iz + zd;
+#define DEF(a, c, e) def[((a) * DY + (c)) * DZ + (e)]
+        const uint8_t d = DEF(dx, dy, dz);
+        bool gx, gy, gz = false;   // np.gradient != 0: central inside, one-sided at the edges
+        if (x == 0) gx = DEF(dx + 1, dy, dz) != d;
+        else if (x == R - 1) gx = d != DEF(dx - 1, dy, dz);
+        else gx = DEF(dx + 1, dy, dz) != DEF(dx - 1, dy, dz);
+        if (y == 0) gy = DEF(dx, dy + 1, dz) != d;
+        else if (y == C - 1) gy = d != DEF(dx, dy - 1, dz);
+        else gy = DEF(dx, dy + 1, dz) != DEF(dx, dy - 1, dz);
+        if (M3D && Z > 1) {
+            if (z == 0) gz = DEF(dx, dy, dz + 1) != d;
+            else if (z == Z - 1) gz = d != DEF(dx, dy, dz - 1);
+            else gz = DEF(dx, dy, dz + 1) != DEF(dx, dy, dz - 1);
+        }
 #undef DEF
         const int64_t i = b * V + (x * C + y) * Z + z;
-        border[i] = gx || gy;
+        border[i] = gx || gy || gz;
         if (CLASSIFY) {
             defect[i] = d;
             n_def += d;
@@ -499,19 +517,20 @@ __global__ void k_counts_to_scalars(const unsigned long long *cnt, int64_t nb, V
     sc[b].n_lb12 = (int64_t)cnt[b * 2 + 1];
 }
 
-static void tile_geometry(const vh_batch *b, int &tz, dim3 &grid, size_t &lds) {
+static void tile_geometry(const vh_batch *b, bool m3d, int &tz, dim3 &grid, size_t &lds) {
     tz = (int)(b->Z < CL_TZMAX ? b->Z : CL_TZMAX);
     const int64_t ntx = (b->R + CL_TX - 1) / CL_TX, nty = (b->C + CL_TY - 1) / CL_TY;
     const int64_t ntz = (b->Z + tz - 1) / tz;
     grid = dim3((unsigned)(ntx * nty * ntz), (unsigned)b->nb, 1);
-    lds = (size_t)(CL_TX + 4) * (CL_TY + 4) * tz + (size_t)(CL_TX + 2) * (CL_TY + 2) * tz;
+    const int hz = m3d ? 4 : 0, dzh = m3d ? 2 : 0;
+    lds = (size_t)(CL_TX + 4) * (CL_TY + 4) * (tz + hz) + (size_t)(CL_TX + 2) * (CL_TY + 2) * (tz + dzh);
 }
 
 void vh_launch_border(vh_batch *b, const uint8_t *d_in, uint8_t *d_out) {
     int tz; dim3 grid; size_t lds;
-    tile_geometry(b, tz, grid, lds);
+    tile_geometry(b, false, tz, grid, lds);
     ScopedKTimer tm(b, "border", 2.0 * (double)b->V);
-    k_tile<false><<<grid, VH_TPB, lds, b->ctx->stream>>>(nullptr, b->d_mask, d_in, b->d_sc, 0.f,
+    k_tile<false, false><<<grid, VH_TPB, lds, b->ctx->stream>>>(nullptr, b->d_mask, d_in, b->d_sc, 0.f,
                                                          b->R, b->C, b->Z, b->V, tz, nullptr,
                                                          d_out, nullptr, nullptr);
     VH_CHECK_LAUNCH();
@@ -811,12 +830,17 @@ void vh_launch_vdp_chain(vh_batch *b, const float *d_n4, const vh_run_opts &o) {
         unsigned long long *cnt = reinterpret_cast<unsigned long long *>(b->d_tilecnt);
         HIP_TRY(hipMemsetAsync(cnt, 0, sizeof(unsigned long long) * 2 * b->nb, st));
         int tz; dim3 grid; size_t lds;
-        tile_geometry(b, tz, grid, lds);
+        tile_geometry(b, o.morph3d != 0, tz, grid, lds);
         {
             ScopedKTimer tm(b, "classify", 8.0 * (double)b->V);
-            k_tile<true><<<grid, VH_TPB, lds, st>>>(d_n4, b->d_mask, nullptr, b->d_sc, o.thresh,
-                                                    b->R, b->C, b->Z, b->V, tz, b->d_defect,
-                                                    b->d_border, b->d_lb, cnt);
+            if (o.morph3d)
+                k_tile<true, true><<<grid, VH_TPB, lds, st>>>(d_n4, b->d_mask, nullptr, b->d_sc,
+                                                              o.thresh, b->R, b->C, b->Z, b->V, tz,
+                                                              b->d_defect, b->d_border, b->d_lb, cnt);
+            else
+                k_tile<true, false><<<grid, VH_TPB, lds, st>>>(d_n4, b->d_mask, nullptr, b->d_sc,
+                                                               o.thresh, b->R, b->C, b->Z, b->V, tz,
+                                                               b->d_defect, b->d_border, b->d_lb, cnt);
             VH_CHECK_LAUNCH();
         }
         k_counts_to_scalars<<<(unsigned)((b->nb + 63) / 64), 64, 0, st>>>(cnt, b->nb, b->d_sc);
