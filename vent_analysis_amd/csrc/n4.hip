@@ -707,28 +707,49 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_hist(const float *__restrict__ U,
 }
 
 // 512-point radix-2 FFT in LDS, 256 threads (one butterfly each per stage); same butterfly and
-// twiddle indexing as oracle/n4_oracle.c fft_inplace.
+// twiddle indexing as oracle/n4_oracle.c fft_inplace.  Twiddles come from LDS; lds_fft2 runs two
+// independent transforms through the same stages (half the barriers, identical arithmetic).
+__device__ __forceinline__ void fft_bitrev(double2 *x, double2 *tmp) {
+    for (int i = threadIdx.x; i < VH_FFT_P; i += VH_TPB) tmp[i] = x[i];
+    __syncthreads();
+    for (int i = threadIdx.x; i < VH_FFT_P; i += VH_TPB) x[(int)(__brev((unsigned)i) >> (32 - 9))] = tmp[i];
+}
+
+__device__ __forceinline__ void fft_butterfly(double2 *x, double2 w, int i0, int i1) {
+    const double2 bb = x[i1];
+    const double tr = w.x * bb.x - w.y * bb.y, ti = w.x * bb.y + w.y * bb.x;
+    const double2 a = x[i0];
+    x[i0] = make_double2(a.x + tr, a.y + ti);
+    x[i1] = make_double2(a.x - tr, a.y - ti);
+}
+
 __device__ void lds_fft(double2 *x, double2 *tmp, const double2 *tw, bool inverse) {
-    const int P = VH_FFT_P;
+    fft_bitrev(x, tmp);
+    __syncthreads();
     const int t = threadIdx.x;
-    for (int i = t; i < P; i += VH_TPB) tmp[i] = x[i];
-    __syncthreads();
-    for (int i = t; i < P; i += VH_TPB) {
-        const int r = (int)(__brev((unsigned)i) >> (32 - 9));
-        x[r] = tmp[i];
-    }
-    __syncthreads();
-    for (int len = 2; len <= P; len <<= 1) {
-        const int half = len >> 1, step = P / len;
+    for (int len = 2; len <= VH_FFT_P; len <<= 1) {
+        const int half = len >> 1, step = VH_FFT_P / len;
         const int g = t / half, j = t % half;
-        const int i0 = g * len + j, i1 = i0 + half;
         double2 w = tw[j * step];
         if (inverse) w.y = -w.y;
-        const double2 bb = x[i1];
-        const double tr = w.x * bb.x - w.y * bb.y, ti = w.x * bb.y + w.y * bb.x;
-        const double2 a = x[i0];
-        x[i0] = make_double2(a.x + tr, a.y + ti);
-        x[i1] = make_double2(a.x - tr, a.y - ti);
+        fft_butterfly(x, w, g * len + j, g * len + j + half);
+        __syncthreads();
+    }
+}
+
+__device__ void lds_fft2(double2 *x, double2 *y, double2 *tx, double2 *ty, const double2 *tw,
+                         bool inverse) {
+    fft_bitrev(x, tx);
+    fft_bitrev(y, ty);
+    __syncthreads();
+    const int t = threadIdx.x;
+    for (int len = 2; len <= VH_FFT_P; len <<= 1) {
+        const int half = len >> 1, step = VH_FFT_P / len;
+        const int g = t / half, j = t % half;
+        double2 w = tw[j * step];
+        if (inverse) w.y = -w.y;
+        fft_butterfly(x, w, g * len + j, g * len + j + half);
+        fft_butterfly(y, w, g * len + j, g * len + j + half);
         __syncthreads();
     }
 }
@@ -741,18 +762,28 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_emap(const uint64_t *hpart, const
                                                    float noise, const N4State *st, float *Eout,
                                                    int64_t vol0) {
     __shared__ double2 V[VH_FFT_P], F[VH_FFT_P], U[VH_FFT_P], NUM[VH_FFT_P], DEN[VH_FFT_P],
-        TMP[VH_FFT_P];
+        TMP[VH_FFT_P], TMP2[VH_FFT_P], TW[VH_FFT_P / 2];
     const int64_t b = vol0 + blockIdx.x;
     if (!st[b].active) return;
     const int P = VH_FFT_P, off = (P - bins) / 2;
     const int t = threadIdx.x;
     const float binMin = st[b].bin_min, slope = st[b].slope;
+    for (int n = t; n < P / 2; n += VH_TPB) TW[n] = tw[n];
+    const int32_t ca = cp[b], ce = cp[b + 1];
     for (int n = t; n < P; n += VH_TPB) {
         const int h = n - off;
-        uint64_t hs = 0ull;   // chunk partials in chunk order (integer: exact)
-        if (h >= 0 && h < bins)
-            for (int32_t c = cp[b]; c < cp[b + 1]; ++c) hs += hpart[(int64_t)c * VH_MAX_BINS + h];
-        V[n] = make_double2((double)hs * (1.0 / 4294967296.0), 0.0);
+        uint64_t h0 = 0ull, h1 = 0ull, h2 = 0ull, h3 = 0ull;   // integer sums: order-free, exact
+        if (h >= 0 && h < bins) {
+            int32_t c = ca;
+            for (; c + 3 < ce; c += 4) {
+                h0 += hpart[(int64_t)c * VH_MAX_BINS + h];
+                h1 += hpart[(int64_t)(c + 1) * VH_MAX_BINS + h];
+                h2 += hpart[(int64_t)(c + 2) * VH_MAX_BINS + h];
+                h3 += hpart[(int64_t)(c + 3) * VH_MAX_BINS + h];
+            }
+            for (; c < ce; ++c) h0 += hpart[(int64_t)c * VH_MAX_BINS + h];
+        }
+        V[n] = make_double2((double)((h0 + h1) + (h2 + h3)) * (1.0 / 4294967296.0), 0.0);
         F[n] = make_double2(0.0, 0.0);
     }
     __syncthreads();
@@ -772,15 +803,14 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_emap(const uint64_t *hpart, const
         }
     }
     __syncthreads();
-    lds_fft(V, TMP, tw, false);
-    lds_fft(F, TMP, tw, false);
+    lds_fft2(V, F, TMP, TMP2, TW, false);
     for (int n = t; n < P; n += VH_TPB) {
         const double a = F[n].x, bb = F[n].y;
         const double g = a / ((a * a - (-bb) * bb) + (double)noise);
         U[n] = make_double2(V[n].x * g, V[n].y * g);
     }
     __syncthreads();
-    lds_fft(U, TMP, tw, true);
+    lds_fft(U, TMP, TW, true);
     for (int n = t; n < P; n += VH_TPB) {
         const double ur = U[n].x > 0.0 ? U[n].x : 0.0;
         U[n] = make_double2(ur, 0.0);
@@ -789,8 +819,7 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_emap(const uint64_t *hpart, const
         DEN[n] = make_double2(ur, 0.0);
     }
     __syncthreads();
-    lds_fft(NUM, TMP, tw, false);
-    lds_fft(DEN, TMP, tw, false);
+    lds_fft2(NUM, DEN, TMP, TMP2, TW, false);
     for (int n = t; n < P; n += VH_TPB) {
         const double a = F[n].x, bb = F[n].y;
         double2 x = NUM[n];
@@ -799,8 +828,7 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_emap(const uint64_t *hpart, const
         DEN[n] = make_double2(x.x * a - x.y * bb, x.x * bb + x.y * a);
     }
     __syncthreads();
-    lds_fft(NUM, TMP, tw, true);
-    lds_fft(DEN, TMP, tw, true);
+    lds_fft2(NUM, DEN, TMP, TMP2, TW, true);
     for (int n = t; n < bins; n += VH_TPB) {
         const double d = DEN[n + off].x;
         Eout[b * VH_MAX_BINS + n] = d != 0.0 ? (float)(NUM[n + off].x / d) : 0.0f;
@@ -1201,11 +1229,16 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_refine(float *lat, int64_t lat_ca
     refine_axis_dev(T2, L, 2 * n0 - 3, 2 * n1 - 3, n2, 2);
 }
 
-// Final field at every voxel and the corrected image I / exp(B).
+// Final field at every voxel and the corrected image I / exp(B).  With keys != nullptr it also
+// emits the VDP chain's sort keys of the mask == 1 voxels in compact tile-row order (coalesced:
+// a wave is one 64-column tile, a row's masked lanes are contiguous), replacing the separate
+// masked gather for volumes whose mask is binary (n_mask == n_mask1).
 __global__ void __launch_bounds__(VH_TPB) k_n4_final(const float *__restrict__ I, float *out,
                                                     int64_t R, int64_t C, int64_t Z, int64_t V,
-                                                    int64_t q2_cap, const double *P1,
-                                                    DevLevel lv) {
+                                                    int64_t q2_cap, const double *P1, DevLevel lv,
+                                                    const uint32_t *colbits, const int32_t *rs,
+                                                    int64_t ntiles, const VolScalars *sc,
+                                                    uint32_t *keys) {
     const int64_t b = blockIdx.y;
     const int64_t CZ = C * Z;
     const int64_t col = blockIdx.x * (int64_t)VH_TPB + threadIdx.x;
@@ -1216,6 +1249,10 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_final(const float *__restrict__ I
     const float4 wy = *reinterpret_cast<const float4 *>(lv.ax[1].w + 4 * y);
     const double *p1 = P1 + b * q2_cap;
     const DevAxis ax = lv.ax[0];
+    const bool emit = keys != nullptr && sc[b].n_mask == sc[b].n_mask1;   // block-uniform
+    const int64_t nw = (R + 31) >> 5;
+    const int32_t *rt = rs + (b * ntiles + col / TILE_W) * R;
+    uint32_t word = 0u;
     int wb = ax.base[0];
     double t0 = col_T(p1, wb, ncy, Z, by, wy, z), t1 = col_T(p1, wb + 1, ncy, Z, by, wy, z);
     double t2 = col_T(p1, wb + 2, ncy, Z, by, wy, z), t3 = col_T(p1, wb + 3, ncy, Z, by, wy, z);
@@ -1229,7 +1266,14 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_final(const float *__restrict__ I
         const float4 w = *reinterpret_cast<const float4 *>(ax.w + 4 * x);
         const float bn = (float)((double)w.x * t0 + (double)w.y * t1 + (double)w.z * t2 + (double)w.w * t3);
         const int64_t v = b * V + x * CZ + col;
-        out[v] = I[v] / (float)exp((double)bn);
+        const float o = I[v] / (float)exp((double)bn);
+        out[v] = o;
+        if (emit) {
+            if ((x & 31) == 0) word = colbits[(b * nw + (x >> 5)) * CZ + col];
+            const bool on = (word >> (x & 31)) & 1u;
+            const uint64_t bal = __ballot(on);
+            if (on) keys[b * V + rt[x] + lanes_below(bal)] = f2key(o);
+        }
     }
 }
 
@@ -1392,7 +1436,9 @@ void vh_launch_n4(vh_batch *b, const vh_n4_params &prm) {
         const DevLevel lv = dev_level(b, prm, prm.n_levels - 1);
         ScopedKTimer tm(b, "n4_final", 9.0 * (double)b->V);
         k_n4_final<<<cg, VH_TPB, 0, st>>>(b->d_hp, b->d_n4, b->R, b->C, b->Z, b->V, b->q2_cap,
-                                          b->d_P1, lv);
+                                          b->d_P1, lv, b->d_colbits, b->d_rowstart, ntiles,
+                                          b->d_sc, b->d_keys0);
+        b->keys_fused = true;   // the VDP chain's gather skips volumes with binary masks
         VH_CHECK_LAUNCH();
     }
 }

@@ -159,8 +159,10 @@ void vh_launch_mask_stats(vh_batch *b) {
 __global__ void __launch_bounds__(VH_TPB) k_gather(const float *__restrict__ n4,
                                                   const uint8_t *__restrict__ mask,
                                                   const int32_t *colrange, const int64_t *colstart,
-                                                  int64_t CZ, int64_t V, uint32_t *keys) {
+                                                  int64_t CZ, int64_t V, const VolScalars *sc,
+                                                  int skip_binary, uint32_t *keys) {
     const int64_t b = blockIdx.y;
+    if (skip_binary && sc[b].n_mask == sc[b].n_mask1) return;   // keys written by k_n4_final
     const int64_t col = blockIdx.x * (int64_t)VH_TPB + threadIdx.x;
     if (col >= CZ) return;
     const int32_t lo = colrange[(b * CZ + col) * 2], hi = colrange[(b * CZ + col) * 2 + 1];
@@ -379,7 +381,6 @@ __global__ void k_mean_p99(const uint32_t *__restrict__ keys, const float *chunk
 // =============================================================================================
 #define CL_TX 8
 #define CL_TY 16
-#define CL_TZMAX 32
 
 __device__ __forceinline__ uint8_t lb_class(float nv) {
     // (x<=.16)*1 + (.16<x<=.34)*2 + ... + (x>.88)*6, float32 edges; NaN -> 0
@@ -392,6 +393,11 @@ __device__ __forceinline__ uint8_t lb_class(float nv) {
     return 0;
 }
 
+// Classify / border tile: a block owns CL_TX rows x CL_TY cols x tz slices (tz <= 32, 28 with the
+// 3-D slice halo) with a 2-voxel halo in LDS.  Threads map to (slice lane = t & 31, col lane =
+// t >> 5): every phase is a loop over rows and col groups with no index division, and a wave
+// reads/writes runs of consecutive slices (contiguous bytes).
+#define CL_YL (VH_TPB / 32)   // col lanes per block
 template <bool CLASSIFY, bool M3D>
 __global__ void __launch_bounds__(VH_TPB) k_tile(const float *__restrict__ n4,
                                                 const uint8_t *__restrict__ mask,
@@ -412,89 +418,116 @@ __global__ void __launch_bounds__(VH_TPB) k_tile(const float *__restrict__ n4,
     // M3D (build-defined 3-D morphology): slice halo of 2 (raw) / 1 (defect) as well
     const int EZ = M3D ? tzn + 4 : tzn, DZ = M3D ? tzn + 2 : tzn;
     const int zr = M3D ? 2 : 0, zd = M3D ? 1 : 0;
-    uint8_t *raw = lds;                                          // [EX][EY][EZ]
-    uint8_t *def = lds + EX * EY * (M3D ? tz + 4 : tz);          // [DX][DY][DZ]
+    const int SZ = 32;                                  // LDS slice pitch
+    uint8_t *raw = lds;                                 // [EX][EY][SZ]
+    uint8_t *def = lds + EX * EY * SZ;                  // [DX][DY][SZ]
+    const int lz = threadIdx.x & 31, ly = threadIdx.x >> 5;
     const float *p4 = CLASSIFY ? n4 + b * V : nullptr;
     const uint8_t *pm = mask + b * V;
     float m = 0.0f, p99 = 0.0f;
     if (CLASSIFY) { m = sc[b].mean_anchor; p99 = sc[b].p99; }
+    uint8_t *lbc = def + DX * DY * SZ;                  // [CL_TX][CL_TY][SZ] LB class (CLASSIFY)
     if (CLASSIFY) {
-        for (int e = threadIdx.x; e < EX * EY * EZ; e += VH_TPB) {
-            const int ex = e / (EY * EZ), r = e % (EY * EZ), ey = r / EZ, ez = r % EZ;
-            const int64_t x = x0 - 2 + ex, y = y0 - 2 + ey, z = z0 - zr + ez;
-            uint8_t v = 0;
-            if (x >= 0 && x < R && y >= 0 && y < C && z >= 0 && z < Z) {
-                const int64_t i = (x * C + y) * Z + z;
-                if (pm[i]) v = (p4[i] / m) < thresh;   // IEEE f32 division, float32(thresh)
+        const int64_t z = z0 - zr + lz;
+        const bool zin = lz < EZ && z >= 0 && z < Z;
+        const bool zint = lz >= zr && lz < zr + tzn;    // slice inside the output tile
+        for (int ey = ly; ey < EY; ey += CL_YL) {
+            const int64_t y = y0 - 2 + ey;
+            const bool yin = zin && y >= 0 && y < C;
+            uint8_t mk[CL_TX + 4];
+            float nv[CL_TX + 4];
+#pragma unroll
+            for (int ex = 0; ex < CL_TX + 4; ++ex) {   // all loads of the column in flight
+                const int64_t x = x0 - 2 + ex;
+                const bool ok = yin && x >= 0 && x < R;
+                const int64_t i = ok ? (x * C + y) * Z + z : 0;
+                mk[ex] = ok ? pm[i] : 0;
+                nv[ex] = ok ? p4[i] : 0.0f;
             }
-            raw[e] = v;
+            const bool yint = ey >= 2 && ey < 2 + CL_TY && zint;
+#pragma unroll
+            for (int ex = 0; ex < CL_TX + 4; ++ex) {
+                // IEEE f32 division, float32(thresh) (Vent_Analysis.py:247-249)
+                const uint8_t v = mk[ex] ? (uint8_t)((nv[ex] / m) < thresh) : (uint8_t)0;
+                if (lz < EZ) raw[(ex * EY + ey) * SZ + lz] = v;
+                if (yint && ex >= 2 && ex < 2 + CL_TX)   // LB class of an output voxel (:255-256)
+                    lbc[((ex - 2) * CL_TY + (ey - 2)) * SZ + (lz - zr)] = mk[ex] ? lb_class(nv[ex] / p99) : 0;
+            }
         }
         __syncthreads();
-        for (int e = threadIdx.x; e < DX * DY * DZ; e += VH_TPB) {
-            const int dx = e / (DY * DZ), r = e % (DY * DZ), dy = r / DZ, dz = r % DZ;
-            int cnt = 0;
-            if (M3D) {   // 3x3x3 median of a 0/1 volume, zero padded: 1 iff >= 14 of 27
+        if (lz < DZ) {
+            for (int dx = 0; dx < DX; ++dx)
+                for (int dy = ly; dy < DY; dy += CL_YL) {
+                    int cnt = 0;
+                    if (M3D) {   // 3x3x3 median of a 0/1 volume, zero padded: 1 iff >= 14 of 27
 #pragma unroll
-                for (int i = 0; i < 3; ++i)
+                        for (int i = 0; i < 3; ++i)
 #pragma unroll
-                    for (int j = 0; j < 3; ++j)
+                            for (int j = 0; j < 3; ++j)
 #pragma unroll
-                        for (int k = 0; k < 3; ++k) cnt += raw[((dx + i) * EY + (dy + j)) * EZ + dz + k];
-                def[e] = cnt >= 14;
-            } else {     // medfilt2d 3x3 per slice (Vent_Analysis.py:249): 1 iff >= 5 of 9
+                                for (int k = 0; k < 3; ++k) cnt += raw[((dx + i) * EY + (dy + j)) * SZ + lz + k];
+                    def[(dx * DY + dy) * SZ + lz] = cnt >= 14;
+                    } else {     // medfilt2d 3x3 per slice (Vent_Analysis.py:249): >= 5 of 9
 #pragma unroll
-                for (int i = 0; i < 3; ++i)
+                        for (int i = 0; i < 3; ++i)
 #pragma unroll
-                    for (int j = 0; j < 3; ++j) cnt += raw[((dx + i) * EY + (dy + j)) * EZ + dz];
-                def[e] = cnt >= 5;
-            }
+                            for (int j = 0; j < 3; ++j) cnt += raw[((dx + i) * EY + (dy + j)) * SZ + lz];
+                        def[(dx * DY + dy) * SZ + lz] = cnt >= 5;
+                    }
+                }
         }
     } else {
         // border of an arbitrary binary volume: stage it as the "defect" map directly
         const uint8_t *pin = in_bin + b * V;
-        for (int e = threadIdx.x; e < DX * DY * DZ; e += VH_TPB) {
-            const int dx = e / (DY * DZ), r = e % (DY * DZ), dy = r / DZ, dz = r % DZ;
-            const int64_t x = x0 - 1 + dx, y = y0 - 1 + dy, z = z0 - zd + dz;
-            uint8_t v = 0;
-            if (x >= 0 && x < R && y >= 0 && y < C && z >= 0 && z < Z) v = pin[(x * C + y) * Z + z];
-            def[e] = v;
+        const int64_t z = z0 - zd + lz;
+        const bool zin = lz < DZ && z >= 0 && z < Z;
+        for (int dx = 0; dx < DX; ++dx) {
+            const int64_t x = x0 - 1 + dx;
+            for (int dy = ly; dy < DY; dy += CL_YL) {
+                const int64_t y = y0 - 1 + dy;
+                uint8_t v = 0;
+                if (zin && x >= 0 && x < R && y >= 0 && y < C) v = pin[(x * C + y) * Z + z];
+                if (lz < DZ) def[(dx * DY + dy) * SZ + lz] = v;
+            }
         }
     }
     __syncthreads();
     unsigned long long n_def = 0, n_lb12 = 0;
-    for (int e = threadIdx.x; e < CL_TX * CL_TY * tzn; e += VH_TPB) {
-        const int ix = e / (CL_TY * tzn), r = e % (CL_TY * tzn), iy = r / tzn, iz = r % tzn;
-        const int64_t x = x0 + ix, y = y0 + iy, z = z0 + iz;
-        if (x >= R || y >= C) continue;
-        const int dx = ix + 1, dy = iy + 1, dz = iz + zd;
-#define DEF(a, c, e) def[((a) * DY + (c)) * DZ + (e)]
-        const uint8_t d = DEF(dx, dy, dz);
-        bool gx, gy, gz = false;   // np.gradient != 0: central inside, one-sided at the edges
-        if (x == 0) gx = DEF(dx + 1, dy, dz) != d;
-        else if (x == R - 1) gx = d != DEF(dx - 1, dy, dz);
-        else gx = DEF(dx + 1, dy, dz) != DEF(dx - 1, dy, dz);
-        if (y == 0) gy = DEF(dx, dy + 1, dz) != d;
-        else if (y == C - 1) gy = d != DEF(dx, dy - 1, dz);
-        else gy = DEF(dx, dy + 1, dz) != DEF(dx, dy - 1, dz);
-        if (M3D && Z > 1) {
-            if (z == 0) gz = DEF(dx, dy, dz + 1) != d;
-            else if (z == Z - 1) gz = d != DEF(dx, dy, dz - 1);
-            else gz = DEF(dx, dy, dz + 1) != DEF(dx, dy, dz - 1);
-        }
+    if (lz < tzn) {
+        const int64_t z = z0 + lz;
+        const int dz = lz + zd;
+        for (int ix = 0; ix < CL_TX; ++ix) {
+            const int64_t x = x0 + ix;
+            if (x >= R) break;
+            for (int iy = ly; iy < CL_TY; iy += CL_YL) {
+                const int64_t y = y0 + iy;
+                if (y >= C) break;
+                const int dx = ix + 1, dy = iy + 1;
+#define DEF(a, c, e) def[((a) * DY + (c)) * SZ + (e)]
+                const uint8_t d = DEF(dx, dy, dz);
+                bool gx, gy, gz = false;   // np.gradient != 0: central inside, one-sided at edges
+                if (x == 0) gx = DEF(dx + 1, dy, dz) != d;
+                else if (x == R - 1) gx = d != DEF(dx - 1, dy, dz);
+                else gx = DEF(dx + 1, dy, dz) != DEF(dx - 1, dy, dz);
+                if (y == 0) gy = DEF(dx, dy + 1, dz) != d;
+                else if (y == C - 1) gy = d != DEF(dx, dy - 1, dz);
+                else gy = DEF(dx, dy + 1, dz) != DEF(dx, dy - 1, dz);
+                if (M3D && Z > 1) {
+                    if (z == 0) gz = DEF(dx, dy, dz + 1) != d;
+                    else if (z == Z - 1) gz = d != DEF(dx, dy, dz - 1);
+                    else gz = DEF(dx, dy, dz + 1) != DEF(dx, dy, dz - 1);
+                }
 #undef DEF
-        const int64_t i = b * V + (x * C + y) * Z + z;
-        border[i] = gx || gy || gz;
-        if (CLASSIFY) {
-            defect[i] = d;
-            n_def += d;
-            uint8_t cls = 0;
-            const uint8_t mk = pm[(x * C + y) * Z + z];
-            if (mk) {
-                const float nv = p4[(x * C + y) * Z + z] / p99;
-                cls = lb_class(nv);
+                const int64_t i = b * V + (x * C + y) * Z + z;
+                border[i] = gx || gy || gz;
+                if (CLASSIFY) {
+                    defect[i] = d;
+                    n_def += d;
+                    const uint8_t cls = lbc[(ix * CL_TY + iy) * SZ + lz];
+                    lb[i] = cls;
+                    n_lb12 += (cls == 1 || cls == 2);
+                }
             }
-            lb[i] = cls;
-            n_lb12 += (cls == 1 || cls == 2);
         }
     }
     if (CLASSIFY) {
@@ -518,12 +551,13 @@ __global__ void k_counts_to_scalars(const unsigned long long *cnt, int64_t nb, V
 }
 
 static void tile_geometry(const vh_batch *b, bool m3d, int &tz, dim3 &grid, size_t &lds) {
-    tz = (int)(b->Z < CL_TZMAX ? b->Z : CL_TZMAX);
+    const int tzmax = m3d ? 28 : 32;   // slice tile + halo <= 32 slice lanes
+    tz = (int)(b->Z < tzmax ? b->Z : tzmax);
     const int64_t ntx = (b->R + CL_TX - 1) / CL_TX, nty = (b->C + CL_TY - 1) / CL_TY;
     const int64_t ntz = (b->Z + tz - 1) / tz;
     grid = dim3((unsigned)(ntx * nty * ntz), (unsigned)b->nb, 1);
-    const int hz = m3d ? 4 : 0, dzh = m3d ? 2 : 0;
-    lds = (size_t)(CL_TX + 4) * (CL_TY + 4) * (tz + hz) + (size_t)(CL_TX + 2) * (CL_TY + 2) * (tz + dzh);
+    lds = ((size_t)(CL_TX + 4) * (CL_TY + 4) + (size_t)(CL_TX + 2) * (CL_TY + 2) +
+           (size_t)CL_TX * CL_TY) * 32;
 }
 
 void vh_launch_border(vh_batch *b, const uint8_t *d_in, uint8_t *d_out) {
@@ -797,7 +831,8 @@ void vh_launch_vdp_chain(vh_batch *b, const float *d_n4, const vh_run_opts &o) {
     {
         ScopedKTimer tm(b, "gather", 5.0 * (double)b->V);
         k_gather<<<col_grid(b), VH_TPB, 0, st>>>(d_n4, b->d_mask, b->d_colrange, b->d_colstart,
-                                                 CZ, b->V, b->d_keys0);
+                                                 CZ, b->V, b->d_sc,
+                                                 (o.do_n4 && b->keys_fused) ? 1 : 0, b->d_keys0);
         VH_CHECK_LAUNCH();
     }
     {

@@ -124,6 +124,7 @@ struct vh_batch {
     // compact N4 state: mask==1 voxels in tile-row order, volume stride VS
     int64_t VS = 0;
     int rsh = 1;                     // compact voxel index = (row << rsh) | column
+    bool keys_fused = false;         // k_n4_final wrote the sort keys of binary-mask volumes
     float *d_U = nullptr;            // [nb][VS] U = L0 - B
     int32_t *d_ridx = nullptr;       // [nb][VS] raster index of each compact voxel
     int32_t *d_cp = nullptr;         // [nb + 1] chunk prefix (N4_CH voxels per chunk)
