@@ -91,6 +91,8 @@ def algorithmic_bytes(name, hp, mk, res, R, C, Z):
         return float(np.sum(iters * 8.0 * vm))
     if name == "n4_hist":        # read U
         return float(np.sum(iters * 4.0 * vm))
+    if name == "n4_study":       # per iteration: hist reads U, fit reads U, eval reads L0 + writes U
+        return float(np.sum(iters * 16.0 * vm))
     if name == "n4_den":         # read ridx, once per level
         return float(np.sum(levels * 4.0 * vm))
     if name == "n4_init":        # read I at masked voxels, write L0, B, U, ridx
@@ -158,6 +160,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true", help="no HIP events in the timed region")
     ap.add_argument("--subbatch", type=int, default=0, help="volumes per N4 sub-batch (0: all)")
+    ap.add_argument("--n4-mode", default="auto", choices=["auto", "sweep", "study"],
+                    help="N4 driver: per-iteration sweeps or one workgroup per study")
     ap.add_argument("--morph3d", action="store_true",
                     help="build-defined 3-D median / border (BASELINE config 5)")
     ap.add_argument("--conv-threshold", type=float, default=0.001,
@@ -192,10 +196,11 @@ def main():
     vox = (1.5, 1.5, 10.0)
     opts = Bt.options(do_n4=not args.no_n4, vox=vox, do_cohort=True,
                       profile=not args.no_profile, n4_subbatch=args.subbatch,
-                      conv_threshold=args.conv_threshold, morph3d=args.morph3d)
+                      conv_threshold=args.conv_threshold, morph3d=args.morph3d,
+                      n4_mode=args.n4_mode)
     warm = Bt.options(do_n4=not args.no_n4, vox=vox, do_cohort=True, profile=False,
                       n4_subbatch=args.subbatch, conv_threshold=args.conv_threshold,
-                      morph3d=args.morph3d)
+                      morph3d=args.morph3d, n4_mode=args.n4_mode)
 
     def step(o):
         Bt.run(o)

@@ -89,6 +89,9 @@ typedef struct {
     int32_t morph3d;         /* build-defined 3-D morphology (BASELINE config 5): 3x3x3 majority
                                 (>= 14 of 27, zero padded) and np.gradient != 0 along all three
                                 axes, instead of the reference's per-slice medfilt2d / 2-D border */
+    int32_t n4_mode;         /* N4 driver: 0 auto, 1 per-iteration sweeps over the batch (any size),
+                                2 volume-resident (one workgroup per study, the whole iteration
+                                loop in one launch; studies whose N4 state fits in LDS) */
 } vh_run_opts;
 
 #define VH_COHORT_BINS 1024

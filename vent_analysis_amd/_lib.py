@@ -41,7 +41,7 @@ class RunOpts(ct.Structure):
     _fields_ = [("do_n4", ct.c_int32), ("n4", N4Params), ("thresh", ct.c_float),
                 ("do_snr", ct.c_int32), ("do_kmeans", ct.c_int32), ("do_cohort", ct.c_int32),
                 ("profile", ct.c_int32), ("vox", ct.c_double * 3), ("n4_subbatch", ct.c_int32),
-                ("morph3d", ct.c_int32)]
+                ("morph3d", ct.c_int32), ("n4_mode", ct.c_int32)]
 
 
 class VentHipError(RuntimeError):
@@ -298,7 +298,7 @@ class Batch:
     @staticmethod
     def options(do_n4=True, thresh=0.6, do_snr=True, do_kmeans=True, do_cohort=False,
                 profile=False, vox=(1.0, 1.0, 1.0), n4_subbatch=0, morph3d=False,
-                **n4kw) -> RunOpts:
+                n4_mode=0, **n4kw) -> RunOpts:
         o = RunOpts()
         lib().vh_default_run_opts(ct.byref(o))
         o.do_n4 = int(bool(do_n4))
@@ -312,6 +312,7 @@ class Batch:
             o.vox[i] = float(vox[i])
         o.n4_subbatch = int(n4_subbatch)
         o.morph3d = int(bool(morph3d))
+        o.n4_mode = {"auto": 0, "sweep": 1, "study": 2}.get(n4_mode, n4_mode)
         return o
 
     def run(self, opts: RunOpts):

@@ -101,8 +101,8 @@ static void batch_free(vh_batch *b) {
     dfree(b->d_sc); dfree(b->d_part); dfree(b->d_keys0); dfree(b->d_keys1); dfree(b->d_tilecnt);
     dfree(b->d_cohort);
     dfree(b->d_L0); dfree(b->d_lat); dfree(b->d_E);
-    dfree(b->d_fitpart); dfree(b->d_rowstart); dfree(b->d_P1); dfree(b->d_num); dfree(b->d_den); dfree(b->d_T);
-    dfree(b->d_U); dfree(b->d_ridx); dfree(b->d_cp); dfree(b->d_cvol); dfree(b->d_hpart); dfree(b->d_cpart); dfree(b->d_st); dfree(b->d_nactive); dfree(b->d_tabs); dfree(b->d_twiddle);
+    dfree(b->d_fitpart); dfree(b->d_rowstart); dfree(b->d_rowmask); dfree(b->d_P1); dfree(b->d_num); dfree(b->d_den); dfree(b->d_T);
+    dfree(b->d_U); dfree(b->d_ridx); dfree(b->d_cp); dfree(b->d_cvol); dfree(b->d_hpart); dfree(b->d_cpart); dfree(b->d_st); dfree(b->d_nactive); dfree(b->d_tabs); dfree(b->d_twiddle); dfree(b->d_study_lv);
     dfree(b->d_bitmap); dfree(b->d_ci_list); dfree(b->d_ci_shell); dfree(b->d_ci_hist);
     delete b;
 }
@@ -163,6 +163,7 @@ static void batch_run(vh_batch *b, const vh_run_opts &o, int n4_src) {
     b->profile = o.profile != 0;
     b->opts = o;
     b->n4_subbatch = o.n4_subbatch;
+    b->n4_mode = o.n4_mode;
     if (o.do_n4) {
         if (o.n4.n_levels < 1 || o.n4.n_levels > VH_MAX_LEVELS || o.n4.spline_order != 3 ||
             o.n4.n_bins < 2 || o.n4.n_bins > VH_MAX_BINS || o.n4.ncp[0] < 4 || o.n4.ncp[1] < 4 ||
@@ -520,7 +521,7 @@ int vh_batch_cohort_hist(vh_batch *b, uint64_t *hist) {
 
 const char *vh_batch_kernel_names(void) {
     return "mask_stats;gather;sort;classify;cohort;kmeans;snr;border;n4_init;n4_den;n4_hist;"
-           "n4_fit;n4_contract;n4_eval;n4_final;ci_walk";
+           "n4_fit;n4_contract;n4_eval;n4_final;n4_study;ci_walk";
 }
 
 int vh_batch_reset_timers(vh_batch *b) {

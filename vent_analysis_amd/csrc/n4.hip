@@ -21,28 +21,8 @@
 #include <climits>
 #include <cstring>
 
-#include "vh_internal.h"
+#include "n4_shared.h"
 
-struct DevAxis {
-    const int32_t *base;
-    const float *w;
-    const double *sw2;
-    const double *isw2;   // 1 / sw2
-    const double *w2;     // [n][4] w^2 (double)
-    const double *w3;     // [n][4] w^3 (double)
-    const int2 *krange;   // [ncp] first / last index whose support contains control point k
-    int32_t n, ncp;
-};
-struct DevLevel {
-    DevAxis ax[3];
-    // per 64-column fit tile: {y0, y1, z0, z1} (first/last column's col and slice), then
-    // {jlo, JT, klo, KT} (lattice cols / slices the tile's slab covers)
-    const int4 *tiles;
-    const int2 *jt;   // per lattice col j: first / last tile whose slab covers j
-};
-
-
-#define TILE_W 64   // columns per compact tile (one wave)
 #define FIT_W 128   // columns per fit block (FIT_W / TILE_W compact tiles, contiguous in compact order)
 #define FIT_TPT (FIT_W / TILE_W)
 #define SEG_R 16    // rows per wave segment
@@ -50,10 +30,6 @@ struct DevLevel {
 #define N4_VPT (N4_CH / VH_TPB)
 #define HIST_COPIES 8   // LDS histogram copies (neighbouring lanes share bins)
 #define FIT_G 8     // fit voxels per thread with loads in flight together
-#define N4_FIX 4294967296.0    // 2^32: fixed-point scale of the fit's LDS row contraction
-#define N4_MAGIC 6755399441055744.0   // 1.5 * 2^52: x + MAGIC rounds x to an integer (|x| < 2^51)
-#define LN2 0.69314718055994530942
-#define PI_D 3.14159265358979323846
 
 // ---------------------------------------------------------------------------------------------
 // host: per-level axis tables (identical expressions to oracle/n4_oracle.c axis_tables)
@@ -102,7 +78,7 @@ static bool same_params(const vh_n4_params &a, const vh_n4_params &b) {
     return true;
 }
 
-static int level_ncp(const vh_n4_params &p, int level, int axis) {
+int vh_level_ncp(const vh_n4_params &p, int level, int axis) {
     int n = p.ncp[axis];
     for (int l = 0; l < level; ++l) n = 2 * n - 3;
     return n;
@@ -121,11 +97,11 @@ void vh_n4_prepare_tables(vh_batch *b, const vh_n4_params &prm) {
     };
     for (int L = 0; L < prm.n_levels; ++L) {
         int ms = 0;
-        for (int a = 0; a < 3; ++a) ms = std::max(ms, level_ncp(prm, L, a));
+        for (int a = 0; a < 3; ++a) ms = std::max(ms, vh_level_ncp(prm, L, a));
         const float eps = vh_bspline_eps(ms - 3);
         for (int a = 0; a < 3; ++a) {
             AxisTab t;
-            vh_axis_tables((int)dims[a], level_ncp(prm, L, a), eps, t);
+            vh_axis_tables((int)dims[a], vh_level_ncp(prm, L, a), eps, t);
             std::vector<double> inv(t.sw2.size()), w2(t.w.size()), w3(t.w.size());
             for (size_t i = 0; i < inv.size(); ++i) inv[i] = 1.0 / t.sw2[i];
             for (size_t i = 0; i < w2.size(); ++i) {
@@ -160,11 +136,11 @@ void vh_n4_prepare_tables(vh_batch *b, const vh_n4_params &prm) {
     b->jt_off.assign((size_t)prm.n_levels, 0);
     b->fit_smax.assign((size_t)prm.n_levels, 0);
     for (int L = 0; L < prm.n_levels; ++L) {
-        const float eps = vh_bspline_eps(std::max({level_ncp(prm, L, 0), level_ncp(prm, L, 1),
-                                                   level_ncp(prm, L, 2)}) - 3);
+        const float eps = vh_bspline_eps(std::max({vh_level_ncp(prm, L, 0), vh_level_ncp(prm, L, 1),
+                                                   vh_level_ncp(prm, L, 2)}) - 3);
         AxisTab ty, tz;
-        vh_axis_tables((int)b->C, level_ncp(prm, L, 1), eps, ty);
-        vh_axis_tables((int)b->Z, level_ncp(prm, L, 2), eps, tz);
+        vh_axis_tables((int)b->C, vh_level_ncp(prm, L, 1), eps, ty);
+        vh_axis_tables((int)b->Z, vh_level_ncp(prm, L, 2), eps, tz);
         std::vector<int32_t> meta(8 * (size_t)ntiles);
         int smax = 0;
         for (int64_t t = 0; t < ntiles; ++t) {
@@ -176,10 +152,10 @@ void vh_n4_prepare_tables(vh_batch *b, const vh_n4_params &prm) {
             const int klo = tz.base[zlo], KT = tz.base[zhi] + 4 - klo;
             const int32_t m[8] = {y0, y1, z0, z1, jlo, JT, klo, KT};
             std::memcpy(&meta[8 * t], m, sizeof(m));
-            smax = std::max(smax, level_ncp(prm, L, 0) * (y1 - y0 + 1) * KT);
+            smax = std::max(smax, vh_level_ncp(prm, L, 0) * (y1 - y0 + 1) * KT);
         }
         // lattice col j -> the contiguous range of tiles whose slab covers it
-        const int ncy = level_ncp(prm, L, 1);
+        const int ncy = vh_level_ncp(prm, L, 1);
         std::vector<int32_t> jt(2 * (size_t)ncy);
         for (int j = 0; j < ncy; ++j) {
             int lo = (int)ntiles, hi = -1;
@@ -214,7 +190,7 @@ void vh_n4_prepare_tables(vh_batch *b, const vh_n4_params &prm) {
     b->tabs_valid = true;
 }
 
-static DevLevel dev_level(const vh_batch *b, const vh_n4_params &prm, int L) {
+DevLevel vh_dev_level(const vh_batch *b, const vh_n4_params &prm, int L) {
     DevLevel lv;
     const int64_t dims[3] = {b->R, b->C, b->Z};
     const uint8_t *base = (const uint8_t *)b->d_tabs;
@@ -227,7 +203,7 @@ static DevLevel dev_level(const vh_batch *b, const vh_n4_params &prm, int L) {
         lv.ax[a].w3 = (const double *)(base + b->tab_off[(L * 3 + a) * 7 + 5]);
         lv.ax[a].krange = (const int2 *)(base + b->tab_off[(L * 3 + a) * 7 + 6]);
         lv.ax[a].n = (int32_t)dims[a];
-        lv.ax[a].ncp = level_ncp(prm, L, a);
+        lv.ax[a].ncp = vh_level_ncp(prm, L, a);
     }
     lv.tiles = (const int4 *)(base + b->tile_off[L]);
     lv.jt = (const int2 *)(base + b->jt_off[L]);
@@ -236,7 +212,7 @@ static DevLevel dev_level(const vh_batch *b, const vh_n4_params &prm, int L) {
 
 void vh_ensure_n4_workspace(vh_batch *b, const vh_n4_params &prm) {
     const int L = prm.n_levels - 1;
-    const int64_t cx = level_ncp(prm, L, 0), cy = level_ncp(prm, L, 1), cz = level_ncp(prm, L, 2);
+    const int64_t cx = vh_level_ncp(prm, L, 0), cy = vh_level_ncp(prm, L, 1), cz = vh_level_ncp(prm, L, 2);
     const int64_t lat = cx * cy * cz;
     const int64_t q2 = cx * cy * b->Z;
     if (b->V >= (int64_t)1 << 29) throw VhError{VH_ERR_ARG, "N4: volume too large (>= 2^29 voxels)"};
@@ -270,7 +246,9 @@ void vh_ensure_n4_workspace(vh_batch *b, const vh_n4_params &prm) {
     const int64_t ntiles = (b->CZ + TILE_W - 1) / TILE_W;
     if (b->d_rowstart == nullptr || b->n4_tiles != ntiles) {
         if (b->d_rowstart) HIP_TRY(hipFree(b->d_rowstart));
+        if (b->d_rowmask) HIP_TRY(hipFree(b->d_rowmask));
         HIP_TRY(hipMalloc(&b->d_rowstart, sizeof(int32_t) * b->nb * ntiles * b->R));
+        HIP_TRY(hipMalloc(&b->d_rowmask, sizeof(uint64_t) * b->nb * ntiles * b->R));
         b->n4_tiles = ntiles;
     }
     const int64_t fp = ((b->CZ + FIT_W - 1) / FIT_W) * lat;   // per-volume fit tile slabs
@@ -295,13 +273,6 @@ void vh_ensure_n4_workspace(vh_batch *b, const vh_n4_params &prm) {
 // ---------------------------------------------------------------------------------------------
 // device helpers
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ float sharpen_value(float u, float bmin, float slope, const float *E,
-                                               int bins) {
-    const float cidx = (u - bmin) / slope;
-    const int idx = (cidx >= 0.0f && cidx < (float)bins) ? (int)floorf(cidx) : bins;
-    if (idx < bins - 1) return E[idx] + (E[idx + 1] - E[idx]) * (cidx - (float)idx);
-    return E[bins - 1];
-}
 
 template <typename T>
 __device__ __forceinline__ T block_sum_fixed(T v, T *s_red) {
@@ -359,7 +330,6 @@ __global__ void k_n4_state_init(N4State *st, int64_t nb) {
 // slot is rs + mbcnt(ballot(its bit)).  A wave processes one tile x 16-row segment: 16 coalesced
 // loads per array in flight, only masked bytes move, one memory round trip per wave.
 // ---------------------------------------------------------------------------------------------
-#define VH_OOB 0x80000000u
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t vol_rsrc(const float *base, int64_t V) {
     return __builtin_amdgcn_make_buffer_rsrc((void *)base, 0, (int)(V * 4), 0x00020000);
@@ -369,9 +339,6 @@ __device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, uint32_t voff) 
 }
 __device__ __forceinline__ void bstore(__amdgpu_buffer_rsrc_t r, uint32_t voff, float v) {
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)voff, 0, 0);
-}
-__device__ __forceinline__ int lanes_below(uint64_t m) {
-    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
 struct Seg {
@@ -402,19 +369,25 @@ __device__ __forceinline__ void seg_begin(Seg &s, const uint32_t *colbits, const
     }
 }
 
-// per (volume, tile, row): number of mask==1 lanes (pass 1 of the compact offsets)
+// per (volume, tile, row): number of mask==1 lanes (pass 1 of the compact offsets) and the lane
+// mask itself (the volume-resident driver walks tile rows from it)
 __global__ void __launch_bounds__(64) k_n4_rowcount(const uint32_t *colbits, int64_t R,
-                                                   int64_t CZ, int64_t ntiles, int32_t *rs) {
+                                                   int64_t CZ, int64_t ntiles, int32_t *rs,
+                                                   uint64_t *rowmask) {
     const int64_t b = blockIdx.y;
     const int tile = blockIdx.x;
     const int64_t col = (int64_t)tile * TILE_W + threadIdx.x;
     const int64_t nw = (R + 31) >> 5;
     int32_t *out = rs + (b * ntiles + tile) * R;
+    uint64_t *rm = rowmask + (b * ntiles + tile) * R;
     for (int64_t w = 0; w < nw; ++w) {
         const uint32_t bits = col < CZ ? colbits[(b * nw + w) * CZ + col] : 0u;
         for (int k = 0; k < 32 && w * 32 + k < R; ++k) {
             const uint64_t bal = __ballot((bits >> k) & 1u);
-            if (threadIdx.x == 0) out[w * 32 + k] = __popcll(bal);
+            if (threadIdx.x == 0) {
+                out[w * 32 + k] = __popcll(bal);
+                rm[w * 32 + k] = bal;
+            }
         }
     }
 }
@@ -440,14 +413,6 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_rowscan(int32_t *rs, int64_t n) {
     for (int64_t i = s0; i < e0; ++i) { const int32_t v = a[i]; a[i] = (int32_t)run; run += v; }
 }
 
-__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
-    for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off, 64));
-    return v;
-}
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-    for (int off = 32; off > 0; off >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, off, 64));
-    return v;
-}
 
 // L0 = log(I) at mask == 1 (non-positive -> 0), U = L0 (B = 0), ridx = (row << rsh) | column
 // (compact, volume stride VS) and the first U range.  grid (ceil(tiles/4), segments, volumes), 4 tile-waves/block.
@@ -668,19 +633,9 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_hist(const float *__restrict__ U,
     unsigned long long w0 = 0ull, w1 = 0ull;
 #pragma unroll
     for (int k = 0; k < N4_VPT; ++k) {
-        const float cidx = (u[k] - bmin) / slope;   // NaN (padding) fails both range tests
-        if (!(cidx >= 0.0f) || !(cidx < (float)bins)) continue;
-        const int idx = (int)floorf(cidx);
-        const float o = cidx - (float)idx;
-        unsigned long long a0, a1 = 0ull;
-        if (o == 0.0f) {
-            a0 = 1ull << 32;
-        } else if (idx < bins - 1) {
-            a0 = (unsigned long long)((double)(1.0f - o) * 4294967296.0);
-            a1 = (unsigned long long)((double)o * 4294967296.0);
-        } else {
-            continue;
-        }
+        int idx;
+        unsigned long long a0, a1;
+        if (!parzen_bin(u[k], bmin, slope, bins, idx, a0, a1)) continue;
         if (idx != cur) {
             if (cur >= 0) {
                 if (w0) atomicAdd(&H[cur], w0);
@@ -754,7 +709,6 @@ __device__ void lds_fft2(double2 *x, double2 *y, double2 *tx, double2 *ty, const
     }
 }
 
-__device__ __forceinline__ float expf_cr(float x) { return (float)exp((double)x); }
 
 // E(u|v) map (Wiener deconvolution of the histogram by the bias Gaussian), one block per volume.
 __global__ void __launch_bounds__(VH_TPB) k_n4_emap(const uint64_t *hpart, const int32_t *cp,
@@ -1300,7 +1254,7 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
     int gi = 0;   // iteration slot within this sub-batch
     try {
         for (int L = 0; L < prm.n_levels; ++L) {
-            const DevLevel lv = dev_level(b, prm, L);
+            const DevLevel lv = vh_dev_level(b, prm, L);
             const int64_t nft = (b->CZ + FIT_W - 1) / FIT_W;
             const dim3 fg((unsigned)nft, (unsigned)ns);
             const int ncx = lv.ax[0].ncp;
@@ -1366,7 +1320,7 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
                 }
                 if (nch > 0) {
                     ScopedKTimer tm(b, "n4_eval", 0.0);
-                    const DevLevel lvo = (it == 0 && L > 0) ? dev_level(b, prm, L - 1) : lv;
+                    const DevLevel lvo = (it == 0 && L > 0) ? vh_dev_level(b, prm, L - 1) : lv;
                     const int bo_mode = (it == 0 && L == 0) ? 0 : 1;
                     k_n4_eval<<<(unsigned)nch, VH_TPB, (size_t)b->R * 40, st>>>(
                         b->d_L0, U, b->d_ridx, b->d_cp, b->d_cvol, b->d_sc, b->R, b->CZ, b->VS, rsh,
@@ -1405,11 +1359,10 @@ void vh_launch_n4(vh_batch *b, const vh_n4_params &prm) {
     HIP_TRY(hipMemsetAsync(b->d_lat, 0, sizeof(float) * b->nb * b->lat_cap, st));
     k_n4_state_init<<<(unsigned)((b->nb + 255) / 256), 256, 0, st>>>(b->d_st, b->nb);
     VH_CHECK_LAUNCH();
-    std::vector<int32_t> hcp(b->nb + 1);
     {
         ScopedKTimer tm(b, "n4_init", 0.0);
         k_n4_rowcount<<<dim3((unsigned)ntiles, (unsigned)b->nb), 64, 0, st>>>(
-            b->d_colbits, b->R, b->CZ, ntiles, b->d_rowstart);
+            b->d_colbits, b->R, b->CZ, ntiles, b->d_rowstart, b->d_rowmask);
         VH_CHECK_LAUNCH();
         k_n4_rowscan<<<(unsigned)b->nb, VH_TPB, 0, st>>>(b->d_rowstart, ntiles * b->R);
         VH_CHECK_LAUNCH();
@@ -1419,21 +1372,34 @@ void vh_launch_n4(vh_batch *b, const vh_n4_params &prm) {
                                          b->V, b->VS, ntiles, b->d_L0, b->d_U, b->d_ridx,
                                          b->rsh, b->d_st);
         VH_CHECK_LAUNCH();
+    }
+    // driver: volume-resident (one workgroup per study) when the batch has studies for the CUs
+    // and a study's state fits in LDS, else per-iteration sweeps over the whole batch
+    int mode = b->n4_mode;
+    if (const char *e = getenv("VH_N4_MODE")) mode = atoi(e);
+    const bool fits = vh_n4_study_eligible(b, prm, nullptr);
+    if (mode == 2 && !fits) throw VhError{VH_ERR_ARG, "n4_mode=2: study state exceeds the LDS budget"};
+    b->n4_used_study = mode == 2 || (mode == 0 && fits && b->nb >= 16);
+    if (b->n4_used_study) {
+        vh_launch_n4_study(b, prm);
+    } else {
+        std::vector<int32_t> hcp(b->nb + 1);
         k_n4_chunks<<<1, VH_TPB, 0, st>>>(b->d_sc, b->nb, b->d_cp, b->d_cvol);
         VH_CHECK_LAUNCH();
         HIP_TRY(hipMemcpyAsync(hcp.data(), b->d_cp, sizeof(int32_t) * (b->nb + 1),
                                hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
+        int64_t sb = b->n4_subbatch > 0 ? b->n4_subbatch : b->nb;
+        if (const char *e = getenv("VH_N4_SUBBATCH")) {
+            const long v = atol(e);
+            if (v > 0) sb = v;
+        }
+        if (sb > b->nb) sb = b->nb;
+        for (int64_t v0 = 0; v0 < b->nb; v0 += sb)
+            n4_subbatch(b, prm, v0, std::min(sb, b->nb - v0), hcp);
     }
-    int64_t sb = b->n4_subbatch > 0 ? b->n4_subbatch : b->nb;
-    if (const char *e = getenv("VH_N4_SUBBATCH")) {
-        const long v = atol(e);
-        if (v > 0) sb = v;
-    }
-    if (sb > b->nb) sb = b->nb;
-    for (int64_t v0 = 0; v0 < b->nb; v0 += sb) n4_subbatch(b, prm, v0, std::min(sb, b->nb - v0), hcp);
     {
-        const DevLevel lv = dev_level(b, prm, prm.n_levels - 1);
+        const DevLevel lv = vh_dev_level(b, prm, prm.n_levels - 1);
         ScopedKTimer tm(b, "n4_final", 9.0 * (double)b->V);
         k_n4_final<<<cg, VH_TPB, 0, st>>>(b->d_hp, b->d_n4, b->R, b->C, b->Z, b->V, b->q2_cap,
                                           b->d_P1, lv, b->d_colbits, b->d_rowstart, ntiles,

@@ -121,6 +121,7 @@ struct vh_batch {
     float *d_L0 = nullptr, *d_lat = nullptr, *d_E = nullptr;
     double *d_fitpart = nullptr;     // [nb][tiles][lattice] per-tile contracted fit slabs
     int32_t *d_rowstart = nullptr;   // [nb][tiles][R] compact offset of each (64-column tile, row)
+    uint64_t *d_rowmask = nullptr;   // [nb][tiles][R] mask == 1 lanes of each (tile, row)
     // compact N4 state: mask==1 voxels in tile-row order, volume stride VS
     int64_t VS = 0;
     int rsh = 1;                     // compact voxel index = (row << rsh) | column
@@ -146,6 +147,7 @@ struct vh_batch {
     vh_n4_params tab_prm{};          // parameters the tables were built for
     bool tabs_valid = false;
     double2 *d_twiddle = nullptr;    // FFT twiddles (host-computed)
+    void *d_study_lv = nullptr;      // n4_study.hip: per-level table pointers + iteration caps
     // CI workspace
     uint32_t *d_bitmap = nullptr;    // [nb][ceil(V/32)] Fortran-order defect bits
     int32_t *d_ci_list = nullptr;    // [nb][V] defect voxel raster indices (compacted)
@@ -153,6 +155,8 @@ struct vh_batch {
     uint32_t *d_ci_hist = nullptr;   // [nb][ci_nb]
     int64_t ci_nb_cap = 0;
     int64_t n4_subbatch = 0;         // volumes per N4 sub-batch (0 = whole batch)
+    int32_t n4_mode = 0;             // vh_run_opts.n4_mode
+    bool n4_used_study = false;      // the last N4 ran the volume-resident kernel
     // timing
     bool profile = false;
     std::map<std::string, KTimer> timers;
