@@ -145,6 +145,39 @@ __device__ __forceinline__ float st_load(__amdgpu_buffer_rsrc_t r, uint32_t voff
 __device__ __forceinline__ void st_store(__amdgpu_buffer_rsrc_t r, uint32_t voff, float v) {
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)voff, 0, 0);
 }
+// c / slope as IEEE float division, evaluated as (double)c * (1 / (double)slope) rounded once to
+// float.  The double product is within 2^-52 (relative) of the exact quotient, and a quotient of
+// two floats is never closer than 2^-49 (relative) to a float rounding midpoint, so the rounding
+// lands on the correctly rounded quotient: bit-equal to c / slope (also checked on 4e8 random
+// pairs), including 0, inf and NaN cases, at a quarter of the instructions.
+__device__ __forceinline__ float div_r(float c, double rinv) { return (float)((double)c * rinv); }
+
+// sharpen_value / parzen_bin (n4_shared.h) with the bin division in div_r form
+__device__ __forceinline__ float sharpen_r(float u, float bmin, double rinv, const float *E, int bins) {
+    const float cidx = div_r(u - bmin, rinv);
+    const int idx = (cidx >= 0.0f && cidx < (float)bins) ? (int)floorf(cidx) : bins;
+    if (idx < bins - 1) return E[idx] + (E[idx + 1] - E[idx]) * (cidx - (float)idx);
+    return E[bins - 1];
+}
+__device__ __forceinline__ bool parzen_bin_r(float u, float bmin, double rinv, int bins, int &idx,
+                                             unsigned long long &a0, unsigned long long &a1) {
+    const float cidx = div_r(u - bmin, rinv);
+    if (!(cidx >= 0.0f) || !(cidx < (float)bins)) return false;
+    idx = (int)floorf(cidx);
+    const float o = cidx - (float)idx;
+    a1 = 0ull;
+    if (o == 0.0f) {
+        a0 = 1ull << 32;
+    } else if (idx < bins - 1) {
+        const float om = 1.0f - o;
+        a0 = om == 1.0f ? (1ull << 32) : (unsigned long long)(uint32_t)((double)om * 4294967296.0);
+        a1 = (unsigned long long)(uint32_t)((double)o * 4294967296.0);
+    } else {
+        return false;
+    }
+    return true;
+}
+
 __device__ __forceinline__ float wsel(float4 w, int d) {
     return d == 0 ? w.x : d == 1 ? w.y : d == 2 ? w.z : w.w;
 }
@@ -259,10 +292,19 @@ __device__ void fit_contract(FitRing &rg, const Item &it, const TabV &T, const d
     const int klo = T.bz[it.y0 == it.y1 ? it.z0 : 0];
     const int KT = T.bz[it.y0 == it.y1 ? it.z1 : Z - 1] + 4 - klo;
     const int nyk = it.ny * KT;
+    // the ST_SO outputs of a lane are independent fma chains over their slices: walk them in
+    // lockstep (step s of every chain together) so the LDS latency of one chain hides behind the
+    // others; each chain still adds its terms in slice order, so the sums are unchanged
     double outv[ST_SO];
+    const double *qp[ST_SO], *wp[ST_SO];
+    int len[ST_SO];
+    int maxlen = 0;
 #pragma unroll
     for (int q = 0; q < ST_SO; ++q) {
         outv[q] = 0.0;
+        len[q] = 0;
+        qp[q] = rg.q;
+        wp[q] = Wk;
         const int o = lane + 64 * q;
         if (o >= nr * nyk) continue;
         const int r = o / nyk, yk = o % nyk;
@@ -270,11 +312,19 @@ __device__ void fit_contract(FitRing &rg, const Item &it, const TabV &T, const d
         const int zlo = yv == it.y0 ? it.z0 : 0, zhi = yv == it.y1 ? it.z1 : Z - 1;
         const int2 kr = T.krz[k];
         const int zs = max(zlo, kr.x), ze = min(zhi, kr.y);
-        const double *qr = rg.q + r * rg.rowcap + (yv * Z - it.c0);
-        const double *wk = Wk + k * Z;
-        double acc = 0.0;
-        for (int zz = zs; zz <= ze; ++zz) acc = fma(wk[zz], qr[zz], acc);
-        outv[q] = acc;
+        qp[q] = rg.q + r * rg.rowcap + (yv * Z - it.c0) + zs;
+        wp[q] = Wk + k * Z + zs;
+        len[q] = max(ze - zs + 1, 0);
+        maxlen = max(maxlen, len[q]);
+    }
+#pragma unroll 1
+    for (int s = 0; s < maxlen; ++s) {
+#pragma unroll
+        for (int q = 0; q < ST_SO; ++q) {
+            const int ss = min(s, max(len[q] - 1, 0));   // in-range read for finished chains
+            const double v = fma(wp[q][ss], qp[q][ss], outv[q]);
+            outv[q] = s < len[q] ? v : outv[q];
+        }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -326,7 +376,7 @@ __device__ __forceinline__ void fit_push(FitRing &rg, double v, int i, const Ite
 template <int MODE>
 __device__ void fit_item(const StudyArgs &a, const Item &it, const TabV &T, const double *Wk,
                          const double2 *Wx, int ncy, int ncz, const float *Ub, int64_t n,
-                         const float *sE, float bmin, float slope, FitRing &rg,
+                         const float *sE, float bmin, double rinv, FitRing &rg,
                          unsigned long long *numfix) {
     constexpr int P = MODE == 0 ? 3 : 2;
     const __amdgpu_buffer_rsrc_t rU = st_rsrc(Ub, n);
@@ -360,7 +410,7 @@ __device__ void fit_item(const StudyArgs &a, const Item &it, const TabV &T, cons
                     const int xg = xb + g;
                     const double2 wa = Wx[2 * xg], wc = Wx[2 * xg + 1];   // wx(x, 0..3)^P
                     if (MODE == 0) {
-                        const float rv = u[g] - sharpen_value(u[g], bmin, slope, sE, a.bins);
+                        const float rv = u[g] - sharpen_r(u[g], bmin, rinv, sE, a.bins);
                         const double q = ((double)rv * T.ix[xg]) * isyz;
                         acc0 += wa.x * q;
                         acc1 += wa.y * q;
@@ -705,6 +755,55 @@ __device__ void wave_fft(double2 *x, const double2 *tw, bool inverse) {
     for (int r = 0; r < 8; ++r) x[r * 64 + lane] = make_double2(vr[r], vi[r]);
 }
 
+// The same transform by ONE wave in place in LDS: in-place bit reversal by pair swaps, then the
+// 9 radix-2 stages with 4 butterflies per lane; identical butterflies and twiddle indexing (so
+// identical results), wave-local ordering only (a wave's LDS operations complete in issue order;
+// the fences keep the compiler from moving them), and only a handful of live registers -- the
+// register-resident form spills inside this large kernel.
+__device__ __forceinline__ void wave_lds_order() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ void wave_fft_lds(double2 *x, const double2 *tw, bool inverse) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int q = 0; q < VH_FFT_P / 64; ++q) {
+        const int i = lane + 64 * q;
+        const int j = (int)(__brev((unsigned)i) >> (32 - 9));
+        if (i < j) {
+            const double2 v = x[i];
+            x[i] = x[j];
+            x[j] = v;
+        }
+    }
+    wave_lds_order();
+#pragma unroll 1
+    for (int len = 2; len <= VH_FFT_P; len <<= 1) {
+        const int half = len >> 1, step = VH_FFT_P / len;
+        double2 w[4], a[4], bb[4];
+        int i0[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int t = lane + 64 * q;
+            const int g = t / half, j = t % half;
+            i0[q] = g * len + j;
+            w[q] = tw[j * step];
+            a[q] = x[i0[q]];
+            bb[q] = x[i0[q] + half];
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const double wy = inverse ? -w[q].y : w[q].y;
+            const double tr = w[q].x * bb[q].x - wy * bb[q].y, ti = w[q].x * bb[q].y + wy * bb[q].x;
+            x[i0[q]] = make_double2(a[q].x + tr, a[q].y + ti);
+            x[i0[q] + half] = make_double2(a[q].x - tr, a[q].y - ti);
+        }
+        wave_lds_order();
+    }
+}
+
 // ---------------------------------------------------------------------------------------------
 // exact ITK bin minimum (rare): min over the voxels that are not running maxima in raster order
 // ---------------------------------------------------------------------------------------------
@@ -882,7 +981,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
             if (item >= a.nitems) break;
             Item it;
             if (!item_begin(it, a, b, item)) continue;
-            fit_item<1>(a, it, T, Wk2, Wx2, ncy, ncz, Ub, n, sE, 0.0f, 1.0f, ring, numfix);
+            fit_item<1>(a, it, T, Wk2, Wx2, ncy, ncz, Ub, n, sE, 0.0f, 1.0, ring, numfix);
         }
         __syncthreads();
         ST_MARK(0);
@@ -933,6 +1032,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
             ST_MARK(1);
             ++itn;
             const float bmin = M.bin_min, slope = M.slope;
+            const double rinv = 1.0 / (double)slope;   // div_r form of the bin division
             // ---- hist ----
             for (int i = t; i < ST_HC * VH_MAX_BINS; i += ST_TPB) Hc[i] = 0ull;
             __syncthreads();
@@ -956,7 +1056,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                     for (int k = 0; k < 16; ++k) {
                         int idx;
                         unsigned long long a0, a1;
-                        if (!parzen_bin(u[k], bmin, slope, bins, idx, a0, a1)) continue;
+                        if (!parzen_bin_r(u[k], bmin, rinv, bins, idx, a0, a1)) continue;
                         if (idx != cb) {
                             if (cb >= 0) {
                                 if (w0) atomicAdd(&H[cb], w0);
@@ -1006,7 +1106,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                     }
                 }
                 __syncthreads();
-                if (wv < 2) wave_fft(wv ? F : V, TW, false);
+                if (wv < 2) wave_fft_lds(wv ? F : V, TW, false);
                 __syncthreads();
                 for (int i = t; i < P; i += ST_TPB) {
                     const double fa = F[i].x, fb = F[i].y;
@@ -1014,7 +1114,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                     V[i] = make_double2(V[i].x * g, V[i].y * g);
                 }
                 __syncthreads();
-                if (wv == 0) wave_fft(V, TW, true);
+                if (wv == 0) wave_fft_lds(V, TW, true);
                 __syncthreads();
                 for (int i = t; i < P; i += ST_TPB) {
                     const double ur = V[i].x > 0.0 ? V[i].x : 0.0;
@@ -1023,7 +1123,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                     DEN[i] = make_double2(ur, 0.0);
                 }
                 __syncthreads();
-                if (wv < 2) wave_fft(wv ? DEN : V, TW, false);
+                if (wv < 2) wave_fft_lds(wv ? DEN : V, TW, false);
                 __syncthreads();
                 for (int i = t; i < P; i += ST_TPB) {
                     const double fa = F[i].x, fb = F[i].y;
@@ -1033,7 +1133,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                     DEN[i] = make_double2(x.x * fa - x.y * fb, x.x * fb + x.y * fa);
                 }
                 __syncthreads();
-                if (wv < 2) wave_fft(wv ? DEN : V, TW, true);
+                if (wv < 2) wave_fft_lds(wv ? DEN : V, TW, true);
                 __syncthreads();
                 for (int i = t; i < bins; i += ST_TPB) {
                     const double d = DEN[i + off].x;
@@ -1053,7 +1153,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                 if (item >= a.nitems) break;
                 Item it;
                 if (!item_begin(it, a, b, item)) continue;
-                fit_item<0>(a, it, T, Wk3, Wx3, ncy, ncz, Ub, n, sE, bmin, slope, ring, numfix);
+                fit_item<0>(a, it, T, Wk3, Wx3, ncy, ncz, Ub, n, sE, bmin, rinv, ring, numfix);
             }
             __syncthreads();
             ST_MARK(4);
