@@ -183,98 +183,109 @@ __global__ void __launch_bounds__(VH_TPB) k_gather(const float *__restrict__ n4,
 }
 
 // =============================================================================================
-// segmented LSD radix sort (4 x 8-bit digits), one segment per volume, tiles of 4096 keys.
-//   up:   per-tile digit counts                    tilecnt[b][digit][tile]
-//   scan: per-volume exclusive scan (digit-major)  -> scatter base of (digit, tile)
-//   down: stable in-tile ranks by wave ballots (8 ballots build the same-digit peer mask), then
-//         scatter.  Stable => LSD correct.
+// Stable LSD radix sort (4 x 8-bit digits) of each volume's masked keys, ONE workgroup (1024
+// threads) per volume: a volume's keys
+// (~330 KB at 128x128x24) stay in L2 / MALL, the four digit histograms come from one read pass
+// (digit counts do not depend on order), and each pass ranks chunks of 8192 keys in order
+// (wave ballots within a wave, wave prefixes per digit across waves, running digit offsets
+// across chunks) -- one launch for the whole sort instead of 12, all volumes in parallel.
 // =============================================================================================
-__global__ void __launch_bounds__(VH_TPB) k_sort_up(const uint32_t *__restrict__ keys,
-                                                   const VolScalars *sc, int64_t V,
-                                                   int64_t max_tiles, int shift,
-                                                   uint32_t *tilecnt) {
-    __shared__ uint32_t h[256];
-    const int64_t b = blockIdx.y, t = blockIdx.x;
-    const int64_t n = sc[b].n_mask;
-    const int64_t s = t * VH_SORT_TILE;
-    if (s >= n) return;
-    h[threadIdx.x] = 0;
-    __syncthreads();
-    const uint32_t *k = keys + b * V;
-    for (int i = 0; i < VH_SORT_KPT; ++i) {
-        const int64_t idx = s + i * VH_TPB + threadIdx.x;
-        if (idx < n) atomicAdd(&h[(k[idx] >> shift) & 255u], 1u);
+#define VS_TPB 1024
+#define VS_WAVES (VS_TPB / 64)
+#define VS_KPT 8                       // keys per lane per chunk
+#define VS_CHUNK (VS_TPB * VS_KPT)
+
+// peers of this lane's digit among the wave's valid lanes (8 ballots)
+__device__ __forceinline__ uint64_t vs_peers(uint32_t d, bool valid) {
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int bit = 0; bit < 8; ++bit) {
+        const uint64_t bb = __ballot(valid && ((d >> bit) & 1u));
+        peers &= ((d >> bit) & 1u) ? bb : ~bb;
     }
-    __syncthreads();
-    tilecnt[(b * 256 + threadIdx.x) * max_tiles + t] = h[threadIdx.x];
+    return peers;
 }
 
-__global__ void __launch_bounds__(VH_TPB) k_sort_scan(uint32_t *tilecnt, const VolScalars *sc,
-                                                     int64_t max_tiles) {
-    __shared__ uint32_t s_row[256];
+__global__ void __launch_bounds__(VS_TPB) k_sort_vol(uint32_t *__restrict__ k0,
+                                                    uint32_t *__restrict__ k1,
+                                                    const VolScalars *sc, int64_t V) {
+    __shared__ uint32_t s_hist[4][256];      // digit counts -> digit bases
+    __shared__ uint32_t s_wc[VS_WAVES][256]; // per-wave digit counts -> per-wave digit offsets
+    __shared__ uint32_t s_run[256];          // keys of each digit placed by earlier chunks
     const int64_t b = blockIdx.x;
     const int64_t n = sc[b].n_mask;
-    const int64_t nt = (n + VH_SORT_TILE - 1) / VH_SORT_TILE;
-    uint32_t *row = tilecnt + (b * 256 + threadIdx.x) * max_tiles;
-    uint32_t sum = 0;
-    for (int64_t t = 0; t < nt; ++t) sum += row[t];
-    s_row[threadIdx.x] = sum;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t run = 0;
-        for (int d = 0; d < 256; ++d) { uint32_t v = s_row[d]; s_row[d] = run; run += v; }
-    }
-    __syncthreads();
-    uint32_t run = s_row[threadIdx.x];
-    for (int64_t t = 0; t < nt; ++t) { uint32_t v = row[t]; row[t] = run; run += v; }
-}
-
-__global__ void __launch_bounds__(VH_TPB) k_sort_down(const uint32_t *__restrict__ kin,
-                                                     uint32_t *__restrict__ kout,
-                                                     const uint32_t *__restrict__ tilecnt,
-                                                     const VolScalars *sc, int64_t V,
-                                                     int64_t max_tiles, int shift) {
-    __shared__ uint32_t s_wc[4][256];
-    const int64_t b = blockIdx.y, t = blockIdx.x;
-    const int64_t n = sc[b].n_mask;
-    const int64_t s = t * VH_SORT_TILE;
-    if (s >= n) return;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    for (int d = lane; d < 256; d += 64) s_wc[w][d] = 0;
-    __syncthreads();
-    const uint32_t *k = kin + b * V;
+    if (n <= 1) return;
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     const uint64_t lt = (1ull << lane) - 1ull;
-    uint32_t key[VH_SORT_KPT];
-    uint32_t rank[VH_SORT_KPT];
+    for (int i = t; i < 4 * 256; i += VS_TPB) (&s_hist[0][0])[i] = 0u;
+    __syncthreads();
+    uint32_t *kin = k0 + b * V, *kout = k1 + b * V;
+    // ---- the four digit histograms, wave-aggregated (one LDS add per distinct digit) ----
+    for (int64_t i0 = (int64_t)w * 64; i0 < n; i0 += VS_TPB) {
+        const int64_t i = i0 + lane;
+        const bool valid = i < n;
+        const uint32_t key = valid ? kin[i] : 0u;
 #pragma unroll
-    for (int r = 0; r < VH_SORT_KPT; ++r) {
-        const int64_t idx = s + (int64_t)w * (VH_SORT_KPT * 64) + r * 64 + lane;
-        const bool valid = idx < n;
-        const uint32_t kk = valid ? k[idx] : 0u;
-        const uint32_t d = (kk >> shift) & 255u;
-        uint64_t peers = __ballot(valid);
-#pragma unroll
-        for (int bit = 0; bit < 8; ++bit) {
-            const uint64_t bb = __ballot(valid && ((d >> bit) & 1u));
-            peers &= ((d >> bit) & 1u) ? bb : ~bb;
+        for (int p = 0; p < 4; ++p) {
+            const uint32_t d = (key >> (8 * p)) & 255u;
+            const uint32_t d0 = (uint32_t)__shfl((int)d, 0, 64);
+            const uint64_t vmask = __ballot(valid);   // outside the lane-0 branch
+            if (__all(!valid || d == d0)) {
+                if (lane == 0) atomicAdd(&s_hist[p][d0], (uint32_t)__popcll(vmask));
+            } else {
+                const uint64_t peers = vs_peers(d, valid);
+                if (valid && (peers & lt) == 0ull) atomicAdd(&s_hist[p][d], (uint32_t)__popcll(peers));
+            }
         }
-        const uint32_t below = (uint32_t)__popcll(peers & lt);
-        const uint32_t base = valid ? s_wc[w][d] : 0u;
-        __builtin_amdgcn_wave_barrier();
-        if (valid && below == 0) s_wc[w][d] = base + (uint32_t)__popcll(peers);
-        __builtin_amdgcn_wave_barrier();
-        key[r] = kk;
-        rank[r] = valid ? base + below : 0xffffffffu;
     }
     __syncthreads();
-    uint32_t *o = kout + b * V;
+    if (t < 4) {   // exclusive scan per digit position
+        uint32_t run = 0;
+        for (int d = 0; d < 256; ++d) { const uint32_t v = s_hist[t][d]; s_hist[t][d] = run; run += v; }
+    }
+    __syncthreads();
+    for (int p = 0; p < 4; ++p) {
+        const int shift = 8 * p;
+        if (t < 256) s_run[t] = 0u;
+        for (int64_t c0 = 0; c0 < n; c0 += VS_CHUNK) {
+            for (int d = lane; d < 256; d += 64) s_wc[w][d] = 0u;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            uint32_t key[VS_KPT], rank[VS_KPT];
 #pragma unroll
-    for (int r = 0; r < VH_SORT_KPT; ++r) {
-        if (rank[r] == 0xffffffffu) continue;
-        const uint32_t d = (key[r] >> shift) & 255u;
-        uint32_t pos = tilecnt[(b * 256 + d) * max_tiles + t] + rank[r];
-        for (int ww = 0; ww < w; ++ww) pos += s_wc[ww][d];
-        o[pos] = key[r];
+            for (int r = 0; r < VS_KPT; ++r) {   // wave w owns keys [c0 + w*512, c0 + (w+1)*512)
+                const int64_t idx = c0 + (int64_t)w * (VS_KPT * 64) + r * 64 + lane;
+                const bool valid = idx < n;
+                const uint32_t kk = valid ? kin[idx] : 0u;
+                const uint32_t d = (kk >> shift) & 255u;
+                const uint64_t peers = vs_peers(d, valid);
+                const uint32_t below = (uint32_t)__popcll(peers & lt);
+                const uint32_t base = valid ? s_wc[w][d] : 0u;
+                __builtin_amdgcn_wave_barrier();
+                if (valid && below == 0) s_wc[w][d] = base + (uint32_t)__popcll(peers);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                key[r] = kk;
+                rank[r] = valid ? base + below : 0xffffffffu;
+            }
+            __syncthreads();
+            if (t < 256) {   // digit t: exclusive prefix over waves, plus the chunk base
+                uint32_t run = s_hist[p][t] + s_run[t];
+                for (int ww = 0; ww < VS_WAVES; ++ww) { const uint32_t v = s_wc[ww][t]; s_wc[ww][t] = run; run += v; }
+                s_run[t] = run - s_hist[p][t];
+            }
+            __syncthreads();
+#pragma unroll
+            for (int r = 0; r < VS_KPT; ++r) {
+                if (rank[r] == 0xffffffffu) continue;
+                kout[s_wc[w][(key[r] >> shift) & 255u] + rank[r]] = key[r];
+            }
+            __syncthreads();
+        }
+        uint32_t *tmp = kin; kin = kout; kout = tmp;
+        __syncthreads();   // this pass's stores before the next pass's loads (same workgroup)
     }
 }
 
@@ -342,16 +353,84 @@ __device__ float pw_sum(const uint32_t *a, int64_t n) {
     }
 }
 
+// One wave per 8192-chunk: the recursion's leaves (blocks of <= 128 values) are enumerated in
+// order by every lane (uniform walk), lane l sums leaf l with pw_leaf, then lane 0 replays the
+// recursion combining the leaf sums in the same left + right order.  Same additions in the same
+// order as pw_sum, so the same float; the leaf sums (the 128-term chains) run in parallel.
+#define PW_MAX_LEAVES 64   // 8192 / 128
+__device__ __forceinline__ int pw_leaves(int64_t n, int want, int64_t &my_s, int64_t &my_n) {
+    int64_t st_s[12], st_n[12];
+    int sp = 0, nl = 0;
+    st_s[0] = 0; st_n[0] = n;
+    my_s = 0; my_n = 0;
+    while (sp >= 0) {   // pre-order with the left child on top: leaves come out in order
+        const int64_t s = st_s[sp], m = st_n[sp];
+        --sp;
+        if (m <= 128) {
+            if (nl == want) { my_s = s; my_n = m; }
+            ++nl;
+        } else {
+            const int64_t n2 = (m / 2) - ((m / 2) % 8);
+            ++sp; st_s[sp] = s + n2; st_n[sp] = m - n2;   // right (popped second)
+            ++sp; st_s[sp] = s; st_n[sp] = n2;            // left
+        }
+    }
+    return nl;
+}
+
+__device__ float pw_combine(int64_t n, const float *leaf) {
+    // pw_sum's post-order walk with leaf values taken in order from leaf[]
+    int64_t st_n[12];
+    float st_left[12];
+    int st_stage[12];
+    int sp = 0, li = 0;
+    st_n[0] = n; st_stage[0] = 0;
+    for (;;) {
+        if (st_n[sp] <= 128) {
+            float ret = leaf[li++];
+            for (;;) {
+                if (sp == 0) return ret;
+                --sp;
+                const int64_t n2 = (st_n[sp] / 2) - ((st_n[sp] / 2) % 8);
+                if (st_stage[sp] == 1) {
+                    st_left[sp] = ret;
+                    st_stage[sp] = 2;
+                    ++sp;
+                    st_n[sp] = st_n[sp - 1] - n2;
+                    st_stage[sp] = 0;
+                    break;
+                }
+                ret = st_left[sp] + ret;
+            }
+        } else {
+            const int64_t n2 = (st_n[sp] / 2) - ((st_n[sp] / 2) % 8);
+            st_stage[sp] = 1;
+            ++sp;
+            st_n[sp] = n2;
+            st_stage[sp] = 0;
+        }
+    }
+}
+
 __global__ void __launch_bounds__(VH_TPB) k_chunk_sums(const uint32_t *__restrict__ keys,
                                                       const VolScalars *sc, int64_t V,
                                                       int64_t max_chunks, float *chunk) {
+    __shared__ float s_leaf[VH_TPB / 64][PW_MAX_LEAVES];
     const int64_t b = blockIdx.y;
-    const int64_t c = blockIdx.x * (int64_t)VH_TPB + threadIdx.x;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t c = blockIdx.x * (int64_t)(VH_TPB / 64) + w;
     const int64_t n = sc[b].n_mask;
     const int64_t s = c * 8192;
-    if (s >= n) return;
+    if (s >= n) return;   // wave-uniform
     const int64_t m = n - s < 8192 ? n - s : 8192;
-    chunk[b * max_chunks + c] = pw_sum(keys + b * V + s, m);
+    const uint32_t *a = keys + b * V + s;
+    int64_t my_s, my_n;
+    const int nl = pw_leaves(m, lane, my_s, my_n);
+    if (lane < nl) s_leaf[w][lane] = pw_leaf(a + my_s, my_n);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane == 0) chunk[b * max_chunks + c] = pw_combine(m, s_leaf[w]);
 }
 
 __global__ void k_mean_p99(const uint32_t *__restrict__ keys, const float *chunk,
@@ -703,38 +782,67 @@ __global__ void __launch_bounds__(VH_TPB) k_kmeans(const uint32_t *__restrict__ 
 // one LDS atomic per run), per-volume rows, then a fixed-order sum over volumes (no float or
 // global atomics: deterministic).
 // =============================================================================================
-__global__ void __launch_bounds__(VH_TPB) k_cohort_vol(const uint32_t *__restrict__ keys,
-                                                      const VolScalars *sc, int64_t V,
-                                                      uint32_t *rows) {
-    __shared__ uint32_t h[VH_COHORT_BINS];
+// Rows by search: over the sorted keys the bin g(i) (-1 below 0, 1024 at
+// or above 1.5 and for NaN) is non-decreasing when p99 > 0, so a bin's count is the distance
+// between the first indices with g >= e and g >= e + 1.  A 1024-key sample in LDS narrows each
+// search to one sample interval.  Volumes with p99 <= 0 / inf / NaN take a scan with per-value LDS adds.
+__device__ __forceinline__ int cohort_g(uint32_t key, float p99) {
+    const float nv = key2f(key) / p99;
+    if (nv >= 0.0f && nv < 1.5f) {
+        const int bi = (int)(nv * ((float)VH_COHORT_BINS / 1.5f));
+        return bi > VH_COHORT_BINS - 1 ? VH_COHORT_BINS - 1 : bi;
+    }
+    return nv < 0.0f ? -1 : VH_COHORT_BINS;
+}
+
+__global__ void __launch_bounds__(VH_TPB) k_cohort_search(const uint32_t *__restrict__ keys,
+                                                         const VolScalars *sc, int64_t V,
+                                                         uint32_t *rows) {
+    __shared__ int s_g[VH_COHORT_BINS];
+    __shared__ int64_t s_first[VH_COHORT_BINS + 1];
     const int64_t b = blockIdx.x;
-    for (int i = threadIdx.x; i < VH_COHORT_BINS; i += VH_TPB) h[i] = 0u;
-    __syncthreads();
     const int64_t n = sc[b].n_mask;
     const float p99 = sc[b].p99;
-    const int64_t per = (n + VH_TPB - 1) / VH_TPB;
-    const int64_t cs = threadIdx.x * per < n ? threadIdx.x * per : n;
-    const int64_t ce = cs + per < n ? cs + per : n;
     const uint32_t *k = keys + b * V;
-    int cur = -1;
-    uint32_t run = 0;
-    for (int64_t i = cs; i < ce; ++i) {
-        const float nv = key2f(k[i]) / p99;
-        int bi = -1;
-        if (nv >= 0.0f && nv < 1.5f) {
-            bi = (int)(nv * ((float)VH_COHORT_BINS / 1.5f));
-            bi = bi > VH_COHORT_BINS - 1 ? VH_COHORT_BINS - 1 : bi;
+    const int t = threadIdx.x;
+    if (n <= 0 || !(p99 > 0.0f) || isinf(p99)) {   // scan path (k_cohort_vol)
+        __shared__ uint32_t h[VH_COHORT_BINS];
+        for (int i = t; i < VH_COHORT_BINS; i += VH_TPB) h[i] = 0u;
+        __syncthreads();
+        const int64_t per = (n + VH_TPB - 1) / VH_TPB;
+        const int64_t cs = t * per < n ? t * per : n, ce = cs + per < n ? cs + per : n;
+        for (int64_t i = cs; i < ce; ++i) {
+            const float nv = key2f(k[i]) / p99;
+            if (nv >= 0.0f && nv < 1.5f) {
+                int bi = (int)(nv * ((float)VH_COHORT_BINS / 1.5f));
+                atomicAdd(&h[bi > VH_COHORT_BINS - 1 ? VH_COHORT_BINS - 1 : bi], 1u);
+            }
         }
-        if (bi != cur) {
-            if (cur >= 0 && run) atomicAdd(&h[cur], run);
-            cur = bi;
-            run = 0;
-        }
-        run += (bi >= 0);
+        __syncthreads();
+        for (int i = t; i < VH_COHORT_BINS; i += VH_TPB) rows[b * VH_COHORT_BINS + i] = h[i];
+        return;
     }
-    if (cur >= 0 && run) atomicAdd(&h[cur], run);
+    const int S = n < VH_COHORT_BINS ? (int)n : VH_COHORT_BINS;
+    for (int j = t; j < S; j += VH_TPB) s_g[j] = cohort_g(k[(j * n) / S], p99);
     __syncthreads();
-    for (int i = threadIdx.x; i < VH_COHORT_BINS; i += VH_TPB) rows[b * VH_COHORT_BINS + i] = h[i];
+    for (int e = t; e <= VH_COHORT_BINS; e += VH_TPB) {
+        // last sample j with g < e (sample positions are increasing, g non-decreasing)
+        int lo = -1, hi = S;   // s_g[lo] < e <= s_g[hi] (virtual ends)
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (s_g[mid] < e) lo = mid; else hi = mid;
+        }
+        // first index i with g(i) >= e lies in (pos(lo), pos(hi)]
+        int64_t a = lo < 0 ? -1 : (lo * n) / S, z = hi >= S ? n : (hi * n) / S;
+        while (z - a > 1) {
+            const int64_t mid = (a + z) >> 1;
+            if (cohort_g(k[mid], p99) < e) a = mid; else z = mid;
+        }
+        s_first[e] = z;
+    }
+    __syncthreads();
+    for (int i = t; i < VH_COHORT_BINS; i += VH_TPB)
+        rows[b * VH_COHORT_BINS + i] = (uint32_t)(s_first[i + 1] - s_first[i]);
 }
 
 __global__ void k_cohort_sum(const uint32_t *rows, int64_t nb, uint64_t *cohort) {
@@ -837,24 +945,13 @@ void vh_launch_vdp_chain(vh_batch *b, const float *d_n4, const vh_run_opts &o) {
     }
     {
         ScopedKTimer tm(b, "sort", 0.0);
-        uint32_t *kin = b->d_keys0, *kout = b->d_keys1;
-        const dim3 tg((unsigned)b->max_tiles, (unsigned)b->nb);
-        for (int pass = 0; pass < 4; ++pass) {
-            const int shift = 8 * pass;
-            k_sort_up<<<tg, VH_TPB, 0, st>>>(kin, b->d_sc, b->V, b->max_tiles, shift, b->d_tilecnt);
-            VH_CHECK_LAUNCH();
-            k_sort_scan<<<(unsigned)b->nb, VH_TPB, 0, st>>>(b->d_tilecnt, b->d_sc, b->max_tiles);
-            VH_CHECK_LAUNCH();
-            k_sort_down<<<tg, VH_TPB, 0, st>>>(kin, kout, b->d_tilecnt, b->d_sc, b->V,
-                                               b->max_tiles, shift);
-            VH_CHECK_LAUNCH();
-            uint32_t *t = kin; kin = kout; kout = t;
-        }
+        k_sort_vol<<<(unsigned)b->nb, VS_TPB, 0, st>>>(b->d_keys0, b->d_keys1, b->d_sc, b->V);
+        VH_CHECK_LAUNCH();
     }
     {
         const int64_t max_chunks = (b->V + 8191) / 8192;
         float *chunk = reinterpret_cast<float *>(b->d_part);   // part holds >= nb*max_chunks floats
-        k_chunk_sums<<<dim3((unsigned)((max_chunks + VH_TPB - 1) / VH_TPB), (unsigned)b->nb),
+        k_chunk_sums<<<dim3((unsigned)((max_chunks + VH_TPB / 64 - 1) / (VH_TPB / 64)), (unsigned)b->nb),
                        VH_TPB, 0, st>>>(b->d_keys0, b->d_sc, b->V, max_chunks, chunk);
         VH_CHECK_LAUNCH();
         k_mean_p99<<<(unsigned)((b->nb + 63) / 64), 64, 0, st>>>(b->d_keys0, chunk, max_chunks,
@@ -884,7 +981,7 @@ void vh_launch_vdp_chain(vh_batch *b, const float *d_n4, const vh_run_opts &o) {
     if (o.do_cohort) {
         ScopedKTimer tm(b, "cohort", 0.0);
         uint32_t *rows = b->d_tilecnt;   // free after the sort: nb*256*max_tiles >= nb*1024 u32
-        k_cohort_vol<<<(unsigned)b->nb, VH_TPB, 0, st>>>(b->d_keys0, b->d_sc, b->V, rows);
+        k_cohort_search<<<(unsigned)b->nb, VH_TPB, 0, st>>>(b->d_keys0, b->d_sc, b->V, rows);
         VH_CHECK_LAUNCH();
         k_cohort_sum<<<VH_COHORT_BINS / 256, 256, 0, st>>>(rows, b->nb, b->d_cohort);
         VH_CHECK_LAUNCH();
