@@ -178,6 +178,24 @@ __device__ __forceinline__ bool parzen_bin_r(float u, float bmin, double rinv, i
     return true;
 }
 
+// parzen_bin_r without branches: idx in [0, bins - 1], zero weights where parzen_bin adds nothing
+__device__ __forceinline__ void parzen_bin_bf(float u, float bmin, double rinv, int bins, int &idx,
+                                              unsigned long long &a0, unsigned long long &a1) {
+    const float cidx = div_r(u - bmin, rinv);
+    const bool in = cidx >= 0.0f && cidx < (float)bins;   // false for NaN
+    const float cf = in ? floorf(cidx) : 0.0f;
+    const float o = in ? cidx - cf : 0.0f;
+    const bool zero = o == 0.0f, inner = (int)cf < bins - 1;
+    const float om = 1.0f - o;
+    // x * 2^32 is exact in float (power-of-two scale, < 2^32): the f32 -> u32 truncation equals
+    // the double-path truncation of n4_shared.h parzen_bin
+    const unsigned long long w0 =
+        (zero || om == 1.0f) ? (1ull << 32) : (unsigned long long)(uint32_t)(om * 4294967296.0f);
+    a0 = in && (zero || inner) ? w0 : 0ull;
+    a1 = in && !zero && inner ? (unsigned long long)(uint32_t)(o * 4294967296.0f) : 0ull;
+    idx = (int)cf;
+}
+
 __device__ __forceinline__ float wsel(float4 w, int d) {
     return d == 0 ? w.x : d == 1 ? w.y : d == 2 ? w.z : w.w;
 }
@@ -1050,28 +1068,15 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
 #pragma unroll
                         for (int k = 0; k < 16; ++k) u[k] = j0 + k < n ? Ub[j0 + k] : __int_as_float(0x7fc00000);
                     }
-                    int cb = -1;
-                    unsigned long long w0 = 0ull, w1 = 0ull;
+                    // branch-free: every value does its two adds (zero weights for values that
+                    // add nothing) -- no divergent run bookkeeping
 #pragma unroll
                     for (int k = 0; k < 16; ++k) {
                         int idx;
                         unsigned long long a0, a1;
-                        if (!parzen_bin_r(u[k], bmin, rinv, bins, idx, a0, a1)) continue;
-                        if (idx != cb) {
-                            if (cb >= 0) {
-                                if (w0) atomicAdd(&H[cb], w0);
-                                if (w1) atomicAdd(&H[cb + 1], w1);
-                            }
-                            cb = idx;
-                            w0 = 0ull;
-                            w1 = 0ull;
-                        }
-                        w0 += a0;
-                        w1 += a1;
-                    }
-                    if (cb >= 0) {
-                        if (w0) atomicAdd(&H[cb], w0);
-                        if (w1) atomicAdd(&H[cb + 1], w1);
+                        parzen_bin_bf(u[k], bmin, rinv, bins, idx, a0, a1);
+                        atomicAdd(&H[idx], a0);
+                        atomicAdd(&H[min(idx + 1, bins - 1)], a1);
                     }
                 }
             }

@@ -657,6 +657,7 @@ void vh_launch_border(vh_batch *b, const uint8_t *d_in, uint8_t *d_out) {
 #define KM_K 4
 #define KM_TILE 1024
 #define KM_LDS_TILES 4096
+#define KM_SAMPLES 4096   // LDS sample of the sorted values for the boundary searches
 
 // wave-cooperative sum of sorted values k[i], i in tile t intersected with [a, e): lane l adds
 // elements t*1024 + j*64 + l for j = 0..15 in order, then a fixed shuffle tree (deterministic)
@@ -676,20 +677,48 @@ __device__ __forceinline__ double km_tile_sum(const uint32_t *k, int64_t t, int6
 }
 
 // first index in [0, n) whose value is strictly closer to chi than to clo (values sorted, so the
-// predicate is monotone): 64-ary search, one probe per lane per round
-__device__ __forceinline__ int64_t km_boundary(const uint32_t *k, int64_t n, double clo, double chi) {
+// predicate is monotone).  The search first runs over an LDS sample of every stride-th value
+// (no memory latency), then 64-ary over the <= stride values left in global memory: one or two
+// dependent global rounds per boundary instead of ~4.
+__device__ __forceinline__ bool km_closer(double x, double clo, double chi) {
+    return fabs(x - chi) < fabs(x - clo);
+}
+
+__device__ __forceinline__ int64_t km_boundary(const uint32_t *k, int64_t n, double clo, double chi,
+                                               const float *samp, int64_t ns, int64_t stride) {
     const int lane = threadIdx.x & 63;
-    int64_t lo = 0, hi = n;   // answer in [lo, hi]
+    // sample: first sample index js with the predicate true (ns if none)
+    int64_t slo = 0, shi = ns;   // answer in [slo, shi]
+    while (shi - slo > 64) {
+        const int64_t span = shi - slo;
+        const int64_t p = slo + (span * (lane + 1)) / 65;
+        const uint64_t m = __ballot(km_closer((double)samp[p], clo, chi));
+        if (m == 0ull) {
+            slo = slo + (span * 64) / 65 + 1;
+        } else {
+            const int f = __ffsll((long long)m) - 1;
+            const int64_t pf = slo + (span * (f + 1)) / 65;
+            const int64_t pprev = f == 0 ? slo - 1 : slo + (span * f) / 65;
+            slo = pprev + 1;
+            shi = pf;
+        }
+    }
+    {
+        const int64_t p = slo + lane;
+        const bool pr = p < shi ? km_closer((double)samp[p], clo, chi) : true;
+        slo = slo + (__ffsll((long long)__ballot(pr)) - 1);
+    }
+    // global: sample js - 1 is false (or none), sample js is true (or none)
+    int64_t lo = slo == 0 ? 0 : (slo - 1) * stride + 1;
+    int64_t hi = slo >= ns ? n : slo * stride;   // answer in [lo, hi]
     while (hi - lo > 64) {
         const int64_t span = hi - lo;
         const int64_t p = lo + (span * (lane + 1)) / 65;
-        const double x = (double)key2f(k[p]);
-        const bool pr = fabs(x - chi) < fabs(x - clo);
-        const uint64_t m = __ballot(pr);
+        const uint64_t m = __ballot(km_closer((double)key2f(k[p]), clo, chi));
         if (m == 0ull) {
             lo = lo + (span * 64) / 65 + 1;
         } else {
-            const int f = __ffsll((long long)m) - 1;        // first lane with predicate true
+            const int f = __ffsll((long long)m) - 1;
             const int64_t pf = lo + (span * (f + 1)) / 65;
             const int64_t pprev = f == 0 ? lo - 1 : lo + (span * f) / 65;
             lo = pprev + 1;
@@ -697,13 +726,8 @@ __device__ __forceinline__ int64_t km_boundary(const uint32_t *k, int64_t n, dou
         }
     }
     const int64_t p = lo + lane;
-    bool pr = true;
-    if (p < hi) {
-        const double x = (double)key2f(k[p]);
-        pr = fabs(x - chi) < fabs(x - clo);
-    }
-    const uint64_t m = __ballot(pr);
-    return lo + (__ffsll((long long)m) - 1);
+    const bool pr = p < hi ? km_closer((double)key2f(k[p]), clo, chi) : true;
+    return lo + (__ffsll((long long)__ballot(pr)) - 1);
 }
 
 // One block (4 waves) per volume.  Cluster sums: head partial tile + whole-tile sums + tail
@@ -712,6 +736,7 @@ __global__ void __launch_bounds__(VH_TPB) k_kmeans(const uint32_t *__restrict__ 
                                                   int64_t V, double *tile_scratch,
                                                   int64_t max_ktiles, VolScalars *sc) {
     __shared__ double s_tiles[KM_LDS_TILES];
+    __shared__ float s_samp[KM_SAMPLES];
     __shared__ double s_c[KM_K];
     __shared__ int64_t s_cut[KM_K + 1], s_new[KM_K + 1];
     __shared__ int s_done;
@@ -730,13 +755,16 @@ __global__ void __launch_bounds__(VH_TPB) k_kmeans(const uint32_t *__restrict__ 
             else gt[tt] = ts;
         }
     }
+    const int64_t stride = n <= (int64_t)KM_SAMPLES * 64 ? 64 : (n + KM_SAMPLES - 1) / KM_SAMPLES;
+    const int64_t ns = (n - 1) / stride + 1;   // samples at 0, stride, 2 stride, ... < n
+    for (int64_t j = t; j < ns; j += VH_TPB) s_samp[j] = key2f(k[j * stride]);
     if (t < KM_K) s_c[t] = (double)key2f(k[(n * (2 * t + 1)) / (2 * KM_K)]);
     if (t == 0) { s_cut[0] = -1; s_done = 0; }
     __syncthreads();
     int it = 0;
     for (it = 1; it <= 300; ++it) {
         if (w < KM_K - 1) {
-            const int64_t c = km_boundary(k, n, s_c[w], s_c[w + 1]);
+            const int64_t c = km_boundary(k, n, s_c[w], s_c[w + 1], s_samp, ns, stride);
             if (lane == 0) s_new[w + 1] = c;
         }
         __syncthreads();
