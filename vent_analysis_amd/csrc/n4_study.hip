@@ -64,7 +64,7 @@ struct StudyArgs {
     float thresh, fwhm, noise;
     const StudyLevels *lvs;   // device copy: per-level tables and iteration caps
     // dynamic-LDS carve (byte offsets)
-    int32_t o_E, o_tab0, o_tab1, o_lat, o_den, o_P10, o_P11, o_ipart, o_misc, o_scr, o_wave;
+    int32_t o_E, o_tab0, o_tab1, o_lat, o_den, o_P10, o_P11, o_ipart, o_misc, o_scr, o_wave, o_order;
     int32_t s_cap;   // doubles of a wave's ring row (>= 64, >= ny * KT)
     int32_t nb_ring; // ring rows per wave (<= ST_NB)
     int32_t o_wx;    // row weights^P of the current level: Wx[2][R][4] doubles (p = 3, p = 2)
@@ -903,6 +903,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
     double *const P1b0 = reinterpret_cast<double *>(smem + a.o_P10);
     double *const P1b1 = reinterpret_cast<double *>(smem + a.o_P11);
     double *ipart = reinterpret_cast<double *>(smem + a.o_ipart);
+    int32_t *ordr = reinterpret_cast<int32_t *>(smem + a.o_order);
     char *scr = smem + a.o_scr;
 
     const int64_t n = a.sc[b].n_mask1;
@@ -940,12 +941,32 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
         M.item_ctr = 0;
     }
     if (wv == 0) find_first3(a, b, fm, M);
+    {   // item schedule: items by row count, largest first (ties by index), so the dynamic item
+        // queue of every pass ends on small items; the item order of every reduction is unchanged
+        int32_t *isz = reinterpret_cast<int32_t *>(scr);
+        for (int item = wv; item < a.nitems; item += ST_WAVES) {
+            Item it;
+            const bool any = item_begin(it, a, b, item);
+            if (lane == 0) isz[item] = any ? it.xe - it.xs + 1 : 0;
+        }
+        __syncthreads();
+        for (int i = t; i < a.nitems; i += ST_TPB) {
+            const int si = isz[i];
+            int rank = 0;
+            for (int j = 0; j < a.nitems; ++j) {
+                const int sj = isz[j];
+                rank += (sj > si || (sj == si && j < i)) ? 1 : 0;
+            }
+            ordr[rank] = i;
+        }
+    }
     __syncthreads();
     for (;;) {   // range of the initial field U = L0
         int item = 0;
         if (lane == 0) item = atomicAdd(&M.item_ctr, 1);
         item = __shfl(item, 0, 64);
         if (item >= a.nitems) break;
+        item = ordr[item];   // largest items first
         Item it;
         if (!item_begin(it, a, b, item)) continue;
         range_item(it, Ub, n, M);
@@ -997,6 +1018,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
             if (lane == 0) item = atomicAdd(&M.item_ctr, 1);
             item = __shfl(item, 0, 64);
             if (item >= a.nitems) break;
+        item = ordr[item];   // largest items first
             Item it;
             if (!item_begin(it, a, b, item)) continue;
             fit_item<1>(a, it, T, Wk2, Wx2, ncy, ncz, Ub, n, sE, 0.0f, 1.0, ring, numfix);
@@ -1156,6 +1178,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                 if (lane == 0) item = atomicAdd(&M.item_ctr, 1);
                 item = __shfl(item, 0, 64);
                 if (item >= a.nitems) break;
+        item = ordr[item];   // largest items first
                 Item it;
                 if (!item_begin(it, a, b, item)) continue;
                 fit_item<0>(a, it, T, Wk3, Wx3, ncy, ncz, Ub, n, sE, bmin, rinv, ring, numfix);
@@ -1194,6 +1217,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                     if (lane == 0) item = atomicAdd(&M.item_ctr, 1);
                     item = __shfl(item, 0, 64);
                     if (item >= a.nitems) break;
+        item = ordr[item];   // largest items first
                     Item it;
                     if (!item_begin(it, a, b, item)) {
                         if (lane == 0) { ipart[2 * item] = 0.0; ipart[2 * item + 1] = 0.0; }
@@ -1316,6 +1340,7 @@ static bool study_layout(const vh_batch *b, const vh_n4_params &prm, StudyLayout
     const int64_t nslots = (b->R + 63) / 64;
     const int64_t nitems = b->n4_tiles * nslots;
     a.o_ipart = (int32_t)o; o += A(sizeof(double) * 2 * (size_t)nitems);
+    a.o_order = (int32_t)o; o += A(sizeof(int32_t) * (size_t)nitems);
     a.o_misc = (int32_t)o; o += A(sizeof(StudyMisc));
     a.o_wk = (int32_t)o; o += A(2 * sizeof(double) * (size_t)kcap * Z);
     a.o_wx = (int32_t)o; o += A(2 * 4 * sizeof(double) * (size_t)R);
