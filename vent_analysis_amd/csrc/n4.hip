@@ -1210,23 +1210,33 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_final(const float *__restrict__ I
     int wb = ax.base[0];
     double t0 = col_T(p1, wb, ncy, Z, by, wy, z), t1 = col_T(p1, wb + 1, ncy, Z, by, wy, z);
     double t2 = col_T(p1, wb + 2, ncy, Z, by, wy, z), t3 = col_T(p1, wb + 3, ncy, Z, by, wy, z);
-    for (int64_t x = 0; x < R; ++x) {
-        const int bx = ax.base[x];
-        while (wb < bx) {
-            ++wb;
-            t0 = t1; t1 = t2; t2 = t3;
-            t3 = col_T(p1, wb + 3, ncy, Z, by, wy, z);
-        }
-        const float4 w = *reinterpret_cast<const float4 *>(ax.w + 4 * x);
-        const float bn = (float)((double)w.x * t0 + (double)w.y * t1 + (double)w.z * t2 + (double)w.w * t3);
-        const int64_t v = b * V + x * CZ + col;
-        const float o = I[v] / (float)exp((double)bn);
-        out[v] = o;
-        if (emit) {
-            if ((x & 31) == 0) word = colbits[(b * nw + (x >> 5)) * CZ + col];
-            const bool on = (word >> (x & 31)) & 1u;
-            const uint64_t bal = __ballot(on);
-            if (on) keys[b * V + rt[x] + lanes_below(bal)] = f2key(o);
+    // rows in groups of 8: the group's image loads are issued together, then the field, exp and
+    // stores (the row walk of one column is otherwise a dependent load -> exp -> store chain)
+    for (int64_t x0 = 0; x0 < R; x0 += 8) {
+        float iv[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) iv[k] = x0 + k < R ? I[b * V + (x0 + k) * CZ + col] : 0.0f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int64_t x = x0 + k;
+            if (x >= R) break;
+            const int bx = ax.base[x];
+            while (wb < bx) {
+                ++wb;
+                t0 = t1; t1 = t2; t2 = t3;
+                t3 = col_T(p1, wb + 3, ncy, Z, by, wy, z);
+            }
+            const float4 w = *reinterpret_cast<const float4 *>(ax.w + 4 * x);
+            const float bn = (float)((double)w.x * t0 + (double)w.y * t1 + (double)w.z * t2 + (double)w.w * t3);
+            const int64_t v = b * V + x * CZ + col;
+            const float o = iv[k] / (float)exp((double)bn);
+            out[v] = o;
+            if (emit) {
+                if ((x & 31) == 0) word = colbits[(b * nw + (x >> 5)) * CZ + col];
+                const bool on = (word >> (x & 31)) & 1u;
+                const uint64_t bal = __ballot(on);
+                if (on) keys[b * V + rt[x] + lanes_below(bal)] = f2key(o);
+            }
         }
     }
 }
