@@ -212,6 +212,8 @@ __global__ void __launch_bounds__(VS_TPB) k_sort_vol(uint32_t *__restrict__ k0,
     __shared__ uint32_t s_hist[4][256];      // digit counts -> digit bases
     __shared__ uint32_t s_wc[VS_WAVES][256]; // per-wave digit counts -> per-wave digit offsets
     __shared__ uint32_t s_run[256];          // keys of each digit placed by earlier chunks
+    __shared__ uint32_t s_tot[256], s_cst[256], s_wsum[4];   // chunk digit totals / starts
+    __shared__ uint32_t s_stage[VS_CHUNK];   // the chunk in digit order
     const int64_t b = blockIdx.x;
     const int64_t n = sc[b].n_mask;
     if (n <= 1) return;
@@ -254,10 +256,15 @@ __global__ void __launch_bounds__(VS_TPB) k_sort_vol(uint32_t *__restrict__ k0,
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             uint32_t key[VS_KPT], rank[VS_KPT];
 #pragma unroll
+            for (int r = 0; r < VS_KPT; ++r) {   // all loads first: the ranking below is fenced
+                const int64_t idx = c0 + (int64_t)w * (VS_KPT * 64) + r * 64 + lane;
+                key[r] = idx < n ? kin[idx] : 0u;
+            }
+#pragma unroll
             for (int r = 0; r < VS_KPT; ++r) {   // wave w owns keys [c0 + w*512, c0 + (w+1)*512)
                 const int64_t idx = c0 + (int64_t)w * (VS_KPT * 64) + r * 64 + lane;
                 const bool valid = idx < n;
-                const uint32_t kk = valid ? kin[idx] : 0u;
+                const uint32_t kk = key[r];
                 const uint32_t d = (kk >> shift) & 255u;
                 const uint64_t peers = vs_peers(d, valid);
                 const uint32_t below = (uint32_t)__popcll(peers & lt);
@@ -271,18 +278,42 @@ __global__ void __launch_bounds__(VS_TPB) k_sort_vol(uint32_t *__restrict__ k0,
                 rank[r] = valid ? base + below : 0xffffffffu;
             }
             __syncthreads();
-            if (t < 256) {   // digit t: exclusive prefix over waves, plus the chunk base
-                uint32_t run = s_hist[p][t] + s_run[t];
-                for (int ww = 0; ww < VS_WAVES; ++ww) { const uint32_t v = s_wc[ww][t]; s_wc[ww][t] = run; run += v; }
-                s_run[t] = run - s_hist[p][t];
+            if (t < 256) {   // digit t: chunk-local wave prefixes and chunk total, then a scan of
+                             // the totals over digits (wave shuffles + wave sums)
+                uint32_t tot = 0;
+                for (int ww = 0; ww < VS_WAVES; ++ww) { const uint32_t v = s_wc[ww][t]; s_wc[ww][t] = tot; tot += v; }
+                uint32_t inc = tot;
+                for (int off = 1; off < 64; off <<= 1) {
+                    const uint32_t o = __shfl_up(inc, off, 64);
+                    if (lane >= off) inc += o;
+                }
+                if (lane == 63) s_wsum[w] = inc;
+                s_tot[t] = tot;
+                s_cst[t] = inc - tot;   // exclusive within this wave of digits
+            }
+            __syncthreads();
+            if (t < 256) {
+                uint32_t pre = 0;
+                for (int ww = 0; ww < w; ++ww) pre += s_wsum[ww];
+                s_cst[t] += pre;        // chunk-local start of digit t
             }
             __syncthreads();
 #pragma unroll
-            for (int r = 0; r < VS_KPT; ++r) {
+            for (int r = 0; r < VS_KPT; ++r) {   // stage at the chunk-local sorted position
                 if (rank[r] == 0xffffffffu) continue;
-                kout[s_wc[w][(key[r] >> shift) & 255u] + rank[r]] = key[r];
+                const uint32_t d = (key[r] >> shift) & 255u;
+                s_stage[s_cst[d] + s_wc[w][d] + rank[r]] = key[r];
             }
             __syncthreads();
+            // write out in staged order: equal digits are consecutive, so are their targets
+            const int cn = (int)(n - c0 < VS_CHUNK ? n - c0 : VS_CHUNK);
+            for (int q = t; q < cn; q += VS_TPB) {
+                const uint32_t kk = s_stage[q];
+                const uint32_t d = (kk >> shift) & 255u;
+                kout[s_hist[p][d] + s_run[d] + ((uint32_t)q - s_cst[d])] = kk;
+            }
+            __syncthreads();
+            if (t < 256) s_run[t] += s_tot[t];
         }
         uint32_t *tmp = kin; kin = kout; kout = tmp;
         __syncthreads();   // this pass's stores before the next pass's loads (same workgroup)
