@@ -97,12 +97,12 @@ def algorithmic_bytes(name, hp, mk, res, R, C, Z):
         return float(np.sum(levels * 4.0 * vm))
     if name == "n4_init":        # read I at masked voxels, write L0, B, U, ridx
         return float(np.sum(20.0 * vm))
-    if name == "n4_final":       # read I, write N4HPvent                        every voxel
-        return float(B * 8.0 * V)
+    if name == "n4_final":       # read I, write N4HPvent (every voxel) + the sort keys (masked)
+        return float(B * 8.0 * V + np.sum(4.0 * vm))
     if name == "classify":       # read N4 + mask, write defect, border, LB      every voxel
         return float(B * 8.0 * V)
-    if name == "sort":           # 4 LSD passes: read keys twice, write once     masked voxels
-        return float(np.sum(4 * 12.0 * vm))
+    if name == "sort":           # digit histograms (read) + 4 LSD passes (read + write), masked
+        return float(np.sum(36.0 * vm))
     if name == "gather":
         return float(np.sum(vr * 5.0 + 4.0 * vm))
     if name == "snr":

@@ -15,7 +15,7 @@ import sys
 CLASSES = [("k_n4_fit<0>", "n4_fit"), ("k_n4_fit<1>", "n4_den"), ("k_n4_eval", "n4_eval"),
            ("k_n4_hist", "n4_hist"), ("k_n4_init", "n4_init"), ("k_n4_final", "n4_final"),
            ("k_n4_study", "n4_study"), ("k_tile<true", "classify"), ("k_gather", "gather"),
-           ("k_snr(", "snr")]
+           ("k_snr(", "snr"), ("k_sort_vol", "sort"), ("k_mask_stats", "mask_stats")]
 
 
 def klass(name):
