@@ -455,13 +455,49 @@ __global__ void __launch_bounds__(VH_TPB) k_chunk_sums(const uint32_t *__restric
     if (s >= n) return;   // wave-uniform
     const int64_t m = n - s < 8192 ? n - s : 8192;
     const uint32_t *a = keys + b * V + s;
+    // leaves 8 at a time: lane = (leaf, accumulator j) -- pw_leaf's 8 stride-8 accumulators run
+    // on 8 lanes (loads of a leaf row are 8 consecutive keys), then its fixed combine tree by
+    // xor shuffles (a + b == b + a bitwise), then the n % 8 tail adds on the leaf's lane 0
     int64_t my_s, my_n;
-    const int nl = pw_leaves(m, lane, my_s, my_n);
-    if (lane < nl) s_leaf[w][lane] = pw_leaf(a + my_s, my_n);
+    const bool full = m == 8192;   // 64 leaves of 128, no recursion walk needed
+    const int nl = full ? 64 : pw_leaves(m, 0, my_s, my_n);
+    for (int g = 0; g * 8 < nl; ++g) {
+        const int leaf = g * 8 + (lane >> 3), j = lane & 7;
+        if (full) { my_s = 128 * leaf; my_n = 128; }
+        else pw_leaves(m, leaf, my_s, my_n);
+        const bool has = leaf < nl;
+        const uint32_t *p = a + my_s;
+        const int64_t ln = has ? my_n : 0;
+        const int64_t lim = ln - ln % 8;
+        float v[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {   // all loads first
+            const int64_t i = 8 * q + j;
+            v[q] = i < lim ? key2f(p[i]) : 0.0f;
+        }
+        float r = v[0];
+#pragma unroll
+        for (int q = 1; q < 16; ++q)
+            if (8 * q + j < lim) r = r + v[q];
+        r = r + __shfl_xor(r, 1, 64);
+        r = r + __shfl_xor(r, 2, 64);
+        r = r + __shfl_xor(r, 4, 64);
+        if (has && j == 0) {
+            float res = ln < 8 ? 0.0f : r;
+            for (int64_t i = lim; i < ln; ++i) res = res + key2f(p[i]);
+            s_leaf[w][leaf] = res;
+        }
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (lane == 0) chunk[b * max_chunks + c] = pw_combine(m, s_leaf[w]);
+    if (full) {   // perfect binary tree over the 64 leaves: xor shuffles, same pairs and order
+        float r = s_leaf[w][lane];
+        for (int off = 1; off < 64; off <<= 1) r = r + __shfl_xor(r, off, 64);
+        if (lane == 0) chunk[b * max_chunks + c] = r;
+    } else if (lane == 0) {
+        chunk[b * max_chunks + c] = pw_combine(m, s_leaf[w]);
+    }
 }
 
 __global__ void k_mean_p99(const uint32_t *__restrict__ keys, const float *chunk,
