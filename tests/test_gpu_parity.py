@@ -424,3 +424,50 @@ def test_n4_study_empty_mask_in_batch():
         ref, its, _ = native.n4(hp[b], mk[b])
         assert list(its) == list(res[b].n4_iters[:4])
         assert rel(n4[b], ref) < 1e-5
+
+
+# ---- sorted-list statistics on adversarial value distributions ------------------------------------
+@pytest.mark.parametrize("kind", ["constant", "two_values", "negative", "ulp_range", "decades"])
+def test_sorted_statistics_adversarial(kind):
+    """The per-volume radix sort (k_sort_vol), the numpy-order mean anchor, p99, k-means and the
+    cohort rows on value distributions the synthetic generator never makes: a single value (every
+    digit of every key in one bin: the histogram's one-add path), two values (degenerate k-means
+    centres), mostly negative values (sign-flipped keys; p99 < 0 takes the cohort scan path), a
+    4-ulp range (only the low digit varies), 8 decades.  N4 := identity; two volumes per batch,
+    the second the first flipped, so two segments of the batch are exercised."""
+    rng = np.random.default_rng(7)
+    shape = (48, 40, 12)
+    M = (rng.random(shape) < 0.6).astype(np.uint8)
+    n = int(M.sum())
+    if kind == "constant":
+        v = np.full(n, 3.25, np.float32)
+    elif kind == "two_values":
+        v = rng.choice(np.float32([1.5, 2.5]), n)
+    elif kind == "negative":
+        v = rng.normal(-150.0, 50.0, n).astype(np.float32)
+    elif kind == "ulp_range":
+        v = np.float32(100) + rng.integers(0, 4, n).astype(np.float32) * np.spacing(np.float32(100))
+    else:
+        v = (10.0 ** rng.uniform(-4, 4, n)).astype(np.float32)
+    X = np.zeros(shape, np.float32)
+    X[M == 1] = v
+    vols = [(X, M), (np.ascontiguousarray(X[::-1]), np.ascontiguousarray(M[::-1]))]
+    B = _lib.Batch(*shape, 2)
+    B.upload(np.stack([a for a, _ in vols]), np.stack([m for _, m in vols]))
+    B.run(B.options(do_n4=False, vox=(1.5, 1.5, 10.0), do_cohort=True))
+    _, d, _, lb, res = B.download()
+    h = B.cohort_hist()
+    B.close()
+    exp_h = np.zeros(_lib.COHORT_BINS, np.uint64)
+    for b, (XX, MM) in enumerate(vols):
+        o = O.calculate_vdp(XX, MM.astype(np.float64), (1.5, 1.5, 10.0))
+        assert np.float32(res[b].mean_anchor) == o["mean_anchor"]
+        assert np.float32(res[b].p99) == o["p99"]
+        assert np.array_equal(d[b], o["defectArray"])
+        assert np.array_equal(lb[b], o["defectArrayLB"])
+        assert res[b].n_km0 * 100 / MM.sum() == pytest.approx(o["VDP_km"], abs=0)
+        nv = (XX / np.float32(res[b].p99)).astype(np.float32)[MM > 0]
+        sel = (nv >= 0) & (nv < np.float32(1.5))
+        bi = np.minimum((nv[sel] * np.float32(_lib.COHORT_BINS / 1.5)).astype(np.int64), 1023)
+        exp_h += np.bincount(bi, minlength=_lib.COHORT_BINS).astype(np.uint64)
+    assert np.array_equal(h, exp_h)

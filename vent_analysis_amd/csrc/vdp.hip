@@ -725,6 +725,7 @@ void vh_launch_border(vh_batch *b, const uint8_t *d_in, uint8_t *d_out) {
 #define KM_TILE 1024
 #define KM_LDS_TILES 4096
 #define KM_SAMPLES 4096   // LDS sample of the sorted values for the boundary searches
+#define KM_TPB 1024
 
 // wave-cooperative sum of sorted values k[i], i in tile t intersected with [a, e): lane l adds
 // elements t*1024 + j*64 + l for j = 0..15 in order, then a fixed shuffle tree (deterministic)
@@ -741,6 +742,29 @@ __device__ __forceinline__ double km_tile_sum(const uint32_t *k, int64_t t, int6
     for (int j = 0; j < 16; ++j) acc += (double)v[j];
     for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
     return __shfl(acc, 0, 64);
+}
+
+// head and tail partial tiles of a cluster together: both tiles' loads are issued before either
+// reduction (one memory round trip instead of two); same per-tile arithmetic as km_tile_sum
+__device__ __forceinline__ void km_tile_sum2(const uint32_t *k, int64_t t0, int64_t t1, int64_t a,
+                                             int64_t e, double &s0, double &s1) {
+    const int lane = threadIdx.x & 63;
+    float v0[16], v1[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const int64_t i0 = t0 * KM_TILE + j * 64 + lane, i1 = t1 * KM_TILE + j * 64 + lane;
+        v0[j] = (i0 >= a && i0 < e) ? key2f(k[i0]) : 0.0f;
+        v1[j] = (i1 >= a && i1 < e) ? key2f(k[i1]) : 0.0f;
+    }
+    double acc0 = 0.0, acc1 = 0.0;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) { acc0 += (double)v0[j]; acc1 += (double)v1[j]; }
+    for (int off = 32; off > 0; off >>= 1) {
+        acc0 += __shfl_down(acc0, off, 64);
+        acc1 += __shfl_down(acc1, off, 64);
+    }
+    s0 = __shfl(acc0, 0, 64);
+    s1 = __shfl(acc1, 0, 64);
 }
 
 // first index in [0, n) whose value is strictly closer to chi than to clo (values sorted, so the
@@ -799,10 +823,11 @@ __device__ __forceinline__ int64_t km_boundary(const uint32_t *k, int64_t n, dou
 
 // One block (4 waves) per volume.  Cluster sums: head partial tile + whole-tile sums + tail
 // partial tile, in tile order (deterministic).
-__global__ void __launch_bounds__(VH_TPB) k_kmeans(const uint32_t *__restrict__ keys,
+__global__ void __launch_bounds__(KM_TPB) k_kmeans(const uint32_t *__restrict__ keys,
                                                   int64_t V, double *tile_scratch,
                                                   int64_t max_ktiles, VolScalars *sc) {
-    __shared__ double s_tiles[KM_LDS_TILES];
+    __shared__ double s_tiles[KM_LDS_TILES + 1];   // tile sums -> exclusive prefix of them
+    __shared__ double s_wtot[KM_TPB / 64];
     __shared__ float s_samp[KM_SAMPLES];
     __shared__ double s_c[KM_K];
     __shared__ int64_t s_cut[KM_K + 1], s_new[KM_K + 1];
@@ -815,7 +840,7 @@ __global__ void __launch_bounds__(VH_TPB) k_kmeans(const uint32_t *__restrict__ 
     const int64_t nt = (n + KM_TILE - 1) / KM_TILE;
     double *gt = tile_scratch + b * max_ktiles;
     const bool in_lds = nt <= KM_LDS_TILES;
-    for (int64_t tt = w; tt < nt; tt += VH_TPB / 64) {
+    for (int64_t tt = w; tt < nt; tt += KM_TPB / 64) {
         const double ts = km_tile_sum(k, tt, 0, n);
         if (lane == 0) {
             if (in_lds) s_tiles[tt] = ts;
@@ -824,7 +849,27 @@ __global__ void __launch_bounds__(VH_TPB) k_kmeans(const uint32_t *__restrict__ 
     }
     const int64_t stride = n <= (int64_t)KM_SAMPLES * 64 ? 64 : (n + KM_SAMPLES - 1) / KM_SAMPLES;
     const int64_t ns = (n - 1) / stride + 1;   // samples at 0, stride, 2 stride, ... < n
-    for (int64_t j = t; j < ns; j += VH_TPB) s_samp[j] = key2f(k[j * stride]);
+    for (int64_t j = t; j < ns; j += KM_TPB) s_samp[j] = key2f(k[j * stride]);
+    __syncthreads();
+    if (in_lds) {   // exclusive prefix of the tile sums (fixed order: thread chunks, wave scan)
+        const int per = (int)((nt + KM_TPB - 1) / KM_TPB);
+        const int64_t t0 = (int64_t)t * per, t1 = t0 + per < nt ? t0 + per : nt;
+        double tv[KM_LDS_TILES / KM_TPB];
+        double mine = 0.0;
+        for (int64_t tt = t0; tt < t1; ++tt) { tv[tt - t0] = s_tiles[tt]; mine += tv[tt - t0]; }
+        double inc = mine;
+        for (int off = 1; off < 64; off <<= 1) {
+            const double o = __shfl_up(inc, off, 64);
+            if (lane >= off) inc += o;
+        }
+        double run = __shfl_up(inc, 1, 64);
+        if (lane == 0) run = 0.0;
+        if (lane == 63) s_wtot[w] = inc;
+        __syncthreads();
+        for (int ww = 0; ww < w; ++ww) run += s_wtot[ww];
+        for (int64_t tt = t0; tt < t1; ++tt) { s_tiles[tt] = run; run += tv[tt - t0]; }
+        if (t1 == nt && t0 < t1) s_tiles[nt] = run;
+    }
     if (t < KM_K) s_c[t] = (double)key2f(k[(n * (2 * t + 1)) / (2 * KM_K)]);
     if (t == 0) { s_cut[0] = -1; s_done = 0; }
     __syncthreads();
@@ -847,15 +892,19 @@ __global__ void __launch_bounds__(VH_TPB) k_kmeans(const uint32_t *__restrict__ 
         }
         __syncthreads();
         if (s_done) break;
-        {   // wave w updates centre w
+        if (w < KM_K) {   // wave w updates centre w: head + whole tiles (prefix) + tail
             const int64_t a = s_cut[w], e = s_cut[w + 1];
             if (e > a) {
                 const int64_t ta = a / KM_TILE, te = (e - 1) / KM_TILE;
-                const double head = km_tile_sum(k, ta, a, e);
-                const double tail = te != ta ? km_tile_sum(k, te, a, e) : 0.0;
+                double head, tail;
+                km_tile_sum2(k, ta, te, a, e, head, tail);
                 if (lane == 0) {
                     double sum = head;
-                    for (int64_t tt = ta + 1; tt < te; ++tt) sum += in_lds ? s_tiles[tt] : gt[tt];
+                    if (in_lds) {
+                        if (te > ta + 1) sum += s_tiles[te] - s_tiles[ta + 1];
+                    } else {
+                        for (int64_t tt = ta + 1; tt < te; ++tt) sum += gt[tt];
+                    }
                     if (te != ta) sum += tail;
                     s_c[w] = sum / (double)(e - a);
                 }
@@ -1085,7 +1134,7 @@ void vh_launch_vdp_chain(vh_batch *b, const float *d_n4, const vh_run_opts &o) {
         ScopedKTimer tm(b, "kmeans", 0.0);
         const int64_t max_ktiles = (b->V + KM_TILE - 1) / KM_TILE;
         double *scratch = reinterpret_cast<double *>(b->d_keys1);   // free after the sort (4V >= 8V/1024 B)
-        k_kmeans<<<(unsigned)b->nb, VH_TPB, 0, st>>>(b->d_keys0, b->V, scratch, max_ktiles, b->d_sc);
+        k_kmeans<<<(unsigned)b->nb, KM_TPB, 0, st>>>(b->d_keys0, b->V, scratch, max_ktiles, b->d_sc);
         VH_CHECK_LAUNCH();
     }
     if (o.do_snr) vh_launch_snr(b);
