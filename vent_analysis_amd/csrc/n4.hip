@@ -1376,12 +1376,6 @@ void vh_launch_n4(vh_batch *b, const vh_n4_params &prm) {
         VH_CHECK_LAUNCH();
         k_n4_rowscan<<<(unsigned)b->nb, VH_TPB, 0, st>>>(b->d_rowstart, ntiles * b->R);
         VH_CHECK_LAUNCH();
-        const dim3 sg((unsigned)((ntiles + 3) / 4), (unsigned)((b->R + SEG_R - 1) / SEG_R),
-                      (unsigned)b->nb);
-        k_n4_init<<<sg, VH_TPB, 0, st>>>(b->d_hp, b->d_colbits, b->d_rowstart, b->d_sc, b->R, b->CZ,
-                                         b->V, b->VS, ntiles, b->d_L0, b->d_U, b->d_ridx,
-                                         b->rsh, b->d_st);
-        VH_CHECK_LAUNCH();
     }
     // driver: volume-resident (one workgroup per study) when the batch has studies for the CUs
     // and a study's state fits in LDS, else per-iteration sweeps over the whole batch
@@ -1390,6 +1384,15 @@ void vh_launch_n4(vh_batch *b, const vh_n4_params &prm) {
     const bool fits = vh_n4_study_eligible(b, prm, nullptr);
     if (mode == 2 && !fits) throw VhError{VH_ERR_ARG, "n4_mode=2: study state exceeds the LDS budget"};
     b->n4_used_study = mode == 2 || (mode == 0 && fits && b->nb >= 16);
+    if (!b->n4_used_study) {   // the study kernel computes L0 / U itself
+        ScopedKTimer tm(b, "n4_init", 0.0);
+        const dim3 sg((unsigned)((ntiles + 3) / 4), (unsigned)((b->R + SEG_R - 1) / SEG_R),
+                      (unsigned)b->nb);
+        k_n4_init<<<sg, VH_TPB, 0, st>>>(b->d_hp, b->d_colbits, b->d_rowstart, b->d_sc, b->R, b->CZ,
+                                         b->V, b->VS, ntiles, b->d_L0, b->d_U, b->d_ridx,
+                                         b->rsh, b->d_st);
+        VH_CHECK_LAUNCH();
+    }
     if (b->n4_used_study) {
         vh_launch_n4_study(b, prm);
     } else {

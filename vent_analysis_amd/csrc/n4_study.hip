@@ -49,7 +49,9 @@ struct StudyLevels {
 };
 
 struct StudyArgs {
-    const float *L0;
+    const float *I;     // HPvent [nb][R][C][Z] (the init pass computes L0 = log I here)
+    int64_t V;
+    float *L0;
     float *U;
     const int32_t *rs;
     const uint64_t *rmask;
@@ -492,6 +494,44 @@ __device__ __forceinline__ void range_commit(StudyMisc &M, float umax, float umi
     }
 }
 
+// Init + range of the initial field over one item: L0 = log(I) at mask == 1 (k_n4_init's
+// expression; non-positive -> 0), U = L0 (B = 0), same range bookkeeping as the eval.  Replaces the
+// separate k_n4_init sweep in this driver (the volume-resident kernel reads I directly).
+__device__ void init_item(const StudyArgs &a, int64_t b, const Item &it, float *Lb, float *Ub,
+                          int64_t n, StudyMisc &M) {
+    const __amdgpu_buffer_rsrc_t rL = st_rsrc(Lb, n), rU = st_rsrc(Ub, n);
+    const float *Ib = a.I + b * a.V + it.col;
+    float umax = -FLT_MAX, umin = FLT_MAX, umin2 = FLT_MAX;
+    const bool has_rv = item_has(it, M.rx[0], M.rc[0]) || item_has(it, M.rx[1], M.rc[1]) ||
+                        item_has(it, M.rx[2], M.rc[2]);
+#pragma unroll 1
+    for (int xb = it.xs; xb <= it.xe; xb += ST_G) {
+        uint32_t offs[ST_G];
+        float iv[ST_G];
+#pragma unroll
+        for (int g = 0; g < ST_G; ++g) {   // the group's image loads together
+            const int xg = xb + g;
+            offs[g] = item_off(it, xg <= it.xe ? xg : it.xe, xg <= it.xe);
+            iv[g] = offs[g] != VH_OOB ? Ib[(int64_t)xg * a.CZ] : 0.0f;
+        }
+#pragma unroll
+        for (int g = 0; g < ST_G; ++g) {
+            if (offs[g] == VH_OOB) continue;
+            const float l = iv[g] > 0.0f ? (float)log((double)iv[g]) : 0.0f;
+            st_store(rL, offs[g], l);
+            st_store(rU, offs[g], l);
+            umax = fmaxf(umax, l);
+            if (has_rv) {
+                range_special(M, xb + g, it.col, l, umin, umin2);
+            } else {
+                umin = fminf(umin, l);
+                umin2 = fminf(umin2, l);
+            }
+        }
+    }
+    range_commit(M, umax, umin, umin2);
+}
+
 // U range of the initial field (U = L0) over one item, same bookkeeping as the eval
 __device__ void range_item(const Item &it, const float *Ub, int64_t n, StudyMisc &M) {
     const __amdgpu_buffer_rsrc_t rU = st_rsrc(Ub, n);
@@ -918,7 +958,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
         }
         return;
     }
-    const float *Lb = a.L0 + b * a.VS;
+    float *Lb = a.L0 + b * a.VS;
     float *Ub = a.U + b * a.VS;
     const int64_t fm = a.sc[b].first_masked;
     // fit / eval scratch: lattice numerator (fixed point), then per-wave Q / S rows
@@ -969,7 +1009,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
         item = ordr[item];   // largest items first
         Item it;
         if (!item_begin(it, a, b, item)) continue;
-        range_item(it, Ub, n, M);
+        init_item(a, b, it, Lb, Ub, n, M);
     }
     {
         const DevLevel &l0 = a.lvs->lv[0];
@@ -1367,6 +1407,8 @@ void vh_launch_n4_study(vh_batch *b, const vh_n4_params &prm) {
     StudyLayout Ly;
     if (!study_layout(b, prm, Ly)) throw VhError{VH_ERR_ARG, "N4 study kernel: LDS budget exceeded"};
     StudyArgs a = Ly.a;
+    a.I = b->d_hp;
+    a.V = b->V;
     a.L0 = b->d_L0;
     a.U = b->d_U;
     a.rs = b->d_rowstart;
