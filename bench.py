@@ -68,7 +68,7 @@ def cpu_baseline(R, C, Z, seconds=15.0, procs=16):
 # ------------------------------------------------------------------------------------------------
 # algorithmic bytes per kernel class (DESIGN.md "Roofline accounting")
 # ------------------------------------------------------------------------------------------------
-def algorithmic_bytes(name, hp, mk, res, R, C, Z):
+def algorithmic_bytes(name, hp, mk, res, R, C, Z, study=True):
     """Total algorithmic HBM bytes moved by all launches of kernel class ``name`` in one step.
 
     N4 state is compact (mask == 1 voxels only, DESIGN.md "HBM layout"), so the per-unit figures
@@ -91,12 +91,13 @@ def algorithmic_bytes(name, hp, mk, res, R, C, Z):
         return float(np.sum(iters * 8.0 * vm))
     if name == "n4_hist":        # read U
         return float(np.sum(iters * 4.0 * vm))
-    if name == "n4_study":       # per iteration: hist reads U, fit reads U, eval reads L0 + writes U
-        return float(np.sum(iters * 16.0 * vm))
+    if name == "n4_study":       # init: read I, write L0 + U; per iteration: hist reads U, fit
+        return float(np.sum(iters * 16.0 * vm + 12.0 * vm))   # reads U, eval reads L0 + writes U
     if name == "n4_den":         # read ridx, once per level
         return float(np.sum(levels * 4.0 * vm))
-    if name == "n4_init":        # read I at masked voxels, write L0, B, U, ridx
-        return float(np.sum(20.0 * vm))
+    if name == "n4_init":        # row masks / offsets from the column bitmaps (+ the sweep
+        tiles = (C * Z + 63) // 64   # driver's init: read I at masked voxels, write L0, U, ridx)
+        return float(B * (V / 8.0 + 12.0 * R * tiles) + (0.0 if study else np.sum(16.0 * vm)))
     if name == "n4_final":       # read I, write N4HPvent (every voxel) + the sort keys (masked)
         return float(B * 8.0 * V + np.sum(4.0 * vm))
     if name == "classify":       # read N4 + mask, write defect, border, LB      every voxel
@@ -231,13 +232,15 @@ def main():
         dt = max_over_ranks(dt, dist)
 
     _, _, _, _, res = Bt.download(n4=False, maps=False)
+    used_study = args.n4_mode == "study" or (args.n4_mode == "auto" and nb >= 16)
     kernels = {}
     if not args.no_profile:
         for name in _lib.lib().vh_batch_kernel_names().decode().split(";"):
             ms, n, _ = Bt.kernel_time(name)
             if n:
                 kernels[name] = {"ms_total": ms, "launches": n,
-                                 "alg_bytes": algorithmic_bytes(name, hp, mk, res, R, C, Z) * args.steps}
+                                 "alg_bytes": algorithmic_bytes(name, hp, mk, res, R, C, Z,
+                                                                study=used_study) * args.steps}
     roof = None
     if kernels:
         dom = max(kernels, key=lambda k: kernels[k]["ms_total"])
