@@ -222,21 +222,28 @@ __global__ void __launch_bounds__(VS_TPB) k_sort_vol(uint32_t *__restrict__ k0,
     for (int i = t; i < 4 * 256; i += VS_TPB) (&s_hist[0][0])[i] = 0u;
     __syncthreads();
     uint32_t *kin = k0 + b * V, *kout = k1 + b * V;
-    // ---- the four digit histograms, wave-aggregated (one LDS add per distinct digit) ----
-    for (int64_t i0 = (int64_t)w * 64; i0 < n; i0 += VS_TPB) {
-        const int64_t i = i0 + lane;
-        const bool valid = i < n;
-        const uint32_t key = valid ? kin[i] : 0u;
+    // ---- the four digit histograms (one add per row when a row shares its digit); each wave
+    // loads VS_KPT rows of 64 keys at a time, so one memory round trip covers 8 rows ----
+    for (int64_t i0 = (int64_t)w * (VS_KPT * 64); i0 < n; i0 += (int64_t)VS_TPB * VS_KPT) {
+        uint32_t kr[VS_KPT];
 #pragma unroll
-        for (int p = 0; p < 4; ++p) {
-            const uint32_t d = (key >> (8 * p)) & 255u;
-            const uint32_t d0 = (uint32_t)__shfl((int)d, 0, 64);
+        for (int r = 0; r < VS_KPT; ++r) {
+            const int64_t i = i0 + r * 64 + lane;
+            kr[r] = i < n ? kin[i] : 0u;
+        }
+#pragma unroll
+        for (int r = 0; r < VS_KPT; ++r) {
+            const bool valid = i0 + r * 64 + lane < n;
             const uint64_t vmask = __ballot(valid);   // outside the lane-0 branch
-            if (__all(!valid || d == d0)) {
-                if (lane == 0) atomicAdd(&s_hist[p][d0], (uint32_t)__popcll(vmask));
-            } else {
-                const uint64_t peers = vs_peers(d, valid);
-                if (valid && (peers & lt) == 0ull) atomicAdd(&s_hist[p][d], (uint32_t)__popcll(peers));
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                const uint32_t d = (kr[r] >> (8 * p)) & 255u;
+                const uint32_t d0 = (uint32_t)__shfl((int)d, 0, 64);
+                if (__all(!valid || d == d0)) {   // one digit in the row (typical of high digits)
+                    if (lane == 0 && vmask) atomicAdd(&s_hist[p][d0], (uint32_t)__popcll(vmask));
+                } else if (valid) {                 // spread digits: plain adds, few collisions
+                    atomicAdd(&s_hist[p][d], 1u);
+                }
             }
         }
     }
@@ -266,14 +273,17 @@ __global__ void __launch_bounds__(VS_TPB) k_sort_vol(uint32_t *__restrict__ k0,
                 const bool valid = idx < n;
                 const uint32_t kk = key[r];
                 const uint32_t d = (kk >> shift) & 255u;
-                const uint64_t peers = vs_peers(d, valid);
+                // a row that shares one digit (typical of high digits) needs no match ballots
+                const uint32_t d0 = (uint32_t)__shfl((int)d, 0, 64);
+                const uint64_t peers = __all(!valid || d == d0) ? __ballot(valid) : vs_peers(d, valid);
                 const uint32_t below = (uint32_t)__popcll(peers & lt);
-                const uint32_t base = valid ? s_wc[w][d] : 0u;
-                __builtin_amdgcn_wave_barrier();
-                if (valid && below == 0) s_wc[w][d] = base + (uint32_t)__popcll(peers);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                // the digit group's leader reserves its slots with a returning LDS add (a wave's
+                // LDS atomics complete in issue order, so rows stay ordered) and hands the base
+                // to its peers
+                uint32_t base = 0u;
+                if (valid && below == 0) base = atomicAdd(&s_wc[w][d], (uint32_t)__popcll(peers));
+                const int leader = peers ? __builtin_ctzll(peers) : lane;
+                base = (uint32_t)__shfl((int)base, leader, 64);
                 key[r] = kk;
                 rank[r] = valid ? base + below : 0xffffffffu;
             }
@@ -281,7 +291,11 @@ __global__ void __launch_bounds__(VS_TPB) k_sort_vol(uint32_t *__restrict__ k0,
             if (t < 256) {   // digit t: chunk-local wave prefixes and chunk total, then a scan of
                              // the totals over digits (wave shuffles + wave sums)
                 uint32_t tot = 0;
-                for (int ww = 0; ww < VS_WAVES; ++ww) { const uint32_t v = s_wc[ww][t]; s_wc[ww][t] = tot; tot += v; }
+                uint32_t wcv[VS_WAVES];
+#pragma unroll
+                for (int ww = 0; ww < VS_WAVES; ++ww) wcv[ww] = s_wc[ww][t];   // loads together
+#pragma unroll
+                for (int ww = 0; ww < VS_WAVES; ++ww) { s_wc[ww][t] = tot; tot += wcv[ww]; }
                 uint32_t inc = tot;
                 for (int off = 1; off < 64; off <<= 1) {
                     const uint32_t o = __shfl_up(inc, off, 64);
