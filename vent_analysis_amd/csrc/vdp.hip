@@ -41,8 +41,15 @@ __global__ void __launch_bounds__(VH_TPB) k_mask_stats(const uint8_t *__restrict
         uint32_t *cb = colbits + (b * nw) * CZ + col;   // bit x&31 of word x>>5: mask == 1
         uint32_t word = 0u;
         int32_t lo = (int32_t)R, hi = -1;
-        for (int64_t x = 0; x < R; ++x) {
-            const uint8_t v = m[x * CZ];
+        for (int64_t x0 = 0; x0 < R; x0 += 8) {   // 8 rows of loads in flight
+          uint8_t mv[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) mv[k] = x0 + k < R ? m[(x0 + k) * CZ] : 0;
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            const int64_t x = x0 + k;
+            if (x >= R) break;
+            const uint8_t v = mv[k];
             if (v == 1) word |= 1u << (x & 31);
             if ((x & 31) == 31 || x == R - 1) {
                 cb[(x >> 5) * CZ] = word;
@@ -59,6 +66,7 @@ __global__ void __launch_bounds__(VH_TPB) k_mask_stats(const uint8_t *__restrict
                     if (idx < first) first = idx;
                 }
             }
+          }
         }
         colrange[(b * CZ + col) * 2] = lo;
         colrange[(b * CZ + col) * 2 + 1] = hi;
