@@ -1229,7 +1229,7 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_final(const float *__restrict__ I
             const float4 w = *reinterpret_cast<const float4 *>(ax.w + 4 * x);
             const float bn = (float)((double)w.x * t0 + (double)w.y * t1 + (double)w.z * t2 + (double)w.w * t3);
             const int64_t v = b * V + x * CZ + col;
-            const float o = iv[k] / (float)exp((double)bn);
+            const float o = iv[k] / expf(bn);   // OCML expf (<= 1 ulp of the double-rounded exp)
             out[v] = o;
             if (emit) {
                 if ((x & 31) == 0) word = colbits[(b * nw + (x >> 5)) * CZ + col];
