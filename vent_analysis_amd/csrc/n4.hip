@@ -1190,9 +1190,8 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_refine(float *lat, int64_t lat_ca
 __global__ void __launch_bounds__(VH_TPB) k_n4_final(const float *__restrict__ I, float *out,
                                                     int64_t R, int64_t C, int64_t Z, int64_t V,
                                                     int64_t q2_cap, const double *P1, DevLevel lv,
-                                                    const uint32_t *colbits, const int32_t *rs,
-                                                    int64_t ntiles, const VolScalars *sc,
-                                                    uint32_t *keys) {
+                                                    const uint32_t *colbits, const int64_t *colstart,
+                                                    const VolScalars *sc, uint32_t *keys) {
     const int64_t b = blockIdx.y;
     const int64_t CZ = C * Z;
     const int64_t col = blockIdx.x * (int64_t)VH_TPB + threadIdx.x;
@@ -1205,7 +1204,9 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_final(const float *__restrict__ I
     const DevAxis ax = lv.ax[0];
     const bool emit = keys != nullptr && sc[b].n_mask == sc[b].n_mask1;   // block-uniform
     const int64_t nw = (R + 31) >> 5;
-    const int32_t *rt = rs + (b * ntiles + col / TILE_W) * R;
+    // keys: the wave's 64 columns own one contiguous run of k_gather's column compaction; the
+    // sort needs the values only, so they are stored row by row across the wave (coalesced)
+    int64_t kpos = emit ? b * V + colstart[b * CZ + (col & ~(int64_t)63)] : 0;
     uint32_t word = 0u;
     int wb = ax.base[0];
     double t0 = col_T(p1, wb, ncy, Z, by, wy, z), t1 = col_T(p1, wb + 1, ncy, Z, by, wy, z);
@@ -1235,7 +1236,8 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_final(const float *__restrict__ I
                 if ((x & 31) == 0) word = colbits[(b * nw + (x >> 5)) * CZ + col];
                 const bool on = (word >> (x & 31)) & 1u;
                 const uint64_t bal = __ballot(on);
-                if (on) keys[b * V + rt[x] + lanes_below(bal)] = f2key(o);
+                if (on) keys[kpos + lanes_below(bal)] = f2key(o);
+                kpos += __popcll(bal);
             }
         }
     }
@@ -1415,7 +1417,7 @@ void vh_launch_n4(vh_batch *b, const vh_n4_params &prm) {
         const DevLevel lv = vh_dev_level(b, prm, prm.n_levels - 1);
         ScopedKTimer tm(b, "n4_final", 9.0 * (double)b->V);
         k_n4_final<<<cg, VH_TPB, 0, st>>>(b->d_hp, b->d_n4, b->R, b->C, b->Z, b->V, b->q2_cap,
-                                          b->d_P1, lv, b->d_colbits, b->d_rowstart, ntiles,
+                                          b->d_P1, lv, b->d_colbits, b->d_colstart,
                                           b->d_sc, b->d_keys0);
         b->keys_fused = true;   // the VDP chain's gather skips volumes with binary masks
         VH_CHECK_LAUNCH();
