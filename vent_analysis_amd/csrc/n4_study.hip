@@ -814,7 +814,7 @@ __device__ void wave_fft(double2 *x, const double2 *tw, bool inverse) {
 }
 
 // The same transform by ONE wave in place in LDS: in-place bit reversal by pair swaps, then the
-// 9 radix-2 stages with 4 butterflies per lane; identical butterflies and twiddle indexing (so
+// 9 radix-2 stages as 3 register passes; identical butterflies and twiddle indexing (so
 // identical results), wave-local ordering only (a wave's LDS operations complete in issue order;
 // the fences keep the compiler from moving them), and only a handful of live registers -- the
 // register-resident form spills inside this large kernel.
@@ -837,27 +837,33 @@ __device__ void wave_fft_lds(double2 *x, const double2 *tw, bool inverse) {
         }
     }
     wave_lds_order();
+    // the 9 stages in 3 passes of 3: in pass p a lane owns the 8 points base + m * 8^p (m < 8),
+    // which the stages of half-length 8^p, 2 * 8^p, 4 * 8^p pair only among themselves, so the
+    // pass runs its 3 stages in registers (same butterflies, same twiddles, same order)
 #pragma unroll 1
-    for (int len = 2; len <= VH_FFT_P; len <<= 1) {
-        const int half = len >> 1, step = VH_FFT_P / len;
-        double2 w[4], a[4], bb[4];
-        int i0[4];
+    for (int p = 0; p < 3; ++p) {
+        const int stride = 1 << (3 * p);
+        const int base = (lane / stride) * 8 * stride + lane % stride;
+        double2 v[8];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const int t = lane + 64 * q;
-            const int g = t / half, j = t % half;
-            i0[q] = g * len + j;
-            w[q] = tw[j * step];
-            a[q] = x[i0[q]];
-            bb[q] = x[i0[q] + half];
+        for (int m = 0; m < 8; ++m) v[m] = x[base + m * stride];
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+            const int half = stride << s, step = VH_FFT_P / (2 * half);
+#pragma unroll
+            for (int m = 0; m < 8; ++m) {
+                if (m & (1 << s)) continue;
+                const int j = stride * (m & ((1 << s) - 1)) + lane % stride;   // (base + m stride) % half
+                const double2 w = tw[j * step];
+                const double wy = inverse ? -w.y : w.y;
+                const double2 a = v[m], bb = v[m + (1 << s)];
+                const double tr = w.x * bb.x - wy * bb.y, ti = w.x * bb.y + wy * bb.x;
+                v[m] = make_double2(a.x + tr, a.y + ti);
+                v[m + (1 << s)] = make_double2(a.x - tr, a.y - ti);
+            }
         }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const double wy = inverse ? -w[q].y : w[q].y;
-            const double tr = w[q].x * bb[q].x - wy * bb[q].y, ti = w[q].x * bb[q].y + wy * bb[q].x;
-            x[i0[q]] = make_double2(a[q].x + tr, a[q].y + ti);
-            x[i0[q] + half] = make_double2(a[q].x - tr, a[q].y - ti);
-        }
+        for (int m = 0; m < 8; ++m) x[base + m * stride] = v[m];
         wave_lds_order();
     }
 }
