@@ -717,136 +717,48 @@ __device__ void eval_item(const StudyArgs &a, const Item &it, int item, const Ta
 }
 
 // ---------------------------------------------------------------------------------------------
-// FFT (512-point radix-2 DIT, same butterflies and twiddle indexing as oracle/n4_oracle.c):
-// in-place bit reversal by pair swaps, then one butterfly per thread per stage; two independent
-// transforms share every stage (threads 0-255 and 256-511).
+// FFT (512-point radix-2 DIT, same butterflies and twiddle indexing as oracle/n4_oracle.c) by ONE
+// wave in place in LDS.  The points sit at padded slots fpad(i) (one spare slot per 8), so the
+// strided passes below hit distinct LDS banks.  Only wave-local ordering is needed (a wave's LDS
+// operations complete in issue order; the fences keep the compiler from moving them).
 // ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ void st_butterfly(double2 *x, double2 w, int i0, int i1) {
-    const double2 bb = x[i1];
-    const double tr = w.x * bb.x - w.y * bb.y, ti = w.x * bb.y + w.y * bb.x;
-    const double2 aa = x[i0];
-    x[i0] = make_double2(aa.x + tr, aa.y + ti);
-    x[i1] = make_double2(aa.x - tr, aa.y - ti);
-}
+#define ST_FFT_N (VH_FFT_P + VH_FFT_P / 8)   // padded slots of one transform
+__device__ __forceinline__ int fpad(int i) { return i + (i >> 3); }
 
-__device__ void st_fft(double2 *x, double2 *y, const double2 *tw, bool inverse) {
-    const int t = threadIdx.x;
-    for (int i = t; i < VH_FFT_P; i += ST_TPB) {
-        const int j = (int)(__brev((unsigned)i) >> (32 - 9));
-        if (i < j) {
-            double2 v = x[i]; x[i] = x[j]; x[j] = v;
-            if (y) { v = y[i]; y[i] = y[j]; y[j] = v; }
-        }
-    }
-    __syncthreads();
-    double2 *tgt = t < 256 ? x : y;
-    const int tt = t & 255;
-    const bool act = t < 256 || (y != nullptr && t < 512);
-#pragma unroll 1
-    for (int len = 2; len <= VH_FFT_P; len <<= 1) {
-        if (act) {
-            const int half = len >> 1, step = VH_FFT_P / len;
-            const int g = tt / half, j = tt % half;
-            double2 w = tw[j * step];
-            if (inverse) w.y = -w.y;
-            st_butterfly(tgt, w, g * len + j, g * len + j + half);
-        }
-        __syncthreads();
-    }
-}
+struct FftId {
+    __device__ double2 operator()(int, double2 v) const { return v; }
+};
 
-// The same transform by ONE wave with the 512 points in registers (point n = 64 r + lane in
-// v[r]): the bit reversal is the LDS gather, stages with half < 64 exchange partners by lane
-// shuffles, the last three stay inside a lane.  Identical butterflies, so identical results; no
-// workgroup barriers, and several transforms run on different waves at once.
-__device__ __forceinline__ void wave_butterfly(double2 &lo, double2 &hi, double2 w) {
-    const double tr = w.x * hi.x - w.y * hi.y, ti = w.x * hi.y + w.y * hi.x;
-    const double2 a = lo;
-    lo = make_double2(a.x + tr, a.y + ti);
-    hi = make_double2(a.x - tr, a.y - ti);
-}
-
-__device__ void wave_fft(double2 *x, const double2 *tw, bool inverse) {
-    const int lane = threadIdx.x & 63;
-    const double sgn = inverse ? -1.0 : 1.0;
-    double vr[8], vi[8];
-#pragma unroll
-    for (int r = 0; r < 8; ++r) {
-        const double2 e = x[(int)(__brev((unsigned)(r * 64 + lane)) >> (32 - 9))];
-        vr[r] = e.x;
-        vi[r] = e.y;
-    }
-#pragma unroll
-    for (int sh = 0; sh < 6; ++sh) {
-        const int half = 1 << sh;
-        const double2 wt = tw[(lane & (half - 1)) * (VH_FFT_P / (2 * half))];
-        const double wr = wt.x, wi = wt.y * sgn;
-        const bool upper = (lane & half) != 0;
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            const double pr = __shfl_xor(vr[r], half, 64), pi = __shfl_xor(vi[r], half, 64);
-            const double br = upper ? vr[r] : pr, bi = upper ? vi[r] : pi;
-            const double ar = upper ? pr : vr[r], ai = upper ? pi : vi[r];
-            const double tr = wr * br - wi * bi, ti = wr * bi + wi * br;
-            vr[r] = upper ? ar - tr : ar + tr;
-            vi[r] = upper ? ai - ti : ai + ti;
-        }
-    }
-#pragma unroll
-    for (int sh = 0; sh < 3; ++sh) {
-        const int hr = 1 << sh;
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-            if (r & hr) continue;
-            const double2 wt = tw[((r % hr) * 64 + lane) * (VH_FFT_P / (128 * hr))];
-            const double wr = wt.x, wi = wt.y * sgn;
-            const double br = vr[r + hr], bi = vi[r + hr];
-            const double tr = wr * br - wi * bi, ti = wr * bi + wi * br;
-            const double ar = vr[r], ai = vi[r];
-            vr[r] = ar + tr;
-            vi[r] = ai + ti;
-            vr[r + hr] = ar - tr;
-            vi[r + hr] = ai - ti;
-        }
-    }
-#pragma unroll
-    for (int r = 0; r < 8; ++r) x[r * 64 + lane] = make_double2(vr[r], vi[r]);
-}
-
-// The same transform by ONE wave in place in LDS: in-place bit reversal by pair swaps, then the
-// 9 radix-2 stages as 3 register passes; identical butterflies and twiddle indexing (so
-// identical results), wave-local ordering only (a wave's LDS operations complete in issue order;
-// the fences keep the compiler from moving them), and only a handful of live registers -- the
-// register-resident form spills inside this large kernel.
 __device__ __forceinline__ void wave_lds_order() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ void wave_fft_lds(double2 *x, const double2 *tw, bool inverse) {
+// The 9 stages run as 3 register passes of 3: in pass p a lane owns the 8 points
+// base + m * 8^p (m < 8), which the stages of half-length 8^p, 2 * 8^p, 4 * 8^p pair only among
+// themselves.  Pass 0 gathers in bit-reversed order (all loads of the wave issue before its
+// stores) through pro(i, v); pass 2 stores epi(i, v) -- the elementwise steps around a transform
+// ride on its first and last pass.
+template <class Pro, class Epi>
+__device__ void wave_fft_lds(double2 *x, const double2 *tw, bool inverse, const Pro &pro,
+                             const Epi &epi) {
     const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int q = 0; q < VH_FFT_P / 64; ++q) {
-        const int i = lane + 64 * q;
-        const int j = (int)(__brev((unsigned)i) >> (32 - 9));
-        if (i < j) {
-            const double2 v = x[i];
-            x[i] = x[j];
-            x[j] = v;
-        }
-    }
-    wave_lds_order();
-    // the 9 stages in 3 passes of 3: in pass p a lane owns the 8 points base + m * 8^p (m < 8),
-    // which the stages of half-length 8^p, 2 * 8^p, 4 * 8^p pair only among themselves, so the
-    // pass runs its 3 stages in registers (same butterflies, same twiddles, same order)
 #pragma unroll 1
     for (int p = 0; p < 3; ++p) {
         const int stride = 1 << (3 * p);
         const int base = (lane / stride) * 8 * stride + lane % stride;
         double2 v[8];
+        if (p == 0) {
 #pragma unroll
-        for (int m = 0; m < 8; ++m) v[m] = x[base + m * stride];
+            for (int m = 0; m < 8; ++m) {
+                const int src = (int)(__brev((unsigned)(base + m)) >> (32 - 9));
+                v[m] = pro(src, x[fpad(src)]);
+            }
+        } else {
+#pragma unroll
+            for (int m = 0; m < 8; ++m) v[m] = x[fpad(base + m * stride)];
+        }
 #pragma unroll
         for (int s = 0; s < 3; ++s) {
             const int half = stride << s, step = VH_FFT_P / (2 * half);
@@ -862,8 +774,12 @@ __device__ void wave_fft_lds(double2 *x, const double2 *tw, bool inverse) {
                 v[m + (1 << s)] = make_double2(a.x - tr, a.y - ti);
             }
         }
+        if (p == 2) {
 #pragma unroll
-        for (int m = 0; m < 8; ++m) x[base + m * stride] = v[m];
+            for (int m = 0; m < 8; ++m) v[m] = epi(base + m * stride, v[m]);
+        }
+#pragma unroll
+        for (int m = 0; m < 8; ++m) x[fpad(base + m * stride)] = v[m];
         wave_lds_order();
     }
 }
@@ -975,8 +891,8 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
     ring.nr = 0;
     double *const Wk3 = reinterpret_cast<double *>(smem + a.o_wk);
     // emap scratch: V (= U = NUM), F, DEN, twiddles, then the histogram copies
-    double2 *V = reinterpret_cast<double2 *>(scr), *F = V + VH_FFT_P, *DEN = F + VH_FFT_P;
-    double2 *TW = DEN + VH_FFT_P;
+    double2 *V = reinterpret_cast<double2 *>(scr), *F = V + ST_FFT_N, *DEN = F + ST_FFT_N;
+    double2 *TW = DEN + ST_FFT_N;
     unsigned long long *Hc = reinterpret_cast<unsigned long long *>(TW + VH_FFT_P / 2);
     const int bins = a.bins;
 
@@ -1153,64 +1069,60 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
             // ---- emap (same arithmetic as n4.hip k_n4_emap) ----
             {
                 const int P = VH_FFT_P, off = (P - bins) / 2;
+                const float sFWHM = a.fwhm / slope;
+                const float ef = (float)(4.0 * LN2 / (double)(sFWHM * sFWHM));
+                const float sf = (float)(2.0 * sqrt(LN2 / PI_D) / (double)sFWHM);
                 for (int i = t; i < P / 2; i += ST_TPB) TW[i] = a.tw[i];
-                for (int i = t; i < P; i += ST_TPB) {
+                for (int i = t; i < P; i += ST_TPB) {   // histogram series and Gaussian kernel
                     const int h = i - off;
                     unsigned long long s = 0ull;
                     if (h >= 0 && h < bins)
                         for (int q = 0; q < ST_HC; ++q) s += Hc[q * VH_MAX_BINS + h];
-                    V[i] = make_double2((double)s * (1.0 / 4294967296.0), 0.0);
-                    F[i] = make_double2(0.0, 0.0);
-                }
-                __syncthreads();
-                const float sFWHM = a.fwhm / slope;
-                const float ef = (float)(4.0 * LN2 / (double)(sFWHM * sFWHM));
-                const float sf = (float)(2.0 * sqrt(LN2 / PI_D) / (double)sFWHM);
-                for (int i = t; i <= P / 2; i += ST_TPB) {
+                    V[fpad(i)] = make_double2((double)s * (1.0 / 4294967296.0), 0.0);
+                    double fx;
                     if (i == 0) {
-                        F[0].x = (double)sf;
+                        fx = (double)sf;
                     } else if (i == P / 2) {
-                        F[i].x = (double)sf * exp(-0.25 * (double)((float)P * (float)P) * (double)ef);
+                        fx = (double)sf * exp(-0.25 * (double)((float)P * (float)P) * (double)ef);
                     } else {
-                        const float nf = (float)i;
-                        const double v = (double)(sf * expf_cr(-(nf * nf) * ef));
-                        F[i].x = v;
-                        F[P - i].x = v;
+                        const float nf = (float)(i < P / 2 ? i : P - i);
+                        fx = (double)(sf * expf_cr(-(nf * nf) * ef));
                     }
+                    F[fpad(i)] = make_double2(fx, 0.0);
                 }
                 __syncthreads();
-                if (wv < 2) wave_fft_lds(wv ? F : V, TW, false);
+                if (wv < 2) wave_fft_lds(wv ? F : V, TW, false, FftId(), FftId());
                 __syncthreads();
-                for (int i = t; i < P; i += ST_TPB) {
-                    const double fa = F[i].x, fb = F[i].y;
-                    const double g = fa / ((fa * fa - (-fb) * fb) + (double)a.noise);
-                    V[i] = make_double2(V[i].x * g, V[i].y * g);
+                if (wv == 0) {   // Wiener filter (first pass), inverse, clamp and the moment series (last pass)
+                    const double noise = (double)a.noise;
+                    wave_fft_lds(V, TW, true,
+                        [&](int i, double2 v) {
+                            const double2 f = F[fpad(i)];
+                            const double fa = f.x, fb = f.y;
+                            const double g = fa / ((fa * fa - (-fb) * fb) + noise);
+                            return make_double2(v.x * g, v.y * g);
+                        },
+                        [&](int i, double2 v) {
+                            const double ur = v.x > 0.0 ? v.x : 0.0;
+                            const float c = bmin + ((float)i - (float)off) * slope;
+                            DEN[fpad(i)] = make_double2(ur, 0.0);
+                            return make_double2((double)c * ur, 0.0);
+                        });
                 }
                 __syncthreads();
-                if (wv == 0) wave_fft_lds(V, TW, true);
-                __syncthreads();
-                for (int i = t; i < P; i += ST_TPB) {
-                    const double ur = V[i].x > 0.0 ? V[i].x : 0.0;
-                    const float c = bmin + ((float)i - (float)off) * slope;
-                    V[i] = make_double2((double)c * ur, 0.0);
-                    DEN[i] = make_double2(ur, 0.0);
+                if (wv < 2) {   // each series: forward, times the kernel's transform (last pass), inverse
+                    double2 *x = wv ? DEN : V;
+                    wave_fft_lds(x, TW, false, FftId(), [&](int i, double2 v) {
+                        const double2 f = F[fpad(i)];
+                        const double fa = f.x, fb = f.y;
+                        return make_double2(v.x * fa - v.y * fb, v.x * fb + v.y * fa);
+                    });
+                    wave_fft_lds(x, TW, true, FftId(), FftId());
                 }
-                __syncthreads();
-                if (wv < 2) wave_fft_lds(wv ? DEN : V, TW, false);
-                __syncthreads();
-                for (int i = t; i < P; i += ST_TPB) {
-                    const double fa = F[i].x, fb = F[i].y;
-                    double2 x = V[i];
-                    V[i] = make_double2(x.x * fa - x.y * fb, x.x * fb + x.y * fa);
-                    x = DEN[i];
-                    DEN[i] = make_double2(x.x * fa - x.y * fb, x.x * fb + x.y * fa);
-                }
-                __syncthreads();
-                if (wv < 2) wave_fft_lds(wv ? DEN : V, TW, true);
                 __syncthreads();
                 for (int i = t; i < bins; i += ST_TPB) {
-                    const double d = DEN[i + off].x;
-                    sE[i] = d != 0.0 ? (float)(V[i + off].x / d) : 0.0f;
+                    const double d = DEN[fpad(i + off)].x;
+                    sE[i] = d != 0.0 ? (float)(V[fpad(i + off)].x / d) : 0.0f;
                 }
                 __syncthreads();
             }
@@ -1363,7 +1275,7 @@ static bool study_layout(const vh_batch *b, const vh_n4_params &prm, StudyLayout
     }
     // refinement temporaries: two lattices of the next level (<= 8x the current)
     const size_t refine = 2 * sizeof(float) * (size_t)nlat_max + 64;
-    const size_t emap = sizeof(double2) * (3 * VH_FFT_P + VH_FFT_P / 2) +
+    const size_t emap = sizeof(double2) * (3 * ST_FFT_N + VH_FFT_P / 2) +
                         sizeof(unsigned long long) * ST_HC * VH_MAX_BINS;
     const bool geom_ok = s_cap <= 64 * ST_SO;   // one ring row's stage-1 outputs fit the lanes
     s_cap = std::max(s_cap, 64);
