@@ -741,7 +741,7 @@ __device__ __forceinline__ void wave_lds_order() {
 // stores) through pro(i, v); pass 2 stores epi(i, v) -- the elementwise steps around a transform
 // ride on its first and last pass.
 template <class Pro, class Epi>
-__device__ void wave_fft_lds(double2 *x, const double2 *tw, bool inverse, const Pro &pro,
+__device__ __forceinline__ void wave_fft_lds(double2 *x, const double2 *tw, bool inverse, const Pro &pro,
                              const Epi &epi) {
     const int lane = threadIdx.x & 63;
 #pragma unroll 1
@@ -940,7 +940,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
     }
     int cur = 0;   // P1b[cur] holds the last evaluated field
 #ifdef ST_PROF
-    unsigned long long st_prof[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_t0 = clock64();
+    unsigned long long st_prof[13] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_t0 = clock64();
     const unsigned long long st_w0 = wall_clock64(), st_c0 = clock64();
 #endif
     for (int L = 0; L < a.nlev; ++L) {
@@ -1072,7 +1072,8 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                 const float sFWHM = a.fwhm / slope;
                 const float ef = (float)(4.0 * LN2 / (double)(sFWHM * sFWHM));
                 const float sf = (float)(2.0 * sqrt(LN2 / PI_D) / (double)sFWHM);
-                for (int i = t; i < P / 2; i += ST_TPB) TW[i] = a.tw[i];
+                static_assert(VH_FFT_P / 2 <= ST_TPB, "one twiddle per thread");
+                const double2 twv = t < P / 2 ? a.tw[t] : make_double2(0.0, 0.0);   // in flight
                 for (int i = t; i < P; i += ST_TPB) {   // histogram series and Gaussian kernel
                     const int h = i - off;
                     unsigned long long s = 0ull;
@@ -1090,19 +1091,22 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                     }
                     F[fpad(i)] = make_double2(fx, 0.0);
                 }
+                if (t < P / 2) TW[t] = twv;
                 __syncthreads();
+                ST_MARK(9);
                 if (wv < 2) wave_fft_lds(wv ? F : V, TW, false, FftId(), FftId());
                 __syncthreads();
+                ST_MARK(10);
                 if (wv == 0) {   // Wiener filter (first pass), inverse, clamp and the moment series (last pass)
                     const double noise = (double)a.noise;
                     wave_fft_lds(V, TW, true,
-                        [&](int i, double2 v) {
+                        [=](int i, double2 v) {
                             const double2 f = F[fpad(i)];
                             const double fa = f.x, fb = f.y;
                             const double g = fa / ((fa * fa - (-fb) * fb) + noise);
                             return make_double2(v.x * g, v.y * g);
                         },
-                        [&](int i, double2 v) {
+                        [=](int i, double2 v) {
                             const double ur = v.x > 0.0 ? v.x : 0.0;
                             const float c = bmin + ((float)i - (float)off) * slope;
                             DEN[fpad(i)] = make_double2(ur, 0.0);
@@ -1110,9 +1114,10 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                         });
                 }
                 __syncthreads();
+                ST_MARK(11);
                 if (wv < 2) {   // each series: forward, times the kernel's transform (last pass), inverse
                     double2 *x = wv ? DEN : V;
-                    wave_fft_lds(x, TW, false, FftId(), [&](int i, double2 v) {
+                    wave_fft_lds(x, TW, false, FftId(), [=](int i, double2 v) {
                         const double2 f = F[fpad(i)];
                         const double fa = f.x, fb = f.y;
                         return make_double2(v.x * fa - v.y * fb, v.x * fb + v.y * fa);
@@ -1120,6 +1125,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                     wave_fft_lds(x, TW, true, FftId(), FftId());
                 }
                 __syncthreads();
+                ST_MARK(12);
                 for (int i = t; i < bins; i += ST_TPB) {
                     const double d = DEN[fpad(i + off)].x;
                     sE[i] = d != 0.0 ? (float)(V[fpad(i + off)].x / d) : 0.0f;
@@ -1231,8 +1237,9 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                clock64() - st_c0, __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)));
     if (t == 0 && blockIdx.x == 0)
         printf("ST_PROF den %llu ctrl %llu hist %llu emap %llu fit %llu latP1 %llu eval %llu loop %llu "
-               "refine %llu\n", st_prof[0], st_prof[1], st_prof[2], st_prof[3], st_prof[4],
-               st_prof[5], st_prof[6], st_prof[7], st_prof[8]);
+               "refine %llu | emap: init %llu fwd %llu wiener %llu conv %llu sE %llu\n", st_prof[0],
+               st_prof[1], st_prof[2], st_prof[3], st_prof[4], st_prof[5], st_prof[6], st_prof[7],
+               st_prof[8], st_prof[9], st_prof[10], st_prof[11], st_prof[12], st_prof[3]);
 #endif
     // final field's P1 for k_n4_final
     const double *P1f = cur ? P1b1 : P1b0;
