@@ -13,13 +13,13 @@ constructor crashes at Vent_Analysis.py:166 because vox is '' -- pass vox to avo
 """
 from __future__ import annotations
 
-import os
 import pickle
 
 import numpy as np
 
 from . import CI
 from . import _lib
+from . import ingest
 
 __all__ = ["Vent_Analysis"]
 
@@ -108,39 +108,23 @@ class Vent_Analysis:
             self.vox = [float(v) for v in vox]
         self.metadata['LungVolume'] = np.sum(self.mask == 1) * np.prod(np.divide(self.vox, 10)) / 1000
 
-    # ---- DICOM ingest (next row; needs pydicom, absent in this image) --------
+    # ---- DICOM ingest (vent_analysis_amd.ingest, no pydicom needed) -------
     def openSingleDICOM(self, dicom_path):
-        import pydicom as dicom   # noqa: F401  (raises ImportError here like any missing module)
-        ds = dicom.dcmread(dicom_path)
-        arr = np.transpose(ds.pixel_array, (1, 2, 0))
+        """Vent_Analysis.py:169-181: (dataset, pixel_array transposed to (rows, cols, frames))."""
+        ds, arr = ingest.open_single_dicom(dicom_path)
         print(f'\033[32mI opened a DICOM of shape {arr.shape}\033[37m')
         return ds, arr
 
     def openDICOMfolder(self, maskFolder):
-        import pydicom as dicom
-        files = [f for f in sorted(os.listdir(maskFolder)) if f.endswith('.dcm')]
-        ds = dicom.dcmread(os.path.join(maskFolder, files[0]))
-        mask = np.zeros((ds.pixel_array.shape[0], ds.pixel_array.shape[1], len(files)))
-        for k, f in enumerate(files):
-            ds = dicom.dcmread(os.path.join(maskFolder, f))
-            mask[:, :, k] = ds.pixel_array
+        """Vent_Analysis.py:184-196: the folder's .dcm slices (sorted) stacked as float64."""
+        ds, mask = ingest.open_dicom_folder(maskFolder)
         print(f'\033[32mI built a mask of shape {mask.shape}\033[37m')
         return ds, mask
 
     def pullDICOMHeader(self):
-        for elem in ['PatientName', 'PatientAge', 'PatientBirthDate', 'PatientSize',
-                     'PatientWeight', 'PatientSex', 'StudyDate', 'StudyTime', 'SeriesTime']:
-            try:
-                self.metadata[elem] = self.ds[elem].value
-            except Exception:
-                self.metadata[elem] = ''
-        for k in range(100):
-            try:
-                self.vox = self.ds[0x5200, 0x9230][k]['PixelMeasuresSequence'][0].PixelSpacing
-                break
-            except Exception:
-                pass
-        self.vox = [float(self.vox[0]), float(self.vox[1]), float(self.ds.SpacingBetweenSlices)]
+        """Vent_Analysis.py:198-223: patient/study elements into metadata, vox from the header."""
+        meta, self.vox = ingest.header_metadata(self.ds)
+        self.metadata.update(meta)
         self.metadata['LungVolume'] = np.sum(self.mask == 1) * np.prod(np.divide(self.vox, 10)) / 1000
 
     # ---- hot path ---------------------------------------------------------------------------
