@@ -13,6 +13,7 @@ constructor crashes at Vent_Analysis.py:166 because vox is '' -- pass vox to avo
 """
 from __future__ import annotations
 
+import os
 import pickle
 
 import numpy as np
@@ -20,6 +21,7 @@ import numpy as np
 from . import CI
 from . import _lib
 from . import ingest
+from . import nifti
 
 __all__ = ["Vent_Analysis"]
 
@@ -260,9 +262,23 @@ class Vent_Analysis:
         for attr, value in pickle_dict.items():
             setattr(self, attr, value)
 
-    def exportNifti(self, *a, **k):
-        raise NotImplementedError("NIfTI export (Vent_Analysis.py:273-290) is outside the GPU hot "
-                                  "path (SURVEY §8f); use build4DdataArray() with nibabel")
+    def exportNifti(self, filepath=None, fileName=None):
+        """Vent_Analysis.py:273-290: build4DdataArray() as <fileName>_dataArray.nii (NIfTI-1,
+        identity affine; vent_analysis_amd.nifti, no nibabel needed).  The reference opens a
+        folder dialog when filepath is None; here filepath is required."""
+        print('\033[34mexportNifti method called...\033[37m')
+        if filepath is None:
+            raise ValueError("exportNifti: filepath is required (the reference asks with a "
+                             "folder dialog)")
+        if fileName is None:
+            fileName = str(self.metadata['PatientName']).replace('^', '_')
+        try:
+            dataArray = self.build4DdataArray()
+            savepath = os.path.join(filepath, fileName + '_dataArray.nii')
+            nifti.save(savepath, dataArray, affine=np.eye(4))
+            print(f'\033[32mNifti HPvent array saved to {savepath}\033[37m')
+        except Exception:
+            print('\033[31mCould not Export 4D HPvent mask Nifti...\033[37m')
 
     def exportDICOM(self, *a, **k):
         raise NotImplementedError("defect-overlay DICOM export (Vent_Analysis.py:381-428) is a "
