@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define VH_ABI_VERSION 1
+#define VH_ABI_VERSION 2
 
 /* status codes */
 #define VH_OK 0
@@ -52,6 +52,12 @@ typedef struct {
     int32_t n_bins;          /* 200 histogram bins (<= 256) */
     float wiener_noise;      /* 0.01 */
     float fwhm;              /* 0.15 bias-field FWHM */
+    int32_t conv_mode;       /* 0 (default): ITK's convergence measure -- the float (RealType) Welford
+                                recurrence over the masked voxels in raster order, whose rounding
+                                drift sets SimpleITK's iteration counts; a serial recurrence.
+                                1: the exact coefficient of variation it approximates (double,
+                                order-free; faster, but stops at different iterations than
+                                SimpleITK -- see DESIGN.md §6) */
 } vh_n4_params;
 
 /* Per-volume scalars of calculate_VDP / calculate_CI (metadata keys of Vent_Analysis.py:78-103). */

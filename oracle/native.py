@@ -33,11 +33,11 @@ class N4Params(ct.Structure):
     _fields_ = [("n_levels", ct.c_int32), ("max_iters", ct.c_int32 * 8),
                 ("conv_threshold", ct.c_float), ("ncp", ct.c_int32 * 3),
                 ("spline_order", ct.c_int32), ("n_bins", ct.c_int32),
-                ("wiener_noise", ct.c_float), ("fwhm", ct.c_float)]
+                ("wiener_noise", ct.c_float), ("fwhm", ct.c_float), ("conv_mode", ct.c_int32)]
 
 
 def n4_params(max_iters=(50, 50, 50, 50), conv_threshold=0.001, ncp=(4, 4, 4), n_bins=200,
-              wiener_noise=0.01, fwhm=0.15):
+              wiener_noise=0.01, fwhm=0.15, conv_mode=0):
     p = N4Params()
     p.n_levels = len(max_iters)
     for i, m in enumerate(max_iters):
@@ -49,6 +49,7 @@ def n4_params(max_iters=(50, 50, 50, 50), conv_threshold=0.001, ncp=(4, 4, 4), n
     p.n_bins = n_bins
     p.wiener_noise = wiener_noise
     p.fwhm = fwhm
+    p.conv_mode = conv_mode
     return p
 
 
@@ -69,6 +70,27 @@ def n4(I, mask, **kw):
                          _ptr(out, ct.c_float), _ptr(its, ct.c_int32), _ptr(conv, ct.c_float))
     if rc:
         raise RuntimeError(f"n4_oracle rc={rc}")
+    return out, its, conv
+
+
+def n4_itk(I, mask, nonpos_raw=False, threads=1, **kw):
+    """n4_oracle.c mode 1: ITK-like float (RealType) arithmetic in raster order, one thread.  Only
+    for measuring how far the build spec's precision choices sit from an ITK-like float pipeline
+    (DESIGN.md §6); the GPU is never compared with it bit for bit."""
+    I = np.ascontiguousarray(I, dtype=np.float32)
+    m = np.ascontiguousarray(mask, dtype=np.uint8)
+    prm = n4_params(**kw)
+    out = np.empty_like(I)
+    its = np.zeros(prm.n_levels, np.int32)
+    conv = np.zeros(prm.n_levels, np.float32)
+    lib().n4_oracle_itk.restype = ct.c_int
+    rc = lib().n4_oracle_itk(_ptr(I, ct.c_float), _ptr(m, ct.c_uint8), ct.c_int64(I.shape[0]),
+                             ct.c_int64(I.shape[1]), ct.c_int64(I.shape[2]), ct.byref(prm),
+                             ct.c_int(1 if nonpos_raw else 0), ct.c_int(threads),
+                             _ptr(out, ct.c_float),
+                             _ptr(its, ct.c_int32), _ptr(conv, ct.c_float))
+    if rc:
+        raise RuntimeError(f"n4_oracle_itk rc={rc}")
     return out, its, conv
 
 

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_status_strings():
     L = _lib.lib()
-    assert L.vh_abi_version() == 1
+    assert L.vh_abi_version() == 2
     assert L.vh_status_string(0) == b"ok"
     assert b"maximum radius" in L.vh_status_string(_lib.VH_ERR_MAXRADIUS)
 
@@ -55,6 +55,7 @@ def test_default_params_are_simpleitk_defaults():
     assert abs(p.conv_threshold - 0.001) < 1e-7 and list(p.ncp) == [4, 4, 4]
     assert p.n_bins == 200 and p.spline_order == 3
     assert abs(p.wiener_noise - 0.01) < 1e-7 and abs(p.fwhm - 0.15) < 1e-7
+    assert p.conv_mode == 0   # ITK's float Welford convergence measure (reference semantics)
 
 
 def test_missing_library_fails_loudly(monkeypatch):

@@ -103,16 +103,39 @@ def test_ci_errors():
         native.ci(np.ones((40, 40, 24), np.uint8), table, (1.5, 1.5, 10.0))
 
 
+def ulps(a, b):
+    """Distance in float32 units in the last place (same-sign values)."""
+    ia = np.ascontiguousarray(a, np.float32).view(np.int32).astype(np.int64)
+    ib = np.ascontiguousarray(b, np.float32).view(np.int32).astype(np.int64)
+    return np.abs(ia - ib)
+
+
+def assert_n4_matches(out, its, conv, ref, its_ref, conv_ref, conv_mode, tag):
+    """GPU N4 against the build-spec oracle (oracle/n4_oracle.c S1-S9).  U = L0 - B is bit-identical
+    after every iteration, so the iteration counts and convergence values are identical; the output
+    I / (float)exp((double)B) may differ by one float ulp only where OCML's and glibc's double exp
+    round differently across a float midpoint (p ~ 2^-28 per voxel).  Tolerance: 1 ulp (north_star:
+    1e-5 relative)."""
+    assert list(its) == list(its_ref), (tag, list(its), list(its_ref))
+    d = ulps(out, ref)
+    assert d.max() <= 1, (tag, int(d.max()), int((d > 0).sum()))
+    assert rel(out, ref) < 1e-5, tag
+    if conv_mode == 0:   # float Welford: the same float recurrence over the same values
+        assert np.array_equal(np.float32(conv), np.float32(conv_ref)), (tag, conv, conv_ref)
+    else:                # exact CoV: double sums in a different order
+        assert np.allclose(conv, conv_ref, rtol=1e-9), (tag, conv, conv_ref)
+
+
+@pytest.mark.parametrize("conv_mode", [0, 1])
 @pytest.mark.parametrize("shape,seed", [((64, 64, 16), 0), ((128, 128, 24), 0), ((96, 112, 20), 5),
                                         ((64, 64, 64), 6)])
-def test_n4_vs_oracle(shape, seed):
+def test_n4_vs_oracle(shape, seed, conv_mode):
+    """Host entry point vh_n4 (one study: the per-iteration sweep driver)."""
     X, M = synth_volume(*shape, seed)
-    ref, its_ref, conv_ref = native.n4(X, M)
-    out, its, conv = _lib.n4(X, M.astype(np.uint8))
-    assert list(its[0]) == list(its_ref)
+    ref, its_ref, conv_ref = native.n4(X, M, conv_mode=conv_mode)
+    out, its, conv = _lib.n4(X, M.astype(np.uint8), conv_mode=conv_mode)
     assert np.all((its[0] >= 1) & (its[0] <= 50))
-    assert rel(out[0], ref) < 1e-5
-    assert np.allclose(conv[0], conv_ref, rtol=1e-4)
+    assert_n4_matches(out[0], its[0], conv[0], ref, its_ref, conv_ref, conv_mode, (shape, seed))
 
 
 def test_batch_pipeline_end_to_end():
@@ -210,16 +233,33 @@ def test_class_full_pipeline_with_n4():
 
 
 # ---- ragged / degenerate shapes and full-size properties -------------------------------------
-@pytest.mark.parametrize("shape,seed", [((37, 45, 7), 11), ((12, 70, 9), 12), ((130, 20, 3), 13)])
-def test_n4_ragged_shapes_vs_oracle(shape, seed):
-    """Rows not a multiple of the 16-row segment / 32-row bitmap word, columns not a multiple of
-    the 64-column tile or the 128-column fit tile."""
+RAGGED = [((37, 45, 7), 11), ((12, 70, 9), 12), ((12, 70, 9), 13), ((130, 20, 3), 13),
+          ((5, 90, 12), 14), ((70, 5, 30), 15), ((66, 66, 2), 16), ((129, 33, 5), 17),
+          ((40, 40, 40), 18), ((31, 97, 11), 19), ((64, 65, 4), 20), ((65, 64, 17), 21),
+          ((100, 30, 23), 22), ((23, 100, 3), 23), ((48, 48, 9), 24), ((80, 24, 24), 25),
+          ((17, 17, 17), 26), ((90, 110, 6), 27), ((127, 61, 8), 28), ((33, 128, 13), 29)]
+
+
+@pytest.mark.parametrize("conv_mode", [0, 1])
+@pytest.mark.parametrize("driver", ["sweep", "study"])
+@pytest.mark.parametrize("shape,seed", RAGGED, ids=lambda v: "x".join(map(str, v)) if isinstance(v, tuple) else str(v))
+def test_n4_ragged_shapes_vs_oracle(shape, seed, driver, conv_mode):
+    """Rows past one 64-row slot, columns not a multiple of the 64-column tile, 2- and 3-slice
+    volumes, single-row-slot studies, masks touching the borders; both drivers, both convergence
+    measures.  (12x70x9 seed 13 is the round-1 case whose 1-ulp U differences flipped ITK's bin
+    minimum; with both sides evaluating S1-S9 it matches like every other case.)"""
     X, M = synth_volume(*shape, seed)
-    assert M.sum() > 10
-    ref, its_ref, _ = native.n4(X, M)
-    out, its, _ = _lib.n4(X, M.astype(np.uint8))
-    assert list(its[0]) == list(its_ref)
-    assert rel(out[0], ref) < 1e-5
+    if M.sum() < 4:
+        pytest.skip("mask too small for the generator at this shape")
+    ref, its_ref, conv_ref = native.n4(X, M, conv_mode=conv_mode)
+    try:
+        n4, d, _, lb, res = _run_batch(X[None], M.astype(np.uint8)[None], driver, conv_mode=conv_mode)
+    except ValueError as e:   # the study driver holds a study's state in LDS: not every shape fits
+        if driver == "study" and "LDS budget" in str(e):
+            pytest.skip(str(e))
+        raise
+    assert_n4_matches(n4[0], res[0].n4_iters[:4], res[0].n4_conv[:4], ref, its_ref, conv_ref,
+                      conv_mode, (shape, seed, driver))
 
 
 def _single_slice(R, C, seed):
@@ -380,38 +420,31 @@ def _run_batch(hp, mk, mode, **kw):
     return out
 
 
+@pytest.mark.parametrize("conv_mode", [0, 1])
 @pytest.mark.parametrize("shape,nb,seed", [((128, 128, 24), 3, 0), ((96, 112, 20), 2, 5),
                                            ((64, 64, 32), 2, 6), ((37, 45, 7), 2, 11),
-                                           ((12, 70, 9), 1, 12), ((130, 20, 3), 2, 13)])
-def test_n4_study_vs_oracle(shape, nb, seed):
-    """n4_mode=2 (k_n4_study) against the C oracle: relative error <= 1e-5 on N4HPvent and the
-    same iteration count at every level, on bench-size and ragged shapes (rows past one 64-row
-    slot, columns not a multiple of the 64-column tile, 3-slice volumes).
-
-    Not included: the 12x70x9 study of seed 13.  Single iterations of it match the oracle bit for
-    bit, but ITK's bin-range rule (the first masked voxel never lowers the minimum) is a
-    discontinuity, and 1-ulp float differences in U (separable float evaluation on the GPU, 64-term
-    double sum in the oracle) flip it in some iterations of that 12-row volume: after 30
-    fixed iterations BOTH GPU drivers differ from the oracle by 2.7e-5 while agreeing with each
-    other to 2e-7, and the full default run ends at 1.8e-5 (study) / 1.1e-6 (sweeps)."""
+                                           ((12, 70, 9), 2, 12), ((130, 20, 3), 2, 13)])
+def test_n4_study_vs_oracle(shape, nb, seed, conv_mode):
+    """n4_mode=2 (k_n4_study), several studies per launch, against the C oracle."""
     hp, mk = synth_batch(*shape, nb, base_seed=seed)
-    n4, d, _, lb, res = _run_batch(hp, mk, "study")
+    n4, d, _, lb, res = _run_batch(hp, mk, "study", conv_mode=conv_mode)
     for b in range(nb):
-        ref, its_ref, conv_ref = native.n4(hp[b], mk[b])
-        assert list(res[b].n4_iters[:4]) == list(its_ref)
-        assert rel(n4[b], ref) < 1e-5
-        assert np.allclose(np.array(res[b].n4_conv[:4]), conv_ref, rtol=1e-4)
+        ref, its_ref, conv_ref = native.n4(hp[b], mk[b], conv_mode=conv_mode)
+        assert_n4_matches(n4[b], res[b].n4_iters[:4], res[b].n4_conv[:4], ref, its_ref, conv_ref,
+                          conv_mode, (shape, seed, b))
 
 
-def test_n4_study_deterministic_and_close_to_sweeps():
+def test_n4_study_deterministic_and_equal_to_sweeps():
+    """Both drivers evaluate S1-S9 operation for operation: identical outputs, not just close."""
     hp, mk = synth_batch(128, 128, 24, 4, base_seed=20)
     a = _run_batch(hp, mk, "study")
     b = _run_batch(hp, mk, "study")
     s = _run_batch(hp, mk, "sweep")
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+    assert np.array_equal(a[0], s[0]) and np.array_equal(a[1], s[1])
     for v in range(4):
         assert list(a[4][v].n4_iters[:4]) == list(s[4][v].n4_iters[:4])
-        assert rel(a[0][v], s[0][v]) < 1e-5
+        assert a[4][v].n4_conv[:4] == s[4][v].n4_conv[:4]
 
 
 def test_n4_study_empty_mask_in_batch():

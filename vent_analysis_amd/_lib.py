@@ -25,7 +25,7 @@ class N4Params(ct.Structure):
     _fields_ = [("n_levels", ct.c_int32), ("max_iters", ct.c_int32 * 8),
                 ("conv_threshold", ct.c_float), ("ncp", ct.c_int32 * 3),
                 ("spline_order", ct.c_int32), ("n_bins", ct.c_int32),
-                ("wiener_noise", ct.c_float), ("fwhm", ct.c_float)]
+                ("wiener_noise", ct.c_float), ("fwhm", ct.c_float), ("conv_mode", ct.c_int32)]
 
 
 class VdpResult(ct.Structure):
@@ -171,7 +171,9 @@ def device_count() -> int:
 
 
 def n4_params(max_iters=(50, 50, 50, 50), conv_threshold=0.001, ncp=(4, 4, 4), n_bins=200,
-              wiener_noise=0.01, fwhm=0.15) -> N4Params:
+              wiener_noise=0.01, fwhm=0.15, conv_mode=0) -> N4Params:
+    """SimpleITK N4BiasFieldCorrectionImageFilter defaults (Vent_Analysis.py:330).  conv_mode 0 is
+    ITK's float Welford convergence measure (reference iteration counts); 1 the exact CoV."""
     p = N4Params()
     lib().vh_n4_default_params(ct.byref(p))
     p.n_levels = len(max_iters)
@@ -183,6 +185,7 @@ def n4_params(max_iters=(50, 50, 50, 50), conv_threshold=0.001, ncp=(4, 4, 4), n
     p.n_bins = n_bins
     p.wiener_noise = wiener_noise
     p.fwhm = fwhm
+    p.conv_mode = int(conv_mode)
     return p
 
 

@@ -101,7 +101,7 @@ static void batch_free(vh_batch *b) {
     dfree(b->d_sc); dfree(b->d_part); dfree(b->d_keys0); dfree(b->d_keys1); dfree(b->d_tilecnt);
     dfree(b->d_cohort);
     dfree(b->d_L0); dfree(b->d_lat); dfree(b->d_E);
-    dfree(b->d_fitpart); dfree(b->d_rowstart); dfree(b->d_rowmask); dfree(b->d_P1); dfree(b->d_num); dfree(b->d_den); dfree(b->d_T);
+    dfree(b->d_numfix); dfree(b->d_rowstart); dfree(b->d_rowmask); dfree(b->d_rrank); dfree(b->d_D); dfree(b->d_P1); dfree(b->d_den); dfree(b->d_T);
     dfree(b->d_U); dfree(b->d_ridx); dfree(b->d_cp); dfree(b->d_cvol); dfree(b->d_hpart); dfree(b->d_cpart); dfree(b->d_st); dfree(b->d_nactive); dfree(b->d_tabs); dfree(b->d_twiddle); dfree(b->d_study_lv);
     dfree(b->d_bitmap); dfree(b->d_ci_list); dfree(b->d_ci_shell); dfree(b->d_ci_hist);
     delete b;
@@ -157,6 +157,20 @@ static void batch_upload(vh_batch *b, const float *hp, const uint8_t *mask) {
     HIP_TRY(hipStreamSynchronize(st));
 }
 
+static void check_n4_params(const vh_batch *b, const vh_n4_params &p) {
+    if (p.n_levels < 1 || p.n_levels > VH_MAX_LEVELS || p.spline_order != 3 || p.n_bins < 2 ||
+        p.n_bins > VH_MAX_BINS || p.ncp[0] < 4 || p.ncp[1] < 4 || p.ncp[2] < 4 || b->Z < 2 ||
+        p.conv_mode < 0 || p.conv_mode > 1)
+        throw VhError{VH_ERR_ARG, "unsupported N4 parameters (spline order 3, bins <= 256, ncp >= 4, "
+                                  "Z >= 2, conv_mode 0 or 1)"};
+    int tot = 0;
+    for (int l = 0; l < p.n_levels; ++l) {
+        if (p.max_iters[l] < 1) throw VhError{VH_ERR_ARG, "max_iters must be >= 1"};
+        tot += p.max_iters[l];
+    }
+    if (tot > 8 * 1024 - 1) throw VhError{VH_ERR_ARG, "too many N4 iterations"};
+}
+
 // n4_src: 0 = run N4 from d_hp, 1 = identity (d_hp), 2 = caller-uploaded d_n4
 static void batch_run(vh_batch *b, const vh_run_opts &o, int n4_src) {
     HIP_TRY(hipSetDevice(b->ctx->device));
@@ -164,18 +178,7 @@ static void batch_run(vh_batch *b, const vh_run_opts &o, int n4_src) {
     b->opts = o;
     b->n4_subbatch = o.n4_subbatch;
     b->n4_mode = o.n4_mode;
-    if (o.do_n4) {
-        if (o.n4.n_levels < 1 || o.n4.n_levels > VH_MAX_LEVELS || o.n4.spline_order != 3 ||
-            o.n4.n_bins < 2 || o.n4.n_bins > VH_MAX_BINS || o.n4.ncp[0] < 4 || o.n4.ncp[1] < 4 ||
-            o.n4.ncp[2] < 4 || b->Z < 2)
-            throw VhError{VH_ERR_ARG, "unsupported N4 parameters (spline order 3, bins <= 256, ncp >= 4, Z >= 2)"};
-        int tot = 0;
-        for (int l = 0; l < o.n4.n_levels; ++l) {
-            if (o.n4.max_iters[l] < 1) throw VhError{VH_ERR_ARG, "max_iters must be >= 1"};
-            tot += o.n4.max_iters[l];
-        }
-        if (tot > 8 * 1024 - 1) throw VhError{VH_ERR_ARG, "too many N4 iterations"};
-    }
+    if (o.do_n4) check_n4_params(b, o.n4);
     vh_launch_mask_stats(b);
     const float *n4 = b->d_hp;
     if (o.do_n4) {
@@ -290,6 +293,7 @@ void vh_n4_default_params(vh_n4_params *p) {
     p->n_bins = 200;
     p->wiener_noise = 0.01f;
     p->fwhm = 0.15f;
+    p->conv_mode = 0;
 }
 
 void vh_default_run_opts(vh_run_opts *o) {
@@ -346,6 +350,7 @@ int vh_n4(vh_ctx *ctx, const float *hp, const uint8_t *mask, int64_t R, int64_t 
     API_TRY(ctx, {
         if (!hp || !mask || !out || !prm) throw VhError{VH_ERR_ARG, "null buffer"};
         vh_batch *b = scratch_batch(ctx, R, C, Z, batch);
+        check_n4_params(b, *prm);
         batch_upload(b, hp, mask);
         vh_run_opts o;
         vh_default_run_opts(&o);
@@ -521,7 +526,7 @@ int vh_batch_cohort_hist(vh_batch *b, uint64_t *hist) {
 
 const char *vh_batch_kernel_names(void) {
     return "mask_stats;gather;sort;classify;cohort;kmeans;snr;border;n4_init;n4_den;n4_hist;"
-           "n4_fit;n4_contract;n4_eval;n4_final;n4_study;ci_walk";
+           "n4_fit;n4_contract;n4_eval;n4_welford;n4_final;n4_study;ci_walk";
 }
 
 int vh_batch_reset_timers(vh_batch *b) {

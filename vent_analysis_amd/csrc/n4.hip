@@ -23,13 +23,11 @@
 
 #include "n4_shared.h"
 
-#define FIT_W 128   // columns per fit block (FIT_W / TILE_W compact tiles, contiguous in compact order)
-#define FIT_TPT (FIT_W / TILE_W)
 #define SEG_R 16    // rows per wave segment
 #define N4_CH 4096  // compact voxels per chunk (flat sweeps: 256 threads x 16)
 #define N4_VPT (N4_CH / VH_TPB)
 #define HIST_COPIES 8   // LDS histogram copies (neighbouring lanes share bins)
-#define FIT_G 8     // fit voxels per thread with loads in flight together
+#define FIT_WAVES 4     // fit items per block (one per wave)
 
 // ---------------------------------------------------------------------------------------------
 // host: per-level axis tables (identical expressions to oracle/n4_oracle.c axis_tables)
@@ -88,7 +86,7 @@ void vh_n4_prepare_tables(vh_batch *b, const vh_n4_params &prm) {
     if (b->tabs_valid && same_params(b->tab_prm, prm)) return;
     const int64_t dims[3] = {b->R, b->C, b->Z};
     std::vector<uint8_t> blob;
-    b->tab_off.assign((size_t)prm.n_levels * 3 * 7, 0);
+    b->tab_off.assign((size_t)prm.n_levels * 3 * 8, 0);
     auto push = [&](const void *p, size_t bytes) {
         size_t off = (blob.size() + 15) & ~(size_t)15;
         blob.resize(off + bytes);
@@ -102,19 +100,21 @@ void vh_n4_prepare_tables(vh_batch *b, const vh_n4_params &prm) {
         for (int a = 0; a < 3; ++a) {
             AxisTab t;
             vh_axis_tables((int)dims[a], vh_level_ncp(prm, L, a), eps, t);
-            std::vector<double> inv(t.sw2.size()), w2(t.w.size()), w3(t.w.size());
+            std::vector<double> inv(t.sw2.size()), w2(t.w.size()), w3(t.w.size()), w3i(t.w.size());
             for (size_t i = 0; i < inv.size(); ++i) inv[i] = 1.0 / t.sw2[i];
             for (size_t i = 0; i < w2.size(); ++i) {
                 const double w = t.w[i];
                 w2[i] = w * w;
                 w3[i] = w * w * w;
+                w3i[i] = w3[i] * inv[i / 4];   // S5 numerator row weight: w^3 / sum w^2
             }
-            b->tab_off[(L * 3 + a) * 7 + 0] = push(t.base.data(), t.base.size() * 4);
-            b->tab_off[(L * 3 + a) * 7 + 1] = push(t.w.data(), t.w.size() * 4);
-            b->tab_off[(L * 3 + a) * 7 + 2] = push(t.sw2.data(), t.sw2.size() * 8);
-            b->tab_off[(L * 3 + a) * 7 + 3] = push(inv.data(), inv.size() * 8);
-            b->tab_off[(L * 3 + a) * 7 + 4] = push(w2.data(), w2.size() * 8);
-            b->tab_off[(L * 3 + a) * 7 + 5] = push(w3.data(), w3.size() * 8);
+            b->tab_off[(L * 3 + a) * 8 + 0] = push(t.base.data(), t.base.size() * 4);
+            b->tab_off[(L * 3 + a) * 8 + 1] = push(t.w.data(), t.w.size() * 4);
+            b->tab_off[(L * 3 + a) * 8 + 2] = push(t.sw2.data(), t.sw2.size() * 8);
+            b->tab_off[(L * 3 + a) * 8 + 3] = push(inv.data(), inv.size() * 8);
+            b->tab_off[(L * 3 + a) * 8 + 4] = push(w2.data(), w2.size() * 8);
+            b->tab_off[(L * 3 + a) * 8 + 5] = push(w3.data(), w3.size() * 8);
+            b->tab_off[(L * 3 + a) * 8 + 7] = push(w3i.data(), w3i.size() * 8);
             // control point k -> the index range whose 4-wide support contains k
             std::vector<int32_t> kr(2 * (size_t)t.ncp);
             for (int k = 0; k < t.ncp; ++k) {
@@ -127,49 +127,36 @@ void vh_n4_prepare_tables(vh_batch *b, const vh_n4_params &prm) {
                 kr[2 * k] = lo;
                 kr[2 * k + 1] = hi;
             }
-            b->tab_off[(L * 3 + a) * 7 + 6] = push(kr.data(), kr.size() * 4);
+            b->tab_off[(L * 3 + a) * 8 + 6] = push(kr.data(), kr.size() * 4);
         }
     }
-    // fit tile metadata per level (64-column tiles of the (col, slice) plane)
-    const int64_t ntiles = (b->CZ + FIT_W - 1) / FIT_W;   // fit tiles
-    b->tile_off.assign((size_t)prm.n_levels, 0);
-    b->jt_off.assign((size_t)prm.n_levels, 0);
-    b->fit_smax.assign((size_t)prm.n_levels, 0);
+    // per level: row-span starts of the row axis and the dense slice weights (S5 stage 1)
+    b->lvx_off.assign((size_t)prm.n_levels * 3, 0);
     for (int L = 0; L < prm.n_levels; ++L) {
         const float eps = vh_bspline_eps(std::max({vh_level_ncp(prm, L, 0), vh_level_ncp(prm, L, 1),
                                                    vh_level_ncp(prm, L, 2)}) - 3);
-        AxisTab ty, tz;
-        vh_axis_tables((int)b->C, vh_level_ncp(prm, L, 1), eps, ty);
+        AxisTab tx, tz;
+        vh_axis_tables((int)b->R, vh_level_ncp(prm, L, 0), eps, tx);
         vh_axis_tables((int)b->Z, vh_level_ncp(prm, L, 2), eps, tz);
-        std::vector<int32_t> meta(8 * (size_t)ntiles);
-        int smax = 0;
-        for (int64_t t = 0; t < ntiles; ++t) {
-            const int64_t c0 = t * FIT_W, c1 = std::min(c0 + FIT_W, b->CZ) - 1;
-            const int y0 = (int)(c0 / b->Z), y1 = (int)(c1 / b->Z);
-            const int z0 = (int)(c0 % b->Z), z1 = (int)(c1 % b->Z);
-            const int zlo = y0 == y1 ? z0 : 0, zhi = y0 == y1 ? z1 : (int)b->Z - 1;
-            const int jlo = ty.base[y0], JT = ty.base[y1] + 4 - jlo;
-            const int klo = tz.base[zlo], KT = tz.base[zhi] + 4 - klo;
-            const int32_t m[8] = {y0, y1, z0, z1, jlo, JT, klo, KT};
-            std::memcpy(&meta[8 * t], m, sizeof(m));
-            smax = std::max(smax, vh_level_ncp(prm, L, 0) * (y1 - y0 + 1) * KT);
+        const int ncx = tx.ncp, ncz = tz.ncp;
+        std::vector<int32_t> xst((size_t)ncx - 2);
+        for (int i = 0; i <= ncx - 3; ++i) {
+            int x = 0;
+            while (x < b->R && tx.base[x] < i) ++x;
+            xst[i] = i == ncx - 3 ? (int32_t)b->R : x;
         }
-        // lattice col j -> the contiguous range of tiles whose slab covers it
-        const int ncy = vh_level_ncp(prm, L, 1);
-        std::vector<int32_t> jt(2 * (size_t)ncy);
-        for (int j = 0; j < ncy; ++j) {
-            int lo = (int)ntiles, hi = -1;
-            for (int64_t t = 0; t < ntiles; ++t)
-                if (j >= meta[8 * t + 4] && j < meta[8 * t + 4] + meta[8 * t + 5]) {
-                    lo = std::min(lo, (int)t);
-                    hi = std::max(hi, (int)t);
-                }
-            jt[2 * j] = lo;
-            jt[2 * j + 1] = hi;
-        }
-        b->tile_off[L] = push(meta.data(), meta.size() * 4);
-        b->jt_off[L] = push(jt.data(), jt.size() * 4);
-        b->fit_smax[L] = smax;
+        std::vector<double> wk3((size_t)ncz * b->Z), wk2((size_t)ncz * b->Z);
+        for (int k = 0; k < ncz; ++k)
+            for (int64_t z = 0; z < b->Z; ++z) {
+                const int d = k - tz.base[z];
+                const bool in = d >= 0 && d <= 3;
+                const double w = in ? (double)tz.w[4 * z + d] : 0.0;
+                wk3[(size_t)k * b->Z + z] = in ? w * w * w : 0.0;
+                wk2[(size_t)k * b->Z + z] = in ? w * w : 0.0;
+            }
+        b->lvx_off[L * 3 + 0] = push(xst.data(), xst.size() * 4);
+        b->lvx_off[L * 3 + 1] = push(wk3.data(), wk3.size() * 8);
+        b->lvx_off[L * 3 + 2] = push(wk2.data(), wk2.size() * 8);
     }
     if (b->d_tabs) HIP_TRY(hipFree(b->d_tabs));
     b->d_tabs = nullptr;
@@ -195,18 +182,20 @@ DevLevel vh_dev_level(const vh_batch *b, const vh_n4_params &prm, int L) {
     const int64_t dims[3] = {b->R, b->C, b->Z};
     const uint8_t *base = (const uint8_t *)b->d_tabs;
     for (int a = 0; a < 3; ++a) {
-        lv.ax[a].base = (const int32_t *)(base + b->tab_off[(L * 3 + a) * 7 + 0]);
-        lv.ax[a].w = (const float *)(base + b->tab_off[(L * 3 + a) * 7 + 1]);
-        lv.ax[a].sw2 = (const double *)(base + b->tab_off[(L * 3 + a) * 7 + 2]);
-        lv.ax[a].isw2 = (const double *)(base + b->tab_off[(L * 3 + a) * 7 + 3]);
-        lv.ax[a].w2 = (const double *)(base + b->tab_off[(L * 3 + a) * 7 + 4]);
-        lv.ax[a].w3 = (const double *)(base + b->tab_off[(L * 3 + a) * 7 + 5]);
-        lv.ax[a].krange = (const int2 *)(base + b->tab_off[(L * 3 + a) * 7 + 6]);
+        lv.ax[a].base = (const int32_t *)(base + b->tab_off[(L * 3 + a) * 8 + 0]);
+        lv.ax[a].w = (const float *)(base + b->tab_off[(L * 3 + a) * 8 + 1]);
+        lv.ax[a].sw2 = (const double *)(base + b->tab_off[(L * 3 + a) * 8 + 2]);
+        lv.ax[a].isw2 = (const double *)(base + b->tab_off[(L * 3 + a) * 8 + 3]);
+        lv.ax[a].w2 = (const double *)(base + b->tab_off[(L * 3 + a) * 8 + 4]);
+        lv.ax[a].w3 = (const double *)(base + b->tab_off[(L * 3 + a) * 8 + 5]);
+        lv.ax[a].krange = (const int2 *)(base + b->tab_off[(L * 3 + a) * 8 + 6]);
+        lv.ax[a].w3i = (const double *)(base + b->tab_off[(L * 3 + a) * 8 + 7]);
         lv.ax[a].n = (int32_t)dims[a];
         lv.ax[a].ncp = vh_level_ncp(prm, L, a);
     }
-    lv.tiles = (const int4 *)(base + b->tile_off[L]);
-    lv.jt = (const int2 *)(base + b->jt_off[L]);
+    lv.xst = (const int32_t *)(base + b->lvx_off[L * 3 + 0]);
+    lv.wk3 = (const double *)(base + b->lvx_off[L * 3 + 1]);
+    lv.wk2 = (const double *)(base + b->lvx_off[L * 3 + 2]);
     return lv;
 }
 
@@ -224,6 +213,7 @@ void vh_ensure_n4_workspace(vh_batch *b, const vh_n4_params &prm) {
         const int64_t nch = b->nb * ((b->VS + N4_CH - 1) / N4_CH);
         HIP_TRY(hipMalloc(&b->d_L0, sizeof(float) * b->nb * b->VS));
         HIP_TRY(hipMalloc(&b->d_U, sizeof(float) * b->nb * b->VS));
+        HIP_TRY(hipMalloc(&b->d_D, sizeof(float) * b->nb * b->VS));
         HIP_TRY(hipMalloc(&b->d_ridx, sizeof(int32_t) * b->nb * b->VS));
         HIP_TRY(hipMalloc(&b->d_cp, sizeof(int32_t) * (b->nb + 1)));
         HIP_TRY(hipMalloc(&b->d_cvol, sizeof(int32_t) * nch));
@@ -235,10 +225,10 @@ void vh_ensure_n4_workspace(vh_batch *b, const vh_n4_params &prm) {
     }
     if (lat > b->lat_cap) {
         if (b->d_lat) HIP_TRY(hipFree(b->d_lat));
-        if (b->d_num) HIP_TRY(hipFree(b->d_num));
+        if (b->d_numfix) HIP_TRY(hipFree(b->d_numfix));
         if (b->d_den) HIP_TRY(hipFree(b->d_den));
         HIP_TRY(hipMalloc(&b->d_lat, sizeof(float) * 3 * b->nb * lat));   // lattice + 2 scratch
-        HIP_TRY(hipMalloc(&b->d_num, sizeof(double) * b->nb * lat));
+        HIP_TRY(hipMalloc(&b->d_numfix, sizeof(uint64_t) * 2 * b->nb * lat));
         HIP_TRY(hipMalloc(&b->d_den, sizeof(double) * b->nb * lat));
         b->lat_cap = lat;
     }
@@ -247,15 +237,11 @@ void vh_ensure_n4_workspace(vh_batch *b, const vh_n4_params &prm) {
     if (b->d_rowstart == nullptr || b->n4_tiles != ntiles) {
         if (b->d_rowstart) HIP_TRY(hipFree(b->d_rowstart));
         if (b->d_rowmask) HIP_TRY(hipFree(b->d_rowmask));
+        if (b->d_rrank) HIP_TRY(hipFree(b->d_rrank));
         HIP_TRY(hipMalloc(&b->d_rowstart, sizeof(int32_t) * b->nb * ntiles * b->R));
         HIP_TRY(hipMalloc(&b->d_rowmask, sizeof(uint64_t) * b->nb * ntiles * b->R));
+        HIP_TRY(hipMalloc(&b->d_rrank, sizeof(int32_t) * b->nb * ntiles * b->R));
         b->n4_tiles = ntiles;
-    }
-    const int64_t fp = ((b->CZ + FIT_W - 1) / FIT_W) * lat;   // per-volume fit tile slabs
-    if (fp > b->q1_cap) {
-        if (b->d_fitpart) HIP_TRY(hipFree(b->d_fitpart));
-        HIP_TRY(hipMalloc(&b->d_fitpart, sizeof(double) * b->nb * fp));
-        b->q1_cap = fp;
     }
     if (cx * b->CZ > b->t_cap) {
         if (b->d_T) HIP_TRY(hipFree(b->d_T));
@@ -413,6 +399,45 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_rowscan(int32_t *rs, int64_t n) {
     for (int64_t i = s0; i < e0; ++i) { const int32_t v = a[i]; a[i] = (int32_t)run; run += v; }
 }
 
+// Raster rank of the first masked voxel of every (tile, row): masked voxels before row x plus
+// those of row x in tiles before t -- the position of the voxel in ITK's raster-order scans (the
+// convergence recurrence S7).  One block per volume; dynamic LDS holds the R row totals.
+__global__ void __launch_bounds__(VH_TPB) k_n4_rrank(const uint64_t *rowmask, int64_t R,
+                                                    int64_t ntiles, int32_t *rrank) {
+    extern __shared__ int32_t s_rowtot[];   // [R]
+    __shared__ int32_t s_part[VH_TPB];
+    const int64_t b = blockIdx.x;
+    const uint64_t *rm = rowmask + b * ntiles * R;
+    int32_t *rr = rrank + b * ntiles * R;
+    for (int64_t x = threadIdx.x; x < R; x += VH_TPB) {
+        int32_t run = 0;
+        for (int64_t t = 0; t < ntiles; ++t) {
+            rr[t * R + x] = run;
+            run += __popcll(rm[t * R + x]);
+        }
+        s_rowtot[x] = run;
+    }
+    __syncthreads();
+    const int t = threadIdx.x;
+    const int64_t per = (R + VH_TPB - 1) / VH_TPB;
+    const int64_t s0 = t * per < R ? t * per : R, e0 = s0 + per < R ? s0 + per : R;
+    int32_t acc = 0;
+    for (int64_t i = s0; i < e0; ++i) acc += s_rowtot[i];
+    s_part[t] = acc;
+    __syncthreads();
+    if (t == 0) {
+        int32_t run = 0;
+        for (int i = 0; i < VH_TPB; ++i) { const int32_t v = s_part[i]; s_part[i] = run; run += v; }
+    }
+    __syncthreads();
+    int32_t run = s_part[t];
+    for (int64_t i = s0; i < e0; ++i) { const int32_t v = s_rowtot[i]; s_rowtot[i] = run; run += v; }
+    __syncthreads();
+    for (int64_t x = threadIdx.x; x < R; x += VH_TPB) {
+        const int32_t base = s_rowtot[x];
+        for (int64_t tt = 0; tt < ntiles; ++tt) rr[tt * R + x] += base;
+    }
+}
 
 // L0 = log(I) at mask == 1 (non-positive -> 0), U = L0 (B = 0), ridx = (row << rsh) | column
 // (compact, volume stride VS) and the first U range.  grid (ceil(tiles/4), segments, volumes), 4 tile-waves/block.
@@ -529,7 +554,8 @@ __device__ float exact_min_block(const float *Uv, const uint32_t *colbits, const
 // pixel is the strict minimum).  One block per volume.
 __global__ void __launch_bounds__(VH_TPB) k_n4_ctrl(N4State *st, const double *part,
                                                    const int32_t *cp, const VolScalars *sc,
-                                                   int level, int it, float thresh, int bins,
+                                                   int conv_mode, int level, int it, float thresh,
+                                                   int bins,
                                                    int64_t vol0, int32_t *nactive, const float *U,
                                                    const uint32_t *colbits, const int32_t *rs,
                                                    int64_t R, int64_t CZ, int64_t VS,
@@ -539,7 +565,8 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_ctrl(N4State *st, const double *p
     const int64_t b = vol0 + blockIdx.x;
     const bool was_active = st[b].active;
     double conv = 0.0;
-    if (threadIdx.x < 64 && it > 0 && was_active)
+    if (conv_mode == 0) conv = (double)st[b].conv_w;
+    else if (threadIdx.x < 64 && it > 0 && was_active)
         conv = conv_from_parts(part, cp, b, (double)sc[b].n_mask1);
     if (threadIdx.x == 0) {
         N4State &s = st[b];
@@ -551,7 +578,8 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_ctrl(N4State *st, const double *p
         } else if (was_active) {
             s.tlast ^= 1;   // the previous iteration's eval used the other T buffer as "new"
             s.conv = conv;
-            if (!(conv > (double)thresh)) {
+            const bool go = conv_mode == 0 ? st[b].conv_w > thresh : conv > (double)thresh;
+            if (!go) {
                 s.active = 0;
                 s.iters_level[level] = s.iters;
                 s.conv_level[level] = (float)conv;
@@ -585,11 +613,12 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_ctrl(N4State *st, const double *p
 
 __global__ void __launch_bounds__(64) k_n4_level_end(N4State *st, const double *part,
                                                     const int32_t *cp, const VolScalars *sc,
-                                                    int level, int64_t vol0) {
+                                                    int conv_mode, int level, int64_t vol0) {
     const int64_t b = vol0 + blockIdx.x;
     N4State &s = st[b];
     if (!s.active) return;
-    const double conv = conv_from_parts(part, cp, b, (double)sc[b].n_mask1);
+    const double conv = conv_mode == 0 ? (double)s.conv_w
+                                       : conv_from_parts(part, cp, b, (double)sc[b].n_mask1);
     if (threadIdx.x != 0) return;
     s.tlast ^= 1;
     s.conv = conv;
@@ -598,10 +627,10 @@ __global__ void __launch_bounds__(64) k_n4_level_end(N4State *st, const double *
     s.active = 0;
 }
 
-// Triangular Parzen histogram of U at mask == 1, unsigned 64-bit fixed point (2^-32 units).
-// One block per chunk of N4_CH compact voxels; a thread takes 16 consecutive voxels (neighbours in
-// a row, so a run (bin, two weights) usually covers several), LDS histogram, then the block writes
-// its partial histogram; k_n4_emap adds a volume's partials in chunk order (deterministic).
+// Packed Parzen histogram of U at mask == 1 (S3, hist_pack: count << 44 | sum of o-weights in
+// 2^-24 units).  One block per chunk of N4_CH compact voxels (< 2^20 values: the packed words stay
+// exact), LDS copies, then the block writes its chunk's packed histogram; k_n4_emap unpacks and adds
+// a volume's chunks (integer sums: order-free).
 __global__ void __launch_bounds__(VH_TPB) k_n4_hist(const float *__restrict__ U, const int32_t *cp,
                                                    const int32_t *cvol, const VolScalars *sc,
                                                    int64_t VS, int bins, const N4State *st,
@@ -628,36 +657,24 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_hist(const float *__restrict__ U,
         for (int k = 0; k < N4_VPT; ++k) u[k] = t0 + k < n ? src[k] : __int_as_float(0x7fc00000);
     }
     __syncthreads();
-    const float bmin = st[b].bin_min, slope = st[b].slope;
-    int cur = -1;
-    unsigned long long w0 = 0ull, w1 = 0ull;
+    const float bmin = st[b].bin_min;
+    const double rinv = 1.0 / (double)st[b].slope;
 #pragma unroll
     for (int k = 0; k < N4_VPT; ++k) {
         int idx;
-        unsigned long long a0, a1;
-        if (!parzen_bin(u[k], bmin, slope, bins, idx, a0, a1)) continue;
-        if (idx != cur) {
-            if (cur >= 0) {
-                if (w0) atomicAdd(&H[cur], w0);
-                if (w1) atomicAdd(&H[cur + 1], w1);
-            }
-            cur = idx;
-            w0 = 0ull;
-            w1 = 0ull;
-        }
-        w0 += a0;
-        w1 += a1;
-    }
-    if (cur >= 0) {
-        if (w0) atomicAdd(&H[cur], w0);
-        if (w1) atomicAdd(&H[cur + 1], w1);
+        const unsigned long long w = hist_pack(u[k], bmin, rinv, bins, idx);
+        if (w) atomicAdd(&H[idx], w);
     }
     __syncthreads();
     for (int i = threadIdx.x; i < bins; i += VH_TPB) {
-        unsigned long long h = 0ull;
+        unsigned long long cnt = 0ull, os = 0ull;
 #pragma unroll
-        for (int q = 0; q < HIST_COPIES; ++q) h += Hc[q * VH_MAX_BINS + i];
-        hpart[(int64_t)c * VH_MAX_BINS + i] = h;
+        for (int q = 0; q < HIST_COPIES; ++q) {
+            const unsigned long long w = Hc[q * VH_MAX_BINS + i];
+            cnt += hist_count(w);
+            os += hist_osum(w);
+        }
+        hpart[(int64_t)c * VH_MAX_BINS + i] = (cnt << HIST_CSHIFT) | os;   // < 4096 values: exact
     }
 }
 
@@ -726,18 +743,14 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_emap(const uint64_t *hpart, const
     const int32_t ca = cp[b], ce = cp[b + 1];
     for (int n = t; n < P; n += VH_TPB) {
         const int h = n - off;
-        uint64_t h0 = 0ull, h1 = 0ull, h2 = 0ull, h3 = 0ull;   // integer sums: order-free, exact
-        if (h >= 0 && h < bins) {
-            int32_t c = ca;
-            for (; c + 3 < ce; c += 4) {
-                h0 += hpart[(int64_t)c * VH_MAX_BINS + h];
-                h1 += hpart[(int64_t)(c + 1) * VH_MAX_BINS + h];
-                h2 += hpart[(int64_t)(c + 2) * VH_MAX_BINS + h];
-                h3 += hpart[(int64_t)(c + 3) * VH_MAX_BINS + h];
+        uint64_t hs = 0ull;   // integer sums: order-free, exact (S3 unpacking)
+        if (h >= 0 && h < bins)
+            for (int32_t c = ca; c < ce; ++c) {
+                const uint64_t w = hpart[(int64_t)c * VH_MAX_BINS + h];
+                hs += (hist_count(w) << 24) - hist_osum(w);
+                if (h > 0) hs += hist_osum(hpart[(int64_t)c * VH_MAX_BINS + h - 1]);
             }
-            for (; c < ce; ++c) h0 += hpart[(int64_t)c * VH_MAX_BINS + h];
-        }
-        V[n] = make_double2((double)((h0 + h1) + (h2 + h3)) * (1.0 / 4294967296.0), 0.0);
+        V[n] = make_double2((double)hs * (1.0 / 16777216.0), 0.0);
         F[n] = make_double2(0.0, 0.0);
     }
     __syncthreads();
@@ -790,191 +803,91 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_emap(const uint64_t *hpart, const
 }
 
 // ---------------------------------------------------------------------------------------------
-// Fit with in-block contraction.  Block = one 64-column tile of one volume: its compact voxels are
-// contiguous (tile-row order), a thread takes every 256th.  Row contraction into LDS
-//   Q1[i][l] = sum_x wx(x,i)^p q(x, l)          (l = column within the tile)
-// with 64-bit fixed-point LDS atomics (2^-36 units: integer adds, so the order does not matter
-// and the result is deterministic), then the block contracts its 64 columns over slices and cols
-//   Pn[i][j][k] = sum_{(y,z) in tile} wy(y,j)^p wz(z,k)^p Q1[i][y][z],  p = 3 (num) / 2 (den)
-// q = r / (sum wx^2 sum wy^2 sum wz^2) for the numerator, 1 for the denominator.  Only the small
-// slab goes to HBM; k_n4_tilesum adds a volume's slabs in tile order.  (A last-block-done fold
-// of that sum into this kernel needs agent-scope fences, which write back / invalidate the XCD's
-// L2 on gfx950: measured 10x slower, so the sum stays a separate launch.)
+// S5 fit, item-ordered (n4_shared.h fit_item, the same code the volume-resident driver runs): a wave
+// owns one (64-column tile, 64-row slot) item of one volume; the finished control rows of its tile
+// are contracted over slices and cols and added to the volume's lattice numerator as 128-bit
+// fixed-point integers with global atomics (order-free).  Tables are read from global memory.
+// grid (ceil(items / FIT_WAVES), volumes); dynamic LDS: per wave a ring of nbmax rows + the
+// stage-1 output buffer, then E.
 // ---------------------------------------------------------------------------------------------
-// round(v * 2^32) as a two's-complement integer without the slow double -> int64 conversion:
-// v * 2^32 is exact, adding 1.5 * 2^52 rounds it to nearest-even (valid while |v| < 2^19; the
-// fit's terms are bounded by |w^3 q| < 2^8 for log-intensity residuals)
-__device__ __forceinline__ unsigned long long fix_round(double v) {
-    const double t = v * N4_FIX + N4_MAGIC;
-    return (unsigned long long)(__double_as_longlong(t) - __double_as_longlong(N4_MAGIC));
-}
-
 template <int MODE>
-__global__ void __launch_bounds__(VH_TPB) k_n4_fit(const float *__restrict__ U,
-                                                  const int32_t *__restrict__ ridx,
-                                                  const int32_t *rs, const VolScalars *sc,
-                                                  int64_t R, int64_t C, int64_t Z, int64_t VS,
-                                                  int64_t ntiles, int bins, const N4State *st,
-                                                  const float *E, DevLevel lv, int rsh,
-                                                  int smax, int64_t slab, double *part,
-                                                  int64_t vol0) {
-    // dynamic LDS: Q1 [ncx][FIT_W] | slab stage [smax] | row weights [R][4] | 1/sum w^2 [R] | base [R]
-    extern __shared__ __attribute__((aligned(16))) double smem[];
+__global__ void __launch_bounds__(FIT_WAVES * 64) k_n4_fit_items(
+    const float *__restrict__ U, const int32_t *rs, const uint64_t *rmask, const VolScalars *sc,
+    int R, int C, int Z, int64_t VS, int ntiles, int nslots, int bins, const N4State *st,
+    const float *E, DevLevel lv, int rowcap, int nbmax, unsigned long long *numfix,
+    int64_t lat_cap, int64_t vol0) {
+    extern __shared__ __attribute__((aligned(16))) double fsm[];
     __shared__ float sE[VH_MAX_BINS];
-    __shared__ double sIyz[FIT_W];
-    __shared__ double sWz[4 * FIT_W];
-    __shared__ int sBz[FIT_W];
     const int64_t b = vol0 + blockIdx.y;
     if (MODE == 0 && !st[b].active) return;
-    const int tile = blockIdx.x;
-    const DevAxis ax = lv.ax[0], ay = lv.ax[1], az = lv.ax[2];
-    const int ncx = ax.ncp;
-    const int64_t CZ = C * Z;
-    const int64_t c0 = (int64_t)tile * FIT_W;
-    const int4 m0 = lv.tiles[2 * tile], m1 = lv.tiles[2 * tile + 1];
-    const int jlo = m1.x, JT = m1.y, klo = m1.z, KT = m1.w;
-    const int64_t nft = (CZ + FIT_W - 1) / FIT_W;
-    double *out = part + (b * nft + tile) * slab;
-    // compact tiles FIT_TPT*tile .. +FIT_TPT-1 hold this block's voxels, contiguously
-    const int64_t ts = rs[(b * ntiles + (int64_t)tile * FIT_TPT) * R];
-    const int64_t te = (int64_t)(tile + 1) * FIT_TPT < ntiles
-                           ? rs[(b * ntiles + (int64_t)(tile + 1) * FIT_TPT) * R]
-                           : sc[b].n_mask1;
-    if (ts >= te) {   // no masked voxel in this tile
-        for (int e = threadIdx.x; e < ncx * JT * KT; e += VH_TPB) out[e] = 0.0;
-        return;
-    }
-    unsigned long long *sQi = reinterpret_cast<unsigned long long *>(smem);   // [ncx][FIT_W]
-    for (int e = threadIdx.x; e < ncx * FIT_W; e += VH_TPB) sQi[e] = 0ull;
-    double *sWx = smem + (size_t)ncx * FIT_W + smax;
-    double *sIx = sWx + 4 * R;
-    int *sBx = reinterpret_cast<int *>(sIx + R);
-    for (int x = threadIdx.x; x < R; x += VH_TPB) {   // per-row tables: no global loads per voxel
-        const double *wx = (MODE == 0 ? ax.w3 : ax.w2) + 4 * x;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) sWx[4 * x + c] = wx[c];
-        sIx[x] = ax.isw2[x];
-        sBx[x] = ax.base[x];
-    }
+    const int wv = threadIdx.x >> 6;
+    const int nitems = ntiles * nslots;
     if (MODE == 0)
-        for (int i = threadIdx.x; i < bins; i += VH_TPB) sE[i] = E[b * VH_MAX_BINS + i];
-    if (threadIdx.x < FIT_W && c0 + threadIdx.x < CZ) {   // per-column slice tables
-        const int col = (int)(c0 + threadIdx.x), iz = (int)Z;
-        const int z = col % iz;
-        if (MODE == 0) sIyz[threadIdx.x] = ay.isw2[col / iz] * az.isw2[z];
-        sBz[threadIdx.x] = az.base[z];
-        const double *wz = (MODE == 0 ? az.w3 : az.w2) + 4 * z;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) sWz[4 * threadIdx.x + c] = wz[c];
-    }
+        for (int i = threadIdx.x; i < bins; i += FIT_WAVES * 64) sE[i] = E[b * VH_MAX_BINS + i];
     __syncthreads();
-    // ---- row contraction: every masked voxel of the tile ----
-    float bmin = 0.0f, slope = 1.0f;
+    const int item = blockIdx.x * FIT_WAVES + wv;
+    if (item >= nitems) return;
+    const int CZ = C * Z;
+    const int64_t tb = b * (int64_t)ntiles * R;
+    Item it;
+    if (!item_begin(it, rmask + tb, rs + tb, nullptr, R, C, Z, CZ, nslots, item)) return;
+    TabV T;
+    T.wx = reinterpret_cast<const float4 *>(lv.ax[0].w);
+    T.wy = reinterpret_cast<const float4 *>(lv.ax[1].w);
+    T.wz = reinterpret_cast<const float4 *>(lv.ax[2].w);
+    T.ix = lv.ax[0].isw2;
+    T.iy = lv.ax[1].isw2;
+    T.iz = lv.ax[2].isw2;
+    T.bx = lv.ax[0].base;
+    T.by = lv.ax[1].base;
+    T.bz = lv.ax[2].base;
+    T.krz = lv.ax[2].krange;
+    T.xst = lv.xst;
+    FitRing rg;
+    rg.q = fsm + (size_t)wv * 2 * nbmax * rowcap;
+    rg.sx = rg.q + (size_t)nbmax * rowcap;
+    rg.rowcap = rowcap;
+    rg.nr = 0;
+    const int ncy = lv.ax[1].ncp, ncz = lv.ax[2].ncp;
+    unsigned long long *nf = numfix + 2 * b * lat_cap;
+    const int64_t n = sc[b].n_mask1;
     if (MODE == 0) {
-        bmin = st[b].bin_min;
-        slope = st[b].slope;
-    }
-    const float *Ub = U + b * VS;
-    const int32_t *Rb = ridx + b * VS;
-    for (int64_t jb = ts + threadIdx.x; jb < te; jb += FIT_G * VH_TPB) {
-        int rr[FIT_G];
-        float uu[FIT_G];
-#pragma unroll
-        for (int k = 0; k < FIT_G; ++k) {   // every load of the group in flight first
-            const int64_t j = jb + (int64_t)k * VH_TPB;
-            rr[k] = j < te ? Rb[j] : -1;
-            if (MODE == 0) uu[k] = j < te ? Ub[j] : 0.0f;
-        }
-#pragma unroll
-        for (int k = 0; k < FIT_G; ++k) {
-            const int r = rr[k];
-            if (r < 0) continue;
-            const int x = r >> rsh;
-            const int l = (r & ((1 << rsh) - 1)) - (int)c0;
-            const int bx = sBx[x];
-            const double *wp = sWx + 4 * x;
-            if (MODE == 0) {
-                const float u = uu[k];
-                const float rv = u - sharpen_value(u, bmin, slope, sE, bins);
-                const double q = ((double)rv * sIx[x]) * sIyz[l];
-#pragma unroll
-                for (int c = 0; c < 4; ++c)
-                    atomicAdd(&sQi[(bx + c) * FIT_W + l], fix_round(wp[c] * q));
-            } else {
-#pragma unroll
-                for (int c = 0; c < 4; ++c)
-                    atomicAdd(&sQi[(bx + c) * FIT_W + l], fix_round(wp[c]));
-            }
-        }
-    }
-    __syncthreads();
-    double *sQ1 = smem;   // in place: each slot converted by the thread that reads it
-    for (int e = threadIdx.x; e < ncx * FIT_W; e += VH_TPB)
-        sQ1[e] = (double)(long long)sQi[e] * (1.0 / N4_FIX);
-    __syncthreads();
-    // ---- contract the tile's columns: over slices per tile row (stage 1), then over cols ----
-    const int y0 = m0.x, y1 = m0.y, ny = y1 - y0 + 1;
-    const double *wyp = MODE == 0 ? ay.w3 : ay.w2;
-    double *sS = smem + (size_t)ncx * FIT_W;   // [ncx][ny][KT]
-    for (int e = threadIdx.x; e < ncx * ny * KT; e += VH_TPB) {
-        const int i = e / (ny * KT), yy = (e / KT) % ny, k = klo + e % KT;
-        const int y = y0 + yy;
-        const int2 zr = az.krange[k];   // slices whose support covers k
-        const int zs = max(y == y0 ? m0.z : 0, zr.x), ze = min(y == y1 ? m0.w : (int)Z - 1, zr.y);
-        const int lb = (int)((int64_t)y * Z - c0);   // lane of (y, z = 0)
-        double acc = 0.0;
-        for (int l = lb + zs; l <= lb + ze; ++l)
-            acc = fma(sWz[4 * l + (k - sBz[l])], sQ1[i * FIT_W + l], acc);
-        sS[e] = acc;
-    }
-    __syncthreads();
-    for (int e = threadIdx.x; e < ncx * JT * KT; e += VH_TPB) {
-        const int i = e / (JT * KT), j = jlo + (e / KT) % JT, kk = e % KT;
-        const int2 yr = ay.krange[j];
-        const int ys = max(y0, yr.x), ye = min(y1, yr.y);
-        double acc = 0.0;
-        for (int y = ys; y <= ye; ++y)
-            acc = fma(wyp[4 * y + (j - ay.base[y])], sS[(i * ny + (y - y0)) * KT + kk], acc);
-        out[e] = acc;
+        const float bmin = st[b].bin_min;
+        const double rinv = 1.0 / (double)st[b].slope;
+        fit_item<0>(it, T, lv.wk3, reinterpret_cast<const double2 *>(lv.ax[0].w3i), ncy, ncz, Z,
+                    bins, U + b * VS, n, sE, bmin, rinv, rg, nbmax, nf);
+    } else {
+        fit_item<1>(it, T, lv.wk2, reinterpret_cast<const double2 *>(lv.ax[0].w2), ncy, ncz, Z,
+                    bins, U + b * VS, n, sE, 0.0f, 1.0, rg, nbmax, nf);
     }
 }
 
-// Sum the tile slabs of each volume in tile order: MODE 1 den; MODE 0 phi = num / den and
-// lattice += phi.  grid (volumes, lattice chunks of 256); a lattice col j only visits the tiles
-// whose slab covers it (lv.jt), eight slab loads in flight before the ordered sum.
+// clear the numerator of active volumes before a fit
 template <int MODE>
-__global__ void __launch_bounds__(VH_TPB) k_n4_tilesum(const double *part, int64_t slab,
-                                                      int64_t ntiles, float *lat, double *den,
-                                                      int64_t lat_cap, const N4State *st,
-                                                      DevLevel lv, int64_t vol0) {
+__global__ void __launch_bounds__(VH_TPB) k_n4_fit_clear(unsigned long long *numfix, int64_t lat_cap,
+                                                        int64_t nlat, const N4State *st, int64_t vol0) {
+    const int64_t b = vol0 + blockIdx.y;
+    if (MODE == 0 && !st[b].active) return;
+    const int64_t e = blockIdx.x * (int64_t)VH_TPB + threadIdx.x;
+    if (e < 2 * nlat) numfix[2 * b * lat_cap + e] = 0ull;
+}
+
+// MODE 1: den = fixed-point sum; MODE 0: phi = num / den (0 where den == 0), lattice += phi (S5)
+template <int MODE>
+__global__ void __launch_bounds__(VH_TPB) k_n4_latupd(const unsigned long long *numfix, float *lat,
+                                                     double *den, int64_t lat_cap, int64_t nlat,
+                                                     const N4State *st, int64_t vol0) {
     const int64_t b = vol0 + blockIdx.x;
     if (MODE == 0 && !st[b].active) return;
-    const int ncx = lv.ax[0].ncp, ncy = lv.ax[1].ncp, ncz = lv.ax[2].ncp;
-    const int e = blockIdx.y * VH_TPB + threadIdx.x;
-    if (e >= ncx * ncy * ncz) return;
-    const int i = e / (ncy * ncz), j = (e / ncz) % ncy, kq = e % ncz;
-    double acc = 0.0;
-    const double *pb = part + b * ntiles * slab;
-    const int2 tr = lv.jt[j];
-    for (int t0 = tr.x; t0 <= tr.y; t0 += 8) {
-        double v[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-            v[q] = 0.0;
-            const int t = t0 + q;
-            if (t > tr.y) continue;
-            const int4 m = lv.tiles[2 * t + 1];   // jlo, JT, klo, KT
-            const int jj = j - m.x, kk = kq - m.z;
-            if (kk >= 0 && kk < m.w) v[q] = pb[(int64_t)t * slab + (i * m.y + jj) * m.w + kk];
-        }
-#pragma unroll
-        for (int q = 0; q < 8; ++q) acc += v[q];
-    }
+    const int64_t e = blockIdx.y * (int64_t)VH_TPB + threadIdx.x;
+    if (e >= nlat) return;
+    const unsigned long long *nf = numfix + 2 * (b * lat_cap + e);
+    const double v = fix128_get(nf, nf + 1);
     if (MODE == 1) {
-        den[b * lat_cap + e] = acc;
+        den[b * lat_cap + e] = v;
     } else {
         const double d = den[b * lat_cap + e];
-        const float phi = d != 0.0 ? (float)(acc / d) : 0.0f;
+        const float phi = d != 0.0 ? (float)(v / d) : 0.0f;
         lat[b * lat_cap + e] += phi;
     }
 }
@@ -1037,7 +950,9 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_eval(const float *__restrict__ L0
                                                    int64_t VS, int rsh, const float *T,
                                                    int64_t tbuf, int64_t tcap, DevLevel lv,
                                                    DevLevel lvo, int bo_mode, N4State *st,
-                                                   double *part, int32_t c0) {
+                                                   double *part, int32_t c0, int conv_mode,
+                                                   const uint64_t *rmask, const int32_t *rrank,
+                                                   int64_t ntiles, float *D) {
     extern __shared__ __attribute__((aligned(16))) float4 sW[];   // [R] new, [R] old, then bases
     __shared__ double s_sd[VH_TPB / 64], s_sd2[VH_TPB / 64];
     __shared__ uint32_t s_max[VH_TPB / 64], s_min[VH_TPB / 64];
@@ -1111,9 +1026,16 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_eval(const float *__restrict__ L0
             }
             const float u = la[h + k] - bn;
             Ub[j] = u;
-            const double d = (double)expm1f(bo - bn);   // p - 1, p = exp(B_old - B_new)
-            sd += d;
-            sd2 = fma(d, d, sd2);
+            if (conv_mode == 0) {   // S7 input: the field difference at the voxel's raster rank
+                const int64_t col = r & cmask, tl = col >> 6;
+                const int64_t e = (b * ntiles + tl) * R + x;
+                const uint64_t m = rmask[e];
+                D[b * VS + rrank[e] + __popcll(m & ((1ull << (col & 63)) - 1ull))] = bo - bn;
+            } else {                // S7x
+                const double d = (double)expm1c(bo - bn);
+                sd += d;
+                sd2 = fma(d, d, sd2);
+            }
             const uint32_t key = f2key(u);
             kmax = key > kmax ? key : kmax;
             if (r == first) st[b].u_first = u;
@@ -1148,6 +1070,26 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_eval(const float *__restrict__ L0
         if (mx) atomicMax(&st[b].umax_key, mx);
         if (mn != 0xffffffffu) atomicMin(&st[b].umin_key, mn);
     }
+}
+
+// S7: ITK's float Welford convergence of the last eval of each active volume (two waves per
+// volume: n4_shared.h chain_wave_mu / chain_wave_sig over the raster-ordered field differences).
+__global__ void __launch_bounds__(128) k_n4_welford(const float *D, int64_t VS, const VolScalars *sc,
+                                                   N4State *st, int64_t vol0) {
+    __shared__ ChainSlot slots[CH_SLOTS];
+    __shared__ ChainState cs;
+    const int64_t b = vol0 + blockIdx.x;
+    if (!st[b].active) return;
+    if (threadIdx.x == 0) {
+        cs.a_done = 0;
+        cs.b_done = 0;
+    }
+    __syncthreads();
+    const int64_t n = sc[b].n_mask1;
+    if (threadIdx.x < 64) chain_wave_mu(D + b * VS, n, slots, &cs);
+    else chain_wave_sig(n, slots, &cs);
+    __syncthreads();
+    if (threadIdx.x == 0) st[b].conv_w = cs.conv;
 }
 
 // Exact cubic B-spline subdivision (spans doubled on every axis), axis by axis, one block/volume.
@@ -1209,8 +1151,9 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_final(const float *__restrict__ I
     int64_t kpos = emit ? b * V + colstart[b * CZ + (col & ~(int64_t)63)] : 0;
     uint32_t word = 0u;
     int wb = ax.base[0];
-    double t0 = col_T(p1, wb, ncy, Z, by, wy, z), t1 = col_T(p1, wb + 1, ncy, Z, by, wy, z);
-    double t2 = col_T(p1, wb + 2, ncy, Z, by, wy, z), t3 = col_T(p1, wb + 3, ncy, Z, by, wy, z);
+    // S9: the final field per S6 (float T window, float row sum), I / (float)exp((double)B)
+    float t0 = (float)col_T(p1, wb, ncy, Z, by, wy, z), t1 = (float)col_T(p1, wb + 1, ncy, Z, by, wy, z);
+    float t2 = (float)col_T(p1, wb + 2, ncy, Z, by, wy, z), t3 = (float)col_T(p1, wb + 3, ncy, Z, by, wy, z);
     // rows in groups of 8: the group's image loads are issued together, then the field, exp and
     // stores (the row walk of one column is otherwise a dependent load -> exp -> store chain)
     for (int64_t x0 = 0; x0 < R; x0 += 8) {
@@ -1225,12 +1168,12 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_final(const float *__restrict__ I
             while (wb < bx) {
                 ++wb;
                 t0 = t1; t1 = t2; t2 = t3;
-                t3 = col_T(p1, wb + 3, ncy, Z, by, wy, z);
+                t3 = (float)col_T(p1, wb + 3, ncy, Z, by, wy, z);
             }
             const float4 w = *reinterpret_cast<const float4 *>(ax.w + 4 * x);
-            const float bn = (float)((double)w.x * t0 + (double)w.y * t1 + (double)w.z * t2 + (double)w.w * t3);
+            const float bn = ((w.x * t0 + w.y * t1) + w.z * t2) + w.w * t3;
             const int64_t v = b * V + x * CZ + col;
-            const float o = iv[k] / expf(bn);   // OCML expf (<= 1 ulp of the double-rounded exp)
+            const float o = iv[k] / expf_cr(bn);
             out[v] = o;
             if (emit) {
                 if ((x & 31) == 0) word = colbits[(b * nw + (x >> 5)) * CZ + col];
@@ -1248,6 +1191,26 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_final(const float *__restrict__ I
 // ---------------------------------------------------------------------------------------------
 // One sub-batch [vol0, vol0 + ns): the whole multi-level loop.  Flat sweeps run over the chunk
 // range [cp[vol0], cp[vol0 + ns]); converged volumes' blocks exit at once.
+// Doubles of one fit ring row for level L: >= 64 and >= the largest tile's stage-1 output count.
+static int fit_rowcap(const vh_batch *b, const vh_n4_params &prm, int L) {
+    const int Z = (int)b->Z;
+    AxisTab tz;
+    const float eps = vh_bspline_eps(std::max({vh_level_ncp(prm, L, 0), vh_level_ncp(prm, L, 1),
+                                               vh_level_ncp(prm, L, 2)}) - 3);
+    vh_axis_tables(Z, vh_level_ncp(prm, L, 2), eps, tz);
+    int cap = 64;
+    for (int64_t c0 = 0; c0 < b->CZ; c0 += TILE_W) {
+        const int64_t c1 = std::min(c0 + TILE_W, b->CZ) - 1;
+        const int y0 = (int)(c0 / Z), y1 = (int)(c1 / Z), z0 = (int)(c0 % Z), z1 = (int)(c1 % Z);
+        const int klo = tz.base[y0 == y1 ? z0 : 0];
+        const int KT = tz.base[y0 == y1 ? z1 : Z - 1] + 4 - klo;
+        cap = std::max(cap, (y1 - y0 + 1) * KT);
+    }
+    return cap;
+}
+
+// One sub-batch [vol0, vol0 + ns): the whole multi-level loop.  Flat sweeps run over the chunk
+// range [cp[vol0], cp[vol0 + ns]); converged volumes' blocks exit at once.
 static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int64_t ns,
                         const std::vector<int32_t> &hcp) {
     hipStream_t st = b->ctx->stream;
@@ -1256,7 +1219,11 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
     const dim3 cg((unsigned)((b->CZ + VH_TPB - 1) / VH_TPB), (unsigned)ns);
     const int rsh = b->rsh;
     const int bins = prm.n_bins;
+    const int cm = prm.conv_mode;
     const int LOOK = 3;
+    const int nslots = (int)((b->R + SLOT_R - 1) / SLOT_R);
+    const int nitems = (int)ntiles * nslots;
+    const dim3 fg((unsigned)((nitems + FIT_WAVES - 1) / FIT_WAVES), (unsigned)ns);
     float *U = b->d_U;
     std::vector<hipEvent_t> evs;
     int32_t *hflag = b->ctx->h_pinned;
@@ -1267,31 +1234,40 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
     try {
         for (int L = 0; L < prm.n_levels; ++L) {
             const DevLevel lv = vh_dev_level(b, prm, L);
-            const int64_t nft = (b->CZ + FIT_W - 1) / FIT_W;
-            const dim3 fg((unsigned)nft, (unsigned)ns);
             const int ncx = lv.ax[0].ncp;
-            const int smax = b->fit_smax[L];
-            const size_t fit_lds = sizeof(double) * ((size_t)ncx * FIT_W + (size_t)smax + 5 * (size_t)b->R) +
-                                   sizeof(int) * (size_t)b->R;
-            if (fit_lds > 64 * 1024)
-                throw VhError{VH_ERR_ARG, "N4 fit: tile slab exceeds the LDS budget"};
+            const int rowcap = fit_rowcap(b, prm, L);
+            const size_t fit_lds = sizeof(double) * FIT_WAVES * 2 * FIT_NB * (size_t)rowcap;
+            if (fit_lds > 150 * 1024)
+                throw VhError{VH_ERR_ARG, "N4 fit: tile contraction rows exceed the LDS budget"};
+            static bool attr_set = false;
+            if (!attr_set) {
+                HIP_TRY(hipFuncSetAttribute((const void *)k_n4_fit_items<0>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));
+                HIP_TRY(hipFuncSetAttribute((const void *)k_n4_fit_items<1>,
+                                            hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));
+                attr_set = true;
+            }
             const int64_t nlat = (int64_t)ncx * lv.ax[1].ncp * lv.ax[2].ncp;
             const dim3 lg((unsigned)ns, (unsigned)((nlat + VH_TPB - 1) / VH_TPB));
+            const dim3 zg((unsigned)((2 * nlat + VH_TPB - 1) / VH_TPB), (unsigned)ns);
             const dim3 pg((unsigned)ns, (unsigned)((nlat / lv.ax[2].ncp * b->Z + VH_TPB - 1) / VH_TPB));
             {
                 ScopedKTimer tm(b, "n4_den", 0.0);
-                k_n4_fit<1><<<fg, VH_TPB, fit_lds, st>>>(
-                    U, b->d_ridx, b->d_rowstart, b->d_sc, b->R, b->C, b->Z, b->VS, ntiles, bins,
-                    b->d_st, b->d_E, lv, rsh, smax, b->lat_cap, b->d_fitpart, vol0);
+                k_n4_fit_clear<1><<<zg, VH_TPB, 0, st>>>(b->d_numfix, b->lat_cap, nlat, b->d_st, vol0);
                 VH_CHECK_LAUNCH();
-                k_n4_tilesum<1><<<lg, VH_TPB, 0, st>>>(b->d_fitpart, b->lat_cap, nft, b->d_lat,
-                                                       b->d_den, b->lat_cap, b->d_st, lv, vol0);
+                k_n4_fit_items<1><<<fg, FIT_WAVES * 64, fit_lds, st>>>(
+                    U, b->d_rowstart, b->d_rowmask, b->d_sc, (int)b->R, (int)b->C, (int)b->Z, b->VS,
+                    (int)ntiles, nslots, bins, b->d_st, b->d_E, lv, rowcap, FIT_NB, b->d_numfix,
+                    b->lat_cap, vol0);
+                VH_CHECK_LAUNCH();
+                k_n4_latupd<1><<<lg, VH_TPB, 0, st>>>(b->d_numfix, b->d_lat, b->d_den, b->lat_cap,
+                                                      nlat, b->d_st, vol0);
                 VH_CHECK_LAUNCH();
             }
             const int level_start = (int)evs.size();
             for (int it = 0; it < prm.max_iters[L]; ++it, ++gi) {
                 k_n4_ctrl<<<(unsigned)ns, VH_TPB, 0, st>>>(
-                    b->d_st, b->d_cpart, b->d_cp, b->d_sc, L, it, prm.conv_threshold, bins, vol0,
+                    b->d_st, b->d_cpart, b->d_cp, b->d_sc, cm, L, it, prm.conv_threshold, bins, vol0,
                     b->d_nactive + gi, U, b->d_colbits, b->d_rowstart, b->R, b->CZ, b->VS, ntiles);
                 VH_CHECK_LAUNCH();
                 HIP_TRY(hipMemcpyAsync(hflag + (gi % 1024), b->d_nactive + gi, sizeof(int32_t),
@@ -1312,16 +1288,18 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
                 VH_CHECK_LAUNCH();
                 {
                     ScopedKTimer tm(b, "n4_fit", 0.0);
-                    k_n4_fit<0><<<fg, VH_TPB, fit_lds, st>>>(
-                        U, b->d_ridx, b->d_rowstart, b->d_sc, b->R, b->C, b->Z, b->VS, ntiles, bins,
-                        b->d_st, b->d_E, lv, rsh, smax, b->lat_cap, b->d_fitpart, vol0);
+                    k_n4_fit_clear<0><<<zg, VH_TPB, 0, st>>>(b->d_numfix, b->lat_cap, nlat, b->d_st, vol0);
+                    VH_CHECK_LAUNCH();
+                    k_n4_fit_items<0><<<fg, FIT_WAVES * 64, fit_lds, st>>>(
+                        U, b->d_rowstart, b->d_rowmask, b->d_sc, (int)b->R, (int)b->C, (int)b->Z,
+                        b->VS, (int)ntiles, nslots, bins, b->d_st, b->d_E, lv, rowcap, FIT_NB,
+                        b->d_numfix, b->lat_cap, vol0);
                     VH_CHECK_LAUNCH();
                 }
                 {
                     ScopedKTimer tm(b, "n4_contract", 0.0);
-                    k_n4_tilesum<0><<<lg, VH_TPB, 0, st>>>(b->d_fitpart, b->lat_cap, nft,
-                                                           b->d_lat, b->d_den, b->lat_cap, b->d_st,
-                                                           lv, vol0);
+                    k_n4_latupd<0><<<lg, VH_TPB, 0, st>>>(b->d_numfix, b->d_lat, b->d_den, b->lat_cap,
+                                                          nlat, b->d_st, vol0);
                     VH_CHECK_LAUNCH();
                     k_n4_P1<<<pg, VH_TPB, 0, st>>>(b->d_lat, b->lat_cap, b->d_P1, b->q2_cap, b->Z,
                                                    b->d_st, lv, vol0);
@@ -1337,7 +1315,12 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
                     k_n4_eval<<<(unsigned)nch, VH_TPB, (size_t)b->R * 40, st>>>(
                         b->d_L0, U, b->d_ridx, b->d_cp, b->d_cvol, b->d_sc, b->R, b->CZ, b->VS, rsh,
                         b->d_T, b->nb * b->t_cap, b->t_cap, lv, lvo, bo_mode, b->d_st, b->d_cpart,
-                        ch0);
+                        ch0, cm, b->d_rowmask, b->d_rrank, ntiles, b->d_D);
+                    VH_CHECK_LAUNCH();
+                }
+                if (cm == 0) {
+                    ScopedKTimer tm(b, "n4_welford", 0.0);
+                    k_n4_welford<<<(unsigned)ns, 128, 0, st>>>(b->d_D, b->VS, b->d_sc, b->d_st, vol0);
                     VH_CHECK_LAUNCH();
                 }
                 const int k = (int)evs.size() - 1 - LOOK;
@@ -1346,7 +1329,7 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
                     if (hflag[(gi - LOOK) % 1024] == 0) { ++gi; break; }
                 }
             }
-            k_n4_level_end<<<(unsigned)ns, 64, 0, st>>>(b->d_st, b->d_cpart, b->d_cp, b->d_sc, L,
+            k_n4_level_end<<<(unsigned)ns, 64, 0, st>>>(b->d_st, b->d_cpart, b->d_cp, b->d_sc, cm, L,
                                                         vol0);
             VH_CHECK_LAUNCH();
             if (L < prm.n_levels - 1) {
@@ -1377,6 +1360,10 @@ void vh_launch_n4(vh_batch *b, const vh_n4_params &prm) {
             b->d_colbits, b->R, b->CZ, ntiles, b->d_rowstart, b->d_rowmask);
         VH_CHECK_LAUNCH();
         k_n4_rowscan<<<(unsigned)b->nb, VH_TPB, 0, st>>>(b->d_rowstart, ntiles * b->R);
+        VH_CHECK_LAUNCH();
+        if (b->R > 16384) throw VhError{VH_ERR_ARG, "N4: more than 16384 rows"};
+        k_n4_rrank<<<(unsigned)b->nb, VH_TPB, sizeof(int32_t) * (size_t)b->R, st>>>(
+            b->d_rowmask, b->R, ntiles, b->d_rrank);
         VH_CHECK_LAUNCH();
     }
     // driver: volume-resident (one workgroup per study) when the batch has studies for the CUs

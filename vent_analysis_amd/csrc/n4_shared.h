@@ -1,5 +1,8 @@
-// Declarations shared by the two N4 drivers: n4.hip (per-iteration sweeps over the whole batch)
-// and n4_study.hip (one workgroup per study, the whole level/iteration loop in one launch).
+// Declarations and device code shared by the two N4 drivers: n4.hip (per-iteration sweeps over
+// the whole batch) and n4_study.hip (one workgroup per study, the whole level/iteration loop in
+// one launch).  Both drivers evaluate the N4 build spec (oracle/n4_oracle.c header, S1-S9)
+// operation for operation, so U = L0 - B is bit-identical between them and the CPU oracle after
+// every iteration.
 #pragma once
 #include "vh_internal.h"
 
@@ -7,24 +10,27 @@ struct DevAxis {
     const int32_t *base;
     const float *w;
     const double *sw2;
-    const double *isw2;   // 1 / sw2
+    const double *isw2;   // 1 / sum w^2
     const double *w2;     // [n][4] w^2 (double)
     const double *w3;     // [n][4] w^3 (double)
+    const double *w3i;    // [n][4] w^3 * isw2 (row axis: the fit's numerator row weights, S5)
     const int2 *krange;   // [ncp] first / last index whose support contains control point k
     int32_t n, ncp;
 };
 struct DevLevel {
     DevAxis ax[3];
-    // per 128-column fit tile: {y0, y1, z0, z1} (first/last column's col and slice), then
-    // {jlo, JT, klo, KT} (lattice cols / slices the tile's slab covers)
-    const int4 *tiles;
-    const int2 *jt;   // per lattice col j: first / last tile whose slab covers j
+    const int32_t *xst;   // [ncx - 2]: first row x with base[x] >= i (xst[ncx - 3] = R)
+    const double *wk3;    // [ncz][Z] dense slice weights w^3 (0 outside the support)
+    const double *wk2;    // [ncz][Z] w^2
 };
 
-#define TILE_W 64   // columns per compact tile (one wave)
+#define TILE_W 64   // columns per compact tile / fit item (one wave)
+#define SLOT_R 64   // rows per fit item
 #define VH_OOB 0x80000000u
-#define N4_FIX 4294967296.0    // 2^32: fixed-point scale of the fit contractions
+#define N4_FIX 4294967296.0    // 2^32
 #define N4_MAGIC 6755399441055744.0   // 1.5 * 2^52: x + MAGIC rounds x to an integer (|x| < 2^51)
+#define HIST_UNIT 16777216.0f   // 2^24: Parzen weight unit (S3)
+#define HIST_CSHIFT 44          // packed histogram word: count << 44 | sum of o-weights
 #define LN2 0.69314718055994530942
 #define PI_D 3.14159265358979323846
 
@@ -35,19 +41,10 @@ DevLevel vh_dev_level(const vh_batch *b, const vh_n4_params &prm, int L);
 bool vh_n4_study_eligible(const vh_batch *b, const vh_n4_params &prm, size_t *lds_bytes);
 void vh_launch_n4_study(vh_batch *b, const vh_n4_params &prm);
 
-// ---- device helpers shared by both drivers ----------------------------------------------------
-__device__ __forceinline__ float sharpen_value(float u, float bmin, float slope, const float *E,
-                                               int bins) {
-    const float cidx = (u - bmin) / slope;
-    const int idx = (cidx >= 0.0f && cidx < (float)bins) ? (int)floorf(cidx) : bins;
-    if (idx < bins - 1) return E[idx] + (E[idx + 1] - E[idx]) * (cidx - (float)idx);
-    return E[bins - 1];
-}
-
+// ---- small device helpers ----------------------------------------------------------------------
 __device__ __forceinline__ int lanes_below(uint64_t m) {
     return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
-
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
     for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, off, 64));
     return v;
@@ -56,28 +53,495 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
     for (int off = 32; off > 0; off >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, off, 64));
     return v;
 }
+__device__ __forceinline__ void wave_lds_order() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
+// correctly rounded float exp through double (S1/S7/S9)
 __device__ __forceinline__ float expf_cr(float x) { return (float)exp((double)x); }
 
-// Histogram bin weights of one U value (triangular Parzen, u64 fixed point 2^-32); same
-// expressions as oracle/n4_oracle.c.  Returns false when the value adds nothing.
-__device__ __forceinline__ bool parzen_bin(float u, float bmin, float slope, int bins, int &idx,
-                                           unsigned long long &a0, unsigned long long &a1) {
-    const float cidx = (u - bmin) / slope;   // NaN (padding) fails both range tests
-    if (!(cidx >= 0.0f) || !(cidx < (float)bins)) return false;
-    idx = (int)floorf(cidx);
-    const float o = cidx - (float)idx;
-    a1 = 0ull;
-    if (o == 0.0f) {
-        a0 = 1ull << 32;
-    } else if (idx < bins - 1) {
-        // both products are < 2^32 (o in (0, 1)), so the single-instruction f64 -> u32
-        // conversion truncates exactly like the u64 one; 1 - o rounds to 1 only for tiny o
-        const float om = 1.0f - o;
-        a0 = om == 1.0f ? (1ull << 32) : (unsigned long long)(uint32_t)((double)om * 4294967296.0);
-        a1 = (unsigned long long)(uint32_t)((double)o * 4294967296.0);
-    } else {
-        return false;
+// S7x (conv_mode 1): expm1 of a float field difference
+__device__ __forceinline__ float expm1c(float x) {
+    if (fabsf(x) < 0.0625f)
+        return x + x * x * (0.5f + x * (0.16666667f + x * (0.041666668f + x * 0.008333334f)));
+    return (float)expm1((double)x);
+}
+
+// c / slope as IEEE float division, evaluated as (double)c * (1 / (double)slope) rounded once to
+// float.  The double product is within 2^-52 (relative) of the exact quotient, and a quotient of
+// two floats is never closer than 2^-49 (relative) to a float rounding midpoint, so the rounding
+// lands on the correctly rounded quotient: bit-equal to c / slope.
+__device__ __forceinline__ float div_r(float c, double rinv) { return (float)((double)c * rinv); }
+
+// S3 sharpen value E(u)
+__device__ __forceinline__ float sharpen_r(float u, float bmin, double rinv, const float *E, int bins) {
+    const float cidx = div_r(u - bmin, rinv);
+    const int idx = (cidx >= 0.0f && cidx < (float)bins) ? (int)floorf(cidx) : bins;
+    if (idx < bins - 1) return E[idx] + (E[idx + 1] - E[idx]) * (cidx - (float)idx);
+    return E[bins - 1];
+}
+
+// S3 Parzen histogram contribution of one U value, packed as (1 << 44) | trunc(o * 2^24) on bin
+// idx; 0 (and idx = 0) when the value adds nothing (outside [0, bins), NaN padding, or the last bin
+// with o > 0 -- ITK's else-if).  Bin b of the histogram is then
+//   H[b] = count[b] * 2^24 - osum[b] + osum[b - 1]      (2^-24 units, exact integers)
+// i.e. the value adds 2^24 - a1 to bin idx and a1 to bin idx + 1.  One 64-bit add per value; a
+// packed bin stays exact for < 2^20 values.
+__device__ __forceinline__ unsigned long long hist_pack(float u, float bmin, double rinv, int bins,
+                                                        int &idx) {
+    const float cidx = div_r(u - bmin, rinv);
+    const bool in = cidx >= 0.0f && cidx < (float)bins;   // false for NaN
+    const float cf = in ? floorf(cidx) : 0.0f;
+    const float o = in ? cidx - cf : 0.0f;
+    idx = (int)cf;
+    const bool keep = in && !(idx == bins - 1 && o > 0.0f);
+    const uint32_t a1 = (uint32_t)(o * HIST_UNIT);   // o * 2^24 is exact in float
+    return keep ? ((1ull << HIST_CSHIFT) | (unsigned long long)a1) : 0ull;
+}
+__device__ __forceinline__ unsigned long long hist_count(unsigned long long w) { return w >> HIST_CSHIFT; }
+__device__ __forceinline__ unsigned long long hist_osum(unsigned long long w) {
+    return w & ((1ull << HIST_CSHIFT) - 1ull);
+}
+
+// ---- 128-bit fixed point -------------------------------------------------------------------------
+// Exact, order-free accumulation of doubles with a huge dynamic range: trunc(|v| 2^80) as a 128-bit
+// two's-complement integer, kept as (lo u64, hi i64) and added with integer atomics (LDS or global),
+// the low word's carry detected from the value the atomic returns.
+__device__ __forceinline__ void fix128_add(unsigned long long *lo, unsigned long long *hi, double v) {
+    const double s = fabs(v) * 65536.0;            // |v| * 2^16, exact
+    const double fh = floor(s);
+    unsigned long long h = (unsigned long long)fh; // s < 2^53
+    const double r = s - fh;                       // fractional bits of s: [0, 1), exact
+    unsigned long long l = (unsigned long long)(r * 18446744073709551616.0);   // < 2^64
+    if (v < 0.0) {                                 // two's-complement negation of (h, l)
+        l = ~l + 1ull;
+        h = ~h + (l == 0ull ? 1ull : 0ull);
     }
+    const unsigned long long old = atomicAdd(lo, l);
+    const unsigned long long carry = old + l < old ? 1ull : 0ull;
+    atomicAdd(hi, h + carry);
+}
+__device__ __forceinline__ double fix128_get(const unsigned long long *lo, const unsigned long long *hi) {
+    return (double)(long long)*hi * (1.0 / 65536.0) + (double)*lo * 8.271806125530277e-25;   // 2^-80
+}
+
+__device__ __forceinline__ float wsel(float4 w, int d) {
+    return d == 0 ? w.x : d == 1 ? w.y : d == 2 ? w.z : w.w;
+}
+template <int P>
+__device__ __forceinline__ double wpow(float w) {
+    const double d = (double)w;
+    return P == 3 ? d * d * d : d * d;
+}
+
+// ---- one level's axis tables as the fit / eval read them (LDS in n4_study, global in n4) ------
+struct TabV {
+    const float4 *wx, *wy, *wz;
+    const double *ix, *iy, *iz;
+    const int32_t *bx, *by, *bz;
+    const int2 *krz;
+    const int32_t *xst;   // [ncx - 2]
+};
+
+// ---------------------------------------------------------------------------------------------
+// work item = (64-column tile, 64-row slot) of one study: the wave's view of its rows
+// ---------------------------------------------------------------------------------------------
+struct Item {
+    int tile, x0, xs, xe;     // wave-uniform: tile, slot's first row, first / last non-empty row
+    uint64_t mreg;            // lane l: mask == 1 lanes of row x0 + l
+    int rsreg;                // lane l: compact offset of row x0 + l
+    int rrreg;                // lane l: raster rank of the first masked voxel of (tile, row x0 + l)
+    int col, y, z;            // this lane's column
+    bool colok;
+    int c0, y0, y1, z0, z1, ny;   // tile geometry (uniform)
+};
+
+// rowmask / rowstart / rrank: [tiles][R] arrays of this study
+__device__ __forceinline__ bool item_begin(Item &it, const uint64_t *rowmask, const int32_t *rowstart,
+                                           const int32_t *rrank, int R, int C, int Z, int CZ,
+                                           int nslots, int item) {
+    const int lane = threadIdx.x & 63;
+    it.tile = item / nslots;
+    it.x0 = (item % nslots) * SLOT_R;
+    const int64_t rbase = (int64_t)it.tile * R;
+    const int xr = it.x0 + lane;
+    it.mreg = xr < R ? rowmask[rbase + xr] : 0ull;
+    it.rsreg = xr < R ? rowstart[rbase + xr] : 0;
+    it.rrreg = (rrank && xr < R) ? rrank[rbase + xr] : 0;
+    const uint64_t nzb = __ballot(it.mreg != 0ull);
+    if (nzb == 0ull) return false;
+    it.xs = it.x0 + __builtin_ctzll(nzb);
+    it.xe = it.x0 + 63 - __builtin_clzll(nzb);
+    it.col = it.tile * TILE_W + lane;
+    it.colok = it.col < CZ;
+    it.y = it.colok ? it.col / Z : 0;
+    it.z = it.colok ? it.col % Z : 0;
+    it.c0 = it.tile * TILE_W;
+    const int c1 = min(it.c0 + TILE_W, CZ) - 1;
+    it.y0 = it.c0 / Z;
+    it.y1 = c1 / Z;
+    it.z0 = it.c0 % Z;
+    it.z1 = c1 % Z;
+    it.ny = it.y1 - it.y0 + 1;
+    (void)C;
     return true;
+}
+
+// Compact byte offset of (row x, this lane) or VH_OOB when the voxel is not in the mask; x is
+// wave-uniform and inside the item's slot.  With rr != nullptr also the voxel's raster rank (index
+// among the study's masked voxels in raster order: the order of ITK's convergence scan).
+__device__ __forceinline__ uint32_t item_off(const Item &it, int x, bool valid, int *rr = nullptr) {
+    const int lane = threadIdx.x & 63;
+    const int xl = x - it.x0;
+    const uint32_t mlo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)it.mreg, xl);
+    const uint32_t mhi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(it.mreg >> 32), xl);
+    const uint64_t m = ((uint64_t)mhi << 32) | mlo;
+    const int r0 = __builtin_amdgcn_readlane(it.rsreg, xl);
+    const bool on = valid && ((m >> lane) & 1ull);
+    const int below = lanes_below(m);
+    if (rr) *rr = __builtin_amdgcn_readlane(it.rrreg, xl) + below;
+    return on ? (uint32_t)(r0 + below) * 4u : VH_OOB;
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t st_rsrc(const float *base, int64_t n) {
+    return __builtin_amdgcn_make_buffer_rsrc((void *)base, 0, (int)(n * 4), 0x00020000);
+}
+__device__ __forceinline__ float st_load(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, 0, 0));
+}
+__device__ __forceinline__ void st_store(__amdgpu_buffer_rsrc_t r, uint32_t voff, float v) {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)voff, 0, 0);
+}
+
+// ---------------------------------------------------------------------------------------------
+// S5 fit: contraction of finished control rows of the item's tile (wave-collective).  A wave keeps
+// up to nbmax finished rows Q[r][lane] (control rows i0 .. i0+nr-1) in its LDS ring and contracts
+// them together:
+//   S[r][y][k]    = fma chain over the tile's slices z of col y (ascending): Wk[k][z] Q[r][(y, z)]
+//   num[i0+r][j][k] += fix128( fma chain over the tile's cols y (ascending): wy(y, j)^P S[r][y][k] )
+// In place (S overwrites Q) when the batch's stage-1 outputs fit the lanes' FIT_SO slots (all reads
+// of a batch finish before its writes); otherwise into the separate buffer Sx, in chunks.
+// ---------------------------------------------------------------------------------------------
+#define FIT_NB 4        // finished control rows per contraction batch (max)
+#define FIT_SO 4        // stage-1 outputs per lane per chunk
+#define FIT_G 8         // rows per lane with loads in flight together
+
+struct FitRing {
+    double *q;        // [nbmax][rowcap] this wave's rows
+    double *sx;       // separate stage-1 output buffer ([nbmax][rowcap]) or nullptr (in place)
+    int rowcap;       // doubles per row (>= 64, >= ny * KT)
+    int nbmax;        // rows per batch for this geometry
+    int nr, i0;       // rows held, control row of row 0
+};
+
+template <int P>
+__device__ void fit_contract(FitRing &rg, const Item &it, const TabV &T, const double *Wk, int ncy,
+                             int ncz, int Z, unsigned long long *numfix) {
+    const int nr = rg.nr;
+    if (nr == 0) return;
+    const int lane = threadIdx.x & 63;
+    wave_lds_order();
+    const int klo = T.bz[it.y0 == it.y1 ? it.z0 : 0];
+    const int KT = T.bz[it.y0 == it.y1 ? it.z1 : Z - 1] + 4 - klo;
+    const int nyk = it.ny * KT;
+    double *S = rg.sx ? rg.sx : rg.q;
+    for (int o0 = 0; o0 < nr * nyk; o0 += 64 * FIT_SO) {
+        // the FIT_SO outputs of a lane are independent fma chains over their slices: walk them in
+        // lockstep (step s of every chain together) so the LDS latency of one chain hides behind
+        // the others; each chain still adds its terms in slice order
+        double outv[FIT_SO];
+        const double *qp[FIT_SO], *wp[FIT_SO];
+        int len[FIT_SO];
+        int maxlen = 0;
+#pragma unroll
+        for (int q = 0; q < FIT_SO; ++q) {
+            outv[q] = 0.0;
+            len[q] = 0;
+            qp[q] = rg.q;
+            wp[q] = Wk;
+            const int o = o0 + lane + 64 * q;
+            if (o >= nr * nyk) continue;
+            const int r = o / nyk, yk = o % nyk;
+            const int yy = yk / KT, k = klo + yk % KT, yv = it.y0 + yy;
+            const int zlo = yv == it.y0 ? it.z0 : 0, zhi = yv == it.y1 ? it.z1 : Z - 1;
+            const int2 kr = T.krz[k];
+            const int zs = max(zlo, kr.x), ze = min(zhi, kr.y);
+            qp[q] = rg.q + r * rg.rowcap + (yv * Z - it.c0) + zs;
+            wp[q] = Wk + k * Z + zs;
+            len[q] = max(ze - zs + 1, 0);
+            maxlen = max(maxlen, len[q]);
+        }
+#pragma unroll 1
+        for (int s = 0; s < maxlen; ++s) {
+#pragma unroll
+            for (int q = 0; q < FIT_SO; ++q) {
+                const int ss = min(s, max(len[q] - 1, 0));   // in-range read for finished chains
+                const double v = fma(wp[q][ss], qp[q][ss], outv[q]);
+                outv[q] = s < len[q] ? v : outv[q];
+            }
+        }
+        if (!rg.sx) wave_lds_order();   // in place: every read of the batch before any write
+#pragma unroll
+        for (int q = 0; q < FIT_SO; ++q) {
+            const int o = o0 + lane + 64 * q;
+            if (o < nr * nyk) S[(o / nyk) * rg.rowcap + o % nyk] = outv[q];
+        }
+    }
+    wave_lds_order();
+    const int jlo = T.by[it.y0];
+    const int JT = T.by[it.y1] + 4 - jlo;
+    const int njk = JT * KT;
+    for (int o = lane; o < nr * njk; o += 64) {
+        const int r = o / njk, jk = o % njk;
+        const int j = jlo + jk / KT, kk = jk % KT, k = klo + kk;
+        const double *sr = S + r * rg.rowcap;
+        double acc = 0.0;
+        for (int yy = 0; yy < it.ny; ++yy) {
+            const int d = j - T.by[it.y0 + yy];
+            if (d < 0 || d > 3) continue;
+            acc = fma(wpow<P>(wsel(T.wy[it.y0 + yy], d)), sr[yy * KT + kk], acc);
+        }
+        if (acc != 0.0) {
+            const int64_t e = ((int64_t)(rg.i0 + r) * ncy + j) * ncz + k;
+            fix128_add(numfix + 2 * e, numfix + 2 * e + 1, acc);
+        }
+    }
+    wave_lds_order();
+    rg.nr = 0;
+}
+
+// control row i (this lane's value v) is finished: into the ring, contract when the batch is full
+template <int P>
+__device__ __forceinline__ void fit_push(FitRing &rg, double v, int i, const Item &it,
+                                         const TabV &T, const double *Wk, int ncy, int ncz, int Z,
+                                         unsigned long long *numfix) {
+    if (rg.nr == 0) rg.i0 = i;
+    rg.q[rg.nr * rg.rowcap + (threadIdx.x & 63)] = v;
+    if (++rg.nr == rg.nbmax) fit_contract<P>(rg, it, T, Wk, ncy, ncz, Z, numfix);
+}
+
+// rows per contraction batch for this item's geometry
+__device__ __forceinline__ void fit_ring_begin(FitRing &rg, const Item &it, const TabV &T, int Z,
+                                               int nb_ring) {
+    const int klo = T.bz[it.y0 == it.y1 ? it.z0 : 0];
+    const int KT = T.bz[it.y0 == it.y1 ? it.z1 : Z - 1] + 4 - klo;
+    rg.nbmax = rg.sx ? nb_ring : max(1, min(nb_ring, 64 * FIT_SO / (it.ny * KT)));
+    rg.nr = 0;
+}
+
+// One item's fit (S5).  MODE 0: numerator, row weights Wx = wx^3 / sum wx^2 (double2 pairs
+// [2x], [2x+1]), p = (double)(u - sharpen(u)) * (1/sum wy^2 * 1/sum wz^2); MODE 1: denominator,
+// Wx = wx^2, p = 1.  Each control row's column partial is an fma chain over the item's rows in
+// row order: acc_a = fma(Wx(x, a), p(x), acc_a) for the window's four control rows.
+template <int MODE>
+__device__ void fit_item(const Item &it, const TabV &T, const double *Wk, const double2 *Wx,
+                         int ncy, int ncz, int Z, int bins, const float *Ub, int64_t n,
+                         const float *sE, float bmin, double rinv, FitRing &rg, int nb_ring,
+                         unsigned long long *numfix) {
+    constexpr int P = MODE == 0 ? 3 : 2;
+    const __amdgpu_buffer_rsrc_t rU = st_rsrc(Ub, n);
+    const double isyz = MODE == 0 ? T.iy[it.y] * T.iz[it.z] : 1.0;
+    int wb = T.bx[it.xs];
+    double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0, acc3 = 0.0;
+    int x = it.xs, tail = 0;
+    fit_ring_begin(rg, it, T, Z, nb_ring);
+#pragma unroll 1
+    for (;;) {
+        if (x <= it.xe) {   // rows of control span wb: the window does not move
+            const int rb = min(it.xe, T.xst[wb + 1] - 1);
+#pragma unroll 1
+            for (int xb = x; xb <= rb; xb += FIT_G) {
+                uint32_t offs[FIT_G];
+                float u[FIT_G];
+#pragma unroll
+                for (int g = 0; g < FIT_G; ++g) {
+                    const int xg = xb + g;
+                    offs[g] = item_off(it, xg <= rb ? xg : rb, xg <= rb);
+                    if (MODE == 0) u[g] = st_load(rU, offs[g]);
+                }
+#pragma unroll
+                for (int g = 0; g < FIT_G; ++g) {
+                    if (offs[g] == VH_OOB) continue;
+                    const int xg = xb + g;
+                    const double2 wa = Wx[2 * xg], wc = Wx[2 * xg + 1];
+                    if (MODE == 0) {
+                        const float rv = u[g] - sharpen_r(u[g], bmin, rinv, sE, bins);
+                        const double p = (double)rv * isyz;
+                        acc0 = fma(wa.x, p, acc0);
+                        acc1 = fma(wa.y, p, acc1);
+                        acc2 = fma(wc.x, p, acc2);
+                        acc3 = fma(wc.y, p, acc3);
+                    } else {
+                        acc0 += wa.x;
+                        acc1 += wa.y;
+                        acc2 += wc.x;
+                        acc3 += wc.y;
+                    }
+                }
+            }
+            x = rb + 1 > x ? rb + 1 : x;
+        }
+        fit_push<P>(rg, acc0, wb, it, T, Wk, ncy, ncz, Z, numfix);   // control row wb is done
+        acc0 = acc1; acc1 = acc2; acc2 = acc3; acc3 = 0.0;
+        ++wb;
+        if (x > it.xe && ++tail == 4) break;
+    }
+    fit_contract<P>(rg, it, T, Wk, ncy, ncz, Z, numfix);
+}
+
+// ---------------------------------------------------------------------------------------------
+// U range for the next histogram (S2).  ITK scans in raster order with
+//   if (u > max) max = u; else if (u < min) min = u;
+// so the minimum skips every "record" voxel (strictly above all earlier ones).  The records that
+// can matter form the strictly increasing run u1 < u2 < ... < uK at the start of the raster order
+// (a later record is above a non-record voxel).  The sweeps keep the maximum and the three smallest
+// values (a multiset) per lane; with u1, u2, u3 read back afterwards, min over all but the run is
+// exact for K <= 2, and a run of 3 or more falls back to the exact raster scan.
+// ---------------------------------------------------------------------------------------------
+struct Range3 {
+    float mx, m1, m2, m3;   // max; three smallest, m1 <= m2 <= m3
+};
+__device__ __forceinline__ void r3_init(Range3 &r) {
+    r.mx = -FLT_MAX;
+    r.m1 = r.m2 = r.m3 = FLT_MAX;
+}
+// insert u into the sorted triple (med3 keeps the three smallest of the multiset)
+__device__ __forceinline__ void r3_ins(Range3 &r, float u) {
+    r.m3 = __builtin_amdgcn_fmed3f(r.m2, r.m3, u);
+    r.m2 = __builtin_amdgcn_fmed3f(r.m1, r.m2, u);
+    r.m1 = fminf(r.m1, u);
+}
+__device__ __forceinline__ void r3_add(Range3 &r, float u) {
+    r.mx = fmaxf(r.mx, u);
+    r3_ins(r, u);
+}
+__device__ __forceinline__ void r3_merge(Range3 &r, const Range3 &o) {
+    r.mx = fmaxf(r.mx, o.mx);
+    r3_ins(r, o.m1);
+    r3_ins(r, o.m2);
+    r3_ins(r, o.m3);
+}
+__device__ __forceinline__ Range3 r3_wave(Range3 r) {
+    for (int off = 32; off > 0; off >>= 1) {
+        Range3 o;
+        o.mx = __shfl_xor(r.mx, off, 64);
+        o.m1 = __shfl_xor(r.m1, off, 64);
+        o.m2 = __shfl_xor(r.m2, off, 64);
+        o.m3 = __shfl_xor(r.m3, off, 64);
+        r3_merge(r, o);
+    }
+    return r;
+}
+// ITK's bin minimum from the merged range and the first three masked voxels' values (u[0..2],
+// nfirst of them exist).  Returns false when the exact raster scan is needed.
+__device__ __forceinline__ bool r3_bin_min(const Range3 &r, const float *u, int nfirst, float &bmin) {
+    if (nfirst < 3) return false;
+    if (!(u[1] > u[0])) {                       // K = 1: exclude u1
+        bmin = u[0] == r.m1 ? r.m2 : r.m1;
+        return true;
+    }
+    if (!(u[2] > u[1])) {                       // K = 2: exclude u1 < u2
+        if (u[0] != r.m1) bmin = r.m1;
+        else bmin = u[1] == r.m2 ? r.m3 : r.m2;
+        return true;
+    }
+    return false;                               // K >= 3
+}
+
+// ---------------------------------------------------------------------------------------------
+// S7 convergence (conv_mode 0): ITK's float Welford recurrence over the masked voxels in raster
+// order, d_k = B_old - B_new read from a raster-ordered buffer.  Two waves of one workgroup:
+//   wave A (mu): per block of 64 steps, all lanes compute p = (float)exp((double)d), 1/k, the mu
+//     step constants (1 - 1/k, p/k) and (k-1)/k into an LDS slot; then lane 0 runs
+//       mu <- (float)fma((double)mu, 1 - 1/k, (double)(p / k))      (one step per voxel)
+//     recording mu before each step for wave B.
+//   wave B (sig): per block, all lanes form s = (p - mu_prev)^2 (float); lane 0 runs
+//       sig <- (float)fma((double)s, (k-1)/k, (double)sig)          (k >= 2)
+// The recurrences are inherently serial (the float running mean drifts); the slot ring and two
+// LDS counters let the two waves overlap.  Result: conv = (float)sqrt(sig / (n-1)) / mu.
+// ---------------------------------------------------------------------------------------------
+#define CH_SLOTS 4
+struct ChainSlot {
+    double2 ab[64];    // (1 - 1/k, p / k) for wave A
+    double c[64];      // (k - 1) / k
+    double s[64];      // (double)(p - mu_prev)^2, written by wave B
+    float p[64];
+    float mu[64];      // mu before step k
+};
+struct ChainState {
+    int a_done, b_done;   // blocks finished by wave A / wave B
+    float mu, conv;
+};
+
+__device__ __forceinline__ int lds_load_acq(int *p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_store_rel(int *p, int v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// wave A.  Dr: the n raster-ordered d values of the study (global).
+__device__ void chain_wave_mu(const float *Dr, int64_t n, ChainSlot *slots, ChainState *cs) {
+    const int lane = threadIdx.x & 63;
+    double mu = 0.0;
+    const int64_t nblk = (n + 63) / 64;
+    for (int64_t blk = 0; blk < nblk; ++blk) {
+        ChainSlot &S = slots[blk % CH_SLOTS];
+        if (blk >= CH_SLOTS)
+            while (lds_load_acq(&cs->b_done) <= (int)(blk - CH_SLOTS)) __builtin_amdgcn_s_sleep(1);
+        const int64_t j = blk * 64 + lane;
+        const bool ok = j < n;
+        const float d = ok ? Dr[j] : 0.0f;
+        const float p = expf_cr(d);
+        const double kd = (double)(j + 1);
+        const double r = 1.0 / kd;
+        S.ab[lane] = make_double2(1.0 - r, (double)(float)((double)p * r));   // p / k, div_r form
+        S.c[lane] = (kd - 1.0) / kd;
+        S.p[lane] = p;
+        wave_lds_order();
+        if (lane == 0) {
+            const int m = (int)min((int64_t)64, n - blk * 64);
+#pragma unroll 4
+            for (int l = 0; l < m; ++l) {
+                const double2 ab = S.ab[l];
+                S.mu[l] = (float)mu;
+                mu = (double)(float)fma(mu, ab.x, ab.y);
+            }
+        }
+        wave_lds_order();
+        if (lane == 0) {
+            if (blk == nblk - 1) cs->mu = (float)mu;   // published by the release below
+            lds_store_rel(&cs->a_done, (int)(blk + 1));
+        }
+    }
+}
+
+// wave B.  Returns conv in cs->conv (also the return value on lane 0).
+__device__ void chain_wave_sig(int64_t n, ChainSlot *slots, ChainState *cs) {
+    const int lane = threadIdx.x & 63;
+    double sig = 0.0;
+    const int64_t nblk = (n + 63) / 64;
+    for (int64_t blk = 0; blk < nblk; ++blk) {
+        ChainSlot &S = slots[blk % CH_SLOTS];
+        while (lds_load_acq(&cs->a_done) <= (int)blk) __builtin_amdgcn_s_sleep(1);
+        const float q = S.p[lane] - S.mu[lane];
+        S.s[lane] = (double)(q * q);
+        wave_lds_order();
+        if (lane == 0) {
+            const int m = (int)min((int64_t)64, n - blk * 64);
+            int l = blk == 0 ? 1 : 0;   // k = 1 adds nothing (N > 1 test)
+#pragma unroll 4
+            for (; l < m; ++l) sig = (double)(float)fma(S.s[l], S.c[l], sig);
+        }
+        wave_lds_order();
+        if (lane == 0) lds_store_rel(&cs->b_done, (int)(blk + 1));
+    }
+    if (lane == 0) {
+        while (lds_load_acq(&cs->a_done) < (int)nblk) __builtin_amdgcn_s_sleep(1);
+        const float mu = cs->mu;
+        const float s = (float)sqrt(sig / ((double)n - 1.0));
+        cs->conv = s / mu;
+    }
 }

@@ -1,28 +1,27 @@
 // n4_study.hip -- volume-resident N4 bias-field correction on gfx950: ONE workgroup (1024 threads,
 // 16 waves) per study runs the whole multi-level iteration loop of
-// sitk.N4BiasFieldCorrectionImageFilter (Vent_Analysis.py:316-334; CPU twin
-// oracle/n4_oracle.c) in a single launch.  Between sweeps the study's small state -- B-spline
-// lattice, fit denominators, the z-contracted lattices P1 (current and previous field), level
-// tables, histogram, FFT buffers, E(u) map -- never leaves LDS, so an iteration costs three
-// streaming passes over the compact masked voxels and workgroup barriers, with no kernel launches,
-// no grid-wide dependencies and no host round trips.  A batch of >= one study per CU fills the
-// chip (256 studies on 256 CUs); per-study work is a fixed 16 B per masked voxel per iteration.
+// sitk.N4BiasFieldCorrectionImageFilter (Vent_Analysis.py:316-334; build spec
+// S1-S9 in oracle/n4_oracle.c, which this kernel matches bit for bit) in a single launch.  Between
+// sweeps the study's small state -- B-spline lattice, fit denominators, the z-contracted lattices
+// P1 (current and previous field), level tables, histogram, FFT buffers, E(u) map -- never leaves
+// LDS, so an iteration costs three streaming passes over the compact masked voxels, workgroup
+// barriers and (conv_mode 0) the serial convergence recurrence, with no kernel launches, no
+// grid-wide dependencies and no host round trips.  A batch of >= one study per CU fills the chip.
 //
 // Per iteration (all inside the workgroup):
-//   ctrl  convergence of the previous field, ITK's while-condition, bin range (+ the exact raster
-//         minimum when the first masked voxel is the strict minimum)
-//   hist  flat pass over compact U: triangular Parzen histogram, u64 fixed point, 8 LDS copies
-//   emap  512-point radix-2 FFT Wiener deconvolution in LDS (two transforms per stage)
+//   ctrl  convergence of the previous iteration, ITK's while-condition, bin range (S2: max and the
+//         three smallest U per item, merged; ITK's else-if minimum from the first masked voxels)
+//   hist  flat pass over compact U: packed Parzen histogram (S3), one 64-bit LDS add per value
+//   emap  512-point radix-2 FFT Wiener deconvolution in LDS (S4)
 //   fit   column walk: a wave owns one (64-column tile, 64-row slot) item; each lane one column,
-//         the row axis contracted in registers by a sliding 4-wide window (fixed row order, f64);
-//         each finished control row i is contracted over the tile's slices and cols in the wave
-//         and added to the lattice numerator with 128-bit fixed-point LDS atomics (order-free)
-//   lat   phi = num / den, lattice += phi, P1 = lattice contracted over slices (f64)
-//   eval  column walk again: per lane the column's T(i) window for the new and the previous
-//         field (same float expressions as n4.hip's k_n4_T / k_n4_eval, so B_old is the previous
-//         B_new exactly), U = L0 - B_new stored, convergence sums per item (summed in item order)
-// Work items are taken from an LDS counter; every reduction is either integer (order-free) or
-// per item in a fixed order, so results are deterministic.
+//         the row axis contracted in registers by a sliding 4-wide window (S5), finished control
+//         rows contracted over the tile's slices and cols, 128-bit fixed-point LDS atomics
+//   lat   phi = num / den, lattice += phi, P1 = lattice contracted over slices (S6)
+//   eval  column walk again: B_new and B_old from the column's T windows, U = L0 - B_new, the field
+//         difference d written in raster order (conv_mode 0) or the exact-CoV sums (conv_mode 1)
+//   conv  (conv_mode 0) two waves run ITK's float Welford recurrence over d in raster order (S7)
+// Work items are taken from an LDS counter; every reduction is either integer (order-free) or in
+// a fixed order, so results are deterministic.
 #include <algorithm>
 #include <cfloat>
 #include <cstring>
@@ -31,17 +30,8 @@
 
 #define ST_TPB 1024
 #define ST_WAVES (ST_TPB / 64)
-#define ST_G 8         // rows per lane with loads in flight together
 #define ST_HC 8        // LDS histogram copies
 #define ST_MAX_LDS (160 * 1024)
-
-// ST_PROF builds (scripts/dev): block 0 prints shader cycles per phase at the end of the launch
-#ifdef ST_PROF
-#define ST_MARK(k) do { if (threadIdx.x == 0) { const unsigned long long _c = clock64(); \
-    st_prof[k] += _c - st_t0; st_t0 = _c; } } while (0)
-#else
-#define ST_MARK(k) do { } while (0)
-#endif
 
 struct StudyLevels {
     DevLevel lv[VH_MAX_LEVELS];
@@ -53,8 +43,10 @@ struct StudyArgs {
     int64_t V;
     float *L0;
     float *U;
+    float *D;           // [nb][VS] B_old - B_new in raster order of the masked voxels (conv_mode 0)
     const int32_t *rs;
     const uint64_t *rmask;
+    const int32_t *rrs;
     const VolScalars *sc;
     N4State *st;
     double *P1out;
@@ -62,30 +54,32 @@ struct StudyArgs {
     const double2 *tw;
     int64_t VS;
     int32_t R, C, Z, CZ, ntiles, nslots, nitems;
-    int32_t nlev, bins;
+    int32_t nlev, bins, conv_mode;
     float thresh, fwhm, noise;
     const StudyLevels *lvs;   // device copy: per-level tables and iteration caps
     // dynamic-LDS carve (byte offsets)
-    int32_t o_E, o_tab0, o_tab1, o_lat, o_den, o_P10, o_P11, o_ipart, o_misc, o_scr, o_wave, o_order;
+    int32_t o_E, o_tab0, o_tab1, o_lat, o_den, o_P10, o_P11, o_ipart, o_rpart, o_misc, o_scr, o_wave,
+        o_order;
     int32_t s_cap;   // doubles of a wave's ring row (>= 64, >= ny * KT)
-    int32_t nb_ring; // ring rows per wave (<= ST_NB)
-    int32_t o_wx;    // row weights^P of the current level: Wx[2][R][4] doubles (p = 3, p = 2)
-    int32_t o_wk;    // dense slice weights Wk[2][ncz][Z] (p = 3, p = 2) of the current level
+    int32_t nb_ring; // ring rows per wave (<= FIT_NB)
+    int32_t o_wx;    // row weights of the current level: Wx[2][R][4] doubles (w^3/sum w^2, w^2)
+    int32_t o_wk;    // dense slice weights Wk[2][ncz][Z] (w^3, w^2) of the current level
     int32_t kcap;    // krange entries per table set
     int64_t vol0;
 };
 
 struct StudyMisc {
-    int32_t item_ctr, stop, exact, pad;
-    uint32_t umax_key, umin_key, umin2_key;   // max; min over all but the 1st / 1st and 2nd voxel
-    float u_first, u_second, u_third, bin_min, slope, bmax;
-    int32_t rx[3], rc[3];    // (row, column) of the first three masked voxels in raster order (-1: none)
+    int32_t item_ctr, stop, exact, nfirst;
+    int32_t foff[3];        // compact offsets of the first three masked voxels in raster order
+    int32_t rx[3], rc[3];   // their (row, column)
+    float bin_min, slope, bmax, pad;
     double sd, sd2, conv;
     int32_t nc[2][3];
+    ChainState ch;
 };
 
 // One level's axis tables staged in LDS.
-struct TabV {
+struct TabW {
     float4 *wx, *wy, *wz;
     double *ix, *iy, *iz;
     int32_t *bx, *by, *bz;
@@ -97,8 +91,8 @@ __host__ __device__ inline size_t study_tab_bytes(int R, int C, int Z, int kcap)
     return (((size_t)28 * (R + C + Z) + 12 * (size_t)kcap + 16) + 15) & ~(size_t)15;
 }
 
-__device__ __forceinline__ TabV tab_view(char *p, int R, int C, int Z, int kcap) {
-    TabV t;
+__device__ __forceinline__ TabW tab_w(char *p, int R, int C, int Z, int kcap) {
+    TabW t;
     t.wx = (float4 *)p; p += 16 * (size_t)R;
     t.wy = (float4 *)p; p += 16 * (size_t)C;
     t.wz = (float4 *)p; p += 16 * (size_t)Z;
@@ -112,8 +106,18 @@ __device__ __forceinline__ TabV tab_view(char *p, int R, int C, int Z, int kcap)
     t.xst = (int32_t *)(t.krz + kcap);
     return t;
 }
+__device__ __forceinline__ TabV tab_view(char *p, int R, int C, int Z, int kcap) {
+    const TabW w = tab_w(p, R, C, Z, kcap);
+    TabV t;
+    t.wx = w.wx; t.wy = w.wy; t.wz = w.wz;
+    t.ix = w.ix; t.iy = w.iy; t.iz = w.iz;
+    t.bx = w.bx; t.by = w.by; t.bz = w.bz;
+    t.krz = w.krz;
+    t.xst = w.xst;
+    return t;
+}
 
-__device__ void load_tables(const TabV &t, const DevLevel &lv, int R, int C, int Z) {
+__device__ void load_tables(const TabW &t, const DevLevel &lv, int R, int C, int Z) {
     for (int x = threadIdx.x; x < R; x += ST_TPB) {
         t.wx[x] = *reinterpret_cast<const float4 *>(lv.ax[0].w + 4 * x);
         t.ix[x] = lv.ax[0].isw2[x];
@@ -130,442 +134,63 @@ __device__ void load_tables(const TabV &t, const DevLevel &lv, int R, int C, int
         t.bz[z] = lv.ax[2].base[z];
     }
     for (int k = threadIdx.x; k < lv.ax[2].ncp; k += ST_TPB) t.krz[k] = lv.ax[2].krange[k];
-    const int ncx = lv.ax[0].ncp;
-    for (int i = threadIdx.x; i <= ncx - 3; i += ST_TPB) {   // spans of the row axis
-        int x = 0;
-        while (x < R && lv.ax[0].base[x] < i) ++x;
-        t.xst[i] = i == ncx - 3 ? R : x;
-    }
+    for (int i = threadIdx.x; i <= lv.ax[0].ncp - 3; i += ST_TPB) t.xst[i] = lv.xst[i];
 }
 
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t st_rsrc(const float *base, int64_t n) {
-    return __builtin_amdgcn_make_buffer_rsrc((void *)base, 0, (int)(n * 4), 0x00020000);
-}
-__device__ __forceinline__ float st_load(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
-    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)voff, 0, 0));
-}
-__device__ __forceinline__ void st_store(__amdgpu_buffer_rsrc_t r, uint32_t voff, float v) {
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)voff, 0, 0);
-}
-// c / slope as IEEE float division, evaluated as (double)c * (1 / (double)slope) rounded once to
-// float.  The double product is within 2^-52 (relative) of the exact quotient, and a quotient of
-// two floats is never closer than 2^-49 (relative) to a float rounding midpoint, so the rounding
-// lands on the correctly rounded quotient: bit-equal to c / slope (also checked on 4e8 random
-// pairs), including 0, inf and NaN cases, at a quarter of the instructions.
-__device__ __forceinline__ float div_r(float c, double rinv) { return (float)((double)c * rinv); }
-
-// sharpen_value / parzen_bin (n4_shared.h) with the bin division in div_r form
-__device__ __forceinline__ float sharpen_r(float u, float bmin, double rinv, const float *E, int bins) {
-    const float cidx = div_r(u - bmin, rinv);
-    const int idx = (cidx >= 0.0f && cidx < (float)bins) ? (int)floorf(cidx) : bins;
-    if (idx < bins - 1) return E[idx] + (E[idx + 1] - E[idx]) * (cidx - (float)idx);
-    return E[bins - 1];
-}
-__device__ __forceinline__ bool parzen_bin_r(float u, float bmin, double rinv, int bins, int &idx,
-                                             unsigned long long &a0, unsigned long long &a1) {
-    const float cidx = div_r(u - bmin, rinv);
-    if (!(cidx >= 0.0f) || !(cidx < (float)bins)) return false;
-    idx = (int)floorf(cidx);
-    const float o = cidx - (float)idx;
-    a1 = 0ull;
-    if (o == 0.0f) {
-        a0 = 1ull << 32;
-    } else if (idx < bins - 1) {
-        const float om = 1.0f - o;
-        a0 = om == 1.0f ? (1ull << 32) : (unsigned long long)(uint32_t)((double)om * 4294967296.0);
-        a1 = (unsigned long long)(uint32_t)((double)o * 4294967296.0);
-    } else {
-        return false;
-    }
-    return true;
+__device__ __forceinline__ bool study_item(Item &it, const StudyArgs &a, int64_t b, int item) {
+    const int64_t tb = b * (int64_t)a.ntiles * a.R;
+    return item_begin(it, a.rmask + tb, a.rs + tb, a.rrs + tb, a.R, a.C, a.Z, a.CZ, a.nslots, item);
 }
 
-// parzen_bin_r without branches: idx in [0, bins - 1], zero weights where parzen_bin adds nothing
-__device__ __forceinline__ void parzen_bin_bf(float u, float bmin, double rinv, int bins, int &idx,
-                                              unsigned long long &a0, unsigned long long &a1) {
-    const float cidx = div_r(u - bmin, rinv);
-    const bool in = cidx >= 0.0f && cidx < (float)bins;   // false for NaN
-    const float cf = in ? floorf(cidx) : 0.0f;
-    const float o = in ? cidx - cf : 0.0f;
-    const bool zero = o == 0.0f, inner = (int)cf < bins - 1;
-    const float om = 1.0f - o;
-    // x * 2^32 is exact in float (power-of-two scale, < 2^32): the f32 -> u32 truncation equals
-    // the double-path truncation of n4_shared.h parzen_bin
-    const unsigned long long w0 =
-        (zero || om == 1.0f) ? (1ull << 32) : (unsigned long long)(uint32_t)(om * 4294967296.0f);
-    a0 = in && (zero || inner) ? w0 : 0ull;
-    a1 = in && !zero && inner ? (unsigned long long)(uint32_t)(o * 4294967296.0f) : 0ull;
-    idx = (int)cf;
+__device__ __forceinline__ void rpart_store(float4 *rpart, int item, const Range3 &r) {
+    if ((threadIdx.x & 63) == 0) rpart[item] = make_float4(r.mx, r.m1, r.m2, r.m3);
 }
 
-__device__ __forceinline__ float wsel(float4 w, int d) {
-    return d == 0 ? w.x : d == 1 ? w.y : d == 2 ? w.z : w.w;
-}
-template <int P>
-__device__ __forceinline__ double wpow(float w) {
-    const double d = (double)w;
-    return P == 3 ? d * d * d : d * d;
-}
-
-// ---------------------------------------------------------------------------------------------
-// work item = (64-column tile, 64-row slot): the wave's view of its rows
-// ---------------------------------------------------------------------------------------------
-struct Item {
-    int tile, x0, xs, xe;     // wave-uniform: tile, slot's first row, first / last non-empty row
-    uint64_t mreg;            // lane l: mask == 1 lanes of row x0 + l
-    int rsreg;                // lane l: compact offset of row x0 + l
-    int col, y, z;            // this lane's column
-    bool colok;
-    // tile geometry (uniform)
-    int c0, y0, y1, z0, z1, ny;
-};
-
-__device__ __forceinline__ bool item_begin(Item &it, const StudyArgs &a, int64_t b, int item) {
-    const int lane = threadIdx.x & 63;
-    it.tile = item / a.nslots;
-    it.x0 = (item % a.nslots) * 64;
-    const int64_t rbase = ((int64_t)b * a.ntiles + it.tile) * a.R;
-    const int xr = it.x0 + lane;
-    it.mreg = xr < a.R ? a.rmask[rbase + xr] : 0ull;
-    it.rsreg = xr < a.R ? a.rs[rbase + xr] : 0;
-    const uint64_t nzb = __ballot(it.mreg != 0ull);
-    if (nzb == 0ull) return false;
-    it.xs = it.x0 + __builtin_ctzll(nzb);
-    it.xe = it.x0 + 63 - __builtin_clzll(nzb);
-    it.col = it.tile * TILE_W + lane;
-    it.colok = it.col < a.CZ;
-    it.y = it.colok ? it.col / a.Z : 0;
-    it.z = it.colok ? it.col % a.Z : 0;
-    it.c0 = it.tile * TILE_W;
-    const int c1 = min(it.c0 + TILE_W, a.CZ) - 1;
-    it.y0 = it.c0 / a.Z;
-    it.y1 = c1 / a.Z;
-    it.z0 = it.c0 % a.Z;
-    it.z1 = c1 % a.Z;
-    it.ny = it.y1 - it.y0 + 1;
-    return true;
-}
-
-// Compact byte offset of (row x, this lane) or VH_OOB when the voxel is not in the mask; x is
-// wave-uniform and inside the item's slot.
-__device__ __forceinline__ uint32_t item_off(const Item &it, int x, bool valid) {
-    const int lane = threadIdx.x & 63;
-    const int xl = x - it.x0;
-    const uint32_t mlo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)it.mreg, xl);
-    const uint32_t mhi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(it.mreg >> 32), xl);
-    const uint64_t m = ((uint64_t)mhi << 32) | mlo;
-    const int r0 = __builtin_amdgcn_readlane(it.rsreg, xl);
-    const bool on = valid && ((m >> lane) & 1ull);
-    return on ? (uint32_t)(r0 + lanes_below(m)) * 4u : VH_OOB;
-}
-
-// Exact, order-free accumulation of doubles with a huge dynamic range: 128-bit two's-complement
-// fixed point in units of 2^-80 (|v| < 2^37), kept as (lo u64, hi i64) and added with integer LDS
-// atomics, the low word's carry detected from the value the atomic returns.  A 64-bit 2^-32 grid
-// is too coarse here: the tile slabs are already contracted over cols and slices, and edge control
-// points collect products of three cubed weights (den ~ 1e-12 and below).
-__device__ __forceinline__ void fix128_add(unsigned long long *lo, unsigned long long *hi, double v) {
-    const double s = fabs(v) * 65536.0;            // |v| * 2^16, exact
-    const double fh = floor(s);
-    unsigned long long h = (unsigned long long)fh; // s < 2^53
-    const double r = s - fh;                       // fractional bits of s: [0, 1), exact
-    unsigned long long l = (unsigned long long)(r * 18446744073709551616.0);   // < 2^64
-    if (v < 0.0) {                                 // two's-complement negation of (h, l)
-        l = ~l + 1ull;
-        h = ~h + (l == 0ull ? 1ull : 0ull);
-    }
-    const unsigned long long old = atomicAdd(lo, l);
-    const unsigned long long carry = old + l < old ? 1ull : 0ull;
-    atomicAdd(hi, h + carry);
-}
-__device__ __forceinline__ double fix128_get(const unsigned long long *lo, const unsigned long long *hi) {
-    return (double)(long long)*hi * (1.0 / 65536.0) + (double)*lo * 8.271806125530277e-25;   // 2^-80
-}
-
-// ---------------------------------------------------------------------------------------------
-// fit: contraction of finished control rows of the item's tile (wave-collective).  A wave keeps
-// up to ST_NB finished rows Q[r][lane] (control rows i0 .. i0+nr-1) in its LDS ring and contracts
-// them together, so the dependent LDS chains of the contraction are paid once per batch:
-//   S[r][y][k]    = sum_{z of row y in the tile} Wk[k][z] Q[r][(y, z)]     (Wk = wz(z, k)^P, dense)
-//   num[i0+r][j][k] += sum_y wy(y, j)^P S[r][y][k]                        (128-bit fixed point)
-// S overwrites Q in place (all reads of a batch finish before its writes).
-// ---------------------------------------------------------------------------------------------
-#define ST_NB 4        // finished control rows per contraction batch
-#define ST_SO 4        // stage-1 outputs per lane per batch (nr * ny * KT <= 64 * ST_SO)
-
-struct FitRing {
-    double *q;        // [ST_NB][rowcap] this wave's rows
-    int rowcap;       // doubles per row (>= 64, >= ny * KT)
-    int nbmax;        // rows per batch for this geometry
-    int nr, i0;       // rows held, control row of row 0
-};
-
-template <int P>
-__device__ void fit_contract(FitRing &rg, const Item &it, const TabV &T, const double *Wk, int ncy,
-                             int ncz, int Z, unsigned long long *numfix) {
-    const int nr = rg.nr;
-    if (nr == 0) return;
-    const int lane = threadIdx.x & 63;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const int klo = T.bz[it.y0 == it.y1 ? it.z0 : 0];
-    const int KT = T.bz[it.y0 == it.y1 ? it.z1 : Z - 1] + 4 - klo;
-    const int nyk = it.ny * KT;
-    // the ST_SO outputs of a lane are independent fma chains over their slices: walk them in
-    // lockstep (step s of every chain together) so the LDS latency of one chain hides behind the
-    // others; each chain still adds its terms in slice order, so the sums are unchanged
-    double outv[ST_SO];
-    const double *qp[ST_SO], *wp[ST_SO];
-    int len[ST_SO];
-    int maxlen = 0;
-#pragma unroll
-    for (int q = 0; q < ST_SO; ++q) {
-        outv[q] = 0.0;
-        len[q] = 0;
-        qp[q] = rg.q;
-        wp[q] = Wk;
-        const int o = lane + 64 * q;
-        if (o >= nr * nyk) continue;
-        const int r = o / nyk, yk = o % nyk;
-        const int yy = yk / KT, k = klo + yk % KT, yv = it.y0 + yy;
-        const int zlo = yv == it.y0 ? it.z0 : 0, zhi = yv == it.y1 ? it.z1 : Z - 1;
-        const int2 kr = T.krz[k];
-        const int zs = max(zlo, kr.x), ze = min(zhi, kr.y);
-        qp[q] = rg.q + r * rg.rowcap + (yv * Z - it.c0) + zs;
-        wp[q] = Wk + k * Z + zs;
-        len[q] = max(ze - zs + 1, 0);
-        maxlen = max(maxlen, len[q]);
-    }
-#pragma unroll 1
-    for (int s = 0; s < maxlen; ++s) {
-#pragma unroll
-        for (int q = 0; q < ST_SO; ++q) {
-            const int ss = min(s, max(len[q] - 1, 0));   // in-range read for finished chains
-            const double v = fma(wp[q][ss], qp[q][ss], outv[q]);
-            outv[q] = s < len[q] ? v : outv[q];
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-    for (int q = 0; q < ST_SO; ++q) {
-        const int o = lane + 64 * q;
-        if (o < nr * nyk) rg.q[(o / nyk) * rg.rowcap + o % nyk] = outv[q];
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const int jlo = T.by[it.y0];
-    const int JT = T.by[it.y1] + 4 - jlo;
-    const int njk = JT * KT;
-    for (int o = lane; o < nr * njk; o += 64) {
-        const int r = o / njk, jk = o % njk;
-        const int j = jlo + jk / KT, kk = jk % KT, k = klo + kk;
-        const double *sr = rg.q + r * rg.rowcap;
-        double acc = 0.0;
-        for (int yy = 0; yy < it.ny; ++yy) {
-            const int d = j - T.by[it.y0 + yy];
-            if (d < 0 || d > 3) continue;
-            acc = fma(wpow<P>(wsel(T.wy[it.y0 + yy], d)), sr[yy * KT + kk], acc);
-        }
-        if (acc != 0.0) {
-            const int64_t e = ((int64_t)(rg.i0 + r) * ncy + j) * ncz + k;
-            fix128_add(numfix + 2 * e, numfix + 2 * e + 1, acc);
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    rg.nr = 0;
-}
-
-// control row i (this lane's value v) is finished: into the ring, contract when the batch is full
-template <int P>
-__device__ __forceinline__ void fit_push(FitRing &rg, double v, int i, const Item &it,
-                                         const TabV &T, const double *Wk, int ncy, int ncz, int Z,
-                                         unsigned long long *numfix) {
-    if (rg.nr == 0) rg.i0 = i;
-    rg.q[rg.nr * rg.rowcap + (threadIdx.x & 63)] = v;
-    if (++rg.nr == rg.nbmax) fit_contract<P>(rg, it, T, Wk, ncy, ncz, Z, numfix);
-}
-
-// MODE 0: numerator (w^3, q = (u - sharpen(u)) / (sum wx^2 sum wy^2 sum wz^2));
-// MODE 1: denominator (w^2, q = 1).
-template <int MODE>
-__device__ void fit_item(const StudyArgs &a, const Item &it, const TabV &T, const double *Wk,
-                         const double2 *Wx, int ncy, int ncz, const float *Ub, int64_t n,
-                         const float *sE, float bmin, double rinv, FitRing &rg,
-                         unsigned long long *numfix) {
-    constexpr int P = MODE == 0 ? 3 : 2;
-    const __amdgpu_buffer_rsrc_t rU = st_rsrc(Ub, n);
-    const double isyz = MODE == 0 ? T.iy[it.y] * T.iz[it.z] : 1.0;
-    int wb = T.bx[it.xs];
-    double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0, acc3 = 0.0;
-    int x = it.xs, tail = 0;
-    {   // rows per batch: the stage-1 outputs of a batch must fit the lanes' ST_SO slots
-        const int klo = T.bz[it.y0 == it.y1 ? it.z0 : 0];
-        const int KT = T.bz[it.y0 == it.y1 ? it.z1 : a.Z - 1] + 4 - klo;
-        rg.nbmax = max(1, min(a.nb_ring, 64 * ST_SO / (it.ny * KT)));
-        rg.nr = 0;
-    }
-#pragma unroll 1
-    for (;;) {
-        if (x <= it.xe) {   // rows of control span wb: the window does not move
-            const int rb = min(it.xe, T.xst[wb + 1] - 1);
-#pragma unroll 1
-            for (int xb = x; xb <= rb; xb += ST_G) {
-                uint32_t offs[ST_G];
-                float u[ST_G];
-#pragma unroll
-                for (int g = 0; g < ST_G; ++g) {
-                    const int xg = xb + g;
-                    offs[g] = item_off(it, xg <= rb ? xg : rb, xg <= rb);
-                    if (MODE == 0) u[g] = st_load(rU, offs[g]);
-                }
-#pragma unroll
-                for (int g = 0; g < ST_G; ++g) {
-                    if (offs[g] == VH_OOB) continue;
-                    const int xg = xb + g;
-                    const double2 wa = Wx[2 * xg], wc = Wx[2 * xg + 1];   // wx(x, 0..3)^P
-                    if (MODE == 0) {
-                        const float rv = u[g] - sharpen_r(u[g], bmin, rinv, sE, a.bins);
-                        const double q = ((double)rv * T.ix[xg]) * isyz;
-                        acc0 += wa.x * q;
-                        acc1 += wa.y * q;
-                        acc2 += wc.x * q;
-                        acc3 += wc.y * q;
-                    } else {
-                        acc0 += wa.x;
-                        acc1 += wa.y;
-                        acc2 += wc.x;
-                        acc3 += wc.y;
-                    }
-                }
-            }
-            x = rb + 1 > x ? rb + 1 : x;
-        }
-        fit_push<P>(rg, acc0, wb, it, T, Wk, ncy, ncz, a.Z, numfix);   // control row wb is done
-        acc0 = acc1; acc1 = acc2; acc2 = acc3; acc3 = 0.0;
-        ++wb;
-        if (x > it.xe && ++tail == 4) break;
-    }
-    fit_contract<P>(rg, it, T, Wk, ncy, ncz, a.Z, numfix);
-}
-
-// ---------------------------------------------------------------------------------------------
-// U range for the next histogram.  ITK scans in raster order with
-//   if (u > max) max = u; else if (u < min) min = u;
-// so the minimum skips every "record" voxel (strictly above all earlier ones).  The records that
-// can matter form the strictly increasing run u1 < u2 < ... < uK at the start of the raster order
-// (a later record is above a non-record voxel), so min = min over voxels after that run.  The
-// sweeps track min over all voxels but the 1st (K = 1) and but the 1st and 2nd (K = 2) together
-// with u1, u2, u3; a run of 3 or more falls back to the exact raster scan.
-// ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ bool item_has(const Item &it, int x, int col) {
-    return x >= it.xs && x <= it.xe && col >= it.c0 && col < it.c0 + TILE_W;
-}
-__device__ __forceinline__ void range_special(StudyMisc &M, int x, int col, float u, float &umin,
-                                              float &umin2) {
-    if (x == M.rx[0] && col == M.rc[0]) {
-        M.u_first = u;
-        return;
-    }
-    umin = fminf(umin, u);
-    if (x == M.rx[1] && col == M.rc[1]) {
-        M.u_second = u;
-        return;
-    }
-    umin2 = fminf(umin2, u);
-    if (x == M.rx[2] && col == M.rc[2]) M.u_third = u;
-}
-__device__ __forceinline__ void range_commit(StudyMisc &M, float umax, float umin, float umin2) {
-    uint32_t kmax = umax == -FLT_MAX ? 0u : f2key(umax);
-    uint32_t kmin = umin == FLT_MAX ? 0xffffffffu : f2key(umin);
-    uint32_t kmin2 = umin2 == FLT_MAX ? 0xffffffffu : f2key(umin2);
-    kmax = wave_max_u32(kmax);
-    kmin = wave_min_u32(kmin);
-    kmin2 = wave_min_u32(kmin2);
-    if ((threadIdx.x & 63) == 0) {
-        if (kmax) atomicMax(&M.umax_key, kmax);
-        if (kmin != 0xffffffffu) atomicMin(&M.umin_key, kmin);
-        if (kmin2 != 0xffffffffu) atomicMin(&M.umin2_key, kmin2);
-    }
-}
-
-// Init + range of the initial field over one item: L0 = log(I) at mask == 1 (k_n4_init's
-// expression; non-positive -> 0), U = L0 (B = 0), same range bookkeeping as the eval.  Replaces the
-// separate k_n4_init sweep in this driver (the volume-resident kernel reads I directly).
-__device__ void init_item(const StudyArgs &a, int64_t b, const Item &it, float *Lb, float *Ub,
-                          int64_t n, StudyMisc &M) {
+// Init + range of the initial field over one item: L0 = (float)log((double)I) at mask == 1 (S1;
+// non-positive -> 0), U = L0 (B = 0).
+__device__ void init_item(const StudyArgs &a, int64_t b, const Item &it, int item, float *Lb,
+                          float *Ub, int64_t n, float4 *rpart) {
     const __amdgpu_buffer_rsrc_t rL = st_rsrc(Lb, n), rU = st_rsrc(Ub, n);
     const float *Ib = a.I + b * a.V + it.col;
-    float umax = -FLT_MAX, umin = FLT_MAX, umin2 = FLT_MAX;
-    const bool has_rv = item_has(it, M.rx[0], M.rc[0]) || item_has(it, M.rx[1], M.rc[1]) ||
-                        item_has(it, M.rx[2], M.rc[2]);
+    Range3 rg;
+    r3_init(rg);
 #pragma unroll 1
-    for (int xb = it.xs; xb <= it.xe; xb += ST_G) {
-        uint32_t offs[ST_G];
-        float iv[ST_G];
+    for (int xb = it.xs; xb <= it.xe; xb += FIT_G) {
+        uint32_t offs[FIT_G];
+        float iv[FIT_G];
 #pragma unroll
-        for (int g = 0; g < ST_G; ++g) {   // the group's image loads together
+        for (int g = 0; g < FIT_G; ++g) {   // the group's image loads together
             const int xg = xb + g;
             offs[g] = item_off(it, xg <= it.xe ? xg : it.xe, xg <= it.xe);
             iv[g] = offs[g] != VH_OOB ? Ib[(int64_t)xg * a.CZ] : 0.0f;
         }
 #pragma unroll
-        for (int g = 0; g < ST_G; ++g) {
+        for (int g = 0; g < FIT_G; ++g) {
             if (offs[g] == VH_OOB) continue;
             const float l = iv[g] > 0.0f ? (float)log((double)iv[g]) : 0.0f;
             st_store(rL, offs[g], l);
             st_store(rU, offs[g], l);
-            umax = fmaxf(umax, l);
-            if (has_rv) {
-                range_special(M, xb + g, it.col, l, umin, umin2);
-            } else {
-                umin = fminf(umin, l);
-                umin2 = fminf(umin2, l);
-            }
+            r3_add(rg, l);
         }
     }
-    range_commit(M, umax, umin, umin2);
+    rpart_store(rpart, item, r3_wave(rg));
 }
 
-// U range of the initial field (U = L0) over one item, same bookkeeping as the eval
-__device__ void range_item(const Item &it, const float *Ub, int64_t n, StudyMisc &M) {
-    const __amdgpu_buffer_rsrc_t rU = st_rsrc(Ub, n);
-    float umax = -FLT_MAX, umin = FLT_MAX, umin2 = FLT_MAX;
-    const bool has_rv = item_has(it, M.rx[0], M.rc[0]) || item_has(it, M.rx[1], M.rc[1]) ||
-                        item_has(it, M.rx[2], M.rc[2]);
-#pragma unroll 1
-    for (int x = it.xs; x <= it.xe; ++x) {
-        const uint32_t off = item_off(it, x, true);
-        if (off == VH_OOB) continue;
-        const float u = st_load(rU, off);
-        umax = fmaxf(umax, u);
-        if (has_rv) {
-            range_special(M, x, it.col, u, umin, umin2);
-        } else {
-            umin = fminf(umin, u);
-            umin2 = fminf(umin2, u);
-        }
-    }
-    range_commit(M, umax, umin, umin2);
-}
-
-// wave 0: the first three masked voxels in raster order (row, then column)
+// wave 0: the first three masked voxels in raster order (row, then column) and their compact offsets
 __device__ void find_first3(const StudyArgs &a, int64_t b, int64_t first, StudyMisc &M) {
     const int lane = threadIdx.x & 63;
     int found = 0;
-    if (lane == 0)
-        for (int q = 0; q < 3; ++q) M.rx[q] = M.rc[q] = -1;
+    if (lane == 0) {
+        for (int q = 0; q < 3; ++q) M.rx[q] = M.rc[q] = M.foff[q] = -1;
+        M.nfirst = 0;
+    }
     if (first < 0) return;
+    const int64_t tb = b * (int64_t)a.ntiles * a.R;
     const int fx = (int)(first / a.CZ), fcol = (int)(first % a.CZ);
     for (int x = fx; x < a.R && found < 3; ++x)
         for (int t0 = x == fx ? fcol / TILE_W : 0; t0 < a.ntiles && found < 3; t0 += 64) {
             const int t = t0 + lane;
-            uint64_t m = t < a.ntiles ? a.rmask[((int64_t)b * a.ntiles + t) * a.R + x] : 0ull;
+            uint64_t m = t < a.ntiles ? a.rmask[tb + (int64_t)t * a.R + x] : 0ull;
             if (x == fx && t < fcol / TILE_W) m = 0ull;
             if (x == fx && t == fcol / TILE_W) m &= ~((2ull << (fcol % TILE_W)) - 1ull) | (1ull << (fcol % TILE_W));
             uint64_t nz = __ballot(m != 0ull);
@@ -579,8 +204,13 @@ __device__ void find_first3(const StudyArgs &a, int64_t b, int64_t first, StudyM
                     const int bit = __builtin_ctzll(mm);
                     mm &= mm - 1;
                     if (lane == 0) {
+                        const int tt = t0 + l;
+                        const int64_t e = tb + (int64_t)tt * a.R + x;
+                        const uint64_t full = a.rmask[e];
                         M.rx[found] = x;
-                        M.rc[found] = (t0 + l) * TILE_W + bit;
+                        M.rc[found] = tt * TILE_W + bit;
+                        M.foff[found] = a.rs[e] + __popcll(full & ((1ull << bit) - 1ull));
+                        M.nfirst = found + 1;
                     }
                     ++found;
                 }
@@ -588,16 +218,8 @@ __device__ void find_first3(const StudyArgs &a, int64_t b, int64_t first, StudyM
         }
 }
 
-// expm1f for the convergence terms: the argument (B_old - B_new) is small after the first
-// iteration of a level, where a degree-5 Taylor polynomial is within float rounding of expm1f
-__device__ __forceinline__ float expm1_small(float x) {
-    if (fabsf(x) < 0.0625f)
-        return x + x * x * (0.5f + x * (0.16666667f + x * (0.041666668f + x * 0.008333334f)));
-    return expm1f(x);
-}
-
 // T(i) of this lane's column: the lattice contracted over slices (P1) then cols, rounded to float
-// (identical expression to n4.hip col_T + k_n4_T)
+// (S6; identical expression to n4.hip col_T / k_n4_T)
 __device__ __forceinline__ float col_T_lds(const double *P1, int i, int ncy, int Z, int by,
                                            float4 wy, int z) {
     const double *r = P1 + ((int64_t)i * ncy + by) * Z + z;
@@ -605,16 +227,16 @@ __device__ __forceinline__ float col_T_lds(const double *P1, int i, int ncy, int
                    (double)wy.w * r[3 * Z]);
 }
 
-// eval: B_new, U = L0 - B_new, convergence sums of exp(B_old - B_new) - 1, U range.  SAME: the
-// previous field uses this level's tables (every iteration but the first of levels > 0), so both
-// T windows move together at the row-span boundaries; otherwise rows are taken one at a time.
-template <bool SAME>
-__device__ void eval_item(const StudyArgs &a, const Item &it, int item, const TabV &Tn,
-                          const TabV &To, int ncyn, int ncyo, const double *P1n, const double *P1o,
-                          bool bo_mode, const float *Lb, float *Ub, int64_t n, int64_t first,
-                          double *ipart, StudyMisc &M) {
-    const __amdgpu_buffer_rsrc_t rL = st_rsrc(Lb, n), rU = st_rsrc(Ub, n);
-    const int Z = a.Z;
+// eval: B_new, U = L0 - B_new, the field difference d = B_old - B_new (conv_mode 0: stored at the
+// voxel's raster rank; conv_mode 1: exact-CoV sums), U range.  SAME: the previous field uses this
+// level's tables (every iteration but the first of levels > 0), so both T windows move together at
+// the row-span boundaries; otherwise rows are taken one at a time.
+template <bool SAME, int CM>
+__device__ void eval_item(const Item &it, int item, int Z, const TabV &Tn, const TabV &To, int ncyn,
+                          int ncyo, const double *P1n, const double *P1o, bool bo_mode,
+                          const float *Lb, float *Ub, float *Db, int64_t n, double *ipart,
+                          float4 *rpart) {
+    const __amdgpu_buffer_rsrc_t rL = st_rsrc(Lb, n), rU = st_rsrc(Ub, n), rD = st_rsrc(Db, n);
     const float4 wyn = it.colok ? Tn.wy[it.y] : make_float4(0.f, 0.f, 0.f, 0.f);
     const float4 wyo = it.colok ? To.wy[it.y] : make_float4(0.f, 0.f, 0.f, 0.f);
     const int byn = Tn.by[it.y], byo = To.by[it.y];
@@ -631,11 +253,9 @@ __device__ void eval_item(const StudyArgs &a, const Item &it, int item, const Ta
         to3 = col_T_lds(P1o, wbo + 3, ncyo, Z, byo, wyo, it.z);
     }
     double sd = 0.0, sd2 = 0.0;
-    float umax = -FLT_MAX, umin = FLT_MAX, umin2 = FLT_MAX;
-    // the study's first three masked voxels (ITK's bin-range rule) only matter in their items
-    const bool has_rv = item_has(it, M.rx[0], M.rc[0]) || item_has(it, M.rx[1], M.rc[1]) ||
-                        item_has(it, M.rx[2], M.rc[2]);
-    auto voxel = [&](uint32_t off, float la, int x) {
+    Range3 rg;
+    r3_init(rg);
+    auto voxel = [&](uint32_t off, int rr, float la, int x) {
         const float4 w = Tn.wx[x];
         const float bn = ((w.x * tn0 + w.y * tn1) + w.z * tn2) + w.w * tn3;
         float bo = 0.0f;
@@ -645,16 +265,14 @@ __device__ void eval_item(const StudyArgs &a, const Item &it, int item, const Ta
         }
         const float u = la - bn;
         st_store(rU, off, u);
-        const double d = (double)expm1_small(bo - bn);   // p - 1, p = exp(B_old - B_new)
-        sd += d;
-        sd2 = fma(d, d, sd2);
-        umax = fmaxf(umax, u);
-        if (has_rv) {
-            range_special(M, x, it.col, u, umin, umin2);
+        if (CM == 0) {
+            st_store(rD, (uint32_t)rr * 4u, bo - bn);
         } else {
-            umin = fminf(umin, u);
-            umin2 = fminf(umin2, u);
+            const double d = (double)expm1c(bo - bn);
+            sd += d;
+            sd2 = fma(d, d, sd2);
         }
+        r3_add(rg, u);
     };
     if (SAME) {
         int x = it.xs;
@@ -662,18 +280,19 @@ __device__ void eval_item(const StudyArgs &a, const Item &it, int item, const Ta
         for (;;) {
             const int rb = min(it.xe, Tn.xst[wbn + 1] - 1);
 #pragma unroll 1
-            for (int xb = x; xb <= rb; xb += ST_G) {
-                uint32_t offs[ST_G];
-                float la[ST_G];
+            for (int xb = x; xb <= rb; xb += FIT_G) {
+                uint32_t offs[FIT_G];
+                int rrs[FIT_G];
+                float la[FIT_G];
 #pragma unroll
-                for (int g = 0; g < ST_G; ++g) {
+                for (int g = 0; g < FIT_G; ++g) {
                     const int xg = xb + g;
-                    offs[g] = item_off(it, xg <= rb ? xg : rb, xg <= rb);
+                    offs[g] = item_off(it, xg <= rb ? xg : rb, xg <= rb, CM == 0 ? &rrs[g] : nullptr);
                     la[g] = st_load(rL, offs[g]);
                 }
 #pragma unroll
-                for (int g = 0; g < ST_G; ++g)
-                    if (offs[g] != VH_OOB) voxel(offs[g], la[g], xb + g);
+                for (int g = 0; g < FIT_G; ++g)
+                    if (offs[g] != VH_OOB) voxel(offs[g], CM == 0 ? rrs[g] : 0, la[g], xb + g);
             }
             x = rb + 1 > x ? rb + 1 : x;
             if (x > it.xe) break;
@@ -701,26 +320,28 @@ __device__ void eval_item(const StudyArgs &a, const Item &it, int item, const Ta
                 to0 = to1; to1 = to2; to2 = to3;
                 to3 = col_T_lds(P1o, wbo + 3, ncyo, Z, byo, wyo, it.z);
             }
-            const uint32_t off = item_off(it, x, true);
-            if (off != VH_OOB) voxel(off, st_load(rL, off), x);
+            int rr = 0;
+            const uint32_t off = item_off(it, x, true, CM == 0 ? &rr : nullptr);
+            if (off != VH_OOB) voxel(off, rr, st_load(rL, off), x);
         }
     }
-    for (int off = 32; off > 0; off >>= 1) {
-        sd += __shfl_down(sd, off, 64);
-        sd2 += __shfl_down(sd2, off, 64);
+    if (CM != 0) {
+        for (int off = 32; off > 0; off >>= 1) {
+            sd += __shfl_down(sd, off, 64);
+            sd2 += __shfl_down(sd2, off, 64);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            ipart[2 * item] = sd;
+            ipart[2 * item + 1] = sd2;
+        }
     }
-    range_commit(M, umax, umin, umin2);
-    if ((threadIdx.x & 63) == 0) {
-        ipart[2 * item] = sd;
-        ipart[2 * item + 1] = sd2;
-    }
+    rpart_store(rpart, item, r3_wave(rg));
 }
 
 // ---------------------------------------------------------------------------------------------
 // FFT (512-point radix-2 DIT, same butterflies and twiddle indexing as oracle/n4_oracle.c) by ONE
 // wave in place in LDS.  The points sit at padded slots fpad(i) (one spare slot per 8), so the
-// strided passes below hit distinct LDS banks.  Only wave-local ordering is needed (a wave's LDS
-// operations complete in issue order; the fences keep the compiler from moving them).
+// strided passes below hit distinct LDS banks.  Only wave-local ordering is needed.
 // ---------------------------------------------------------------------------------------------
 #define ST_FFT_N (VH_FFT_P + VH_FFT_P / 8)   // padded slots of one transform
 __device__ __forceinline__ int fpad(int i) { return i + (i >> 3); }
@@ -729,17 +350,9 @@ struct FftId {
     __device__ double2 operator()(int, double2 v) const { return v; }
 };
 
-__device__ __forceinline__ void wave_lds_order() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 // The 9 stages run as 3 register passes of 3: in pass p a lane owns the 8 points
 // base + m * 8^p (m < 8), which the stages of half-length 8^p, 2 * 8^p, 4 * 8^p pair only among
-// themselves.  Pass 0 gathers in bit-reversed order (all loads of the wave issue before its
-// stores) through pro(i, v); pass 2 stores epi(i, v) -- the elementwise steps around a transform
-// ride on its first and last pass.
+// themselves.  Pass 0 gathers in bit-reversed order through pro(i, v); pass 2 stores epi(i, v).
 template <class Pro, class Epi>
 __device__ __forceinline__ void wave_fft_lds(double2 *x, const double2 *tw, bool inverse, const Pro &pro,
                              const Epi &epi) {
@@ -765,7 +378,7 @@ __device__ __forceinline__ void wave_fft_lds(double2 *x, const double2 *tw, bool
 #pragma unroll
             for (int m = 0; m < 8; ++m) {
                 if (m & (1 << s)) continue;
-                const int j = stride * (m & ((1 << s) - 1)) + lane % stride;   // (base + m stride) % half
+                const int j = stride * (m & ((1 << s) - 1)) + lane % stride;
                 const double2 w = tw[j * step];
                 const double wy = inverse ? -w.y : w.y;
                 const double2 a = v[m], bb = v[m + (1 << s)];
@@ -851,6 +464,14 @@ __device__ void refine_axis_st(const float *in, float *out, int d0, int d1, int 
     }
 }
 
+// take the next item of the current pass (largest first)
+__device__ __forceinline__ int next_item(StudyMisc &M, const int32_t *ordr, int nitems) {
+    int item = 0;
+    if ((threadIdx.x & 63) == 0) item = atomicAdd(&M.item_ctr, 1);
+    item = __shfl(item, 0, 64);
+    return item >= nitems ? -1 : ordr[item];
+}
+
 // ---------------------------------------------------------------------------------------------
 // the kernel: one workgroup per study
 // ---------------------------------------------------------------------------------------------
@@ -865,6 +486,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
     double *const P1b0 = reinterpret_cast<double *>(smem + a.o_P10);
     double *const P1b1 = reinterpret_cast<double *>(smem + a.o_P11);
     double *ipart = reinterpret_cast<double *>(smem + a.o_ipart);
+    float4 *rpart = reinterpret_cast<float4 *>(smem + a.o_rpart);
     int32_t *ordr = reinterpret_cast<int32_t *>(smem + a.o_order);
     char *scr = smem + a.o_scr;
 
@@ -882,11 +504,13 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
     }
     float *Lb = a.L0 + b * a.VS;
     float *Ub = a.U + b * a.VS;
+    float *Db = a.D + b * a.VS;
     const int64_t fm = a.sc[b].first_masked;
     // fit / eval scratch: lattice numerator (fixed point), then per-wave Q / S rows
     unsigned long long *numfix = reinterpret_cast<unsigned long long *>(scr);
     FitRing ring;
     ring.q = reinterpret_cast<double *>(scr + a.o_wave) + (size_t)wv * a.nb_ring * a.s_cap;
+    ring.sx = nullptr;
     ring.rowcap = a.s_cap;
     ring.nr = 0;
     double *const Wk3 = reinterpret_cast<double *>(smem + a.o_wk);
@@ -894,21 +518,17 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
     double2 *V = reinterpret_cast<double2 *>(scr), *F = V + ST_FFT_N, *DEN = F + ST_FFT_N;
     double2 *TW = DEN + ST_FFT_N;
     unsigned long long *Hc = reinterpret_cast<unsigned long long *>(TW + VH_FFT_P / 2);
+    ChainSlot *slots = reinterpret_cast<ChainSlot *>(scr);
     const int bins = a.bins;
 
-    if (t == 0) {
-        M.umax_key = 0u;
-        M.umin_key = M.umin2_key = 0xffffffffu;
-        M.u_first = M.u_second = M.u_third = 0.0f;
-        M.item_ctr = 0;
-    }
+    if (t == 0) M.item_ctr = 0;
     if (wv == 0) find_first3(a, b, fm, M);
     {   // item schedule: items by row count, largest first (ties by index), so the dynamic item
         // queue of every pass ends on small items; the item order of every reduction is unchanged
         int32_t *isz = reinterpret_cast<int32_t *>(scr);
         for (int item = wv; item < a.nitems; item += ST_WAVES) {
             Item it;
-            const bool any = item_begin(it, a, b, item);
+            const bool any = study_item(it, a, b, item);
             if (lane == 0) isz[item] = any ? it.xe - it.xs + 1 : 0;
         }
         __syncthreads();
@@ -923,15 +543,15 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
         }
     }
     __syncthreads();
-    for (;;) {   // range of the initial field U = L0
-        int item = 0;
-        if (lane == 0) item = atomicAdd(&M.item_ctr, 1);
-        item = __shfl(item, 0, 64);
-        if (item >= a.nitems) break;
-        item = ordr[item];   // largest items first
+    for (;;) {   // L0, U = L0 and its range
+        const int item = next_item(M, ordr, a.nitems);
+        if (item < 0) break;
         Item it;
-        if (!item_begin(it, a, b, item)) continue;
-        init_item(a, b, it, Lb, Ub, n, M);
+        if (!study_item(it, a, b, item)) {
+            if (lane == 0) rpart[item] = make_float4(-FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX);
+            continue;
+        }
+        init_item(a, b, it, item, Lb, Ub, n, rpart);
     }
     {
         const DevLevel &l0 = a.lvs->lv[0];
@@ -939,16 +559,13 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
         for (int e = t; e < nl0; e += ST_TPB) lat[e] = 0.0f;
     }
     int cur = 0;   // P1b[cur] holds the last evaluated field
-#ifdef ST_PROF
-    unsigned long long st_prof[13] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_t0 = clock64();
-    const unsigned long long st_w0 = wall_clock64(), st_c0 = clock64();
-#endif
     for (int L = 0; L < a.nlev; ++L) {
         const DevLevel &lv = a.lvs->lv[L];
-        const TabV T = tab_view(smem + ((L & 1) ? a.o_tab1 : a.o_tab0), a.R, a.C, a.Z, a.kcap);
+        char *tabp = smem + ((L & 1) ? a.o_tab1 : a.o_tab0);
+        load_tables(tab_w(tabp, a.R, a.C, a.Z, a.kcap), lv, a.R, a.C, a.Z);
+        const TabV T = tab_view(tabp, a.R, a.C, a.Z, a.kcap);
         const int ncx = lv.ax[0].ncp, ncy = lv.ax[1].ncp, ncz = lv.ax[2].ncp;
         const int nlat = ncx * ncy * ncz;
-        load_tables(T, lv, a.R, a.C, a.Z);
         if (t == 0) {
             M.nc[L & 1][0] = ncx;
             M.nc[L & 1][1] = ncy;
@@ -956,71 +573,73 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
         }
         double *const Wk2 = Wk3 + (size_t)ncz * a.Z;
         for (int e = t; e < ncz * a.Z; e += ST_TPB) {   // dense slice weights of this level
-            const int k = e / a.Z, z = e % a.Z;
-            const float4 w = *reinterpret_cast<const float4 *>(lv.ax[2].w + 4 * z);
-            const int d = k - lv.ax[2].base[z];
-            const bool in = d >= 0 && d <= 3;
-            Wk3[e] = in ? wpow<3>(wsel(w, d)) : 0.0;
-            Wk2[e] = in ? wpow<2>(wsel(w, d)) : 0.0;
+            Wk3[e] = lv.wk3[e];
+            Wk2[e] = lv.wk2[e];
         }
         double2 *const Wx3 = reinterpret_cast<double2 *>(smem + a.o_wx), *const Wx2 = Wx3 + 2 * a.R;
-        for (int x = t; x < a.R; x += ST_TPB) {   // row weights^P of this level (wave-uniform reads)
-            const float4 w = *reinterpret_cast<const float4 *>(lv.ax[0].w + 4 * x);
-            Wx3[2 * x] = make_double2(wpow<3>(w.x), wpow<3>(w.y));
-            Wx3[2 * x + 1] = make_double2(wpow<3>(w.z), wpow<3>(w.w));
-            Wx2[2 * x] = make_double2(wpow<2>(w.x), wpow<2>(w.y));
-            Wx2[2 * x + 1] = make_double2(wpow<2>(w.z), wpow<2>(w.w));
+        for (int x = t; x < a.R; x += ST_TPB) {   // row weights of this level (wave-uniform reads)
+            const double2 *w3 = reinterpret_cast<const double2 *>(lv.ax[0].w3i + 4 * x);
+            const double2 *w2 = reinterpret_cast<const double2 *>(lv.ax[0].w2 + 4 * x);
+            Wx3[2 * x] = w3[0];
+            Wx3[2 * x + 1] = w3[1];
+            Wx2[2 * x] = w2[0];
+            Wx2[2 * x + 1] = w2[1];
         }
         // ---- denominator of this level: sum of w^2 over the mask ----
         for (int e = t; e < 2 * nlat; e += ST_TPB) numfix[e] = 0ull;
         if (t == 0) M.item_ctr = 0;
         __syncthreads();
         for (;;) {
-            int item = 0;
-            if (lane == 0) item = atomicAdd(&M.item_ctr, 1);
-            item = __shfl(item, 0, 64);
-            if (item >= a.nitems) break;
-        item = ordr[item];   // largest items first
+            const int item = next_item(M, ordr, a.nitems);
+            if (item < 0) break;
             Item it;
-            if (!item_begin(it, a, b, item)) continue;
-            fit_item<1>(a, it, T, Wk2, Wx2, ncy, ncz, Ub, n, sE, 0.0f, 1.0, ring, numfix);
+            if (!study_item(it, a, b, item)) continue;
+            fit_item<1>(it, T, Wk2, Wx2, ncy, ncz, a.Z, bins, Ub, n, sE, 0.0f, 1.0, ring, a.nb_ring,
+                        numfix);
         }
         __syncthreads();
-        ST_MARK(0);
         for (int e = t; e < nlat; e += ST_TPB) den[e] = fix128_get(numfix + 2 * e, numfix + 2 * e + 1);
         // ---- iterations ----
         int itn = 0;
         for (;;) {
             __syncthreads();
-            ST_MARK(7);
-            if (t == 0) {
-                M.stop = 0;
-                M.exact = 0;
-                if (itn > 0) {
-                    const double conv = conv_of(M.sd, M.sd2, (double)n);
-                    M.conv = conv;
-                    if (!(conv > (double)a.thresh) || itn >= a.lvs->max_iters[L]) M.stop = 1;
+            if (wv == 0) {   // ctrl: convergence, ITK's while-condition, bin range
+                Range3 r;
+                r3_init(r);
+                for (int i = lane; i < a.nitems; i += 64) {
+                    const float4 p = rpart[i];
+                    Range3 o;
+                    o.mx = p.x; o.m1 = p.y; o.m2 = p.z; o.m3 = p.w;
+                    r3_merge(r, o);
                 }
-                if (!M.stop) {
-                    const float bmax = key2f(M.umax_key);
-                    const float umin = M.umin_key == 0xffffffffu ? FLT_MAX : key2f(M.umin_key);
-                    const float umin2 = M.umin2_key == 0xffffffffu ? FLT_MAX : key2f(M.umin2_key);
-                    M.bmax = bmax;
-                    if (umin <= M.u_first) {                       // u1 is not the strict minimum
-                        M.bin_min = umin;
-                        M.slope = (bmax - umin) / (float)(bins - 1);
-                    } else if (M.rx[2] >= 0 && !(M.u_third > M.u_second)) {   // run u1 < u2 >= u3
-                        M.bin_min = umin2;
-                        M.slope = (bmax - umin2) / (float)(bins - 1);
-                    } else {
-                        M.exact = 1;
+                r = r3_wave(r);
+                if (lane == 0) {
+                    M.stop = 0;
+                    M.exact = 0;
+                    if (itn > 0) {
+                        if (a.conv_mode == 0) {
+                            M.conv = (double)M.ch.conv;
+                            if (!(M.ch.conv > a.thresh) || itn >= a.lvs->max_iters[L]) M.stop = 1;
+                        } else {
+                            M.conv = conv_of(M.sd, M.sd2, (double)n);
+                            if (!(M.conv > (double)a.thresh) || itn >= a.lvs->max_iters[L]) M.stop = 1;
+                        }
                     }
-                    M.umax_key = 0u;
-                    M.umin_key = M.umin2_key = 0xffffffffu;
+                    if (!M.stop) {
+                        float u[3];
+                        for (int q = 0; q < M.nfirst; ++q) u[q] = Ub[M.foff[q]];
+                        float bmin;
+                        M.bmax = r.mx;
+                        if (r3_bin_min(r, u, M.nfirst, bmin)) {
+                            M.bin_min = bmin;
+                            M.slope = (r.mx - bmin) / (float)(bins - 1);
+                        } else {
+                            M.exact = 1;
+                        }
+                    }
                 }
             }
             __syncthreads();
-            ST_MARK(1);
             if (M.stop) break;
             if (M.exact) {
                 float *s_cmax = reinterpret_cast<float *>(scr);
@@ -1031,11 +650,10 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                 }
                 __syncthreads();
             }
-            ST_MARK(1);
             ++itn;
             const float bmin = M.bin_min, slope = M.slope;
             const double rinv = 1.0 / (double)slope;   // div_r form of the bin division
-            // ---- hist ----
+            // ---- hist (S3): one packed 64-bit add per value ----
             for (int i = t; i < ST_HC * VH_MAX_BINS; i += ST_TPB) Hc[i] = 0ull;
             __syncthreads();
             {
@@ -1052,21 +670,16 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
 #pragma unroll
                         for (int k = 0; k < 16; ++k) u[k] = j0 + k < n ? Ub[j0 + k] : __int_as_float(0x7fc00000);
                     }
-                    // branch-free: every value does its two adds (zero weights for values that
-                    // add nothing) -- no divergent run bookkeeping
 #pragma unroll
                     for (int k = 0; k < 16; ++k) {
                         int idx;
-                        unsigned long long a0, a1;
-                        parzen_bin_bf(u[k], bmin, rinv, bins, idx, a0, a1);
-                        atomicAdd(&H[idx], a0);
-                        atomicAdd(&H[min(idx + 1, bins - 1)], a1);
+                        const unsigned long long w = hist_pack(u[k], bmin, rinv, bins, idx);
+                        atomicAdd(&H[idx], w);
                     }
                 }
             }
             __syncthreads();
-            ST_MARK(2);
-            // ---- emap (same arithmetic as n4.hip k_n4_emap) ----
+            // ---- emap (same arithmetic as n4.hip k_n4_emap and the oracle) ----
             {
                 const int P = VH_FFT_P, off = (P - bins) / 2;
                 const float sFWHM = a.fwhm / slope;
@@ -1078,8 +691,12 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                     const int h = i - off;
                     unsigned long long s = 0ull;
                     if (h >= 0 && h < bins)
-                        for (int q = 0; q < ST_HC; ++q) s += Hc[q * VH_MAX_BINS + h];
-                    V[fpad(i)] = make_double2((double)s * (1.0 / 4294967296.0), 0.0);
+                        for (int q = 0; q < ST_HC; ++q) {
+                            const unsigned long long w = Hc[q * VH_MAX_BINS + h];
+                            s += (hist_count(w) << 24) - hist_osum(w);
+                            if (h > 0) s += hist_osum(Hc[q * VH_MAX_BINS + h - 1]);
+                        }
+                    V[fpad(i)] = make_double2((double)s * (1.0 / 16777216.0), 0.0);
                     double fx;
                     if (i == 0) {
                         fx = (double)sf;
@@ -1093,10 +710,8 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                 }
                 if (t < P / 2) TW[t] = twv;
                 __syncthreads();
-                ST_MARK(9);
                 if (wv < 2) wave_fft_lds(wv ? F : V, TW, false, FftId(), FftId());
                 __syncthreads();
-                ST_MARK(10);
                 if (wv == 0) {   // Wiener filter (first pass), inverse, clamp and the moment series (last pass)
                     const double noise = (double)a.noise;
                     wave_fft_lds(V, TW, true,
@@ -1114,7 +729,6 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                         });
                 }
                 __syncthreads();
-                ST_MARK(11);
                 if (wv < 2) {   // each series: forward, times the kernel's transform (last pass), inverse
                     double2 *x = wv ? DEN : V;
                     wave_fft_lds(x, TW, false, FftId(), [=](int i, double2 v) {
@@ -1125,31 +739,26 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                     wave_fft_lds(x, TW, true, FftId(), FftId());
                 }
                 __syncthreads();
-                ST_MARK(12);
                 for (int i = t; i < bins; i += ST_TPB) {
                     const double d = DEN[fpad(i + off)].x;
                     sE[i] = d != 0.0 ? (float)(V[fpad(i + off)].x / d) : 0.0f;
                 }
                 __syncthreads();
             }
-            ST_MARK(3);
             // ---- fit ----
             for (int e = t; e < 2 * nlat; e += ST_TPB) numfix[e] = 0ull;
             if (t == 0) M.item_ctr = 0;
             __syncthreads();
             for (;;) {
-                int item = 0;
-                if (lane == 0) item = atomicAdd(&M.item_ctr, 1);
-                item = __shfl(item, 0, 64);
-                if (item >= a.nitems) break;
-        item = ordr[item];   // largest items first
+                const int item = next_item(M, ordr, a.nitems);
+                if (item < 0) break;
                 Item it;
-                if (!item_begin(it, a, b, item)) continue;
-                fit_item<0>(a, it, T, Wk3, Wx3, ncy, ncz, Ub, n, sE, bmin, rinv, ring, numfix);
+                if (!study_item(it, a, b, item)) continue;
+                fit_item<0>(it, T, Wk3, Wx3, ncy, ncz, a.Z, bins, Ub, n, sE, bmin, rinv, ring,
+                            a.nb_ring, numfix);
             }
             __syncthreads();
-            ST_MARK(4);
-            // ---- lattice update (k_n4_tilesum<0>) and P1 (k_n4_P1) ----
+            // ---- lattice update and P1 ----
             for (int e = t; e < nlat; e += ST_TPB) {
                 const double d = den[e];
                 const double num = fix128_get(numfix + 2 * e, numfix + 2 * e + 1);
@@ -1168,7 +777,6 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
             }
             if (t == 0) M.item_ctr = 0;
             __syncthreads();
-            ST_MARK(5);
             // ---- eval ----
             {
                 const bool first_of_level = itn == 1;
@@ -1177,27 +785,41 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                 const TabV To = tab_view(smem + (so ? a.o_tab1 : a.o_tab0), a.R, a.C, a.Z, a.kcap);
                 const int ncyo = M.nc[so][1];
                 for (;;) {
-                    int item = 0;
-                    if (lane == 0) item = atomicAdd(&M.item_ctr, 1);
-                    item = __shfl(item, 0, 64);
-                    if (item >= a.nitems) break;
-        item = ordr[item];   // largest items first
+                    const int item = next_item(M, ordr, a.nitems);
+                    if (item < 0) break;
                     Item it;
-                    if (!item_begin(it, a, b, item)) {
-                        if (lane == 0) { ipart[2 * item] = 0.0; ipart[2 * item + 1] = 0.0; }
+                    if (!study_item(it, a, b, item)) {
+                        if (lane == 0) {
+                            ipart[2 * item] = 0.0;
+                            ipart[2 * item + 1] = 0.0;
+                            rpart[item] = make_float4(-FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX);
+                        }
                         continue;
                     }
-                    if (so == (L & 1))
-                        eval_item<true>(a, it, item, T, To, ncy, ncyo, P1n, P1o, bo_mode, Lb, Ub,
-                                        n, fm, ipart, M);
-                    else
-                        eval_item<false>(a, it, item, T, To, ncy, ncyo, P1n, P1o, bo_mode, Lb, Ub,
-                                         n, fm, ipart, M);
+                    const bool same = so == (L & 1);
+                    if (a.conv_mode == 0) {
+                        if (same)
+                            eval_item<true, 0>(it, item, a.Z, T, To, ncy, ncyo, P1n, P1o, bo_mode, Lb, Ub, Db, n, ipart, rpart);
+                        else
+                            eval_item<false, 0>(it, item, a.Z, T, To, ncy, ncyo, P1n, P1o, bo_mode, Lb, Ub, Db, n, ipart, rpart);
+                    } else {
+                        if (same)
+                            eval_item<true, 1>(it, item, a.Z, T, To, ncy, ncyo, P1n, P1o, bo_mode, Lb, Ub, Db, n, ipart, rpart);
+                        else
+                            eval_item<false, 1>(it, item, a.Z, T, To, ncy, ncyo, P1n, P1o, bo_mode, Lb, Ub, Db, n, ipart, rpart);
+                    }
                 }
             }
+            if (t == 0) {
+                M.ch.a_done = 0;
+                M.ch.b_done = 0;
+            }
             __syncthreads();
-            ST_MARK(6);
-            if (wv == 0) {   // item partials in item order: deterministic
+            // ---- convergence of this iteration ----
+            if (a.conv_mode == 0) {   // S7: ITK's float Welford recurrence, two waves
+                if (wv == 0) chain_wave_mu(Db, n, slots, &M.ch);
+                else if (wv == 1) chain_wave_sig(n, slots, &M.ch);
+            } else if (wv == 0) {   // S7x: item partials in item order
                 double sd = 0.0, sd2 = 0.0;
                 for (int i = lane; i < a.nitems; i += 64) {
                     sd += ipart[2 * i];
@@ -1228,19 +850,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
             refine_axis_st(T2, lat, 2 * ncx - 3, 2 * ncy - 3, ncz, 2);
             __syncthreads();
         }
-        ST_MARK(8);
     }
-#ifdef ST_PROF
-    if (t == 0) stb->conv_level[3] = (float)(wall_clock64() - st_w0) * 0.01f;   // us
-    if (t == 0 && blockIdx.x == 0)
-        printf("ST_BLK %d wall %llu %llu cycles %llu xcc %u\n", (int)blockIdx.x, st_w0, wall_clock64(),
-               clock64() - st_c0, __builtin_amdgcn_s_getreg((20 << 0) | (0 << 6) | (3 << 11)));
-    if (t == 0 && blockIdx.x == 0)
-        printf("ST_PROF den %llu ctrl %llu hist %llu emap %llu fit %llu latP1 %llu eval %llu loop %llu "
-               "refine %llu | emap: init %llu fwd %llu wiener %llu conv %llu sE %llu\n", st_prof[0],
-               st_prof[1], st_prof[2], st_prof[3], st_prof[4], st_prof[5], st_prof[6], st_prof[7],
-               st_prof[8], st_prof[9], st_prof[10], st_prof[11], st_prof[12], st_prof[3]);
-#endif
     // final field's P1 for k_n4_final
     const double *P1f = cur ? P1b1 : P1b0;
     for (int e = t; e < p1last; e += ST_TPB) a.P1out[b * a.q2cap + e] = P1f[e];
@@ -1284,14 +894,15 @@ static bool study_layout(const vh_batch *b, const vh_n4_params &prm, StudyLayout
     const size_t refine = 2 * sizeof(float) * (size_t)nlat_max + 64;
     const size_t emap = sizeof(double2) * (3 * ST_FFT_N + VH_FFT_P / 2) +
                         sizeof(unsigned long long) * ST_HC * VH_MAX_BINS;
-    const bool geom_ok = s_cap <= 64 * ST_SO;   // one ring row's stage-1 outputs fit the lanes
+    const bool geom_ok = s_cap <= 64 * FIT_SO;   // one ring row's stage-1 outputs fit the lanes
     s_cap = std::max(s_cap, 64);
-    // ring rows per wave: up to ST_NB within ~40 KB for all waves
-    const int nb_ring = std::max(1, std::min(ST_NB, (int)(40960 / (ST_WAVES * 8 * (size_t)s_cap))));
+    // ring rows per wave: up to FIT_NB within ~40 KB for all waves
+    const int nb_ring = std::max(1, std::min(FIT_NB, (int)(40960 / (ST_WAVES * 8 * (size_t)s_cap))));
     const size_t fit_num = 2 * sizeof(unsigned long long) * (size_t)nlat_max;
     const size_t fit = ((fit_num + 15) & ~(size_t)15) + sizeof(double) * ST_WAVES * nb_ring * (size_t)s_cap;
     const size_t exact = sizeof(float) * 2 * ST_TPB;
-    const size_t scr = std::max({refine, emap, fit, exact});
+    const size_t chain = sizeof(ChainSlot) * CH_SLOTS;
+    const size_t scr = std::max({refine, emap, fit, exact, chain});
     auto A = [](size_t v) { return (v + 15) & ~(size_t)15; };
     size_t o = 0;
     a.o_E = (int32_t)o; o += A(sizeof(float) * VH_MAX_BINS);
@@ -1302,9 +913,10 @@ static bool study_layout(const vh_batch *b, const vh_n4_params &prm, StudyLayout
     a.o_den = (int32_t)o; o += A(sizeof(double) * nlat_max);
     a.o_P10 = (int32_t)o; o += A(sizeof(double) * p1_max);
     a.o_P11 = (int32_t)o; o += A(sizeof(double) * p1_max);
-    const int64_t nslots = (b->R + 63) / 64;
+    const int64_t nslots = (b->R + SLOT_R - 1) / SLOT_R;
     const int64_t nitems = b->n4_tiles * nslots;
     a.o_ipart = (int32_t)o; o += A(sizeof(double) * 2 * (size_t)nitems);
+    a.o_rpart = (int32_t)o; o += A(sizeof(float4) * (size_t)nitems);
     a.o_order = (int32_t)o; o += A(sizeof(int32_t) * (size_t)nitems);
     a.o_misc = (int32_t)o; o += A(sizeof(StudyMisc));
     a.o_wk = (int32_t)o; o += A(2 * sizeof(double) * (size_t)kcap * Z);
@@ -1317,7 +929,8 @@ static bool study_layout(const vh_batch *b, const vh_n4_params &prm, StudyLayout
     a.nslots = (int32_t)nslots;
     a.nitems = (int32_t)nitems;
     out.bytes = o;
-    return geom_ok && o <= ST_MAX_LDS && prm.n_levels <= VH_MAX_LEVELS && b->V < ((int64_t)1 << 29);
+    // packed histogram bins stay exact below 2^20 values per study (hist_pack)
+    return geom_ok && o <= ST_MAX_LDS && prm.n_levels <= VH_MAX_LEVELS && b->V < ((int64_t)1 << 20);
 }
 
 bool vh_n4_study_eligible(const vh_batch *b, const vh_n4_params &prm, size_t *lds_bytes) {
@@ -1336,8 +949,10 @@ void vh_launch_n4_study(vh_batch *b, const vh_n4_params &prm) {
     a.V = b->V;
     a.L0 = b->d_L0;
     a.U = b->d_U;
+    a.D = b->d_D;
     a.rs = b->d_rowstart;
     a.rmask = b->d_rowmask;
+    a.rrs = b->d_rrank;
     a.sc = b->d_sc;
     a.st = b->d_st;
     a.P1out = b->d_P1;
@@ -1351,6 +966,7 @@ void vh_launch_n4_study(vh_batch *b, const vh_n4_params &prm) {
     a.ntiles = (int32_t)b->n4_tiles;
     a.nlev = prm.n_levels;
     a.bins = prm.n_bins;
+    a.conv_mode = prm.conv_mode;
     a.thresh = prm.conv_threshold;
     a.fwhm = prm.fwhm;
     a.noise = prm.wiener_noise;

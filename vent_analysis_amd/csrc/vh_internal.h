@@ -64,6 +64,7 @@ struct N4State {
     int32_t tlast;           // T buffer (0/1) holding the column tables of the last evaluated field
     uint32_t umax_key, umin_key;  // sortable keys: max over all masked, min over all but first
     float u_first;
+    float conv_w;            // S7: ITK's float Welford convergence of the last eval (k_n4_welford)
     double conv;
     int32_t iters_level[VH_MAX_LEVELS];
     float conv_level[VH_MAX_LEVELS];
@@ -119,9 +120,11 @@ struct vh_batch {
     uint64_t *d_cohort = nullptr;
     // N4 workspace
     float *d_L0 = nullptr, *d_lat = nullptr, *d_E = nullptr;
-    double *d_fitpart = nullptr;     // [nb][tiles][lattice] per-tile contracted fit slabs
+    unsigned long long *d_numfix = nullptr;   // [nb][lattice][2] 128-bit fixed-point fit sums (S5)
     int32_t *d_rowstart = nullptr;   // [nb][tiles][R] compact offset of each (64-column tile, row)
     uint64_t *d_rowmask = nullptr;   // [nb][tiles][R] mask == 1 lanes of each (tile, row)
+    int32_t *d_rrank = nullptr;      // [nb][tiles][R] raster rank of the first masked voxel of (tile, row)
+    float *d_D = nullptr;            // [nb][VS] B_old - B_new in raster order (S7 convergence input)
     // compact N4 state: mask==1 voxels in tile-row order, volume stride VS
     int64_t VS = 0;
     int rsh = 1;                     // compact voxel index = (row << rsh) | column
@@ -133,16 +136,14 @@ struct vh_batch {
     uint64_t *d_hpart = nullptr;     // [chunks][VH_MAX_BINS] per-chunk histograms
     double *d_cpart = nullptr;       // [chunks][2] per-chunk convergence sums
     int64_t n4_tiles = 0;
-    std::vector<int> fit_smax;       // per level: doubles of the fit's slice-contracted tile slab
-    std::vector<size_t> tile_off;    // per level: offset of the fit tile metadata in d_tabs
-    std::vector<size_t> jt_off;      // per level: lattice col -> tile range table in d_tabs
-    double *d_P1 = nullptr, *d_num = nullptr, *d_den = nullptr;
+    std::vector<size_t> lvx_off;     // per level: xst / wk3 / wk2 offsets in d_tabs
+    double *d_P1 = nullptr, *d_den = nullptr;
     float *d_T = nullptr;            // [2][nb][CZ][ncx] per-column lattice contraction (new / previous field)
     int64_t t_cap = 0;
     N4State *d_st = nullptr;
     int32_t *d_nactive = nullptr;
     void *d_tabs = nullptr;          // device copy of all per-level axis tables
-    int64_t lat_cap = 0, q1_cap = 0, q2_cap = 0;
+    int64_t lat_cap = 0, q2_cap = 0;
     std::vector<size_t> tab_off;     // offsets of each (level, axis) table in d_tabs
     vh_n4_params tab_prm{};          // parameters the tables were built for
     bool tabs_valid = false;
