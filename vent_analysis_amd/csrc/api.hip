@@ -19,12 +19,12 @@ ScopedKTimer::ScopedKTimer(vh_batch *bb, const char *name, double bytes) : b(bb)
     hipEvent_t e0;
     HIP_TRY(hipEventCreate(&e0));
     HIP_TRY(hipEventCreate(&e1));
-    HIP_TRY(hipEventRecord(e0, b->ctx->stream));
+    HIP_TRY(hipEventRecord(e0, b->stream));
     t->ev.push_back(e0);
 }
 ScopedKTimer::~ScopedKTimer() {
     if (!t) return;
-    (void)hipEventRecord(e1, b->ctx->stream);
+    (void)hipEventRecord(e1, b->stream);
     t->ev.push_back(e1);
 }
 
@@ -104,6 +104,10 @@ static void batch_free(vh_batch *b) {
     dfree(b->d_numfix); dfree(b->d_rowstart); dfree(b->d_rowmask); dfree(b->d_rrank); dfree(b->d_D); dfree(b->d_P1); dfree(b->d_den); dfree(b->d_T);
     dfree(b->d_U); dfree(b->d_ridx); dfree(b->d_cp); dfree(b->d_cvol); dfree(b->d_hpart); dfree(b->d_cpart); dfree(b->d_st); dfree(b->d_nactive); dfree(b->d_tabs); dfree(b->d_twiddle); dfree(b->d_study_lv);
     dfree(b->d_bitmap); dfree(b->d_ci_list); dfree(b->d_ci_shell); dfree(b->d_ci_hist);
+    dfree(b->d_ci_offL); dfree(b->d_ci_bounds); dfree(b->d_ci_radii); dfree(b->d_ci_status);
+    dfree(b->d_ci_count); dfree(b->d_ci_map);
+    if (b->stream) (void)hipStreamDestroy(b->stream);
+    if (b->h_flags) (void)hipHostFree(b->h_flags);
     delete b;
 }
 
@@ -112,6 +116,10 @@ static vh_batch *batch_new(vh_ctx *ctx, int64_t R, int64_t C, int64_t Z, int64_t
     HIP_TRY(hipSetDevice(ctx->device));
     vh_batch *b = new vh_batch;
     b->ctx = ctx;
+    if (hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete b;
+        throw VhError{VH_ERR_HIP, "hipStreamCreateWithFlags failed"};
+    }
     b->R = R; b->C = C; b->Z = Z; b->nb = nb;
     b->V = R * C * Z;
     b->CZ = C * Z;
@@ -150,7 +158,7 @@ static vh_batch *batch_new(vh_ctx *ctx, int64_t R, int64_t C, int64_t Z, int64_t
 }
 
 static void batch_upload(vh_batch *b, const float *hp, const uint8_t *mask) {
-    hipStream_t st = b->ctx->stream;
+    hipStream_t st = b->stream;
     const size_t NV = (size_t)b->nb * b->V;
     if (hp) HIP_TRY(hipMemcpyAsync(b->d_hp, hp, sizeof(float) * NV, hipMemcpyHostToDevice, st));
     if (mask) HIP_TRY(hipMemcpyAsync(b->d_mask, mask, NV, hipMemcpyHostToDevice, st));
@@ -230,7 +238,7 @@ static void fill_results(vh_batch *b, vh_vdp_result *res) {
 
 static void batch_download(vh_batch *b, float *n4, uint8_t *defect, uint8_t *border, uint8_t *lb,
                            vh_vdp_result *res) {
-    hipStream_t st = b->ctx->stream;
+    hipStream_t st = b->stream;
     HIP_TRY(hipStreamSynchronize(st));
     const size_t NV = (size_t)b->nb * b->V;
     if (n4) HIP_TRY(hipMemcpy(n4, b->opts.do_n4 ? b->d_n4 : b->d_hp, sizeof(float) * NV, hipMemcpyDeviceToHost));
@@ -240,19 +248,17 @@ static void batch_download(vh_batch *b, float *n4, uint8_t *defect, uint8_t *bor
     if (res) fill_results(b, res);
 }
 
-// a cached scratch batch per context for the host-buffer entry points
-struct CtxScratch {
-    vh_batch *b = nullptr;
-};
-static std::map<vh_ctx *, CtxScratch> g_scratch;
-
+// The context's cached scratch batch for the host-buffer entry points (caller holds ctx->mu).
 static vh_batch *scratch_batch(vh_ctx *ctx, int64_t R, int64_t C, int64_t Z, int64_t nb) {
-    CtxScratch &s = g_scratch[ctx];
-    if (s.b && s.b->R == R && s.b->C == C && s.b->Z == Z && s.b->nb == nb) return s.b;
-    if (s.b) batch_free(s.b);
-    s.b = nullptr;
-    s.b = batch_new(ctx, R, C, Z, nb);
-    return s.b;
+    vh_batch *&s = ctx->scratch;
+    if (s && s->R == R && s->C == C && s->Z == Z && s->nb == nb) return s;
+    if (s) {
+        (void)hipStreamSynchronize(s->stream);
+        batch_free(s);
+    }
+    s = nullptr;
+    s = batch_new(ctx, R, C, Z, nb);
+    return s;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -318,7 +324,6 @@ int vh_create(int device, vh_ctx **out) {
     c->device = device;
     API_TRY(c, {
         HIP_TRY(hipSetDevice(device));
-        HIP_TRY(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
         HIP_TRY(hipHostMalloc((void **)&c->h_pinned, sizeof(int32_t) * 1024));
         *out = c;
     })
@@ -327,13 +332,12 @@ int vh_create(int device, vh_ctx **out) {
 int vh_destroy(vh_ctx *ctx) {
     if (!ctx) return VH_OK;
     (void)hipSetDevice(ctx->device);
-    auto it = g_scratch.find(ctx);
-    if (it != g_scratch.end()) {
-        batch_free(it->second.b);
-        g_scratch.erase(it);
+    if (ctx->scratch) {
+        (void)hipStreamSynchronize(ctx->scratch->stream);
+        batch_free(ctx->scratch);
+        ctx->scratch = nullptr;
     }
     if (ctx->comm) ncclCommDestroy((ncclComm_t)ctx->comm);
-    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
     delete ctx;
     return VH_OK;
@@ -342,12 +346,16 @@ int vh_destroy(vh_ctx *ctx) {
 const char *vh_last_error(const vh_ctx *ctx) { return ctx ? ctx->last_error.c_str() : ""; }
 
 int vh_synchronize(vh_ctx *ctx) {
-    API_TRY(ctx, { HIP_TRY(hipStreamSynchronize(ctx->stream)); })
+    API_TRY(ctx, {
+        HIP_TRY(hipSetDevice(ctx->device));
+        HIP_TRY(hipDeviceSynchronize());
+    })
 }
 
 int vh_n4(vh_ctx *ctx, const float *hp, const uint8_t *mask, int64_t R, int64_t C, int64_t Z,
           int64_t batch, const vh_n4_params *prm, float *out, int32_t *iters, float *conv) {
     API_TRY(ctx, {
+        std::lock_guard<std::mutex> lock(ctx->mu);
         if (!hp || !mask || !out || !prm) throw VhError{VH_ERR_ARG, "null buffer"};
         vh_batch *b = scratch_batch(ctx, R, C, Z, batch);
         check_n4_params(b, *prm);
@@ -362,7 +370,7 @@ int vh_n4(vh_ctx *ctx, const float *hp, const uint8_t *mask, int64_t R, int64_t 
         HIP_TRY(hipSetDevice(ctx->device));
         vh_launch_mask_stats(b);
         vh_launch_n4(b, o.n4);
-        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        HIP_TRY(hipStreamSynchronize(b->stream));
         HIP_TRY(hipMemcpy(out, b->d_n4, sizeof(float) * batch * b->V, hipMemcpyDeviceToHost));
         std::vector<N4State> st(batch);
         HIP_TRY(hipMemcpy(st.data(), b->d_st, sizeof(N4State) * batch, hipMemcpyDeviceToHost));
@@ -381,21 +389,23 @@ int vh_n4(vh_ctx *ctx, const float *hp, const uint8_t *mask, int64_t R, int64_t 
 int vh_border(vh_ctx *ctx, const uint8_t *a, int64_t R, int64_t C, int64_t Z, int64_t batch,
               uint8_t *border) {
     API_TRY(ctx, {
+        std::lock_guard<std::mutex> lock(ctx->mu);
         if (!a || !border) throw VhError{VH_ERR_ARG, "null buffer"};
         vh_batch *b = scratch_batch(ctx, R, C, Z, batch);
         HIP_TRY(hipSetDevice(ctx->device));
         b->profile = false;
         const size_t NV = (size_t)batch * b->V;
-        HIP_TRY(hipMemcpyAsync(b->d_defect, a, NV, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(b->d_defect, a, NV, hipMemcpyHostToDevice, b->stream));
         vh_launch_border(b, b->d_defect, b->d_border);
-        HIP_TRY(hipMemcpyAsync(border, b->d_border, NV, hipMemcpyDeviceToHost, ctx->stream));
-        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        HIP_TRY(hipMemcpyAsync(border, b->d_border, NV, hipMemcpyDeviceToHost, b->stream));
+        HIP_TRY(hipStreamSynchronize(b->stream));
     })
 }
 
 int vh_snr(vh_ctx *ctx, const float *hp, const uint8_t *mask, int64_t R, int64_t C, int64_t Z,
            int64_t batch, double *snr) {
     API_TRY(ctx, {
+        std::lock_guard<std::mutex> lock(ctx->mu);
         if (!hp || !mask || !snr) throw VhError{VH_ERR_ARG, "null buffer"};
         vh_batch *b = scratch_batch(ctx, R, C, Z, batch);
         batch_upload(b, hp, mask);
@@ -403,7 +413,7 @@ int vh_snr(vh_ctx *ctx, const float *hp, const uint8_t *mask, int64_t R, int64_t
         b->profile = false;
         vh_launch_mask_stats(b);
         vh_launch_snr(b);
-        HIP_TRY(hipStreamSynchronize(ctx->stream));
+        HIP_TRY(hipStreamSynchronize(b->stream));
         std::vector<VolScalars> sc(batch);
         HIP_TRY(hipMemcpy(sc.data(), b->d_sc, sizeof(VolScalars) * batch, hipMemcpyDeviceToHost));
         for (int64_t i = 0; i < batch; ++i) {
@@ -417,10 +427,11 @@ int vh_vdp(vh_ctx *ctx, const float *hp, const float *n4, const uint8_t *mask, i
            int64_t C, int64_t Z, int64_t batch, float thresh, const double vox[3],
            uint8_t *defect, uint8_t *defect_border, uint8_t *lb, vh_vdp_result *res) {
     API_TRY(ctx, {
+        std::lock_guard<std::mutex> lock(ctx->mu);
         if (!n4 || !mask || !res || !vox) throw VhError{VH_ERR_ARG, "null buffer"};
         vh_batch *b = scratch_batch(ctx, R, C, Z, batch);
         const size_t NV = (size_t)batch * b->V;
-        HIP_TRY(hipMemcpyAsync(b->d_n4, n4, sizeof(float) * NV, hipMemcpyHostToDevice, ctx->stream));
+        HIP_TRY(hipMemcpyAsync(b->d_n4, n4, sizeof(float) * NV, hipMemcpyHostToDevice, b->stream));
         batch_upload(b, hp, mask);
         vh_run_opts o;
         vh_default_run_opts(&o);
@@ -444,6 +455,7 @@ int vh_ci(vh_ctx *ctx, const uint8_t *defect, int64_t R, int64_t C, int64_t Z, i
           const double *radii, int64_t nb, double minvox, double *ci_array, double *ci_scalar,
           int32_t *shell) {
     API_TRY(ctx, {
+        std::lock_guard<std::mutex> lock(ctx->mu);
         if (!defect || !offs || !dup || !bounds || !radii || rows < 1 || nb < 1)
             throw VhError{VH_ERR_ARG, "null buffer / empty table"};
         for (int64_t q = 0; q < nb; ++q)
@@ -453,18 +465,11 @@ int vh_ci(vh_ctx *ctx, const uint8_t *defect, int64_t R, int64_t C, int64_t Z, i
         HIP_TRY(hipSetDevice(ctx->device));
         b->profile = false;
         const size_t NV = (size_t)batch * b->V;
-        HIP_TRY(hipMemcpyAsync(b->d_defect, defect, NV, hipMemcpyHostToDevice, ctx->stream));
-        double *d_ci = nullptr;
-        if (ci_array) HIP_TRY(hipMalloc(&d_ci, sizeof(double) * NV));
-        try {
-            vh_ci_run(b, offs, dup, rows, bounds, radii, nb, minvox, d_ci);
-            if (ci_array) HIP_TRY(hipMemcpy(ci_array, d_ci, sizeof(double) * NV, hipMemcpyDeviceToHost));
-            if (shell) HIP_TRY(hipMemcpy(shell, b->d_ci_shell, sizeof(int32_t) * NV, hipMemcpyDeviceToHost));
-        } catch (...) {
-            if (d_ci) (void)hipFree(d_ci);
-            throw;
-        }
-        if (d_ci) HIP_TRY(hipFree(d_ci));
+        HIP_TRY(hipMemcpyAsync(b->d_defect, defect, NV, hipMemcpyHostToDevice, b->stream));
+        if (ci_array && !b->d_ci_map) HIP_TRY(hipMalloc(&b->d_ci_map, sizeof(double) * NV));
+        vh_ci_run(b, offs, dup, rows, bounds, radii, nb, minvox, ci_array ? b->d_ci_map : nullptr);
+        if (ci_array) HIP_TRY(hipMemcpy(ci_array, b->d_ci_map, sizeof(double) * NV, hipMemcpyDeviceToHost));
+        if (shell) HIP_TRY(hipMemcpy(shell, b->d_ci_shell, sizeof(int32_t) * NV, hipMemcpyDeviceToHost));
         std::vector<VolScalars> sc(batch);
         HIP_TRY(hipMemcpy(sc.data(), b->d_sc, sizeof(VolScalars) * batch, hipMemcpyDeviceToHost));
         for (int64_t i = 0; i < batch; ++i) {
@@ -485,7 +490,7 @@ int vh_batch_create(vh_ctx *ctx, int64_t R, int64_t C, int64_t Z, int64_t batch,
 int vh_batch_destroy(vh_batch *b) {
     if (b) {
         (void)hipSetDevice(b->ctx->device);
-        (void)hipStreamSynchronize(b->ctx->stream);
+        (void)hipStreamSynchronize(b->stream);
         batch_free(b);
     }
     return VH_OK;
@@ -506,7 +511,7 @@ int vh_batch_run(vh_batch *b, const vh_run_opts *opts) {
 }
 
 int vh_batch_sync(vh_batch *b) {
-    API_TRY(b->ctx, { HIP_TRY(hipStreamSynchronize(b->ctx->stream)); })
+    API_TRY(b->ctx, { HIP_TRY(hipStreamSynchronize(b->stream)); })
 }
 
 int vh_batch_download(vh_batch *b, float *n4, uint8_t *defect, uint8_t *defect_border, uint8_t *lb,
@@ -519,7 +524,7 @@ int vh_batch_download(vh_batch *b, float *n4, uint8_t *defect, uint8_t *defect_b
 
 int vh_batch_cohort_hist(vh_batch *b, uint64_t *hist) {
     API_TRY(b->ctx, {
-        HIP_TRY(hipStreamSynchronize(b->ctx->stream));
+        HIP_TRY(hipStreamSynchronize(b->stream));
         HIP_TRY(hipMemcpy(hist, b->d_cohort, sizeof(uint64_t) * VH_COHORT_BINS, hipMemcpyDeviceToHost));
     })
 }
@@ -531,7 +536,7 @@ const char *vh_batch_kernel_names(void) {
 
 int vh_batch_reset_timers(vh_batch *b) {
     API_TRY(b->ctx, {
-        HIP_TRY(hipStreamSynchronize(b->ctx->stream));
+        HIP_TRY(hipStreamSynchronize(b->stream));
         clear_timers(b);
     })
 }
@@ -579,7 +584,7 @@ int vh_batch_cohort_allreduce(vh_batch *b) {
         vh_ctx *c = b->ctx;
         if (!c->comm) throw VhError{VH_ERR_ARG, "vh_comm_init has not been called"};
         ncclResult_t r = ncclAllReduce(b->d_cohort, b->d_cohort, VH_COHORT_BINS, ncclUint64, ncclSum,
-                                       (ncclComm_t)c->comm, c->stream);
+                                       (ncclComm_t)c->comm, b->stream);
         if (r != ncclSuccess) throw VhError{VH_ERR_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r)};
     })
 }

@@ -124,7 +124,7 @@ __global__ void k_ci_scatter(const int32_t *shell_of, const uint8_t *defect, con
 void vh_ci_run(vh_batch *b, const int16_t *offs, const uint8_t *dup, int64_t rows,
                const int32_t *bounds, const double *radii, int64_t nbs, double minvox,
                double *d_ci) {
-    hipStream_t st = b->ctx->stream;
+    hipStream_t st = b->stream;
     const int64_t words = (b->V + 31) / 32;
     // px2vec strides (CI.py:65-68): s0 = R (rows), s1 = C (cols): L = i + j R + k R C
     std::vector<int32_t> offL(rows);
@@ -132,14 +132,19 @@ void vh_ci_run(vh_batch *b, const int16_t *offs, const uint8_t *dup, int64_t row
         offL[r] = dup[r] ? CI_SENTINEL
                          : (int32_t)(offs[3 * r] + (int64_t)offs[3 * r + 1] * b->R +
                                      (int64_t)offs[3 * r + 2] * b->R * b->C);
-    int32_t *d_offL = nullptr, *d_bounds = nullptr, *d_status = nullptr;
-    double *d_radii = nullptr;
-    unsigned long long *d_count = nullptr;
-    HIP_TRY(hipMalloc(&d_offL, sizeof(int32_t) * rows));
-    HIP_TRY(hipMalloc(&d_bounds, sizeof(int32_t) * nbs));
-    HIP_TRY(hipMalloc(&d_radii, sizeof(double) * nbs));
-    HIP_TRY(hipMalloc(&d_status, sizeof(int32_t) * b->nb));
-    HIP_TRY(hipMalloc(&d_count, sizeof(unsigned long long) * b->nb));
+    // workspace owned by the batch (freed with it): no allocation, and nothing to leak, per call
+    if (rows > b->ci_rows_cap) {
+        if (b->d_ci_offL) HIP_TRY(hipFree(b->d_ci_offL));
+        b->d_ci_offL = nullptr;
+        HIP_TRY(hipMalloc(&b->d_ci_offL, sizeof(int32_t) * rows));
+        b->ci_rows_cap = rows;
+    }
+    if (!b->d_ci_status) {
+        HIP_TRY(hipMalloc(&b->d_ci_status, sizeof(int32_t) * b->nb));
+        HIP_TRY(hipMalloc(&b->d_ci_count, sizeof(unsigned long long) * b->nb));
+    }
+    int32_t *d_offL = b->d_ci_offL, *d_status = b->d_ci_status;
+    unsigned long long *d_count = b->d_ci_count;
     if (!b->d_bitmap) {
         HIP_TRY(hipMalloc(&b->d_bitmap, sizeof(uint32_t) * b->nb * words));
         HIP_TRY(hipMalloc(&b->d_ci_list, sizeof(int32_t) * b->nb * b->V));
@@ -147,9 +152,19 @@ void vh_ci_run(vh_batch *b, const int16_t *offs, const uint8_t *dup, int64_t row
     }
     if (nbs > b->ci_nb_cap) {
         if (b->d_ci_hist) HIP_TRY(hipFree(b->d_ci_hist));
+        if (b->d_ci_bounds) HIP_TRY(hipFree(b->d_ci_bounds));
+        if (b->d_ci_radii) HIP_TRY(hipFree(b->d_ci_radii));
+        b->d_ci_hist = nullptr;
+        b->d_ci_bounds = nullptr;
+        b->d_ci_radii = nullptr;
+        b->ci_nb_cap = 0;
         HIP_TRY(hipMalloc(&b->d_ci_hist, sizeof(uint32_t) * b->nb * nbs));
+        HIP_TRY(hipMalloc(&b->d_ci_bounds, sizeof(int32_t) * nbs));
+        HIP_TRY(hipMalloc(&b->d_ci_radii, sizeof(double) * nbs));
         b->ci_nb_cap = nbs;
     }
+    int32_t *d_bounds = b->d_ci_bounds;
+    double *d_radii = b->d_ci_radii;
     HIP_TRY(hipMemcpyAsync(d_offL, offL.data(), sizeof(int32_t) * rows, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(d_bounds, bounds, sizeof(int32_t) * nbs, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemcpyAsync(d_radii, radii, sizeof(double) * nbs, hipMemcpyHostToDevice, st));
@@ -176,9 +191,4 @@ void vh_ci_run(vh_batch *b, const int16_t *offs, const uint8_t *dup, int64_t row
         VH_CHECK_LAUNCH();
     }
     HIP_TRY(hipStreamSynchronize(st));
-    HIP_TRY(hipFree(d_offL));
-    HIP_TRY(hipFree(d_bounds));
-    HIP_TRY(hipFree(d_radii));
-    HIP_TRY(hipFree(d_status));
-    HIP_TRY(hipFree(d_count));
 }

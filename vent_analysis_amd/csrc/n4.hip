@@ -1213,7 +1213,7 @@ static int fit_rowcap(const vh_batch *b, const vh_n4_params &prm, int L) {
 // range [cp[vol0], cp[vol0 + ns]); converged volumes' blocks exit at once.
 static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int64_t ns,
                         const std::vector<int32_t> &hcp) {
-    hipStream_t st = b->ctx->stream;
+    hipStream_t st = b->stream;
     const int64_t ntiles = b->n4_tiles;
     const int32_t ch0 = hcp[vol0], nch = hcp[vol0 + ns] - hcp[vol0];
     const dim3 cg((unsigned)((b->CZ + VH_TPB - 1) / VH_TPB), (unsigned)ns);
@@ -1226,7 +1226,8 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
     const dim3 fg((unsigned)((nitems + FIT_WAVES - 1) / FIT_WAVES), (unsigned)ns);
     float *U = b->d_U;
     std::vector<hipEvent_t> evs;
-    int32_t *hflag = b->ctx->h_pinned;
+    if (!b->h_flags) HIP_TRY(hipHostMalloc((void **)&b->h_flags, sizeof(int32_t) * 1024));
+    int32_t *hflag = b->h_flags;
     int total_iters = 0;
     for (int L = 0; L < prm.n_levels; ++L) total_iters += prm.max_iters[L];
     HIP_TRY(hipMemsetAsync(b->d_nactive, 0, sizeof(int32_t) * (total_iters + 1), st));
@@ -1347,7 +1348,7 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
 }
 
 void vh_launch_n4(vh_batch *b, const vh_n4_params &prm) {
-    hipStream_t st = b->ctx->stream;
+    hipStream_t st = b->stream;
     vh_ensure_n4_workspace(b, prm);
     const dim3 cg = col_grid(b);
     const int64_t ntiles = b->n4_tiles;

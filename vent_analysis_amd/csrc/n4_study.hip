@@ -553,6 +553,9 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
         }
         init_item(a, b, it, item, Lb, Ub, n, rpart);
     }
+    // every wave must have left the init queue before thread 0 resets the item counter for the
+    // denominator pass (a late wave would otherwise take den-pass items)
+    __syncthreads();
     {
         const DevLevel &l0 = a.lvs->lv[0];
         const int nl0 = l0.ax[0].ncp * l0.ax[1].ncp * l0.ax[2].ncp;
@@ -977,7 +980,7 @@ void vh_launch_n4_study(vh_batch *b, const vh_n4_params &prm) {
     }
     if (!b->d_study_lv) HIP_TRY(hipMalloc(&b->d_study_lv, sizeof(StudyLevels)));
     HIP_TRY(hipMemcpyAsync(b->d_study_lv, &h, sizeof(StudyLevels), hipMemcpyHostToDevice,
-                           b->ctx->stream));
+                           b->stream));
     a.lvs = (const StudyLevels *)b->d_study_lv;
     a.vol0 = 0;
     static bool attr_set = false;
@@ -987,6 +990,6 @@ void vh_launch_n4_study(vh_batch *b, const vh_n4_params &prm) {
         attr_set = true;
     }
     ScopedKTimer tm(b, "n4_study", 0.0);
-    k_n4_study<<<(unsigned)b->nb, ST_TPB, Ly.bytes, b->ctx->stream>>>(a);
+    k_n4_study<<<(unsigned)b->nb, ST_TPB, Ly.bytes, b->stream>>>(a);
     VH_CHECK_LAUNCH();
 }

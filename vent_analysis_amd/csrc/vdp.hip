@@ -141,7 +141,7 @@ __global__ void __launch_bounds__(VH_TPB) k_mask_finish(const int32_t *colcount,
 }
 
 void vh_launch_mask_stats(vh_batch *b) {
-    hipStream_t st = b->ctx->stream;
+    hipStream_t st = b->stream;
     HIP_TRY(hipMemsetAsync(b->d_rowany, 0, b->nb * b->R, st));
     HIP_TRY(hipMemsetAsync(b->d_colany, 0, b->nb * b->C, st));
     HIP_TRY(hipMemsetAsync(b->d_sliceany, 0, b->nb * b->Z, st));
@@ -732,7 +732,7 @@ void vh_launch_border(vh_batch *b, const uint8_t *d_in, uint8_t *d_out) {
     int tz; dim3 grid; size_t lds;
     tile_geometry(b, false, tz, grid, lds);
     ScopedKTimer tm(b, "border", 2.0 * (double)b->V);
-    k_tile<false, false><<<grid, VH_TPB, lds, b->ctx->stream>>>(nullptr, b->d_mask, d_in, b->d_sc, 0.f,
+    k_tile<false, false><<<grid, VH_TPB, lds, b->stream>>>(nullptr, b->d_mask, d_in, b->d_sc, 0.f,
                                                          b->R, b->C, b->Z, b->V, tz, nullptr,
                                                          d_out, nullptr, nullptr);
     VH_CHECK_LAUNCH();
@@ -1085,7 +1085,7 @@ __global__ void k_snr_finish(const double *part, int64_t nparts, int64_t nb, Vol
 }
 
 void vh_launch_snr(vh_batch *b) {
-    hipStream_t st = b->ctx->stream;
+    hipStream_t st = b->stream;
     const int64_t nparts = (b->CZ + VH_TPB - 1) / VH_TPB;
     ScopedKTimer tm(b, "snr", 5.0 * (double)b->V);
     k_snr<<<col_grid(b), VH_TPB, 0, st>>>(
@@ -1100,7 +1100,7 @@ void vh_launch_snr(vh_batch *b) {
 // the chain
 // =============================================================================================
 void vh_launch_vdp_chain(vh_batch *b, const float *d_n4, const vh_run_opts &o) {
-    hipStream_t st = b->ctx->stream;
+    hipStream_t st = b->stream;
     const int64_t CZ = b->CZ;
     {
         ScopedKTimer tm(b, "gather", 5.0 * (double)b->V);

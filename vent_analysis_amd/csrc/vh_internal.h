@@ -5,6 +5,7 @@
 #include <cstdint>
 #include <cstdio>
 #include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -87,16 +88,21 @@ struct KTimer {
 
 struct vh_ctx {
     int device = 0;
-    hipStream_t stream = nullptr;
     std::string last_error;
     void *comm = nullptr;           // ncclComm_t
     int nranks = 1, rank = 0;
     // pinned scratch for small readbacks
     int32_t *h_pinned = nullptr;
+    // the host-buffer entry points (vh_n4, vh_vdp, ...) share one cached scratch batch per
+    // context; mu serialises them, so a context may be used from several host threads
+    vh_batch *scratch = nullptr;
+    std::mutex mu;
 };
 
 struct vh_batch {
     vh_ctx *ctx = nullptr;
+    hipStream_t stream = nullptr;    // every launch and copy of this batch (batches overlap)
+    int32_t *h_flags = nullptr;      // pinned: the sweep driver's per-iteration active counts
     int64_t R = 0, C = 0, Z = 0, V = 0, nb = 0, CZ = 0;
     int64_t max_tiles = 0;
     // inputs / outputs
@@ -155,6 +161,13 @@ struct vh_batch {
     int32_t *d_ci_shell = nullptr;   // [nb][V]
     uint32_t *d_ci_hist = nullptr;   // [nb][ci_nb]
     int64_t ci_nb_cap = 0;
+    int32_t *d_ci_offL = nullptr;    // [ci_rows_cap] linear sphere-table offsets
+    int64_t ci_rows_cap = 0;
+    int32_t *d_ci_bounds = nullptr;  // [ci_nb_cap]
+    double *d_ci_radii = nullptr;    // [ci_nb_cap]
+    int32_t *d_ci_status = nullptr;  // [nb]
+    unsigned long long *d_ci_count = nullptr;   // [nb]
+    double *d_ci_map = nullptr;      // [nb][V] float64 CI map (vh_ci)
     int64_t n4_subbatch = 0;         // volumes per N4 sub-batch (0 = whole batch)
     int32_t n4_mode = 0;             // vh_run_opts.n4_mode
     bool n4_used_study = false;      // the last N4 ran the volume-resident kernel
