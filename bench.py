@@ -68,7 +68,7 @@ def cpu_baseline(R, C, Z, seconds=15.0, procs=16):
 # ------------------------------------------------------------------------------------------------
 # algorithmic bytes per kernel class (DESIGN.md "Roofline accounting")
 # ------------------------------------------------------------------------------------------------
-def algorithmic_bytes(name, hp, mk, res, R, C, Z, study=True):
+def algorithmic_bytes(name, hp, mk, res, R, C, Z, study=True, conv_mode=0):
     """Total algorithmic HBM bytes moved by all launches of kernel class ``name`` in one step.
 
     N4 state is compact (mask == 1 voxels only, DESIGN.md "HBM layout"), so the per-unit figures
@@ -85,14 +85,17 @@ def algorithmic_bytes(name, hp, mk, res, R, C, Z, study=True):
     vr = np.maximum(hi - lo + 1, 0).sum(axis=1).astype(np.float64)   # voxels in column ranges
     iters = np.array([sum(r.n4_iters[:4]) for r in res], np.float64)
     levels = np.array([sum(1 for k in range(4) if r.n4_iters[k] > 0) for r in res], np.float64)
-    if name == "n4_eval":        # read ridx + L0 + B_old, write B_new + U
-        return float(np.sum(iters * 20.0 * vm))
+    if name == "n4_eval":        # read ridx + L0 + T windows, write U (+ d)
+        return float(np.sum(iters * (12.0 + cw / 2) * vm))
     if name == "n4_fit":         # read ridx + U
         return float(np.sum(iters * 8.0 * vm))
     if name == "n4_hist":        # read U
         return float(np.sum(iters * 4.0 * vm))
+    cw = 8.0 if conv_mode == 0 else 0.0   # S7: eval writes d (raster order), the recurrence reads it
     if name == "n4_study":       # init: read I, write L0 + U; per iteration: hist reads U, fit
-        return float(np.sum(iters * 16.0 * vm + 12.0 * vm))   # reads U, eval reads L0 + writes U
+        return float(np.sum(iters * (16.0 + cw) * vm + 12.0 * vm))   # reads U, eval L0 in, U out
+    if name == "n4_welford":     # read d
+        return float(np.sum(iters * 4.0 * vm))
     if name == "n4_den":         # read ridx, once per level
         return float(np.sum(levels * 4.0 * vm))
     if name == "n4_init":        # row masks / offsets from the column bitmaps (+ the sweep
@@ -165,6 +168,9 @@ def main():
                     help="N4 driver: per-iteration sweeps or one workgroup per study")
     ap.add_argument("--morph3d", action="store_true",
                     help="build-defined 3-D median / border (BASELINE config 5)")
+    ap.add_argument("--conv-mode", type=int, default=0, choices=[0, 1],
+                    help="N4 convergence measure: 0 ITK's float Welford recurrence (SimpleITK "
+                         "semantics, default), 1 exact CoV (faster, different iteration counts)")
     ap.add_argument("--conv-threshold", type=float, default=0.001,
                     help="N4 convergence threshold (SimpleITK default 0.001; 0 = fixed 4x50 "
                          "iterations, for kernel A/B runs at constant work)")
@@ -198,10 +204,10 @@ def main():
     opts = Bt.options(do_n4=not args.no_n4, vox=vox, do_cohort=True,
                       profile=not args.no_profile, n4_subbatch=args.subbatch,
                       conv_threshold=args.conv_threshold, morph3d=args.morph3d,
-                      n4_mode=args.n4_mode)
+                      n4_mode=args.n4_mode, conv_mode=args.conv_mode)
     warm = Bt.options(do_n4=not args.no_n4, vox=vox, do_cohort=True, profile=False,
                       n4_subbatch=args.subbatch, conv_threshold=args.conv_threshold,
-                      morph3d=args.morph3d, n4_mode=args.n4_mode)
+                      morph3d=args.morph3d, n4_mode=args.n4_mode, conv_mode=args.conv_mode)
 
     def step(o):
         Bt.run(o)
@@ -240,7 +246,8 @@ def main():
             if n:
                 kernels[name] = {"ms_total": ms, "launches": n,
                                  "alg_bytes": algorithmic_bytes(name, hp, mk, res, R, C, Z,
-                                                                study=used_study) * args.steps}
+                                                                study=used_study,
+                                                                conv_mode=args.conv_mode) * args.steps}
     roof = None
     if kernels:
         dom = max(kernels, key=lambda k: kernels[k]["ms_total"])

@@ -210,9 +210,18 @@ def kmeans_1d_sorted(s: np.ndarray, k: int = 4, max_iter: int = 300):
         newcuts = np.empty(k + 1, np.int64)
         newcuts[0], newcuts[k] = 0, n
         for j in range(k - 1):
-            d_lo = np.abs(x - c[j])
-            d_hi = np.abs(x - c[j + 1])
-            newcuts[j + 1] = np.searchsorted((d_hi < d_lo).astype(np.int8), 1, side="left")
+            # np.searchsorted((|x - c[j+1]| < |x - c[j]|).astype(int8), 1, side="left"), with the
+            # predicate evaluated only at the midpoints numpy's binary search visits (same result,
+            # O(log n) instead of two full passes per boundary)
+            lo_c, hi_c = c[j], c[j + 1]
+            lo, hi = 0, n
+            while lo < hi:
+                mid = lo + ((hi - lo) >> 1)
+                if not (abs(x[mid] - hi_c) < abs(x[mid] - lo_c)):
+                    lo = mid + 1
+                else:
+                    hi = mid
+            newcuts[j + 1] = lo
         newcuts[1:k] = np.maximum.accumulate(newcuts[1:k])
         if cuts is not None and np.array_equal(newcuts, cuts):
             break

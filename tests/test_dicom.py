@@ -159,6 +159,9 @@ def test_errors_and_pixel_variants(tmp_path):
     write_xenon(tmp_path / "nogroups.dcm", vol, (1.5, 1.5, 10.0), groups=False)
     with pytest.raises(ValueError, match="PixelSpacing"):
         ingest.header_metadata(dicom.dcmread(tmp_path / "nogroups.dcm"))
+    # ... but the patient/study fields are still available (the reference stores them first)
+    info = ingest.header_info(dicom.dcmread(tmp_path / "nogroups.dcm"))
+    assert info["PatientName"] == "Doe^Jane" and info["StudyDate"] == "20240131"
     # signed 12-bit stored in 16: sign extension like pydicom's numpy handler
     ds = dicom.Dataset()
     vals = np.array([[0x0FFF, 0x0800], [0x07FF, 0x0001]], np.uint16)   # -1, -2048, 2047, 1
@@ -208,3 +211,15 @@ def test_dicom_study_matches_array_path(tmp_path):
     assert np.array_equal(a.defectArray, b.defectArray)
     for k in ("VDP", "VDP_lb", "VDP_km", "SNR", "LungVolume", "DefectVolume"):
         assert a.metadata[k] == b.metadata[k], k
+
+
+def test_load_study_mask_validation(tmp_path):
+    """Non-binary or empty masks raise instead of silently becoming empty studies."""
+    vol, mk = synth_study(seed=4)
+    write_xenon(tmp_path / "xe.dcm", vol, (2.0, 2.0, 11.5))
+    write_mask_folder(tmp_path / "m255", (mk * 255).astype(mk.dtype))
+    with pytest.raises(ValueError, match="0/1"):
+        ingest.load_study(tmp_path / "xe.dcm", tmp_path / "m255")
+    write_mask_folder(tmp_path / "m0", np.zeros_like(mk))
+    with pytest.raises(ValueError, match="no mask voxels"):
+        ingest.load_study(tmp_path / "xe.dcm", tmp_path / "m0")

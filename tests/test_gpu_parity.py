@@ -409,6 +409,26 @@ def test_config5_512_cubed_n4_morph3d():
     assert res[0].vdp == ref["VDP"] and res[0].vdp_lb == ref["VDP_lb"]
 
 
+@pytest.mark.parametrize("shape", [(256, 256, 256), (192, 160, 96)])
+def test_n4_sweep_rerun_bit_identical(shape):
+    """Re-running one batch gives bit-identical fields, iteration counts and convergence values
+    (the sweep driver's multi-workgroup eval once scattered the convergence input across lines
+    shared by workgroups; 256^3 lost ~1e4 values per iteration run-to-run)."""
+    X, M = synth_volume(*shape, 11)
+    B = _lib.Batch(*shape, 1)
+    B.upload(X[None], M.astype(np.uint8)[None])
+    o = B.options(do_n4=True, vox=(1.0, 1.0, 1.0), n4_mode="sweep", do_snr=False, do_kmeans=False)
+    outs = []
+    for _ in range(3):
+        B.run(o)
+        n4, _, _, _, res = B.download(n4=True, maps=False)
+        outs.append((n4[0].copy(), list(res[0].n4_iters[:4]), [float(c) for c in res[0].n4_conv[:4]]))
+    B.close()
+    for n4, its, conv in outs[1:]:
+        assert its == outs[0][1] and conv == outs[0][2]
+        assert np.array_equal(n4, outs[0][0])
+
+
 # ---- volume-resident N4 driver (one workgroup per study) ------------------------------------------
 def _run_batch(hp, mk, mode, **kw):
     R, C, Z = hp.shape[1:]

@@ -125,8 +125,8 @@ class Vent_Analysis:
 
     def pullDICOMHeader(self):
         """Vent_Analysis.py:198-223: patient/study elements into metadata, vox from the header."""
-        meta, self.vox = ingest.header_metadata(self.ds)
-        self.metadata.update(meta)
+        self.metadata.update(ingest.header_info(self.ds))   # stored before the spacing lookup
+        self.vox = ingest.header_vox(self.ds)
         self.metadata['LungVolume'] = np.sum(self.mask == 1) * np.prod(np.divide(self.vox, 10)) / 1000
 
     # ---- hot path ---------------------------------------------------------------------------

@@ -214,6 +214,7 @@ void vh_ensure_n4_workspace(vh_batch *b, const vh_n4_params &prm) {
         HIP_TRY(hipMalloc(&b->d_L0, sizeof(float) * b->nb * b->VS));
         HIP_TRY(hipMalloc(&b->d_U, sizeof(float) * b->nb * b->VS));
         HIP_TRY(hipMalloc(&b->d_D, sizeof(float) * b->nb * b->VS));
+        HIP_TRY(hipMalloc(&b->d_perm, sizeof(int32_t) * b->nb * b->VS));
         HIP_TRY(hipMalloc(&b->d_ridx, sizeof(int32_t) * b->nb * b->VS));
         HIP_TRY(hipMalloc(&b->d_cp, sizeof(int32_t) * (b->nb + 1)));
         HIP_TRY(hipMalloc(&b->d_cvol, sizeof(int32_t) * nch));
@@ -402,8 +403,9 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_rowscan(int32_t *rs, int64_t n) {
 // Raster rank of the first masked voxel of every (tile, row): masked voxels before row x plus
 // those of row x in tiles before t -- the position of the voxel in ITK's raster-order scans (the
 // convergence recurrence S7).  One block per volume; dynamic LDS holds the R row totals.
-__global__ void __launch_bounds__(VH_TPB) k_n4_rrank(const uint64_t *rowmask, int64_t R,
-                                                    int64_t ntiles, int32_t *rrank) {
+__global__ void __launch_bounds__(VH_TPB) k_n4_rrank(const uint64_t *rowmask, const int32_t *rowstart,
+                                                    int64_t R, int64_t ntiles, int64_t VS,
+                                                    int32_t *rrank, int32_t *perm) {
     extern __shared__ int32_t s_rowtot[];   // [R]
     __shared__ int32_t s_part[VH_TPB];
     const int64_t b = blockIdx.x;
@@ -433,9 +435,20 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_rrank(const uint64_t *rowmask, in
     int32_t run = s_part[t];
     for (int64_t i = s0; i < e0; ++i) { const int32_t v = s_rowtot[i]; s_rowtot[i] = run; run += v; }
     __syncthreads();
+    // perm (raster rank -> compact index) for the sweep driver's convergence walk.  Written by
+    // this one workgroup only: the multi-workgroup eval writes its differences in compact order
+    // (whole lines per workgroup, like U) instead of scattering them to raster ranks.
+    const int32_t *rs = rowstart + b * ntiles * R;
+    int32_t *pm = perm + b * VS;
     for (int64_t x = threadIdx.x; x < R; x += VH_TPB) {
         const int32_t base = s_rowtot[x];
-        for (int64_t tt = 0; tt < ntiles; ++tt) rr[tt * R + x] += base;
+        for (int64_t tt = 0; tt < ntiles; ++tt) {
+            const int32_t r0 = rr[tt * R + x] + base;
+            rr[tt * R + x] = r0;
+            uint64_t m = rm[tt * R + x];
+            const int32_t c0 = rs[tt * R + x];
+            for (int32_t i = 0; m; ++i, m &= m - 1ull) pm[r0 + i] = c0 + i;
+        }
     }
 }
 
@@ -854,10 +867,10 @@ __global__ void __launch_bounds__(FIT_WAVES * 64) k_n4_fit_items(
     if (MODE == 0) {
         const float bmin = st[b].bin_min;
         const double rinv = 1.0 / (double)st[b].slope;
-        fit_item<0>(it, T, lv.wk3, reinterpret_cast<const double2 *>(lv.ax[0].w3i), ncy, ncz, Z,
+        fit_item<0, false>(it, T, lv.wk3, reinterpret_cast<const double2 *>(lv.ax[0].w3i), ncy, ncz, Z,
                     bins, U + b * VS, n, sE, bmin, rinv, rg, nbmax, nf);
     } else {
-        fit_item<1>(it, T, lv.wk2, reinterpret_cast<const double2 *>(lv.ax[0].w2), ncy, ncz, Z,
+        fit_item<1, false>(it, T, lv.wk2, reinterpret_cast<const double2 *>(lv.ax[0].w2), ncy, ncz, Z,
                     bins, U + b * VS, n, sE, 0.0f, 1.0, rg, nbmax, nf);
     }
 }
@@ -951,8 +964,7 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_eval(const float *__restrict__ L0
                                                    int64_t tbuf, int64_t tcap, DevLevel lv,
                                                    DevLevel lvo, int bo_mode, N4State *st,
                                                    double *part, int32_t c0, int conv_mode,
-                                                   const uint64_t *rmask, const int32_t *rrank,
-                                                   int64_t ntiles, float *D) {
+                                                   float *D) {
     extern __shared__ __attribute__((aligned(16))) float4 sW[];   // [R] new, [R] old, then bases
     __shared__ double s_sd[VH_TPB / 64], s_sd2[VH_TPB / 64];
     __shared__ uint32_t s_max[VH_TPB / 64], s_min[VH_TPB / 64];
@@ -975,6 +987,7 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_eval(const float *__restrict__ L0
     const int first = f < 0 ? -1 : (int)(((f / CZ) << rsh) | (f % CZ));
     const float *Lb = L0 + b * VS + j0;
     float *Ub = U + b * VS + j0;
+    float *Db = D + b * VS + j0;
     const int32_t *Rb = ridx + b * VS + j0;
     const int tl = st[b].tlast;
     const __amdgpu_buffer_rsrc_t rTn = __builtin_amdgcn_make_buffer_rsrc(
@@ -1026,11 +1039,8 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_eval(const float *__restrict__ L0
             }
             const float u = la[h + k] - bn;
             Ub[j] = u;
-            if (conv_mode == 0) {   // S7 input: the field difference at the voxel's raster rank
-                const int64_t col = r & cmask, tl = col >> 6;
-                const int64_t e = (b * ntiles + tl) * R + x;
-                const uint64_t m = rmask[e];
-                D[b * VS + rrank[e] + __popcll(m & ((1ull << (col & 63)) - 1ull))] = bo - bn;
+            if (conv_mode == 0) {   // S7 input: the field difference, compact order (like U)
+                Db[j] = bo - bn;
             } else {                // S7x
                 const double d = (double)expm1c(bo - bn);
                 sd += d;
@@ -1073,9 +1083,10 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_eval(const float *__restrict__ L0
 }
 
 // S7: ITK's float Welford convergence of the last eval of each active volume (two waves per
-// volume: n4_shared.h chain_wave_mu / chain_wave_sig over the raster-ordered field differences).
-__global__ void __launch_bounds__(128) k_n4_welford(const float *D, int64_t VS, const VolScalars *sc,
-                                                   N4State *st, int64_t vol0) {
+// volume: n4_shared.h chain_wave_mu / chain_wave_sig over the field differences, read in raster
+// order through the volume's raster -> compact permutation).
+__global__ void __launch_bounds__(128) k_n4_welford(const float *D, const int32_t *perm, int64_t VS,
+                                                   const VolScalars *sc, N4State *st, int64_t vol0) {
     __shared__ ChainSlot slots[CH_SLOTS];
     __shared__ ChainState cs;
     const int64_t b = vol0 + blockIdx.x;
@@ -1086,7 +1097,7 @@ __global__ void __launch_bounds__(128) k_n4_welford(const float *D, int64_t VS, 
     }
     __syncthreads();
     const int64_t n = sc[b].n_mask1;
-    if (threadIdx.x < 64) chain_wave_mu(D + b * VS, n, slots, &cs);
+    if (threadIdx.x < 64) chain_wave_mu(D + b * VS, perm + b * VS, n, slots, &cs);
     else chain_wave_sig(n, slots, &cs);
     __syncthreads();
     if (threadIdx.x == 0) st[b].conv_w = cs.conv;
@@ -1209,6 +1220,26 @@ static int fit_rowcap(const vh_batch *b, const vh_n4_params &prm, int L) {
     return cap;
 }
 
+// VH_N4_TRACE (diagnostics): per iteration, hashes of volume vol0's U and D and its conv_w
+static void n4_trace(vh_batch *b, int64_t vol0, int L, int it) {
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    VolScalars sc;
+    N4State s;
+    HIP_TRY(hipMemcpy(&sc, b->d_sc + vol0, sizeof(sc), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(&s, b->d_st + vol0, sizeof(s), hipMemcpyDeviceToHost));
+    const int64_t n = sc.n_mask1;
+    std::vector<uint32_t> h((size_t)n);
+    auto fnv = [&](const float *dp) {
+        HIP_TRY(hipMemcpy(h.data(), dp + vol0 * b->VS, 4 * (size_t)n, hipMemcpyDeviceToHost));
+        uint64_t x = 1469598103934665603ull;
+        for (int64_t i = 0; i < n; ++i) x = (x ^ h[(size_t)i]) * 1099511628211ull;
+        return x;
+    };
+    const uint64_t hu = fnv(b->d_U), hd = fnv(b->d_D);
+    fprintf(stderr, "N4TRACE L%d it%d active %d U %016llx D %016llx conv_w %.9g\n", L, it, s.active,
+            (unsigned long long)hu, (unsigned long long)hd, s.conv_w);
+}
+
 // One sub-batch [vol0, vol0 + ns): the whole multi-level loop.  Flat sweeps run over the chunk
 // range [cp[vol0], cp[vol0 + ns]); converged volumes' blocks exit at once.
 static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int64_t ns,
@@ -1226,6 +1257,7 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
     const dim3 fg((unsigned)((nitems + FIT_WAVES - 1) / FIT_WAVES), (unsigned)ns);
     float *U = b->d_U;
     std::vector<hipEvent_t> evs;
+    std::vector<int> ev_slot;   // iteration slot (d_nactive / h_flags index) behind each event
     if (!b->h_flags) HIP_TRY(hipHostMalloc((void **)&b->h_flags, sizeof(int32_t) * 1024));
     int32_t *hflag = b->h_flags;
     int total_iters = 0;
@@ -1276,6 +1308,7 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
                 hipEvent_t ev;
                 HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
                 evs.push_back(ev);
+                ev_slot.push_back(gi);
                 HIP_TRY(hipEventRecord(ev, st));
                 if (nch > 0) {
                     ScopedKTimer tm(b, "n4_hist", 0.0);
@@ -1316,18 +1349,21 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
                     k_n4_eval<<<(unsigned)nch, VH_TPB, (size_t)b->R * 40, st>>>(
                         b->d_L0, U, b->d_ridx, b->d_cp, b->d_cvol, b->d_sc, b->R, b->CZ, b->VS, rsh,
                         b->d_T, b->nb * b->t_cap, b->t_cap, lv, lvo, bo_mode, b->d_st, b->d_cpart,
-                        ch0, cm, b->d_rowmask, b->d_rrank, ntiles, b->d_D);
+                        ch0, cm, b->d_D);
                     VH_CHECK_LAUNCH();
                 }
                 if (cm == 0) {
                     ScopedKTimer tm(b, "n4_welford", 0.0);
-                    k_n4_welford<<<(unsigned)ns, 128, 0, st>>>(b->d_D, b->VS, b->d_sc, b->d_st, vol0);
+                    k_n4_welford<<<(unsigned)ns, 128, 0, st>>>(b->d_D, b->d_perm, b->VS, b->d_sc,
+                                                               b->d_st, vol0);
                     VH_CHECK_LAUNCH();
                 }
+                if (getenv("VH_N4_TRACE")) n4_trace(b, vol0, L, it);
                 const int k = (int)evs.size() - 1 - LOOK;
                 if (k >= level_start) {
                     HIP_TRY(hipEventSynchronize(evs[k]));
-                    if (hflag[(gi - LOOK) % 1024] == 0) { ++gi; break; }
+                    // the flag the event covers (slots skip one per early exit: gi != event index)
+                    if (hflag[ev_slot[k] % 1024] == 0) { ++gi; break; }
                 }
             }
             k_n4_level_end<<<(unsigned)ns, 64, 0, st>>>(b->d_st, b->d_cpart, b->d_cp, b->d_sc, cm, L,
@@ -1364,7 +1400,7 @@ void vh_launch_n4(vh_batch *b, const vh_n4_params &prm) {
         VH_CHECK_LAUNCH();
         if (b->R > 16384) throw VhError{VH_ERR_ARG, "N4: more than 16384 rows"};
         k_n4_rrank<<<(unsigned)b->nb, VH_TPB, sizeof(int32_t) * (size_t)b->R, st>>>(
-            b->d_rowmask, b->R, ntiles, b->d_rrank);
+            b->d_rowmask, b->d_rowstart, b->R, ntiles, b->VS, b->d_rrank, b->d_perm);
         VH_CHECK_LAUNCH();
     }
     // driver: volume-resident (one workgroup per study) when the batch has studies for the CUs

@@ -236,7 +236,8 @@ struct FitRing {
     int nr, i0;       // rows held, control row of row 0
 };
 
-template <int P>
+// INPLACE (n4_study): one chunk, S overwrites Q; otherwise (n4) chunks into the separate rg.sx.
+template <int P, bool INPLACE>
 __device__ void fit_contract(FitRing &rg, const Item &it, const TabV &T, const double *Wk, int ncy,
                              int ncz, int Z, unsigned long long *numfix) {
     const int nr = rg.nr;
@@ -246,7 +247,7 @@ __device__ void fit_contract(FitRing &rg, const Item &it, const TabV &T, const d
     const int klo = T.bz[it.y0 == it.y1 ? it.z0 : 0];
     const int KT = T.bz[it.y0 == it.y1 ? it.z1 : Z - 1] + 4 - klo;
     const int nyk = it.ny * KT;
-    double *S = rg.sx ? rg.sx : rg.q;
+    double *S = INPLACE ? rg.q : rg.sx;
     for (int o0 = 0; o0 < nr * nyk; o0 += 64 * FIT_SO) {
         // the FIT_SO outputs of a lane are independent fma chains over their slices: walk them in
         // lockstep (step s of every chain together) so the LDS latency of one chain hides behind
@@ -282,12 +283,13 @@ __device__ void fit_contract(FitRing &rg, const Item &it, const TabV &T, const d
                 outv[q] = s < len[q] ? v : outv[q];
             }
         }
-        if (!rg.sx) wave_lds_order();   // in place: every read of the batch before any write
+        if (INPLACE) wave_lds_order();   // in place: every read of the batch before any write
 #pragma unroll
         for (int q = 0; q < FIT_SO; ++q) {
             const int o = o0 + lane + 64 * q;
             if (o < nr * nyk) S[(o / nyk) * rg.rowcap + o % nyk] = outv[q];
         }
+        if (INPLACE) break;   // nbmax keeps a batch within one chunk
     }
     wave_lds_order();
     const int jlo = T.by[it.y0];
@@ -313,21 +315,22 @@ __device__ void fit_contract(FitRing &rg, const Item &it, const TabV &T, const d
 }
 
 // control row i (this lane's value v) is finished: into the ring, contract when the batch is full
-template <int P>
+template <int P, bool INPLACE>
 __device__ __forceinline__ void fit_push(FitRing &rg, double v, int i, const Item &it,
                                          const TabV &T, const double *Wk, int ncy, int ncz, int Z,
                                          unsigned long long *numfix) {
     if (rg.nr == 0) rg.i0 = i;
     rg.q[rg.nr * rg.rowcap + (threadIdx.x & 63)] = v;
-    if (++rg.nr == rg.nbmax) fit_contract<P>(rg, it, T, Wk, ncy, ncz, Z, numfix);
+    if (++rg.nr == rg.nbmax) fit_contract<P, INPLACE>(rg, it, T, Wk, ncy, ncz, Z, numfix);
 }
 
 // rows per contraction batch for this item's geometry
+template <bool INPLACE>
 __device__ __forceinline__ void fit_ring_begin(FitRing &rg, const Item &it, const TabV &T, int Z,
                                                int nb_ring) {
     const int klo = T.bz[it.y0 == it.y1 ? it.z0 : 0];
     const int KT = T.bz[it.y0 == it.y1 ? it.z1 : Z - 1] + 4 - klo;
-    rg.nbmax = rg.sx ? nb_ring : max(1, min(nb_ring, 64 * FIT_SO / (it.ny * KT)));
+    rg.nbmax = INPLACE ? max(1, min(nb_ring, 64 * FIT_SO / (it.ny * KT))) : nb_ring;
     rg.nr = 0;
 }
 
@@ -335,7 +338,7 @@ __device__ __forceinline__ void fit_ring_begin(FitRing &rg, const Item &it, cons
 // [2x], [2x+1]), p = (double)(u - sharpen(u)) * (1/sum wy^2 * 1/sum wz^2); MODE 1: denominator,
 // Wx = wx^2, p = 1.  Each control row's column partial is an fma chain over the item's rows in
 // row order: acc_a = fma(Wx(x, a), p(x), acc_a) for the window's four control rows.
-template <int MODE>
+template <int MODE, bool INPLACE>
 __device__ void fit_item(const Item &it, const TabV &T, const double *Wk, const double2 *Wx,
                          int ncy, int ncz, int Z, int bins, const float *Ub, int64_t n,
                          const float *sE, float bmin, double rinv, FitRing &rg, int nb_ring,
@@ -346,7 +349,7 @@ __device__ void fit_item(const Item &it, const TabV &T, const double *Wk, const 
     int wb = T.bx[it.xs];
     double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0, acc3 = 0.0;
     int x = it.xs, tail = 0;
-    fit_ring_begin(rg, it, T, Z, nb_ring);
+    fit_ring_begin<INPLACE>(rg, it, T, Z, nb_ring);
 #pragma unroll 1
     for (;;) {
         if (x <= it.xe) {   // rows of control span wb: the window does not move
@@ -383,12 +386,12 @@ __device__ void fit_item(const Item &it, const TabV &T, const double *Wk, const 
             }
             x = rb + 1 > x ? rb + 1 : x;
         }
-        fit_push<P>(rg, acc0, wb, it, T, Wk, ncy, ncz, Z, numfix);   // control row wb is done
+        fit_push<P, INPLACE>(rg, acc0, wb, it, T, Wk, ncy, ncz, Z, numfix);   // control row wb is done
         acc0 = acc1; acc1 = acc2; acc2 = acc3; acc3 = 0.0;
         ++wb;
         if (x > it.xe && ++tail == 4) break;
     }
-    fit_contract<P>(rg, it, T, Wk, ncy, ncz, Z, numfix);
+    fit_contract<P, INPLACE>(rg, it, T, Wk, ncy, ncz, Z, numfix);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -482,18 +485,27 @@ __device__ __forceinline__ void lds_store_rel(int *p, int v) {
     __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// wave A.  Dr: the n raster-ordered d values of the study (global).
-__device__ void chain_wave_mu(const float *Dr, int64_t n, ChainSlot *slots, ChainState *cs) {
+// wave A.  The n d values in raster order: Dr[k] (perm == nullptr), else Dr[perm[k]].  The
+// next block's values are loaded before lane 0 runs this block's steps (the loads overlap the
+// serial chain).
+__device__ __forceinline__ float chain_load(const float *Dr, const int32_t *perm, int64_t j, int64_t n) {
+    if (j >= n) return 0.0f;
+    return perm ? Dr[perm[j]] : Dr[j];
+}
+
+__device__ void chain_wave_mu(const float *Dr, const int32_t *perm, int64_t n, ChainSlot *slots,
+                              ChainState *cs) {
     const int lane = threadIdx.x & 63;
     double mu = 0.0;
     const int64_t nblk = (n + 63) / 64;
+    float dnext = chain_load(Dr, perm, lane, n);
     for (int64_t blk = 0; blk < nblk; ++blk) {
         ChainSlot &S = slots[blk % CH_SLOTS];
+        const int64_t j = blk * 64 + lane;
+        const float d = dnext;
+        dnext = chain_load(Dr, perm, j + 64, n);
         if (blk >= CH_SLOTS)
             while (lds_load_acq(&cs->b_done) <= (int)(blk - CH_SLOTS)) __builtin_amdgcn_s_sleep(1);
-        const int64_t j = blk * 64 + lane;
-        const bool ok = j < n;
-        const float d = ok ? Dr[j] : 0.0f;
         const float p = expf_cr(d);
         const double kd = (double)(j + 1);
         const double r = 1.0 / kd;

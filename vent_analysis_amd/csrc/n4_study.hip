@@ -33,6 +33,14 @@
 #define ST_HC 8        // LDS histogram copies
 #define ST_MAX_LDS (160 * 1024)
 
+// ST_PROF builds (scripts/dev/phase_ab.sh): block 0 prints shader cycles per phase at the end
+#ifdef ST_PROF
+#define ST_MARK(k) do { if (threadIdx.x == 0) { const unsigned long long _c = clock64(); \
+    st_prof[k] += _c - st_t0; st_t0 = _c; } } while (0)
+#else
+#define ST_MARK(k) do { } while (0)
+#endif
+
 struct StudyLevels {
     DevLevel lv[VH_MAX_LEVELS];
     int32_t max_iters[VH_MAX_LEVELS];
@@ -562,6 +570,9 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
         for (int e = t; e < nl0; e += ST_TPB) lat[e] = 0.0f;
     }
     int cur = 0;   // P1b[cur] holds the last evaluated field
+#ifdef ST_PROF
+    unsigned long long st_prof[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_t0 = clock64();
+#endif
     for (int L = 0; L < a.nlev; ++L) {
         const DevLevel &lv = a.lvs->lv[L];
         char *tabp = smem + ((L & 1) ? a.o_tab1 : a.o_tab0);
@@ -597,10 +608,11 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
             if (item < 0) break;
             Item it;
             if (!study_item(it, a, b, item)) continue;
-            fit_item<1>(it, T, Wk2, Wx2, ncy, ncz, a.Z, bins, Ub, n, sE, 0.0f, 1.0, ring, a.nb_ring,
+            fit_item<1, true>(it, T, Wk2, Wx2, ncy, ncz, a.Z, bins, Ub, n, sE, 0.0f, 1.0, ring, a.nb_ring,
                         numfix);
         }
         __syncthreads();
+        ST_MARK(0);
         for (int e = t; e < nlat; e += ST_TPB) den[e] = fix128_get(numfix + 2 * e, numfix + 2 * e + 1);
         // ---- iterations ----
         int itn = 0;
@@ -643,6 +655,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                 }
             }
             __syncthreads();
+            ST_MARK(1);
             if (M.stop) break;
             if (M.exact) {
                 float *s_cmax = reinterpret_cast<float *>(scr);
@@ -654,6 +667,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                 __syncthreads();
             }
             ++itn;
+            ST_MARK(1);
             const float bmin = M.bin_min, slope = M.slope;
             const double rinv = 1.0 / (double)slope;   // div_r form of the bin division
             // ---- hist (S3): one packed 64-bit add per value ----
@@ -682,6 +696,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                 }
             }
             __syncthreads();
+            ST_MARK(2);
             // ---- emap (same arithmetic as n4.hip k_n4_emap and the oracle) ----
             {
                 const int P = VH_FFT_P, off = (P - bins) / 2;
@@ -748,6 +763,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                 }
                 __syncthreads();
             }
+            ST_MARK(3);
             // ---- fit ----
             for (int e = t; e < 2 * nlat; e += ST_TPB) numfix[e] = 0ull;
             if (t == 0) M.item_ctr = 0;
@@ -757,10 +773,11 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                 if (item < 0) break;
                 Item it;
                 if (!study_item(it, a, b, item)) continue;
-                fit_item<0>(it, T, Wk3, Wx3, ncy, ncz, a.Z, bins, Ub, n, sE, bmin, rinv, ring,
+                fit_item<0, true>(it, T, Wk3, Wx3, ncy, ncz, a.Z, bins, Ub, n, sE, bmin, rinv, ring,
                             a.nb_ring, numfix);
             }
             __syncthreads();
+            ST_MARK(4);
             // ---- lattice update and P1 ----
             for (int e = t; e < nlat; e += ST_TPB) {
                 const double d = den[e];
@@ -780,6 +797,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
             }
             if (t == 0) M.item_ctr = 0;
             __syncthreads();
+            ST_MARK(5);
             // ---- eval ----
             {
                 const bool first_of_level = itn == 1;
@@ -818,9 +836,10 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                 M.ch.b_done = 0;
             }
             __syncthreads();
+            ST_MARK(6);
             // ---- convergence of this iteration ----
             if (a.conv_mode == 0) {   // S7: ITK's float Welford recurrence, two waves
-                if (wv == 0) chain_wave_mu(Db, n, slots, &M.ch);
+                if (wv == 0) chain_wave_mu(Db, nullptr, n, slots, &M.ch);
                 else if (wv == 1) chain_wave_sig(n, slots, &M.ch);
             } else if (wv == 0) {   // S7x: item partials in item order
                 double sd = 0.0, sd2 = 0.0;
@@ -838,6 +857,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                 }
             }
             cur ^= 1;
+            ST_MARK(7);
         }
         if (t == 0) {
             stb->iters_level[L] = itn;
@@ -853,7 +873,14 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
             refine_axis_st(T2, lat, 2 * ncx - 3, 2 * ncy - 3, ncz, 2);
             __syncthreads();
         }
+        ST_MARK(8);
     }
+#ifdef ST_PROF
+    if (t == 0 && blockIdx.x == 0)
+        printf("ST_PROF den %llu ctrl %llu hist %llu emap %llu fit %llu latP1 %llu eval %llu "
+               "conv %llu level %llu\n", st_prof[0], st_prof[1], st_prof[2], st_prof[3], st_prof[4],
+               st_prof[5], st_prof[6], st_prof[7], st_prof[8]);
+#endif
     // final field's P1 for k_n4_final
     const double *P1f = cur ? P1b1 : P1b0;
     for (int e = t; e < p1last; e += ST_TPB) a.P1out[b * a.q2cap + e] = P1f[e];

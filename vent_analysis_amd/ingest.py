@@ -7,14 +7,18 @@ Restates the reference's loaders (Vent_Analysis.py:169-223) on top of ``vent_ana
   *view*; batch loading makes it contiguous once (the C-ABI needs C-order).
 * ``open_dicom_folder``  -- :184-196: every ``*.dcm`` of the folder in sorted name order, one
   slice each, stacked on the last axis as float64 (the reference's ``np.zeros`` dtype).
-* ``header_metadata``    -- :198-223: the patient/study elements (missing ones -> ''), and
-  vox = [PixelSpacing of the first per-frame functional group that has one, SpacingBetweenSlices].
-  Where the reference prompts on stdin for a missing spacing this raises ValueError instead.
+* ``header_info`` / ``header_vox`` / ``header_metadata`` -- :198-223: the patient/study elements
+  (missing ones -> ''), and vox = [PixelSpacing of the first per-frame functional group that has
+  one, SpacingBetweenSlices].  Where the reference prompts on stdin for a missing spacing
+  ``header_vox`` raises ValueError instead; the info elements are read separately first, as the
+  reference stores them before it looks at the spacing (:200-206).
 * ``load_study`` / ``load_batch`` -- one study or many into the (B, R, C, Z) float32 / uint8
   arrays ``_lib.Batch.upload`` takes, plus vox and the metadata; files are parsed on a thread pool.
 
-The mask is handed to the device as ``mask == 1`` (uint8), the voxel set every mask use in the
-reference selects (the chain multiplies by the 0/1 mask; N4 uses MaskLabel 1).
+The mask must be binary (0/1, as ``Vent_Analysis._binary_u8`` demands for the class path) and
+non-empty; it is handed to the device as uint8.  Other label values raise ValueError rather than
+silently becoming an empty study (the reference's chain selects mask > 0 at :245 while N4 uses
+MaskLabel 1 -- the two agree only for binary masks, the case the GPU path implements).
 """
 from __future__ import annotations
 
@@ -26,8 +30,8 @@ import numpy as np
 
 from .dicom import dcmread
 
-__all__ = ["open_single_dicom", "open_dicom_folder", "header_metadata", "Study", "load_study",
-           "load_batch"]
+__all__ = ["open_single_dicom", "open_dicom_folder", "header_info", "header_vox",
+           "header_metadata", "Study", "load_study", "load_batch"]
 
 INFO_ELEMENTS = ['PatientName', 'PatientAge', 'PatientBirthDate', 'PatientSize', 'PatientWeight',
                  'PatientSex', 'StudyDate', 'StudyTime', 'SeriesTime']
@@ -57,14 +61,20 @@ def open_dicom_folder(folder, workers=8):
     return dss[-1], mask
 
 
-def header_metadata(ds):
-    """(metadata dict, vox) from the xenon header -- Vent_Analysis.py:198-223."""
+def header_info(ds):
+    """The patient/study elements of the xenon header (absent ones -> '') -- Vent_Analysis.py:200-206."""
     meta = {}
     for elem in INFO_ELEMENTS:
         try:
             meta[elem] = ds[elem].value
         except KeyError:
             meta[elem] = ''
+    return meta
+
+
+def header_vox(ds):
+    """vox = [dx, dy, dz] from the xenon header -- Vent_Analysis.py:207-223 (ValueError where the
+    reference prompts on stdin)."""
     spacing = None
     try:
         groups = ds[0x5200, 0x9230]
@@ -84,7 +94,24 @@ def header_metadata(ds):
     except AttributeError:
         raise ValueError("SpacingBetweenSlices missing (the reference prompts for it on stdin, "
                          "Vent_Analysis.py:219-221)") from None
-    return meta, [float(spacing[0]), float(spacing[1]), dz]
+    return [float(spacing[0]), float(spacing[1]), dz]
+
+
+def header_metadata(ds):
+    """(metadata dict, vox) from the xenon header -- Vent_Analysis.py:198-223."""
+    return header_info(ds), header_vox(ds)
+
+
+def binary_mask(mask, what="mask"):
+    """uint8 0/1 copy of a binary mask; ValueError for other labels or an empty mask."""
+    m = np.asarray(mask)
+    u8 = (m != 0).astype(np.uint8)
+    if not np.array_equal(u8, m):
+        raise ValueError(f"{what}: labels other than 0/1 (the GPU path implements binary masks; "
+                         "binarise before loading)")
+    if not u8.any():
+        raise ValueError(f"{what}: no mask voxels")
+    return np.ascontiguousarray(u8)
 
 
 @dataclass
@@ -104,7 +131,7 @@ def load_study(xenon_path, mask_folder, workers=8):
     if mask.shape != hp.shape:
         raise ValueError(f"{xenon_path}: mask shape {mask.shape} != image shape {hp.shape}")
     return Study(hp=np.ascontiguousarray(hp, dtype=np.float32),
-                 mask=np.ascontiguousarray(mask == 1, dtype=np.uint8), vox=vox, metadata=meta,
+                 mask=binary_mask(mask, f"{mask_folder}"), vox=vox, metadata=meta,
                  path=os.fspath(xenon_path))
 
 
