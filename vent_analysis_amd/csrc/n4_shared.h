@@ -457,7 +457,8 @@ __device__ __forceinline__ bool r3_bin_min(const Range3 &r, const float *u, int 
 // S7 convergence (conv_mode 0): ITK's float Welford recurrence over the masked voxels in raster
 // order, d_k = B_old - B_new read from a raster-ordered buffer.  Two waves of one workgroup:
 //   wave A (mu): per block of 64 steps, all lanes compute p = (float)exp((double)d), 1/k, the mu
-//     step constants (1 - 1/k, p/k) and (k-1)/k into an LDS slot; then lane 0 runs
+//     step constants (1 - 1/k, p/k) and (k-1)/k into an LDS slot; then lane 0 runs (pipelined,
+//     chain_block64)
 //       mu <- (float)fma((double)mu, 1 - 1/k, (double)(p / k))      (one step per voxel)
 //     recording mu before each step for wave B.
 //   wave B (sig): per block, all lanes form s = (p - mu_prev)^2 (float); lane 0 runs
@@ -467,9 +468,8 @@ __device__ __forceinline__ bool r3_bin_min(const Range3 &r, const float *u, int 
 // ---------------------------------------------------------------------------------------------
 #define CH_SLOTS 4
 struct ChainSlot {
-    double2 ab[64];    // (1 - 1/k, p / k) for wave A
-    double c[64];      // (k - 1) / k
-    double s[64];      // (double)(p - mu_prev)^2, written by wave B
+    double2 ab[64];    // (1 - 1/k, p / k) for wave A; (1, 0) past the end (a no-op step)
+    double2 cs[64];    // ((k - 1) / k, (double)(p - mu_prev)^2): c by wave A, s by wave B
     float p[64];
     float mu[64];      // mu before step k
 };
@@ -483,6 +483,99 @@ __device__ __forceinline__ int lds_load_acq(int *p) {
 }
 __device__ __forceinline__ void lds_store_rel(int *p, int v) {
     __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// ---- the 64 serial steps of one block on lane 0, software-pipelined -------------------------
+// The step operands are 64 double2 in LDS; they are read in groups of 8 (ds_read_b128), group g+1
+// issued before group g's steps, with an explicit lgkmcnt wait tied to the group's registers (the
+// compiler otherwise batches all reads behind one full wait: ~31 -> ~53 cycles per step measured,
+// scripts/microbench/chain_fast.hip).  MU: x <- (float)fma(x, q.x, q.y), recording x before each
+// step as float (two b128 writes per group at mbase); SIG: x <- (float)fma(q.y, q.x, x).
+// LDS addresses are the low 32 bits of the generic address of a __shared__ object.  The read
+// outputs are early-clobber: a data register that doubled as the address would be overwritten by
+// an early return while later reads of the same statement still use it (seen in n4_study).
+typedef double ch_d2 __attribute__((ext_vector_type(2)));
+typedef float ch_f4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint32_t lds_addr(const void *p) { return (uint32_t)(uintptr_t)p; }
+
+#define CH_RD8(q, base, g)                                                                         \
+    asm volatile("ds_read_b128 %0, %8 offset:%9\n\t"                                               \
+                 "ds_read_b128 %1, %8 offset:%10\n\t"                                              \
+                 "ds_read_b128 %2, %8 offset:%11\n\t"                                              \
+                 "ds_read_b128 %3, %8 offset:%12\n\t"                                              \
+                 "ds_read_b128 %4, %8 offset:%13\n\t"                                              \
+                 "ds_read_b128 %5, %8 offset:%14\n\t"                                              \
+                 "ds_read_b128 %6, %8 offset:%15\n\t"                                              \
+                 "ds_read_b128 %7, %8 offset:%16"                                                  \
+                 : "=&v"(q[0]), "=&v"(q[1]), "=&v"(q[2]), "=&v"(q[3]), "=&v"(q[4]),               \
+                   "=&v"(q[5]), "=&v"(q[6]), "=&v"(q[7])                                           \
+                 : "v"(base), "i"(128 * (g)), "i"(128 * (g) + 16), "i"(128 * (g) + 32),             \
+                   "i"(128 * (g) + 48), "i"(128 * (g) + 64), "i"(128 * (g) + 80),                   \
+                   "i"(128 * (g) + 96), "i"(128 * (g) + 112)                                      \
+                 : "memory")
+
+template <int N>
+__device__ __forceinline__ void ch_wait(ch_d2 *q) {   // N LDS ops may still be in flight
+    asm volatile("s_waitcnt lgkmcnt(%8)"
+                 : "+v"(q[0]), "+v"(q[1]), "+v"(q[2]), "+v"(q[3]), "+v"(q[4]), "+v"(q[5]),
+                   "+v"(q[6]), "+v"(q[7])
+                 : "i"(N)
+                 : "memory");
+}
+
+template <bool MU, int G>
+__device__ __forceinline__ void ch_group(uint32_t base, uint32_t mbase, double &x, ch_d2 *cur,
+                                         ch_d2 *nxt) {
+    if constexpr (G < 7) {
+        CH_RD8(nxt, base, G + 1);
+        ch_wait<(G == 0 || !MU) ? 8 : 10>(cur);   // MU: the previous group's 2 writes follow cur
+    } else {
+        ch_wait<MU ? 2 : 0>(cur);
+    }
+    if constexpr (MU) {
+        float mr[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            mr[i] = (float)x;
+            x = (double)(float)fma(x, cur[i].x, cur[i].y);
+        }
+        const ch_f4 w0 = {mr[0], mr[1], mr[2], mr[3]}, w1 = {mr[4], mr[5], mr[6], mr[7]};
+        asm volatile("ds_write_b128 %0, %1 offset:%3\n\tds_write_b128 %0, %2 offset:%4"
+                     :
+                     : "v"(mbase), "v"(w0), "v"(w1), "i"(32 * G), "i"(32 * G + 16)
+                     : "memory");
+    } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) x = (double)(float)fma(cur[i].y, cur[i].x, x);
+    }
+    if constexpr (G < 7) ch_group<MU, G + 1>(base, mbase, x, nxt, cur);
+}
+
+#ifndef CH_ASM
+#define CH_ASM 1
+#endif
+template <bool MU>
+__device__ __forceinline__ double chain_block64(const double2 *q, float *murec, double x) {
+    if constexpr (!CH_ASM) {   // reference form (A/B builds)
+#pragma unroll 4
+        for (int l = 0; l < 64; ++l) {
+            const double2 v = q[l];
+            if (MU) {
+                murec[l] = (float)x;
+                x = (double)(float)fma(x, v.x, v.y);
+            } else {
+                x = (double)(float)fma(v.y, v.x, x);
+            }
+        }
+        return x;
+    }
+    const uint32_t base = lds_addr(q), mbase = MU ? lds_addr(murec) : 0u;
+    ch_d2 qa[8], qb[8];
+    CH_RD8(qa, base, 0);
+    ch_group<MU, 0>(base, mbase, x, qa, qb);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    return x;
 }
 
 // wave A.  The n d values in raster order: Dr[k] (perm == nullptr), else Dr[perm[k]].  The
@@ -504,24 +597,20 @@ __device__ void chain_wave_mu(const float *Dr, const int32_t *perm, int64_t n, C
         const int64_t j = blk * 64 + lane;
         const float d = dnext;
         dnext = chain_load(Dr, perm, j + 64, n);
-        if (blk >= CH_SLOTS)
-            while (lds_load_acq(&cs->b_done) <= (int)(blk - CH_SLOTS)) __builtin_amdgcn_s_sleep(1);
+        const bool ok = j < n;
         const float p = expf_cr(d);
         const double kd = (double)(j + 1);
         const double r = 1.0 / kd;
-        S.ab[lane] = make_double2(1.0 - r, (double)(float)((double)p * r));   // p / k, div_r form
-        S.c[lane] = (kd - 1.0) / kd;
+        const double2 ab = ok ? make_double2(1.0 - r, (double)(float)((double)p * r))   // p / k, div_r form
+                              : make_double2(1.0, 0.0);
+        const double c = (kd - 1.0) / kd;
+        if (blk >= CH_SLOTS)
+            while (lds_load_acq(&cs->b_done) <= (int)(blk - CH_SLOTS)) __builtin_amdgcn_s_sleep(1);
+        S.ab[lane] = ab;
+        S.cs[lane] = make_double2(c, 0.0);
         S.p[lane] = p;
         wave_lds_order();
-        if (lane == 0) {
-            const int m = (int)min((int64_t)64, n - blk * 64);
-#pragma unroll 4
-            for (int l = 0; l < m; ++l) {
-                const double2 ab = S.ab[l];
-                S.mu[l] = (float)mu;
-                mu = (double)(float)fma(mu, ab.x, ab.y);
-            }
-        }
+        if (lane == 0) mu = chain_block64<true>(S.ab, S.mu, mu);
         wave_lds_order();
         if (lane == 0) {
             if (blk == nblk - 1) cs->mu = (float)mu;   // published by the release below
@@ -530,23 +619,21 @@ __device__ void chain_wave_mu(const float *Dr, const int32_t *perm, int64_t n, C
     }
 }
 
-// wave B.  Returns conv in cs->conv (also the return value on lane 0).
+// wave B.  Returns conv in cs->conv.
 __device__ void chain_wave_sig(int64_t n, ChainSlot *slots, ChainState *cs) {
     const int lane = threadIdx.x & 63;
     double sig = 0.0;
     const int64_t nblk = (n + 63) / 64;
     for (int64_t blk = 0; blk < nblk; ++blk) {
         ChainSlot &S = slots[blk % CH_SLOTS];
+        const int64_t j = blk * 64 + lane;
         while (lds_load_acq(&cs->a_done) <= (int)blk) __builtin_amdgcn_s_sleep(1);
         const float q = S.p[lane] - S.mu[lane];
-        S.s[lane] = (double)(q * q);
+        // k = 1 adds nothing (ITK's N > 1 test), nor do the steps past the end: (0, 0) is a no-op
+        const bool ok = j < n && j > 0;
+        S.cs[lane] = ok ? make_double2(S.cs[lane].x, (double)(q * q)) : make_double2(0.0, 0.0);
         wave_lds_order();
-        if (lane == 0) {
-            const int m = (int)min((int64_t)64, n - blk * 64);
-            int l = blk == 0 ? 1 : 0;   // k = 1 adds nothing (N > 1 test)
-#pragma unroll 4
-            for (; l < m; ++l) sig = (double)(float)fma(S.s[l], S.c[l], sig);
-        }
+        if (lane == 0) sig = chain_block64<false>(S.cs, nullptr, sig);
         wave_lds_order();
         if (lane == 0) lds_store_rel(&cs->b_done, (int)(blk + 1));
     }
