@@ -131,9 +131,56 @@ __device__ __forceinline__ void chain_mu_ring(uint32_t base, uint32_t mbase, dou
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
 
+
+// mode 12: A_k from a global table by scalar loads (8 doubles per s_load_dwordx16), B_k as floats
+// from LDS (4 per ds_read_b128); one lgkmcnt(0) wait per 8-step group, next group's loads in flight
+typedef int sg16 __attribute__((ext_vector_type(16)));
+__device__ __forceinline__ void s_ld16(sg16 &o, const double *p) {
+    asm volatile("s_load_dwordx16 %0, %1, 0x0" : "=s"(o) : "s"(p) : "memory");
+}
+template <int OFF>
+__device__ __forceinline__ void ds_rd2(flt4v &a, flt4v &b, uint32_t base) {
+    asm volatile("ds_read_b128 %0, %2 offset:%3\n\tds_read_b128 %1, %2 offset:%4"
+                 : "=&v"(a), "=&v"(b) : "v"(base), "i"(OFF), "i"(OFF + 16) : "memory");
+}
+__device__ __forceinline__ void wait0(sg16 &a, flt4v &b0, flt4v &b1) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(a), "+v"(b0), "+v"(b1) : : "memory");
+}
+template <int G>
+__device__ __forceinline__ void g12(const double *At, uint32_t bbase, uint32_t mbase, double &x,
+                                    sg16 &ac, flt4v &b0c, flt4v &b1c, sg16 &an, flt4v &b0n, flt4v &b1n) {
+    wait0(ac, b0c, b1c);
+    if constexpr (G < 7) {
+        s_ld16(an, At + 8 * (G + 1));
+        ds_rd2<32 * (G + 1)>(b0n, b1n, bbase);
+    }
+    asm volatile("" : "+v"(x));   // pins this group's steps after the next group's loads
+    float mr[8];
+    const float bf[8] = {b0c.x, b0c.y, b0c.z, b0c.w, b1c.x, b1c.y, b1c.z, b1c.w};
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const double a = __longlong_as_double(((long long)ac[2 * i + 1] << 32) | (unsigned)ac[2 * i]);
+        mr[i] = (float)x;
+        x = (double)(float)fma(x, a, (double)bf[i]);
+    }
+    const flt4v w0 = {mr[0], mr[1], mr[2], mr[3]}, w1 = {mr[4], mr[5], mr[6], mr[7]};
+    asm volatile("ds_write_b128 %0, %1 offset:%3\n\tds_write_b128 %0, %2 offset:%4"
+                 : : "v"(mbase), "v"(w0), "v"(w1), "i"(32 * G), "i"(32 * G + 16) : "memory");
+    if constexpr (G < 7) g12<G + 1>(At, bbase, mbase, x, an, b0n, b1n, ac, b0c, b1c);
+}
+__device__ __forceinline__ void chain_mu_smem(const double *At, uint32_t bbase, uint32_t mbase, double &x) {
+    sg16 a0, a1;
+    flt4v b00, b01, b10, b11;
+    s_ld16(a0, At);
+    ds_rd2<0>(b00, b01, bbase);
+    g12<0>(At, bbase, mbase, x, a0, b00, b01, a1, b10, b11);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
 template <int MODE>
-__global__ void k_chain(float *out, unsigned long long *cyc) {
+__global__ void k_chain(float *out, unsigned long long *cyc, const double *__restrict__ Atab) {
     __shared__ double2 ab[64];
+    __shared__ float bfs[64];
     __shared__ float mus[64];
     const int lane = threadIdx.x;
     double mu = 0.0, sig = 0.0;
@@ -143,7 +190,10 @@ __global__ void k_chain(float *out, unsigned long long *cyc) {
         const double kd = (double)(blk * 64 + lane + 1);
         const double r = 1.0 / kd;
         const double A = 1.0 - r, Bv = (double)(float)(1.0001 * r);
-        if (MODE != 2 && ((MODE != 8 && MODE < 9) || MODE == 11 || blk == 0)) {
+        if (MODE == 12) {
+            bfs[lane] = (float)Bv;
+            lds_order();
+        } else if (MODE != 2 && ((MODE != 8 && MODE < 9) || MODE == 11 || blk == 0)) {
             ab[lane] = make_double2(A, Bv);
             lds_order();
         }
@@ -213,6 +263,9 @@ __global__ void k_chain(float *out, unsigned long long *cyc) {
                 for (int i = 0; i < 16; ++i)
                     reinterpret_cast<float4 *>(mus)[i] = make_float4(mr[4 * i], mr[4 * i + 1], mr[4 * i + 2], mr[4 * i + 3]);
             }
+        } else if (MODE == 12) {
+            if (lane == 0)
+                chain_mu_smem(Atab + blk * 64, (uint32_t)(uintptr_t)&bfs[0], (uint32_t)(uintptr_t)&mus[0], mu);
         } else if (MODE == 11) {
             if (lane == 0) chain_mu_ring((uint32_t)(uintptr_t)&ab[0], (uint32_t)(uintptr_t)&mus[0], mu);
         } else if (MODE == 9 || MODE == 10) {
@@ -263,6 +316,7 @@ __global__ void k_chain(float *out, unsigned long long *cyc) {
     }
 }
 
+static const double *g_atab;
 template <int MODE>
 void run(const char *name, float *dout, unsigned long long *dcyc) {
     for (int rep = 0; rep < 2; ++rep) {
@@ -270,7 +324,7 @@ void run(const char *name, float *dout, unsigned long long *dcyc) {
         (void)hipEventCreate(&e0);
         (void)hipEventCreate(&e1);
         (void)hipEventRecord(e0);
-        k_chain<MODE><<<1, 64>>>(dout, dcyc);
+        k_chain<MODE><<<1, 64>>>(dout, dcyc, g_atab);
         (void)hipEventRecord(e1);
         (void)hipEventSynchronize(e1);
         float ms = 0;
@@ -289,6 +343,14 @@ int main() {
     unsigned long long *dcyc;
     (void)hipMalloc(&dout, 16);
     (void)hipMalloc(&dcyc, 8);
+    {
+        static double h[NBLK * 64];
+        for (int k = 0; k < NBLK * 64; ++k) h[k] = 1.0 - 1.0 / (double)(k + 1);
+        double *d;
+        (void)hipMalloc(&d, sizeof(h));
+        (void)hipMemcpy(d, h, sizeof(h), hipMemcpyHostToDevice);
+        g_atab = d;
+    }
     run<0>("0 lane0 unroll4 (round 2)", dout, dcyc);
     run<1>("1 lane0 unroll64 + 8-deep ring", dout, dcyc);
     run<2>("2 all lanes readlane", dout, dcyc);
@@ -301,5 +363,6 @@ int main() {
     run<9>("9 VGPR operands, no LDS in loop", dout, dcyc);
     run<10>("10 as 9 + mu capture/writes", dout, dcyc);
     run<11>("11 per-step ring read (asm), 8 deep", dout, dcyc);
+    run<12>("12 A by s_load, B float LDS, 8/group", dout, dcyc);
     return 0;
 }

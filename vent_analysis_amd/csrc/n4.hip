@@ -1083,9 +1083,9 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_eval(const float *__restrict__ L0
 }
 
 // S7: ITK's float Welford convergence of the last eval of each active volume (two waves per
-// volume: n4_shared.h chain_wave_mu / chain_wave_sig over the field differences, read in raster
-// order through the volume's raster -> compact permutation).
-__global__ void __launch_bounds__(128) k_n4_welford(const float *D, const int32_t *perm, int64_t VS,
+// volume: n4_shared.h chain_wave_mu / chain_wave_sig fed by chain_wave_prod, over the field
+// differences read in raster order through the volume's raster -> compact permutation).
+__global__ void __launch_bounds__(192) k_n4_welford(const float *D, const int32_t *perm, int64_t VS,
                                                    const VolScalars *sc, N4State *st, int64_t vol0) {
     __shared__ ChainSlot slots[CH_SLOTS];
     __shared__ ChainState cs;
@@ -1094,11 +1094,13 @@ __global__ void __launch_bounds__(128) k_n4_welford(const float *D, const int32_
     if (threadIdx.x == 0) {
         cs.a_done = 0;
         cs.b_done = 0;
+        cs.c_done = 0;
     }
     __syncthreads();
     const int64_t n = sc[b].n_mask1;
-    if (threadIdx.x < 64) chain_wave_mu(D + b * VS, perm + b * VS, n, slots, &cs);
-    else chain_wave_sig(n, slots, &cs);
+    if (threadIdx.x < 64) chain_wave_mu(n, slots, &cs);
+    else if (threadIdx.x < 128) chain_wave_sig(n, slots, &cs);
+    else chain_wave_prod(D + b * VS, perm + b * VS, n, slots, &cs);
     __syncthreads();
     if (threadIdx.x == 0) st[b].conv_w = cs.conv;
 }
@@ -1354,7 +1356,7 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
                 }
                 if (cm == 0) {
                     ScopedKTimer tm(b, "n4_welford", 0.0);
-                    k_n4_welford<<<(unsigned)ns, 128, 0, st>>>(b->d_D, b->d_perm, b->VS, b->d_sc,
+                    k_n4_welford<<<(unsigned)ns, 192, 0, st>>>(b->d_D, b->d_perm, b->VS, b->d_sc,
                                                                b->d_st, vol0);
                     VH_CHECK_LAUNCH();
                 }

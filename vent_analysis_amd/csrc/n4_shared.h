@@ -5,6 +5,7 @@
 // every iteration.
 #pragma once
 #include "vh_internal.h"
+#include <cfloat>
 
 struct DevAxis {
     const int32_t *base;
@@ -455,16 +456,16 @@ __device__ __forceinline__ bool r3_bin_min(const Range3 &r, const float *u, int 
 
 // ---------------------------------------------------------------------------------------------
 // S7 convergence (conv_mode 0): ITK's float Welford recurrence over the masked voxels in raster
-// order, d_k = B_old - B_new read from a raster-ordered buffer.  Two waves of one workgroup:
-//   wave A (mu): per block of 64 steps, all lanes compute p = (float)exp((double)d), 1/k, the mu
-//     step constants (1 - 1/k, p/k) and (k-1)/k into an LDS slot; then lane 0 runs (pipelined,
-//     chain_block64)
+// order, d_k = B_old - B_new read from a raster-ordered buffer.  Three waves of one workgroup:
+//   producer (C): per block of 64 steps, all lanes compute p = (float)exp((double)d), 1/k, the
+//     mu step constants (1 - 1/k, p/k) and (k-1)/k into an LDS slot;
+//   wave A (mu): lane 0 runs (pipelined, chain_block64)
 //       mu <- (float)fma((double)mu, 1 - 1/k, (double)(p / k))      (one step per voxel)
 //     recording mu before each step for wave B.
 //   wave B (sig): per block, all lanes form s = (p - mu_prev)^2 (float); lane 0 runs
 //       sig <- (float)fma((double)s, (k-1)/k, (double)sig)          (k >= 2)
-// The recurrences are inherently serial (the float running mean drifts); the slot ring and two
-// LDS counters let the two waves overlap.  Result: conv = (float)sqrt(sig / (n-1)) / mu.
+// The recurrences are inherently serial (the float running mean drifts); the slot ring and three
+// LDS counters let the three waves overlap (A and B then do nothing but their steps).  Result: conv = (float)sqrt(sig / (n-1)) / mu.
 // ---------------------------------------------------------------------------------------------
 #define CH_SLOTS 4
 struct ChainSlot {
@@ -474,7 +475,7 @@ struct ChainSlot {
     float mu[64];      // mu before step k
 };
 struct ChainState {
-    int a_done, b_done;   // blocks finished by wave A / wave B
+    int a_done, b_done, c_done;   // blocks finished by wave A / wave B / the producer
     float mu, conv;
 };
 
@@ -578,25 +579,52 @@ __device__ __forceinline__ double chain_block64(const double2 *q, float *murec, 
     return x;
 }
 
-// wave A.  The n d values in raster order: Dr[k] (perm == nullptr), else Dr[perm[k]].  The
-// next block's values are loaded before lane 0 runs this block's steps (the loads overlap the
-// serial chain).
-__device__ __forceinline__ float chain_load(const float *Dr, const int32_t *perm, int64_t j, int64_t n) {
-    if (j >= n) return 0.0f;
-    return perm ? Dr[perm[j]] : Dr[j];
-}
-
-__device__ void chain_wave_mu(const float *Dr, const int32_t *perm, int64_t n, ChainSlot *slots,
-                              ChainState *cs) {
+// Producer wave (C): per block of 64 steps, all lanes compute p = (float)exp((double)d), 1/k,
+// the mu step constants (1 - 1/k, p / k) and (k - 1) / k into the block's LDS slot, up to CH_SLOTS
+// blocks ahead of wave B.  The n d values are in raster order: Dr[k] (perm == nullptr), else
+// Dr[perm[k]]; a block's values are loaded CH_PF blocks ahead (its perm entries 2 CH_PF ahead).
+#define CH_PF 8
+__device__ void chain_wave_prod(const float *Dr, const int32_t *perm, int64_t n, ChainSlot *slots,
+                                ChainState *cs) {
     const int lane = threadIdx.x & 63;
-    double mu = 0.0;
     const int64_t nblk = (n + 63) / 64;
-    float dnext = chain_load(Dr, perm, lane, n);
+    float dq[CH_PF];
+    int32_t pq[2 * CH_PF];
+    if (perm) {
+#pragma unroll
+        for (int i = 0; i < 2 * CH_PF; ++i) {
+            const int64_t j = (int64_t)i * 64 + lane;
+            pq[i] = j < n ? perm[j] : 0;
+        }
+#pragma unroll
+        for (int i = 0; i < CH_PF; ++i) {
+            const int64_t j = (int64_t)i * 64 + lane;
+            dq[i] = j < n ? Dr[pq[i]] : 0.0f;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < CH_PF; ++i) {
+            const int64_t j = (int64_t)i * 64 + lane;
+            dq[i] = j < n ? Dr[j] : 0.0f;
+        }
+    }
+    int bseen = 0;   // last b_done read: slots of blocks < bseen + CH_SLOTS are free
     for (int64_t blk = 0; blk < nblk; ++blk) {
         ChainSlot &S = slots[blk % CH_SLOTS];
         const int64_t j = blk * 64 + lane;
-        const float d = dnext;
-        dnext = chain_load(Dr, perm, j + 64, n);
+        const float d = dq[0];
+#pragma unroll
+        for (int i = 0; i < CH_PF - 1; ++i) dq[i] = dq[i + 1];
+        const int64_t jd = j + 64 * CH_PF;
+        if (perm) {
+            dq[CH_PF - 1] = jd < n ? Dr[pq[CH_PF]] : 0.0f;
+#pragma unroll
+            for (int i = 0; i < 2 * CH_PF - 1; ++i) pq[i] = pq[i + 1];
+            const int64_t jp = j + 2 * 64 * CH_PF;
+            pq[2 * CH_PF - 1] = jp < n ? perm[jp] : 0;
+        } else {
+            dq[CH_PF - 1] = jd < n ? Dr[jd] : 0.0f;
+        }
         const bool ok = j < n;
         const float p = expf_cr(d);
         const double kd = (double)(j + 1);
@@ -604,12 +632,26 @@ __device__ void chain_wave_mu(const float *Dr, const int32_t *perm, int64_t n, C
         const double2 ab = ok ? make_double2(1.0 - r, (double)(float)((double)p * r))   // p / k, div_r form
                               : make_double2(1.0, 0.0);
         const double c = (kd - 1.0) / kd;
-        if (blk >= CH_SLOTS)
-            while (lds_load_acq(&cs->b_done) <= (int)(blk - CH_SLOTS)) __builtin_amdgcn_s_sleep(1);
+        if (blk >= CH_SLOTS + bseen)
+            while ((bseen = lds_load_acq(&cs->b_done)) <= (int)(blk - CH_SLOTS)) __builtin_amdgcn_s_sleep(1);
         S.ab[lane] = ab;
         S.cs[lane] = make_double2(c, 0.0);
         S.p[lane] = p;
         wave_lds_order();
+        if (lane == 0) lds_store_rel(&cs->c_done, (int)(blk + 1));
+    }
+}
+
+// wave A: the mu recurrence on lane 0, block by block as the producer fills them.
+__device__ void chain_wave_mu(int64_t n, ChainSlot *slots, ChainState *cs) {
+    const int lane = threadIdx.x & 63;
+    double mu = 0.0;
+    const int64_t nblk = (n + 63) / 64;
+    int cseen = 0;   // last c_done read
+    for (int64_t blk = 0; blk < nblk; ++blk) {
+        ChainSlot &S = slots[blk % CH_SLOTS];
+        if (blk >= cseen)
+            while ((cseen = lds_load_acq(&cs->c_done)) <= (int)blk) __builtin_amdgcn_s_sleep(1);
         if (lane == 0) mu = chain_block64<true>(S.ab, S.mu, mu);
         wave_lds_order();
         if (lane == 0) {

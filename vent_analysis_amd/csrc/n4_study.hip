@@ -834,13 +834,15 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
             if (t == 0) {
                 M.ch.a_done = 0;
                 M.ch.b_done = 0;
+                M.ch.c_done = 0;
             }
             __syncthreads();
             ST_MARK(6);
             // ---- convergence of this iteration ----
             if (a.conv_mode == 0) {   // S7: ITK's float Welford recurrence, two waves
-                if (wv == 0) chain_wave_mu(Db, nullptr, n, slots, &M.ch);
+                if (wv == 0) chain_wave_mu(n, slots, &M.ch);
                 else if (wv == 1) chain_wave_sig(n, slots, &M.ch);
+                else if (wv == 2) chain_wave_prod(Db, nullptr, n, slots, &M.ch);
             } else if (wv == 0) {   // S7x: item partials in item order
                 double sd = 0.0, sd2 = 0.0;
                 for (int i = lane; i < a.nitems; i += 64) {
