@@ -516,6 +516,15 @@ __device__ __forceinline__ uint32_t lds_addr(const void *p) { return (uint32_t)(
                    "i"(128 * (g) + 96), "i"(128 * (g) + 112)                                      \
                  : "memory")
 
+#define CH_RD4(q, base, off)                                                                       \
+    asm volatile("ds_read_b128 %0, %4 offset:%5\n\t"                                               \
+                 "ds_read_b128 %1, %4 offset:%6\n\t"                                              \
+                 "ds_read_b128 %2, %4 offset:%7\n\t"                                              \
+                 "ds_read_b128 %3, %4 offset:%8"                                                    \
+                 : "=&v"(q[0]), "=&v"(q[1]), "=&v"(q[2]), "=&v"(q[3])                              \
+                 : "v"(base), "i"(off), "i"((off) + 16), "i"((off) + 32), "i"((off) + 48)           \
+                 : "memory")
+
 template <int N>
 __device__ __forceinline__ void ch_wait(ch_d2 *q) {   // N LDS ops may still be in flight
     asm volatile("s_waitcnt lgkmcnt(%8)"
@@ -524,39 +533,60 @@ __device__ __forceinline__ void ch_wait(ch_d2 *q) {   // N LDS ops may still be 
                  : "i"(N)
                  : "memory");
 }
+template <int N>
+__device__ __forceinline__ void ch_wait4(ch_d2 *q) {
+    asm volatile("s_waitcnt lgkmcnt(%4)"
+                 : "+v"(q[0]), "+v"(q[1]), "+v"(q[2]), "+v"(q[3])
+                 : "i"(N)
+                 : "memory");
+}
 
-template <bool MU, int G>
+// GS = 8: groups of 8 steps (64 VGPRs of operands in flight); GS = 4: groups of 4 (32 VGPRs),
+// for the volume-resident kernel whose register budget would otherwise spill inside the loop.
+template <bool MU, int GS, int G>
 __device__ __forceinline__ void ch_group(uint32_t base, uint32_t mbase, double &x, ch_d2 *cur,
                                          ch_d2 *nxt) {
-    if constexpr (G < 7) {
-        CH_RD8(nxt, base, G + 1);
-        ch_wait<(G == 0 || !MU) ? 8 : 10>(cur);   // MU: the previous group's 2 writes follow cur
+    constexpr int NG = 64 / GS;
+    // MU writes 8 / GS b128 records per group (one per 4 steps)
+    constexpr int WPG = MU ? GS / 4 : 0;
+    if constexpr (G < NG - 1) {
+        if constexpr (GS == 8) {
+            CH_RD8(nxt, base, G + 1);
+            ch_wait<G == 0 ? 8 : 8 + WPG>(cur);
+        } else {
+            CH_RD4(nxt, base, 64 * (G + 1));
+            ch_wait4<G == 0 ? 4 : 4 + WPG>(cur);
+        }
     } else {
-        ch_wait<MU ? 2 : 0>(cur);
+        if constexpr (GS == 8) ch_wait<WPG>(cur);
+        else ch_wait4<WPG>(cur);
     }
     if constexpr (MU) {
-        float mr[8];
+        float mr[GS];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < GS; ++i) {
             mr[i] = (float)x;
             x = (double)(float)fma(x, cur[i].x, cur[i].y);
         }
-        const ch_f4 w0 = {mr[0], mr[1], mr[2], mr[3]}, w1 = {mr[4], mr[5], mr[6], mr[7]};
-        asm volatile("ds_write_b128 %0, %1 offset:%3\n\tds_write_b128 %0, %2 offset:%4"
-                     :
-                     : "v"(mbase), "v"(w0), "v"(w1), "i"(32 * G), "i"(32 * G + 16)
-                     : "memory");
+#pragma unroll
+        for (int h = 0; h < GS / 4; ++h) {
+            const ch_f4 w = {mr[4 * h], mr[4 * h + 1], mr[4 * h + 2], mr[4 * h + 3]};
+            asm volatile("ds_write_b128 %0, %1 offset:%2"
+                         :
+                         : "v"(mbase), "v"(w), "i"(4 * GS * G + 16 * h)
+                         : "memory");
+        }
     } else {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) x = (double)(float)fma(cur[i].y, cur[i].x, x);
+        for (int i = 0; i < GS; ++i) x = (double)(float)fma(cur[i].y, cur[i].x, x);
     }
-    if constexpr (G < 7) ch_group<MU, G + 1>(base, mbase, x, nxt, cur);
+    if constexpr (G < NG - 1) ch_group<MU, GS, G + 1>(base, mbase, x, nxt, cur);
 }
 
 #ifndef CH_ASM
 #define CH_ASM 1
 #endif
-template <bool MU>
+template <bool MU, int GS = 8>
 __device__ __forceinline__ double chain_block64(const double2 *q, float *murec, double x) {
     if constexpr (!CH_ASM) {   // reference form (A/B builds)
 #pragma unroll 4
@@ -572,9 +602,10 @@ __device__ __forceinline__ double chain_block64(const double2 *q, float *murec, 
         return x;
     }
     const uint32_t base = lds_addr(q), mbase = MU ? lds_addr(murec) : 0u;
-    ch_d2 qa[8], qb[8];
-    CH_RD8(qa, base, 0);
-    ch_group<MU, 0>(base, mbase, x, qa, qb);
+    ch_d2 qa[GS], qb[GS];
+    if constexpr (GS == 8) CH_RD8(qa, base, 0);
+    else CH_RD4(qa, base, 0);
+    ch_group<MU, GS, 0>(base, mbase, x, qa, qb);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     return x;
 }
@@ -643,6 +674,7 @@ __device__ void chain_wave_prod(const float *Dr, const int32_t *perm, int64_t n,
 }
 
 // wave A: the mu recurrence on lane 0, block by block as the producer fills them.
+template <int GS = 8>
 __device__ void chain_wave_mu(int64_t n, ChainSlot *slots, ChainState *cs) {
     const int lane = threadIdx.x & 63;
     double mu = 0.0;
@@ -652,7 +684,7 @@ __device__ void chain_wave_mu(int64_t n, ChainSlot *slots, ChainState *cs) {
         ChainSlot &S = slots[blk % CH_SLOTS];
         if (blk >= cseen)
             while ((cseen = lds_load_acq(&cs->c_done)) <= (int)blk) __builtin_amdgcn_s_sleep(1);
-        if (lane == 0) mu = chain_block64<true>(S.ab, S.mu, mu);
+        if (lane == 0) mu = chain_block64<true, GS>(S.ab, S.mu, mu);
         wave_lds_order();
         if (lane == 0) {
             if (blk == nblk - 1) cs->mu = (float)mu;   // published by the release below
@@ -662,6 +694,7 @@ __device__ void chain_wave_mu(int64_t n, ChainSlot *slots, ChainState *cs) {
 }
 
 // wave B.  Returns conv in cs->conv.
+template <int GS = 8>
 __device__ void chain_wave_sig(int64_t n, ChainSlot *slots, ChainState *cs) {
     const int lane = threadIdx.x & 63;
     double sig = 0.0;
@@ -675,7 +708,7 @@ __device__ void chain_wave_sig(int64_t n, ChainSlot *slots, ChainState *cs) {
         const bool ok = j < n && j > 0;
         S.cs[lane] = ok ? make_double2(S.cs[lane].x, (double)(q * q)) : make_double2(0.0, 0.0);
         wave_lds_order();
-        if (lane == 0) sig = chain_block64<false>(S.cs, nullptr, sig);
+        if (lane == 0) sig = chain_block64<false, GS>(S.cs, nullptr, sig);
         wave_lds_order();
         if (lane == 0) lds_store_rel(&cs->b_done, (int)(blk + 1));
     }

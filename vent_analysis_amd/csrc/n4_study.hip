@@ -32,6 +32,9 @@
 #define ST_WAVES (ST_TPB / 64)
 #define ST_HC 8        // LDS histogram copies
 #define ST_MAX_LDS (160 * 1024)
+#ifndef ST_CH_GS
+#define ST_CH_GS 8   // convergence-chain group size here (n4_shared.h ch_group): 8 measured 135M vs 167M cycles for 4
+#endif
 
 // ST_PROF builds (scripts/dev/phase_ab.sh): block 0 prints shader cycles per phase at the end
 #ifdef ST_PROF
@@ -840,8 +843,8 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
             ST_MARK(6);
             // ---- convergence of this iteration ----
             if (a.conv_mode == 0) {   // S7: ITK's float Welford recurrence, two waves
-                if (wv == 0) chain_wave_mu(n, slots, &M.ch);
-                else if (wv == 1) chain_wave_sig(n, slots, &M.ch);
+                if (wv == 0) chain_wave_mu<ST_CH_GS>(n, slots, &M.ch);
+                else if (wv == 1) chain_wave_sig<ST_CH_GS>(n, slots, &M.ch);
                 else if (wv == 2) chain_wave_prod(Db, nullptr, n, slots, &M.ch);
             } else if (wv == 0) {   // S7x: item partials in item order
                 double sd = 0.0, sd2 = 0.0;
