@@ -59,9 +59,11 @@ def cpu_baseline(R, C, Z, seconds=15.0, procs=16):
             done += len(ts)
             busy += sum(ts)
         wall = time.perf_counter() - t0
-    return {"value": done / wall, "unit": "volumes/s", "cores": procs, "kind": "port",
-            "sample": f"{done} synthetic {R}x{C}x{Z} volumes (oracle/n4_oracle.c N4 + "
-                      f"oracle/vdp_oracle.py chain), {procs} processes, {wall:.1f} s wall, "
+    return {"value": done / wall, "unit": "volumes/s", "cores": procs, "host_cpus": os.cpu_count(),
+            "kind": "port",
+            "sample": f"{done} synthetic {R}x{C}x{Z} volumes (oracle/n4_oracle.c N4, conv_mode 0 = "
+                      f"ITK float Welford, + oracle/vdp_oracle.py chain), {procs} processes of "
+                      f"{os.cpu_count()} host CPUs, {wall:.1f} s wall, "
                       f"{busy / max(done, 1):.3f} s per volume per core"}
 
 
@@ -85,17 +87,17 @@ def algorithmic_bytes(name, hp, mk, res, R, C, Z, study=True, conv_mode=0):
     vr = np.maximum(hi - lo + 1, 0).sum(axis=1).astype(np.float64)   # voxels in column ranges
     iters = np.array([sum(r.n4_iters[:4]) for r in res], np.float64)
     levels = np.array([sum(1 for k in range(4) if r.n4_iters[k] > 0) for r in res], np.float64)
-    if name == "n4_eval":        # read ridx + L0 + T windows, write U (+ d)
+    cw = 8.0 if conv_mode == 0 else 0.0   # S7: the field differences d written once, read once
+    if name == "n4_eval":        # read ridx + L0 + T windows, write U (+ d, compact order)
         return float(np.sum(iters * (12.0 + cw / 2) * vm))
     if name == "n4_fit":         # read ridx + U
         return float(np.sum(iters * 8.0 * vm))
     if name == "n4_hist":        # read U
         return float(np.sum(iters * 4.0 * vm))
-    cw = 8.0 if conv_mode == 0 else 0.0   # S7: eval writes d (raster order), the recurrence reads it
     if name == "n4_study":       # init: read I, write L0 + U; per iteration: hist reads U, fit
         return float(np.sum(iters * (16.0 + cw) * vm + 12.0 * vm))   # reads U, eval L0 in, U out
-    if name == "n4_welford":     # read d
-        return float(np.sum(iters * 4.0 * vm))
+    if name == "n4_welford":     # read perm + d (raster walk of the compact d)
+        return float(np.sum(iters * 8.0 * vm))
     if name == "n4_den":         # read ridx, once per level
         return float(np.sum(levels * 4.0 * vm))
     if name == "n4_init":        # row masks / offsets from the column bitmaps (+ the sweep
@@ -152,6 +154,83 @@ def max_over_ranks(dt, dist):
     return float(t.item())
 
 
+def host_to_host(R, C, Z, nb, args, device, opts, seed):
+    """Volumes/s from host memory to host memory: args.h2h_batches sub-batches of nb studies
+    through vh_pipe (3 slots, pinned staging, one stream each), inputs HPvent + mask in, every
+    output the class returns out (N4HPvent, defectArray, defectBorder, defectArrayLB, scalars).
+    The slowest rank's time is what the caller's aggregate uses (ranks run independently)."""
+    from vent_analysis_amd import _lib
+    from vent_analysis_amd.synth import synth_batch
+    slots = 3
+    n = max(1, args.h2h_batches) * nb
+    hp, mk = synth_batch(R, C, Z, n, base_seed=seed, unique=16)
+    P = _lib.Pipe(R, C, Z, nb, slots=slots, device=device)
+    out = (np.empty(hp.shape, np.float32), np.empty(hp.shape, np.uint8),
+           np.empty(hp.shape, np.uint8), np.empty(hp.shape, np.uint8))
+    P.run(hp[:slots * nb], mk[:slots * nb], opts,
+          out=tuple(a[:slots * nb] for a in out))          # warm: every slot's workspaces
+    t = time.perf_counter()
+    P.run(hp, mk, opts, out=out)
+    dt = time.perf_counter() - t
+    P.close()
+    return {"volumes": n, "seconds": round(dt, 4), "sub_batch": nb, "slots": slots,
+            "includes": "H2D of HPvent f32 + mask u8, the full pipeline, D2H of N4HPvent f32 + "
+                        "defect / border / LB u8 + per-study scalars, host staging memcpys",
+            "bytes_per_volume": int(R * C * Z * (4 + 1 + 4 + 3))}
+
+
+def main_ci(args):
+    """CI line: defect-voxels/s and sphere-probes/s of the cluster-index map
+    on 128x128x24 studies, host-to-host through vh_ci (defect map in, float64 CI map out).  Two
+    inputs: the seed-0 study's defect map from the GPU pipeline itself (golden-identical), and a
+    clustered map of ~5 900 defects like the one the reference timing used (44.4 s)."""
+    from vent_analysis_amd import _lib
+    from vent_analysis_amd.sphere import compact_table, sphere_pix
+    from vent_analysis_amd.synth import synth_volume
+    R, C, Z = 128, 128, 24
+    vox = (1.5, 1.5, 10.0)
+    X, M = synth_volume(R, C, Z, 0)
+    Bt = _lib.Batch(R, C, Z, 1)
+    Bt.upload(X[None], M.astype(np.uint8)[None])
+    Bt.run(Bt.options(do_n4=True, vox=vox))
+    _, d0, _, _, _ = Bt.download(n4=False)
+    Bt.close()
+    rng = np.random.default_rng(0)
+    i, j, k = np.meshgrid(np.arange(R), np.arange(C), np.arange(Z), indexing="ij")
+    blobs = np.zeros((R, C, Z), bool)
+    while blobs.sum() < 5900:
+        c = [rng.uniform(0.15, 0.85) * s for s in (R, C, Z)]
+        r = rng.uniform(4, 9)
+        blobs |= ((i - c[0]) ** 2 + (j - c[1]) ** 2 + ((k - c[2]) * 6.67) ** 2 <= r * r) & (M > 0)
+    table = compact_table(sphere_pix(vox, 50), (R, C, Z))
+    cases = {}
+    for name, d in (("seed0_pipeline", d0[0]), ("clustered", blobs)):
+        d = d.astype(np.uint8)
+        for _ in range(max(1, args.warmup)):
+            ci, sc, shell = _lib.ci(d, table, float(np.min(vox)))
+        t = time.perf_counter()
+        for _ in range(args.steps):
+            ci, sc, shell = _lib.ci(d, table, float(np.min(vox)))
+        dt = (time.perf_counter() - t) / args.steps
+        nd = int((d > 0).sum())
+        probes = int(np.sum(table.bounds[shell[0][d > 0]].astype(np.int64)))
+        cases[name] = {"defect_voxels": nd, "seconds_per_map": round(dt, 6),
+                       "defect_voxels_per_s": round(nd / dt, 1), "sphere_probes_per_s": round(probes / dt, 1),
+                       "sphere_probes": probes, "CI": float(sc[0])}
+    head = cases["clustered"]
+    line = {"metric": "CI defect-voxels/s (cluster-index map, 128x128x24, host-to-host)",
+            "value": head["defect_voxels_per_s"], "unit": "defect-voxels/s", "n_gpus": 1,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(head["seconds_per_map"] * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": round(head["defect_voxels_per_s"] / (5917 / 44.4), 1),
+            "dtype": "u8/f64", "data": "synthetic",
+            "config": {"workload": "CI.calculate_CI + the 95th-percentile CI on one 128x128x24 "
+                                   "study, Rmax 50, vox [1.5, 1.5, 10]", "cases": cases},
+            "roofline": None, "cpu_baseline": None,
+            "baseline_note": "reference: 5917 clustered defect voxels in 44.4 s (BASELINE.md)"}
+    print(json.dumps(line))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -171,10 +250,21 @@ def main():
     ap.add_argument("--conv-mode", type=int, default=0, choices=[0, 1],
                     help="N4 convergence measure: 0 ITK's float Welford recurrence (SimpleITK "
                          "semantics, default), 1 exact CoV (faster, different iteration counts)")
+    ap.add_argument("--comm", action="store_true",
+                    help="at --gpus 1: go through the RCCL path anyway (comm_init(1, 0) + one "
+                         "cohort all-reduce per step)")
+    ap.add_argument("--no-h2h", action="store_true",
+                    help="skip the host-to-host pipeline measurement (host_to_host_vol_s)")
+    ap.add_argument("--h2h-batches", type=int, default=4,
+                    help="host-to-host sample: this many sub-batches of --batch volumes")
+    ap.add_argument("--workload", default="vdp", choices=["vdp", "ci"],
+                    help="vdp: the BASELINE metric (default); ci: the cluster-index line")
     ap.add_argument("--conv-threshold", type=float, default=0.001,
                     help="N4 convergence threshold (SimpleITK default 0.001; 0 = fixed 4x50 "
                          "iterations, for kernel A/B runs at constant work)")
     args = ap.parse_args()
+    if args.workload == "ci":
+        return main_ci(args)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -197,9 +287,12 @@ def main():
     hp, mk = synth_batch(R, C, Z, nb, base_seed=shard_seed(rank), unique=16)
     Bt = _lib.Batch(R, C, Z, nb, device=local)
     Bt.upload(hp, mk)
+    use_comm = world > 1 or args.comm
     if world > 1:
         uid = broadcast_uid(_lib.comm_unique_id() if rank == 0 else None, dist)
         _lib.comm_init(world, rank, uid, device=local)
+    elif args.comm:
+        _lib.comm_init(1, 0, _lib.comm_unique_id(), device=local)
     vox = (1.5, 1.5, 10.0)
     opts = Bt.options(do_n4=not args.no_n4, vox=vox, do_cohort=True,
                       profile=not args.no_profile, n4_subbatch=args.subbatch,
@@ -211,7 +304,7 @@ def main():
 
     def step(o):
         Bt.run(o)
-        if world > 1:
+        if use_comm:
             Bt.cohort_allreduce()
         Bt.sync()
 
@@ -266,6 +359,9 @@ def main():
                 "kernel_us_per_launch": {n: round(v["ms_total"] / v["launches"] * 1e3, 2)
                                          for n, v in kernels.items()}}
     its = np.array([list(r.n4_iters[:4]) for r in res])
+    h2h = None
+    if not args.no_h2h:
+        h2h = host_to_host(R, C, Z, nb, args, local, warm, shard_seed(rank) + 500)
     total = world * nb * args.steps
     line = {
         "metric": METRIC,
@@ -289,10 +385,14 @@ def main():
                    "n4_iterations_mean": float(its.sum(axis=1).mean()) if its.size else 0.0},
         "roofline": roof,
         "cpu_baseline": cpu,
+        "host_to_host_vol_s": round(world * h2h["volumes"] / h2h["seconds"], 2) if h2h else None,
+        "host_to_host": h2h,
     }
     if rank == 0:
         print(json.dumps(line))
     Bt.close()
+    if use_comm:
+        _lib.comm_destroy(device=local)
     if dist:
         dist.destroy_process_group()
 

@@ -5,8 +5,9 @@
  * and never throws across the boundary; vh_last_error() gives the message of the last failure on
  * a context.  Host buffers are caller-allocated and C-contiguous in numpy's (rows, cols, slices)
  * order (slice axis fastest, as Vent_Analysis.openSingleDICOM produces, Vent_Analysis.py:179);
- * device buffers are owned by the library.  A context is bound to one GPU and one HIP stream and
- * is re-entrant per context (one context per thread/GPU).
+ * device buffers are owned by the library.  A context is bound to one GPU; each batch owns its HIP
+ * stream.  The host-buffer entry points (vh_n4 ... vh_ci) share a per-context scratch batch behind a
+ * per-context mutex, so a context may be used from several host threads; batches are independent.
  *
  * Reference interface each entry point replaces (file:line in thomenr/Vent_Analysis):
  *   vh_n4        Vent_Analysis.N4_bias_correction            Vent_Analysis.py:316-334
@@ -15,6 +16,7 @@
  *   vh_vdp       Vent_Analysis.calculate_VDP (post-N4 part)  Vent_Analysis.py:239-263
  *   vh_ci        CI.calculate_CI + Vent_Analysis.calculate_CI CI.py:107-145, Vent_Analysis.py:265-271
  *   vh_batch_*   the same pipeline over a device-resident batch of studies (build-defined)
+ *   vh_pipe_*    the batch pipeline fed from host memory with overlapped transfers (build-defined)
  *   vh_comm_*    cohort histogram all-reduce over RCCL (build-defined, BASELINE config 4)
  */
 #ifndef VENT_HIP_H
@@ -26,7 +28,7 @@
 extern "C" {
 #endif
 
-#define VH_ABI_VERSION 2
+#define VH_ABI_VERSION 3
 
 /* status codes */
 #define VH_OK 0
@@ -152,6 +154,20 @@ const char *vh_batch_kernel_names(void);
 int vh_batch_reset_timers(vh_batch *b);
 int vh_batch_kernel_time(vh_batch *b, const char *name, double *total_ms, int64_t *launches,
                          double *bytes_per_launch);
+
+/* ---- host-to-host pipeline ------------------------------------------------------------------ */
+/* Streams n host-resident studies through `slots` device batches of `sub` volumes each (one HIP
+ * stream and one host thread per slot, pinned staging per slot): while one slot computes, the
+ * others upload their next sub-batch or download their last results.  Outputs are host arrays of
+ * n volumes (any may be NULL); res[n].  A ragged last sub-batch is padded with copies of its last
+ * study (results discarded).  Build-defined: SURVEY section 8(e) partitioning on one GPU. */
+typedef struct vh_pipe vh_pipe;
+int vh_pipe_create(vh_ctx *ctx, int64_t R, int64_t C, int64_t Z, int64_t sub, int slots,
+                   vh_pipe **out);
+int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, const vh_run_opts *opts,
+                float *n4, uint8_t *defect, uint8_t *defect_border, uint8_t *lb,
+                vh_vdp_result *res);
+int vh_pipe_destroy(vh_pipe *p);
 
 /* ---- multi-GPU (RCCL over xGMI) -------------------------------------------------------------- */
 #define VH_COMM_ID_BYTES 128

@@ -11,7 +11,7 @@ rc=$?; echo "gpu tests rc=$rc"; tail -1 gpurun_out/${TAG}_pytest_gpu.log; [ $rc 
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1
 rc=$?; echo "smoke rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_prof -o run -- \
-    python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile > gpurun_out/${TAG}_prof.log 2>&1
+    python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-profile --no-h2h > gpurun_out/${TAG}_prof.log 2>&1
 rc=$?; echo "rocprof rc=$rc"; [ $rc -eq 0 ] || exit $rc
 REGEX='k_n4_|k_tile|k_gather|k_snr|k_sort_vol|k_mask_stats' bash scripts/gpu_pmc.sh ${TAG}
 rc=$?; echo "pmc rc=$rc"; [ $rc -eq 0 ] || exit $rc

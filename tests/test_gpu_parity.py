@@ -1,6 +1,9 @@
 """GPU parity tests (MI355X): the HIP path through the C-ABI against the reference goldens and the
 CPU oracle.  Tolerances: masks / indices / counts bit-exact; VDP scalars exact (they are ratios of
 exact counts); SNR rel 1e-5; N4 rel 1e-5 (north_star), identical iteration counts."""
+import hashlib
+import os
+
 import numpy as np
 import pytest
 
@@ -169,6 +172,49 @@ def test_batch_pipeline_end_to_end():
         exp += np.bincount(bi, minlength=_lib.COHORT_BINS).astype(np.uint64)
     assert np.array_equal(h, exp)
     B.close()
+
+
+def test_rccl_cohort_allreduce_one_rank():
+    """The RCCL path on one GPU (config 4's per-GPU shard): comm_unique_id -> comm_init(1, 0) ->
+    a 256-volume 128x128x24 batch with the cohort histogram -> ncclAllReduce over one rank must
+    leave the local histogram unchanged (api.hip vh_comm_init / vh_batch_cohort_allreduce)."""
+    uid = _lib.comm_unique_id()
+    assert len(uid) == _lib.COMM_ID_BYTES
+    _lib.comm_init(1, 0, uid)
+    try:
+        hp, mk = synth_batch(128, 128, 24, 256, base_seed=4000, unique=16)
+        B = _lib.Batch(128, 128, 24, 256)
+        B.upload(hp, mk)
+        B.run(B.options(do_n4=True, vox=(1.5, 1.5, 10.0), do_cohort=True))
+        local = B.cohort_hist()
+        assert local.sum() > 0
+        B.cohort_allreduce()
+        B.sync()
+        assert np.array_equal(B.cohort_hist(), local)
+        B.close()
+    finally:
+        _lib.comm_destroy()
+
+
+def test_pipe_host_to_host_equals_batch():
+    """vh_pipe (3 slots x 4-volume sub-batches, ragged last sub-batch) returns exactly what one
+    device-resident batch returns for the same 10 studies."""
+    hp, mk = synth_batch(64, 64, 16, 10, base_seed=77)
+    vox = (1.5, 1.5, 10.0)
+    B = _lib.Batch(64, 64, 16, 10)
+    B.upload(hp, mk)
+    o = B.options(do_n4=True, vox=vox)
+    B.run(o)
+    ref = B.download(n4=True)
+    B.close()
+    P = _lib.Pipe(64, 64, 16, 4, slots=3)
+    got = P.run(hp, mk, o)
+    P.close()
+    for a, b in zip(got[:4], ref[:4]):
+        assert np.array_equal(a, b)
+    for r, q in zip(got[4], ref[4]):
+        assert (r.vdp, r.vdp_lb, r.n_km0, r.snr, list(r.n4_iters[:4])) == \
+            (q.vdp, q.vdp_lb, q.n_km0, q.snr, list(q.n4_iters[:4]))
 
 
 def test_batch_equals_single():
@@ -384,10 +430,11 @@ def test_config2_256x256x24_full_pipeline_vs_oracle():
 
 
 def test_config5_512_cubed_n4_morph3d():
-    """Config 5: one 512^3 isotropic study, N4 multiresolution + 3-D morphology.  The CPU N4
-    restatement cannot finish at this size in test time, so the N4 is checked through properties
-    (iteration caps, positivity, determinism, scale covariance of a re-run is covered at small
-    sizes) and the post-N4 chain bit-exactly against the oracle applied to the GPU's N4 output."""
+    """Config 5: one 512^3 isotropic study, N4 multiresolution + 3-D morphology.  N4 is pinned by
+    tests/golden/n4_512_seed11.npz (scripts/make_n4_512_fixture.py ran the C oracle once in the
+    build container): per-level iterations and convergence values, a strided voxel sample and the
+    sha256 of the whole N4HPvent; plus run-to-run determinism.  The post-N4 chain is checked
+    bit-exactly against the oracle applied to the GPU's N4 output."""
     n = 512
     X, M = synth_volume(n, n, n, 11)
     vox = (1.0, 1.0, 1.0)
@@ -400,8 +447,12 @@ def test_config5_512_cubed_n4_morph3d():
     n4b, _, _, _, res2 = B.download(n4=True, maps=False)
     B.close()
     assert np.array_equal(n4[0], n4b[0]) and list(res[0].n4_iters) == list(res2[0].n4_iters)
-    its = list(res[0].n4_iters[:4])
-    assert all(1 <= k <= 50 for k in its)
+    fx = np.load(os.path.join(os.path.dirname(__file__), "golden", "n4_512_seed11.npz"))
+    assert list(res[0].n4_iters[:4]) == fx["iters"].tolist()
+    assert np.array_equal(np.float32(res[0].n4_conv[:4]), fx["conv"])
+    flat = n4[0].reshape(-1)
+    assert rel(flat[fx["sample_idx"]], fx["sample_val"]) < 1e-5
+    assert hashlib.sha256(np.ascontiguousarray(n4[0]).tobytes()).hexdigest() == str(fx["sha256"])
     assert np.all(np.isfinite(n4[0])) and np.all((n4[0] > 0) == (X > 0))
     ref = O.calculate_vdp(n4[0], M, vox, morph3d=True)
     assert np.array_equal(d[0], ref["defectArray"])

@@ -77,6 +77,9 @@ _SIGS = {
     "vh_batch_reset_timers": ([_P], ct.c_int),
     "vh_batch_kernel_time": ([_P, ct.c_char_p, ct.POINTER(ct.c_double), ct.POINTER(ct.c_int64),
                               ct.POINTER(ct.c_double)], ct.c_int),
+    "vh_pipe_create": ([_P, _I64, _I64, _I64, _I64, ct.c_int, ct.POINTER(_P)], ct.c_int),
+    "vh_pipe_run": ([_P, _P, _P, _I64, ct.POINTER(RunOpts), _P, _P, _P, _P, _P], ct.c_int),
+    "vh_pipe_destroy": ([_P], ct.c_int),
     "vh_comm_unique_id": ([_P], ct.c_int),
     "vh_comm_init": ([_P, ct.c_int, ct.c_int, _P], ct.c_int),
     "vh_batch_cohort_allreduce": ([_P], ct.c_int),
@@ -354,6 +357,50 @@ class Batch:
         return ms.value, n.value, by.value
 
 
+class Pipe:
+    """Host-to-host pipeline (vh_pipe): n host-resident studies streamed through `slots` device
+    batches of `sub` volumes, transfers of one sub-batch overlapping the compute of another."""
+
+    def __init__(self, R, C, Z, sub, slots=3, device=0):
+        self.ctx = context(device)
+        self.L = self.ctx.L
+        self.vshape = (int(R), int(C), int(Z))
+        h = _P()
+        self.ctx.check(self.L.vh_pipe_create(self.ctx.h, R, C, Z, sub, slots, ct.byref(h)),
+                       "vh_pipe_create")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.vh_pipe_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def run(self, hp, mask, opts: RunOpts, n4=True, maps=True, out=None):
+        """Returns (n4, defect, border, lb, results) host arrays for all len(hp) studies; `out`
+        may pass preallocated (n4, defect, border, lb) arrays."""
+        h = np.ascontiguousarray(hp, dtype=np.float32)
+        m = np.ascontiguousarray(mask, dtype=np.uint8)
+        n = h.shape[0]
+        if h.shape[1:] != self.vshape or m.shape != h.shape:
+            raise ValueError(f"pipe expects (n,) + {self.vshape}")
+        if out is None:
+            out = (np.empty(h.shape, np.float32) if n4 else None,
+                   np.empty(h.shape, np.uint8) if maps else None,
+                   np.empty(h.shape, np.uint8) if maps else None,
+                   np.empty(h.shape, np.uint8) if maps else None)
+        res = (VdpResult * n)()
+        self.ctx.check(self.L.vh_pipe_run(self.h, _ptr(h), _ptr(m), n, ct.byref(opts),
+                                          *[_ptr(a) for a in out], ct.cast(res, ct.c_void_p)),
+                       "vh_pipe_run")
+        return (*out, list(res))
+
+
 def comm_unique_id() -> bytes:
     buf = np.zeros(COMM_ID_BYTES, np.uint8)
     rc = lib().vh_comm_unique_id(_ptr(buf))
@@ -366,3 +413,9 @@ def comm_init(nranks: int, rank: int, uid: bytes, device=0):
     c = context(device)
     buf = np.frombuffer(uid, np.uint8).copy()
     c.check(c.L.vh_comm_init(c.h, nranks, rank, _ptr(buf)), "vh_comm_init")
+
+
+def comm_destroy(device=0):
+    """Releases the context's RCCL communicator (vh_comm_destroy)."""
+    c = context(device)
+    c.L.vh_comm_destroy(c.h)

@@ -248,6 +248,20 @@ static void batch_download(vh_batch *b, float *n4, uint8_t *defect, uint8_t *bor
     if (res) fill_results(b, res);
 }
 
+static void pipe_free(vh_pipe *p) {
+    if (!p) return;
+    for (auto &q : p->slot) {
+        if (q.b) {
+            (void)hipStreamSynchronize(q.b->stream);
+            batch_free(q.b);
+        }
+        if (q.hp) (void)hipHostFree(q.hp);
+        if (q.n4) (void)hipHostFree(q.n4);
+        if (q.u8) (void)hipHostFree(q.u8);
+    }
+    delete p;
+}
+
 // The context's cached scratch batch for the host-buffer entry points (caller holds ctx->mu).
 static vh_batch *scratch_batch(vh_ctx *ctx, int64_t R, int64_t C, int64_t Z, int64_t nb) {
     vh_batch *&s = ctx->scratch;
@@ -555,6 +569,106 @@ int vh_batch_kernel_time(vh_batch *b, const char *name, double *total_ms, int64_
             if (bytes_per_launch) *bytes_per_launch = it->second.bytes_per_launch;
         }
     })
+}
+
+// ---- host-to-host pipeline -------------------------------------------------------------------
+// One host thread per slot; slot s owns batch b[s] (its own stream) and pinned staging, and takes
+// sub-batches s, s + slots, ...  Within a slot the steps are serial (stage in -> H2D -> pipeline ->
+// D2H -> stage out); across slots they overlap, so the copy engines, the host memcpys and the
+// compute of different sub-batches run at the same time.
+int vh_pipe_create(vh_ctx *ctx, int64_t R, int64_t C, int64_t Z, int64_t sub, int slots,
+                   vh_pipe **out) {
+    *out = nullptr;
+    API_TRY(ctx, {
+        if (sub < 1 || slots < 1 || slots > 8) throw VhError{VH_ERR_ARG, "pipe: sub >= 1, 1 <= slots <= 8"};
+        HIP_TRY(hipSetDevice(ctx->device));
+        vh_pipe *p = new vh_pipe;
+        p->ctx = ctx;
+        p->R = R; p->C = C; p->Z = Z; p->sub = sub;
+        const size_t NV = (size_t)sub * R * C * Z;
+        try {
+            for (int s = 0; s < slots; ++s) {
+                p->slot.emplace_back();
+                vh_pipe::Slot &q = p->slot.back();
+                q.b = batch_new(ctx, R, C, Z, sub);
+                HIP_TRY(hipHostMalloc((void **)&q.hp, sizeof(float) * NV));
+                HIP_TRY(hipHostMalloc((void **)&q.n4, sizeof(float) * NV));
+                HIP_TRY(hipHostMalloc((void **)&q.u8, 4 * NV));   // mask, defect, border, lb
+                q.res.resize(sub);
+            }
+        } catch (...) {
+            pipe_free(p);
+            throw;
+        }
+        *out = p;
+    })
+}
+
+int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, const vh_run_opts *opts,
+                float *n4, uint8_t *defect, uint8_t *defect_border, uint8_t *lb, vh_vdp_result *res) {
+    API_TRY(p->ctx, {
+        if (!opts || !hp || !mask || n < 1) throw VhError{VH_ERR_ARG, "pipe: null input or n < 1"};
+        const int64_t V = p->R * p->C * p->Z, sub = p->sub;
+        const int64_t nchunk = (n + sub - 1) / sub;
+        const int slots = (int)p->slot.size();
+        std::vector<VhError> err(slots);
+        std::vector<int> failed(slots, 0);
+        auto work = [&](int s) {
+            vh_pipe::Slot &q = p->slot[s];
+            vh_batch *b = q.b;
+            try {
+                HIP_TRY(hipSetDevice(p->ctx->device));
+                for (int64_t k = s; k < nchunk; k += slots) {
+                    const int64_t v0 = k * sub, cnt = std::min(sub, n - v0);
+                    uint8_t *qm = q.u8, *qd = q.u8 + sub * V, *qb = q.u8 + 2 * sub * V,
+                            *ql = q.u8 + 3 * sub * V;
+                    memcpy(q.hp, hp + v0 * V, sizeof(float) * cnt * V);
+                    memcpy(qm, mask + v0 * V, cnt * V);
+                    for (int64_t i = cnt; i < sub; ++i) {   // ragged tail: repeat the last study
+                        memcpy(q.hp + i * V, hp + (v0 + cnt - 1) * V, sizeof(float) * V);
+                        memcpy(qm + i * V, mask + (v0 + cnt - 1) * V, V);
+                    }
+                    HIP_TRY(hipMemcpyAsync(b->d_hp, q.hp, sizeof(float) * sub * V, hipMemcpyHostToDevice, b->stream));
+                    HIP_TRY(hipMemcpyAsync(b->d_mask, qm, sub * V, hipMemcpyHostToDevice, b->stream));
+                    batch_run(b, *opts, opts->do_n4 ? 0 : 1);
+                    const float *dn4 = opts->do_n4 ? b->d_n4 : b->d_hp;
+                    if (n4) HIP_TRY(hipMemcpyAsync(q.n4, dn4, sizeof(float) * cnt * V, hipMemcpyDeviceToHost, b->stream));
+                    if (defect) HIP_TRY(hipMemcpyAsync(qd, b->d_defect, cnt * V, hipMemcpyDeviceToHost, b->stream));
+                    if (defect_border) HIP_TRY(hipMemcpyAsync(qb, b->d_border, cnt * V, hipMemcpyDeviceToHost, b->stream));
+                    if (lb) HIP_TRY(hipMemcpyAsync(ql, b->d_lb, cnt * V, hipMemcpyDeviceToHost, b->stream));
+                    HIP_TRY(hipStreamSynchronize(b->stream));
+                    if (res) {
+                        fill_results(b, q.res.data());
+                        memcpy(res + v0, q.res.data(), sizeof(vh_vdp_result) * cnt);
+                    }
+                    if (n4) memcpy(n4 + v0 * V, q.n4, sizeof(float) * cnt * V);
+                    if (defect) memcpy(defect + v0 * V, qd, cnt * V);
+                    if (defect_border) memcpy(defect_border + v0 * V, qb, cnt * V);
+                    if (lb) memcpy(lb + v0 * V, ql, cnt * V);
+                }
+            } catch (const VhError &e) {
+                err[s] = e;
+                failed[s] = 1;
+            } catch (const std::exception &e) {
+                err[s] = VhError{VH_ERR_HIP, e.what()};
+                failed[s] = 1;
+            }
+        };
+        std::vector<std::thread> th;
+        for (int s = 1; s < slots; ++s) th.emplace_back(work, s);
+        work(0);
+        for (auto &t : th) t.join();
+        for (int s = 0; s < slots; ++s)
+            if (failed[s]) throw err[s];
+    })
+}
+
+int vh_pipe_destroy(vh_pipe *p) {
+    if (p) {
+        (void)hipSetDevice(p->ctx->device);
+        pipe_free(p);
+    }
+    return VH_OK;
 }
 
 int vh_comm_unique_id(uint8_t id[VH_COMM_ID_BYTES]) {

@@ -1274,14 +1274,8 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
             const size_t fit_lds = sizeof(double) * FIT_WAVES * 2 * FIT_NB * (size_t)rowcap;
             if (fit_lds > 150 * 1024)
                 throw VhError{VH_ERR_ARG, "N4 fit: tile contraction rows exceed the LDS budget"};
-            static bool attr_set = false;
-            if (!attr_set) {
-                HIP_TRY(hipFuncSetAttribute((const void *)k_n4_fit_items<0>,
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));
-                HIP_TRY(hipFuncSetAttribute((const void *)k_n4_fit_items<1>,
-                                            hipFuncAttributeMaxDynamicSharedMemorySize, 150 * 1024));
-                attr_set = true;
-            }
+            vh_set_max_lds((const void *)k_n4_fit_items<0>, 150 * 1024);
+            vh_set_max_lds((const void *)k_n4_fit_items<1>, 150 * 1024);
             const int64_t nlat = (int64_t)ncx * lv.ax[1].ncp * lv.ax[2].ncp;
             const dim3 lg((unsigned)ns, (unsigned)((nlat + VH_TPB - 1) / VH_TPB));
             const dim3 zg((unsigned)((2 * nlat + VH_TPB - 1) / VH_TPB), (unsigned)ns);

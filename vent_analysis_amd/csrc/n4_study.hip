@@ -1015,12 +1015,7 @@ void vh_launch_n4_study(vh_batch *b, const vh_n4_params &prm) {
                            b->stream));
     a.lvs = (const StudyLevels *)b->d_study_lv;
     a.vol0 = 0;
-    static bool attr_set = false;
-    if (!attr_set) {
-        HIP_TRY(hipFuncSetAttribute((const void *)k_n4_study,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, ST_MAX_LDS));
-        attr_set = true;
-    }
+    vh_set_max_lds((const void *)k_n4_study, ST_MAX_LDS);
     ScopedKTimer tm(b, "n4_study", 0.0);
     k_n4_study<<<(unsigned)b->nb, ST_TPB, Ly.bytes, b->stream>>>(a);
     VH_CHECK_LAUNCH();

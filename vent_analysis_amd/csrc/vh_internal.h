@@ -5,7 +5,9 @@
 #include <cstdint>
 #include <cstdio>
 #include <map>
+#include <set>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -33,6 +35,19 @@ struct VhError {
     } while (0)
 
 #define VH_CHECK_LAUNCH() HIP_TRY(hipGetLastError())
+
+// hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device): the attribute is
+// per device, and batches of several contexts / pipeline slots launch from several host threads.
+inline void vh_set_max_lds(const void *fn, int bytes) {
+    static std::mutex m;
+    static std::set<std::pair<const void *, int>> done;
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    std::lock_guard<std::mutex> g(m);
+    if (done.count({fn, dev})) return;
+    HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+    done.insert({fn, dev});
+}
 
 // Per-volume device scalars (one record per study).
 struct VolScalars {
@@ -97,6 +112,18 @@ struct vh_ctx {
     // context; mu serialises them, so a context may be used from several host threads
     vh_batch *scratch = nullptr;
     std::mutex mu;
+};
+
+struct vh_pipe {
+    struct Slot {
+        vh_batch *b = nullptr;
+        float *hp = nullptr, *n4 = nullptr;   // pinned staging [sub][V]
+        uint8_t *u8 = nullptr;                // pinned: mask, defect, border, lb ([4][sub][V])
+        std::vector<vh_vdp_result> res;
+    };
+    vh_ctx *ctx = nullptr;
+    int64_t R = 0, C = 0, Z = 0, sub = 0;
+    std::vector<Slot> slot;
 };
 
 struct vh_batch {
