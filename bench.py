@@ -182,8 +182,8 @@ def host_to_host(R, C, Z, nb, args, device, opts, seed):
 def main_ci(args):
     """CI line: defect-voxels/s and sphere-probes/s of the cluster-index map
     on 128x128x24 studies, host-to-host through vh_ci (defect map in, float64 CI map out).  Two
-    inputs: the seed-0 study's defect map from the GPU pipeline itself (golden-identical), and a
-    clustered map of ~5 900 defects like the one the reference timing used (44.4 s)."""
+    inputs: the seed-0 study's defect map from the GPU pipeline itself (5917 defect voxels, CI
+    22.5: the study BASELINE.md timed at 44.4 s), and a random clustered map of ~6 000 defects."""
     from vent_analysis_amd import _lib
     from vent_analysis_amd.sphere import compact_table, sphere_pix
     from vent_analysis_amd.synth import synth_volume
@@ -217,7 +217,7 @@ def main_ci(args):
         cases[name] = {"defect_voxels": nd, "seconds_per_map": round(dt, 6),
                        "defect_voxels_per_s": round(nd / dt, 1), "sphere_probes_per_s": round(probes / dt, 1),
                        "sphere_probes": probes, "CI": float(sc[0])}
-    head = cases["clustered"]
+    head = cases["seed0_pipeline"]   # 5917 defects, CI 22.5: the study BASELINE.md timed
     line = {"metric": "CI defect-voxels/s (cluster-index map, 128x128x24, host-to-host)",
             "value": head["defect_voxels_per_s"], "unit": "defect-voxels/s", "n_gpus": 1,
             "steps": args.steps, "warmup": args.warmup,
@@ -255,7 +255,7 @@ def main():
                          "cohort all-reduce per step)")
     ap.add_argument("--no-h2h", action="store_true",
                     help="skip the host-to-host pipeline measurement (host_to_host_vol_s)")
-    ap.add_argument("--h2h-batches", type=int, default=4,
+    ap.add_argument("--h2h-batches", type=int, default=6,
                     help="host-to-host sample: this many sub-batches of --batch volumes")
     ap.add_argument("--workload", default="vdp", choices=["vdp", "ci"],
                     help="vdp: the BASELINE metric (default); ci: the cluster-index line")
