@@ -6,20 +6,16 @@
 #include <cstdio>
 #include <vector>
 
-__global__ void __launch_bounds__(192) k_real(const float *D, int64_t n, float *out,
+__global__ void __launch_bounds__(384) k_real(const float *D, int64_t n, float *out,
                                               unsigned long long *cyc) {
     __shared__ ChainSlot slots[CH_SLOTS];
     __shared__ ChainState cs;
-    if (threadIdx.x == 0) {
-        cs.a_done = 0;
-        cs.b_done = 0;
-        cs.c_done = 0;
-    }
+    chain_reset(slots, &cs);
     __syncthreads();
     const unsigned long long t0 = clock64();
     if (threadIdx.x < 64) chain_wave_mu(n, slots, &cs);
     else if (threadIdx.x < 128) chain_wave_sig(n, slots, &cs);
-    else chain_wave_prod(D + blockIdx.x * n, nullptr, n, slots, &cs);
+    else chain_wave_prod(D + blockIdx.x * n, nullptr, n, slots, &cs, (threadIdx.x >> 6) - 2, 4);
     __syncthreads();
     if (threadIdx.x == 0) {
         out[blockIdx.x] = cs.conv;
@@ -47,7 +43,7 @@ int main() {
         (void)hipEventCreate(&e0);
         (void)hipEventCreate(&e1);
         (void)hipEventRecord(e0);
-        k_real<<<nb, 192>>>(d, n, o, c);
+        k_real<<<nb, 384>>>(d, n, o, c);
         (void)hipEventRecord(e1);
         (void)hipEventSynchronize(e1);
         float ms = 0;

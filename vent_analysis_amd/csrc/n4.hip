@@ -1085,22 +1085,21 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_eval(const float *__restrict__ L0
 // S7: ITK's float Welford convergence of the last eval of each active volume (two waves per
 // volume: n4_shared.h chain_wave_mu / chain_wave_sig fed by chain_wave_prod, over the field
 // differences read in raster order through the volume's raster -> compact permutation).
-__global__ void __launch_bounds__(192) k_n4_welford(const float *D, const int32_t *perm, int64_t VS,
-                                                   const VolScalars *sc, N4State *st, int64_t vol0) {
+#define WF_PROD 4   // producer waves of k_n4_welford
+__global__ void __launch_bounds__(64 * (2 + WF_PROD)) k_n4_welford(const float *D, const int32_t *perm,
+                                                                  int64_t VS, const VolScalars *sc,
+                                                                  N4State *st, int64_t vol0) {
     __shared__ ChainSlot slots[CH_SLOTS];
     __shared__ ChainState cs;
     const int64_t b = vol0 + blockIdx.x;
     if (!st[b].active) return;
-    if (threadIdx.x == 0) {
-        cs.a_done = 0;
-        cs.b_done = 0;
-        cs.c_done = 0;
-    }
+    chain_reset(slots, &cs);
     __syncthreads();
     const int64_t n = sc[b].n_mask1;
-    if (threadIdx.x < 64) chain_wave_mu(n, slots, &cs);
-    else if (threadIdx.x < 128) chain_wave_sig(n, slots, &cs);
-    else chain_wave_prod(D + b * VS, perm + b * VS, n, slots, &cs);
+    const int w = threadIdx.x >> 6;
+    if (w == 0) chain_wave_mu(n, slots, &cs);
+    else if (w == 1) chain_wave_sig(n, slots, &cs);
+    else chain_wave_prod(D + b * VS, perm + b * VS, n, slots, &cs, w - 2, WF_PROD);
     __syncthreads();
     if (threadIdx.x == 0) st[b].conv_w = cs.conv;
 }
@@ -1350,7 +1349,7 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
                 }
                 if (cm == 0) {
                     ScopedKTimer tm(b, "n4_welford", 0.0);
-                    k_n4_welford<<<(unsigned)ns, 192, 0, st>>>(b->d_D, b->d_perm, b->VS, b->d_sc,
+                    k_n4_welford<<<(unsigned)ns, 64 * (2 + WF_PROD), 0, st>>>(b->d_D, b->d_perm, b->VS, b->d_sc,
                                                                b->d_st, vol0);
                     VH_CHECK_LAUNCH();
                 }

@@ -457,8 +457,8 @@ __device__ __forceinline__ bool r3_bin_min(const Range3 &r, const float *u, int 
 // ---------------------------------------------------------------------------------------------
 // S7 convergence (conv_mode 0): ITK's float Welford recurrence over the masked voxels in raster
 // order, d_k = B_old - B_new read from a raster-ordered buffer.  Three waves of one workgroup:
-//   producer (C): per block of 64 steps, all lanes compute p = (float)exp((double)d), 1/k, the
-//     mu step constants (1 - 1/k, p/k) and (k-1)/k into an LDS slot;
+//   producers (C, several waves): per block of 64 steps, all lanes compute p = (float)exp((double)d),
+//     1/k, the mu step constants (1 - 1/k, p/k) and (k-1)/k into the block's LDS slot;
 //   wave A (mu): lane 0 runs (pipelined, chain_block64)
 //       mu <- (float)fma((double)mu, 1 - 1/k, (double)(p / k))      (one step per voxel)
 //     recording mu before each step for wave B.
@@ -467,23 +467,46 @@ __device__ __forceinline__ bool r3_bin_min(const Range3 &r, const float *u, int 
 // The recurrences are inherently serial (the float running mean drifts); the slot ring and three
 // LDS counters let the three waves overlap (A and B then do nothing but their steps).  Result: conv = (float)sqrt(sig / (n-1)) / mu.
 // ---------------------------------------------------------------------------------------------
-#define CH_SLOTS 4
+#define CH_SLOTS 16
 struct ChainSlot {
     double2 ab[64];    // (1 - 1/k, p / k) for wave A; (1, 0) past the end (a no-op step)
-    double2 cs[64];    // ((k - 1) / k, (double)(p - mu_prev)^2): c by wave A, s by wave B
+    double2 cs[64];    // ((k - 1) / k, (double)(p - mu_prev)^2): c by the producer, s by wave B
     float p[64];
     float mu[64];      // mu before step k
+    int ready;         // block + 1 once a producer has filled the slot for that block
+    int pad[3];
 };
 struct ChainState {
     int a_done, b_done, c_done;   // blocks finished by wave A / wave B / the producer
     float mu, conv;
+#ifdef CH_PROF
+    unsigned long long wait[3], total[3];   // cycles polling / in the loop: A, B, producer
+#endif
 };
+#ifdef CH_PROF
+#define CH_T0() const unsigned long long _ch_t0 = clock64()
+#define CH_WAIT(w, loop) do { const unsigned long long _t = clock64(); loop; w += clock64() - _t; } while (0)
+#define CH_DONE(i, w) do { if ((threadIdx.x & 63) == 0) { cs->wait[i] = w; cs->total[i] = clock64() - _ch_t0; } } while (0)
+#else
+#define CH_T0() do { } while (0)
+#define CH_WAIT(w, loop) do { (void)(w); loop; } while (0)
+#define CH_DONE(i, w) do { (void)(w); } while (0)
+#endif
 
+// Counter hand-off between waves of one workgroup through LDS only.  LDS executes a wave's DS
+// instructions in order, so a counter written after the data (and read before it) needs no
+// hardware fence -- only a compiler barrier.  (A workgroup-scope atomic release would also wait
+// for this wave's outstanding global loads, vmcnt(0): it serialised the producer's prefetch.)
+// (Relaxed atomics rather than volatile: a volatile access through a generic pointer stays a flat
+// access, which counts against vmcnt too.)
 __device__ __forceinline__ int lds_load_acq(int *p) {
-    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const int v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    asm volatile("" ::: "memory");
+    return v;
 }
 __device__ __forceinline__ void lds_store_rel(int *p, int v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    asm volatile("" ::: "memory");
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
 // ---- the 64 serial steps of one block on lane 0, software-pipelined -------------------------
@@ -614,48 +637,34 @@ __device__ __forceinline__ double chain_block64(const double2 *q, float *murec, 
 // the mu step constants (1 - 1/k, p / k) and (k - 1) / k into the block's LDS slot, up to CH_SLOTS
 // blocks ahead of wave B.  The n d values are in raster order: Dr[k] (perm == nullptr), else
 // Dr[perm[k]]; a block's values are loaded CH_PF blocks ahead (its perm entries 2 CH_PF ahead).
-#define CH_PF 8
+// np producer waves share the blocks round-robin (producer pid takes blk = pid mod np): one wave
+// took ~3.3k cycles per block (its global loads wait at every hand-off), several keep the serial
+// waves fed.  Each prefetches its next block's d (and perm entries two blocks ahead) while it
+// processes the current one.
 __device__ void chain_wave_prod(const float *Dr, const int32_t *perm, int64_t n, ChainSlot *slots,
-                                ChainState *cs) {
+                                ChainState *cs, int pid, int np) {
     const int lane = threadIdx.x & 63;
     const int64_t nblk = (n + 63) / 64;
-    float dq[CH_PF];
-    int32_t pq[2 * CH_PF];
-    if (perm) {
-#pragma unroll
-        for (int i = 0; i < 2 * CH_PF; ++i) {
-            const int64_t j = (int64_t)i * 64 + lane;
-            pq[i] = j < n ? perm[j] : 0;
-        }
-#pragma unroll
-        for (int i = 0; i < CH_PF; ++i) {
-            const int64_t j = (int64_t)i * 64 + lane;
-            dq[i] = j < n ? Dr[pq[i]] : 0.0f;
-        }
-    } else {
-#pragma unroll
-        for (int i = 0; i < CH_PF; ++i) {
-            const int64_t j = (int64_t)i * 64 + lane;
-            dq[i] = j < n ? Dr[j] : 0.0f;
-        }
-    }
+    int64_t blk = pid;
+    auto ld_perm = [&](int64_t b) -> int32_t {
+        const int64_t j = b * 64 + lane;
+        return perm && j < n ? perm[j] : 0;
+    };
+    auto ld_d = [&](int64_t b, int32_t pj) -> float {
+        const int64_t j = b * 64 + lane;
+        return j < n ? Dr[perm ? (int64_t)pj : j] : 0.0f;
+    };
+    int32_t p1 = ld_perm(blk + np);
+    float dnext = ld_d(blk, ld_perm(blk));
     int bseen = 0;   // last b_done read: slots of blocks < bseen + CH_SLOTS are free
-    for (int64_t blk = 0; blk < nblk; ++blk) {
+    unsigned long long wt = 0;
+    CH_T0();
+    for (; blk < nblk; blk += np) {
         ChainSlot &S = slots[blk % CH_SLOTS];
         const int64_t j = blk * 64 + lane;
-        const float d = dq[0];
-#pragma unroll
-        for (int i = 0; i < CH_PF - 1; ++i) dq[i] = dq[i + 1];
-        const int64_t jd = j + 64 * CH_PF;
-        if (perm) {
-            dq[CH_PF - 1] = jd < n ? Dr[pq[CH_PF]] : 0.0f;
-#pragma unroll
-            for (int i = 0; i < 2 * CH_PF - 1; ++i) pq[i] = pq[i + 1];
-            const int64_t jp = j + 2 * 64 * CH_PF;
-            pq[2 * CH_PF - 1] = jp < n ? perm[jp] : 0;
-        } else {
-            dq[CH_PF - 1] = jd < n ? Dr[jd] : 0.0f;
-        }
+        const float d = dnext;
+        dnext = ld_d(blk + np, p1);
+        p1 = ld_perm(blk + 2 * np);
         const bool ok = j < n;
         const float p = expf_cr(d);
         const double kd = (double)(j + 1);
@@ -664,12 +673,24 @@ __device__ void chain_wave_prod(const float *Dr, const int32_t *perm, int64_t n,
                               : make_double2(1.0, 0.0);
         const double c = (kd - 1.0) / kd;
         if (blk >= CH_SLOTS + bseen)
-            while ((bseen = lds_load_acq(&cs->b_done)) <= (int)(blk - CH_SLOTS)) __builtin_amdgcn_s_sleep(1);
+            CH_WAIT(wt, while ((bseen = lds_load_acq(&cs->b_done)) <= (int)(blk - CH_SLOTS)) __builtin_amdgcn_s_sleep(1));
         S.ab[lane] = ab;
         S.cs[lane] = make_double2(c, 0.0);
         S.p[lane] = p;
         wave_lds_order();
-        if (lane == 0) lds_store_rel(&cs->c_done, (int)(blk + 1));
+        if (lane == 0) lds_store_rel(&S.ready, (int)(blk + 1));
+    }
+    if (pid == 0) CH_DONE(2, wt);
+}
+
+// Before a chain: every slot's ready flag cleared (a flag left from the previous chain could name
+// the same block).  Threads [0, CH_SLOTS) of the workgroup, then a workgroup barrier.
+__device__ __forceinline__ void chain_reset(ChainSlot *slots, ChainState *cs) {
+    if (threadIdx.x < CH_SLOTS) slots[threadIdx.x].ready = 0;
+    if (threadIdx.x == 0) {
+        cs->a_done = 0;
+        cs->b_done = 0;
+        cs->c_done = 0;
     }
 }
 
@@ -679,11 +700,11 @@ __device__ void chain_wave_mu(int64_t n, ChainSlot *slots, ChainState *cs) {
     const int lane = threadIdx.x & 63;
     double mu = 0.0;
     const int64_t nblk = (n + 63) / 64;
-    int cseen = 0;   // last c_done read
+    unsigned long long wt = 0;
+    CH_T0();
     for (int64_t blk = 0; blk < nblk; ++blk) {
         ChainSlot &S = slots[blk % CH_SLOTS];
-        if (blk >= cseen)
-            while ((cseen = lds_load_acq(&cs->c_done)) <= (int)blk) __builtin_amdgcn_s_sleep(1);
+        CH_WAIT(wt, while (lds_load_acq(&S.ready) != (int)(blk + 1)) __builtin_amdgcn_s_sleep(1));
         if (lane == 0) mu = chain_block64<true, GS>(S.ab, S.mu, mu);
         wave_lds_order();
         if (lane == 0) {
@@ -691,6 +712,7 @@ __device__ void chain_wave_mu(int64_t n, ChainSlot *slots, ChainState *cs) {
             lds_store_rel(&cs->a_done, (int)(blk + 1));
         }
     }
+    CH_DONE(0, wt);
 }
 
 // wave B.  Returns conv in cs->conv.
@@ -699,10 +721,12 @@ __device__ void chain_wave_sig(int64_t n, ChainSlot *slots, ChainState *cs) {
     const int lane = threadIdx.x & 63;
     double sig = 0.0;
     const int64_t nblk = (n + 63) / 64;
+    unsigned long long wt = 0;
+    CH_T0();
     for (int64_t blk = 0; blk < nblk; ++blk) {
         ChainSlot &S = slots[blk % CH_SLOTS];
         const int64_t j = blk * 64 + lane;
-        while (lds_load_acq(&cs->a_done) <= (int)blk) __builtin_amdgcn_s_sleep(1);
+        CH_WAIT(wt, while (lds_load_acq(&cs->a_done) <= (int)blk) __builtin_amdgcn_s_sleep(1));
         const float q = S.p[lane] - S.mu[lane];
         // k = 1 adds nothing (ITK's N > 1 test), nor do the steps past the end: (0, 0) is a no-op
         const bool ok = j < n && j > 0;
@@ -712,6 +736,7 @@ __device__ void chain_wave_sig(int64_t n, ChainSlot *slots, ChainState *cs) {
         wave_lds_order();
         if (lane == 0) lds_store_rel(&cs->b_done, (int)(blk + 1));
     }
+    CH_DONE(1, wt);
     if (lane == 0) {
         while (lds_load_acq(&cs->a_done) < (int)nblk) __builtin_amdgcn_s_sleep(1);
         const float mu = cs->mu;

@@ -32,6 +32,9 @@
 #define ST_WAVES (ST_TPB / 64)
 #define ST_HC 8        // LDS histogram copies
 #define ST_MAX_LDS (160 * 1024)
+#ifndef ST_CH_PROD
+#define ST_CH_PROD 8   // producer waves of the convergence chain (n4_shared.h chain_wave_prod)
+#endif
 #ifndef ST_CH_GS
 #define ST_CH_GS 8   // convergence-chain group size here (n4_shared.h ch_group): 8 measured 135M vs 167M cycles for 4
 #endif
@@ -576,6 +579,9 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
 #ifdef ST_PROF
     unsigned long long st_prof[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_t0 = clock64();
 #endif
+#ifdef CH_PROF
+    unsigned long long ch_w[3] = {0, 0, 0}, ch_t[3] = {0, 0, 0};
+#endif
     for (int L = 0; L < a.nlev; ++L) {
         const DevLevel &lv = a.lvs->lv[L];
         char *tabp = smem + ((L & 1) ? a.o_tab1 : a.o_tab0);
@@ -834,18 +840,15 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                     }
                 }
             }
-            if (t == 0) {
-                M.ch.a_done = 0;
-                M.ch.b_done = 0;
-                M.ch.c_done = 0;
-            }
+            chain_reset(slots, &M.ch);
             __syncthreads();
             ST_MARK(6);
             // ---- convergence of this iteration ----
             if (a.conv_mode == 0) {   // S7: ITK's float Welford recurrence, two waves
                 if (wv == 0) chain_wave_mu<ST_CH_GS>(n, slots, &M.ch);
                 else if (wv == 1) chain_wave_sig<ST_CH_GS>(n, slots, &M.ch);
-                else if (wv == 2) chain_wave_prod(Db, nullptr, n, slots, &M.ch);
+                else if (wv < 2 + ST_CH_PROD)
+                    chain_wave_prod(Db, nullptr, n, slots, &M.ch, wv - 2, ST_CH_PROD);
             } else if (wv == 0) {   // S7x: item partials in item order
                 double sd = 0.0, sd2 = 0.0;
                 for (int i = lane; i < a.nitems; i += 64) {
@@ -863,6 +866,13 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
             }
             cur ^= 1;
             ST_MARK(7);
+#ifdef CH_PROF
+            if (t == 0 && a.conv_mode == 0)
+                for (int i = 0; i < 3; ++i) {
+                    ch_w[i] += M.ch.wait[i];
+                    ch_t[i] += M.ch.total[i];
+                }
+#endif
         }
         if (t == 0) {
             stb->iters_level[L] = itn;
@@ -885,6 +895,11 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
         printf("ST_PROF den %llu ctrl %llu hist %llu emap %llu fit %llu latP1 %llu eval %llu "
                "conv %llu level %llu\n", st_prof[0], st_prof[1], st_prof[2], st_prof[3], st_prof[4],
                st_prof[5], st_prof[6], st_prof[7], st_prof[8]);
+#endif
+#ifdef CH_PROF
+    if (t == 0 && blockIdx.x == 0)
+        printf("CH_PROF A wait %llu total %llu | B wait %llu total %llu | C wait %llu total %llu\n",
+               ch_w[0], ch_t[0], ch_w[1], ch_t[1], ch_w[2], ch_t[2]);
 #endif
     // final field's P1 for k_n4_final
     const double *P1f = cur ? P1b1 : P1b0;
