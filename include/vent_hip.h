@@ -15,6 +15,8 @@
  *   vh_border    Vent_Analysis.calculateBorder               Vent_Analysis.py:225-231
  *   vh_vdp       Vent_Analysis.calculate_VDP (post-N4 part)  Vent_Analysis.py:239-263
  *   vh_ci        CI.calculate_CI + Vent_Analysis.calculate_CI CI.py:107-145, Vent_Analysis.py:265-271
+ *   vh_overlay   Vent_Analysis.exportDICOM (pixel data)       Vent_Analysis.py:381-428
+ *   vh_montage   Vent_Analysis.screenShot (montage array)     Vent_Analysis.py:458-520
  *   vh_batch_*   the same pipeline over a device-resident batch of studies (build-defined)
  *   vh_pipe_*    the batch pipeline fed from host memory with overlapped transfers (build-defined)
  *   vh_comm_*    cohort histogram all-reduce over RCCL (build-defined, BASELINE config 4)
@@ -39,6 +41,7 @@ extern "C" {
 #define VH_ERR_EMPTY 5        /* empty mask / defect list (Vent_Analysis.py:270 IndexError) */
 #define VH_ERR_RCCL 6         /* RCCL failure */
 #define VH_ERR_NODEV 7        /* no GPU visible */
+#define VH_ERR_INDEX 8        /* index out of range (maps to IndexError): screenShot's parula lookup */
 
 typedef struct vh_ctx vh_ctx;
 typedef struct vh_batch vh_batch;
@@ -154,6 +157,24 @@ const char *vh_batch_kernel_names(void);
 int vh_batch_reset_timers(vh_batch *b);
 int vh_batch_kernel_time(vh_batch *b, const char *name, double *total_ms, int64_t *launches,
                          double *bytes_per_launch);
+
+/* ---- rendering after the hot path ---------------------------------- */
+/* exportDICOM's pixel data (Vent_Analysis.py:387-393): BW = uint8(normalize(|N4HPvent|) * 255) in
+ * float32, RGB = (BW*(defect==0) + 255*(defect==1), BW*(defect==0), BW*(defect==0)).  n4 float32
+ * and defect uint8 volumes [batch][R][C][Z]; rgb uint8 [batch][Z][R][C][3] -- the frame order of
+ * np.transpose(RGB, (2,0,1,3)) (:393) and, frame by frame, the PACS branch's RGB[:,:,i,:] (:411). */
+int vh_overlay(vh_ctx *ctx, const float *n4, const uint8_t *defect, int64_t R, int64_t C, int64_t Z,
+               int64_t batch, uint8_t *rgb);
+/* screenShot's montage array (Vent_Analysis.py:467-495) before the text overlay: the 7 x ns grid
+ * (blank, blank, proton, HPvent, N4 + mask border, N4 + defects, N4 + parula CI) over the crop
+ * crop = {r0, nr, c0, nc, s0, ns} (cropToData(mask, border=5), :430-456), as uint8(IMAGE * 255)
+ * [7 nr][ns nc][3].  proton / hp are float32 (is64 = 0) or float64 (is64 = 1); ci float64 or NULL
+ * (the reference's blank CI panel); parula float64 [prow][3].  A CI colour index outside the table
+ * returns VH_ERR_INDEX (IndexError), a NaN CI VH_ERR_ARG (ValueError). */
+int vh_montage(vh_ctx *ctx, int64_t R, int64_t C, int64_t Z, const void *proton, int proton_is64,
+               const void *hp, int hp_is64, const float *n4, const uint8_t *mask_border,
+               const uint8_t *defect, const double *ci, const double *parula, int64_t prow,
+               const int64_t crop[6], uint8_t *image);
 
 /* ---- host-to-host pipeline ------------------------------------------------------------------ */
 /* Streams n host-resident studies through `slots` device batches of `sub` volumes each (one HIP

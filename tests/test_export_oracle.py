@@ -1,0 +1,70 @@
+"""CPU: the rendering restatement (oracle/export_oracle.py -- parity unpinned, see its header)
+against properties that follow from the cited reference lines by hand."""
+import os
+
+import numpy as np
+
+from oracle import export_oracle as E
+
+PARULA = np.linspace(0.0, 1.0, 64 * 3).reshape(64, 3)   # stand-in colour table (64 rows)
+
+
+def _case(R=20, C=18, Z=6, seed=0):
+    rng = np.random.default_rng(seed)
+    i, j, k = np.meshgrid(np.arange(R), np.arange(C), np.arange(Z), indexing="ij")
+    mask = (((i - R / 2) / (0.35 * R)) ** 2 + ((j - C / 2) / (0.3 * C)) ** 2 <= 1) & (k >= 1) & (k < Z - 1)
+    n4 = (rng.normal(10, 4, (R, C, Z)) * mask).astype(np.float32)
+    defect = (mask & (rng.random((R, C, Z)) < 0.2)).astype(np.float64)
+    return mask, n4, defect
+
+
+def test_overlay_rgb_properties():
+    mask, n4, defect = _case()
+    n4[0, 0, 0] = -30.0                      # |x| is what is normalised
+    rgb = E.overlay_rgb(n4, defect)
+    assert rgb.shape == (n4.shape[2], n4.shape[0], n4.shape[1], 3) and rgb.dtype == np.uint8
+    a = np.abs(n4)
+    bw = ((a - a.min()) / (a.max() - a.min()) * 255).astype(np.uint8)
+    d = np.transpose(defect, (2, 0, 1)) == 1
+    bwt = np.transpose(bw, (2, 0, 1))
+    assert np.array_equal(rgb[..., 0], np.where(d, 255, bwt))
+    assert np.array_equal(rgb[..., 1], np.where(d, 0, bwt)) and np.array_equal(rgb[..., 1], rgb[..., 2])
+    assert rgb[0, 0, 0, 0] == 255 or d[0, 0, 0]   # the largest |x| maps to 255
+    flat = E.overlay_rgb(np.full_like(n4, 2.0), defect)   # max == min: normalize returns x, so
+    wrapped = np.array([2.0 * 255], np.float32).astype(np.uint8)[0]   # 510 -> numpy's wrap
+    assert np.all(flat[..., 1][~d] == wrapped)
+
+
+def test_crop_to_data_index0_quirk():
+    A = np.zeros((10, 12, 5))
+    A[0, 3, 2] = 1                            # row 0 never counts (multiplied by its index 0)
+    A[4, 0, 3] = 1                            # col 0 never counts
+    rr, cc, ss = E.crop_to_data(A, border=1)
+    assert rr == list(range(3, 6)) and cc == list(range(2, 5)) and ss == [2, 3]
+
+
+def test_screenshot_layout_and_panels():
+    mask, n4, defect = _case(seed=2)
+    rng = np.random.default_rng(3)
+    hp = rng.gamma(3.0, 2.0, n4.shape).astype(np.float32)
+    proton = rng.normal(100, 20, n4.shape)
+    mb = np.zeros(n4.shape)
+    mb[5, 5, :] = 1
+    ci = np.where(defect > 0, rng.uniform(0.5, 39.0, n4.shape), 0.0)
+    img = E.screenshot_image(proton, hp, n4, mask.astype(float), mb, defect, ci, PARULA)
+    rr, cc, ss = E.crop_to_data(mask.astype(float), border=5)
+    nr, nc, ns = len(rr), len(cc), len(ss)
+    assert img.shape == (7 * nr, ns * nc, 3) and img.dtype == np.uint8
+    assert not img[: 2 * nr].any()           # two blank panel rows
+    p = img[2 * nr:3 * nr]
+    assert np.array_equal(p[..., 0], p[..., 1]) and p.max() == 255 and p.min() == 0
+    ix = np.ix_(rr, cc, ss)
+    t = (ci[ix] * 64 / 40).astype(np.int64)
+    red = img[6 * nr:7 * nr].reshape(nr, ns, nc, 3).transpose(0, 2, 1, 3)[..., 0]
+    on = ci[ix] > 0
+    assert np.array_equal(red[on], np.uint8(PARULA[t[on], 0] * 255))
+    try:
+        E.screenshot_image(proton, hp, n4, mask.astype(float), mb, defect, ci * 3, PARULA)
+        raise AssertionError("expected IndexError")
+    except IndexError:
+        pass

@@ -579,3 +579,65 @@ def test_sorted_statistics_adversarial(kind):
         bi = np.minimum((nv[sel] * np.float32(_lib.COHORT_BINS / 1.5)).astype(np.int64), 1023)
         exp_h += np.bincount(bi, minlength=_lib.COHORT_BINS).astype(np.uint64)
     assert np.array_equal(h, exp_h)
+
+
+# ---- rendering after the hot path (oracle parity unpinned) -----------
+def _render_case(R, C, Z, seed):
+    rng = np.random.default_rng(seed)
+    i, j, k = np.meshgrid(np.arange(R), np.arange(C), np.arange(Z), indexing="ij")
+    mask = (((i - R / 2) / (0.35 * R)) ** 2 + ((j - C / 2) / (0.3 * C)) ** 2 <= 1) & (k >= 1) & (k < Z - 1)
+    n4 = (rng.normal(10, 4, (R, C, Z)) * mask).astype(np.float32)
+    n4[0, 0, 0] = -25.0
+    defect = (mask & (rng.random((R, C, Z)) < 0.2)).astype(np.float64)
+    hp = rng.gamma(3.0, 2.0, (R, C, Z)).astype(np.float32)
+    proton = rng.normal(100, 20, (R, C, Z))
+    mb = np.zeros((R, C, Z))
+    mb[1:-1, 1:-1] = (mask[2:, 1:-1] != mask[:-2, 1:-1]) | (mask[1:-1, 2:] != mask[1:-1, :-2])
+    ci = np.where(defect > 0, rng.uniform(0.0, 39.9, (R, C, Z)), 0.0)
+    return mask.astype(np.float64), n4, defect, hp, proton, mb, ci
+
+
+@pytest.mark.parametrize("shape,seed", [((40, 36, 9), 1), ((33, 50, 7), 2), ((128, 128, 24), 3)])
+def test_overlay_vs_oracle(shape, seed):
+    from oracle import export_oracle as E
+    _, n4, defect, *_ = _render_case(*shape, seed)
+    assert np.array_equal(_lib.overlay(n4, defect), E.overlay_rgb(n4, defect))
+    flat = np.full_like(n4, 2.0)   # max == min: normalize returns x (uint8 wrap of 510)
+    assert np.array_equal(_lib.overlay(flat, defect), E.overlay_rgb(flat, defect))
+    d2 = defect.copy()
+    d2[d2 > 0] = 2.0               # defect values other than 0/1: neither branch of :389
+    assert np.array_equal(_lib.overlay(n4, d2), E.overlay_rgb(n4, d2))
+
+
+@pytest.mark.parametrize("shape,seed", [((40, 36, 9), 1), ((33, 50, 7), 2), ((128, 128, 24), 3)])
+def test_montage_vs_oracle(shape, seed):
+    from oracle import export_oracle as E
+    mask, n4, defect, hp, proton, mb, ci = _render_case(*shape, seed)
+    pal = np.linspace(0.0, 1.0, 64 * 3).reshape(64, 3)
+    rr, cc, ss = E.crop_to_data(mask, border=5)
+    crop = (rr[0], len(rr), cc[0], len(cc), ss[0], len(ss))
+    for c in (ci, None):
+        got = _lib.montage(proton, hp, n4, mb, defect, c, pal, crop)
+        assert np.array_equal(got, E.screenshot_image(proton, hp, n4, mask, mb, defect, c, pal))
+    with pytest.raises(IndexError):   # int(CI * 64 / 40) past the 64-row table
+        _lib.montage(proton, hp, n4, mb, defect, ci * 2, pal, crop)
+
+
+def test_export_class_methods(tmp_path):
+    from oracle import export_oracle as E
+    from vent_analysis_amd import Vent_Analysis
+    from vent_analysis_amd import dicom
+    mask, n4, defect, hp, proton, mb, ci = _render_case(48, 40, 8, 4)
+    v = Vent_Analysis(xenon_array=hp, mask_array=mask, proton_array=proton, vox=(1.5, 1.5, 10.0))
+    v.calculate_VDP()
+    rgb = v.exportDICOM(None)
+    assert np.array_equal(rgb, E.overlay_rgb(v.N4HPvent, v.defectArray))
+    ds = dicom.Dataset()
+    v.exportDICOM(ds, save_dir=str(tmp_path), forPACS=False)
+    back = dicom.dcmread(tmp_path / f"{v.metadata['PatientName']}_defectDICOM.dcm")
+    assert back.Rows == 48 and back.NumberOfFrames == 8 and back["PixelData"].value == rgb.tobytes()
+    pal = np.linspace(0.0, 1.0, 64 * 3).reshape(64, 3)
+    img = v.screenShot(path=str(tmp_path / "shot.png"), parula=pal)
+    exp = E.screenshot_image(v.proton, v.HPvent, v.N4HPvent, v.mask, v.mask_border, v.defectArray,
+                             None, pal)
+    assert np.array_equal(img, exp) and (tmp_path / "shot.png").exists()

@@ -232,10 +232,14 @@ class Vent_Analysis:
         return dataArray
 
     def cropToData(self, A, border=0, borderSlices=False):
-        """Vent_Analysis.py:430-456."""
-        slices = [x for x in range(A.shape[2]) if np.sum(A[:, :, x]) > 0]
-        rows = [x for x in range(A.shape[0]) if np.sum(A[x, :, :]) > 0]
-        cols = [x for x in range(A.shape[1]) if np.sum(A[:, x, :]) > 0]
+        """Vent_Analysis.py:430-456, including its quirk: the per-axis "non-empty" flags are
+        multiplied by the index list, so index 0 never counts as non-empty."""
+        fs = np.multiply(np.sum(np.sum(A, axis=0), axis=0) > 0, list(range(0, A.shape[2])))
+        fr = np.multiply(np.sum(np.sum(A, axis=1), axis=1) > 0, list(range(0, A.shape[0])))
+        fc = np.multiply(np.sum(np.sum(A, axis=2), axis=0) > 0, list(range(0, A.shape[1])))
+        slices = [x for x in range(A.shape[2]) if fs[x]]
+        rows = [x for x in range(A.shape[0]) if fr[x]]
+        cols = [x for x in range(A.shape[1]) if fc[x]]
         if borderSlices:
             s0, s1 = max(slices[0] - border, 0), min(slices[-1] + border + 1, A.shape[2])
         else:
@@ -280,13 +284,80 @@ class Vent_Analysis:
         except Exception:
             print('\033[31mCould not Export 4D HPvent mask Nifti...\033[37m')
 
-    def exportDICOM(self, *a, **k):
-        raise NotImplementedError("defect-overlay DICOM export (Vent_Analysis.py:381-428) is a "
-                                  "next row (SURVEY §8f rank 3)")
+    def exportDICOM(self, ds, save_dir='C:/PIRL/data/', optional_text='', forPACS=True):
+        """Vent_Analysis.py:381-428.  The RGB defect overlay is rendered on the GPU (vh_overlay,
+        csrc/export.hip) and returned as uint8 [slices][rows][cols][3]; with a dataset ``ds``
+        (vent_analysis_amd.dicom.Dataset, or any object with pydicom-style attributes and
+        save_as) the reference's files are written: one multi-frame RGB object (forPACS=False,
+        :393-404) or one file per slice under save_dir/defectDICOMS (:405-428)."""
+        if self.metadata['VDP'] == '':
+            print('\033[31mCant export dicoms until you run calculate_VDP()...\033[37m')
+            return None
+        rgb = _lib.overlay(np.asarray(self.N4HPvent), np.asarray(self.defectArray),
+                           device=self.device)
+        if ds is None:
+            return rgb
+        from .dicom import generate_uid
+        desc = f"{optional_text} - VDP: {np.round(self.metadata['VDP'], 1)}"
+        R, C, Z = np.shape(self.N4HPvent)
+        if forPACS is False:
+            ds.PhotometricInterpretation = 'RGB'
+            ds.SamplesPerPixel = 3
+            ds.Rows, ds.Columns, ds.NumberOfFrames = R, C, Z
+            ds.BitsAllocated = ds.BitsStored = 8
+            ds.HighBit = 7
+            ds.SOPInstanceUID = ds.SeriesInstanceUID = generate_uid()
+            ds.PixelData = rgb.tobytes()
+            ds.SeriesDescription = desc
+            save_path = os.path.join(save_dir, f"{self.metadata['PatientName']}_defectDICOM.dcm")
+            ds.save_as(save_path)
+            print(f'\033[32mdefect DICOM saved to {save_path}\033[37m')
+        else:
+            try:   # the reference re-keys the study's own header (:406-407)
+                self.ds.SeriesInstanceUID = generate_uid()
+            except AttributeError:   # array-constructed object: self.ds is ''
+                pass
+            dicom_path = os.path.join(save_dir, 'defectDICOMS')
+            os.makedirs(dicom_path, exist_ok=True)
+            for i in range(Z):
+                ds.BitsAllocated = 8
+                ds.PixelData = rgb[i].tobytes()
+                ds.Rows, ds.Columns = R, C
+                ds.SamplesPerPixel = 3
+                ds.PhotometricInterpretation = 'RGB'
+                ds.BitsStored = 8
+                ds.SeriesDescription = desc
+                ds.InstanceNumber = i + 1
+                ds.SliceLocation = i
+                ds.SOPInstanceUID = generate_uid()
+                ds.NumberOfFrames = 1
+                ds.save_as(os.path.join(dicom_path, f"dicom_{i}.dcm"))
+        return rgb
 
-    def screenShot(self, *a, **k):
-        raise NotImplementedError("montage rendering (Vent_Analysis.py:458-520) is a next row "
-                                  "(SURVEY §8f rank 3)")
+    def screenShot(self, path='C:/PIRL/data/screenShotTest.png', normalize95=False, parula=None):
+        """Vent_Analysis.py:458-520: the 7-row montage (blank, blank, proton, HPvent, N4 + mask
+        border, N4 + defects, N4 + parula CI) over cropToData(mask, border=5), rendered on the
+        GPU (vh_montage) as the uint8(IMAGE * 255) array, returned and -- when PIL is present --
+        saved as PNG.  parula: the 64 x 3 colour table the reference loads from
+        'C:\\PIRL\\data\\parula.np.npy' (same default path).  The text annotations need the
+        reference's arial.ttf and are not drawn."""
+        if parula is None:
+            parula = np.load('C:\\PIRL\\data\\parula.np.npy', allow_pickle=False)
+        _, rr, cc, ss = self.cropToData(self.mask, border=5)
+        crop = (rr[0], len(rr), cc[0], len(cc), ss[0], len(ss))
+        ci = None if isinstance(self.CIarray, str) else np.asarray(self.CIarray)
+        proton = self.proton if not isinstance(self.proton, str) else np.zeros_like(self.HPvent)
+        img = _lib.montage(np.asarray(proton), np.asarray(self.HPvent), np.asarray(self.N4HPvent),
+                           np.asarray(self.mask_border), np.asarray(self.defectArray), ci,
+                           np.asarray(parula), crop, device=self.device)
+        try:
+            from PIL import Image
+        except ImportError:
+            return img
+        if path:
+            Image.fromarray(img).save(path, 'PNG')
+            print(f'\033[32mScreenshot saved to {path}\033[37m')
+        return img
 
     def process_RAW(self, *a, **k):
         raise NotImplementedError("TWIX recon (Vent_Analysis.py:522-540) is disabled in the "

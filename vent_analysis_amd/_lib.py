@@ -16,7 +16,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("VH_LIB_PATH") or os.path.join(HERE, "libventhip.so")   # override: A/B builds
 
 VH_OK, VH_ERR_ARG, VH_ERR_HIP, VH_ERR_NOMEM, VH_ERR_MAXRADIUS, VH_ERR_EMPTY, VH_ERR_RCCL, \
-    VH_ERR_NODEV = range(8)
+    VH_ERR_NODEV, VH_ERR_INDEX = range(9)
 COHORT_BINS = 1024
 COMM_ID_BYTES = 128
 
@@ -77,6 +77,9 @@ _SIGS = {
     "vh_batch_reset_timers": ([_P], ct.c_int),
     "vh_batch_kernel_time": ([_P, ct.c_char_p, ct.POINTER(ct.c_double), ct.POINTER(ct.c_int64),
                               ct.POINTER(ct.c_double)], ct.c_int),
+    "vh_overlay": ([_P, _P, _P, _I64, _I64, _I64, _I64, _P], ct.c_int),
+    "vh_montage": ([_P, _I64, _I64, _I64, _P, ct.c_int, _P, ct.c_int, _P, _P, _P, _P, _P, _I64, _P,
+                    _P], ct.c_int),
     "vh_pipe_create": ([_P, _I64, _I64, _I64, _I64, ct.c_int, ct.POINTER(_P)], ct.c_int),
     "vh_pipe_run": ([_P, _P, _P, _I64, ct.POINTER(RunOpts), _P, _P, _P, _P, _P], ct.c_int),
     "vh_pipe_destroy": ([_P], ct.c_int),
@@ -144,7 +147,7 @@ class Context:
         text = f"{where}: {self.L.vh_status_string(rc).decode()}: {msg}"
         if rc == VH_ERR_MAXRADIUS:
             raise ValueError(text)
-        if rc == VH_ERR_EMPTY:
+        if rc in (VH_ERR_EMPTY, VH_ERR_INDEX):
             raise IndexError(text)
         if rc == VH_ERR_ARG:
             raise ValueError(text)
@@ -268,6 +271,45 @@ def ci(defect, table, minvox, device=0):
                       _ptr(table.bounds), _ptr(table.radii), table.bounds.shape[0],
                       ct.c_double(minvox), _ptr(out), _ptr(sc), _ptr(shell)), "vh_ci")
     return out, sc, shell
+
+
+def overlay(n4, defect, device=0):
+    """exportDICOM pixel data (vh_overlay): uint8 [B][Z][R][C][3] for (B, R, C, Z) inputs (a
+    single volume gives [Z][R][C][3])."""
+    c = context(device)
+    single = np.ndim(n4) == 3
+    n = as_batch(n4, np.float32)
+    d = as_batch(defect, np.uint8) if np.asarray(defect).dtype == np.uint8 else \
+        as_batch(np.where(np.asarray(defect) == 1, 1, np.where(np.asarray(defect) == 0, 0, 2)), np.uint8)
+    B, R, C, Z = n.shape
+    out = np.empty((B, Z, R, C, 3), np.uint8)
+    c.check(c.L.vh_overlay(c.h, _ptr(n), _ptr(d), R, C, Z, B, _ptr(out)), "vh_overlay")
+    return out[0] if single else out
+
+
+def montage(proton, hp, n4, mask_border, defect, ci, parula, crop, device=0):
+    """screenShot's montage array (vh_montage): uint8 [7 nr][ns nc][3].  crop = (r0, nr, c0, nc,
+    s0, ns); ci None = the blank CI panel."""
+    c = context(device)
+
+    def fl(a):
+        a = np.asarray(a)
+        if a.dtype == np.float64:
+            return np.ascontiguousarray(a), 1
+        return np.ascontiguousarray(a, dtype=np.float32), 0
+    p, p64 = fl(proton)
+    h, h64 = fl(hp)
+    n = np.ascontiguousarray(n4, dtype=np.float32)
+    R, C, Z = n.shape
+    mb = np.ascontiguousarray(np.asarray(mask_border) != 0, dtype=np.uint8)
+    df = np.ascontiguousarray(np.asarray(defect) != 0, dtype=np.uint8)
+    ci64 = None if ci is None else np.ascontiguousarray(ci, dtype=np.float64)
+    pal = np.ascontiguousarray(parula, dtype=np.float64)
+    cr = np.ascontiguousarray(crop, dtype=np.int64)
+    img = np.empty((7 * int(cr[1]), int(cr[5]) * int(cr[3]), 3), np.uint8)
+    c.check(c.L.vh_montage(c.h, R, C, Z, _ptr(p), p64, _ptr(h), h64, _ptr(n), _ptr(mb), _ptr(df),
+                           _ptr(ci64), _ptr(pal), pal.shape[0], _ptr(cr), _ptr(img)), "vh_montage")
+    return img
 
 
 class Batch:

@@ -292,6 +292,7 @@ const char *vh_status_string(int s) {
         case VH_ERR_EMPTY: return "empty mask or defect list";
         case VH_ERR_RCCL: return "RCCL error";
         case VH_ERR_NODEV: return "no GPU device";
+        case VH_ERR_INDEX: return "index out of range";
         default: return "unknown status";
     }
 }
@@ -568,6 +569,42 @@ int vh_batch_kernel_time(vh_batch *b, const char *name, double *total_ms, int64_
             *launches = it->second.launches;
             if (bytes_per_launch) *bytes_per_launch = it->second.bytes_per_launch;
         }
+    })
+}
+
+// ---- rendering (export.hip) ------------------------------------------------------------------
+int vh_overlay(vh_ctx *ctx, const float *n4, const uint8_t *defect, int64_t R, int64_t C, int64_t Z,
+               int64_t batch, uint8_t *rgb) {
+    API_TRY(ctx, {
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        if (!n4 || !defect || !rgb) throw VhError{VH_ERR_ARG, "overlay: null buffer"};
+        HIP_TRY(hipSetDevice(ctx->device));
+        vh_batch *b = scratch_batch(ctx, R, C, Z, batch);
+        const size_t NV = (size_t)batch * R * C * Z;
+        HIP_TRY(hipMemcpyAsync(b->d_n4, n4, sizeof(float) * NV, hipMemcpyHostToDevice, b->stream));
+        HIP_TRY(hipMemcpyAsync(b->d_defect, defect, NV, hipMemcpyHostToDevice, b->stream));
+        // rgb (3 B/voxel) in the sort-key buffer (4 B/voxel), the |x| min/max in the partials
+        uint8_t *d_rgb = reinterpret_cast<uint8_t *>(b->d_keys0);
+        uint32_t *d_mm = reinterpret_cast<uint32_t *>(b->d_part);
+        vh_overlay_launch(b->stream, b->d_n4, b->d_defect, R, C, Z, batch, d_mm, d_rgb);
+        HIP_TRY(hipMemcpyAsync(rgb, d_rgb, 3 * NV, hipMemcpyDeviceToHost, b->stream));
+        HIP_TRY(hipStreamSynchronize(b->stream));
+    })
+}
+
+int vh_montage(vh_ctx *ctx, int64_t R, int64_t C, int64_t Z, const void *proton, int proton_is64,
+               const void *hp, int hp_is64, const float *n4, const uint8_t *mask_border,
+               const uint8_t *defect, const double *ci, const double *parula, int64_t prow,
+               const int64_t crop[6], uint8_t *image) {
+    API_TRY(ctx, {
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        if (!proton || !hp || !n4 || !mask_border || !defect || !parula || !crop || !image)
+            throw VhError{VH_ERR_ARG, "montage: null buffer"};
+        check_dims(R, C, Z, 1);
+        HIP_TRY(hipSetDevice(ctx->device));
+        vh_batch *b = scratch_batch(ctx, R, C, Z, 1);
+        vh_montage_run(b->stream, R, C, Z, proton, proton_is64, hp, hp_is64, n4, mask_border, defect,
+                       ci, parula, prow, crop, image);
     })
 }
 

@@ -245,3 +245,11 @@ __device__ __forceinline__ float key2f(uint32_t k) {
     uint32_t u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
     return __uint_as_float(u);
 }
+
+// export.hip (rendering after the hot path)
+void vh_overlay_launch(hipStream_t s, const float *d_n4, const uint8_t *d_def, int64_t R, int64_t C,
+                       int64_t Z, int64_t nb, uint32_t *d_mm, uint8_t *d_rgb);
+void vh_montage_run(hipStream_t s, int64_t R, int64_t C, int64_t Z, const void *proton, int p64,
+                    const void *hp, int h64, const float *n4, const uint8_t *mborder,
+                    const uint8_t *def, const double *ci, const double *parula, int64_t prow,
+                    const int64_t crop[6], uint8_t *image);

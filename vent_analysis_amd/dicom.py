@@ -51,6 +51,7 @@ _DICT = {
     "SeriesTime": (0x00080031, "TM"),
     "Modality": (0x00080060, "CS"),
     "SeriesDescription": (0x0008103E, "LO"),
+    "SliceLocation": (0x00201041, "DS"),
     "PatientName": (0x00100010, "PN"),
     "PatientID": (0x00100020, "LO"),
     "PatientBirthDate": (0x00100030, "DA"),
@@ -95,6 +96,12 @@ _TEXT_VR = {"LT", "ST", "UT"}   # single-valued free text: backslash is not a se
 _NUM_VR = {"US": "H", "SS": "h", "UL": "I", "SL": "i", "FL": "f", "FD": "d", "UV": "Q", "SV": "q"}
 _ITEM, _ITEM_END, _SEQ_END = 0xFFFEE000, 0xFFFEE00D, 0xFFFEE0DD
 _UNDEFINED = 0xFFFFFFFF
+
+
+def generate_uid():
+    """A fresh UID under the 2.25 (UUID-derived) root, as pydicom.uid.generate_uid(None) makes."""
+    import uuid
+    return "2.25." + str(uuid.uuid4().int)
 
 
 class InvalidDicomError(Exception):
@@ -161,6 +168,22 @@ class Dataset:
         if t not in elems:
             raise AttributeError(name)
         return elems[t].value
+
+    def __setattr__(self, name, value):
+        """pydicom-style ds.Keyword = value for the keywords this module knows (exportDICOM,
+        Vent_Analysis.py:394-421); other names are plain attributes."""
+        if name in _DICT:
+            t, vr = _DICT[name]
+            if name == "PixelData" and isinstance(value, (bytes, bytearray)):
+                bits = self.get("BitsAllocated", 16)
+                vr = "OB" if bits == 8 else "OW"
+            self._elems[t] = DataElement(t, vr, value)
+        else:
+            object.__setattr__(self, name, value)
+
+    def save_as(self, path):
+        """pydicom's Dataset.save_as (Explicit VR Little Endian Part-10 file)."""
+        write_dataset(path, self)
 
     def __iter__(self):
         return iter(self._elems[t] for t in sorted(self._elems))
