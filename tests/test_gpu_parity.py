@@ -412,6 +412,41 @@ def test_vdp_chain_morph3d_vs_oracle(shape, seed):
         assert res[b].vdp == o["VDP"]
 
 
+@pytest.mark.parametrize("shape,m3d", [((37, 45, 7), False), ((20, 300, 16), False),
+                                        ((10, 150, 30), False), ((33, 70, 13), True),
+                                        ((12, 90, 64), True), ((5, 8, 1), False)])
+def test_plane_sweep_equals_tile_kernel_and_oracle(shape, m3d, monkeypatch):
+    """classify / border: the plane-sweep kernel (default) against the halo-tile kernel
+    (VH_CLASSIFY_TILE=1) and the oracle, on dense random masks (many median flips), Z % 4 != 0
+    and planes split into column bands (C * ceil(Z / 4) > 1024 words)."""
+    rng = np.random.default_rng(sum(shape))
+    hp = rng.rayleigh(10.0, (2,) + shape).astype(np.float32) + 1.0
+    mk = (rng.random((2,) + shape) < 0.7).astype(np.uint8)
+    vox = (1.0, 1.0, 1.0)
+
+    def run():
+        B = _lib.Batch(*shape, 2)
+        B.upload(hp, mk)
+        B.run(B.options(do_n4=False, vox=vox, morph3d=m3d, do_snr=False))
+        out = B.download()
+        B.close()
+        return out, _lib.border(mk)
+
+    (_, d, bo, lb, res), mb = run()
+    monkeypatch.setenv("VH_CLASSIFY_TILE", "1")
+    (_, d2, bo2, lb2, res2), mb2 = run()
+    assert np.array_equal(d, d2) and np.array_equal(bo, bo2) and np.array_equal(lb, lb2)
+    assert np.array_equal(mb, mb2)
+    for b in range(2):
+        assert res[b].n_defect == res2[b].n_defect == int(d[b].sum())
+        assert res[b].n_lb12 == res2[b].n_lb12
+        o = O.calculate_vdp(hp[b], mk[b].astype(np.float64), vox, HP=hp[b], morph3d=m3d)
+        assert np.array_equal(d[b], o["defectArray"])
+        assert np.array_equal(bo[b] == 1, o["defectBorder"])
+        assert np.array_equal(lb[b], o["defectArrayLB"])
+    assert np.array_equal(mb[0], O.calculate_border(mk[0].astype(np.float64)))
+
+
 def test_config2_256x256x24_full_pipeline_vs_oracle():
     """Config 2: one 256x256x24 study, N4 + normalise + mean-anchored VDP."""
     X, M = synth_volume(256, 256, 24, 7)

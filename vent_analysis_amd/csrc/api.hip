@@ -96,7 +96,7 @@ static void batch_free(vh_batch *b) {
     clear_timers(b);
     dfree(b->d_hp); dfree(b->d_mask); dfree(b->d_n4);
     dfree(b->d_defect); dfree(b->d_border); dfree(b->d_lb);
-    dfree(b->d_colrange); dfree(b->d_colcount); dfree(b->d_colstart); dfree(b->d_colbits);
+    dfree(b->d_colrange); dfree(b->d_colcount); dfree(b->d_colstart); dfree(b->d_colbits); dfree(b->d_colbnz); dfree(b->d_snrpart);
     dfree(b->d_rowany); dfree(b->d_colany); dfree(b->d_sliceany);
     dfree(b->d_sc); dfree(b->d_part); dfree(b->d_keys0); dfree(b->d_keys1); dfree(b->d_tilecnt);
     dfree(b->d_cohort);
@@ -135,12 +135,15 @@ static vh_batch *batch_new(vh_ctx *ctx, int64_t R, int64_t C, int64_t Z, int64_t
         dalloc(&b->d_colrange, (size_t)nb * b->CZ * 2);
         dalloc(&b->d_colcount, (size_t)nb * b->CZ);
         dalloc(&b->d_colbits, (size_t)nb * ((R + 31) / 32) * b->CZ);
+        dalloc(&b->d_colbnz, (size_t)nb * ((R + 31) / 32) * b->CZ);
         dalloc(&b->d_colstart, (size_t)nb * b->CZ);
         dalloc(&b->d_rowany, (size_t)nb * R);
         dalloc(&b->d_colany, (size_t)nb * C);
         dalloc(&b->d_sliceany, (size_t)nb * Z);
         dalloc(&b->d_sc, (size_t)nb);
         b->part_blocks = (b->CZ + VH_TPB - 1) / VH_TPB;
+        b->slab_blocks = b->part_blocks * ((R + VH_SLAB - 1) / VH_SLAB);
+        dalloc(&b->d_snrpart, (size_t)nb * b->slab_blocks * 4);
         const int64_t max_chunks = (b->V + 8191) / 8192;
         const int64_t eval_slots = ((b->CZ + 63) / 64) * ((R + 15) / 16);   // n4 eval partial slots
         dalloc(&b->d_part, (size_t)nb * std::max<int64_t>(std::max<int64_t>(b->part_blocks * 4, max_chunks),

@@ -1137,65 +1137,90 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_refine(float *lat, int64_t lat_ca
     refine_axis_dev(T2, L, 2 * n0 - 3, 2 * n1 - 3, n2, 2);
 }
 
-// Final field at every voxel and the corrected image I / exp(B).  With keys != nullptr it also
-// emits the VDP chain's sort keys of the mask == 1 voxels in compact tile-row order (coalesced:
-// a wave is one 64-column tile, a row's masked lanes are contiguous), replacing the separate
-// masked gather for volumes whose mask is binary (n_mask == n_mask1).
+// Final field at every voxel and the corrected image I / exp(B), in 32-row slabs (one bitmap word)
+// with one column per lane.  With keys != nullptr it also emits the VDP chain's sort keys of the
+// mask == 1 voxels (coalesced: a wave is 64 columns, a row's masked lanes are contiguous),
+// replacing the separate masked gather for volumes whose mask is binary (n_mask == n_mask1); and
+// it accumulates calculate_SNR's partial sums from the image it streams (k_snr's arithmetic).
 __global__ void __launch_bounds__(VH_TPB) k_n4_final(const float *__restrict__ I, float *out,
                                                     int64_t R, int64_t C, int64_t Z, int64_t V,
-                                                    int64_t q2_cap, const double *P1, DevLevel lv,
-                                                    const uint32_t *colbits, const int64_t *colstart,
-                                                    const VolScalars *sc, uint32_t *keys) {
+                                                    int64_t ncb, int64_t q2_cap, const double *P1,
+                                                    DevLevel lv, const uint32_t *colbits,
+                                                    const uint32_t *colbnz, const int64_t *colstart,
+                                                    const VolScalars *sc, uint32_t *keys, SnrBox sb) {
+    __shared__ uint32_t s_rows[2];
+    __shared__ double s_red[4][VH_TPB / 64];
     const int64_t b = blockIdx.y;
     const int64_t CZ = C * Z;
-    const int64_t col = blockIdx.x * (int64_t)VH_TPB + threadIdx.x;
-    if (col >= CZ) return;
-    const int64_t y = col / Z, z = col % Z;
-    const int ncy = lv.ax[1].ncp;
-    const int by = lv.ax[1].base[y];
-    const float4 wy = *reinterpret_cast<const float4 *>(lv.ax[1].w + 4 * y);
-    const double *p1 = P1 + b * q2_cap;
-    const DevAxis ax = lv.ax[0];
-    const bool emit = keys != nullptr && sc[b].n_mask == sc[b].n_mask1;   // block-uniform
+    const int64_t sl = blockIdx.x / ncb;
+    const int64_t col = (blockIdx.x % ncb) * VH_TPB + threadIdx.x;
+    const int64_t x0 = sl * VH_SLAB;
+    const int nr = (int)(R - x0 < VH_SLAB ? R - x0 : VH_SLAB);
+    const VolScalars s = sc[b];
+    snr_slab_rows(sb, s, b, R, x0, nr, s_rows);
+    __syncthreads();
+    const bool act = col < CZ;
     const int64_t nw = (R + 31) >> 5;
-    // keys: the wave's 64 columns own one contiguous run of k_gather's column compaction; the
-    // sort needs the values only, so they are stored row by row across the wave (coalesced)
-    int64_t kpos = emit ? b * V + colstart[b * CZ + (col & ~(int64_t)63)] : 0;
-    uint32_t word = 0u;
-    int wb = ax.base[0];
-    // S9: the final field per S6 (float T window, float row sum), I / (float)exp((double)B)
-    float t0 = (float)col_T(p1, wb, ncy, Z, by, wy, z), t1 = (float)col_T(p1, wb + 1, ncy, Z, by, wy, z);
-    float t2 = (float)col_T(p1, wb + 2, ncy, Z, by, wy, z), t3 = (float)col_T(p1, wb + 3, ncy, Z, by, wy, z);
-    // rows in groups of 8: the group's image loads are issued together, then the field, exp and
-    // stores (the row walk of one column is otherwise a dependent load -> exp -> store chain)
-    for (int64_t x0 = 0; x0 < R; x0 += 8) {
-        float iv[8];
+    const bool emit = keys != nullptr && s.n_mask == s.n_mask1;   // block-uniform
+    // keys: the wave's 64 columns own one contiguous run of k_gather's column compaction, slab by
+    // slab; the sort needs the values only, so they are stored row by row across the wave
+    int64_t kpos = 0;
+    if (emit) {
+        int before = 0;   // this column's keys in the earlier slabs
+        if (act)
+            for (int64_t w = 0; w < sl; ++w) before += __popc(colbits[(b * nw + w) * CZ + col]);
+        for (int off = 32; off > 0; off >>= 1) before += __shfl_xor(before, off, 64);
+        if (act) kpos = b * V + colstart[b * CZ + (col & ~(int64_t)63)] + before;
+    }
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    if (act) {
+        const int64_t y = col / Z, z = col % Z;
+        const int ncy = lv.ax[1].ncp;
+        const int by = lv.ax[1].base[y];
+        const float4 wy = *reinterpret_cast<const float4 *>(lv.ax[1].w + 4 * y);
+        const double *p1 = P1 + b * q2_cap;
+        const DevAxis ax = lv.ax[0];
+        const uint32_t word = colbits[(b * nw + sl) * CZ + col];
+        const uint32_t sig = colbnz[(b * nw + sl) * CZ + col];
+        const uint32_t noise = snr_col_noise(sb, s, b, Z, col, s_rows);
+        int wb = ax.base[x0];
+        // S9: the final field per S6 (float T window, float row sum), I / (float)exp((double)B)
+        float t0 = (float)col_T(p1, wb, ncy, Z, by, wy, z), t1 = (float)col_T(p1, wb + 1, ncy, Z, by, wy, z);
+        float t2 = (float)col_T(p1, wb + 2, ncy, Z, by, wy, z), t3 = (float)col_T(p1, wb + 3, ncy, Z, by, wy, z);
+        const float *src = I + b * V + x0 * CZ + col;
+        float *dst = out + b * V + x0 * CZ + col;
+        // rows in groups of 8: the group's image loads are issued together, then the field, exp and
+        // stores (the row walk of one column is otherwise a dependent load -> exp -> store chain)
+        for (int i0 = 0; i0 < nr; i0 += 8) {
+            float iv[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) iv[k] = x0 + k < R ? I[b * V + (x0 + k) * CZ + col] : 0.0f;
+            for (int k = 0; k < 8; ++k) iv[k] = i0 + k < nr ? src[(int64_t)(i0 + k) * CZ] : 0.0f;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int64_t x = x0 + k;
-            if (x >= R) break;
-            const int bx = ax.base[x];
-            while (wb < bx) {
-                ++wb;
-                t0 = t1; t1 = t2; t2 = t3;
-                t3 = (float)col_T(p1, wb + 3, ncy, Z, by, wy, z);
-            }
-            const float4 w = *reinterpret_cast<const float4 *>(ax.w + 4 * x);
-            const float bn = ((w.x * t0 + w.y * t1) + w.z * t2) + w.w * t3;
-            const int64_t v = b * V + x * CZ + col;
-            const float o = iv[k] / expf_cr(bn);
-            out[v] = o;
-            if (emit) {
-                if ((x & 31) == 0) word = colbits[(b * nw + (x >> 5)) * CZ + col];
-                const bool on = (word >> (x & 31)) & 1u;
-                const uint64_t bal = __ballot(on);
-                if (on) keys[kpos + lanes_below(bal)] = f2key(o);
-                kpos += __popcll(bal);
+            for (int k = 0; k < 8; ++k) {
+                const int i = i0 + k;
+                if (i >= nr) break;
+                const int64_t x = x0 + i;
+                const int bx = ax.base[x];
+                while (wb < bx) {
+                    ++wb;
+                    t0 = t1; t1 = t2; t2 = t3;
+                    t3 = (float)col_T(p1, wb + 3, ncy, Z, by, wy, z);
+                }
+                const float4 w = *reinterpret_cast<const float4 *>(ax.w + 4 * x);
+                const float bn = ((w.x * t0 + w.y * t1) + w.z * t2) + w.w * t3;
+                const float o = iv[k] / expf_cr(bn);
+                dst[(int64_t)i * CZ] = o;
+                snr_add(acc, iv[k], (sig >> i) & 1u, (noise >> i) & 1u);
+                if (emit) {
+                    const bool on = (word >> i) & 1u;
+                    const uint64_t bal = __ballot(on);
+                    if (on) keys[kpos + lanes_below(bal)] = f2key(o);
+                    kpos += __popcll(bal);
+                }
             }
         }
     }
+    snr_block_write(acc, s_red, sb.part + (b * sb.nparts + blockIdx.x) * 4);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1381,7 +1406,6 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
 void vh_launch_n4(vh_batch *b, const vh_n4_params &prm) {
     hipStream_t st = b->stream;
     vh_ensure_n4_workspace(b, prm);
-    const dim3 cg = col_grid(b);
     const int64_t ntiles = b->n4_tiles;
     HIP_TRY(hipMemsetAsync(b->d_lat, 0, sizeof(float) * b->nb * b->lat_cap, st));
     k_n4_state_init<<<(unsigned)((b->nb + 255) / 256), 256, 0, st>>>(b->d_st, b->nb);
@@ -1435,10 +1459,13 @@ void vh_launch_n4(vh_batch *b, const vh_n4_params &prm) {
     {
         const DevLevel lv = vh_dev_level(b, prm, prm.n_levels - 1);
         ScopedKTimer tm(b, "n4_final", 9.0 * (double)b->V);
-        k_n4_final<<<cg, VH_TPB, 0, st>>>(b->d_hp, b->d_n4, b->R, b->C, b->Z, b->V, b->q2_cap,
-                                          b->d_P1, lv, b->d_colbits, b->d_colstart,
-                                          b->d_sc, b->d_keys0);
+        const SnrBox sbox{b->d_rowany, b->d_sliceany, b->d_snrpart, b->slab_blocks};
+        k_n4_final<<<slab_grid(b), VH_TPB, 0, st>>>(b->d_hp, b->d_n4, b->R, b->C, b->Z, b->V,
+                                                    b->part_blocks, b->q2_cap, b->d_P1, lv,
+                                                    b->d_colbits, b->d_colbnz, b->d_colstart,
+                                                    b->d_sc, b->d_keys0, sbox);
         b->keys_fused = true;   // the VDP chain's gather skips volumes with binary masks
+        b->snr_fused = true;    // and the SNR partials of the input image are done
         VH_CHECK_LAUNCH();
     }
 }

@@ -476,6 +476,9 @@ struct ChainSlot {
     int ready;         // block + 1 once a producer has filled the slot for that block
     int pad[3];
 };
+#ifndef CH_PRIO
+#define CH_PRIO 3
+#endif
 struct ChainState {
     int a_done, b_done, c_done;   // blocks finished by wave A / wave B / the producer
     float mu, conv;
@@ -701,6 +704,7 @@ __device__ void chain_wave_mu(int64_t n, ChainSlot *slots, ChainState *cs) {
     double mu = 0.0;
     const int64_t nblk = (n + 63) / 64;
     unsigned long long wt = 0;
+    __builtin_amdgcn_s_setprio(CH_PRIO);   // the serial waves win issue arbitration on their SIMD
     CH_T0();
     for (int64_t blk = 0; blk < nblk; ++blk) {
         ChainSlot &S = slots[blk % CH_SLOTS];
@@ -713,6 +717,7 @@ __device__ void chain_wave_mu(int64_t n, ChainSlot *slots, ChainState *cs) {
         }
     }
     CH_DONE(0, wt);
+    __builtin_amdgcn_s_setprio(0);
 }
 
 // wave B.  Returns conv in cs->conv.
@@ -722,6 +727,7 @@ __device__ void chain_wave_sig(int64_t n, ChainSlot *slots, ChainState *cs) {
     double sig = 0.0;
     const int64_t nblk = (n + 63) / 64;
     unsigned long long wt = 0;
+    __builtin_amdgcn_s_setprio(CH_PRIO);
     CH_T0();
     for (int64_t blk = 0; blk < nblk; ++blk) {
         ChainSlot &S = slots[blk % CH_SLOTS];
@@ -737,6 +743,7 @@ __device__ void chain_wave_sig(int64_t n, ChainSlot *slots, ChainState *cs) {
         if (lane == 0) lds_store_rel(&cs->b_done, (int)(blk + 1));
     }
     CH_DONE(1, wt);
+    __builtin_amdgcn_s_setprio(0);
     if (lane == 0) {
         while (lds_load_acq(&cs->a_done) < (int)nblk) __builtin_amdgcn_s_sleep(1);
         const float mu = cs->mu;

@@ -20,73 +20,111 @@ __global__ void k_init_scalars(VolScalars *sc, int64_t nb) {
     sc[b] = s;
 }
 
+// One pass over the mask in 32-row slabs (one bitmap word) x 4 columns per lane (a 32-bit load
+// per row: 256 B per wave).  Writes the slab's bitmap words of mask == 1 (N4 label) and mask != 0
+// (VDP / SNR mask), the row / col / slice "any" flags, and per volume the masked counts and the
+// first mask == 1 voxel (atomics on integers: order-free).  k_mask_cols then derives each
+// column's masked row range and count from the mask != 0 words.
+template <bool VEC>
 __global__ void __launch_bounds__(VH_TPB) k_mask_stats(const uint8_t *__restrict__ mask, int64_t R,
-                                                      int64_t C, int64_t Z, int64_t V,
-                                                      int32_t *colrange, int32_t *colcount,
-                                                      uint32_t *colbits, uint8_t *rowany,
-                                                      uint8_t *colany, uint8_t *sliceany,
-                                                      VolScalars *sc) {
-    extern __shared__ uint8_t s_row[];   // [R]
+                                                      int64_t C, int64_t Z, int64_t V, int64_t ncb4,
+                                                      uint32_t *colbits, uint32_t *colbnz,
+                                                      uint8_t *rowany, uint8_t *colany,
+                                                      uint8_t *sliceany, VolScalars *sc) {
+    __shared__ uint32_t s_row;
     __shared__ unsigned long long s_n, s_n1, s_first;
     const int64_t b = blockIdx.y;
     const int64_t CZ = C * Z;
-    const int64_t col = blockIdx.x * (int64_t)VH_TPB + threadIdx.x;
-    for (int64_t x = threadIdx.x; x < R; x += VH_TPB) s_row[x] = 0;
-    if (threadIdx.x == 0) { s_n = 0; s_n1 = 0; s_first = ULLONG_MAX; }
+    const int64_t sl = blockIdx.x / ncb4;
+    const int64_t c0 = ((blockIdx.x % ncb4) * VH_TPB + threadIdx.x) * 4;
+    const int64_t x0 = sl * VH_SLAB;
+    const int nr = (int)(R - x0 < VH_SLAB ? R - x0 : VH_SLAB);
+    if (threadIdx.x == 0) { s_row = 0u; s_n = 0; s_n1 = 0; s_first = ULLONG_MAX; }
     __syncthreads();
-    unsigned long long n = 0, n1 = 0, first = ULLONG_MAX;
-    if (col < CZ) {
-        const uint8_t *m = mask + b * V + col;
-        const int64_t nw = (R + 31) >> 5;
-        uint32_t *cb = colbits + (b * nw) * CZ + col;   // bit x&31 of word x>>5: mask == 1
-        uint32_t word = 0u;
-        int32_t lo = (int32_t)R, hi = -1;
-        for (int64_t x0 = 0; x0 < R; x0 += 8) {   // 8 rows of loads in flight
-          uint8_t mv[8];
+    uint32_t w1[4] = {0u, 0u, 0u, 0u}, wn[4] = {0u, 0u, 0u, 0u};
+    const int nc = c0 < CZ ? (int)(CZ - c0 < 4 ? CZ - c0 : 4) : 0;
+    if (nc) {
+        const uint8_t *m = mask + b * V + x0 * CZ + c0;
+        for (int i0 = 0; i0 < nr; i0 += 8) {   // 8 rows of loads in flight
+            uint32_t mv[8];
 #pragma unroll
-          for (int k = 0; k < 8; ++k) mv[k] = x0 + k < R ? m[(x0 + k) * CZ] : 0;
-#pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            const int64_t x = x0 + k;
-            if (x >= R) break;
-            const uint8_t v = mv[k];
-            if (v == 1) word |= 1u << (x & 31);
-            if ((x & 31) == 31 || x == R - 1) {
-                cb[(x >> 5) * CZ] = word;
-                word = 0u;
-            }
-            if (v) {
-                ++n;
-                if (lo == (int32_t)R) lo = (int32_t)x;
-                hi = (int32_t)x;
-                s_row[x] = 1;
-                if (v == 1) {
-                    ++n1;
-                    const unsigned long long idx = (unsigned long long)(x * CZ + col);
-                    if (idx < first) first = idx;
+            for (int k = 0; k < 8; ++k) {
+                mv[k] = 0u;
+                if (i0 + k < nr) {
+                    const uint8_t *p = m + (int64_t)(i0 + k) * CZ;
+                    if (VEC) mv[k] = *reinterpret_cast<const uint32_t *>(p);
+                    else
+                        for (int q = 0; q < nc; ++q) mv[k] |= (uint32_t)p[q] << (8 * q);
                 }
             }
-          }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int i = i0 + k;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t v = (mv[k] >> (8 * q)) & 0xFFu;
+                    w1[q] |= (uint32_t)(v == 1u) << (i & 31);
+                    wn[q] |= (uint32_t)(v != 0u) << (i & 31);
+                }
+            }
         }
-        colrange[(b * CZ + col) * 2] = lo;
-        colrange[(b * CZ + col) * 2 + 1] = hi;
-        colcount[b * CZ + col] = (int32_t)n;
-        if (n) {
+        const int64_t nw = (R + 31) >> 5;
+        uint32_t *cb = colbits + (b * nw + sl) * CZ + c0, *cn = colbnz + (b * nw + sl) * CZ + c0;
+        if (VEC) {
+            *reinterpret_cast<uint4 *>(cb) = make_uint4(w1[0], w1[1], w1[2], w1[3]);
+            *reinterpret_cast<uint4 *>(cn) = make_uint4(wn[0], wn[1], wn[2], wn[3]);
+        } else {
+            for (int q = 0; q < nc; ++q) { cb[q] = w1[q]; cn[q] = wn[q]; }
+        }
+    }
+    unsigned long long n = 0, n1 = 0, first = ULLONG_MAX;
+    uint32_t rows = 0u;
+    for (int q = 0; q < nc; ++q) {
+        n += (unsigned)__popc(wn[q]);
+        n1 += (unsigned)__popc(w1[q]);
+        rows |= wn[q];
+        const int64_t col = c0 + q;
+        if (wn[q]) {
             colany[b * C + col / Z] = 1;
             sliceany[b * Z + col % Z] = 1;
         }
+        if (w1[q]) {
+            const unsigned long long idx =
+                (unsigned long long)((x0 + __builtin_ctz(w1[q])) * CZ + col);
+            if (idx < first) first = idx;
+        }
     }
+    if (rows) atomicOr(&s_row, rows);
     if (n) atomicAdd(&s_n, n);
     if (n1) atomicAdd(&s_n1, n1);
     if (first != ULLONG_MAX) atomicMin(&s_first, first);
     __syncthreads();
-    for (int64_t x = threadIdx.x; x < R; x += VH_TPB)
-        if (s_row[x]) rowany[b * R + x] = 1;
+    if ((int)threadIdx.x < nr && ((s_row >> threadIdx.x) & 1u)) rowany[b * R + x0 + threadIdx.x] = 1;
     if (threadIdx.x == 0) {
         if (s_n) atomicAdd((unsigned long long *)&sc[b].n_mask, s_n);
         if (s_n1) atomicAdd((unsigned long long *)&sc[b].n_mask1, s_n1);
         if (s_first != ULLONG_MAX) atomicMin((unsigned long long *)&sc[b].first_masked, s_first);
     }
+}
+
+// each column's masked (mask != 0) row range [lo, hi] (lo = R, hi = -1 when empty) and count
+__global__ void __launch_bounds__(VH_TPB) k_mask_cols(const uint32_t *colbnz, int64_t R, int64_t CZ,
+                                                     int32_t *colrange, int32_t *colcount) {
+    const int64_t b = blockIdx.y;
+    const int64_t col = blockIdx.x * (int64_t)VH_TPB + threadIdx.x;
+    if (col >= CZ) return;
+    const int64_t nw = (R + 31) >> 5;
+    int32_t lo = (int32_t)R, hi = -1, n = 0;
+    for (int64_t w = 0; w < nw; ++w) {
+        const uint32_t v = colbnz[(b * nw + w) * CZ + col];
+        if (!v) continue;
+        n += __popc(v);
+        if (lo == (int32_t)R) lo = (int32_t)(w * 32 + __builtin_ctz(v));
+        hi = (int32_t)(w * 32 + 31 - __builtin_clz(v));
+    }
+    colrange[(b * CZ + col) * 2] = lo;
+    colrange[(b * CZ + col) * 2 + 1] = hi;
+    colcount[b * CZ + col] = n;
 }
 
 // exclusive prefix of the per-column masked counts (compaction offsets for the sort keys) and
@@ -142,6 +180,7 @@ __global__ void __launch_bounds__(VH_TPB) k_mask_finish(const int32_t *colcount,
 
 void vh_launch_mask_stats(vh_batch *b) {
     hipStream_t st = b->stream;
+    b->snr_fused = false;
     HIP_TRY(hipMemsetAsync(b->d_rowany, 0, b->nb * b->R, st));
     HIP_TRY(hipMemsetAsync(b->d_colany, 0, b->nb * b->C, st));
     HIP_TRY(hipMemsetAsync(b->d_sliceany, 0, b->nb * b->Z, st));
@@ -149,9 +188,14 @@ void vh_launch_mask_stats(vh_batch *b) {
     VH_CHECK_LAUNCH();
     {
         ScopedKTimer tm(b, "mask_stats", (double)b->V);
-        k_mask_stats<<<col_grid(b), VH_TPB, (size_t)b->R, st>>>(
-            b->d_mask, b->R, b->C, b->Z, b->V, b->d_colrange, b->d_colcount, b->d_colbits,
-            b->d_rowany, b->d_colany, b->d_sliceany, b->d_sc);
+        const int64_t ncb4 = (b->CZ + 4 * VH_TPB - 1) / (4 * VH_TPB);
+        const dim3 grid((unsigned)(ncb4 * ((b->R + VH_SLAB - 1) / VH_SLAB)), (unsigned)b->nb);
+        auto fn = (b->CZ & 3) == 0 ? k_mask_stats<true> : k_mask_stats<false>;
+        fn<<<grid, VH_TPB, 0, st>>>(b->d_mask, b->R, b->C, b->Z, b->V, ncb4, b->d_colbits,
+                                    b->d_colbnz, b->d_rowany, b->d_colany, b->d_sliceany, b->d_sc);
+        VH_CHECK_LAUNCH();
+        k_mask_cols<<<col_grid(b), VH_TPB, 0, st>>>(b->d_colbnz, b->R, b->CZ, b->d_colrange,
+                                                   b->d_colcount);
         VH_CHECK_LAUNCH();
     }
     k_mask_finish<<<(unsigned)b->nb, VH_TPB, 0, st>>>(b->d_colcount, b->d_colstart, b->d_rowany,
@@ -728,10 +772,333 @@ static void tile_geometry(const vh_batch *b, bool m3d, int &tz, dim3 &grid, size
            (size_t)CL_TX * CL_TY) * 32;
 }
 
+// =============================================================================================
+// Plane-sweep classify / border (the default; k_tile above stays for planes too wide for it).
+// A block owns one volume's slab of rows [xa, xb) and a band of columns [ya, yb) with every
+// slice -- the whole (y, z) plane when it fits, so there is no y halo -- and walks the slab plane
+// by plane with one barrier per plane.  LDS holds rings of the last 4 planes of the raw
+// threshold map and of the median-filtered defect map, 4 slices per 32-bit word: the 3x3 (x, y)
+// median is a byte-lane sum of 9 words (every byte sum <= 27, so no carries) and a compare by
+// adding 128 - k.  Words whose 4 columns hold no mask voxel at this row (outside the columns'
+// masked row range, k_mask_stats) are not loaded: their raw and LB bytes are 0.
+// Iteration p: loads of plane p + 1 issued; raw(p) -> LDS (and LB of plane p); def(p - 2) from
+// raw(p - 3 .. p - 1); defect / border of plane p - 4 from def(p - 5 .. p - 3).  Rings of 4
+// slots make every slot written in iteration p distinct from the ones read in it.
+// =============================================================================================
+#define PS_TPB 256
+#define PS_K 4          // words per thread per plane (host picks the band so the plane fits)
+#define PS_XS 32        // slab rows
+
+struct PsGeom {
+    int R, C, Z, ZW;    // ZW = ceil(Z / 4) words per (x, y) row
+    int64_t V, CZ;
+    int XS, TY, nxs, nyt;
+};
+
+enum { PS_CL2 = 0, PS_CL3 = 1, PS_BORDER = 2 };
+
+// byte lanes >= k (bias = 128 - k, added to every byte lane): 1, else 0
+__device__ __forceinline__ uint32_t ps_atleast(uint32_t s, uint32_t bias) {
+    return ((s + bias * 0x01010101u) >> 7) & 0x01010101u;
+}
+// byte lanes != 0: 1, else 0
+__device__ __forceinline__ uint32_t ps_nonzero(uint32_t g) {
+    return ((((g & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | g) >> 7) & 0x01010101u;
+}
+
+// per-word flags (precomputed once per block; the word set is the same for every plane)
+#define PSF_ZW0 1u      // zw == 0
+#define PSF_ZWL 2u      // zw == ZW - 1
+#define PSF_Y0 4u       // y == 0
+#define PSF_YL 8u       // y == C - 1
+#define PSF_ZLAST 16u   // word holds slice Z - 1
+#define PSF_BAND 32u    // row inside the band [ya, yb)
+#define PSF_NV_SHIFT 8  // bits 8..10: valid slices in the word (1..4)
+
+template <int MODE, bool VEC>
+__global__ void __launch_bounds__(PS_TPB) k_plane(const float *__restrict__ n4,
+                                                 const uint8_t *__restrict__ mask,
+                                                 const uint8_t *__restrict__ in_bin,
+                                                 const int32_t *__restrict__ colrange,
+                                                 const VolScalars *__restrict__ sc, float thresh,
+                                                 PsGeom g, uint8_t *defect, uint8_t *border,
+                                                 uint8_t *lb, unsigned long long *cnt_out) {
+    constexpr bool CL = MODE != PS_BORDER;
+    extern __shared__ uint32_t ps_lds[];
+    const int64_t b = blockIdx.y;
+    const int xs = (int)(blockIdx.x % (unsigned)g.nxs), yt = (int)(blockIdx.x / (unsigned)g.nxs);
+    const int R = g.R, C = g.C, Z = g.Z, ZW = g.ZW;
+    const int xa = xs * g.XS, xb = min(xa + g.XS, R);
+    const int ya = yt * g.TY, yb = min(ya + g.TY, C);
+    const int RW = CL ? (g.TY + 4) * ZW : 0;   // raw slot: rows ya - 2 .. ya + TY + 1
+    const int DW = (g.TY + 2) * ZW;            // def slot: rows ya - 1 .. ya + TY
+    uint32_t *raw = ps_lds;                    // [4][TY + 4][ZW]
+    uint32_t *def = ps_lds + 4 * RW;           // [4][TY + 2][ZW]
+    for (int i = threadIdx.x; i < 4 * (RW + DW); i += PS_TPB) ps_lds[i] = 0u;
+    const int64_t vb = b * g.V;
+    float m = 0.0f, p99 = 0.0f;
+    if (CL) { m = sc[b].mean_anchor; p99 = sc[b].p99; }
+
+    // word sets: loads (raw rows, or def rows in border mode), def rows, output rows
+    const int hl = CL ? 2 : 1;
+    const int lylo = max(ya - hl, 0), lyhi = min(yb + hl, C);
+    const int dylo = max(ya - 1, 0), dyhi = min(yb + 1, C);
+    const int nld = (lyhi - lylo) * ZW, ndf = (dyhi - dylo) * ZW, nout = (yb - ya) * ZW;
+    auto flags = [&](int y, int zw) {
+        uint32_t f = 0;
+        if (zw == 0) f |= PSF_ZW0;
+        if (zw == ZW - 1) f |= PSF_ZWL;
+        if (y == 0) f |= PSF_Y0;
+        if (y == C - 1) f |= PSF_YL;
+        if (zw == ((Z - 1) >> 2)) f |= PSF_ZLAST;
+        if (y >= ya && y < yb) f |= PSF_BAND;
+        f |= (uint32_t)min(4, Z - 4 * zw) << PSF_NV_SHIFT;
+        return f;
+    };
+    int l_goff[PS_K], l_lds[PS_K], l_lo[PS_K], l_hi[PS_K];
+    uint32_t l_f[PS_K];
+    int d_idx[PS_K];
+    uint32_t d_f[PS_K];
+    int o_idx[PS_K], o_goff[PS_K];
+    uint32_t o_f[PS_K];
+#pragma unroll
+    for (int k = 0; k < PS_K; ++k) {
+        const int w = threadIdx.x + k * PS_TPB;
+        l_lo[k] = INT_MAX; l_hi[k] = -1; l_goff[k] = 0; l_lds[k] = 0; l_f[k] = 0;
+        if (w < nld) {
+            const int y = lylo + w / ZW, zw = w % ZW;
+            l_goff[k] = y * Z + 4 * zw;
+            l_lds[k] = (y - ya + hl) * ZW + zw;
+            l_f[k] = flags(y, zw);
+            if (CL) {
+                const int nv = min(4, Z - 4 * zw);
+                for (int q = 0; q < nv; ++q) {
+                    const int32_t *cr = colrange + (b * g.CZ + l_goff[k] + q) * 2;
+                    l_lo[k] = min(l_lo[k], cr[0]);
+                    l_hi[k] = max(l_hi[k], cr[1]);
+                }
+            } else {
+                l_lo[k] = 0; l_hi[k] = R - 1;
+            }
+        }
+        d_idx[k] = -1; d_f[k] = 0;
+        if (CL && w < ndf) {
+            const int y = dylo + w / ZW, zw = w % ZW;
+            d_idx[k] = (y - ya + 1) * ZW + zw;
+            d_f[k] = flags(y, zw);
+        }
+        o_idx[k] = -1; o_goff[k] = 0; o_f[k] = 0;
+        if (w < nout) {
+            const int y = ya + w / ZW, zw = w % ZW;
+            o_idx[k] = (y - ya + 1) * ZW + zw;
+            o_goff[k] = y * Z + 4 * zw;
+            o_f[k] = flags(y, zw);
+        }
+    }
+
+    // plane q's words into registers (zeros for rows outside the volume or the masked range)
+    auto load = [&](int q, float4 (&nv)[PS_K], uint32_t (&mk)[PS_K]) {
+        const bool qin = q >= 0 && q < R && q <= (CL ? xb + 1 : xb);
+        const int64_t base = vb + (int64_t)q * g.CZ;
+#pragma unroll
+        for (int k = 0; k < PS_K; ++k) {
+            nv[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+            mk[k] = 0u;
+            if (qin && q >= l_lo[k] && q <= l_hi[k]) {
+                const int64_t i = base + l_goff[k];
+                const uint8_t *src = CL ? mask : in_bin;
+                if (VEC) {
+                    mk[k] = *reinterpret_cast<const uint32_t *>(src + i);
+                    if (CL) nv[k] = *reinterpret_cast<const float4 *>(n4 + i);
+                } else {
+                    const int nvd = (int)(l_f[k] >> PSF_NV_SHIFT) & 7;
+                    float t[4] = {0.f, 0.f, 0.f, 0.f};
+                    for (int q2 = 0; q2 < nvd; ++q2) {
+                        mk[k] |= (uint32_t)src[i + q2] << (8 * q2);
+                        if (CL) t[q2] = n4[i + q2];
+                    }
+                    nv[k] = make_float4(t[0], t[1], t[2], t[3]);
+                }
+            }
+        }
+    };
+    auto store_word = [&](uint8_t *dst, int64_t i, uint32_t v, uint32_t f) {
+        if (VEC) {
+            *reinterpret_cast<uint32_t *>(dst + i) = v;
+        } else {
+            const int nvd = (int)(f >> PSF_NV_SHIFT) & 7;
+            for (int q2 = 0; q2 < nvd; ++q2) dst[i + q2] = (uint8_t)(v >> (8 * q2));
+        }
+    };
+
+    unsigned long long n_def = 0, n_lb12 = 0;
+    auto step = [&](int p, float4 (&nv)[PS_K], uint32_t (&mk)[PS_K], float4 (&nvn)[PS_K],
+                    uint32_t (&mkn)[PS_K]) {
+        load(p + 1, nvn, mkn);
+        if (CL) {
+            // raw(p) and the LB classes of plane p (Vent_Analysis.py:247-249, 255-256)
+            if (p <= xb + 1) {
+                const bool lbp = p >= xa && p < xb;
+#pragma unroll
+                for (int k = 0; k < PS_K; ++k) {
+                    if (threadIdx.x + k * PS_TPB >= nld) continue;
+                    const bool lbk = lbp && (l_f[k] & PSF_BAND);   // halo rows: raw only
+                    const float v[4] = {nv[k].x, nv[k].y, nv[k].z, nv[k].w};
+                    uint32_t r = 0u, c = 0u;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        if (!((mk[k] >> (8 * q)) & 0xFFu)) continue;
+                        // IEEE f32 division, float32(thresh)
+                        r |= (uint32_t)((v[q] / m) < thresh) << (8 * q);
+                        if (lbk) {
+                            const uint32_t cls = lb_class(v[q] / p99);
+                            c |= cls << (8 * q);
+                            n_lb12 += (cls == 1u || cls == 2u);
+                        }
+                    }
+                    raw[(p & 3) * RW + l_lds[k]] = r;
+                    if (lbk)
+                        store_word(lb, vb + (int64_t)p * g.CZ + l_goff[k], c, l_f[k]);
+                }
+            }
+            // def(p - 2): zero-padded 3x3 median per slice (>= 5 of 9) or 3x3x3 (>= 14 of 27)
+            const int xd = p - 2;
+            if (xd >= xa - 1 && xd <= xb) {
+                const uint32_t *r0 = raw + ((p - 3) & 3) * RW, *r1 = raw + ((p - 2) & 3) * RW,
+                               *r2 = raw + ((p - 1) & 3) * RW;
+#pragma unroll
+                for (int k = 0; k < PS_K; ++k) {
+                    const int i = d_idx[k];
+                    if (i < 0) continue;
+                    auto sum9 = [&](int j) {
+                        return ((r0[j] + r0[j + ZW]) + r0[j + 2 * ZW]) +
+                               ((r1[j] + r1[j + ZW]) + r1[j + 2 * ZW]) +
+                               ((r2[j] + r2[j + ZW]) + r2[j + 2 * ZW]);
+                    };
+                    const uint32_t s0 = sum9(i);
+                    uint32_t d;
+                    if (MODE == PS_CL3) {
+                        const uint32_t sm = (d_f[k] & PSF_ZW0) ? 0u : sum9(i - 1);
+                        const uint32_t sp = (d_f[k] & PSF_ZWL) ? 0u : sum9(i + 1);
+                        const uint32_t s = s0 + ((s0 << 8) | (sm >> 24)) + ((s0 >> 8) | (sp << 24));
+                        d = ps_atleast(s, 128u - 14u);
+                    } else {
+                        d = ps_atleast(s0, 128u - 5u);
+                    }
+                    def[(xd & 3) * DW + i] = d;
+                }
+            }
+        } else if (p <= xb) {
+            // border of an arbitrary binary volume: the input is the "defect" map
+#pragma unroll
+            for (int k = 0; k < PS_K; ++k)
+                if (threadIdx.x + k * PS_TPB < nld) def[(p & 3) * DW + l_lds[k]] = mk[k];
+        }
+        // outputs of plane x: np.gradient != 0 (central inside, one-sided at the edges)
+        const int x = CL ? p - 4 : p - 2;
+        if (x >= xa && x < xb) {
+            const uint32_t *dm = def + ((x - 1) & 3) * DW, *d0 = def + (x & 3) * DW,
+                           *dp = def + ((x + 1) & 3) * DW;
+            const bool xe0 = x == 0, xel = x == R - 1;
+#pragma unroll
+            for (int k = 0; k < PS_K; ++k) {
+                const int i = o_idx[k];
+                if (i < 0) continue;
+                const uint32_t f = o_f[k];
+                const uint32_t D = d0[i];
+                const uint32_t ax = (!xe0 && xel) ? D : dp[i], bx = xe0 ? D : dm[i];
+                const uint32_t ay = (!(f & PSF_Y0) && (f & PSF_YL)) ? D : d0[i + ZW];
+                const uint32_t by = (f & PSF_Y0) ? D : d0[i - ZW];
+                uint32_t gr = (ax ^ bx) | (ay ^ by);
+                if (MODE == PS_CL3 && Z > 1) {
+                    const uint32_t dn = (f & PSF_ZWL) ? 0u : d0[i + 1];
+                    const uint32_t dv = (f & PSF_ZW0) ? 0u : d0[i - 1];
+                    const uint32_t zp = (D >> 8) | (dn << 24), zm = (D << 8) | (dv >> 24);
+                    const uint32_t m0 = (f & PSF_ZW0) ? 0xFFu : 0u;
+                    const uint32_t ml = (f & PSF_ZLAST) ? 0xFFu << (8 * ((Z - 1) & 3)) : 0u;
+                    gr |= ((zp & ~ml) | (D & ml)) ^ ((zm & ~m0) | (D & m0));
+                }
+                const int64_t gi = vb + (int64_t)x * g.CZ + o_goff[k];
+                store_word(border, gi, ps_nonzero(gr), f);
+                if (CL) {
+                    store_word(defect, gi, D, f);
+                    n_def += (unsigned)__popc(D);
+                }
+            }
+        }
+        __syncthreads();
+    };
+
+    const int p0 = CL ? xa - 2 : xa - 1, p1 = CL ? xb + 3 : xb + 1;
+    float4 nvA[PS_K], nvB[PS_K];
+    uint32_t mkA[PS_K], mkB[PS_K];
+    load(p0, nvA, mkA);
+    __syncthreads();   // LDS cleared
+    for (int p = p0; p <= p1; p += 2) {
+        step(p, nvA, mkA, nvB, mkB);
+        if (p + 1 <= p1) step(p + 1, nvB, mkB, nvA, mkA);
+    }
+    if (CL) {
+        for (int off = 32; off > 0; off >>= 1) {
+            n_def += __shfl_down(n_def, off, 64);
+            n_lb12 += __shfl_down(n_lb12, off, 64);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            if (n_def) atomicAdd(&cnt_out[b * 2 + 0], n_def);
+            if (n_lb12) atomicAdd(&cnt_out[b * 2 + 1], n_lb12);
+        }
+    }
+}
+
+// plane-sweep geometry; false when a band of one row does not fit PS_K words per thread
+static bool plane_geometry(const vh_batch *b, int mode, PsGeom &g, dim3 &grid, size_t &lds) {
+    if (const char *e = getenv("VH_CLASSIFY_TILE"))
+        if (atoi(e)) return false;
+    g.R = (int)b->R; g.C = (int)b->C; g.Z = (int)b->Z; g.ZW = (g.Z + 3) / 4;
+    g.V = b->V; g.CZ = b->CZ;
+    const int cap = PS_K * PS_TPB;
+    const int hl = mode == PS_BORDER ? 1 : 2;
+    if ((1 + 2 * hl) * g.ZW > cap) return false;
+    int nyt = 1;
+    while (true) {
+        const int ty = (g.C + nyt - 1) / nyt;
+        const int rows = nyt == 1 ? g.C : ty + 2 * hl;
+        if (rows * g.ZW <= cap) break;
+        ++nyt;
+    }
+    g.nyt = nyt;
+    g.TY = (g.C + nyt - 1) / nyt;
+    g.XS = PS_XS;
+    if (const char *e = getenv("VH_PS_XS")) {
+        const int v = atoi(e);
+        if (v >= 1) g.XS = v;
+    }
+    g.nxs = (g.R + g.XS - 1) / g.XS;
+    grid = dim3((unsigned)(g.nxs * g.nyt), (unsigned)b->nb, 1);
+    lds = (size_t)4 * ((mode == PS_BORDER ? 0 : (g.TY + 4) * g.ZW) + (g.TY + 2) * g.ZW) * 4;
+    return lds <= 64 * 1024;
+}
+
+template <int MODE>
+static void launch_plane(vh_batch *b, const PsGeom &g, dim3 grid, size_t lds, const float *n4,
+                         const uint8_t *in_bin, float thresh, uint8_t *border,
+                         unsigned long long *cnt) {
+    const bool vec = (g.Z & 3) == 0;
+    auto fn = vec ? k_plane<MODE, true> : k_plane<MODE, false>;
+    fn<<<grid, PS_TPB, lds, b->stream>>>(n4, b->d_mask, in_bin, b->d_colrange, b->d_sc, thresh, g,
+                                         b->d_defect, border, b->d_lb, cnt);
+}
+
 void vh_launch_border(vh_batch *b, const uint8_t *d_in, uint8_t *d_out) {
+    ScopedKTimer tm(b, "border", 2.0 * (double)b->V);
+    PsGeom g; dim3 pgrid; size_t plds;
+    if (plane_geometry(b, PS_BORDER, g, pgrid, plds)) {
+        launch_plane<PS_BORDER>(b, g, pgrid, plds, nullptr, d_in, 0.f, d_out, nullptr);
+        VH_CHECK_LAUNCH();
+        return;
+    }
     int tz; dim3 grid; size_t lds;
     tile_geometry(b, false, tz, grid, lds);
-    ScopedKTimer tm(b, "border", 2.0 * (double)b->V);
     k_tile<false, false><<<grid, VH_TPB, lds, b->stream>>>(nullptr, b->d_mask, d_in, b->d_sc, 0.f,
                                                          b->R, b->C, b->Z, b->V, tz, nullptr,
                                                          d_out, nullptr, nullptr);
@@ -1021,48 +1388,47 @@ __global__ void k_cohort_sum(const uint32_t *rows, int64_t nb, uint64_t *cohort)
 
 // =============================================================================================
 // SNR (Vent_Analysis.py:337-357): signal = A[mask>0]; noise = A outside the ix_(rr, cc, ss) box and
-// outside the first/last 20 rows.  Per-block double partials (fixed order), then a finish kernel.
+// outside the first/last 20 rows.  32-row slabs, one column per lane; signal rows from the
+// mask != 0 bitmap, rows that are neither signal nor noise are not loaded.  Per-block double
+// partials (fixed order), then a finish kernel.  With N4, k_n4_final computes the same partials
+// from the image it already streams (vh_batch::snr_fused) and only the finish runs here.
 // =============================================================================================
 __global__ void __launch_bounds__(VH_TPB) k_snr(const float *__restrict__ hp,
-                                               const uint8_t *__restrict__ mask,
-                                               const uint8_t *rowany, const uint8_t *sliceany,
+                                               const uint32_t *__restrict__ colbnz,
                                                const VolScalars *sc, int64_t R, int64_t C,
-                                               int64_t Z, int64_t V, int64_t nparts,
-                                               double *part) {
-    // column sweep: one thread per (col, slice), rows walked in order
+                                               int64_t Z, int64_t V, int64_t ncb, SnrBox sb) {
+    __shared__ uint32_t s_rows[2];
     __shared__ double s_red[4][VH_TPB / 64];
     const int64_t b = blockIdx.y;
     const int64_t CZ = C * Z;
-    const int64_t col = blockIdx.x * (int64_t)VH_TPB + threadIdx.x;
+    const int64_t sl = blockIdx.x / ncb;
+    const int64_t col = (blockIdx.x % ncb) * VH_TPB + threadIdx.x;
+    const int64_t x0 = sl * VH_SLAB;
+    const int nr = (int)(R - x0 < VH_SLAB ? R - x0 : VH_SLAB);
     const VolScalars s = sc[b];
-    double ssig = 0.0, sn = 0.0, sn2 = 0.0, nn = 0.0;
-    const int64_t FOV = 20;
+    snr_slab_rows(sb, s, b, R, x0, nr, s_rows);
+    __syncthreads();
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
     if (col < CZ) {
-        const int64_t y = col / Z, z = col % Z;
-        const bool cin = y >= s.cmin && y < s.cmax;
-        const bool sin_ = sliceany[b * Z + z] || (z == 0 && s.any_slice_empty);
-        const float *a = hp + b * V + col;
-        const uint8_t *m = mask + b * V + col;
-        for (int64_t x = 0; x < R; ++x) {
-            const float v = a[x * CZ];
-            if (m[x * CZ]) ssig += (double)v;
-            if (x < FOV || x >= R - FOV) continue;
-            const bool rin = rowany[b * R + x] || (x == 0 && s.any_row_empty);
-            if (!(rin && cin && sin_)) { sn += (double)v; sn2 += (double)v * (double)v; nn += 1.0; }
+        const int64_t nw = (R + 31) >> 5;
+        const uint32_t sig = colbnz[(b * nw + sl) * CZ + col];
+        const uint32_t noise = snr_col_noise(sb, s, b, Z, col, s_rows);
+        const uint32_t need = sig | noise;
+        const float *a = hp + b * V + x0 * CZ + col;
+        for (int i0 = 0; i0 < nr; i0 += 8) {   // 8 rows of loads in flight
+            float v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                v[k] = (i0 + k < nr && ((need >> (i0 + k)) & 1u)) ? a[(int64_t)(i0 + k) * CZ] : 0.0f;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int i = i0 + k;
+                if (i >= nr) break;
+                snr_add(acc, v[k], (sig >> i) & 1u, (noise >> i) & 1u);
+            }
         }
     }
-    double v[4] = {ssig, sn, sn2, nn};
-    for (int q = 0; q < 4; ++q) {
-        double x = v[q];
-        for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
-        if ((threadIdx.x & 63) == 0) s_red[q][threadIdx.x >> 6] = x;
-    }
-    __syncthreads();
-    if (threadIdx.x < 4) {
-        double x = 0.0;
-        for (int w = 0; w < VH_TPB / 64; ++w) x += s_red[threadIdx.x][w];
-        part[(b * nparts + blockIdx.x) * 4 + threadIdx.x] = x;
-    }
+    snr_block_write(acc, s_red, sb.part + (b * sb.nparts + blockIdx.x) * 4);
 }
 
 __global__ void k_snr_finish(const double *part, int64_t nparts, int64_t nb, VolScalars *sc) {
@@ -1086,13 +1452,15 @@ __global__ void k_snr_finish(const double *part, int64_t nparts, int64_t nb, Vol
 
 void vh_launch_snr(vh_batch *b) {
     hipStream_t st = b->stream;
-    const int64_t nparts = (b->CZ + VH_TPB - 1) / VH_TPB;
-    ScopedKTimer tm(b, "snr", 5.0 * (double)b->V);
-    k_snr<<<col_grid(b), VH_TPB, 0, st>>>(
-        b->d_hp, b->d_mask, b->d_rowany, b->d_sliceany, b->d_sc, b->R, b->C, b->Z, b->V, nparts,
-        b->d_part);
-    VH_CHECK_LAUNCH();
-    k_snr_finish<<<(unsigned)((b->nb + 63) / 64), 64, 0, st>>>(b->d_part, nparts, b->nb, b->d_sc);
+    const SnrBox sb{b->d_rowany, b->d_sliceany, b->d_snrpart, b->slab_blocks};
+    if (!b->snr_fused) {
+        ScopedKTimer tm(b, "snr", 5.0 * (double)b->V);
+        k_snr<<<slab_grid(b), VH_TPB, 0, st>>>(b->d_hp, b->d_colbnz, b->d_sc, b->R, b->C, b->Z,
+                                               b->V, b->part_blocks, sb);
+        VH_CHECK_LAUNCH();
+    }
+    k_snr_finish<<<(unsigned)((b->nb + 63) / 64), 64, 0, st>>>(b->d_snrpart, b->slab_blocks, b->nb,
+                                                              b->d_sc);
     VH_CHECK_LAUNCH();
 }
 
@@ -1129,7 +1497,15 @@ void vh_launch_vdp_chain(vh_batch *b, const float *d_n4, const vh_run_opts &o) {
         HIP_TRY(hipMemsetAsync(cnt, 0, sizeof(unsigned long long) * 2 * b->nb, st));
         int tz; dim3 grid; size_t lds;
         tile_geometry(b, o.morph3d != 0, tz, grid, lds);
-        {
+        PsGeom g; dim3 pgrid; size_t plds;
+        if (plane_geometry(b, o.morph3d ? PS_CL3 : PS_CL2, g, pgrid, plds)) {
+            ScopedKTimer tm(b, "classify", 8.0 * (double)b->V);
+            if (o.morph3d)
+                launch_plane<PS_CL3>(b, g, pgrid, plds, d_n4, nullptr, o.thresh, b->d_border, cnt);
+            else
+                launch_plane<PS_CL2>(b, g, pgrid, plds, d_n4, nullptr, o.thresh, b->d_border, cnt);
+            VH_CHECK_LAUNCH();
+        } else {
             ScopedKTimer tm(b, "classify", 8.0 * (double)b->V);
             if (o.morph3d)
                 k_tile<true, true><<<grid, VH_TPB, lds, st>>>(d_n4, b->d_mask, nullptr, b->d_sc,

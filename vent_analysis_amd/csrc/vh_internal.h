@@ -141,11 +141,15 @@ struct vh_batch {
     int32_t *d_colrange = nullptr;   // [nb][CZ][2]  first/last masked row of each (col, slice) column
     int32_t *d_colcount = nullptr;   // [nb][CZ]
     uint32_t *d_colbits = nullptr;   // [nb][ceil(R/32)][CZ]  row bitmap of mask == 1 per column
+    uint32_t *d_colbnz = nullptr;    // [nb][ceil(R/32)][CZ]  row bitmap of mask != 0 per column
     int64_t *d_colstart = nullptr;   // [nb][CZ]     exclusive prefix of colcount
     uint8_t *d_rowany = nullptr, *d_colany = nullptr, *d_sliceany = nullptr;
     VolScalars *d_sc = nullptr;
     double *d_part = nullptr;        // [nb][part_blocks][4] deterministic partial sums
     int64_t part_blocks = 0;
+    double *d_snrpart = nullptr;     // [nb][slab_blocks][4] SNR partial sums (k_snr / k_n4_final)
+    int64_t slab_blocks = 0;         // column blocks x 32-row slabs per volume
+    bool snr_fused = false;          // k_n4_final computed the SNR partials of this run
     // sort
     uint32_t *d_keys0 = nullptr, *d_keys1 = nullptr;
     uint32_t *d_tilecnt = nullptr;   // [nb][256][max_tiles]
@@ -235,6 +239,17 @@ float vh_bspline_eps(int max_spans);
 inline dim3 col_grid(const vh_batch *b) {
     return dim3((unsigned)((b->CZ + VH_TPB - 1) / VH_TPB), (unsigned)b->nb, 1);
 }
+// row-slab column sweeps: blockIdx.x = slab * col_blocks + column block, slabs of 32 rows (one
+// bitmap word of d_colbits / d_colbnz), so a column's rows are walked by R / 32 threads
+#define VH_SLAB 32
+inline dim3 slab_grid(const vh_batch *b) { return dim3((unsigned)b->slab_blocks, (unsigned)b->nb, 1); }
+
+// calculate_SNR's noise box (Vent_Analysis.py:340-351) for the slab sweeps
+struct SnrBox {
+    const uint8_t *rowany, *sliceany;
+    double *part;                    // [nb][nparts][4]: signal sum, noise sum, noise sum of squares, noise count
+    int64_t nparts;
+};
 
 // ---- device helpers ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t f2key(float f) {
@@ -244,6 +259,48 @@ __device__ __forceinline__ uint32_t f2key(float f) {
 __device__ __forceinline__ float key2f(uint32_t k) {
     uint32_t u = (k & 0x80000000u) ? (k & 0x7fffffffu) : ~k;
     return __uint_as_float(u);
+}
+
+// SNR over a 32-row slab: wave 0 sets s_rows[0] = rows inside the noise FOV band (rows 20 ..
+// R - 21), s_rows[1] = rows of the box (rows holding mask, row 0 when some row is empty) --
+// Vent_Analysis.py:344-351, the quirks as in oracle/vdp_oracle.calculate_snr
+__device__ inline void snr_slab_rows(const SnrBox &sb, const VolScalars &s, int64_t b, int64_t R,
+                                     int64_t x0, int nr, uint32_t *s_rows) {
+    if (threadIdx.x < 64) {
+        const int64_t x = x0 + threadIdx.x;
+        const bool ok = (int)threadIdx.x < nr;
+        const bool fov = ok && x >= 20 && x < R - 20;
+        const bool rin = ok && (sb.rowany[b * R + x] || (x == 0 && s.any_row_empty));
+        const uint64_t a = __ballot(fov), c = __ballot(rin);
+        if (threadIdx.x == 0) { s_rows[0] = (uint32_t)a; s_rows[1] = (uint32_t)c; }
+    }
+}
+// the slab rows of column col that are noise: in the FOV band and outside the box
+__device__ inline uint32_t snr_col_noise(const SnrBox &sb, const VolScalars &s, int64_t b,
+                                         int64_t Z, int64_t col, const uint32_t *s_rows) {
+    const int64_t y = col / Z, z = col % Z;
+    const bool cin = y >= s.cmin && y < s.cmax;
+    const bool sin_ = sb.sliceany[b * Z + z] || (z == 0 && s.any_slice_empty);
+    return s_rows[0] & ~((cin && sin_) ? s_rows[1] : 0u);
+}
+// one voxel's contributions (double accumulation, as k_snr always did)
+__device__ __forceinline__ void snr_add(double (&acc)[4], float v, bool sig, bool noise) {
+    if (sig) acc[0] += (double)v;
+    if (noise) { acc[1] += (double)v; acc[2] += (double)v * (double)v; acc[3] += 1.0; }
+}
+// block sums of the 4 partials in a fixed order -> dst[0..3]
+__device__ inline void snr_block_write(double (&acc)[4], double (*s_red)[VH_TPB / 64], double *dst) {
+    for (int q = 0; q < 4; ++q) {
+        double x = acc[q];
+        for (int off = 32; off > 0; off >>= 1) x += __shfl_down(x, off, 64);
+        if ((threadIdx.x & 63) == 0) s_red[q][threadIdx.x >> 6] = x;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        double x = 0.0;
+        for (int w = 0; w < VH_TPB / 64; ++w) x += s_red[threadIdx.x][w];
+        dst[threadIdx.x] = x;
+    }
 }
 
 // export.hip (rendering after the hot path)
