@@ -1086,7 +1086,8 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_eval(const float *__restrict__ L0
 // volume: n4_shared.h chain_wave_mu / chain_wave_sig fed by chain_wave_prod, over the field
 // differences read in raster order through the volume's raster -> compact permutation).
 #define WF_PROD 4   // producer waves of k_n4_welford
-__global__ void __launch_bounds__(64 * (2 + WF_PROD)) k_n4_welford(const float *D, const int32_t *perm,
+#define WF_TPB (64 * chain_waves(WF_PROD))
+__global__ void __launch_bounds__(WF_TPB) k_n4_welford(const float *D, const int32_t *perm,
                                                                   int64_t VS, const VolScalars *sc,
                                                                   N4State *st, int64_t vol0) {
     __shared__ ChainSlot slots[CH_SLOTS];
@@ -1096,10 +1097,11 @@ __global__ void __launch_bounds__(64 * (2 + WF_PROD)) k_n4_welford(const float *
     chain_reset(slots, &cs);
     __syncthreads();
     const int64_t n = sc[b].n_mask1;
-    const int w = threadIdx.x >> 6;
+    const int w = threadIdx.x >> 6, pid = chain_prod_id(w);
     if (w == 0) chain_wave_mu(n, slots, &cs);
     else if (w == 1) chain_wave_sig(n, slots, &cs);
-    else chain_wave_prod(D + b * VS, perm + b * VS, n, slots, &cs, w - 2, WF_PROD);
+    else if (pid >= 0 && pid < WF_PROD)
+        chain_wave_prod(D + b * VS, perm + b * VS, n, slots, &cs, pid, WF_PROD);
     __syncthreads();
     if (threadIdx.x == 0) st[b].conv_w = cs.conv;
 }
@@ -1137,6 +1139,9 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_refine(float *lat, int64_t lat_ca
     refine_axis_dev(T2, L, 2 * n0 - 3, 2 * n1 - 3, n2, 2);
 }
 
+#ifndef NF_PF
+#define NF_PF 16   // k_n4_final: image rows in flight per lane (8, 16 or 32)
+#endif
 // Final field at every voxel and the corrected image I / exp(B), in 32-row slabs (one bitmap word)
 // with one column per lane.  With keys != nullptr it also emits the VDP chain's sort keys of the
 // mask == 1 voxels (coalesced: a wave is 64 columns, a row's masked lanes are contiguous),
@@ -1150,6 +1155,8 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_final(const float *__restrict__ I
                                                     const VolScalars *sc, uint32_t *keys, SnrBox sb) {
     __shared__ uint32_t s_rows[2];
     __shared__ double s_red[4][VH_TPB / 64];
+    __shared__ float4 s_w[VH_SLAB];   // the slab's row weights and lattice bases: uniform per row,
+    __shared__ int s_base[VH_SLAB];   // read from LDS instead of a global load + wait per voxel
     const int64_t b = blockIdx.y;
     const int64_t CZ = C * Z;
     const int64_t sl = blockIdx.x / ncb;
@@ -1157,6 +1164,11 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_final(const float *__restrict__ I
     const int64_t x0 = sl * VH_SLAB;
     const int nr = (int)(R - x0 < VH_SLAB ? R - x0 : VH_SLAB);
     const VolScalars s = sc[b];
+    const DevAxis ax = lv.ax[0];
+    if ((int)threadIdx.x < nr) {
+        s_w[threadIdx.x] = *reinterpret_cast<const float4 *>(ax.w + 4 * (x0 + threadIdx.x));
+        s_base[threadIdx.x] = ax.base[x0 + threadIdx.x];
+    }
     snr_slab_rows(sb, s, b, R, x0, nr, s_rows);
     __syncthreads();
     const bool act = col < CZ;
@@ -1174,48 +1186,63 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_final(const float *__restrict__ I
     }
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
     if (act) {
-        const int64_t y = col / Z, z = col % Z;
+        const int64_t y = (uint32_t)col / (uint32_t)Z, z = col - y * Z;
         const int ncy = lv.ax[1].ncp;
         const int by = lv.ax[1].base[y];
         const float4 wy = *reinterpret_cast<const float4 *>(lv.ax[1].w + 4 * y);
         const double *p1 = P1 + b * q2_cap;
-        const DevAxis ax = lv.ax[0];
         const uint32_t word = colbits[(b * nw + sl) * CZ + col];
         const uint32_t sig = colbnz[(b * nw + sl) * CZ + col];
         const uint32_t noise = snr_col_noise(sb, s, b, Z, col, s_rows);
-        int wb = ax.base[x0];
+        snr_count(acc, noise);
+        int wb = s_base[0];
         // S9: the final field per S6 (float T window, float row sum), I / (float)exp((double)B)
         float t0 = (float)col_T(p1, wb, ncy, Z, by, wy, z), t1 = (float)col_T(p1, wb + 1, ncy, Z, by, wy, z);
         float t2 = (float)col_T(p1, wb + 2, ncy, Z, by, wy, z), t3 = (float)col_T(p1, wb + 3, ncy, Z, by, wy, z);
         const float *src = I + b * V + x0 * CZ + col;
         float *dst = out + b * V + x0 * CZ + col;
-        // rows in groups of 8: the group's image loads are issued together, then the field, exp and
-        // stores (the row walk of one column is otherwise a dependent load -> exp -> store chain)
-        for (int i0 = 0; i0 < nr; i0 += 8) {
-            float iv[8];
+        // the image loads of NF_PF rows are issued together, ahead of the field, exp and stores of
+        // their rows (the row walk of one column is otherwise a dependent load -> exp -> store
+        // chain); row weights and bases come from LDS 8 rows at a time
 #pragma unroll
-            for (int k = 0; k < 8; ++k) iv[k] = i0 + k < nr ? src[(int64_t)(i0 + k) * CZ] : 0.0f;
+        for (int f0 = 0; f0 < VH_SLAB; f0 += NF_PF) {
+            if (f0 >= nr) break;
+            float iv[NF_PF];
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const int i = i0 + k;
-                if (i >= nr) break;
-                const int64_t x = x0 + i;
-                const int bx = ax.base[x];
-                while (wb < bx) {
-                    ++wb;
-                    t0 = t1; t1 = t2; t2 = t3;
-                    t3 = (float)col_T(p1, wb + 3, ncy, Z, by, wy, z);
+            for (int k = 0; k < NF_PF; ++k) iv[k] = f0 + k < nr ? src[(int64_t)(f0 + k) * CZ] : 0.0f;
+#pragma unroll
+            for (int g0 = 0; g0 < NF_PF; g0 += 8) {
+                const int i0 = f0 + g0;
+                if (i0 >= nr) break;
+                float4 wv[8];
+                int bv[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {   // the group's LDS reads together, one wait
+                    wv[k] = s_w[(i0 + k) & (VH_SLAB - 1)];
+                    bv[k] = s_base[(i0 + k) & (VH_SLAB - 1)];
                 }
-                const float4 w = *reinterpret_cast<const float4 *>(ax.w + 4 * x);
-                const float bn = ((w.x * t0 + w.y * t1) + w.z * t2) + w.w * t3;
-                const float o = iv[k] / expf_cr(bn);
-                dst[(int64_t)i * CZ] = o;
-                snr_add(acc, iv[k], (sig >> i) & 1u, (noise >> i) & 1u);
-                if (emit) {
-                    const bool on = (word >> i) & 1u;
-                    const uint64_t bal = __ballot(on);
-                    if (on) keys[kpos + lanes_below(bal)] = f2key(o);
-                    kpos += __popcll(bal);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const int i = i0 + k;
+                    if (i >= nr) break;
+                    const int bx = bv[k];
+                    while (wb < bx) {
+                        ++wb;
+                        t0 = t1; t1 = t2; t2 = t3;
+                        t3 = (float)col_T(p1, wb + 3, ncy, Z, by, wy, z);
+                    }
+                    const float4 w = wv[k];
+                    const float bn = ((w.x * t0 + w.y * t1) + w.z * t2) + w.w * t3;
+                    const float x = iv[g0 + k];
+                    const float o = x / expf_cr(bn);
+                    dst[(int64_t)i * CZ] = o;
+                    snr_add(acc, x, (sig >> i) & 1u, (noise >> i) & 1u);
+                    if (emit) {
+                        const bool on = (word >> i) & 1u;
+                        const uint64_t bal = __ballot(on);
+                        if (on) keys[kpos + lanes_below(bal)] = f2key(o);
+                        kpos += __popcll(bal);
+                    }
                 }
             }
         }
@@ -1374,7 +1401,7 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
                 }
                 if (cm == 0) {
                     ScopedKTimer tm(b, "n4_welford", 0.0);
-                    k_n4_welford<<<(unsigned)ns, 64 * (2 + WF_PROD), 0, st>>>(b->d_D, b->d_perm, b->VS, b->d_sc,
+                    k_n4_welford<<<(unsigned)ns, WF_TPB, 0, st>>>(b->d_D, b->d_perm, b->VS, b->d_sc,
                                                                b->d_st, vol0);
                     VH_CHECK_LAUNCH();
                 }

@@ -479,6 +479,19 @@ struct ChainSlot {
 #ifndef CH_PRIO
 #define CH_PRIO 3
 #endif
+// Wave roles by SIMD.  A workgroup's waves are dealt to the CU's 4 SIMDs round-robin (wave w on
+// SIMD w % 4), and a producer's VALU instruction in flight on wave A's SIMD delays A's next
+// dependent step however A is prioritised.  So wave 0 (A) and wave 1 (B) keep SIMDs 0 and 1 to
+// themselves and the producers are the waves on SIMDs 2 and 3.  Producer index of wave w, or -1.
+#ifndef CH_SIMD_ROLES
+#define CH_SIMD_ROLES 1
+#endif
+__device__ __forceinline__ int chain_prod_id(int w) {
+    if (!CH_SIMD_ROLES) return w >= 2 ? w - 2 : -1;
+    return (w & 3) >= 2 ? (w >> 2) * 2 + (w & 1) : -1;
+}
+// waves a workgroup needs for np producers
+constexpr int chain_waves(int np) { return CH_SIMD_ROLES ? 4 * ((np + 1) / 2) : 2 + np; }
 struct ChainState {
     int a_done, b_done, c_done;   // blocks finished by wave A / wave B / the producer
     float mu, conv;

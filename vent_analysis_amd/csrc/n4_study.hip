@@ -35,6 +35,7 @@
 #ifndef ST_CH_PROD
 #define ST_CH_PROD 8   // producer waves of the convergence chain (n4_shared.h chain_wave_prod)
 #endif
+static_assert(chain_waves(ST_CH_PROD) <= ST_WAVES, "chain roles need more waves");
 #ifndef ST_CH_GS
 #define ST_CH_GS 8   // convergence-chain group size here (n4_shared.h ch_group): 8 measured 135M vs 167M cycles for 4
 #endif
@@ -845,10 +846,11 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
             ST_MARK(6);
             // ---- convergence of this iteration ----
             if (a.conv_mode == 0) {   // S7: ITK's float Welford recurrence, two waves
+                const int pid = chain_prod_id(wv);
                 if (wv == 0) chain_wave_mu<ST_CH_GS>(n, slots, &M.ch);
                 else if (wv == 1) chain_wave_sig<ST_CH_GS>(n, slots, &M.ch);
-                else if (wv < 2 + ST_CH_PROD)
-                    chain_wave_prod(Db, nullptr, n, slots, &M.ch, wv - 2, ST_CH_PROD);
+                else if (pid >= 0 && pid < ST_CH_PROD)
+                    chain_wave_prod(Db, nullptr, n, slots, &M.ch, pid, ST_CH_PROD);
             } else if (wv == 0) {   // S7x: item partials in item order
                 double sd = 0.0, sd2 = 0.0;
                 for (int i = lane; i < a.nitems; i += 64) {

@@ -4,6 +4,7 @@
 // Layout: volume b at [b][R][C][Z] (numpy C order, slice axis fastest).  A "column" is one
 // (col, slice) pair; column sweeps put one thread per column and walk the rows, so consecutive
 // lanes touch consecutive bytes for every row (coalesced).
+#include <cfloat>
 #include <climits>
 
 #include "vh_internal.h"
@@ -45,27 +46,24 @@ __global__ void __launch_bounds__(VH_TPB) k_mask_stats(const uint8_t *__restrict
     const int nc = c0 < CZ ? (int)(CZ - c0 < 4 ? CZ - c0 : 4) : 0;
     if (nc) {
         const uint8_t *m = mask + b * V + x0 * CZ + c0;
-        for (int i0 = 0; i0 < nr; i0 += 8) {   // 8 rows of loads in flight
-            uint32_t mv[8];
+        uint32_t mv[VH_SLAB];   // the slab's 32 row loads all in flight
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                mv[k] = 0u;
-                if (i0 + k < nr) {
-                    const uint8_t *p = m + (int64_t)(i0 + k) * CZ;
-                    if (VEC) mv[k] = *reinterpret_cast<const uint32_t *>(p);
-                    else
-                        for (int q = 0; q < nc; ++q) mv[k] |= (uint32_t)p[q] << (8 * q);
-                }
+        for (int k = 0; k < VH_SLAB; ++k) {
+            mv[k] = 0u;
+            if (k < nr) {
+                const uint8_t *p = m + (int64_t)k * CZ;
+                if (VEC) mv[k] = *reinterpret_cast<const uint32_t *>(p);
+                else
+                    for (int q = 0; q < nc; ++q) mv[k] |= (uint32_t)p[q] << (8 * q);
             }
+        }
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const int i = i0 + k;
+        for (int k = 0; k < VH_SLAB; ++k) {
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const uint32_t v = (mv[k] >> (8 * q)) & 0xFFu;
-                    w1[q] |= (uint32_t)(v == 1u) << (i & 31);
-                    wn[q] |= (uint32_t)(v != 0u) << (i & 31);
-                }
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t v = (mv[k] >> (8 * q)) & 0xFFu;
+                w1[q] |= (uint32_t)(v == 1u) << k;
+                wn[q] |= (uint32_t)(v != 0u) << k;
             }
         }
         const int64_t nw = (R + 31) >> 5;
@@ -84,9 +82,10 @@ __global__ void __launch_bounds__(VH_TPB) k_mask_stats(const uint8_t *__restrict
         n1 += (unsigned)__popc(w1[q]);
         rows |= wn[q];
         const int64_t col = c0 + q;
-        if (wn[q]) {
-            colany[b * C + col / Z] = 1;
-            sliceany[b * Z + col % Z] = 1;
+        if (wn[q]) {   // 32-bit division (CZ < 2^31, check_dims)
+            const uint32_t y = (uint32_t)col / (uint32_t)Z;
+            colany[b * C + y] = 1;
+            sliceany[b * Z + ((uint32_t)col - y * (uint32_t)Z)] = 1;
         }
         if (w1[q]) {
             const unsigned long long idx =
@@ -806,6 +805,22 @@ __device__ __forceinline__ uint32_t ps_nonzero(uint32_t g) {
     return ((((g & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | g) >> 7) & 0x01010101u;
 }
 
+// Division-free forms of the classify tests (bit-identical to the IEEE float division): for
+// 0 < m < inf and a positive normal float e, RN(v / m) <= e  <=>  v < u * m, or v == u * m when e's
+// significand is even (round-half-even picks e), where u = (e + succ(e)) / 2.  u has 25
+// significant bits and m 24, so u * m is exact in double; the tie folds into the bound by moving
+// it up one double ulp, and as v is a float, "v < bound" equals "v < the bound rounded up to a
+// float".  So each test is one float compare; NaN v fails every one, as RN(NaN) <= e does.
+// RN(q) < t is RN(q) <= pred(t).
+__device__ __forceinline__ float le_bound(float e, float m) {
+    const float s = __uint_as_float(__float_as_uint(e) + 1u);
+    double u = (((double)e + (double)s) * 0.5) * (double)m;
+    if ((__float_as_uint(e) & 1u) == 0u) u = __longlong_as_double(__double_as_longlong(u) + 1);
+    float f = (float)u;
+    if ((double)f < u) f = __uint_as_float(__float_as_uint(f) + 1u);   // round up (inf stays)
+    return f;
+}
+
 // per-word flags (precomputed once per block; the word set is the same for every plane)
 #define PSF_ZW0 1u      // zw == 0
 #define PSF_ZWL 2u      // zw == ZW - 1
@@ -838,6 +853,16 @@ __global__ void __launch_bounds__(PS_TPB) k_plane(const float *__restrict__ n4,
     const int64_t vb = b * g.V;
     float m = 0.0f, p99 = 0.0f;
     if (CL) { m = sc[b].mean_anchor; p99 = sc[b].p99; }
+    // division-free tests when the scalars allow them (block-uniform), else IEEE divisions
+    const float tpred = __uint_as_float(__float_as_uint(thresh) - 1u);
+    const bool fast = CL && m > 0.0f && m <= FLT_MAX && p99 > 0.0f && p99 <= FLT_MAX &&
+                      thresh >= FLT_MIN && thresh <= FLT_MAX && tpred >= FLT_MIN;
+    float f_thr = 0.0f, f_lb[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    if (fast) {
+        f_thr = le_bound(tpred, m);
+        const float edges[5] = {0.16f, 0.34f, 0.52f, 0.7f, 0.88f};
+        for (int e = 0; e < 5; ++e) f_lb[e] = le_bound(edges[e], p99);
+    }
 
     // word sets: loads (raw rows, or def rows in border mode), def rows, output rows
     const int hl = CL ? 2 : 1;
@@ -946,15 +971,26 @@ __global__ void __launch_bounds__(PS_TPB) k_plane(const float *__restrict__ n4,
                     const float v[4] = {nv[k].x, nv[k].y, nv[k].z, nv[k].w};
                     uint32_t r = 0u, c = 0u;
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        if (!((mk[k] >> (8 * q)) & 0xFFu)) continue;
-                        // IEEE f32 division, float32(thresh)
-                        r |= (uint32_t)((v[q] / m) < thresh) << (8 * q);
-                        if (lbk) {
-                            const uint32_t cls = lb_class(v[q] / p99);
-                            c |= cls << (8 * q);
-                            n_lb12 += (cls == 1u || cls == 2u);
+                    for (int q = 0; q < 4; ++q) {   // branch-free: deselected bytes give 0
+                        const bool on = ((mk[k] >> (8 * q)) & 0xFFu) != 0u;
+                        uint32_t below, cls;
+                        if (fast) {
+                            below = v[q] < f_thr;
+                            // LB class = 6 - #(edges with RN(v / p99) <= edge); NaN -> 0
+                            const uint32_t nle = (uint32_t)(v[q] < f_lb[0]) + (uint32_t)(v[q] < f_lb[1]) +
+                                                 (uint32_t)(v[q] < f_lb[2]) + (uint32_t)(v[q] < f_lb[3]) +
+                                                 (uint32_t)(v[q] < f_lb[4]);
+                            cls = v[q] == v[q] ? 6u - nle : 0u;
+                        } else {
+                            // IEEE f32 division, float32(thresh)
+                            below = (v[q] / m) < thresh;
+                            cls = lb_class(v[q] / p99);
                         }
+                        below = on ? below : 0u;
+                        cls = (on && lbk) ? cls : 0u;
+                        r |= below << (8 * q);
+                        c |= cls << (8 * q);
+                        n_lb12 += (cls == 1u || cls == 2u);
                     }
                     raw[(p & 3) * RW + l_lds[k]] = r;
                     if (lbk)
@@ -1413,6 +1449,7 @@ __global__ void __launch_bounds__(VH_TPB) k_snr(const float *__restrict__ hp,
         const int64_t nw = (R + 31) >> 5;
         const uint32_t sig = colbnz[(b * nw + sl) * CZ + col];
         const uint32_t noise = snr_col_noise(sb, s, b, Z, col, s_rows);
+        snr_count(acc, noise);
         const uint32_t need = sig | noise;
         const float *a = hp + b * V + x0 * CZ + col;
         for (int i0 = 0; i0 < nr; i0 += 8) {   // 8 rows of loads in flight

@@ -278,15 +278,22 @@ __device__ inline void snr_slab_rows(const SnrBox &sb, const VolScalars &s, int6
 // the slab rows of column col that are noise: in the FOV band and outside the box
 __device__ inline uint32_t snr_col_noise(const SnrBox &sb, const VolScalars &s, int64_t b,
                                          int64_t Z, int64_t col, const uint32_t *s_rows) {
-    const int64_t y = col / Z, z = col % Z;
+    const int32_t y = (int32_t)((uint32_t)col / (uint32_t)Z), z = (int32_t)col - y * (int32_t)Z;
     const bool cin = y >= s.cmin && y < s.cmax;
     const bool sin_ = sb.sliceany[b * Z + z] || (z == 0 && s.any_slice_empty);
     return s_rows[0] & ~((cin && sin_) ? s_rows[1] : 0u);
 }
-// one voxel's contributions (double accumulation, as k_snr always did)
+// one voxel's contributions (double accumulation, as k_snr always did; a deselected voxel adds
+// +0.0, which leaves every sum unchanged).  The noise count is added per slab by snr_count.
 __device__ __forceinline__ void snr_add(double (&acc)[4], float v, bool sig, bool noise) {
-    if (sig) acc[0] += (double)v;
-    if (noise) { acc[1] += (double)v; acc[2] += (double)v * (double)v; acc[3] += 1.0; }
+    const double d = (double)v;
+    acc[0] += sig ? d : 0.0;
+    const double t = noise ? d : 0.0;
+    acc[1] += t;
+    acc[2] += t * t;
+}
+__device__ __forceinline__ void snr_count(double (&acc)[4], uint32_t noise) {
+    acc[3] += (double)__popc(noise);
 }
 // block sums of the 4 partials in a fixed order -> dst[0..3]
 __device__ inline void snr_block_write(double (&acc)[4], double (*s_red)[VH_TPB / 64], double *dst) {
