@@ -202,6 +202,12 @@ static void batch_run(vh_batch *b, const vh_run_opts &o, int n4_src) {
     b->have_result = true;
 }
 
+// the study kernel's spin-wait watchdog (n4_study.hip st_spin) leaves N4State.active = -2
+static void check_n4_watchdog(const N4State *st, int64_t nb) {
+    for (int64_t i = 0; i < nb; ++i)
+        if (st[i].active == -2) throw VhError{VH_ERR_HIP, "N4 study kernel: a synchronisation wait timed out"};
+}
+
 static void fill_results(vh_batch *b, vh_vdp_result *res) {
     std::vector<VolScalars> sc(b->nb);
     HIP_TRY(hipMemcpy(sc.data(), b->d_sc, sizeof(VolScalars) * b->nb, hipMemcpyDeviceToHost));
@@ -209,6 +215,7 @@ static void fill_results(vh_batch *b, vh_vdp_result *res) {
     if (b->opts.do_n4) {
         st.resize(b->nb);
         HIP_TRY(hipMemcpy(st.data(), b->d_st, sizeof(N4State) * b->nb, hipMemcpyDeviceToHost));
+        check_n4_watchdog(st.data(), b->nb);
     }
     const double *vox = b->opts.vox;
     // np.prod(np.divide(vox, 10)): sequential multiply (Vent_Analysis.py:166, 252)
@@ -392,6 +399,7 @@ int vh_n4(vh_ctx *ctx, const float *hp, const uint8_t *mask, int64_t R, int64_t 
         HIP_TRY(hipMemcpy(out, b->d_n4, sizeof(float) * batch * b->V, hipMemcpyDeviceToHost));
         std::vector<N4State> st(batch);
         HIP_TRY(hipMemcpy(st.data(), b->d_st, sizeof(N4State) * batch, hipMemcpyDeviceToHost));
+        check_n4_watchdog(st.data(), batch);
         for (int64_t i = 0; i < batch; ++i)
             for (int l = 0; l < prm->n_levels; ++l) {
                 if (iters) iters[i * prm->n_levels + l] = st[i].iters_level[l];

@@ -212,8 +212,9 @@ void vh_ensure_n4_workspace(vh_batch *b, const vh_n4_params &prm) {
         b->VS = (b->V + 63) & ~(int64_t)63;   // compact-array stride: 256-byte aligned volumes
         const int64_t nch = b->nb * ((b->VS + N4_CH - 1) / N4_CH);
         HIP_TRY(hipMalloc(&b->d_L0, sizeof(float) * b->nb * b->VS));
-        HIP_TRY(hipMalloc(&b->d_U, sizeof(float) * b->nb * b->VS));
-        HIP_TRY(hipMalloc(&b->d_D, sizeof(float) * b->nb * b->VS));
+        // U and D twice: the study driver keeps the last kept iteration's while computing the next
+        HIP_TRY(hipMalloc(&b->d_U, sizeof(float) * 2 * b->nb * b->VS));
+        HIP_TRY(hipMalloc(&b->d_D, sizeof(float) * 2 * b->nb * b->VS));
         HIP_TRY(hipMalloc(&b->d_perm, sizeof(int32_t) * b->nb * b->VS));
         HIP_TRY(hipMalloc(&b->d_ridx, sizeof(int32_t) * b->nb * b->VS));
         HIP_TRY(hipMalloc(&b->d_cp, sizeof(int32_t) * (b->nb + 1)));
@@ -1453,7 +1454,10 @@ void vh_launch_n4(vh_batch *b, const vh_n4_params &prm) {
     // and a study's state fits in LDS, else per-iteration sweeps over the whole batch
     int mode = b->n4_mode;
     if (const char *e = getenv("VH_N4_MODE")) mode = atoi(e);
-    const bool fits = vh_n4_study_eligible(b, prm, nullptr);
+    size_t study_lds = 0;
+    const bool fits = vh_n4_study_eligible(b, prm, &study_lds);
+    if (getenv("VH_N4_DEBUG"))
+        fprintf(stderr, "N4 study driver: %s, %zu B LDS\n", fits ? "eligible" : "not eligible", study_lds);
     if (mode == 2 && !fits) throw VhError{VH_ERR_ARG, "n4_mode=2: study state exceeds the LDS budget"};
     b->n4_used_study = mode == 2 || (mode == 0 && fits && b->nb >= 16);
     if (!b->n4_used_study) {   // the study kernel computes L0 / U itself

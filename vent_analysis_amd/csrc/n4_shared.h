@@ -467,7 +467,9 @@ __device__ __forceinline__ bool r3_bin_min(const Range3 &r, const float *u, int 
 // The recurrences are inherently serial (the float running mean drifts); the slot ring and three
 // LDS counters let the three waves overlap (A and B then do nothing but their steps).  Result: conv = (float)sqrt(sig / (n-1)) / mu.
 // ---------------------------------------------------------------------------------------------
+#ifndef CH_SLOTS
 #define CH_SLOTS 16
+#endif
 struct ChainSlot {
     double2 ab[64];    // (1 - 1/k, p / k) for wave A; (1, 0) past the end (a no-op step)
     double2 cs[64];    // ((k - 1) / k, (double)(p - mu_prev)^2): c by the producer, s by wave B
@@ -657,6 +659,7 @@ __device__ __forceinline__ double chain_block64(const double2 *q, float *murec, 
 // took ~3.3k cycles per block (its global loads wait at every hand-off), several keep the serial
 // waves fed.  Each prefetches its next block's d (and perm entries two blocks ahead) while it
 // processes the current one.
+template <int NS = CH_SLOTS>
 __device__ void chain_wave_prod(const float *Dr, const int32_t *perm, int64_t n, ChainSlot *slots,
                                 ChainState *cs, int pid, int np) {
     const int lane = threadIdx.x & 63;
@@ -672,11 +675,11 @@ __device__ void chain_wave_prod(const float *Dr, const int32_t *perm, int64_t n,
     };
     int32_t p1 = ld_perm(blk + np);
     float dnext = ld_d(blk, ld_perm(blk));
-    int bseen = 0;   // last b_done read: slots of blocks < bseen + CH_SLOTS are free
+    int bseen = 0;   // last b_done read: slots of blocks < bseen + NS are free
     unsigned long long wt = 0;
     CH_T0();
     for (; blk < nblk; blk += np) {
-        ChainSlot &S = slots[blk % CH_SLOTS];
+        ChainSlot &S = slots[blk % NS];
         const int64_t j = blk * 64 + lane;
         const float d = dnext;
         dnext = ld_d(blk + np, p1);
@@ -688,8 +691,8 @@ __device__ void chain_wave_prod(const float *Dr, const int32_t *perm, int64_t n,
         const double2 ab = ok ? make_double2(1.0 - r, (double)(float)((double)p * r))   // p / k, div_r form
                               : make_double2(1.0, 0.0);
         const double c = (kd - 1.0) / kd;
-        if (blk >= CH_SLOTS + bseen)
-            CH_WAIT(wt, while ((bseen = lds_load_acq(&cs->b_done)) <= (int)(blk - CH_SLOTS)) __builtin_amdgcn_s_sleep(1));
+        if (blk >= NS + bseen)
+            CH_WAIT(wt, while ((bseen = lds_load_acq(&cs->b_done)) <= (int)(blk - NS)) __builtin_amdgcn_s_sleep(1));
         S.ab[lane] = ab;
         S.cs[lane] = make_double2(c, 0.0);
         S.p[lane] = p;
@@ -700,10 +703,11 @@ __device__ void chain_wave_prod(const float *Dr, const int32_t *perm, int64_t n,
 }
 
 // Before a chain: every slot's ready flag cleared (a flag left from the previous chain could name
-// the same block).  Threads [0, CH_SLOTS) of the workgroup, then a workgroup barrier.
-__device__ __forceinline__ void chain_reset(ChainSlot *slots, ChainState *cs) {
-    if (threadIdx.x < CH_SLOTS) slots[threadIdx.x].ready = 0;
-    if (threadIdx.x == 0) {
+// the same block).  Threads (or lanes, tid = lane) [0, NS), then a barrier / the go signal.
+template <int NS = CH_SLOTS>
+__device__ __forceinline__ void chain_reset(ChainSlot *slots, ChainState *cs, int tid = threadIdx.x) {
+    if (tid < NS) slots[tid].ready = 0;
+    if (tid == 0) {
         cs->a_done = 0;
         cs->b_done = 0;
         cs->c_done = 0;
@@ -711,7 +715,7 @@ __device__ __forceinline__ void chain_reset(ChainSlot *slots, ChainState *cs) {
 }
 
 // wave A: the mu recurrence on lane 0, block by block as the producer fills them.
-template <int GS = 8>
+template <int GS = 8, int NS = CH_SLOTS>
 __device__ void chain_wave_mu(int64_t n, ChainSlot *slots, ChainState *cs) {
     const int lane = threadIdx.x & 63;
     double mu = 0.0;
@@ -720,7 +724,7 @@ __device__ void chain_wave_mu(int64_t n, ChainSlot *slots, ChainState *cs) {
     __builtin_amdgcn_s_setprio(CH_PRIO);   // the serial waves win issue arbitration on their SIMD
     CH_T0();
     for (int64_t blk = 0; blk < nblk; ++blk) {
-        ChainSlot &S = slots[blk % CH_SLOTS];
+        ChainSlot &S = slots[blk % NS];
         CH_WAIT(wt, while (lds_load_acq(&S.ready) != (int)(blk + 1)) __builtin_amdgcn_s_sleep(1));
         if (lane == 0) mu = chain_block64<true, GS>(S.ab, S.mu, mu);
         wave_lds_order();
@@ -734,7 +738,7 @@ __device__ void chain_wave_mu(int64_t n, ChainSlot *slots, ChainState *cs) {
 }
 
 // wave B.  Returns conv in cs->conv.
-template <int GS = 8>
+template <int GS = 8, int NS = CH_SLOTS>
 __device__ void chain_wave_sig(int64_t n, ChainSlot *slots, ChainState *cs) {
     const int lane = threadIdx.x & 63;
     double sig = 0.0;
@@ -743,7 +747,7 @@ __device__ void chain_wave_sig(int64_t n, ChainSlot *slots, ChainState *cs) {
     __builtin_amdgcn_s_setprio(CH_PRIO);
     CH_T0();
     for (int64_t blk = 0; blk < nblk; ++blk) {
-        ChainSlot &S = slots[blk % CH_SLOTS];
+        ChainSlot &S = slots[blk % NS];
         const int64_t j = blk * 64 + lane;
         CH_WAIT(wt, while (lds_load_acq(&cs->a_done) <= (int)blk) __builtin_amdgcn_s_sleep(1));
         const float q = S.p[lane] - S.mu[lane];

@@ -33,16 +33,19 @@
 #define ST_HC 8        // LDS histogram copies
 #define ST_MAX_LDS (160 * 1024)
 #ifndef ST_CH_PROD
-#define ST_CH_PROD 8   // producer waves of the convergence chain (n4_shared.h chain_wave_prod)
+#define ST_CH_PROD 2   // producer waves of the convergence chain (n4_shared.h chain_wave_prod)
 #endif
-static_assert(chain_waves(ST_CH_PROD) <= ST_WAVES, "chain roles need more waves");
+#define ST_CW (2 + ST_CH_PROD)   // chain waves (conv_mode 0): A, B, producers
+#ifndef ST_CH_NS
+#define ST_CH_NS 4     // chain slot ring here (2 producers, 4 slots: within 1 % of 16 slots)
+#endif
 #ifndef ST_CH_GS
 #define ST_CH_GS 8   // convergence-chain group size here (n4_shared.h ch_group): 8 measured 135M vs 167M cycles for 4
 #endif
 
 // ST_PROF builds (scripts/dev/phase_ab.sh): block 0 prints shader cycles per phase at the end
 #ifdef ST_PROF
-#define ST_MARK(k) do { if (threadIdx.x == 0) { const unsigned long long _c = clock64(); \
+#define ST_MARK(k) do { if (t == st_pt) { const unsigned long long _c = clock64(); \
     st_prof[k] += _c - st_t0; st_t0 = _c; } } while (0)
 #else
 #define ST_MARK(k) do { } while (0)
@@ -75,6 +78,8 @@ struct StudyArgs {
     // dynamic-LDS carve (byte offsets)
     int32_t o_E, o_tab0, o_tab1, o_lat, o_den, o_P10, o_P11, o_ipart, o_rpart, o_misc, o_scr, o_wave,
         o_order;
+    int32_t o_chain, o_latp;   // conv_mode 0: the chain's slot ring; the lattice before the last update
+    int64_t half;              // U and D are double-buffered: second buffer at + half floats
     int32_t s_cap;   // doubles of a wave's ring row (>= 64, >= ny * KT)
     int32_t nb_ring; // ring rows per wave (<= FIT_NB)
     int32_t o_wx;    // row weights of the current level: Wx[2][R][4] doubles (w^3/sum w^2, w^2)
@@ -91,7 +96,24 @@ struct StudyMisc {
     double sd, sd2, conv;
     int32_t nc[2][3];
     ChainState ch;
+    // conv_mode 0 hand-offs between the compute waves and the chain waves
+    int32_t go, go_op, go_d;   // request sequence number; 0 = run the chain on D[go_d], 1 = level end
+    int32_t ch_seq;            // sequence number of the last finished chain (after ch.conv)
+    int32_t gb_cnt, gb_gen;    // the compute waves' barrier
+    int32_t itn, cur, uin;     // iterations of the level, P1 buffer of the last field, U buffer
+    int32_t wd;                // a spin-wait watchdog fired (N4State.active = -2; the host raises)
 };
+
+// Spin-wait step with a budget: ~0.5 s of s_sleep, far beyond any legitimate wait (a study's whole
+// N4 takes ~70 ms).  When it is spent the wait gives up and the kernel runs to its end with the
+// watchdog flag set, rather than leaving waves that never finish.
+#define ST_SPIN_MAX (1 << 22)
+__device__ __forceinline__ bool st_spin(int &budget, int32_t *wd) {
+    __builtin_amdgcn_s_sleep(2);
+    if (--budget > 0) return true;
+    *wd = 1;
+    return false;
+}
 
 // One level's axis tables staged in LDS.
 struct TabW {
@@ -430,27 +452,55 @@ __device__ void exact_row(const StudyArgs &a, int64_t b, const float *Ub, int x,
     }
 }
 
+// Barrier of the compute waves (conv_mode 0: the chain waves run alongside): one lane per wave
+// counts in at an LDS counter and the last flips the generation.  Workgroup-scope release before
+// (this wave's stores complete) and acquire after, as __syncthreads.
+struct Grp {
+    int t, n, w, nw;   // thread / threads, wave / waves of the group
+    bool hw;           // the group is the whole workgroup: __syncthreads
+};
+__device__ __forceinline__ void gsync(const Grp &g, StudyMisc &M) {
+    if (g.hw) {
+        __syncthreads();
+        return;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if ((threadIdx.x & 63) == 0) {
+        const int gen = __hip_atomic_load(&M.gb_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (atomicAdd(&M.gb_cnt, 1) == g.nw - 1) {
+            __hip_atomic_store(&M.gb_cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_store(&M.gb_gen, gen + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else {
+            int bud = ST_SPIN_MAX;
+            while (__hip_atomic_load(&M.gb_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == gen &&
+                   st_spin(bud, &M.wd)) {
+            }
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
 __device__ float exact_min_study(const StudyArgs &a, int64_t b, const float *Ub, float *s_cmax,
-                                 float *s_min) {
-    const int t = threadIdx.x;
-    const int per = (a.R + ST_TPB - 1) / ST_TPB;
+                                 float *s_min, const Grp &g, StudyMisc &M) {
+    const int t = g.t;
+    const int per = (a.R + g.n - 1) / g.n;
     const int s0 = min(t * per, a.R), e0 = min(s0 + per, a.R);
     float cmax = -FLT_MAX, dummy = FLT_MAX;
     for (int x = s0; x < e0; ++x) exact_row(a, b, Ub, x, cmax, dummy, false);
     s_cmax[t] = cmax;
-    __syncthreads();
+    gsync(g, M);
     if (t == 0) {
         float run = -FLT_MAX;
-        for (int i = 0; i < ST_TPB; ++i) { const float v = s_cmax[i]; s_cmax[i] = run; run = v > run ? v : run; }
+        for (int i = 0; i < g.n; ++i) { const float v = s_cmax[i]; s_cmax[i] = run; run = v > run ? v : run; }
     }
-    __syncthreads();
+    gsync(g, M);
     float run = s_cmax[t], mn = FLT_MAX;
     for (int x = s0; x < e0; ++x) exact_row(a, b, Ub, x, run, mn, true);
     s_min[t] = mn;
-    __syncthreads();
+    gsync(g, M);
     float m = FLT_MAX;
     if (t == 0)
-        for (int i = 0; i < ST_TPB; ++i) m = s_min[i] < m ? s_min[i] : m;
+        for (int i = 0; i < g.n; ++i) m = s_min[i] < m ? s_min[i] : m;
     return m;
 }
 
@@ -501,7 +551,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
     double *const P1b0 = reinterpret_cast<double *>(smem + a.o_P10);
     double *const P1b1 = reinterpret_cast<double *>(smem + a.o_P11);
     double *ipart = reinterpret_cast<double *>(smem + a.o_ipart);
-    float4 *rpart = reinterpret_cast<float4 *>(smem + a.o_rpart);
+    float4 *const rpart0 = reinterpret_cast<float4 *>(smem + a.o_rpart);   // [2][nitems]: per U buffer
     int32_t *ordr = reinterpret_cast<int32_t *>(smem + a.o_order);
     char *scr = smem + a.o_scr;
 
@@ -517,14 +567,25 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
         }
         return;
     }
+    // Waves.  conv_mode 0: waves [0, ST_CW) run ITK's float Welford recurrence (S7) of each kept
+    // iteration while the other waves already compute the next iteration; ITK's while-condition on
+    // that recurrence's result then keeps the new iteration or discards it (the lattice, the U
+    // buffer and the field buffer of the last kept iteration are still there).  The arithmetic of
+    // every kept iteration is unchanged.  conv_mode 1: all waves compute, no speculation.
+    const bool split = a.conv_mode == 0;
+    Grp g;
+    g.hw = !split;
+    g.t = split ? t - 64 * ST_CW : t;
+    g.n = split ? ST_TPB - 64 * ST_CW : ST_TPB;
+    g.w = g.t >> 6;
+    g.nw = g.n >> 6;
+    const bool in_g = g.t >= 0;
     float *Lb = a.L0 + b * a.VS;
-    float *Ub = a.U + b * a.VS;
-    float *Db = a.D + b * a.VS;
     const int64_t fm = a.sc[b].first_masked;
-    // fit / eval scratch: lattice numerator (fixed point), then per-wave Q / S rows
+    // fit / eval scratch: lattice numerator (fixed point), then per-wave Q / S rows of the group
     unsigned long long *numfix = reinterpret_cast<unsigned long long *>(scr);
     FitRing ring;
-    ring.q = reinterpret_cast<double *>(scr + a.o_wave) + (size_t)wv * a.nb_ring * a.s_cap;
+    ring.q = reinterpret_cast<double *>(scr + a.o_wave) + (size_t)(in_g ? g.w : 0) * a.nb_ring * a.s_cap;
     ring.sx = nullptr;
     ring.rowcap = a.s_cap;
     ring.nr = 0;
@@ -533,10 +594,25 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
     double2 *V = reinterpret_cast<double2 *>(scr), *F = V + ST_FFT_N, *DEN = F + ST_FFT_N;
     double2 *TW = DEN + ST_FFT_N;
     unsigned long long *Hc = reinterpret_cast<unsigned long long *>(TW + VH_FFT_P / 2);
-    ChainSlot *slots = reinterpret_cast<ChainSlot *>(scr);
+    ChainSlot *const cslots = reinterpret_cast<ChainSlot *>(smem + a.o_chain);
+    float *const latp = reinterpret_cast<float *>(smem + a.o_latp);
     const int bins = a.bins;
+#ifdef ST_PROF
+    const int st_pt = split ? 64 * ST_CW : 0;   // the compute waves' first thread keeps the marks
+#endif
 
-    if (t == 0) M.item_ctr = 0;
+    if (t == 0) {
+        M.item_ctr = 0;
+        M.go = 0;
+        M.go_op = 0;
+        M.go_d = 0;
+        M.ch_seq = 0;
+        M.gb_cnt = 0;
+        M.gb_gen = 0;
+        M.cur = 0;
+        M.uin = 0;
+        M.wd = 0;
+    }
     if (wv == 0) find_first3(a, b, fm, M);
     {   // item schedule: items by row count, largest first (ties by index), so the dynamic item
         // queue of every pass ends on small items; the item order of every reduction is unchanged
@@ -558,15 +634,15 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
         }
     }
     __syncthreads();
-    for (;;) {   // L0, U = L0 and its range
+    for (;;) {   // L0, U = L0 (U buffer 0) and its range
         const int item = next_item(M, ordr, a.nitems);
         if (item < 0) break;
         Item it;
         if (!study_item(it, a, b, item)) {
-            if (lane == 0) rpart[item] = make_float4(-FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX);
+            if (lane == 0) rpart0[item] = make_float4(-FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX);
             continue;
         }
-        init_item(a, b, it, item, Lb, Ub, n, rpart);
+        init_item(a, b, it, item, Lb, a.U + b * a.VS, n, rpart0);
     }
     // every wave must have left the init queue before thread 0 resets the item counter for the
     // denominator pass (a late wave would otherwise take den-pass items)
@@ -576,13 +652,10 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
         const int nl0 = l0.ax[0].ncp * l0.ax[1].ncp * l0.ax[2].ncp;
         for (int e = t; e < nl0; e += ST_TPB) lat[e] = 0.0f;
     }
-    int cur = 0;   // P1b[cur] holds the last evaluated field
 #ifdef ST_PROF
     unsigned long long st_prof[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_t0 = clock64();
 #endif
-#ifdef CH_PROF
-    unsigned long long ch_w[3] = {0, 0, 0}, ch_t[3] = {0, 0, 0};
-#endif
+    int ch_seen = 0;   // chain waves: the last request taken
     for (int L = 0; L < a.nlev; ++L) {
         const DevLevel &lv = a.lvs->lv[L];
         char *tabp = smem + ((L & 1) ? a.o_tab1 : a.o_tab0);
@@ -609,275 +682,336 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
             Wx2[2 * x] = w2[0];
             Wx2[2 * x + 1] = w2[1];
         }
-        // ---- denominator of this level: sum of w^2 over the mask ----
+        // ---- denominator of this level: sum of w^2 over the mask (the compute waves' rings) ----
         for (int e = t; e < 2 * nlat; e += ST_TPB) numfix[e] = 0ull;
         if (t == 0) M.item_ctr = 0;
         __syncthreads();
-        for (;;) {
-            const int item = next_item(M, ordr, a.nitems);
-            if (item < 0) break;
-            Item it;
-            if (!study_item(it, a, b, item)) continue;
-            fit_item<1, true>(it, T, Wk2, Wx2, ncy, ncz, a.Z, bins, Ub, n, sE, 0.0f, 1.0, ring, a.nb_ring,
-                        numfix);
-        }
-        __syncthreads();
-        ST_MARK(0);
-        for (int e = t; e < nlat; e += ST_TPB) den[e] = fix128_get(numfix + 2 * e, numfix + 2 * e + 1);
-        // ---- iterations ----
-        int itn = 0;
-        for (;;) {
-            __syncthreads();
-            if (wv == 0) {   // ctrl: convergence, ITK's while-condition, bin range
-                Range3 r;
-                r3_init(r);
-                for (int i = lane; i < a.nitems; i += 64) {
-                    const float4 p = rpart[i];
-                    Range3 o;
-                    o.mx = p.x; o.m1 = p.y; o.m2 = p.z; o.m3 = p.w;
-                    r3_merge(r, o);
-                }
-                r = r3_wave(r);
-                if (lane == 0) {
-                    M.stop = 0;
-                    M.exact = 0;
-                    if (itn > 0) {
-                        if (a.conv_mode == 0) {
-                            M.conv = (double)M.ch.conv;
-                            if (!(M.ch.conv > a.thresh) || itn >= a.lvs->max_iters[L]) M.stop = 1;
-                        } else {
-                            M.conv = conv_of(M.sd, M.sd2, (double)n);
-                            if (!(M.conv > (double)a.thresh) || itn >= a.lvs->max_iters[L]) M.stop = 1;
-                        }
-                    }
-                    if (!M.stop) {
-                        float u[3];
-                        for (int q = 0; q < M.nfirst; ++q) u[q] = Ub[M.foff[q]];
-                        float bmin;
-                        M.bmax = r.mx;
-                        if (r3_bin_min(r, u, M.nfirst, bmin)) {
-                            M.bin_min = bmin;
-                            M.slope = (r.mx - bmin) / (float)(bins - 1);
-                        } else {
-                            M.exact = 1;
-                        }
-                    }
-                }
-            }
-            __syncthreads();
-            ST_MARK(1);
-            if (M.stop) break;
-            if (M.exact) {
-                float *s_cmax = reinterpret_cast<float *>(scr);
-                const float m = exact_min_study(a, b, Ub, s_cmax, s_cmax + ST_TPB);
-                if (t == 0) {
-                    M.bin_min = m;
-                    M.slope = (M.bmax - m) / (float)(bins - 1);
-                }
-                __syncthreads();
-            }
-            ++itn;
-            ST_MARK(1);
-            const float bmin = M.bin_min, slope = M.slope;
-            const double rinv = 1.0 / (double)slope;   // div_r form of the bin division
-            // ---- hist (S3): one packed 64-bit add per value ----
-            for (int i = t; i < ST_HC * VH_MAX_BINS; i += ST_TPB) Hc[i] = 0ull;
-            __syncthreads();
-            {
-                unsigned long long *H = Hc + (lane & (ST_HC - 1)) * VH_MAX_BINS;
-                for (int64_t j0 = (int64_t)t * 16; j0 < n; j0 += (int64_t)ST_TPB * 16) {
-                    float u[16];
-                    if (j0 + 16 <= n) {
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            const float4 v = reinterpret_cast<const float4 *>(Ub + j0)[q];
-                            u[4 * q] = v.x; u[4 * q + 1] = v.y; u[4 * q + 2] = v.z; u[4 * q + 3] = v.w;
-                        }
-                    } else {
-#pragma unroll
-                        for (int k = 0; k < 16; ++k) u[k] = j0 + k < n ? Ub[j0 + k] : __int_as_float(0x7fc00000);
-                    }
-#pragma unroll
-                    for (int k = 0; k < 16; ++k) {
-                        int idx;
-                        const unsigned long long w = hist_pack(u[k], bmin, rinv, bins, idx);
-                        atomicAdd(&H[idx], w);
-                    }
-                }
-            }
-            __syncthreads();
-            ST_MARK(2);
-            // ---- emap (same arithmetic as n4.hip k_n4_emap and the oracle) ----
-            {
-                const int P = VH_FFT_P, off = (P - bins) / 2;
-                const float sFWHM = a.fwhm / slope;
-                const float ef = (float)(4.0 * LN2 / (double)(sFWHM * sFWHM));
-                const float sf = (float)(2.0 * sqrt(LN2 / PI_D) / (double)sFWHM);
-                static_assert(VH_FFT_P / 2 <= ST_TPB, "one twiddle per thread");
-                const double2 twv = t < P / 2 ? a.tw[t] : make_double2(0.0, 0.0);   // in flight
-                for (int i = t; i < P; i += ST_TPB) {   // histogram series and Gaussian kernel
-                    const int h = i - off;
-                    unsigned long long s = 0ull;
-                    if (h >= 0 && h < bins)
-                        for (int q = 0; q < ST_HC; ++q) {
-                            const unsigned long long w = Hc[q * VH_MAX_BINS + h];
-                            s += (hist_count(w) << 24) - hist_osum(w);
-                            if (h > 0) s += hist_osum(Hc[q * VH_MAX_BINS + h - 1]);
-                        }
-                    V[fpad(i)] = make_double2((double)s * (1.0 / 16777216.0), 0.0);
-                    double fx;
-                    if (i == 0) {
-                        fx = (double)sf;
-                    } else if (i == P / 2) {
-                        fx = (double)sf * exp(-0.25 * (double)((float)P * (float)P) * (double)ef);
-                    } else {
-                        const float nf = (float)(i < P / 2 ? i : P - i);
-                        fx = (double)(sf * expf_cr(-(nf * nf) * ef));
-                    }
-                    F[fpad(i)] = make_double2(fx, 0.0);
-                }
-                if (t < P / 2) TW[t] = twv;
-                __syncthreads();
-                if (wv < 2) wave_fft_lds(wv ? F : V, TW, false, FftId(), FftId());
-                __syncthreads();
-                if (wv == 0) {   // Wiener filter (first pass), inverse, clamp and the moment series (last pass)
-                    const double noise = (double)a.noise;
-                    wave_fft_lds(V, TW, true,
-                        [=](int i, double2 v) {
-                            const double2 f = F[fpad(i)];
-                            const double fa = f.x, fb = f.y;
-                            const double g = fa / ((fa * fa - (-fb) * fb) + noise);
-                            return make_double2(v.x * g, v.y * g);
-                        },
-                        [=](int i, double2 v) {
-                            const double ur = v.x > 0.0 ? v.x : 0.0;
-                            const float c = bmin + ((float)i - (float)off) * slope;
-                            DEN[fpad(i)] = make_double2(ur, 0.0);
-                            return make_double2((double)c * ur, 0.0);
-                        });
-                }
-                __syncthreads();
-                if (wv < 2) {   // each series: forward, times the kernel's transform (last pass), inverse
-                    double2 *x = wv ? DEN : V;
-                    wave_fft_lds(x, TW, false, FftId(), [=](int i, double2 v) {
-                        const double2 f = F[fpad(i)];
-                        const double fa = f.x, fb = f.y;
-                        return make_double2(v.x * fa - v.y * fb, v.x * fb + v.y * fa);
-                    });
-                    wave_fft_lds(x, TW, true, FftId(), FftId());
-                }
-                __syncthreads();
-                for (int i = t; i < bins; i += ST_TPB) {
-                    const double d = DEN[fpad(i + off)].x;
-                    sE[i] = d != 0.0 ? (float)(V[fpad(i + off)].x / d) : 0.0f;
-                }
-                __syncthreads();
-            }
-            ST_MARK(3);
-            // ---- fit ----
-            for (int e = t; e < 2 * nlat; e += ST_TPB) numfix[e] = 0ull;
-            if (t == 0) M.item_ctr = 0;
-            __syncthreads();
-            for (;;) {
-                const int item = next_item(M, ordr, a.nitems);
-                if (item < 0) break;
-                Item it;
-                if (!study_item(it, a, b, item)) continue;
-                fit_item<0, true>(it, T, Wk3, Wx3, ncy, ncz, a.Z, bins, Ub, n, sE, bmin, rinv, ring,
-                            a.nb_ring, numfix);
-            }
-            __syncthreads();
-            ST_MARK(4);
-            // ---- lattice update and P1 ----
-            for (int e = t; e < nlat; e += ST_TPB) {
-                const double d = den[e];
-                const double num = fix128_get(numfix + 2 * e, numfix + 2 * e + 1);
-                const float phi = d != 0.0 ? (float)(num / d) : 0.0f;
-                lat[e] += phi;
-            }
-            __syncthreads();
-            double *P1n = cur ? P1b0 : P1b1;
-            double *P1o = cur ? P1b1 : P1b0;
-            for (int e = t; e < ncx * ncy * a.Z; e += ST_TPB) {
-                const int ij = e / a.Z, z = e % a.Z;
-                const float4 w = T.wz[z];
-                const float *l = lat + ij * ncz + T.bz[z];
-                P1n[e] = (double)w.x * (double)l[0] + (double)w.y * (double)l[1] +
-                         (double)w.z * (double)l[2] + (double)w.w * (double)l[3];
-            }
-            if (t == 0) M.item_ctr = 0;
-            __syncthreads();
-            ST_MARK(5);
-            // ---- eval ----
-            {
-                const bool first_of_level = itn == 1;
-                const bool bo_mode = !(L == 0 && first_of_level);
-                const int so = (first_of_level && L > 0) ? ((L - 1) & 1) : (L & 1);
-                const TabV To = tab_view(smem + (so ? a.o_tab1 : a.o_tab0), a.R, a.C, a.Z, a.kcap);
-                const int ncyo = M.nc[so][1];
+        {
+            const int uin = M.uin;
+            float *const Ub = a.U + uin * a.half + b * a.VS;
+            if (in_g)
                 for (;;) {
                     const int item = next_item(M, ordr, a.nitems);
                     if (item < 0) break;
                     Item it;
-                    if (!study_item(it, a, b, item)) {
-                        if (lane == 0) {
-                            ipart[2 * item] = 0.0;
-                            ipart[2 * item + 1] = 0.0;
-                            rpart[item] = make_float4(-FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX);
-                        }
-                        continue;
-                    }
-                    const bool same = so == (L & 1);
-                    if (a.conv_mode == 0) {
-                        if (same)
-                            eval_item<true, 0>(it, item, a.Z, T, To, ncy, ncyo, P1n, P1o, bo_mode, Lb, Ub, Db, n, ipart, rpart);
-                        else
-                            eval_item<false, 0>(it, item, a.Z, T, To, ncy, ncyo, P1n, P1o, bo_mode, Lb, Ub, Db, n, ipart, rpart);
-                    } else {
-                        if (same)
-                            eval_item<true, 1>(it, item, a.Z, T, To, ncy, ncyo, P1n, P1o, bo_mode, Lb, Ub, Db, n, ipart, rpart);
-                        else
-                            eval_item<false, 1>(it, item, a.Z, T, To, ncy, ncyo, P1n, P1o, bo_mode, Lb, Ub, Db, n, ipart, rpart);
-                    }
+                    if (!study_item(it, a, b, item)) continue;
+                    fit_item<1, true>(it, T, Wk2, Wx2, ncy, ncz, a.Z, bins, Ub, n, sE, 0.0f, 1.0, ring,
+                                      a.nb_ring, numfix);
                 }
-            }
-            chain_reset(slots, &M.ch);
-            __syncthreads();
-            ST_MARK(6);
-            // ---- convergence of this iteration ----
-            if (a.conv_mode == 0) {   // S7: ITK's float Welford recurrence, two waves
-                const int pid = chain_prod_id(wv);
-                if (wv == 0) chain_wave_mu<ST_CH_GS>(n, slots, &M.ch);
-                else if (wv == 1) chain_wave_sig<ST_CH_GS>(n, slots, &M.ch);
-                else if (pid >= 0 && pid < ST_CH_PROD)
-                    chain_wave_prod(Db, nullptr, n, slots, &M.ch, pid, ST_CH_PROD);
-            } else if (wv == 0) {   // S7x: item partials in item order
-                double sd = 0.0, sd2 = 0.0;
-                for (int i = lane; i < a.nitems; i += 64) {
-                    sd += ipart[2 * i];
-                    sd2 += ipart[2 * i + 1];
-                }
-                for (int off = 32; off > 0; off >>= 1) {
-                    sd += __shfl_down(sd, off, 64);
-                    sd2 += __shfl_down(sd2, off, 64);
-                }
-                if (lane == 0) {
-                    M.sd = sd;
-                    M.sd2 = sd2;
-                }
-            }
-            cur ^= 1;
-            ST_MARK(7);
-#ifdef CH_PROF
-            if (t == 0 && a.conv_mode == 0)
-                for (int i = 0; i < 3; ++i) {
-                    ch_w[i] += M.ch.wait[i];
-                    ch_t[i] += M.ch.total[i];
-                }
-#endif
         }
+        __syncthreads();
+        ST_MARK(0);
+        for (int e = t; e < nlat; e += ST_TPB) den[e] = fix128_get(numfix + 2 * e, numfix + 2 * e + 1);
+        if (split && !in_g) {
+            // ---- chain waves: the recurrence of each kept iteration, on request ----
+            for (;;) {
+                int req, bud = ST_SPIN_MAX;
+                while ((req = lds_load_acq(&M.go)) == ch_seen && st_spin(bud, &M.wd)) {
+                }
+                if (req == ch_seen) break;   // watchdog
+                ch_seen = req;
+                if (M.go_op) break;   // level end
+                const float *Dk = a.D + M.go_d * a.half + b * a.VS;
+                if (wv == 0) {
+                    chain_wave_mu<ST_CH_GS, ST_CH_NS>(n, cslots, &M.ch);
+                } else if (wv == 1) {
+                    chain_wave_sig<ST_CH_GS, ST_CH_NS>(n, cslots, &M.ch);
+                    wave_lds_order();
+                    if (lane == 0) lds_store_rel(&M.ch_seq, req);   // after ch.conv
+                } else {
+                    chain_wave_prod<ST_CH_NS>(Dk, nullptr, n, cslots, &M.ch, wv - 2, ST_CH_PROD);
+                }
+            }
+        } else {
+            // ---- the iterations (compute waves) ----
+            int itn = 0;          // iterations kept in this level
+            int cur = M.cur;      // P1 buffer of the last kept field
+            int uin = M.uin;      // U buffer (and its rpart row) of the last kept iteration
+            for (;;) {
+                gsync(g, M);
+                float *const Ub = a.U + uin * a.half + b * a.VS;
+                const float4 *const rp_in = rpart0 + uin * a.nitems;
+                if (g.w == 0) {   // ctrl: ITK's while-condition (at the cap, or conv_mode 1), bin range
+                    Range3 r;
+                    r3_init(r);
+                    for (int i = lane; i < a.nitems; i += 64) {
+                        const float4 p = rp_in[i];
+                        Range3 o;
+                        o.mx = p.x; o.m1 = p.y; o.m2 = p.z; o.m3 = p.w;
+                        r3_merge(r, o);
+                    }
+                    r = r3_wave(r);
+                    if (lane == 0) {
+                        M.stop = 0;
+                        M.exact = 0;
+                        if (itn > 0) {
+                            if (split) {
+                                if (itn >= a.lvs->max_iters[L]) {   // no speculation past the cap
+                                    int bud = ST_SPIN_MAX;
+                                    while (lds_load_acq(&M.ch_seq) != M.go && st_spin(bud, &M.wd)) {
+                                    }
+                                    M.conv = (double)M.ch.conv;
+                                    M.stop = 1;
+                                }
+                            } else {
+                                M.conv = conv_of(M.sd, M.sd2, (double)n);
+                                if (!(M.conv > (double)a.thresh) || itn >= a.lvs->max_iters[L]) M.stop = 1;
+                            }
+                        }
+                        if (!M.stop) {
+                            float u[3];
+                            for (int q = 0; q < M.nfirst; ++q) u[q] = Ub[M.foff[q]];
+                            float bmin;
+                            M.bmax = r.mx;
+                            if (r3_bin_min(r, u, M.nfirst, bmin)) {
+                                M.bin_min = bmin;
+                                M.slope = (r.mx - bmin) / (float)(bins - 1);
+                            } else {
+                                M.exact = 1;
+                            }
+                        }
+                    }
+                }
+                gsync(g, M);
+                ST_MARK(1);
+                if (M.stop) break;
+                if (M.exact) {
+                    float *s_cmax = reinterpret_cast<float *>(scr);
+                    const float m = exact_min_study(a, b, Ub, s_cmax, s_cmax + g.n, g, M);
+                    if (g.t == 0) {
+                        M.bin_min = m;
+                        M.slope = (M.bmax - m) / (float)(bins - 1);
+                    }
+                    gsync(g, M);
+                }
+                const int itk = itn + 1;   // the iteration computed now
+                ST_MARK(1);
+                const float bmin = M.bin_min, slope = M.slope;
+                const double rinv = 1.0 / (double)slope;   // div_r form of the bin division
+                // ---- hist (S3): one packed 64-bit add per value ----
+                for (int i = g.t; i < ST_HC * VH_MAX_BINS; i += g.n) Hc[i] = 0ull;
+                gsync(g, M);
+                {
+                    unsigned long long *H = Hc + (lane & (ST_HC - 1)) * VH_MAX_BINS;
+                    for (int64_t j0 = (int64_t)g.t * 16; j0 < n; j0 += (int64_t)g.n * 16) {
+                        float u[16];
+                        if (j0 + 16 <= n) {
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) {
+                                const float4 v = reinterpret_cast<const float4 *>(Ub + j0)[q];
+                                u[4 * q] = v.x; u[4 * q + 1] = v.y; u[4 * q + 2] = v.z; u[4 * q + 3] = v.w;
+                            }
+                        } else {
+#pragma unroll
+                            for (int k = 0; k < 16; ++k) u[k] = j0 + k < n ? Ub[j0 + k] : __int_as_float(0x7fc00000);
+                        }
+#pragma unroll
+                        for (int k = 0; k < 16; ++k) {
+                            int idx;
+                            const unsigned long long w = hist_pack(u[k], bmin, rinv, bins, idx);
+                            atomicAdd(&H[idx], w);
+                        }
+                    }
+                }
+                gsync(g, M);
+                ST_MARK(2);
+                // ---- emap (same arithmetic as n4.hip k_n4_emap and the oracle) ----
+                {
+                    const int P = VH_FFT_P, off = (P - bins) / 2;
+                    const float sFWHM = a.fwhm / slope;
+                    const float ef = (float)(4.0 * LN2 / (double)(sFWHM * sFWHM));
+                    const float sf = (float)(2.0 * sqrt(LN2 / PI_D) / (double)sFWHM);
+                    // one twiddle per thread: P / 2 <= g.n (ST_TPB - 64 ST_CW)
+                    const double2 twv = g.t < P / 2 ? a.tw[g.t] : make_double2(0.0, 0.0);   // in flight
+                    for (int i = g.t; i < P; i += g.n) {   // histogram series and Gaussian kernel
+                        const int h = i - off;
+                        unsigned long long s = 0ull;
+                        if (h >= 0 && h < bins)
+                            for (int q = 0; q < ST_HC; ++q) {
+                                const unsigned long long w = Hc[q * VH_MAX_BINS + h];
+                                s += (hist_count(w) << 24) - hist_osum(w);
+                                if (h > 0) s += hist_osum(Hc[q * VH_MAX_BINS + h - 1]);
+                            }
+                        V[fpad(i)] = make_double2((double)s * (1.0 / 16777216.0), 0.0);
+                        double fx;
+                        if (i == 0) {
+                            fx = (double)sf;
+                        } else if (i == P / 2) {
+                            fx = (double)sf * exp(-0.25 * (double)((float)P * (float)P) * (double)ef);
+                        } else {
+                            const float nf = (float)(i < P / 2 ? i : P - i);
+                            fx = (double)(sf * expf_cr(-(nf * nf) * ef));
+                        }
+                        F[fpad(i)] = make_double2(fx, 0.0);
+                    }
+                    if (g.t < P / 2) TW[g.t] = twv;
+                    gsync(g, M);
+                    if (g.w < 2) wave_fft_lds(g.w ? F : V, TW, false, FftId(), FftId());
+                    gsync(g, M);
+                    if (g.w == 0) {   // Wiener filter (first pass), inverse, clamp and the moment series (last pass)
+                        const double noise = (double)a.noise;
+                        wave_fft_lds(V, TW, true,
+                            [=](int i, double2 v) {
+                                const double2 f = F[fpad(i)];
+                                const double fa = f.x, fb = f.y;
+                                const double gg = fa / ((fa * fa - (-fb) * fb) + noise);
+                                return make_double2(v.x * gg, v.y * gg);
+                            },
+                            [=](int i, double2 v) {
+                                const double ur = v.x > 0.0 ? v.x : 0.0;
+                                const float c = bmin + ((float)i - (float)off) * slope;
+                                DEN[fpad(i)] = make_double2(ur, 0.0);
+                                return make_double2((double)c * ur, 0.0);
+                            });
+                    }
+                    gsync(g, M);
+                    if (g.w < 2) {   // each series: forward, times the kernel's transform (last pass), inverse
+                        double2 *x = g.w ? DEN : V;
+                        wave_fft_lds(x, TW, false, FftId(), [=](int i, double2 v) {
+                            const double2 f = F[fpad(i)];
+                            const double fa = f.x, fb = f.y;
+                            return make_double2(v.x * fa - v.y * fb, v.x * fb + v.y * fa);
+                        });
+                        wave_fft_lds(x, TW, true, FftId(), FftId());
+                    }
+                    gsync(g, M);
+                    for (int i = g.t; i < bins; i += g.n) {
+                        const double d = DEN[fpad(i + off)].x;
+                        sE[i] = d != 0.0 ? (float)(V[fpad(i + off)].x / d) : 0.0f;
+                    }
+                    gsync(g, M);
+                }
+                ST_MARK(3);
+                // ---- fit ----
+                for (int e = g.t; e < 2 * nlat; e += g.n) numfix[e] = 0ull;
+                if (g.t == 0) M.item_ctr = 0;
+                gsync(g, M);
+                for (;;) {
+                    const int item = next_item(M, ordr, a.nitems);
+                    if (item < 0) break;
+                    Item it;
+                    if (!study_item(it, a, b, item)) continue;
+                    fit_item<0, true>(it, T, Wk3, Wx3, ncy, ncz, a.Z, bins, Ub, n, sE, bmin, rinv, ring,
+                                      a.nb_ring, numfix);
+                }
+                gsync(g, M);
+                ST_MARK(4);
+                // ---- lattice update (the kept lattice saved first) and P1 ----
+                for (int e = g.t; e < nlat; e += g.n) {
+                    const double d = den[e];
+                    const double num = fix128_get(numfix + 2 * e, numfix + 2 * e + 1);
+                    const float phi = d != 0.0 ? (float)(num / d) : 0.0f;
+                    if (split) latp[e] = lat[e];
+                    lat[e] += phi;
+                }
+                gsync(g, M);
+                double *P1n = cur ? P1b0 : P1b1;
+                double *P1o = cur ? P1b1 : P1b0;
+                for (int e = g.t; e < ncx * ncy * a.Z; e += g.n) {
+                    const int ij = e / a.Z, z = e % a.Z;
+                    const float4 w = T.wz[z];
+                    const float *l = lat + ij * ncz + T.bz[z];
+                    P1n[e] = (double)w.x * (double)l[0] + (double)w.y * (double)l[1] +
+                             (double)w.z * (double)l[2] + (double)w.w * (double)l[3];
+                }
+                if (g.t == 0) M.item_ctr = 0;
+                gsync(g, M);
+                ST_MARK(5);
+                // ---- eval: U into the other buffer, d into D[itk & 1] ----
+                {
+                    float *const Uo = a.U + (uin ^ 1) * a.half + b * a.VS;
+                    float *const Dw = a.D + (split ? (itk & 1) * a.half : 0) + b * a.VS;
+                    float4 *const rp_out = rpart0 + (uin ^ 1) * a.nitems;
+                    const bool first_of_level = itk == 1;
+                    const bool bo_mode = !(L == 0 && first_of_level);
+                    const int so = (first_of_level && L > 0) ? ((L - 1) & 1) : (L & 1);
+                    const TabV To = tab_view(smem + (so ? a.o_tab1 : a.o_tab0), a.R, a.C, a.Z, a.kcap);
+                    const int ncyo = M.nc[so][1];
+                    const bool same = so == (L & 1);
+                    for (;;) {
+                        const int item = next_item(M, ordr, a.nitems);
+                        if (item < 0) break;
+                        Item it;
+                        if (!study_item(it, a, b, item)) {
+                            if (lane == 0) {
+                                ipart[2 * item] = 0.0;
+                                ipart[2 * item + 1] = 0.0;
+                                rp_out[item] = make_float4(-FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX);
+                            }
+                            continue;
+                        }
+                        if (a.conv_mode == 0) {
+                            if (same)
+                                eval_item<true, 0>(it, item, a.Z, T, To, ncy, ncyo, P1n, P1o, bo_mode, Lb, Uo, Dw, n, ipart, rp_out);
+                            else
+                                eval_item<false, 0>(it, item, a.Z, T, To, ncy, ncyo, P1n, P1o, bo_mode, Lb, Uo, Dw, n, ipart, rp_out);
+                        } else {
+                            if (same)
+                                eval_item<true, 1>(it, item, a.Z, T, To, ncy, ncyo, P1n, P1o, bo_mode, Lb, Uo, Dw, n, ipart, rp_out);
+                            else
+                                eval_item<false, 1>(it, item, a.Z, T, To, ncy, ncyo, P1n, P1o, bo_mode, Lb, Uo, Dw, n, ipart, rp_out);
+                        }
+                    }
+                }
+                gsync(g, M);
+                ST_MARK(6);
+                // ---- keep iteration itk or not ----
+                if (split) {
+                    if (g.t == 0) {
+                        M.stop = 0;
+                        if (itn > 0) {   // ITK's while-condition on iteration itn's recurrence
+                            int bud = ST_SPIN_MAX;
+                                    while (lds_load_acq(&M.ch_seq) != M.go && st_spin(bud, &M.wd)) {
+                                    }
+                            M.conv = (double)M.ch.conv;
+                            if (!(M.ch.conv > a.thresh)) M.stop = 1;
+                        }
+                        if (!M.stop) {   // keep: request the recurrence of iteration itk
+                            for (int i = 0; i < ST_CH_NS; ++i) chain_reset<ST_CH_NS>(cslots, &M.ch, i);
+                            M.go_op = 0;
+                            M.go_d = itk & 1;
+                            lds_store_rel(&M.go, M.go + 1);
+                        }
+                    }
+                    gsync(g, M);
+                    if (M.stop) {   // discard iteration itk: the kept lattice goes back
+                        for (int e = g.t; e < nlat; e += g.n) lat[e] = latp[e];
+                        break;
+                    }
+                } else if (g.w == 0) {   // S7x: item partials in item order
+                    double sd = 0.0, sd2 = 0.0;
+                    for (int i = lane; i < a.nitems; i += 64) {
+                        sd += ipart[2 * i];
+                        sd2 += ipart[2 * i + 1];
+                    }
+                    for (int off = 32; off > 0; off >>= 1) {
+                        sd += __shfl_down(sd, off, 64);
+                        sd2 += __shfl_down(sd2, off, 64);
+                    }
+                    if (lane == 0) {
+                        M.sd = sd;
+                        M.sd2 = sd2;
+                    }
+                }
+                ST_MARK(7);
+                cur ^= 1;
+                uin ^= 1;
+                itn = itk;
+            }
+            if (g.t == 0) {
+                M.itn = itn;
+                M.cur = cur;
+                M.uin = uin;
+                if (split) {   // level end: release the chain waves
+                    M.go_op = 1;
+                    lds_store_rel(&M.go, M.go + 1);
+                }
+            }
+        }
+        __syncthreads();
+        ST_MARK(8);
         if (t == 0) {
-            stb->iters_level[L] = itn;
+            stb->iters_level[L] = M.itn;
             stb->conv_level[L] = (float)M.conv;
         }
         if (L < a.nlev - 1) {   // exact subdivision of the lattice for the next level
@@ -890,25 +1024,19 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
             refine_axis_st(T2, lat, 2 * ncx - 3, 2 * ncy - 3, ncz, 2);
             __syncthreads();
         }
-        ST_MARK(8);
     }
 #ifdef ST_PROF
-    if (t == 0 && blockIdx.x == 0)
+    if (t == st_pt && blockIdx.x == 0)
         printf("ST_PROF den %llu ctrl %llu hist %llu emap %llu fit %llu latP1 %llu eval %llu "
-               "conv %llu level %llu\n", st_prof[0], st_prof[1], st_prof[2], st_prof[3], st_prof[4],
+               "wait %llu level %llu\n", st_prof[0], st_prof[1], st_prof[2], st_prof[3], st_prof[4],
                st_prof[5], st_prof[6], st_prof[7], st_prof[8]);
 #endif
-#ifdef CH_PROF
-    if (t == 0 && blockIdx.x == 0)
-        printf("CH_PROF A wait %llu total %llu | B wait %llu total %llu | C wait %llu total %llu\n",
-               ch_w[0], ch_t[0], ch_w[1], ch_t[1], ch_w[2], ch_t[2]);
-#endif
     // final field's P1 for k_n4_final
-    const double *P1f = cur ? P1b1 : P1b0;
+    const double *P1f = M.cur ? P1b1 : P1b0;
     for (int e = t; e < p1last; e += ST_TPB) a.P1out[b * a.q2cap + e] = P1f[e];
     if (t == 0) {
         stb->conv = M.conv;
-        stb->active = 0;
+        stb->active = M.wd ? -2 : 0;
     }
 }
 
@@ -948,13 +1076,16 @@ static bool study_layout(const vh_batch *b, const vh_n4_params &prm, StudyLayout
                         sizeof(unsigned long long) * ST_HC * VH_MAX_BINS;
     const bool geom_ok = s_cap <= 64 * FIT_SO;   // one ring row's stage-1 outputs fit the lanes
     s_cap = std::max(s_cap, 64);
-    // ring rows per wave: up to FIT_NB within ~40 KB for all waves
-    const int nb_ring = std::max(1, std::min(FIT_NB, (int)(40960 / (ST_WAVES * 8 * (size_t)s_cap))));
+    // conv_mode 0: ST_CW waves run the recurrence beside the compute waves (own slot ring, the
+    // lattice kept for a discarded iteration); the fit rings are the compute waves' only
+    const bool split = prm.conv_mode == 0;
+    const int fit_waves = split ? ST_WAVES - ST_CW : ST_WAVES;
+    // ring rows per wave: up to FIT_NB within ~32 KB for the computing waves
+    const int nb_ring = std::max(1, std::min(FIT_NB, (int)(32768 / (fit_waves * 8 * (size_t)s_cap))));
     const size_t fit_num = 2 * sizeof(unsigned long long) * (size_t)nlat_max;
-    const size_t fit = ((fit_num + 15) & ~(size_t)15) + sizeof(double) * ST_WAVES * nb_ring * (size_t)s_cap;
+    const size_t fit = ((fit_num + 15) & ~(size_t)15) + sizeof(double) * fit_waves * nb_ring * (size_t)s_cap;
     const size_t exact = sizeof(float) * 2 * ST_TPB;
-    const size_t chain = sizeof(ChainSlot) * CH_SLOTS;
-    const size_t scr = std::max({refine, emap, fit, exact, chain});
+    const size_t scr = std::max({refine, emap, fit, exact});
     auto A = [](size_t v) { return (v + 15) & ~(size_t)15; };
     size_t o = 0;
     a.o_E = (int32_t)o; o += A(sizeof(float) * VH_MAX_BINS);
@@ -968,12 +1099,14 @@ static bool study_layout(const vh_batch *b, const vh_n4_params &prm, StudyLayout
     const int64_t nslots = (b->R + SLOT_R - 1) / SLOT_R;
     const int64_t nitems = b->n4_tiles * nslots;
     a.o_ipart = (int32_t)o; o += A(sizeof(double) * 2 * (size_t)nitems);
-    a.o_rpart = (int32_t)o; o += A(sizeof(float4) * (size_t)nitems);
+    a.o_rpart = (int32_t)o; o += A(sizeof(float4) * 2 * (size_t)nitems);
     a.o_order = (int32_t)o; o += A(sizeof(int32_t) * (size_t)nitems);
     a.o_misc = (int32_t)o; o += A(sizeof(StudyMisc));
     a.o_wk = (int32_t)o; o += A(2 * sizeof(double) * (size_t)kcap * Z);
     a.o_wx = (int32_t)o; o += A(2 * 4 * sizeof(double) * (size_t)R);
     a.o_scr = (int32_t)o; o += A(scr);
+    a.o_chain = (int32_t)o; o += split ? A(sizeof(ChainSlot) * ST_CH_NS) : 0;
+    a.o_latp = (int32_t)o; o += split ? A(sizeof(float) * nlat_max) : 0;
     a.o_wave = (int32_t)((fit_num + 15) & ~(size_t)15);   // ring offset inside the scratch
     a.s_cap = s_cap;
     a.nb_ring = nb_ring;
@@ -1002,6 +1135,7 @@ void vh_launch_n4_study(vh_batch *b, const vh_n4_params &prm) {
     a.L0 = b->d_L0;
     a.U = b->d_U;
     a.D = b->d_D;
+    a.half = b->nb * b->VS;   // second U / D buffers (vh_ensure_n4_workspace)
     a.rs = b->d_rowstart;
     a.rmask = b->d_rowmask;
     a.rrs = b->d_rrank;
