@@ -714,7 +714,95 @@ __device__ __forceinline__ void chain_reset(ChainSlot *slots, ChainState *cs, in
     }
 }
 
-// wave A: the mu recurrence on lane 0, block by block as the producer fills them.
+// ---- the 64 serial steps of one block, systolic (CH_SYS, the default) ---------------------------
+// Lane j holds step j's constants (one LDS read of the block by all lanes).  Every tick all lanes
+// take the float x of lane j - 1 (DPP wave_shr:1; lane 0, which has no source lane, keeps the
+// carried-in x) and apply their own step.  After tick t lanes 0..t hold the chain's values and keep
+// them (their inputs no longer change), so after 64 ticks lane j holds x after step j, and the
+// shifted copy holds x before it.  4 VALU per step (DPP move, cvt, fma, cvt) and no LDS access:
+// the lane-0 form above needs an LDS read per step, which the other waves' LDS traffic delays.
+// MU: x <- (float)fma(x, q0, q1); SIG: x <- (float)fma(q1, q0, x).  xin is wave-uniform; returns
+// lane 63's x (wave-uniform); rec = x before the lane's step.
+#ifndef CH_SYS
+#define CH_SYS 1
+#endif
+template <bool MU>
+__device__ __forceinline__ float chain_sys64(double q0, double q1, float xin, float &rec) {
+    float xf = xin, xs = xin;
+    double x;
+    if (MU)
+        asm volatile(".rept 64\n\t"
+                     "s_nop 1\n\t"   // VALU write -> DPP read: 2 wait states
+                     "v_mov_b32_dpp %1, %0 wave_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+                     "v_cvt_f64_f32 %2, %1\n\t"
+                     "v_fma_f64 %2, %2, %3, %4\n\t"
+                     "v_cvt_f32_f64 %0, %2\n\t"
+                     ".endr"
+                     : "+v"(xf), "+v"(xs), "=&v"(x)
+                     : "v"(q0), "v"(q1));
+    else
+        asm volatile(".rept 64\n\t"
+                     "s_nop 1\n\t"
+                     "v_mov_b32_dpp %1, %0 wave_shr:1 row_mask:0xf bank_mask:0xf\n\t"
+                     "v_cvt_f64_f32 %2, %1\n\t"
+                     "v_fma_f64 %2, %4, %3, %2\n\t"
+                     "v_cvt_f32_f64 %0, %2\n\t"
+                     ".endr"
+                     : "+v"(xf), "+v"(xs), "=&v"(x)
+                     : "v"(q0), "v"(q1));
+    rec = xs;
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xf), 63));
+}
+
+// Row form (CH_SYS 2): the 64 steps as 4 rows of 16 lanes taken one after the other (EXEC = the
+// row).  Inside a row the move rides on the cvt (DPP row_newbcast:k gives every lane of the row
+// lane k's x: 3 VALU per step); the first step of a row takes lane 15 of the row before
+// (row_bcast:15) or, in row 0, the carried-in x.  Lanes outside the row keep their values.
+#define CH_ROW_TICKS(FMA)                                                                          \
+    "s_nop 4\n\t"                                                                               \
+    "v_cvt_f64_f32 %2, %1\n\t" FMA "v_cvt_f32_f64 %0, %2\n\t"                                  \
+    ".irp k, 0,1,2,3,4,5,6,7,8,9,10,11,12,13,14\n\t"                                            \
+    "s_nop 1\n\t"                                                                               \
+    "v_cvt_f64_f32_dpp %2, %0 row_newbcast:\\k row_mask:0xf bank_mask:0xf\n\t" FMA             \
+    "v_cvt_f32_f64 %0, %2\n\t"                                                                   \
+    ".endr\n\t"
+#define CH_ROWS(FMA)                                                                               \
+    "s_mov_b64 %3, exec\n\t"                                                                     \
+    "s_mov_b32 exec_lo, 0xffff\n\t"                                                              \
+    "s_mov_b32 exec_hi, 0\n\t" CH_ROW_TICKS(FMA)                                                  \
+    "s_mov_b32 exec_lo, 0xffff0000\n\t"                                                          \
+    "s_nop 4\n\t"                                                                               \
+    "v_mov_b32_dpp %1, %0 row_bcast:15 row_mask:0xf bank_mask:0xf\n\t" CH_ROW_TICKS(FMA)         \
+    "s_mov_b32 exec_lo, 0\n\t"                                                                   \
+    "s_mov_b32 exec_hi, 0xffff\n\t"                                                              \
+    "s_nop 4\n\t"                                                                               \
+    "v_mov_b32_dpp %1, %0 row_bcast:15 row_mask:0xf bank_mask:0xf\n\t" CH_ROW_TICKS(FMA)         \
+    "s_mov_b32 exec_hi, 0xffff0000\n\t"                                                          \
+    "s_nop 4\n\t"                                                                               \
+    "v_mov_b32_dpp %1, %0 row_bcast:15 row_mask:0xf bank_mask:0xf\n\t" CH_ROW_TICKS(FMA)         \
+    "s_mov_b64 exec, %3\n\t"
+template <bool MU>
+__device__ __forceinline__ float chain_rows64(double q0, double q1, float xin, float &rec) {
+    float xf = xin, xs = xin;
+    double x;
+    uint64_t sv;
+    if (MU)
+        asm volatile(CH_ROWS("v_fma_f64 %2, %2, %4, %5\n\t")
+                     : "+v"(xf), "+v"(xs), "=&v"(x), "=&s"(sv)
+                     : "v"(q0), "v"(q1));
+    else
+        asm volatile(CH_ROWS("v_fma_f64 %2, %5, %4, %2\n\t")
+                     : "+v"(xf), "+v"(xs), "=&v"(x), "=&s"(sv)
+                     : "v"(q0), "v"(q1));
+    // x before each lane's step: lane j - 1's x (lane 0: the carried-in x)
+    float r = xin;
+    asm volatile("s_nop 1\n\tv_mov_b32_dpp %0, %1 wave_shr:1 row_mask:0xf bank_mask:0xf"
+                 : "+v"(r) : "v"(xf));
+    rec = r;
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xf), 63));
+}
+
+// wave A: the mu recurrence, block by block as the producers fill them.
 template <int GS = 8, int NS = CH_SLOTS>
 __device__ void chain_wave_mu(int64_t n, ChainSlot *slots, ChainState *cs) {
     const int lane = threadIdx.x & 63;
@@ -723,10 +811,19 @@ __device__ void chain_wave_mu(int64_t n, ChainSlot *slots, ChainState *cs) {
     unsigned long long wt = 0;
     __builtin_amdgcn_s_setprio(CH_PRIO);   // the serial waves win issue arbitration on their SIMD
     CH_T0();
+    float muf = 0.0f;
     for (int64_t blk = 0; blk < nblk; ++blk) {
         ChainSlot &S = slots[blk % NS];
         CH_WAIT(wt, while (lds_load_acq(&S.ready) != (int)(blk + 1)) __builtin_amdgcn_s_sleep(1));
-        if (lane == 0) mu = chain_block64<true, GS>(S.ab, S.mu, mu);
+        if (CH_SYS) {
+            const double2 q = S.ab[lane];
+            float rec;
+            muf = CH_SYS == 2 ? chain_rows64<true>(q.x, q.y, muf, rec) : chain_sys64<true>(q.x, q.y, muf, rec);
+            S.mu[lane] = rec;
+            mu = (double)muf;
+        } else if (lane == 0) {
+            mu = chain_block64<true, GS>(S.ab, S.mu, mu);
+        }
         wave_lds_order();
         if (lane == 0) {
             if (blk == nblk - 1) cs->mu = (float)mu;   // published by the release below
@@ -753,9 +850,18 @@ __device__ void chain_wave_sig(int64_t n, ChainSlot *slots, ChainState *cs) {
         const float q = S.p[lane] - S.mu[lane];
         // k = 1 adds nothing (ITK's N > 1 test), nor do the steps past the end: (0, 0) is a no-op
         const bool ok = j < n && j > 0;
-        S.cs[lane] = ok ? make_double2(S.cs[lane].x, (double)(q * q)) : make_double2(0.0, 0.0);
-        wave_lds_order();
-        if (lane == 0) sig = chain_block64<false, GS>(S.cs, nullptr, sig);
+        if (CH_SYS) {
+            const double c = S.cs[lane].x;
+            float rec;
+            const double q0 = ok ? c : 0.0, q1 = ok ? (double)(q * q) : 0.0;
+            sig = (double)(CH_SYS == 2 ? chain_rows64<false>(q0, q1, (float)sig, rec)
+                                       : chain_sys64<false>(q0, q1, (float)sig, rec));
+            (void)rec;
+        } else {
+            S.cs[lane] = ok ? make_double2(S.cs[lane].x, (double)(q * q)) : make_double2(0.0, 0.0);
+            wave_lds_order();
+            if (lane == 0) sig = chain_block64<false, GS>(S.cs, nullptr, sig);
+        }
         wave_lds_order();
         if (lane == 0) lds_store_rel(&cs->b_done, (int)(blk + 1));
     }

@@ -36,6 +36,10 @@
 #define ST_CH_PROD 2   // producer waves of the convergence chain (n4_shared.h chain_wave_prod)
 #endif
 #define ST_CW (2 + ST_CH_PROD)   // chain waves (conv_mode 0): A, B, producers
+#ifndef ST_CG
+#define ST_CG 0        // conv_mode 0 compute waves: 0 = all 12 others, 1 = the 6 on SIMDs 2 and 3
+#endif
+static_assert(ST_CW <= 4, "the chain waves are waves 0..3");
 #ifndef ST_CH_NS
 #define ST_CH_NS 4     // chain slot ring here (2 producers, 4 slots: within 1 % of 16 slots)
 #endif
@@ -575,11 +579,19 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
     const bool split = a.conv_mode == 0;
     Grp g;
     g.hw = !split;
-    g.t = split ? t - 64 * ST_CW : t;
-    g.n = split ? ST_TPB - 64 * ST_CW : ST_TPB;
-    g.w = g.t >> 6;
-    g.nw = g.n >> 6;
-    const bool in_g = g.t >= 0;
+    if (!split) {
+        g.w = wv;
+        g.nw = ST_WAVES;
+    } else if (ST_CG == 0) {   // every wave but the chain's
+        g.w = wv - ST_CW;
+        g.nw = ST_WAVES - ST_CW;
+    } else {   // only waves on SIMDs 2 and 3 (wave w on SIMD w % 4): A and B keep their SIMDs
+        g.w = (wv >= 4 && (wv & 3) >= 2) ? ((wv >> 2) - 1) * 2 + (wv & 1) : -1;
+        g.nw = 2 * (ST_WAVES / 4 - 1);
+    }
+    g.t = g.w >= 0 ? g.w * 64 + lane : -1;
+    g.n = g.nw * 64;
+    const bool in_g = g.w >= 0;
     float *Lb = a.L0 + b * a.VS;
     const int64_t fm = a.sc[b].first_masked;
     // fit / eval scratch: lattice numerator (fixed point), then per-wave Q / S rows of the group
@@ -598,7 +610,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
     float *const latp = reinterpret_cast<float *>(smem + a.o_latp);
     const int bins = a.bins;
 #ifdef ST_PROF
-    const int st_pt = split ? 64 * ST_CW : 0;   // the compute waves' first thread keeps the marks
+    const int st_pt = split ? (ST_CG == 0 ? 64 * ST_CW : 6 * 64) : 0;   // first compute thread keeps the marks
 #endif
 
     if (t == 0) {
@@ -702,7 +714,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
         __syncthreads();
         ST_MARK(0);
         for (int e = t; e < nlat; e += ST_TPB) den[e] = fix128_get(numfix + 2 * e, numfix + 2 * e + 1);
-        if (split && !in_g) {
+        if (split && wv < ST_CW) {
             // ---- chain waves: the recurrence of each kept iteration, on request ----
             for (;;) {
                 int req, bud = ST_SPIN_MAX;
@@ -722,7 +734,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                     chain_wave_prod<ST_CH_NS>(Dk, nullptr, n, cslots, &M.ch, wv - 2, ST_CH_PROD);
                 }
             }
-        } else {
+        } else if (in_g) {
             // ---- the iterations (compute waves) ----
             int itn = 0;          // iterations kept in this level
             int cur = M.cur;      // P1 buffer of the last kept field
@@ -1079,7 +1091,7 @@ static bool study_layout(const vh_batch *b, const vh_n4_params &prm, StudyLayout
     // conv_mode 0: ST_CW waves run the recurrence beside the compute waves (own slot ring, the
     // lattice kept for a discarded iteration); the fit rings are the compute waves' only
     const bool split = prm.conv_mode == 0;
-    const int fit_waves = split ? ST_WAVES - ST_CW : ST_WAVES;
+    const int fit_waves = !split ? ST_WAVES : ST_CG == 0 ? ST_WAVES - ST_CW : 2 * (ST_WAVES / 4 - 1);
     // ring rows per wave: up to FIT_NB within ~32 KB for the computing waves
     const int nb_ring = std::max(1, std::min(FIT_NB, (int)(32768 / (fit_waves * 8 * (size_t)s_cap))));
     const size_t fit_num = 2 * sizeof(unsigned long long) * (size_t)nlat_max;
