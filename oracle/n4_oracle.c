@@ -49,6 +49,7 @@
 #include <float.h>
 #include <math.h>
 #include <stdint.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -587,6 +588,13 @@ int n4_oracle(const float *I, const uint8_t *mask, int64_t R, int64_t C, int64_t
                     dr[k++] = B[v] - bn;
                     B[v] = bn;
                 }
+            {   /* dev hook: append each iteration's raster-ordered d to $N4_DUMP_D (scripts/dev) */
+                const char *dump = getenv("N4_DUMP_D");
+                if (dump) {
+                    FILE *f = fopen(dump, "ab");
+                    if (f) { fwrite(&nmask, sizeof nmask, 1, f); fwrite(dr, sizeof(float), (size_t)nmask, f); fclose(f); }
+                }
+            }
             conv = prm->conv_mode == 1 ? conv_exact(dr, nmask) : (double)conv_welford(dr, nmask);
         }
         iters_out[level] = it - 1;

@@ -1107,6 +1107,24 @@ __global__ void __launch_bounds__(WF_TPB) k_n4_welford(const float *D, const int
     if (threadIdx.x == 0) st[b].conv_w = cs.conv;
 }
 
+// S7 by guess and verify (n4_shared.h pcw_run): one 1024-thread workgroup per active volume, one
+// chain block per thread.  d is read through the raster -> compact permutation in pass 0; P (the
+// p values in block layout) lives in the second half of the D buffer.  For a large study this
+// replaces the serial chain's n dependent steps (~30 cycles each) by ~13 parallel rounds.
+__global__ void __launch_bounds__(PC_TPB) k_n4_pcw(const float *D, const int32_t *perm, float *Pbuf,
+                                                   int64_t VS, const VolScalars *sc, N4State *st,
+                                                   int64_t vol0) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int64_t b = vol0 + blockIdx.x;
+    if (!st[b].active) return;
+    PcShared<PC_TPB> &S = *reinterpret_cast<PcShared<PC_TPB> *>(smem);
+    __shared__ ChainState ch;
+    const float *const Db = D + b * VS;
+    const int32_t *const pb = perm + b * VS;
+    pcw_run([=](int64_t r) { return Db[pb[r]]; }, Pbuf + b * VS, sc[b].n_mask1, S, ch, 1);
+    if (threadIdx.x == 0) st[b].conv_w = ch.conv;
+}
+
 // Exact cubic B-spline subdivision (spans doubled on every axis), axis by axis, one block/volume.
 __device__ void refine_axis_dev(const float *in, float *out, int d0, int d1, int d2, int axis) {
     int od[3] = {d0, d1, d2};
@@ -1346,6 +1364,8 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
                 VH_CHECK_LAUNCH();
             }
             const int level_start = (int)evs.size();
+            // S7: PC (k_n4_pcw) unless VH_N4_SERIAL_CHAIN selects the serial chain (A/B runs)
+            const bool pc = getenv("VH_N4_SERIAL_CHAIN") == nullptr;
             for (int it = 0; it < prm.max_iters[L]; ++it, ++gi) {
                 k_n4_ctrl<<<(unsigned)ns, VH_TPB, 0, st>>>(
                     b->d_st, b->d_cpart, b->d_cp, b->d_sc, cm, L, it, prm.conv_threshold, bins, vol0,
@@ -1400,10 +1420,15 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
                         ch0, cm, b->d_D);
                     VH_CHECK_LAUNCH();
                 }
-                if (cm == 0) {
+                if (cm == 0 && !pc) {
                     ScopedKTimer tm(b, "n4_welford", 0.0);
                     k_n4_welford<<<(unsigned)ns, WF_TPB, 0, st>>>(b->d_D, b->d_perm, b->VS, b->d_sc,
                                                                b->d_st, vol0);
+                    VH_CHECK_LAUNCH();
+                } else if (cm == 0) {
+                    ScopedKTimer tm(b, "n4_pcw", 0.0);
+                    k_n4_pcw<<<(unsigned)ns, PC_TPB, sizeof(PcShared<PC_TPB>), st>>>(
+                        b->d_D, b->d_perm, b->d_D + b->nb * b->VS, b->VS, b->d_sc, b->d_st, vol0);
                     VH_CHECK_LAUNCH();
                 }
                 if (getenv("VH_N4_TRACE")) n4_trace(b, vol0, L, it);

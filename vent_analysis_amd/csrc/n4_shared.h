@@ -802,6 +802,618 @@ __device__ __forceinline__ float chain_rows64(double q0, double q1, float xin, f
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xf), 63));
 }
 
+// ---- S7 by guess and verify ("PC") ------------------------------------------------------------
+// The recurrence is serial, but one step is cheap to *check*: given the float state before a step,
+// the state after it is a pure function of that state and the step's inputs.  So the n steps are cut
+// into NL consecutive blocks, one per lane; every lane runs its block from a GUESS of the state at
+// the block's start, and the guesses are exact iff every block's computed end equals the next
+// block's guess (block 0 starts from the exact (0, 0)).  That check is the termination test, so the
+// result is the serial recurrence bit for bit whatever the guesses were; the guesses only decide how
+// many rounds it takes.  Between rounds the block ends propagate into new guesses through an affine
+// model of each block's map (delta_{j+1} = a_j delta_j + (end_j - guess_{j+1}); a = 1 for sig, whose
+// float steps add the same rounded increment anywhere inside a binade; for mu the secant of the
+// block's map from the previous round, clamped to [0, 1], else the linear model (k0 - 1) / k1 of the
+// running mean).  A block whose predecessor matched gets the predecessor's end exactly (delta = 0),
+// so the exact prefix grows every round; after PC_RMAX rounds the rest runs serially from the
+// first mismatch.  Measured on the bench studies' d sequences: 6 - 21 rounds (scripts/dev/pc_sim.c).
+//
+// Step arithmetic is that of the serial chain (chain_wave_prod / _mu / _sig) with the two divisions
+// replaced by exact equivalents: r = RN(1/k) by rcp and two Newton steps (pc_rcp), and
+// c = RN((k-1)/k) = RN(1 - 1/k) from r, the exact residual 1 - k r and Fast2Sum(1, -r) (pc_step).
+// Both were checked bit-exact against IEEE division for every k < 2^25 (scripts/microbench/recip_exact.hip).
+//
+// Layout of the step inputs: block j holds steps [k0_j, k0_j + len_j) (1-based), len_j = L + (j < rem),
+// L = n / NL, rem = n % NL; step s of block j lives at s NL + j, so one wave-wide load reads 64
+// consecutive floats.  pc_addr maps a raster rank (0-based step index) to that position; the map is
+// a bijection of [0, n).
+#ifndef PC_RMAX
+#define PC_RMAX 48
+#endif
+struct PcMap {
+    uint32_t L, rem, big;   // big = rem (L + 1): raster ranks below it are in the long blocks
+    double rL, rL1;         // 1 / L, 1 / (L + 1)
+};
+__device__ __forceinline__ PcMap pc_map(int64_t n, int NL) {
+    PcMap m;
+    m.L = (uint32_t)(n / NL);
+    m.rem = (uint32_t)(n % NL);
+    m.big = m.rem * (m.L + 1);
+    m.rL = m.L ? 1.0 / (double)m.L : 0.0;
+    m.rL1 = 1.0 / (double)(m.L + 1);
+    return m;
+}
+__device__ __forceinline__ uint32_t pc_udiv(uint32_t r, uint32_t d, double rd) {
+    uint32_t q = (uint32_t)((double)r * rd);
+    if ((uint64_t)q * d > r) --q;
+    else if ((uint64_t)(q + 1) * d <= r) ++q;
+    return q;
+}
+template <int NL>
+__device__ __forceinline__ uint32_t pc_addr(uint32_t r, const PcMap &m) {
+    uint32_t j, s;
+    if (r < m.big) {
+        j = pc_udiv(r, m.L + 1, m.rL1);
+        s = r - j * (m.L + 1);
+    } else {
+        const uint32_t r2 = r - m.big, j2 = pc_udiv(r2, m.L, m.rL);
+        j = m.rem + j2;
+        s = r2 - j2 * m.L;
+    }
+    return s * NL + j;
+}
+__device__ __forceinline__ uint32_t pc_len(const PcMap &m, uint32_t j) { return m.L + (j < m.rem ? 1u : 0u); }
+__device__ __forceinline__ uint32_t pc_k0(const PcMap &m, uint32_t j) { return j * m.L + min(j, m.rem) + 1u; }
+
+// RN(1 / k) for an integer k < 2^25: rcp, then two Newton steps with exact fma residuals
+__device__ __forceinline__ double pc_rcp(double kd) {
+    double y = __builtin_amdgcn_rcp(kd);
+    double e = fma(-kd, y, 1.0);
+    y = fma(y, e, y);
+    e = fma(-kd, y, 1.0);
+    return fma(y, e, y);
+}
+// the constants of step k (= kd): A = 1 - 1/k and B = p / k as chain_wave_prod forms them (div_r
+// form, r = RN(1/k)), c = RN((k - 1) / k) = RN(1 - 1/k)
+struct PcK {
+    double A, B, c;
+};
+__device__ __forceinline__ PcK pc_consts(double kd, float p) {
+    PcK q;
+    const double r = pc_rcp(kd);
+    q.A = 1.0 - r;
+    q.B = (double)(float)((double)p * r);
+    const double z = q.A - 1.0, err = -r - z;   // 1 - r = A + err exactly (Fast2Sum)
+    const double res = fma(-kd, r, 1.0);        // 1 - k r exactly: 1/k = r + res / k
+    q.c = q.A + fma(-res, r, err);
+    return q;
+}
+// one step on the float state (mu, sig); sig is untouched at k = 1 (ITK's N > 1 test)
+__device__ __forceinline__ void pc_apply(const PcK &q, float p, bool first, float &mu, float &sig) {
+    if (!first) {
+        const float d = p - mu;
+        sig = (float)fma((double)(d * d), q.c, (double)sig);
+    }
+    mu = (float)fma((double)mu, q.A, q.B);
+}
+__device__ __forceinline__ void pc_step(double kd, float p, float &mu, float &sig) {
+    pc_apply(pc_consts(kd, p), p, kd == 1.0, mu, sig);
+}
+// a lane's block: len steps from k0 over the inputs at P[s NL + j].  Groups of 8 steps without
+// guards (the constants of the 8 steps are independent of the state, so they overlap the two
+// 8-step chains), the next group's loads in flight; the tail step by step.
+template <int NL>
+__device__ __forceinline__ void pc_block(const float *P, uint32_t j, uint32_t len, uint32_t k0,
+                                         float &mu, float &sig) {
+    float cur[8], nxt[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) cur[i] = (uint32_t)i < len ? P[(size_t)i * NL + j] : 0.0f;
+    double kd = (double)k0;
+    uint32_t s0 = 0;
+    for (; s0 + 8 <= len; s0 += 8) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) nxt[i] = s0 + 8 + i < len ? P[(size_t)(s0 + 8 + i) * NL + j] : 0.0f;
+        PcK q[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) q[i] = pc_consts(kd + (double)i, cur[i]);
+        const bool first = kd == 1.0;
+        pc_apply(q[0], cur[0], first, mu, sig);
+#pragma unroll
+        for (int i = 1; i < 8; ++i) pc_apply(q[i], cur[i], false, mu, sig);
+        kd += 8.0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) cur[i] = nxt[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 7; ++i)
+        if (s0 + i < len) {
+            pc_step(kd, cur[i], mu, sig);
+            kd += 1.0;
+        }
+}
+
+// 32 bytes, 16-aligned: the compiler merges neighbouring fields into b64 / b128 LDS accesses, and a
+// b128 access at an address that is only 8-aligned stores the wrong bytes (seen with a 24-byte
+// block: the pass-0 sums came back as garbage).
+struct alignas(16) PcBlk {
+    float gmu, gsig;     // guess of the state at the block start
+    float emu, esig;     // the block's computed end
+    float gmu_o, emu_o;  // the previous round's guess and end (secant of the mu map)
+    float sp0, sp1;      // pass 0 only: (s1, s2) below
+};
+template <int NL>
+struct PcShared {
+    PcBlk b[NL];
+    int done, fallback, first_bad, rounds;   // done / fallback: the request number they refer to
+    float mu, sig;
+    int bar_cnt, bar_gen;
+    // all-wave update (pcw_*): per-wave aggregates of the block transitions
+    double agA[NL / 64], agB[NL / 64], agS[NL / 64];
+    int agFirst[NL / 64];
+    // pass-0 block sums of p - 1 and (p - 1)^2 (double, 16-aligned pair over gmu_o .. sp1: those
+    // fields are written by round 0 before they are next read)
+    __device__ double &s1(int j) { return *reinterpret_cast<double *>(&b[j].gmu_o); }
+    __device__ double &s2(int j) { return *reinterpret_cast<double *>(&b[j].sp0); }
+};
+
+// Initial guesses from the running mean / variance sum in double (one wave, PB = NL / 64 blocks per
+// lane, fixed-order scan).
+template <int NL>
+__device__ void pc_guess(PcShared<NL> &S, const PcMap &m) {
+    constexpr int PB = NL / 64;
+    const int lane = threadIdx.x & 63;
+    double l1[PB], l2[PB], t1 = 0.0, t2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < PB; ++i) {
+        l1[i] = t1;
+        l2[i] = t2;
+        t1 += S.s1(lane * PB + i);
+        t2 += S.s2(lane * PB + i);
+    }
+    double x1 = t1, x2 = t2;   // inclusive scan of the lane totals
+    for (int off = 1; off < 64; off <<= 1) {
+        const double y1 = __shfl_up(x1, off, 64), y2 = __shfl_up(x2, off, 64);
+        if (lane >= off) {
+            x1 = y1 + x1;
+            x2 = y2 + x2;
+        }
+    }
+    double e1 = __shfl_up(x1, 1, 64), e2 = __shfl_up(x2, 1, 64);
+    if (lane == 0) e1 = e2 = 0.0;
+#pragma unroll
+    for (int i = 0; i < PB; ++i) {
+        const uint32_t jb = lane * PB + i;
+        const double K = (double)(pc_k0(m, jb) - 1u);
+        const double S1 = e1 + l1[i], S2 = e2 + l2[i];
+        float g = 0.0f, gs = 0.0f;
+        if (K > 0.0) {
+            g = (float)(1.0 + S1 / K);
+            const double v = S2 - S1 * (S1 / K);
+            gs = (float)(v > 0.0 ? v : 0.0);
+        }
+        S.b[jb].gmu = g;
+        S.b[jb].gsig = gs;
+    }
+}
+
+// Check and update after a round (one wave).  Sets S.done (every block end matched: S.mu / S.sig
+// hold the result) or S.fallback (round cap: S.first_bad = the first transition that failed), else
+// writes the next guesses.
+template <int NL>
+__device__ void pc_update(PcShared<NL> &S, const PcMap &m, int round, int req) {
+    constexpr int PB = NL / 64;
+    const int lane = threadIdx.x & 63;
+    const int nbe = m.L ? NL : (int)m.rem;   // non-empty blocks
+    double am[PB], bm[PB], bs[PB];
+    float em[PB], es[PB];
+    bool mism = false;
+    int firstm = PB;
+#pragma unroll
+    for (int i = 0; i < PB; ++i) {
+        const int jb = lane * PB + i;
+        am[i] = 1.0;
+        bm[i] = bs[i] = 0.0;
+        em[i] = es[i] = 0.0f;
+        if (jb < nbe - 1) {
+            const PcBlk B = S.b[jb];
+            const float gn = S.b[jb + 1].gmu, gsn = S.b[jb + 1].gsig;
+            em[i] = B.emu;
+            es[i] = B.esig;
+            const bool mm = __float_as_uint(B.emu) != __float_as_uint(gn) ||
+                            __float_as_uint(B.esig) != __float_as_uint(gsn);
+            if (mm && firstm == PB) firstm = i;
+            mism |= mm;
+            bm[i] = (double)B.emu - (double)gn;
+            bs[i] = (double)B.esig - (double)gsn;
+            const uint32_t k0 = pc_k0(m, jb), k1 = k0 + pc_len(m, jb) - 1u;
+            double a = (double)(k0 - 1u) / (double)k1;
+            if (round > 0 && B.gmu != B.gmu_o) {
+                const double sl = ((double)B.emu - (double)B.emu_o) / ((double)B.gmu - (double)B.gmu_o);
+                if (sl >= 0.0 && sl <= 1.0) a = sl;
+            }
+            am[i] = a;
+            S.b[jb].gmu_o = B.gmu;   // this round's guess and end, for the next round's secant
+            S.b[jb].emu_o = B.emu;
+        }
+    }
+    const uint64_t bal = __ballot(mism);
+    if (bal == 0ull) {
+        if (lane == 0) {
+            S.mu = S.b[nbe - 1].emu;
+            S.sig = S.b[nbe - 1].esig;
+            S.rounds = round + 1;
+            S.done = req;
+        }
+        return;
+    }
+    if (round + 1 >= PC_RMAX) {
+        const int fl = __ffsll((unsigned long long)bal) - 1;
+        if (lane == fl) {
+            S.first_bad = lane * PB + firstm;
+            S.rounds = round + 1;
+            S.fallback = req;
+        }
+        return;
+    }
+    double Am = 1.0, Bm = 0.0, Bs = 0.0;   // the lane's transitions composed
+#pragma unroll
+    for (int i = 0; i < PB; ++i) {
+        Bm = am[i] * Bm + bm[i];
+        Am = am[i] * Am;
+        Bs = Bs + bs[i];
+    }
+    for (int off = 1; off < 64; off <<= 1) {
+        const double ya = __shfl_up(Am, off, 64), yb = __shfl_up(Bm, off, 64), ys = __shfl_up(Bs, off, 64);
+        if (lane >= off) {
+            Bm = Am * yb + Bm;
+            Am = Am * ya;
+            Bs = ys + Bs;
+        }
+    }
+    double dm = __shfl_up(Bm, 1, 64), ds = __shfl_up(Bs, 1, 64);
+    if (lane == 0) dm = ds = 0.0;
+#pragma unroll
+    for (int i = 0; i < PB; ++i) {
+        const int jb = lane * PB + i;
+        if (jb < nbe - 1) {
+            S.b[jb + 1].gmu = dm == 0.0 ? em[i] : (float)((double)em[i] + am[i] * dm);
+            S.b[jb + 1].gsig = ds == 0.0 ? es[i] : (float)((double)es[i] + ds);
+            dm = am[i] * dm + bm[i];
+            ds = ds + bs[i];
+        }
+    }
+}
+
+// Serial remainder after the round cap (one lane): blocks first_bad + 1 .. nbe - 1 from the exact
+// end of block first_bad.
+template <int NL>
+__device__ void pc_serial(PcShared<NL> &S, const PcMap &m, const float *P) {
+    const int nbe = m.L ? NL : (int)m.rem;
+    const int f = S.first_bad;
+    float mu = S.b[f].emu, sig = S.b[f].esig;
+    for (int jb = f + 1; jb < nbe; ++jb) {
+        const uint32_t len = pc_len(m, jb);
+        double kd = (double)pc_k0(m, jb);
+        for (uint32_t s = 0; s < len; ++s, kd += 1.0) pc_step(kd, P[(size_t)s * NL + jb], mu, sig);
+    }
+    S.mu = mu;
+    S.sig = sig;
+}
+
+// ---- PC phase A: certified float steps --------------------------------------------------------
+// The same recurrence with float-float step constants: r ~ r0 + rl (r0 = rcp(k), rl from the exact
+// residual 1 - k r0), p/k ~ B = fma(p, r0, p rl), c ~ ch + cl.  mu: t = B - mu (r0 + rl) (two fmas)
+// is within E of the exact increment (E = 2^-22 (|t1| + |t|) + 2^-46 |mu| bounds the roundings, the
+// float-float error and the double rounding of the exact step), and the step's result is CERTIFIED
+// when mu + (t - E) and mu + (t + E) round to the same float: the exact step then gives that float.
+// Otherwise (a few steps per study and iteration) the lane takes the exact double step.  sig:
+// y = RN(sig + q^2 ch), its rounding error rho, w = rho + q^2 cl, sig' = RN(y + w) (uncertified:
+// equal to the exact step unless sig + q^2 c lies within ~2^-24 ulp of a tie).  Phase A iterates
+// these rounds to their own fixed point; phase B (exact rounds) then verifies it, usually in one
+// round (scripts/dev/pc_sim.c: 12 A + 1.2 B rounds on the bench studies, against 13 exact rounds).
+// consts of one step for phase A
+struct PcKf {
+    float r0, rl, B, ch, cl, e0;
+};
+__device__ __forceinline__ PcKf pc_kf(float k, float p) {
+    PcKf q;
+    q.r0 = __builtin_amdgcn_rcpf(k);
+    q.rl = q.r0 * fmaf(-k, q.r0, 1.0f);
+    q.B = fmaf(p, q.r0, p * q.rl);
+    q.ch = 1.0f - q.r0;
+    q.cl = ((-q.r0) - (q.ch - 1.0f)) - q.rl;
+    q.e0 = fmaf(q.r0, 0x1p-40f, 0x1p-44f);   // >= 2^-22 |mu rl| + 2^-46 |mu| for mu < 4 (see below)
+    return q;
+}
+// one phase-A step; returns false when the mu step is not certified (the state is then approximate)
+__device__ __forceinline__ bool pc_apx_step(const PcKf &q, float p, bool first, float &mu, float &sig) {
+    if (!first) {
+        const float d = p - mu, q2 = d * d;
+        const float y = fmaf(q2, q.ch, sig);
+        const float rho = fmaf(q2, q.ch, sig - y);
+        sig = y + fmaf(q2, q.cl, rho);
+    }
+    // E = 2^-21 |t| + e0 bounds 2^-22 (|t1| + |t|) + 2^-46 |mu| (|t1| <= |t| + |mu rl|, |rl| <=
+    // 2^-23 r0); e0 assumes |mu| < 4 (p = exp(d) of a smooth field difference, mu a running mean of
+    // them): a larger mu only makes a step uncertified-but-wrong, which phase B then corrects
+    const float t1 = fmaf(-mu, q.r0, q.B);
+    const float t = fmaf(-mu, q.rl, t1);
+    const float E = fmaf(fabsf(t), 0x1p-21f, q.e0);
+    const float ya = mu + (t - E);
+    const bool ok = ya == mu + (t + E);
+    mu = ya;   // = RN(mu + t) whenever ok
+    return ok;
+}
+// a lane's block in phase A: groups of 8 steps without guards; a group with an uncertified step is
+// redone with the exact steps (rare: the wave branches only when one of its lanes needs it)
+template <int NL>
+__device__ __forceinline__ void pc_block_apx(const float *P, uint32_t j, uint32_t len, uint32_t k0,
+                                             float &mu, float &sig) {
+    float cur[8], nxt[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) cur[i] = (uint32_t)i < len ? P[(size_t)i * NL + j] : 0.0f;
+    float kf = (float)k0;
+    uint32_t s0 = 0;
+    for (; s0 + 8 <= len; s0 += 8) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) nxt[i] = s0 + 8 + i < len ? P[(size_t)(s0 + 8 + i) * NL + j] : 0.0f;
+        PcKf q[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) q[i] = pc_kf(kf + (float)i, cur[i]);
+        const float mu0 = mu, sig0 = sig;
+        bool ok = pc_apx_step(q[0], cur[0], kf == 1.0f, mu, sig);
+#pragma unroll
+        for (int i = 1; i < 8; ++i) ok &= pc_apx_step(q[i], cur[i], false, mu, sig);
+        if (!ok) {   // redo the group exactly
+            mu = mu0;
+            sig = sig0;
+            double kd = (double)kf;
+#pragma unroll 1
+            for (int i = 0; i < 8; ++i, kd += 1.0) pc_step(kd, cur[i], mu, sig);
+        }
+        kf += 8.0f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) cur[i] = nxt[i];
+    }
+    double kd = (double)kf;
+#pragma unroll
+    for (int i = 0; i < 7; ++i)   // the tail: exact steps
+        if (s0 + i < len) {
+            pc_step(kd, cur[i], mu, sig);
+            kd += 1.0;
+        }
+}
+
+// ---- all-wave PC helpers (NL = threads of the workgroup, one block per thread) -----------------
+// Affine transition maps T_j: delta -> a delta + b composed in block order: a wave-level inclusive
+// scan (shuffles), per-wave aggregates in LDS, then each wave composes the aggregates before it.
+// Fixed order, so deterministic; exact zeros stay exact zeros (the property the convergence proof
+// uses: a block whose predecessors all matched gets the exact predecessor end).
+template <int NL>
+__device__ __forceinline__ void pcw_scan(PcShared<NL> &S, double a, double b, double bs, double &dm,
+                                         double &ds) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    double A = a, B = b, Bs = bs;
+    for (int off = 1; off < 64; off <<= 1) {
+        const double ya = __shfl_up(A, off, 64), yb = __shfl_up(B, off, 64), ys = __shfl_up(Bs, off, 64);
+        if (lane >= off) {
+            B = A * yb + B;
+            A = A * ya;
+            Bs = ys + Bs;
+        }
+    }
+    if (lane == 63) {
+        S.agA[w] = A;
+        S.agB[w] = B;
+        S.agS[w] = Bs;
+    }
+    double ea = __shfl_up(A, 1, 64), eb = __shfl_up(B, 1, 64), es = __shfl_up(Bs, 1, 64);
+    if (lane == 0) {
+        ea = 1.0;
+        eb = 0.0;
+        es = 0.0;
+    }
+    __syncthreads();
+    double pb = 0.0, ps = 0.0;   // aggregates of the waves before this one, applied to delta = 0
+    for (int v = 0; v < w; ++v) {
+        pb = S.agA[v] * pb + S.agB[v];
+        ps = ps + S.agS[v];
+    }
+    dm = ea * pb + eb;
+    ds = ps + es;
+}
+
+// initial guesses (all threads): running mean / variance sum in double from the pass-0 block sums
+template <int NL>
+__device__ void pcw_guess(PcShared<NL> &S, const PcMap &m) {
+    const uint32_t j = threadIdx.x;
+    double dm, ds;
+    pcw_scan<NL>(S, 1.0, S.s1(j), S.s2(j), dm, ds);   // exclusive sums of s1 (dm) and s2 (ds)
+    const double K = (double)(pc_k0(m, j) - 1u);
+    float g = 0.0f, gs = 0.0f;
+    if (K > 0.0) {
+        g = (float)(1.0 + dm / K);
+        const double v = ds - dm * (dm / K);
+        gs = (float)(v > 0.0 ? v : 0.0);
+    }
+    S.b[j].gmu = g;
+    S.b[j].gsig = gs;
+}
+
+// Check and update after a round (all threads).  S.done = req when every block end matched (S.mu /
+// S.sig hold the result); at the round cap (cap_fallback) S.fallback = req and S.first_bad = the
+// first failing transition; else the next guesses.  Ends with the caller's barrier.
+template <int NL>
+__device__ void pcw_update(PcShared<NL> &S, const PcMap &m, int round, int req, bool at_cap,
+                           bool cap_fallback) {
+    const int j = threadIdx.x, lane = j & 63, w = j >> 6;
+    const int nbe = m.L ? NL : (int)m.rem;
+    double a = 1.0, bm = 0.0, bs = 0.0;
+    float em = 0.0f, es = 0.0f;
+    bool mm = false;
+    if (j < nbe - 1) {
+        const PcBlk B = S.b[j];
+        const float gn = S.b[j + 1].gmu, gsn = S.b[j + 1].gsig;
+        em = B.emu;
+        es = B.esig;
+        mm = __float_as_uint(B.emu) != __float_as_uint(gn) || __float_as_uint(B.esig) != __float_as_uint(gsn);
+        bm = (double)B.emu - (double)gn;
+        bs = (double)B.esig - (double)gsn;
+        const uint32_t k0 = pc_k0(m, j), k1 = k0 + pc_len(m, j) - 1u;
+        // model slopes (deterministic float arithmetic; they only steer the guesses)
+        float af = (float)(k0 - 1u) * __builtin_amdgcn_rcpf((float)k1);
+        if (round > 0 && B.gmu != B.gmu_o) {
+            const float sl = (B.emu - B.emu_o) * __builtin_amdgcn_rcpf(B.gmu - B.gmu_o);
+            if (sl >= 0.0f && sl <= 1.0f) af = sl;
+        }
+        a = (double)af;
+        S.b[j].gmu_o = B.gmu;
+        S.b[j].emu_o = B.emu;
+    }
+    const uint64_t bal = __ballot(mm);
+    if (lane == 0) S.agFirst[w] = bal ? w * 64 + __ffsll((unsigned long long)bal) - 1 : NL;
+    double dm, ds;
+    pcw_scan<NL>(S, a, bm, bs, dm, ds);   // its barrier also publishes agFirst
+    int first = NL;
+    for (int v = 0; v < NL / 64; ++v) first = min(first, S.agFirst[v]);
+    if (first == NL) {
+        if (j == 0) {
+            S.mu = S.b[nbe - 1].emu;
+            S.sig = S.b[nbe - 1].esig;
+            S.rounds = round + 1;
+            S.done = req;
+        }
+        return;
+    }
+    if (at_cap) {
+        if (j == 0 && cap_fallback) {
+            S.first_bad = first;
+            S.rounds = round + 1;
+            S.fallback = req;
+        }
+        return;
+    }
+    if (j < nbe - 1) {
+        S.b[j + 1].gmu = dm == 0.0 ? em : (float)((double)em + a * dm);
+        S.b[j + 1].gsig = ds == 0.0 ? es : (float)((double)es + ds);
+    }
+}
+
+#define PC_TPB 1024
+// The recurrence of one iteration on a whole 1024-thread workgroup (one block per thread), shared by
+// the study kernel (ST_PC 2) and the sweep driver (k_n4_pcw).  ld(r) returns d at raster rank r
+// (the study's raster-ordered stores, or the sweep's compact d through the raster permutation);
+// pass 0 reads each block's run of it, writes
+// p = exp(d) into P in block layout (one wave-wide load per step afterwards) and the block sums;
+// then phase A (certified float rounds) and phase B (exact rounds, the verification); after
+// PC_RMAX exact rounds the rest runs serially from the first failing block.  ch.conv = result.
+#ifndef PC_AMAX
+#define PC_AMAX 40
+#endif
+template <class LoadD>
+__device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n, PcShared<PC_TPB> &S,
+                                                  ChainState &ch, int req) {
+    const int tid = threadIdx.x;
+    const PcMap m = pc_map(n, PC_TPB);
+    const uint32_t j = (uint32_t)tid, len = pc_len(m, j), k0 = pc_k0(m, j);
+#ifdef PC_PROF
+    const unsigned long long c0 = clock64();
+    unsigned long long c1 = 0, c2 = 0;
+    int ra = 0;
+#endif
+    if (tid == 0) {
+        S.done = 0;
+        S.fallback = 0;
+    }
+    double s1 = 0.0, s2 = 0.0;
+    for (uint32_t s0 = 0; s0 < len; s0 += 8) {
+        float v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = s0 + i < len ? ld((int64_t)(k0 - 1u + s0 + i)) : 0.0f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            if (s0 + i < len) {
+                const float p = expf_cr(v[i]);
+                P[(size_t)(s0 + i) * PC_TPB + j] = p;
+                const double e = (double)p - 1.0;
+                s1 += e;
+                s2 = fma(e, e, s2);
+            }
+    }
+    S.s1(j) = s1;
+    S.s2(j) = s2;
+    __syncthreads();
+    pcw_guess<PC_TPB>(S, m);
+    __syncthreads();
+#ifdef PC_PROF
+    c1 = clock64();
+#endif
+    int round = 0;
+    // phase A: certified float rounds to their fixed point.  A thread whose start did not change
+    // keeps its end; a wave whose threads all kept theirs skips the round.
+    float lg = __int_as_float(0x7fc00000), ls = lg, le = 0.0f, les = 0.0f;
+#ifdef PC_PROF
+    unsigned long long cblk = 0;
+#endif
+    for (int ra0 = 0; ra0 < PC_AMAX; ++ra0, ++round) {
+#ifdef PC_PROF
+        const unsigned long long cq = clock64();
+#endif
+        const float g = S.b[j].gmu, gs = S.b[j].gsig;
+        const bool same = __float_as_uint(g) == __float_as_uint(lg) && __float_as_uint(gs) == __float_as_uint(ls);
+        if (__ballot(!same) != 0ull && !same) {
+            float mu = g, sig = gs;
+            pc_block_apx<PC_TPB>(P, j, len, k0, mu, sig);
+            lg = g;
+            ls = gs;
+            le = mu;
+            les = sig;
+        }
+        S.b[j].emu = le;
+        S.b[j].esig = les;
+        __syncthreads();
+#ifdef PC_PROF
+        cblk += clock64() - cq;
+#endif
+        pcw_update<PC_TPB>(S, m, round, req, ra0 == PC_AMAX - 1, false);
+        __syncthreads();
+        if (S.done == req) break;
+    }
+#ifdef PC_PROF
+    ra = round + 1;
+    c2 = clock64();
+#endif
+    // phase B: exact rounds (the verification; usually one)
+    if (tid == 0) S.done = 0;
+    __syncthreads();
+    for (int rb = 0; rb < PC_RMAX; ++rb) {
+        ++round;
+        float mu = S.b[j].gmu, sig = S.b[j].gsig;
+        pc_block<PC_TPB>(P, j, len, k0, mu, sig);
+        S.b[j].emu = mu;
+        S.b[j].esig = sig;
+        __syncthreads();
+        pcw_update<PC_TPB>(S, m, round, req, rb == PC_RMAX - 1, true);
+        __syncthreads();
+        if (S.done == req) break;
+        if (S.fallback == req) {
+            if (tid == 0) pc_serial<PC_TPB>(S, m, P);
+            __syncthreads();
+            break;
+        }
+    }
+    if (tid == 0) {
+        const float sd = (float)sqrt((double)S.sig / ((double)n - 1.0));
+        ch.mu = S.mu;
+        ch.conv = sd / S.mu;
+#ifdef PC_PROF
+        if (blockIdx.x == 0)
+            printf("PCW_PROF n %lld roundsA %d roundsB %d fallback %d pass0 %llu A %llu (blocks %llu) B %llu\n",
+                   (long long)n, ra, S.rounds - ra + 0, S.fallback == req, c1 - c0, c2 - c1, cblk, clock64() - c2);
+#endif
+    }
+}
+
+
 // wave A: the mu recurrence, block by block as the producers fill them.
 template <int GS = 8, int NS = CH_SLOTS>
 __device__ void chain_wave_mu(int64_t n, ChainSlot *slots, ChainState *cs) {

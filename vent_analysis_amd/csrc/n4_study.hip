@@ -43,6 +43,19 @@ static_assert(ST_CW <= 4, "the chain waves are waves 0..3");
 #ifndef ST_CH_NS
 #define ST_CH_NS 4     // chain slot ring here (2 producers, 4 slots: within 1 % of 16 slots)
 #endif
+// conv_mode 0, the S7 recurrence: 0 = the serial chain on ST_CW waves beside the compute waves of
+// the next iteration (speculative); 1 = S7 by guess and verify (n4_shared.h PC) on those waves;
+// 2 = PC on all 16 waves after each iteration's eval (no speculation).  Measured per 256-study bench
+// step: 0 45.8 ms, 1 54 ms, 2 49-50 ms.  PC's ~12 rounds re-run every step, so per study it is VALU
+// throughput work of ~12x25 instructions per masked voxel and iteration, more than the serial chain
+// costs when it hides behind the next iteration's compute; PC wins where one study has the GPU to
+// itself (the sweep driver, k_n4_pcw).
+#ifndef ST_PC
+#define ST_PC 0
+#endif
+constexpr bool ST_SPLIT = ST_PC != 2;
+static_assert(ST_PC != 2 || ST_TPB == PC_TPB, "pcw_run takes the whole 1024-thread workgroup");   // conv_mode 0 runs chain waves beside compute waves
+constexpr int ST_PCL = ST_SPLIT ? 64 * ST_CW : ST_TPB;   // PC blocks: one per participating lane
 #ifndef ST_CH_GS
 #define ST_CH_GS 8   // convergence-chain group size here (n4_shared.h ch_group): 8 measured 135M vs 167M cycles for 4
 #endif
@@ -276,7 +289,7 @@ template <bool SAME, int CM>
 __device__ void eval_item(const Item &it, int item, int Z, const TabV &Tn, const TabV &To, int ncyn,
                           int ncyo, const double *P1n, const double *P1o, bool bo_mode,
                           const float *Lb, float *Ub, float *Db, int64_t n, double *ipart,
-                          float4 *rpart) {
+                          float4 *rpart, const PcMap &pm) {
     const __amdgpu_buffer_rsrc_t rL = st_rsrc(Lb, n), rU = st_rsrc(Ub, n), rD = st_rsrc(Db, n);
     const float4 wyn = it.colok ? Tn.wy[it.y] : make_float4(0.f, 0.f, 0.f, 0.f);
     const float4 wyo = it.colok ? To.wy[it.y] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -307,7 +320,7 @@ __device__ void eval_item(const Item &it, int item, int Z, const TabV &Tn, const
         const float u = la - bn;
         st_store(rU, off, u);
         if (CM == 0) {
-            st_store(rD, (uint32_t)rr * 4u, bo - bn);
+            st_store(rD, (ST_PC == 1 ? pc_addr<ST_PCL>((uint32_t)rr, pm) : (uint32_t)rr) * 4u, bo - bn);
         } else {
             const double d = (double)expm1c(bo - bn);
             sd += d;
@@ -542,6 +555,106 @@ __device__ __forceinline__ int next_item(StudyMisc &M, const int32_t *ordr, int 
 }
 
 // ---------------------------------------------------------------------------------------------
+// S7 by guess and verify (n4_shared.h PC) on the ST_CW chain waves: a barrier of their own (an LDS
+// counter and generation, as gsync), pass 0 (p = exp(d) in place, block sums), rounds.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ void pc_bar(PcShared<ST_PCL> &S, int32_t *wd) {
+    if (!ST_SPLIT) {   // every wave of the workgroup takes part
+        __syncthreads();
+        return;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if ((threadIdx.x & 63) == 0) {
+        const int gen = __hip_atomic_load(&S.bar_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (atomicAdd(&S.bar_cnt, 1) == ST_CW - 1) {
+            __hip_atomic_store(&S.bar_cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_store(&S.bar_gen, gen + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else {
+            int bud = ST_SPIN_MAX;
+            while (__hip_atomic_load(&S.bar_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == gen &&
+                   st_spin(bud, wd)) {
+            }
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// The recurrence of one iteration over Dk (d in PC block layout, overwritten by p); ch.conv = result.
+__device__ __attribute__((noinline)) void pc_run(float *Dk, int64_t n, PcShared<ST_PCL> &S, ChainState &ch,
+                                                 int32_t *wd, int req) {
+    // ST_SPLIT: threads [0, ST_PCL) are the chain waves; else the whole workgroup
+    const int tid = threadIdx.x, w = tid >> 6;
+    const PcMap m = pc_map(n, ST_PCL);
+    const uint32_t j = (uint32_t)tid, len = pc_len(m, j), k0 = pc_k0(m, j);
+    if (!ST_SPLIT && tid == 0) {   // the state lives in scratch here: nothing survives a pass
+        S.done = 0;
+        S.fallback = 0;
+    }
+#ifdef PC_PROF
+    const unsigned long long c0 = clock64();
+    unsigned long long c1 = 0, cr = 0, cu = 0;
+#endif
+    double s1 = 0.0, s2 = 0.0;
+    for (uint32_t s0 = 0; s0 < len; s0 += 8) {   // pass 0: p = exp(d) in place, block sums
+        float v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = s0 + i < len ? Dk[(size_t)(s0 + i) * ST_PCL + j] : 0.0f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            if (s0 + i < len) {
+                const float p = expf_cr(v[i]);
+                Dk[(size_t)(s0 + i) * ST_PCL + j] = p;
+                const double e = (double)p - 1.0;
+                s1 += e;
+                s2 = fma(e, e, s2);
+            }
+    }
+    S.s1(j) = s1;
+    S.s2(j) = s2;
+    pc_bar(S, wd);
+    if (w == 0) pc_guess<ST_PCL>(S, m);
+    pc_bar(S, wd);
+#ifdef PC_PROF
+    c1 = clock64();
+#endif
+    for (int round = 0; round < PC_RMAX + 2; ++round) {
+#ifdef PC_PROF
+        const unsigned long long ca = clock64();
+#endif
+        float mu = S.b[j].gmu, sig = S.b[j].gsig;
+        pc_block<ST_PCL>(Dk, j, len, k0, mu, sig);
+        S.b[j].emu = mu;
+        S.b[j].esig = sig;
+        pc_bar(S, wd);
+#ifdef PC_PROF
+        const unsigned long long cb = clock64();
+        cr += cb - ca;
+#endif
+        if (w == 0) pc_update<ST_PCL>(S, m, round, req);
+        pc_bar(S, wd);
+#ifdef PC_PROF
+        cu += clock64() - cb;
+#endif
+        if (S.done == req) break;
+        if (S.fallback == req) {
+            if (tid == 0) pc_serial<ST_PCL>(S, m, Dk);
+            pc_bar(S, wd);
+            break;
+        }
+    }
+    if (tid == 0) {
+        const float sd = (float)sqrt((double)S.sig / ((double)n - 1.0));
+        ch.mu = S.mu;
+        ch.conv = sd / S.mu;
+#ifdef PC_PROF
+        if (blockIdx.x == 0)
+            printf("PC_PROF req %d n %lld rounds %d fallback %d pass0 %llu rounds %llu update %llu total %llu\n", req,
+                   (long long)n, S.rounds, S.fallback == req, c1 - c0, cr, cu, clock64() - c0);
+#endif
+    }
+}
+
+// ---------------------------------------------------------------------------------------------
 // the kernel: one workgroup per study
 // ---------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
@@ -576,7 +689,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
     // that recurrence's result then keeps the new iteration or discards it (the lattice, the U
     // buffer and the field buffer of the last kept iteration are still there).  The arithmetic of
     // every kept iteration is unchanged.  conv_mode 1: all waves compute, no speculation.
-    const bool split = a.conv_mode == 0;
+    const bool split = a.conv_mode == 0 && ST_SPLIT;
     Grp g;
     g.hw = !split;
     if (!split) {
@@ -607,6 +720,10 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
     double2 *TW = DEN + ST_FFT_N;
     unsigned long long *Hc = reinterpret_cast<unsigned long long *>(TW + VH_FFT_P / 2);
     ChainSlot *const cslots = reinterpret_cast<ChainSlot *>(smem + a.o_chain);
+    // PC state: the chain region beside the compute waves (split), else the scratch region, which
+    // nothing else holds between an iteration's eval and the next iteration's histogram
+    PcShared<ST_PCL> &PS = *reinterpret_cast<PcShared<ST_PCL> *>(smem + (ST_SPLIT ? a.o_chain : a.o_scr));
+    const PcMap pm = pc_map(n, ST_PCL);
     float *const latp = reinterpret_cast<float *>(smem + a.o_latp);
     const int bins = a.bins;
 #ifdef ST_PROF
@@ -624,6 +741,12 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
         M.cur = 0;
         M.uin = 0;
         M.wd = 0;
+        if (a.conv_mode == 0 && ST_PC) {
+            PS.bar_cnt = 0;
+            PS.bar_gen = 0;
+            PS.done = 0;
+            PS.fallback = 0;
+        }
     }
     if (wv == 0) find_first3(a, b, fm, M);
     {   // item schedule: items by row count, largest first (ties by index), so the dynamic item
@@ -723,8 +846,14 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                 if (req == ch_seen) break;   // watchdog
                 ch_seen = req;
                 if (M.go_op) break;   // level end
-                const float *Dk = a.D + M.go_d * a.half + b * a.VS;
-                if (wv == 0) {
+                float *const Dk = a.D + M.go_d * a.half + b * a.VS;
+                if (ST_PC) {
+                    pc_run(Dk, n, PS, M.ch, &M.wd, req);
+                    if (wv == 0) {
+                        wave_lds_order();
+                        if (lane == 0) lds_store_rel(&M.ch_seq, req);   // after ch.conv
+                    }
+                } else if (wv == 0) {
                     chain_wave_mu<ST_CH_GS, ST_CH_NS>(n, cslots, &M.ch);
                 } else if (wv == 1) {
                     chain_wave_sig<ST_CH_GS, ST_CH_NS>(n, cslots, &M.ch);
@@ -766,7 +895,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                                     M.stop = 1;
                                 }
                             } else {
-                                M.conv = conv_of(M.sd, M.sd2, (double)n);
+                                if (a.conv_mode == 1) M.conv = conv_of(M.sd, M.sd2, (double)n);
                                 if (!(M.conv > (double)a.thresh) || itn >= a.lvs->max_iters[L]) M.stop = 1;
                             }
                         }
@@ -954,14 +1083,14 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                         }
                         if (a.conv_mode == 0) {
                             if (same)
-                                eval_item<true, 0>(it, item, a.Z, T, To, ncy, ncyo, P1n, P1o, bo_mode, Lb, Uo, Dw, n, ipart, rp_out);
+                                eval_item<true, 0>(it, item, a.Z, T, To, ncy, ncyo, P1n, P1o, bo_mode, Lb, Uo, Dw, n, ipart, rp_out, pm);
                             else
-                                eval_item<false, 0>(it, item, a.Z, T, To, ncy, ncyo, P1n, P1o, bo_mode, Lb, Uo, Dw, n, ipart, rp_out);
+                                eval_item<false, 0>(it, item, a.Z, T, To, ncy, ncyo, P1n, P1o, bo_mode, Lb, Uo, Dw, n, ipart, rp_out, pm);
                         } else {
                             if (same)
-                                eval_item<true, 1>(it, item, a.Z, T, To, ncy, ncyo, P1n, P1o, bo_mode, Lb, Uo, Dw, n, ipart, rp_out);
+                                eval_item<true, 1>(it, item, a.Z, T, To, ncy, ncyo, P1n, P1o, bo_mode, Lb, Uo, Dw, n, ipart, rp_out, pm);
                             else
-                                eval_item<false, 1>(it, item, a.Z, T, To, ncy, ncyo, P1n, P1o, bo_mode, Lb, Uo, Dw, n, ipart, rp_out);
+                                eval_item<false, 1>(it, item, a.Z, T, To, ncy, ncyo, P1n, P1o, bo_mode, Lb, Uo, Dw, n, ipart, rp_out, pm);
                         }
                     }
                 }
@@ -979,7 +1108,8 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                             if (!(M.ch.conv > a.thresh)) M.stop = 1;
                         }
                         if (!M.stop) {   // keep: request the recurrence of iteration itk
-                            for (int i = 0; i < ST_CH_NS; ++i) chain_reset<ST_CH_NS>(cslots, &M.ch, i);
+                            if (!ST_PC)
+                                for (int i = 0; i < ST_CH_NS; ++i) chain_reset<ST_CH_NS>(cslots, &M.ch, i);
                             M.go_op = 0;
                             M.go_d = itk & 1;
                             lds_store_rel(&M.go, M.go + 1);
@@ -990,6 +1120,11 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                         for (int e = g.t; e < nlat; e += g.n) lat[e] = latp[e];
                         break;
                     }
+                } else if (a.conv_mode == 0) {   // S7 on the whole workgroup (ST_PC 2)
+                    PcShared<ST_TPB> &PW = *reinterpret_cast<PcShared<ST_TPB> *>(smem + a.o_scr);
+                    const float *const Dr = a.D + b * a.VS;
+                    pcw_run([=](int64_t r) { return Dr[r]; }, a.D + a.half + b * a.VS, n, PW, M.ch, itk);
+                    if (t == 0) M.conv = (double)M.ch.conv;
                 } else if (g.w == 0) {   // S7x: item partials in item order
                     double sd = 0.0, sd2 = 0.0;
                     for (int i = lane; i < a.nitems; i += 64) {
@@ -1090,14 +1225,15 @@ static bool study_layout(const vh_batch *b, const vh_n4_params &prm, StudyLayout
     s_cap = std::max(s_cap, 64);
     // conv_mode 0: ST_CW waves run the recurrence beside the compute waves (own slot ring, the
     // lattice kept for a discarded iteration); the fit rings are the compute waves' only
-    const bool split = prm.conv_mode == 0;
+    const bool split = prm.conv_mode == 0 && ST_SPLIT;
     const int fit_waves = !split ? ST_WAVES : ST_CG == 0 ? ST_WAVES - ST_CW : 2 * (ST_WAVES / 4 - 1);
     // ring rows per wave: up to FIT_NB within ~32 KB for the computing waves
     const int nb_ring = std::max(1, std::min(FIT_NB, (int)(32768 / (fit_waves * 8 * (size_t)s_cap))));
     const size_t fit_num = 2 * sizeof(unsigned long long) * (size_t)nlat_max;
     const size_t fit = ((fit_num + 15) & ~(size_t)15) + sizeof(double) * fit_waves * nb_ring * (size_t)s_cap;
     const size_t exact = sizeof(float) * 2 * ST_TPB;
-    const size_t scr = std::max({refine, emap, fit, exact});
+    const size_t pcs = (prm.conv_mode == 0 && !ST_SPLIT) ? sizeof(PcShared<ST_TPB>) : 0;
+    const size_t scr = std::max({refine, emap, fit, exact, pcs});
     auto A = [](size_t v) { return (v + 15) & ~(size_t)15; };
     size_t o = 0;
     a.o_E = (int32_t)o; o += A(sizeof(float) * VH_MAX_BINS);
@@ -1117,7 +1253,8 @@ static bool study_layout(const vh_batch *b, const vh_n4_params &prm, StudyLayout
     a.o_wk = (int32_t)o; o += A(2 * sizeof(double) * (size_t)kcap * Z);
     a.o_wx = (int32_t)o; o += A(2 * 4 * sizeof(double) * (size_t)R);
     a.o_scr = (int32_t)o; o += A(scr);
-    a.o_chain = (int32_t)o; o += split ? A(sizeof(ChainSlot) * ST_CH_NS) : 0;
+    a.o_chain = (int32_t)o;
+    o += split ? A(ST_PC ? sizeof(PcShared<ST_PCL>) : sizeof(ChainSlot) * ST_CH_NS) : 0;
     a.o_latp = (int32_t)o; o += split ? A(sizeof(float) * nlat_max) : 0;
     a.o_wave = (int32_t)((fit_num + 15) & ~(size_t)15);   // ring offset inside the scratch
     a.s_cap = s_cap;
