@@ -98,7 +98,7 @@ def algorithmic_bytes(name, hp, mk, res, R, C, Z, study=True, conv_mode=0):
         return float(np.sum(iters * (16.0 + cw) * vm + 12.0 * vm))   # reads U, eval L0 in, U out
     if name == "n4_welford":     # read perm + d (raster walk of the compact d)
         return float(np.sum(iters * 8.0 * vm))
-    if name == "n4_pcw":         # pass 0: read perm + d, write p; rounds re-read p (counted once)
+    if name in ("n4_pcw", "n4_pcg"):   # pass 0: read perm + d, write p; rounds re-read p (once)
         return float(np.sum(iters * 16.0 * vm))
     if name == "n4_den":         # read ridx, once per level
         return float(np.sum(levels * 4.0 * vm))

@@ -515,6 +515,29 @@ def test_n4_sweep_rerun_bit_identical(shape):
         assert np.array_equal(n4, outs[0][0])
 
 
+@pytest.mark.parametrize("shape,grid", [((96, 112, 20), "0"), ((256, 256, 24), "1"), ((128, 128, 96), "1")])
+def test_n4_pc_equals_serial_chain(shape, grid, monkeypatch):
+    """S7 by guess and verify (k_n4_pcw one workgroup, k_n4_pcg the cooperative grid for one large
+    volume) against the serial float Welford chain (VH_N4_SERIAL_CHAIN) on the sweep driver: the same
+    iteration counts, the same convergence values and the same field, bit for bit."""
+    X, M = synth_volume(*shape, 31)
+    outs = []
+    for serial in (False, True):
+        if serial:
+            monkeypatch.setenv("VH_N4_SERIAL_CHAIN", "1")
+        else:
+            monkeypatch.delenv("VH_N4_SERIAL_CHAIN", raising=False)
+        monkeypatch.setenv("VH_N4_PCG", grid)
+        B = _lib.Batch(*shape, 1)
+        B.upload(X[None], M.astype(np.uint8)[None])
+        B.run(B.options(do_n4=True, vox=(1.5, 1.5, 10.0), n4_mode="sweep", do_snr=False, do_kmeans=False))
+        n4, _, _, _, res = B.download(n4=True, maps=False)
+        B.close()
+        outs.append((n4[0].copy(), list(res[0].n4_iters[:4]), [float(c) for c in res[0].n4_conv[:4]]))
+    assert outs[0][1] == outs[1][1] and outs[0][2] == outs[1][2]
+    assert np.array_equal(outs[0][0], outs[1][0])
+
+
 # ---- volume-resident N4 driver (one workgroup per study) ------------------------------------------
 def _run_batch(hp, mk, mode, **kw):
     R, C, Z = hp.shape[1:]

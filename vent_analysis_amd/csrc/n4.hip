@@ -21,6 +21,8 @@
 #include <climits>
 #include <cstring>
 
+#include <hip/hip_cooperative_groups.h>
+
 #include "n4_shared.h"
 
 #define SEG_R 16    // rows per wave segment
@@ -1125,6 +1127,233 @@ __global__ void __launch_bounds__(PC_TPB) k_n4_pcw(const float *D, const int32_t
     if (threadIdx.x == 0) st[b].conv_w = ch.conv;
 }
 
+// S7 by guess and verify over the whole GPU, for one large study (the sweep driver with a single
+// volume, e.g. BASELINE config 5): a cooperative grid of G 1024-thread workgroups, one chain block per
+// thread (NB = 1024 G blocks of n / NB steps).  The per-block state lives in global memory (struct of
+// arrays); the affine transition maps are scanned in three levels (wave shuffles, the workgroup's
+// waves in LDS, the workgroups' aggregates after a grid barrier).  Two grid barriers per round.
+struct PcgArgs {
+    const float *D;
+    const int32_t *perm;
+    float *P;                        // p in block layout: step s of block j at s NB + j
+    const VolScalars *sc;
+    N4State *st;
+    int64_t b;
+    float *gmu, *gsig, *emu, *esig, *gmu_o, *emu_o;   // [NB]
+    double *s1, *s2;                                   // [NB] pass-0 sums
+    double *agA, *agB, *agS;                           // [G] workgroup aggregates
+    int *agF;                                          // [G] first failing transition of a workgroup
+};
+struct PcgLds {
+    double wA[PC_TPB / 64], wB[PC_TPB / 64], wS[PC_TPB / 64];
+    int wF[PC_TPB / 64];
+    double pB, pS;   // the workgroups before this one, applied to delta = 0
+    int first;
+};
+// Exclusive grid-wide composition of the maps (a, b) (and sums bs) in block order, applied to 0:
+// dm, ds.  *first (in: this thread's failing flag) -> the smallest failing block index of the grid
+// (NB when none).  Contains one grid barrier.
+__device__ void pcg_scan(const PcgArgs &A, PcgLds &L, cooperative_groups::grid_group &grid, double a,
+                         double b, double bs, bool fail, double &dm, double &ds, int &first) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, G = gridDim.x;
+    const int NB = G * PC_TPB;
+    double Aw = a, Bw = b, Sw = bs;
+    for (int off = 1; off < 64; off <<= 1) {
+        const double ya = __shfl_up(Aw, off, 64), yb = __shfl_up(Bw, off, 64), ys = __shfl_up(Sw, off, 64);
+        if (lane >= off) {
+            Bw = Aw * yb + Bw;
+            Aw = Aw * ya;
+            Sw = ys + Sw;
+        }
+    }
+    const uint64_t bal = __ballot(fail);
+    if (lane == 63) {
+        L.wA[w] = Aw;
+        L.wB[w] = Bw;
+        L.wS[w] = Sw;
+    }
+    if (lane == 0) L.wF[w] = bal ? (int)(blockIdx.x * PC_TPB + w * 64 + __ffsll((unsigned long long)bal) - 1) : NB;
+    double ea = __shfl_up(Aw, 1, 64), eb = __shfl_up(Bw, 1, 64), es = __shfl_up(Sw, 1, 64);
+    if (lane == 0) {
+        ea = 1.0;
+        eb = 0.0;
+        es = 0.0;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {   // this workgroup's aggregate
+        double At = 1.0, Bt = 0.0, St = 0.0;
+        int f = NB;
+        for (int v = 0; v < PC_TPB / 64; ++v) {
+            Bt = L.wA[v] * Bt + L.wB[v];
+            At = At * L.wA[v];
+            St = St + L.wS[v];
+            f = min(f, L.wF[v]);
+        }
+        A.agA[blockIdx.x] = At;
+        A.agB[blockIdx.x] = Bt;
+        A.agS[blockIdx.x] = St;
+        A.agF[blockIdx.x] = f;
+    }
+    grid.sync();
+    if (w == 0) {   // the workgroups before this one (ordered: lane l folds [4l, 4l + 4)), and the grid's first failure
+        double Al = 1.0, Bl = 0.0, Sl = 0.0;
+        int f = NB;
+        for (int i = 0; i < 4; ++i) {
+            const int u = 4 * lane + i;
+            if (u < G) {
+                f = min(f, A.agF[u]);
+                if (u < (int)blockIdx.x) {
+                    const double au = A.agA[u];
+                    Bl = au * Bl + A.agB[u];
+                    Al = Al * au;
+                    Sl = Sl + A.agS[u];
+                }
+            }
+        }
+        for (int off = 1; off < 64; off <<= 1) {
+            const double ya = __shfl_up(Al, off, 64), yb = __shfl_up(Bl, off, 64), ys = __shfl_up(Sl, off, 64);
+            if (lane >= off) {
+                Bl = Al * yb + Bl;
+                Al = Al * ya;
+                Sl = ys + Sl;
+            }
+            f = min(f, __shfl_xor(f, off, 64));
+        }
+        if (lane == 63) {
+            L.pB = Bl;
+            L.pS = Sl;
+            L.first = f;
+        }
+    }
+    __syncthreads();
+    double x = L.pB, xs = L.pS;
+    for (int v = 0; v < w; ++v) {
+        x = L.wA[v] * x + L.wB[v];
+        xs = xs + L.wS[v];
+    }
+    dm = ea * x + eb;
+    ds = xs + es;
+    first = L.first;
+}
+
+__global__ void __launch_bounds__(PC_TPB) k_n4_pcg(PcgArgs A) {
+    namespace cg = cooperative_groups;
+    cg::grid_group grid = cg::this_grid();
+    if (!A.st[A.b].active) return;   // uniform over the grid
+    __shared__ PcgLds L;
+    const int64_t n = A.sc[A.b].n_mask1;
+    const int NB = gridDim.x * PC_TPB;
+    const PcMap m = pc_map(n, NB);
+    const uint32_t j = blockIdx.x * PC_TPB + threadIdx.x, len = pc_len(m, j), k0 = pc_k0(m, j);
+    const int nbe = m.L ? NB : (int)m.rem;
+    const float *const Db = A.D + A.b * 0;   // D, perm, P are this volume's (host offsets)
+    // pass 0: p = exp(d) in block layout, block sums
+    double s1 = 0.0, s2 = 0.0;
+    for (uint32_t s0 = 0; s0 < len; s0 += 8) {
+        int32_t pi[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) pi[i] = s0 + i < len ? A.perm[k0 - 1u + s0 + i] : 0;
+        float v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = s0 + i < len ? Db[pi[i]] : 0.0f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            if (s0 + i < len) {
+                const float p = expf_cr(v[i]);
+                A.P[(size_t)(s0 + i) * NB + j] = p;
+                const double e = (double)p - 1.0;
+                s1 += e;
+                s2 = fma(e, e, s2);
+            }
+    }
+    double dm, ds;
+    int first;
+    pcg_scan(A, L, grid, 1.0, s1, s2, false, dm, ds, first);   // exclusive sums: dm = S1, ds = S2
+    {
+        const double K = (double)(k0 - 1u);
+        float g = 0.0f, gs = 0.0f;
+        if (K > 0.0) {
+            g = (float)(1.0 + dm / K);
+            const double v = ds - dm * (dm / K);
+            gs = (float)(v > 0.0 ? v : 0.0);
+        }
+        A.gmu[j] = g;
+        A.gsig[j] = gs;
+    }
+    grid.sync();
+    float lg = __int_as_float(0x7fc00000), ls = lg, le = 0.0f, les = 0.0f;
+    bool done = false;
+    int round = 0;
+    for (int phase = 0; phase < 2 && !done; ++phase) {
+        const int cap = phase == 0 ? PC_AMAX : PC_RMAX;
+        for (int r = 0; r < cap; ++r, ++round) {
+            const float g = A.gmu[j], gs = A.gsig[j];
+            float mu = g, sig = gs;
+            if (phase == 1) {
+                pc_block<0>(A.P, j, len, k0, mu, sig, NB);
+            } else {
+                const bool same = __float_as_uint(g) == __float_as_uint(lg) && __float_as_uint(gs) == __float_as_uint(ls);
+                if (__ballot(!same) != 0ull && !same) {
+                    pc_block_apx<0>(A.P, j, len, k0, mu, sig, NB);
+                    lg = g;
+                    ls = gs;
+                    le = mu;
+                    les = sig;
+                }
+                mu = le;
+                sig = les;
+            }
+            // the transition j -> j + 1 (as pcw_update)
+            double a = 1.0, bm = 0.0, bsv = 0.0;
+            bool mm = false;
+            if ((int)j < nbe - 1) {
+                const float gn = A.gmu[j + 1], gsn = A.gsig[j + 1];
+                mm = __float_as_uint(mu) != __float_as_uint(gn) || __float_as_uint(sig) != __float_as_uint(gsn);
+                bm = (double)mu - (double)gn;
+                bsv = (double)sig - (double)gsn;
+                const uint32_t k1 = k0 + len - 1u;
+                float af = (float)(k0 - 1u) * __builtin_amdgcn_rcpf((float)k1);
+                const float go = A.gmu_o[j], eo = A.emu_o[j];
+                if (round > 0 && g != go) {
+                    const float sl = (mu - eo) * __builtin_amdgcn_rcpf(g - go);
+                    if (sl >= 0.0f && sl <= 1.0f) af = sl;
+                }
+                a = (double)af;
+                A.gmu_o[j] = g;
+                A.emu_o[j] = mu;
+            }
+            A.emu[j] = mu;
+            A.esig[j] = sig;
+            pcg_scan(A, L, grid, a, bm, bsv, mm, dm, ds, first);
+            if (first == NB) {   // every block end matched its successor's guess: exact
+                if (j == (uint32_t)(nbe - 1)) {
+                    const float sd = (float)sqrt((double)sig / ((double)n - 1.0));
+                    A.st[A.b].conv_w = sd / mu;
+                }
+                done = true;
+                break;
+            }
+            if (r == cap - 1) break;   // phase A cap: on to the exact rounds; phase B cap: serial below
+            if ((int)j < nbe - 1) {
+                A.gmu[j + 1] = dm == 0.0 ? mu : (float)((double)mu + a * dm);
+                A.gsig[j + 1] = ds == 0.0 ? sig : (float)((double)sig + ds);
+            }
+            grid.sync();
+        }
+        if (phase == 0 && !done) grid.sync();   // the last phase-A ends, then exact rounds
+    }
+    if (!done && j == 0) {   // round cap: serial from the first failing transition (ends are exact up to it)
+        float mu = A.emu[first], sig = A.esig[first];
+        for (int jb = first + 1; jb < nbe; ++jb) {
+            const uint32_t l = pc_len(m, jb);
+            double kd = (double)pc_k0(m, jb);
+            for (uint32_t s = 0; s < l; ++s, kd += 1.0) pc_step(kd, A.P[(size_t)s * NB + jb], mu, sig);
+        }
+        const float sd = (float)sqrt((double)sig / ((double)n - 1.0));
+        A.st[A.b].conv_w = sd / mu;
+    }
+}
+
 // Exact cubic B-spline subdivision (spans doubled on every axis), axis by axis, one block/volume.
 __device__ void refine_axis_dev(const float *in, float *out, int d0, int d1, int d2, int axis) {
     int od[3] = {d0, d1, d2};
@@ -1366,6 +1595,41 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
             const int level_start = (int)evs.size();
             // S7: PC (k_n4_pcw) unless VH_N4_SERIAL_CHAIN selects the serial chain (A/B runs)
             const bool pc = getenv("VH_N4_SERIAL_CHAIN") == nullptr;
+            // a launch of one large volume: the grid form (k_n4_pcg) over up to one workgroup per CU,
+            // ~64+ steps per chain block (VH_N4_PCG=0 keeps the one-workgroup form)
+            int pcg_grid = 0;
+            PcgArgs pcg_args{};
+            if (cm == 0 && pc && ns == 1 && b->V >= ((int64_t)1 << 20) &&
+                !(getenv("VH_N4_PCG") && atoi(getenv("VH_N4_PCG")) == 0)) {
+                int dev = 0, ncu = 0, per = 0;
+                HIP_TRY(hipGetDevice(&dev));
+                HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+                HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)k_n4_pcg, PC_TPB, 0));
+                const int64_t want = (b->V / 4 + PC_TPB * 64 - 1) / (PC_TPB * 64);   // ~1/4 of V masked
+                pcg_grid = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)per * ncu));
+                const int64_t NB = (int64_t)pcg_grid * PC_TPB;
+                const size_t need = NB * (6 * sizeof(float) + 2 * sizeof(double)) +
+                                    (size_t)pcg_grid * (3 * sizeof(double) + sizeof(int)) + 256;
+                if ((int64_t)need > b->pcg_cap) {
+                    if (b->d_pcg) HIP_TRY(hipFree(b->d_pcg));
+                    b->d_pcg = nullptr;
+                    b->pcg_cap = 0;
+                    HIP_TRY(hipMalloc(&b->d_pcg, need));
+                    b->pcg_cap = (int64_t)need;
+                }
+                char *w = (char *)b->d_pcg;
+                pcg_args.s1 = (double *)w; w += NB * sizeof(double);
+                pcg_args.s2 = (double *)w; w += NB * sizeof(double);
+                pcg_args.agA = (double *)w; w += pcg_grid * sizeof(double);
+                pcg_args.agB = (double *)w; w += pcg_grid * sizeof(double);
+                pcg_args.agS = (double *)w; w += pcg_grid * sizeof(double);
+                float **fa[6] = {&pcg_args.gmu, &pcg_args.gsig, &pcg_args.emu, &pcg_args.esig,
+                                 &pcg_args.gmu_o, &pcg_args.emu_o};
+                for (int q = 0; q < 6; ++q) { *fa[q] = (float *)w; w += NB * sizeof(float); }
+                pcg_args.agF = (int *)w;
+                pcg_args.sc = b->d_sc;
+                pcg_args.st = b->d_st;
+            }
             for (int it = 0; it < prm.max_iters[L]; ++it, ++gi) {
                 k_n4_ctrl<<<(unsigned)ns, VH_TPB, 0, st>>>(
                     b->d_st, b->d_cpart, b->d_cp, b->d_sc, cm, L, it, prm.conv_threshold, bins, vol0,
@@ -1425,6 +1689,16 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
                     k_n4_welford<<<(unsigned)ns, WF_TPB, 0, st>>>(b->d_D, b->d_perm, b->VS, b->d_sc,
                                                                b->d_st, vol0);
                     VH_CHECK_LAUNCH();
+                } else if (cm == 0 && pcg_grid > 0) {   // one large study: PC over the whole GPU
+                    ScopedKTimer tm(b, "n4_pcg", 0.0);
+                    PcgArgs A = pcg_args;
+                    A.b = vol0;
+                    A.D = b->d_D + vol0 * b->VS;
+                    A.perm = b->d_perm + vol0 * b->VS;
+                    A.P = b->d_D + (b->nb + vol0) * b->VS;
+                    void *args[] = {&A};
+                    HIP_TRY(hipLaunchCooperativeKernel((const void *)k_n4_pcg, dim3((unsigned)pcg_grid),
+                                                       dim3(PC_TPB), args, 0, st));
                 } else if (cm == 0) {
                     ScopedKTimer tm(b, "n4_pcw", 0.0);
                     k_n4_pcw<<<(unsigned)ns, PC_TPB, sizeof(PcShared<PC_TPB>), st>>>(

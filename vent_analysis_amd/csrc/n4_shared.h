@@ -903,15 +903,15 @@ __device__ __forceinline__ void pc_step(double kd, float p, float &mu, float &si
 // 8-step chains), the next group's loads in flight; the tail step by step.
 template <int NL>
 __device__ __forceinline__ void pc_block(const float *P, uint32_t j, uint32_t len, uint32_t k0,
-                                         float &mu, float &sig) {
+                                         float &mu, float &sig, uint32_t nl = NL) {
     float cur[8], nxt[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) cur[i] = (uint32_t)i < len ? P[(size_t)i * NL + j] : 0.0f;
+    for (int i = 0; i < 8; ++i) cur[i] = (uint32_t)i < len ? P[(size_t)i * nl + j] : 0.0f;
     double kd = (double)k0;
     uint32_t s0 = 0;
     for (; s0 + 8 <= len; s0 += 8) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) nxt[i] = s0 + 8 + i < len ? P[(size_t)(s0 + 8 + i) * NL + j] : 0.0f;
+        for (int i = 0; i < 8; ++i) nxt[i] = s0 + 8 + i < len ? P[(size_t)(s0 + 8 + i) * nl + j] : 0.0f;
         PcK q[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) q[i] = pc_consts(kd + (double)i, cur[i]);
@@ -1147,15 +1147,15 @@ __device__ __forceinline__ bool pc_apx_step(const PcKf &q, float p, bool first, 
 // redone with the exact steps (rare: the wave branches only when one of its lanes needs it)
 template <int NL>
 __device__ __forceinline__ void pc_block_apx(const float *P, uint32_t j, uint32_t len, uint32_t k0,
-                                             float &mu, float &sig) {
+                                             float &mu, float &sig, uint32_t nl = NL) {
     float cur[8], nxt[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) cur[i] = (uint32_t)i < len ? P[(size_t)i * NL + j] : 0.0f;
+    for (int i = 0; i < 8; ++i) cur[i] = (uint32_t)i < len ? P[(size_t)i * nl + j] : 0.0f;
     float kf = (float)k0;
     uint32_t s0 = 0;
     for (; s0 + 8 <= len; s0 += 8) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) nxt[i] = s0 + 8 + i < len ? P[(size_t)(s0 + 8 + i) * NL + j] : 0.0f;
+        for (int i = 0; i < 8; ++i) nxt[i] = s0 + 8 + i < len ? P[(size_t)(s0 + 8 + i) * nl + j] : 0.0f;
         PcKf q[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) q[i] = pc_kf(kf + (float)i, cur[i]);
