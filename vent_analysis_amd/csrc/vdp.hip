@@ -385,6 +385,146 @@ __global__ void __launch_bounds__(VS_TPB) k_sort_vol(uint32_t *__restrict__ k0,
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// The same stable LSD sort over the whole GPU for ONE large volume (config 5: ~28 M keys, where the
+// one-workgroup sort took 118 ms).  Per 8-bit pass: k_sortg_count (one workgroup per 8192-key chunk:
+// the chunk's digit counts), k_sortg_offsets (one workgroup: per digit, the exclusive prefix over
+// chunks in chunk order plus the digit's base), k_sortg_scatter (one workgroup per chunk: the
+// chunk ranked exactly as k_sort_vol ranks it, written at its chunk's digit offsets).  Chunk c of
+// every pass holds keys [8192 c, 8192 (c + 1)), so the order of equal digits is the input order:
+// stable, and the result is the same array k_sort_vol produces.
+// ---------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(VS_TPB) k_sortg_count(const uint32_t *__restrict__ kin,
+                                                       const VolScalars *sc, int64_t b, int shift,
+                                                       uint32_t *cnt) {
+    __shared__ uint32_t s_c[256];
+    const int64_t n = sc[b].n_mask;
+    const int64_t c0 = (int64_t)blockIdx.x * VS_CHUNK;
+    if (n <= 1 || c0 >= n) return;
+    const int t = threadIdx.x;
+    if (t < 256) s_c[t] = 0u;
+    __syncthreads();
+    uint32_t kr[VS_KPT];
+#pragma unroll
+    for (int r = 0; r < VS_KPT; ++r) {
+        const int64_t i = c0 + (int64_t)r * VS_TPB + t;
+        kr[r] = i < n ? kin[i] : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < VS_KPT; ++r)
+        if (c0 + (int64_t)r * VS_TPB + t < n) atomicAdd(&s_c[(kr[r] >> shift) & 255u], 1u);
+    __syncthreads();
+    if (t < 256) cnt[(int64_t)blockIdx.x * 256 + t] = s_c[t];
+}
+
+__global__ void __launch_bounds__(VS_TPB) k_sortg_offsets(uint32_t *cnt, const VolScalars *sc,
+                                                         int64_t b) {
+    // thread (q, d): digit d = t & 255 over the q-th quarter of the chunks; cnt -> offsets in place
+    __shared__ uint32_t s_q[4][256];
+    __shared__ uint32_t s_base[256];
+    const int64_t n = sc[b].n_mask;
+    if (n <= 1) return;
+    const int64_t nch = (n + VS_CHUNK - 1) / VS_CHUNK;
+    const int t = threadIdx.x, d = t & 255, q = t >> 8;
+    const int64_t per = (nch + 3) / 4, lo = min(nch, q * per), hi = min(nch, lo + per);
+    uint32_t sum = 0;
+    for (int64_t c = lo; c < hi; ++c) sum += cnt[c * 256 + d];
+    s_q[q][d] = sum;
+    __syncthreads();
+    if (t < 256) {   // digit totals, bases by a serial scan over digits (256 adds)
+        uint32_t tot = s_q[0][t] + s_q[1][t] + s_q[2][t] + s_q[3][t];
+        s_base[t] = tot;
+    }
+    __syncthreads();
+    if (t == 0) {
+        uint32_t run = 0;
+        for (int dd = 0; dd < 256; ++dd) { const uint32_t v = s_base[dd]; s_base[dd] = run; run += v; }
+    }
+    __syncthreads();
+    uint32_t run = s_base[d];
+    for (int qq = 0; qq < q; ++qq) run += s_q[qq][d];
+    for (int64_t c = lo; c < hi; ++c) {
+        const uint32_t v = cnt[c * 256 + d];
+        cnt[c * 256 + d] = run;
+        run += v;
+    }
+}
+
+__global__ void __launch_bounds__(VS_TPB) k_sortg_scatter(const uint32_t *__restrict__ kin,
+                                                         uint32_t *__restrict__ kout,
+                                                         const uint32_t *off, const VolScalars *sc,
+                                                         int64_t b, int shift) {
+    __shared__ uint32_t s_wc[VS_WAVES][256];
+    __shared__ uint32_t s_tot[256], s_cst[256], s_wsum[4], s_off[256];
+    __shared__ uint32_t s_stage[VS_CHUNK];
+    const int64_t n = sc[b].n_mask;
+    const int64_t c0 = (int64_t)blockIdx.x * VS_CHUNK;
+    if (n <= 1 || c0 >= n) return;
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    const uint64_t lt = (1ull << lane) - 1ull;
+    for (int d = lane; d < 256; d += 64) s_wc[w][d] = 0u;
+    if (t < 256) s_off[t] = off[(int64_t)blockIdx.x * 256 + t];
+    __syncthreads();
+    uint32_t key[VS_KPT], rank[VS_KPT];
+#pragma unroll
+    for (int r = 0; r < VS_KPT; ++r) {
+        const int64_t idx = c0 + (int64_t)w * (VS_KPT * 64) + r * 64 + lane;
+        key[r] = idx < n ? kin[idx] : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < VS_KPT; ++r) {   // as k_sort_vol: wave w owns keys [c0 + 512 w, c0 + 512 (w + 1))
+        const int64_t idx = c0 + (int64_t)w * (VS_KPT * 64) + r * 64 + lane;
+        const bool valid = idx < n;
+        const uint32_t kk = key[r];
+        const uint32_t d = (kk >> shift) & 255u;
+        const uint32_t d0 = (uint32_t)__shfl((int)d, 0, 64);
+        const uint64_t peers = __all(!valid || d == d0) ? __ballot(valid) : vs_peers(d, valid);
+        const uint32_t below = (uint32_t)__popcll(peers & lt);
+        uint32_t base = 0u;
+        if (valid && below == 0) base = atomicAdd(&s_wc[w][d], (uint32_t)__popcll(peers));
+        const int leader = peers ? __builtin_ctzll(peers) : lane;
+        base = (uint32_t)__shfl((int)base, leader, 64);
+        rank[r] = valid ? base + below : 0xffffffffu;
+    }
+    __syncthreads();
+    if (t < 256) {
+        uint32_t tot = 0;
+        uint32_t wcv[VS_WAVES];
+#pragma unroll
+        for (int ww = 0; ww < VS_WAVES; ++ww) wcv[ww] = s_wc[ww][t];
+#pragma unroll
+        for (int ww = 0; ww < VS_WAVES; ++ww) { s_wc[ww][t] = tot; tot += wcv[ww]; }
+        uint32_t inc = tot;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t v = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += v;
+        }
+        if (lane == 63) s_wsum[w] = inc;
+        s_tot[t] = tot;
+        s_cst[t] = inc - tot;
+    }
+    __syncthreads();
+    if (t < 256) {
+        uint32_t pre = 0;
+        for (int ww = 0; ww < w; ++ww) pre += s_wsum[ww];
+        s_cst[t] += pre;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < VS_KPT; ++r) {
+        if (rank[r] == 0xffffffffu) continue;
+        const uint32_t d = (key[r] >> shift) & 255u;
+        s_stage[s_cst[d] + s_wc[w][d] + rank[r]] = key[r];
+    }
+    __syncthreads();
+    const int cn = (int)(n - c0 < VS_CHUNK ? n - c0 : VS_CHUNK);
+    for (int q = t; q < cn; q += VS_TPB) {
+        const uint32_t kk = s_stage[q];
+        const uint32_t d = (kk >> shift) & 255u;
+        kout[s_off[d] + ((uint32_t)q - s_cst[d])] = kk;
+    }
+}
+
 // =============================================================================================
 // mean anchor (Vent_Analysis.py:246): np.mean of the sorted float32 list is
 //   float32( float64( serial float32 sum over 8192-chunks of numpy pairwise_sum(chunk) ) / n ).
@@ -1516,8 +1656,30 @@ void vh_launch_vdp_chain(vh_batch *b, const float *d_n4, const vh_run_opts &o) {
     }
     {
         ScopedKTimer tm(b, "sort", 0.0);
-        k_sort_vol<<<(unsigned)b->nb, VS_TPB, 0, st>>>(b->d_keys0, b->d_keys1, b->d_sc, b->V);
-        VH_CHECK_LAUNCH();
+        if (b->nb == 1 && b->V >= ((int64_t)1 << 22)) {   // one large volume: the grid sort
+            const int64_t nchunk = (b->V + VS_CHUNK - 1) / VS_CHUNK;
+            if (b->sortg_cap < nchunk * 256) {
+                if (b->d_sortg) HIP_TRY(hipFree(b->d_sortg));
+                b->d_sortg = nullptr;
+                b->sortg_cap = 0;
+                HIP_TRY(hipMalloc(&b->d_sortg, sizeof(uint32_t) * nchunk * 256));
+                b->sortg_cap = nchunk * 256;
+            }
+            uint32_t *cnt = (uint32_t *)b->d_sortg;
+            uint32_t *kin = b->d_keys0, *kout = b->d_keys1;
+            for (int p = 0; p < 4; ++p) {
+                k_sortg_count<<<(unsigned)nchunk, VS_TPB, 0, st>>>(kin, b->d_sc, 0, 8 * p, cnt);
+                VH_CHECK_LAUNCH();
+                k_sortg_offsets<<<1, VS_TPB, 0, st>>>(cnt, b->d_sc, 0);
+                VH_CHECK_LAUNCH();
+                k_sortg_scatter<<<(unsigned)nchunk, VS_TPB, 0, st>>>(kin, kout, cnt, b->d_sc, 0, 8 * p);
+                VH_CHECK_LAUNCH();
+                std::swap(kin, kout);
+            }
+        } else {
+            k_sort_vol<<<(unsigned)b->nb, VS_TPB, 0, st>>>(b->d_keys0, b->d_keys1, b->d_sc, b->V);
+            VH_CHECK_LAUNCH();
+        }
     }
     {
         const int64_t max_chunks = (b->V + 8191) / 8192;

@@ -189,6 +189,8 @@ struct vh_batch {
     void *d_study_lv = nullptr;      // n4_study.hip: per-level table pointers + iteration caps
     void *d_pcg = nullptr;           // n4.hip k_n4_pcg: per-block guesses / ends / sums, aggregates
     int64_t pcg_cap = 0;             // bytes of d_pcg
+    void *d_sortg = nullptr;         // vdp.hip grid sort: per-chunk digit counts / offsets
+    int64_t sortg_cap = 0;           // entries of d_sortg
     // CI workspace
     uint32_t *d_bitmap = nullptr;    // [nb][ceil(V/32)] Fortran-order defect bits
     int32_t *d_ci_list = nullptr;    // [nb][V] defect voxel raster indices (compacted)
