@@ -1463,12 +1463,17 @@ __global__ void __launch_bounds__(KM_TPB) k_kmeans(const uint32_t *__restrict__ 
                 const int64_t ta = a / KM_TILE, te = (e - 1) / KM_TILE;
                 double head, tail;
                 km_tile_sum2(k, ta, te, a, e, head, tail);
+                double mid = 0.0;   // tiles held in global memory (large volumes): the wave sums them
+                if (!in_lds) {      // in a fixed order (lane-strided partials, shuffle tree)
+                    for (int64_t tt = ta + 1 + lane; tt < te; tt += 64) mid += gt[tt];
+                    for (int off = 32; off > 0; off >>= 1) mid += __shfl_down(mid, off, 64);
+                }
                 if (lane == 0) {
                     double sum = head;
                     if (in_lds) {
                         if (te > ta + 1) sum += s_tiles[te] - s_tiles[ta + 1];
                     } else {
-                        for (int64_t tt = ta + 1; tt < te; ++tt) sum += gt[tt];
+                        sum += mid;
                     }
                     if (te != ta) sum += tail;
                     s_c[w] = sum / (double)(e - a);
