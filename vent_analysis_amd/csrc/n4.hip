@@ -1636,7 +1636,10 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
                 HIP_TRY(hipGetDevice(&dev));
                 HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
                 HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)k_n4_pcg, PC_TPB, 0));
-                const int64_t want = (b->V / 4 + PC_TPB * 64 - 1) / (PC_TPB * 64);   // ~1/4 of V masked
+                // ~1/4 of V masked, VH_PCG_STEPS (default 16) steps per chain block (config 2: 64 -> 16
+                // steps: n4_pcg 14.4 -> 10.3 ms per study; config 5 is at one workgroup per CU anyway)
+                const int64_t spb = getenv("VH_PCG_STEPS") ? std::max(1, atoi(getenv("VH_PCG_STEPS"))) : 16;
+                const int64_t want = (b->V / 4 + PC_TPB * spb - 1) / (PC_TPB * spb);
                 pcg_grid = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)per * ncu));
                 const int64_t NB = (int64_t)pcg_grid * PC_TPB;
                 const size_t need = NB * (6 * sizeof(float) + 2 * sizeof(double)) +
