@@ -214,9 +214,10 @@ void vh_ensure_n4_workspace(vh_batch *b, const vh_n4_params &prm) {
         b->VS = (b->V + 63) & ~(int64_t)63;   // compact-array stride: 256-byte aligned volumes
         const int64_t nch = b->nb * ((b->VS + N4_CH - 1) / N4_CH);
         HIP_TRY(hipMalloc(&b->d_L0, sizeof(float) * b->nb * b->VS));
-        // U and D twice: the study driver keeps the last kept iteration's while computing the next
-        HIP_TRY(hipMalloc(&b->d_U, sizeof(float) * 2 * b->nb * b->VS));
-        HIP_TRY(hipMalloc(&b->d_D, sizeof(float) * 2 * b->nb * b->VS));
+        // U and D three times: the study driver speculates up to two iterations past the last
+        // decided one (rings of 3); the sweep driver keeps PC's p values in D's second third
+        HIP_TRY(hipMalloc(&b->d_U, sizeof(float) * 3 * b->nb * b->VS));
+        HIP_TRY(hipMalloc(&b->d_D, sizeof(float) * 3 * b->nb * b->VS));
         HIP_TRY(hipMalloc(&b->d_perm, sizeof(int32_t) * b->nb * b->VS));
         HIP_TRY(hipMalloc(&b->d_ridx, sizeof(int32_t) * b->nb * b->VS));
         HIP_TRY(hipMalloc(&b->d_cp, sizeof(int32_t) * (b->nb + 1)));

@@ -37,25 +37,41 @@
 #endif
 #define ST_CW (2 + ST_CH_PROD)   // chain waves (conv_mode 0): A, B, producers
 #ifndef ST_CG
-#define ST_CG 0        // conv_mode 0 compute waves: 0 = all 12 others, 1 = the 6 on SIMDs 2 and 3
+#define ST_CG 0        // conv_mode 0 compute waves: 0 = all the others, 1 = the 6 on SIMDs 2 and 3 (depth 1)
 #endif
-static_assert(ST_CW <= 4, "the chain waves are waves 0..3");
-#ifndef ST_CH_NS
-#define ST_CH_NS 4     // chain slot ring here (2 producers, 4 slots: within 1 % of 16 slots)
-#endif
-// conv_mode 0, the S7 recurrence: 0 = the serial chain on ST_CW waves beside the compute waves of
-// the next iteration (speculative); 1 = S7 by guess and verify (n4_shared.h PC) on those waves;
-// 2 = PC on all 16 waves after each iteration's eval (no speculation).  Measured per 256-study bench
-// step: 0 45.8 ms, 1 54 ms, 2 49-50 ms.  PC's ~12 rounds re-run every step, so per study it is VALU
-// throughput work of ~12x25 instructions per masked voxel and iteration, more than the serial chain
-// costs when it hides behind the next iteration's compute; PC wins where one study has the GPU to
-// itself (the sweep driver, k_n4_pcw).
+static_assert(ST_CW == 4, "a chain group is 4 waves, one per SIMD (mu, sig, 2 producers)");
+// conv_mode 0, the S7 recurrence: 0 = serial chains on chain waves beside the compute waves, which
+// speculate ST_DEPTH iterations ahead (below); 2 = S7 by guess and verify (n4_shared.h PC) on all
+// 16 waves after each iteration's eval (no speculation).  Measured per 256-study bench step (depth
+// 1): 0 45.8 ms, 2 49-50 ms, and PC on the 4 chain waves (removed) 54 ms: PC's ~12 rounds are VALU
+// throughput work of ~12x25 instructions per masked voxel and iteration, more than a serial chain
+// costs when it hides behind the compute; PC wins where one study has the GPU to itself (the sweep
+// driver, k_n4_pcw / k_n4_pcg).
 #ifndef ST_PC
 #define ST_PC 0
 #endif
-constexpr bool ST_SPLIT = ST_PC != 2;
-static_assert(ST_PC != 2 || ST_TPB == PC_TPB, "pcw_run takes the whole 1024-thread workgroup");   // conv_mode 0 runs chain waves beside compute waves
-constexpr int ST_PCL = ST_SPLIT ? 64 * ST_CW : ST_TPB;   // PC blocks: one per participating lane
+static_assert(ST_PC == 0 || ST_PC == 2, "ST_PC 0 (serial chains) or 2 (PC on all waves)");
+constexpr bool ST_SPLIT = ST_PC != 2;   // conv_mode 0 runs chain waves beside compute waves
+static_assert(ST_PC != 2 || ST_TPB == PC_TPB, "pcw_run takes the whole 1024-thread workgroup");
+// Speculation depth of the split mode: the compute waves run up to ST_DEPTH iterations ahead of
+// the last iteration whose recurrence has finished.  Depth 2 keeps two chains in flight (chain
+// group g = iteration & 1, ST_CW waves each), so two serial recurrences overlap each other and the
+// compute of the next iteration: U / D rings of 3 buffers, the lattice before each of the last two
+// updates saved in global memory, up to two iterations discarded when ITK's while-condition stops.
+#ifndef ST_DEPTH
+#define ST_DEPTH 1
+#endif
+// Depth 2 is bit-exact (all study tests) but measured slower: 57.4 ms against 46.4 per bench step.
+// Its 8 chain waves leave 8 compute waves (compute phases 34.9 M -> 53.6 M cycles of block 0, two
+// iterations discarded per level end) while the waits only halve (70.2 M -> 33.5 M).
+#ifndef ST_CH_NS
+#define ST_CH_NS (ST_DEPTH == 1 ? 4 : 2)   // chain slots per group (depth 1: 4 within 1 % of 16;
+#endif                                      // depth 2: two rings of 2 keep the LDS of one ring of 4)
+static_assert(ST_DEPTH == 1 || ST_DEPTH == 2, "speculation depth 1 or 2");
+static_assert(ST_CG == 0 || ST_DEPTH == 1, "compute waves on SIMDs 2 and 3 only with one chain group");
+constexpr int ST_NG = ST_DEPTH;             // chain groups
+constexpr int ST_CWT = ST_NG * ST_CW;       // chain waves in all
+constexpr int ST_NB = ST_DEPTH + 1;         // U / D ring buffers
 #ifndef ST_CH_GS
 #define ST_CH_GS 8   // convergence-chain group size here (n4_shared.h ch_group): 8 measured 135M vs 167M cycles for 4
 #endif
@@ -103,6 +119,8 @@ struct StudyArgs {
     int32_t o_wk;    // dense slice weights Wk[2][ncz][Z] (w^3, w^2) of the current level
     int32_t kcap;    // krange entries per table set
     int64_t vol0;
+    float *latg;     // depth 2: [nb][2][lat_cap] the lattice before each of the last two updates
+    int32_t lat_cap;
 };
 
 struct StudyMisc {
@@ -112,13 +130,14 @@ struct StudyMisc {
     float bin_min, slope, bmax, pad;
     double sd, sd2, conv;
     int32_t nc[2][3];
-    ChainState ch;
-    // conv_mode 0 hand-offs between the compute waves and the chain waves
-    int32_t go, go_op, go_d;   // request sequence number; 0 = run the chain on D[go_d], 1 = level end
-    int32_t ch_seq;            // sequence number of the last finished chain (after ch.conv)
+    ChainState ch[ST_NG];
+    // conv_mode 0 hand-offs between the compute waves and chain group g
+    int32_t go[ST_NG], go_op[ST_NG], go_d[ST_NG];   // request number; op 0 = run the chain on D[go_d], 1 = level end
+    int32_t ch_seq[ST_NG];     // request number of the group's last finished chain (after ch.conv)
     int32_t gb_cnt, gb_gen;    // the compute waves' barrier
     int32_t itn, cur, uin;     // iterations of the level, P1 buffer of the last field, U buffer
     int32_t wd;                // a spin-wait watchdog fired (N4State.active = -2; the host raises)
+    int32_t restore;           // depth 2, at the cap: the last computed iteration is discarded
 };
 
 // Spin-wait step with a budget: ~0.5 s of s_sleep, far beyond any legitimate wait (a study's whole
@@ -320,7 +339,7 @@ __device__ void eval_item(const Item &it, int item, int Z, const TabV &Tn, const
         const float u = la - bn;
         st_store(rU, off, u);
         if (CM == 0) {
-            st_store(rD, (ST_PC == 1 ? pc_addr<ST_PCL>((uint32_t)rr, pm) : (uint32_t)rr) * 4u, bo - bn);
+            st_store(rD, (uint32_t)rr * 4u, bo - bn);
         } else {
             const double d = (double)expm1c(bo - bn);
             sd += d;
@@ -555,106 +574,6 @@ __device__ __forceinline__ int next_item(StudyMisc &M, const int32_t *ordr, int 
 }
 
 // ---------------------------------------------------------------------------------------------
-// S7 by guess and verify (n4_shared.h PC) on the ST_CW chain waves: a barrier of their own (an LDS
-// counter and generation, as gsync), pass 0 (p = exp(d) in place, block sums), rounds.
-// ---------------------------------------------------------------------------------------------
-__device__ __forceinline__ void pc_bar(PcShared<ST_PCL> &S, int32_t *wd) {
-    if (!ST_SPLIT) {   // every wave of the workgroup takes part
-        __syncthreads();
-        return;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if ((threadIdx.x & 63) == 0) {
-        const int gen = __hip_atomic_load(&S.bar_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (atomicAdd(&S.bar_cnt, 1) == ST_CW - 1) {
-            __hip_atomic_store(&S.bar_cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_store(&S.bar_gen, gen + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        } else {
-            int bud = ST_SPIN_MAX;
-            while (__hip_atomic_load(&S.bar_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == gen &&
-                   st_spin(bud, wd)) {
-            }
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-
-// The recurrence of one iteration over Dk (d in PC block layout, overwritten by p); ch.conv = result.
-__device__ __attribute__((noinline)) void pc_run(float *Dk, int64_t n, PcShared<ST_PCL> &S, ChainState &ch,
-                                                 int32_t *wd, int req) {
-    // ST_SPLIT: threads [0, ST_PCL) are the chain waves; else the whole workgroup
-    const int tid = threadIdx.x, w = tid >> 6;
-    const PcMap m = pc_map(n, ST_PCL);
-    const uint32_t j = (uint32_t)tid, len = pc_len(m, j), k0 = pc_k0(m, j);
-    if (!ST_SPLIT && tid == 0) {   // the state lives in scratch here: nothing survives a pass
-        S.done = 0;
-        S.fallback = 0;
-    }
-#ifdef PC_PROF
-    const unsigned long long c0 = clock64();
-    unsigned long long c1 = 0, cr = 0, cu = 0;
-#endif
-    double s1 = 0.0, s2 = 0.0;
-    for (uint32_t s0 = 0; s0 < len; s0 += 8) {   // pass 0: p = exp(d) in place, block sums
-        float v[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = s0 + i < len ? Dk[(size_t)(s0 + i) * ST_PCL + j] : 0.0f;
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-            if (s0 + i < len) {
-                const float p = expf_cr(v[i]);
-                Dk[(size_t)(s0 + i) * ST_PCL + j] = p;
-                const double e = (double)p - 1.0;
-                s1 += e;
-                s2 = fma(e, e, s2);
-            }
-    }
-    S.s1(j) = s1;
-    S.s2(j) = s2;
-    pc_bar(S, wd);
-    if (w == 0) pc_guess<ST_PCL>(S, m);
-    pc_bar(S, wd);
-#ifdef PC_PROF
-    c1 = clock64();
-#endif
-    for (int round = 0; round < PC_RMAX + 2; ++round) {
-#ifdef PC_PROF
-        const unsigned long long ca = clock64();
-#endif
-        float mu = S.b[j].gmu, sig = S.b[j].gsig;
-        pc_block<ST_PCL>(Dk, j, len, k0, mu, sig);
-        S.b[j].emu = mu;
-        S.b[j].esig = sig;
-        pc_bar(S, wd);
-#ifdef PC_PROF
-        const unsigned long long cb = clock64();
-        cr += cb - ca;
-#endif
-        if (w == 0) pc_update<ST_PCL>(S, m, round, req);
-        pc_bar(S, wd);
-#ifdef PC_PROF
-        cu += clock64() - cb;
-#endif
-        if (S.done == req) break;
-        if (S.fallback == req) {
-            if (tid == 0) pc_serial<ST_PCL>(S, m, Dk);
-            pc_bar(S, wd);
-            break;
-        }
-    }
-    if (tid == 0) {
-        const float sd = (float)sqrt((double)S.sig / ((double)n - 1.0));
-        ch.mu = S.mu;
-        ch.conv = sd / S.mu;
-#ifdef PC_PROF
-        if (blockIdx.x == 0)
-            printf("PC_PROF req %d n %lld rounds %d fallback %d pass0 %llu rounds %llu update %llu total %llu\n", req,
-                   (long long)n, S.rounds, S.fallback == req, c1 - c0, cr, cu, clock64() - c0);
-#endif
-    }
-}
-
-// ---------------------------------------------------------------------------------------------
 // the kernel: one workgroup per study
 // ---------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
@@ -695,9 +614,9 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
     if (!split) {
         g.w = wv;
         g.nw = ST_WAVES;
-    } else if (ST_CG == 0) {   // every wave but the chain's
-        g.w = wv - ST_CW;
-        g.nw = ST_WAVES - ST_CW;
+    } else if (ST_CG == 0) {   // every wave but the chains'
+        g.w = wv - ST_CWT;
+        g.nw = ST_WAVES - ST_CWT;
     } else {   // only waves on SIMDs 2 and 3 (wave w on SIMD w % 4): A and B keep their SIMDs
         g.w = (wv >= 4 && (wv & 3) >= 2) ? ((wv >> 2) - 1) * 2 + (wv & 1) : -1;
         g.nw = 2 * (ST_WAVES / 4 - 1);
@@ -720,33 +639,28 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
     double2 *TW = DEN + ST_FFT_N;
     unsigned long long *Hc = reinterpret_cast<unsigned long long *>(TW + VH_FFT_P / 2);
     ChainSlot *const cslots = reinterpret_cast<ChainSlot *>(smem + a.o_chain);
-    // PC state: the chain region beside the compute waves (split), else the scratch region, which
-    // nothing else holds between an iteration's eval and the next iteration's histogram
-    PcShared<ST_PCL> &PS = *reinterpret_cast<PcShared<ST_PCL> *>(smem + (ST_SPLIT ? a.o_chain : a.o_scr));
-    const PcMap pm = pc_map(n, ST_PCL);
+    const PcMap pm = pc_map(n, 64 * ST_CW);   // (eval_item's PC layout argument: unused here)
+    float *const latg = a.latg ? a.latg + (size_t)b * 2 * a.lat_cap : nullptr;
     float *const latp = reinterpret_cast<float *>(smem + a.o_latp);
     const int bins = a.bins;
 #ifdef ST_PROF
-    const int st_pt = split ? (ST_CG == 0 ? 64 * ST_CW : 6 * 64) : 0;   // first compute thread keeps the marks
+    const int st_pt = split ? (ST_CG == 0 ? 64 * ST_CWT : 6 * 64) : 0;   // first compute thread keeps the marks
 #endif
 
     if (t == 0) {
         M.item_ctr = 0;
-        M.go = 0;
-        M.go_op = 0;
-        M.go_d = 0;
-        M.ch_seq = 0;
+        for (int q = 0; q < ST_NG; ++q) {
+            M.go[q] = 0;
+            M.go_op[q] = 0;
+            M.go_d[q] = 0;
+            M.ch_seq[q] = 0;
+        }
+        M.restore = 0;
         M.gb_cnt = 0;
         M.gb_gen = 0;
         M.cur = 0;
         M.uin = 0;
         M.wd = 0;
-        if (a.conv_mode == 0 && ST_PC) {
-            PS.bar_cnt = 0;
-            PS.bar_gen = 0;
-            PS.done = 0;
-            PS.fallback = 0;
-        }
     }
     if (wv == 0) find_first3(a, b, fm, M);
     {   // item schedule: items by row count, largest first (ties by index), so the dynamic item
@@ -837,37 +751,51 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
         __syncthreads();
         ST_MARK(0);
         for (int e = t; e < nlat; e += ST_TPB) den[e] = fix128_get(numfix + 2 * e, numfix + 2 * e + 1);
-        if (split && wv < ST_CW) {
-            // ---- chain waves: the recurrence of each kept iteration, on request ----
+        if (split && wv < ST_CWT) {
+            // ---- chain waves: group cg runs the recurrence of the iterations requested of it ----
+            // roles: 0 mu, 1 sig, 2-3 producers.  Wave w runs on SIMD w % 4, and a serial wave is
+            // issue-bound on its SIMD's VALU (4 full-wave VALU per step), so group 1 puts its mu
+            // and sig waves on SIMDs 2 and 3, beside group 0's producers
+            const int cg = wv / ST_CW, wl = (cg == 1) ? (wv % ST_CW + 2) % 4 : wv % ST_CW;
+            ChainSlot *const gslots = cslots + cg * ST_CH_NS;
             for (;;) {
                 int req, bud = ST_SPIN_MAX;
-                while ((req = lds_load_acq(&M.go)) == ch_seen && st_spin(bud, &M.wd)) {
+                while ((req = lds_load_acq(&M.go[cg])) == ch_seen && st_spin(bud, &M.wd)) {
                 }
                 if (req == ch_seen) break;   // watchdog
                 ch_seen = req;
-                if (M.go_op) break;   // level end
-                float *const Dk = a.D + M.go_d * a.half + b * a.VS;
-                if (ST_PC) {
-                    pc_run(Dk, n, PS, M.ch, &M.wd, req);
-                    if (wv == 0) {
-                        wave_lds_order();
-                        if (lane == 0) lds_store_rel(&M.ch_seq, req);   // after ch.conv
-                    }
-                } else if (wv == 0) {
-                    chain_wave_mu<ST_CH_GS, ST_CH_NS>(n, cslots, &M.ch);
-                } else if (wv == 1) {
-                    chain_wave_sig<ST_CH_GS, ST_CH_NS>(n, cslots, &M.ch);
+                if (M.go_op[cg]) break;   // level end
+                const float *const Dk = a.D + M.go_d[cg] * a.half + b * a.VS;
+                if (wl == 0) {
+                    chain_wave_mu<ST_CH_GS, ST_CH_NS>(n, gslots, &M.ch[cg]);
+                } else if (wl == 1) {
+                    chain_wave_sig<ST_CH_GS, ST_CH_NS>(n, gslots, &M.ch[cg]);
                     wave_lds_order();
-                    if (lane == 0) lds_store_rel(&M.ch_seq, req);   // after ch.conv
+                    if (lane == 0) lds_store_rel(&M.ch_seq[cg], req);   // after ch.conv
                 } else {
-                    chain_wave_prod<ST_CH_NS>(Dk, nullptr, n, cslots, &M.ch, wv - 2, ST_CH_PROD);
+                    chain_wave_prod<ST_CH_NS>(Dk, nullptr, n, gslots, &M.ch[cg], wl - 2, ST_CH_PROD);
                 }
             }
         } else if (in_g) {
             // ---- the iterations (compute waves) ----
-            int itn = 0;          // iterations kept in this level
-            int cur = M.cur;      // P1 buffer of the last kept field
-            int uin = M.uin;      // U buffer (and its rpart row) of the last kept iteration
+            int itn = 0;          // iterations computed in this level (split: the last ST_DEPTH undecided)
+            int cur = M.cur;      // P1 buffer of the last computed field
+            int uin = M.uin;      // U buffer (and its rpart row) of the last computed iteration
+            // (thread g.t == 0) the recurrence of iteration j: wait for it / request it of group j % ST_NG
+            auto cwait = [&](int j) -> float {
+                const int q = j % ST_NG;
+                int bud = ST_SPIN_MAX;
+                while (lds_load_acq(&M.ch_seq[q]) != M.go[q] && st_spin(bud, &M.wd)) {
+                }
+                return M.ch[q].conv;
+            };
+            auto creq = [&](int j) {
+                const int q = j % ST_NG;
+                for (int i = 0; i < ST_CH_NS; ++i) chain_reset<ST_CH_NS>(cslots + q * ST_CH_NS, &M.ch[q], i);
+                M.go_op[q] = 0;
+                M.go_d[q] = j % ST_NB;
+                lds_store_rel(&M.go[q], M.go[q] + 1);
+            };
             for (;;) {
                 gsync(g, M);
                 float *const Ub = a.U + uin * a.half + b * a.VS;
@@ -885,14 +813,23 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                     if (lane == 0) {
                         M.stop = 0;
                         M.exact = 0;
+                        M.restore = 0;
                         if (itn > 0) {
                             if (split) {
                                 if (itn >= a.lvs->max_iters[L]) {   // no speculation past the cap
-                                    int bud = ST_SPIN_MAX;
-                                    while (lds_load_acq(&M.ch_seq) != M.go && st_spin(bud, &M.wd)) {
-                                    }
-                                    M.conv = (double)M.ch.conv;
                                     M.stop = 1;
+                                    if (ST_DEPTH == 1 || itn == 1) {
+                                        M.conv = (double)cwait(itn);
+                                    } else {   // iteration itn runs iff conv(itn - 1) > threshold
+                                        const float c1 = cwait(itn - 1);
+                                        const float c2 = cwait(itn);
+                                        if (!(c1 > a.thresh)) {
+                                            M.conv = (double)c1;
+                                            M.restore = 1;
+                                        } else {
+                                            M.conv = (double)c2;
+                                        }
+                                    }
                                 }
                             } else {
                                 if (a.conv_mode == 1) M.conv = conv_of(M.sd, M.sd2, (double)n);
@@ -915,7 +852,16 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                 }
                 gsync(g, M);
                 ST_MARK(1);
-                if (M.stop) break;
+                if (M.stop) {
+                    if (M.restore) {   // depth 2 at the cap: iteration itn discarded (its field's
+                        // P1 is in buffer cur, the previous one's still in the other)
+                        for (int e = g.t; e < nlat; e += g.n) lat[e] = latg[(size_t)(itn & 1) * a.lat_cap + e];
+                        cur ^= 1;
+                        uin = (uin + ST_NB - 1) % ST_NB;
+                        itn -= 1;
+                    }
+                    break;
+                }
                 if (M.exact) {
                     float *s_cmax = reinterpret_cast<float *>(scr);
                     const float m = exact_min_study(a, b, Ub, s_cmax, s_cmax + g.n, g, M);
@@ -1042,7 +988,10 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                     const double d = den[e];
                     const double num = fix128_get(numfix + 2 * e, numfix + 2 * e + 1);
                     const float phi = d != 0.0 ? (float)(num / d) : 0.0f;
-                    if (split) latp[e] = lat[e];
+                    if (split) {
+                        if (ST_DEPTH == 1) latp[e] = lat[e];
+                        else latg[(size_t)(itk & 1) * a.lat_cap + e] = lat[e];
+                    }
                     lat[e] += phi;
                 }
                 gsync(g, M);
@@ -1060,9 +1009,10 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                 ST_MARK(5);
                 // ---- eval: U into the other buffer, d into D[itk & 1] ----
                 {
-                    float *const Uo = a.U + (uin ^ 1) * a.half + b * a.VS;
-                    float *const Dw = a.D + (split ? (itk & 1) * a.half : 0) + b * a.VS;
-                    float4 *const rp_out = rpart0 + (uin ^ 1) * a.nitems;
+                    const int uo = (uin + 1) % ST_NB;
+                    float *const Uo = a.U + uo * a.half + b * a.VS;
+                    float *const Dw = a.D + (split ? (itk % ST_NB) * a.half : 0) + b * a.VS;
+                    float4 *const rp_out = rpart0 + uo * a.nitems;
                     const bool first_of_level = itk == 1;
                     const bool bo_mode = !(L == 0 && first_of_level);
                     const int so = (first_of_level && L > 0) ? ((L - 1) & 1) : (L & 1);
@@ -1100,31 +1050,48 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                 if (split) {
                     if (g.t == 0) {
                         M.stop = 0;
-                        if (itn > 0) {   // ITK's while-condition on iteration itn's recurrence
-                            int bud = ST_SPIN_MAX;
-                                    while (lds_load_acq(&M.ch_seq) != M.go && st_spin(bud, &M.wd)) {
-                                    }
-                            M.conv = (double)M.ch.conv;
-                            if (!(M.ch.conv > a.thresh)) M.stop = 1;
+                        if (ST_DEPTH == 1) {
+                            if (itn > 0) {   // ITK's while-condition on iteration itn's recurrence
+                                const float c = cwait(itn);
+                                M.conv = (double)c;
+                                if (!(c > a.thresh)) M.stop = 1;
+                            }
+                        } else if (itk >= 3) {   // iteration itk - 1 runs iff conv(itk - 2) > threshold
+                            const float c = cwait(itk - 2);
+                            if (!(c > a.thresh)) {
+                                (void)cwait(itk - 1);   // drain the other group
+                                M.conv = (double)c;
+                                M.stop = 1;
+                            }
                         }
-                        if (!M.stop) {   // keep: request the recurrence of iteration itk
-                            if (!ST_PC)
-                                for (int i = 0; i < ST_CH_NS; ++i) chain_reset<ST_CH_NS>(cslots, &M.ch, i);
-                            M.go_op = 0;
-                            M.go_d = itk & 1;
-                            lds_store_rel(&M.go, M.go + 1);
-                        }
+                        if (!M.stop) creq(itk);   // the recurrence of iteration itk
                     }
                     gsync(g, M);
-                    if (M.stop) {   // discard iteration itk: the kept lattice goes back
-                        for (int e = g.t; e < nlat; e += g.n) lat[e] = latp[e];
+                    if (M.stop) {
+                        if (ST_DEPTH == 1) {   // discard iteration itk: the kept lattice goes back
+                            for (int e = g.t; e < nlat; e += g.n) lat[e] = latp[e];
+                        } else {   // discard itk - 1 and itk: the lattice before itk - 1's update,
+                            // its P1 recomputed into the buffer of itk - 1's field, U of itk - 2
+                            for (int e = g.t; e < nlat; e += g.n) lat[e] = latg[(size_t)((itk - 1) & 1) * a.lat_cap + e];
+                            gsync(g, M);
+                            for (int e = g.t; e < ncx * ncy * a.Z; e += g.n) {
+                                const int ij = e / a.Z, z = e % a.Z;
+                                const float4 w = T.wz[z];
+                                const float *l = lat + ij * ncz + T.bz[z];
+                                P1o[e] = (double)w.x * (double)l[0] + (double)w.y * (double)l[1] +
+                                         (double)w.z * (double)l[2] + (double)w.w * (double)l[3];
+                            }
+                            uin = (uin + ST_NB - 1) % ST_NB;
+                            itn = itk - 2;
+                            gsync(g, M);
+                        }
                         break;
                     }
                 } else if (a.conv_mode == 0) {   // S7 on the whole workgroup (ST_PC 2)
                     PcShared<ST_TPB> &PW = *reinterpret_cast<PcShared<ST_TPB> *>(smem + a.o_scr);
                     const float *const Dr = a.D + b * a.VS;
-                    pcw_run([=](int64_t r) { return Dr[r]; }, a.D + a.half + b * a.VS, n, PW, M.ch, itk);
-                    if (t == 0) M.conv = (double)M.ch.conv;
+                    pcw_run([=](int64_t r) { return Dr[r]; }, a.D + a.half + b * a.VS, n, PW, M.ch[0], itk);
+                    if (t == 0) M.conv = (double)M.ch[0].conv;
                 } else if (g.w == 0) {   // S7x: item partials in item order
                     double sd = 0.0, sd2 = 0.0;
                     for (int i = lane; i < a.nitems; i += 64) {
@@ -1142,17 +1109,18 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                 }
                 ST_MARK(7);
                 cur ^= 1;
-                uin ^= 1;
+                uin = (uin + 1) % ST_NB;
                 itn = itk;
             }
             if (g.t == 0) {
                 M.itn = itn;
                 M.cur = cur;
                 M.uin = uin;
-                if (split) {   // level end: release the chain waves
-                    M.go_op = 1;
-                    lds_store_rel(&M.go, M.go + 1);
-                }
+                if (split)   // level end: release the chain waves (every requested chain has finished)
+                    for (int q = 0; q < ST_NG; ++q) {
+                        M.go_op[q] = 1;
+                        lds_store_rel(&M.go[q], M.go[q] + 1);
+                    }
             }
         }
         __syncthreads();
@@ -1226,7 +1194,7 @@ static bool study_layout(const vh_batch *b, const vh_n4_params &prm, StudyLayout
     // conv_mode 0: ST_CW waves run the recurrence beside the compute waves (own slot ring, the
     // lattice kept for a discarded iteration); the fit rings are the compute waves' only
     const bool split = prm.conv_mode == 0 && ST_SPLIT;
-    const int fit_waves = !split ? ST_WAVES : ST_CG == 0 ? ST_WAVES - ST_CW : 2 * (ST_WAVES / 4 - 1);
+    const int fit_waves = !split ? ST_WAVES : ST_CG == 0 ? ST_WAVES - ST_CWT : 2 * (ST_WAVES / 4 - 1);
     // ring rows per wave: up to FIT_NB within ~32 KB for the computing waves
     const int nb_ring = std::max(1, std::min(FIT_NB, (int)(32768 / (fit_waves * 8 * (size_t)s_cap))));
     const size_t fit_num = 2 * sizeof(unsigned long long) * (size_t)nlat_max;
@@ -1247,15 +1215,16 @@ static bool study_layout(const vh_batch *b, const vh_n4_params &prm, StudyLayout
     const int64_t nslots = (b->R + SLOT_R - 1) / SLOT_R;
     const int64_t nitems = b->n4_tiles * nslots;
     a.o_ipart = (int32_t)o; o += A(sizeof(double) * 2 * (size_t)nitems);
-    a.o_rpart = (int32_t)o; o += A(sizeof(float4) * 2 * (size_t)nitems);
+    a.o_rpart = (int32_t)o; o += A(sizeof(float4) * ST_NB * (size_t)nitems);
     a.o_order = (int32_t)o; o += A(sizeof(int32_t) * (size_t)nitems);
     a.o_misc = (int32_t)o; o += A(sizeof(StudyMisc));
     a.o_wk = (int32_t)o; o += A(2 * sizeof(double) * (size_t)kcap * Z);
     a.o_wx = (int32_t)o; o += A(2 * 4 * sizeof(double) * (size_t)R);
     a.o_scr = (int32_t)o; o += A(scr);
     a.o_chain = (int32_t)o;
-    o += split ? A(ST_PC ? sizeof(PcShared<ST_PCL>) : sizeof(ChainSlot) * ST_CH_NS) : 0;
-    a.o_latp = (int32_t)o; o += split ? A(sizeof(float) * nlat_max) : 0;
+    o += split ? A(sizeof(ChainSlot) * ST_CH_NS * ST_NG) : 0;
+    a.o_latp = (int32_t)o; o += (split && ST_DEPTH == 1) ? A(sizeof(float) * nlat_max) : 0;
+    a.lat_cap = nlat_max;
     a.o_wave = (int32_t)((fit_num + 15) & ~(size_t)15);   // ring offset inside the scratch
     a.s_cap = s_cap;
     a.nb_ring = nb_ring;
@@ -1315,6 +1284,18 @@ void vh_launch_n4_study(vh_batch *b, const vh_n4_params &prm) {
                            b->stream));
     a.lvs = (const StudyLevels *)b->d_study_lv;
     a.vol0 = 0;
+    a.latg = nullptr;
+    if (prm.conv_mode == 0 && ST_SPLIT && ST_DEPTH == 2) {   // the two lattice saves per study
+        const size_t need = sizeof(float) * 2 * (size_t)a.lat_cap * (size_t)b->nb;
+        if (need > b->study_latg_cap) {
+            if (b->d_study_latg) HIP_TRY(hipFree(b->d_study_latg));
+            b->d_study_latg = nullptr;
+            b->study_latg_cap = 0;
+            HIP_TRY(hipMalloc(&b->d_study_latg, need));
+            b->study_latg_cap = need;
+        }
+        a.latg = (float *)b->d_study_latg;
+    }
     vh_set_max_lds((const void *)k_n4_study, ST_MAX_LDS);
     ScopedKTimer tm(b, "n4_study", 0.0);
     k_n4_study<<<(unsigned)b->nb, ST_TPB, Ly.bytes, b->stream>>>(a);

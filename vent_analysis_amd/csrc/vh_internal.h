@@ -188,6 +188,8 @@ struct vh_batch {
     double2 *d_twiddle = nullptr;    // FFT twiddles (host-computed)
     void *d_study_lv = nullptr;      // n4_study.hip: per-level table pointers + iteration caps
     void *d_pcg = nullptr;           // n4.hip k_n4_pcg: per-block guesses / ends / sums, aggregates
+    void *d_study_latg = nullptr;    // n4_study.hip depth 2: the lattice before the last two updates
+    size_t study_latg_cap = 0;
     int64_t pcg_cap = 0;             // bytes of d_pcg
     void *d_sortg = nullptr;         // vdp.hip grid sort: per-chunk digit counts / offsets
     int64_t sortg_cap = 0;           // entries of d_sortg
