@@ -1641,7 +1641,10 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
                 // steps: n4_pcg 14.4 -> 10.3 ms per study; config 5 is at one workgroup per CU anyway)
                 const int64_t spb = getenv("VH_PCG_STEPS") ? std::max(1, atoi(getenv("VH_PCG_STEPS"))) : 16;
                 const int64_t want = (b->V / 4 + PC_TPB * spb - 1) / (PC_TPB * spb);
-                pcg_grid = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)per * ncu));
+                // at most one workgroup per CU whatever the occupancy API says: it can report one
+                // block per CU too many, and the cooperative launch accepts an over-size grid
+                // whose grid barrier would then never complete (MI355X_MICROARCH.md, correctness)
+                pcg_grid = (int)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)std::min(per, 1) * ncu));
                 const int64_t NB = (int64_t)pcg_grid * PC_TPB;
                 const size_t need = NB * (6 * sizeof(float) + 2 * sizeof(double)) +
                                     (size_t)pcg_grid * (3 * sizeof(double) + sizeof(int)) + 256;
