@@ -25,6 +25,9 @@ sys.path.insert(0, HERE)
 
 METRIC = "volumes/sec end-to-end VDP, 128×128×24 Xe volume, 1 GPU and 8-GPU batch"
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+# synthetic batch: 64 distinct studies per rank, each with its own lung geometry (masked voxels vary
+# by about +-20 %, so the one-workgroup-per-study N4 sees unequal studies; synth.py vary=True)
+BENCH_UNIQUE = 64
 
 
 # ------------------------------------------------------------------------------------------------
@@ -165,7 +168,7 @@ def host_to_host(R, C, Z, nb, args, device, opts, seed):
     from vent_analysis_amd.synth import synth_batch
     slots = 3
     n = max(1, args.h2h_batches) * nb
-    hp, mk = synth_batch(R, C, Z, n, base_seed=seed, unique=16)
+    hp, mk = synth_batch(R, C, Z, n, base_seed=seed, unique=BENCH_UNIQUE, vary=True)
     P = _lib.Pipe(R, C, Z, nb, slots=slots, device=device)
     out = (np.empty(hp.shape, np.float32), np.empty(hp.shape, np.uint8),
            np.empty(hp.shape, np.uint8), np.empty(hp.shape, np.uint8))
@@ -286,7 +289,7 @@ def main():
     from vent_analysis_amd import _lib
     from vent_analysis_amd.synth import synth_batch
 
-    hp, mk = synth_batch(R, C, Z, nb, base_seed=shard_seed(rank), unique=16)
+    hp, mk = synth_batch(R, C, Z, nb, base_seed=shard_seed(rank), unique=BENCH_UNIQUE, vary=True)
     Bt = _lib.Batch(R, C, Z, nb, device=local)
     Bt.upload(hp, mk)
     use_comm = world > 1 or args.comm
@@ -383,6 +386,7 @@ def main():
                                "mean-anchored + linear-binning + k-means VDP + defect border + "
                                "SNR + cohort histogram" + (" (N4 skipped)" if args.no_n4 else ""),
                    "volumes_per_gpu": nb, "shape": [R, C, Z],
+                   "distinct_studies_per_gpu": min(nb, BENCH_UNIQUE), "lung_geometry": "per study",
                    "parallelism": f"dp{world}", "n4_subbatch": args.subbatch or nb,
                    "n4_iterations_mean": float(its.sum(axis=1).mean()) if its.size else 0.0},
         "roofline": roof,

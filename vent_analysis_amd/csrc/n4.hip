@@ -439,21 +439,28 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_rrank(const uint64_t *rowmask, co
     int32_t run = s_part[t];
     for (int64_t i = s0; i < e0; ++i) { const int32_t v = s_rowtot[i]; s_rowtot[i] = run; run += v; }
     __syncthreads();
-    // perm (raster rank -> compact index) for the sweep driver's convergence walk.  Written by
-    // this one workgroup only: the multi-workgroup eval writes its differences in compact order
-    // (whole lines per workgroup, like U) instead of scattering them to raster ranks.
-    const int32_t *rs = rowstart + b * ntiles * R;
-    int32_t *pm = perm + b * VS;
+    // raster rank of each (tile, row)'s first masked voxel; perm (raster rank -> compact index,
+    // the sweep driver's convergence walk) is scattered by k_n4_perm over the whole GPU (one
+    // workgroup here took 22 ms at 512^3)
     for (int64_t x = threadIdx.x; x < R; x += VH_TPB) {
         const int32_t base = s_rowtot[x];
-        for (int64_t tt = 0; tt < ntiles; ++tt) {
-            const int32_t r0 = rr[tt * R + x] + base;
-            rr[tt * R + x] = r0;
-            uint64_t m = rm[tt * R + x];
-            const int32_t c0 = rs[tt * R + x];
-            for (int32_t i = 0; m; ++i, m &= m - 1ull) pm[r0 + i] = c0 + i;
-        }
+        for (int64_t tt = 0; tt < ntiles; ++tt) rr[tt * R + x] += base;
     }
+}
+
+// perm[raster rank] = compact index: one wave per (tile, row), one lane per column of the tile
+__global__ void __launch_bounds__(VH_TPB) k_n4_perm(const uint64_t *rowmask, const int32_t *rowstart,
+                                                   const int32_t *rrank, int64_t R, int64_t ntiles,
+                                                   int64_t VS, int32_t *perm) {
+    const int64_t b = blockIdx.y;
+    const int64_t e = (int64_t)blockIdx.x * (VH_TPB / 64) + (threadIdx.x >> 6);   // tile * R + row
+    if (e >= ntiles * R) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t o = b * ntiles * R + e;
+    const uint64_t m = rowmask[o];
+    if (!((m >> lane) & 1ull)) return;
+    const int32_t i = __popcll(m & ((1ull << lane) - 1ull));
+    perm[b * VS + rrank[o] + i] = rowstart[o] + i;
 }
 
 // L0 = log(I) at mask == 1 (non-positive -> 0), U = L0 (B = 0), ridx = (row << rsh) | column
@@ -1785,6 +1792,10 @@ void vh_launch_n4(vh_batch *b, const vh_n4_params &prm) {
         if (b->R > 16384) throw VhError{VH_ERR_ARG, "N4: more than 16384 rows"};
         k_n4_rrank<<<(unsigned)b->nb, VH_TPB, sizeof(int32_t) * (size_t)b->R, st>>>(
             b->d_rowmask, b->d_rowstart, b->R, ntiles, b->VS, b->d_rrank, b->d_perm);
+        VH_CHECK_LAUNCH();
+        const int64_t pairs = ntiles * b->R;
+        k_n4_perm<<<dim3((unsigned)((pairs + VH_TPB / 64 - 1) / (VH_TPB / 64)), (unsigned)b->nb), VH_TPB, 0, st>>>(
+            b->d_rowmask, b->d_rowstart, b->d_rrank, b->R, ntiles, b->VS, b->d_perm);
         VH_CHECK_LAUNCH();
     }
     // driver: volume-resident (one workgroup per study) when the batch has studies for the CUs

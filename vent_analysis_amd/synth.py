@@ -8,6 +8,9 @@ slice axis fastest, exactly as ``Vent_Analysis.openSingleDICOM`` produces it
 * mask  = union of two ellipsoids (the two lungs)
 * image = exp(0.4 (i - R/2) / R) * 200 * mask + Rayleigh(10) noise   (a smooth bias field)
 * 6 ventilation defects: spheres (slice axis scaled) inside the mask, intensity x 0.2
+* ``vary=True`` (benchmark batches): per-seed lung geometry -- each ellipsoid's semi-axes scaled by
+  0.8-1.2 and its centre moved by up to 6 % of the extent (a separate stream, so ``vary=False``
+  volumes, which the committed fixtures pin by sha256, are unchanged)
 """
 from __future__ import annotations
 
@@ -18,16 +21,19 @@ import numpy as np
 __all__ = ["synth_volume", "synth_batch", "volume_digest"]
 
 
-def synth_volume(R: int, C: int, Z: int, seed: int):
+def synth_volume(R: int, C: int, Z: int, seed: int, vary: bool = False):
     """Return ``(HPvent float32 (R,C,Z), mask float64 0/1 (R,C,Z))`` for one study."""
     R, C, Z, seed = int(R), int(C), int(Z), int(seed)   # python ints: numpy scalars change promotion
     rng = np.random.default_rng(seed)
     i, j, k = np.meshgrid(np.arange(R, dtype=np.float32), np.arange(C, dtype=np.float32),
                           np.arange(Z, dtype=np.float32), indexing="ij")
     m = np.zeros((R, C, Z), bool)
+    geo = np.random.default_rng(seed + 1_000_003) if vary else None
     for cc in (0.32, 0.68):
-        m |= (((i - R / 2) / (0.35 * R)) ** 2 + ((j - cc * C) / (0.17 * C)) ** 2
-              + ((k - Z / 2) / (0.42 * Z)) ** 2) <= 1
+        sa, sc, sz = geo.uniform(0.8, 1.2, 3) if vary else (1.0, 1.0, 1.0)
+        da, dc, dz = geo.uniform(-0.06, 0.06, 3) if vary else (0.0, 0.0, 0.0)
+        m |= (((i - (0.5 + da) * R) / (0.35 * sa * R)) ** 2 + ((j - (cc + dc) * C) / (0.17 * sc * C)) ** 2
+              + ((k - (0.5 + dz) * Z) / (0.42 * sz * Z)) ** 2) <= 1
     X = np.exp(0.4 * (i - R / 2) / R) * 200 * m + rng.rayleigh(10, (R, C, Z))
     for _ in range(6):
         c = [rng.uniform(0.2, 0.8) * s for s in (R, C, Z)]
@@ -37,7 +43,8 @@ def synth_volume(R: int, C: int, Z: int, seed: int):
     return X.astype(np.float32), m.astype(np.float64)
 
 
-def synth_batch(R: int, C: int, Z: int, n: int, base_seed: int = 0, unique: int | None = None):
+def synth_batch(R: int, C: int, Z: int, n: int, base_seed: int = 0, unique: int | None = None,
+                vary: bool = False):
     """Batch of ``n`` volumes as contiguous ``float32 [n,R,C,Z]`` and ``uint8 [n,R,C,Z]``.
 
     Volume b uses seed ``base_seed + (b % unique)``: ``unique`` bounds host generation time for
@@ -50,7 +57,7 @@ def synth_batch(R: int, C: int, Z: int, n: int, base_seed: int = 0, unique: int 
     for b in range(n):
         s = base_seed + (b % u)
         if s not in cache:
-            x, m = synth_volume(R, C, Z, s)
+            x, m = synth_volume(R, C, Z, s, vary)
             cache[s] = (x, m.astype(np.uint8))
         hp[b], mk[b] = cache[s]
     return hp, mk
