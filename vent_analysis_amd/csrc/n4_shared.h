@@ -754,6 +754,8 @@ __device__ __forceinline__ float chain_sys64(double q0, double q1, float xin, fl
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xf), 63));
 }
 
+// (A fused form -- the shift riding on v_cvt_f64_f32_dpp wave_shr:1, 3 VALU per step -- does not
+// assemble: gfx950's DP-ALU DPP accepts only row_newbcast.)
 // Row form (CH_SYS 2): the 64 steps as 4 rows of 16 lanes taken one after the other (EXEC = the
 // row).  Inside a row the move rides on the cvt (DPP row_newbcast:k gives every lane of the row
 // lane k's x: 3 VALU per step); the first step of a row takes lane 15 of the row before
