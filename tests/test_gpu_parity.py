@@ -335,6 +335,25 @@ def test_vdp_chain_ragged_vs_oracle(case):
     assert np.array_equal(_lib.border(M.astype(np.uint8))[0], O.calculate_border(M))
 
 
+@pytest.mark.parametrize("shape", [(256, 256, 64), (160, 200, 140)])
+def test_large_single_volume_grid_sort_vs_oracle(shape):
+    """One volume of >= 2^22 voxels takes the grid radix sort (k_sortg_*, 4 passes over 8192-key
+    chunks) and the wave-parallel k-means tile sums: the sorted-key statistics (numpy-order mean,
+    p99 order statistic) and the maps equal the oracle bit for bit; the k-means partition matches
+    the oracle's Lloyd run on the sorted values."""
+    X, M = synth_volume(*shape, 41)
+    vox = (1.0, 1.0, 1.0)
+    d, bo, lb, res = _lib.vdp(X, M.astype(np.uint8), vox)
+    o = O.calculate_vdp(X, M, vox, HP=X)
+    assert np.float32(res[0].mean_anchor) == o["mean_anchor"] and np.float32(res[0].p99) == o["p99"]
+    assert np.array_equal(d[0], o["defectArray"]) and np.array_equal(lb[0], o["defectArrayLB"])
+    assert res[0].vdp == o["VDP"] and res[0].vdp_lb == o["VDP_lb"]
+    s = np.sort(X[M > 0].astype(np.float32))
+    counts, centres, _ = O.kmeans_1d_sorted(s)
+    assert int(res[0].n_km0) == int(counts[0])
+    assert np.allclose(list(res[0].km_centres), centres, rtol=1e-12)
+
+
 def test_empty_mask_volume_in_batch():
     """A study with an empty mask must not disturb its neighbours; the class raises IndexError
     like the reference's sorted-list indexing (Vent_Analysis.py:255)."""
