@@ -1691,7 +1691,7 @@ void vh_launch_vdp_chain(vh_batch *b, const float *d_n4, const vh_run_opts &o) {
     }
     {
         ScopedKTimer tm(b, "sort", 0.0);
-        if (b->nb == 1 && b->V >= ((int64_t)1 << 22)) {   // one large volume: the grid sort
+        if (b->nb == 1 && b->V >= ((int64_t)1 << 20)) {   // one large volume: the grid sort
             const int64_t nchunk = (b->V + VS_CHUNK - 1) / VS_CHUNK;
             if (b->sortg_cap < nchunk * 256) {
                 if (b->d_sortg) HIP_TRY(hipFree(b->d_sortg));
