@@ -398,11 +398,13 @@ __device__ void fit_item(const Item &it, const TabV &T, const double *Wk, const 
 // ---------------------------------------------------------------------------------------------
 // U range for the next histogram (S2).  ITK scans in raster order with
 //   if (u > max) max = u; else if (u < min) min = u;
-// so the minimum skips every "record" voxel (strictly above all earlier ones).  The records that
-// can matter form the strictly increasing run u1 < u2 < ... < uK at the start of the raster order
-// (a later record is above a non-record voxel).  The sweeps keep the maximum and the three smallest
-// values (a multiset) per lane; with u1, u2, u3 read back afterwards, min over all but the run is
-// exact for K <= 2, and a run of 3 or more falls back to the exact raster scan.
+// so the minimum skips every "record" voxel (strictly above all earlier ones).  Let u1 < ... < uK be
+// the strictly increasing run at the start of the raster order (u(K+1) <= uK).  Every later record
+// lies above uK >= u(K+1), a non-record, so it never is the minimum: ITK's minimum is the minimum
+// over all voxels but the run.  The sweeps keep the maximum and the three smallest values (a
+// multiset) per lane; the run is read back from the first masked voxels and taken out of the
+// triple; the exact raster scan is left for a run that outlasts the voxels read back or that
+// swallows the whole triple.
 // ---------------------------------------------------------------------------------------------
 struct Range3 {
     float mx, m1, m2, m3;   // max; three smallest, m1 <= m2 <= m3
@@ -438,20 +440,22 @@ __device__ __forceinline__ Range3 r3_wave(Range3 r) {
     }
     return r;
 }
-// ITK's bin minimum from the merged range and the first three masked voxels' values (u[0..2],
-// nfirst of them exist).  Returns false when the exact raster scan is needed.
+// ITK's bin minimum from the merged range and the first masked voxels' values (u[0..nfirst)).
+// Returns false when the exact raster scan is needed.
 __device__ __forceinline__ bool r3_bin_min(const Range3 &r, const float *u, int nfirst, float &bmin) {
     if (nfirst < 3) return false;
-    if (!(u[1] > u[0])) {                       // K = 1: exclude u1
-        bmin = u[0] == r.m1 ? r.m2 : r.m1;
+    int K = 1;
+    while (K < nfirst && u[K] > u[K - 1]) ++K;
+    if (K == nfirst || !(u[K] <= u[K - 1])) return false;   // run may go on / NaN ends it
+    const float m[3] = {r.m1, r.m2, r.m3};
+    int j = 0;   // multiset difference of two ascending lists: triple minus run
+    for (int i = 0; i < 3; ++i) {
+        while (j < K && u[j] < m[i]) ++j;
+        if (j < K && u[j] == m[i]) { ++j; continue; }
+        bmin = m[i];
         return true;
     }
-    if (!(u[2] > u[1])) {                       // K = 2: exclude u1 < u2
-        if (u[0] != r.m1) bmin = r.m1;
-        else bmin = u[1] == r.m2 ? r.m3 : r.m2;
-        return true;
-    }
-    return false;                               // K >= 3
+    return false;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1416,6 +1420,66 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
 }
 
 
+// ---- block steps that skip work the float arithmetic makes redundant (CH_SKIP) -----------------
+// mu: late in a chain the float running mean mostly stays put (|p - mu| / k below half an ulp: in
+// the bench studies' last 20 iterations 4-13 % of the steps change it).  Every lane evaluates its
+// step from the current mu exactly (the spec's fma and roundings); the first lane whose result
+// differs is the next change, the lanes before it leave mu as it is.  One dependent round per
+// change instead of one per step; a block whose predecessor changed mu more than CH_SKIP_MAX times
+// takes the systolic form.  Bit-identical by construction (every step is the exact step applied to
+// the exact state).  rec = mu before the lane's step.  Measured on the 256-study bench (serial
+// chains, ST_PC 0): mu skip 60.7 ms, sig blocks 66.2 ms, both 69.7 ms against 54.1 ms systolic --
+// one skip round (convert, f64 fma, convert, compare, ballot, find-first, readlane) is a dependent
+// chain about twice a systolic step, and too few steps stagnate on whole blocks; kept opt-in.
+#ifndef CH_SKIP
+#define CH_SKIP 0   // bit 0: mu skip, bit 1: sig block (opt-in: measured slower, see above)
+#endif
+#ifndef CH_SKIP_MAX
+#define CH_SKIP_MAX 24
+#endif
+__device__ __forceinline__ float chain_mu_skip(double q0, double q1, float m, float &rec, int &changes) {
+    const int lane = threadIdx.x & 63;
+    uint64_t pending = ~0ull;
+    changes = 0;
+    for (;;) {
+        const float cand = (float)fma((double)m, q0, q1);
+        const uint64_t chg = __ballot(cand != m) & pending;
+        if (!chg) {
+            if ((pending >> lane) & 1ull) rec = m;
+            return m;
+        }
+        const int j0 = __ffsll((unsigned long long)chg) - 1;
+        const uint64_t upto = (j0 == 63) ? ~0ull : ((2ull << j0) - 1ull);
+        if (((pending & upto) >> lane) & 1ull) rec = m;
+        m = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cand), j0));
+        pending &= ~upto;
+        ++changes;
+        if (!pending) return m;
+    }
+}
+// sig: inside one binade [2^e, 2^(e+1)) a float step adds RN(sig + t) - sig, the same amount for
+// every sig of the binade (the double rounding of sig + t is anchored on sig's own grid, whose low
+// 29 bits are zero; only an exact float tie would depend on sig's last bit).  So the block's 64
+// increments are taken from the block's first state sig0 in parallel and summed exactly (multiples
+// of ulp(sig0)).  Valid when sig0 > 0, no step lands on an exact tie, and the sum stays in sig0's
+// binade (the steps only add); otherwise the caller runs the block serially.  Returns false then.
+__device__ __forceinline__ bool chain_sig_block(double q0, double q1, float sig0, float &sig_end) {
+    if (!(sig0 > 0.0f)) return false;
+    const double y = fma(q1, q0, (double)sig0);           // q1 = s (or 0), q0 = (k - 1) / k (or 0)
+    const uint64_t yb = (uint64_t)__double_as_longlong(y);
+    const bool tie = (yb & 0x1fffffffull) == 0x10000000ull;
+    const float inc = (float)y - sig0;                     // exact: same binade (checked below)
+    double sum = (double)inc;
+    for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 64);
+    if (__ballot(tie) != 0ull) return false;
+    const double e = (double)sig0 + sum;
+    const float ef = (float)e;
+    const int b0 = (__float_as_int(sig0) >> 23) & 0xff, b1 = (__float_as_int(ef) >> 23) & 0xff;
+    if (b0 != b1 || (double)ef != e) return false;
+    sig_end = ef;
+    return true;
+}
+
 // wave A: the mu recurrence, block by block as the producers fill them.
 template <int GS = 8, int NS = CH_SLOTS>
 __device__ void chain_wave_mu(int64_t n, ChainSlot *slots, ChainState *cs) {
@@ -1426,13 +1490,19 @@ __device__ void chain_wave_mu(int64_t n, ChainSlot *slots, ChainState *cs) {
     __builtin_amdgcn_s_setprio(CH_PRIO);   // the serial waves win issue arbitration on their SIMD
     CH_T0();
     float muf = 0.0f;
+    int last_changes = 64;   // the first block (k from 1) moves mu at nearly every step
     for (int64_t blk = 0; blk < nblk; ++blk) {
         ChainSlot &S = slots[blk % NS];
         CH_WAIT(wt, while (lds_load_acq(&S.ready) != (int)(blk + 1)) __builtin_amdgcn_s_sleep(1));
         if (CH_SYS) {
             const double2 q = S.ab[lane];
             float rec;
-            muf = CH_SYS == 2 ? chain_rows64<true>(q.x, q.y, muf, rec) : chain_sys64<true>(q.x, q.y, muf, rec);
+            if ((CH_SKIP & 1) && last_changes <= CH_SKIP_MAX)
+                muf = chain_mu_skip(q.x, q.y, muf, rec, last_changes);
+            else {
+                muf = CH_SYS == 2 ? chain_rows64<true>(q.x, q.y, muf, rec) : chain_sys64<true>(q.x, q.y, muf, rec);
+                last_changes = __popcll(__ballot(rec != __shfl_down(rec, 1, 64)));   // changes seen
+            }
             S.mu[lane] = rec;
             mu = (double)muf;
         } else if (lane == 0) {
@@ -1468,8 +1538,12 @@ __device__ void chain_wave_sig(int64_t n, ChainSlot *slots, ChainState *cs) {
             const double c = S.cs[lane].x;
             float rec;
             const double q0 = ok ? c : 0.0, q1 = ok ? (double)(q * q) : 0.0;
-            sig = (double)(CH_SYS == 2 ? chain_rows64<false>(q0, q1, (float)sig, rec)
-                                       : chain_sys64<false>(q0, q1, (float)sig, rec));
+            float se;
+            if ((CH_SKIP & 2) && chain_sig_block(q0, q1, (float)sig, se))
+                sig = (double)se;
+            else
+                sig = (double)(CH_SYS == 2 ? chain_rows64<false>(q0, q1, (float)sig, rec)
+                                           : chain_sys64<false>(q0, q1, (float)sig, rec));
             (void)rec;
         } else {
             S.cs[lane] = ok ? make_double2(S.cs[lane].x, (double)(q * q)) : make_double2(0.0, 0.0);

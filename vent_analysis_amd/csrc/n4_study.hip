@@ -31,6 +31,7 @@
 #define ST_TPB 1024
 #define ST_WAVES (ST_TPB / 64)
 #define ST_HC 8        // LDS histogram copies
+#define ST_NFIRST 16   // first masked voxels (raster order) tracked for the bin minimum (n4_shared.h r3_bin_min)
 #define ST_MAX_LDS (160 * 1024)
 #ifndef ST_CH_PROD
 #define ST_CH_PROD 2   // producer waves of the convergence chain (n4_shared.h chain_wave_prod)
@@ -42,13 +43,12 @@
 static_assert(ST_CW == 4, "a chain group is 4 waves, one per SIMD (mu, sig, 2 producers)");
 // conv_mode 0, the S7 recurrence: 0 = serial chains on chain waves beside the compute waves, which
 // speculate ST_DEPTH iterations ahead (below); 2 = S7 by guess and verify (n4_shared.h PC) on all
-// 16 waves after each iteration's eval (no speculation).  Measured per 256-study bench step (depth
-// 1): 0 45.8 ms, 2 49-50 ms, and PC on the 4 chain waves (removed) 54 ms: PC's ~12 rounds are VALU
-// throughput work of ~12x25 instructions per masked voxel and iteration, more than a serial chain
-// costs when it hides behind the compute; PC wins where one study has the GPU to itself (the sweep
-// driver, k_n4_pcw / k_n4_pcg).
+// 16 waves after each iteration's eval (no speculation).  Measured per 256-study bench step
+// (heterogeneous studies): 2 33.1 ms, 0 depth 1 53.7 ms, 0 depth 2 48.8 ms.  (Before the bin
+// minimum stopped falling back to the raster scan, r3_bin_min, the compute waves spent that scan's
+// time beside the serial chain and 0 came out ahead: 45.8 vs 49-50 ms.)
 #ifndef ST_PC
-#define ST_PC 0
+#define ST_PC 2
 #endif
 static_assert(ST_PC == 0 || ST_PC == 2, "ST_PC 0 (serial chains) or 2 (PC on all waves)");
 constexpr bool ST_SPLIT = ST_PC != 2;   // conv_mode 0 runs chain waves beside compute waves
@@ -125,8 +125,9 @@ struct StudyArgs {
 
 struct StudyMisc {
     int32_t item_ctr, stop, exact, nfirst;
-    int32_t foff[3];        // compact offsets of the first three masked voxels in raster order
-    int32_t rx[3], rc[3];   // their (row, column)
+    int32_t foff[ST_NFIRST];   // compact offsets of the first masked voxels in raster order
+    int32_t rx[ST_NFIRST], rc[ST_NFIRST];   // their (row, column)
+    float fu[ST_NFIRST];   // their values in the current field (ctrl wave)
     float bin_min, slope, bmax, pad;
     double sd, sd2, conv;
     int32_t nc[2][3];
@@ -249,31 +250,31 @@ __device__ void init_item(const StudyArgs &a, int64_t b, const Item &it, int ite
     rpart_store(rpart, item, r3_wave(rg));
 }
 
-// wave 0: the first three masked voxels in raster order (row, then column) and their compact offsets
-__device__ void find_first3(const StudyArgs &a, int64_t b, int64_t first, StudyMisc &M) {
+// wave 0: the first ST_NFIRST masked voxels in raster order (row, then column) and their compact offsets
+__device__ void find_first(const StudyArgs &a, int64_t b, int64_t first, StudyMisc &M) {
     const int lane = threadIdx.x & 63;
     int found = 0;
     if (lane == 0) {
-        for (int q = 0; q < 3; ++q) M.rx[q] = M.rc[q] = M.foff[q] = -1;
+        for (int q = 0; q < ST_NFIRST; ++q) M.rx[q] = M.rc[q] = M.foff[q] = -1;
         M.nfirst = 0;
     }
     if (first < 0) return;
     const int64_t tb = b * (int64_t)a.ntiles * a.R;
     const int fx = (int)(first / a.CZ), fcol = (int)(first % a.CZ);
-    for (int x = fx; x < a.R && found < 3; ++x)
-        for (int t0 = x == fx ? fcol / TILE_W : 0; t0 < a.ntiles && found < 3; t0 += 64) {
+    for (int x = fx; x < a.R && found < ST_NFIRST; ++x)
+        for (int t0 = x == fx ? fcol / TILE_W : 0; t0 < a.ntiles && found < ST_NFIRST; t0 += 64) {
             const int t = t0 + lane;
             uint64_t m = t < a.ntiles ? a.rmask[tb + (int64_t)t * a.R + x] : 0ull;
             if (x == fx && t < fcol / TILE_W) m = 0ull;
             if (x == fx && t == fcol / TILE_W) m &= ~((2ull << (fcol % TILE_W)) - 1ull) | (1ull << (fcol % TILE_W));
             uint64_t nz = __ballot(m != 0ull);
-            while (nz && found < 3) {
+            while (nz && found < ST_NFIRST) {
                 const int l = __builtin_ctzll(nz);
                 nz &= nz - 1;
                 const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)m, l);
                 const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(m >> 32), l);
                 uint64_t mm = ((uint64_t)hi << 32) | lo;
-                while (mm && found < 3) {
+                while (mm && found < ST_NFIRST) {
                     const int bit = __builtin_ctzll(mm);
                     mm &= mm - 1;
                     if (lane == 0) {
@@ -662,7 +663,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
         M.uin = 0;
         M.wd = 0;
     }
-    if (wv == 0) find_first3(a, b, fm, M);
+    if (wv == 0) find_first(a, b, fm, M);
     {   // item schedule: items by row count, largest first (ties by index), so the dynamic item
         // queue of every pass ends on small items; the item order of every reduction is unchanged
         int32_t *isz = reinterpret_cast<int32_t *>(scr);
@@ -702,7 +703,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
         for (int e = t; e < nl0; e += ST_TPB) lat[e] = 0.0f;
     }
 #ifdef ST_PROF
-    unsigned long long st_prof[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_t0 = clock64();
+    unsigned long long st_prof[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_t0 = clock64();
 #endif
     int ch_seen = 0;   // chain waves: the last request taken
     for (int L = 0; L < a.nlev; ++L) {
@@ -798,6 +799,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
             };
             for (;;) {
                 gsync(g, M);
+                ST_MARK(10);
                 float *const Ub = a.U + uin * a.half + b * a.VS;
                 const float4 *const rp_in = rpart0 + uin * a.nitems;
                 if (g.w == 0) {   // ctrl: ITK's while-condition (at the cap, or conv_mode 1), bin range
@@ -810,6 +812,8 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                         r3_merge(r, o);
                     }
                     r = r3_wave(r);
+                    if (lane < M.nfirst) M.fu[lane] = Ub[M.foff[lane]];   // the run's values
+                    wave_lds_order();
                     if (lane == 0) {
                         M.stop = 0;
                         M.exact = 0;
@@ -837,11 +841,9 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                             }
                         }
                         if (!M.stop) {
-                            float u[3];
-                            for (int q = 0; q < M.nfirst; ++q) u[q] = Ub[M.foff[q]];
                             float bmin;
                             M.bmax = r.mx;
-                            if (r3_bin_min(r, u, M.nfirst, bmin)) {
+                            if (r3_bin_min(r, M.fu, M.nfirst, bmin)) {
                                 M.bin_min = bmin;
                                 M.slope = (r.mx - bmin) / (float)(bins - 1);
                             } else {
@@ -872,7 +874,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                     gsync(g, M);
                 }
                 const int itk = itn + 1;   // the iteration computed now
-                ST_MARK(1);
+                ST_MARK(9);
                 const float bmin = M.bin_min, slope = M.slope;
                 const double rinv = 1.0 / (double)slope;   // div_r form of the bin division
                 // ---- hist (S3): one packed 64-bit add per value ----
@@ -1143,8 +1145,8 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
 #ifdef ST_PROF
     if (t == st_pt && blockIdx.x == 0)
         printf("ST_PROF den %llu ctrl %llu hist %llu emap %llu fit %llu latP1 %llu eval %llu "
-               "wait %llu level %llu\n", st_prof[0], st_prof[1], st_prof[2], st_prof[3], st_prof[4],
-               st_prof[5], st_prof[6], st_prof[7], st_prof[8]);
+               "wait %llu level %llu exact %llu top %llu\n", st_prof[0], st_prof[1], st_prof[2], st_prof[3],
+               st_prof[4], st_prof[5], st_prof[6], st_prof[7], st_prof[8], st_prof[9], st_prof[10]);
 #endif
     // final field's P1 for k_n4_final
     const double *P1f = M.cur ? P1b1 : P1b0;
