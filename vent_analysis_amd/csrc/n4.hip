@@ -1364,7 +1364,8 @@ __global__ void __launch_bounds__(PC_TPB) k_n4_pcg(PcgArgs A) {
             A.emu[j] = mu;
             A.esig[j] = sig;
             pcg_scan(A, L, grid, a, bm, bsv, mm, dm, ds, first);
-            if (first == NB) {   // every block end matched its successor's guess: exact
+            if (first == NB) {   // every block end matched its successor's guess
+                if (phase == 0) break;   // phase A's fixed point (sig steps uncertified): verify it exactly
                 if (j == (uint32_t)(nbe - 1)) {
                     const float sd = (float)sqrt((double)sig / ((double)n - 1.0));
                     A.st[A.b].conv_w = sd / mu;
