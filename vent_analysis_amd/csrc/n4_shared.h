@@ -1130,6 +1130,19 @@ __device__ __forceinline__ PcKf pc_kf(float k, float p) {
     q.e0 = fmaf(q.r0, 0x1p-40f, 0x1p-44f);   // >= 2^-22 |mu rl| + 2^-46 |mu| for mu < 4 (see below)
     return q;
 }
+// the same constants for two steps at once (packed FP32: v_pk_fma / v_pk_mul / v_pk_add issue two
+// lanes' worth per instruction; identical roundings to pc_kf)
+typedef float pc_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void pc_kf2(pc_f2 k, pc_f2 p, PcKf &qa, PcKf &qb) {
+    const pc_f2 r0 = {__builtin_amdgcn_rcpf(k.x), __builtin_amdgcn_rcpf(k.y)};
+    const pc_f2 rl = r0 * __builtin_elementwise_fma(-k, r0, (pc_f2)1.0f);
+    const pc_f2 B = __builtin_elementwise_fma(p, r0, p * rl);
+    const pc_f2 ch = 1.0f - r0;
+    const pc_f2 cl = ((-r0) - (ch - 1.0f)) - rl;
+    const pc_f2 e0 = __builtin_elementwise_fma(r0, (pc_f2)0x1p-40f, (pc_f2)0x1p-44f);
+    qa = PcKf{r0.x, rl.x, B.x, ch.x, cl.x, e0.x};
+    qb = PcKf{r0.y, rl.y, B.y, ch.y, cl.y, e0.y};
+}
 // one phase-A step; returns false when the mu step is not certified (the state is then approximate)
 __device__ __forceinline__ bool pc_apx_step(const PcKf &q, float p, bool first, float &mu, float &sig) {
     if (!first) {
@@ -1164,7 +1177,8 @@ __device__ __forceinline__ void pc_block_apx(const float *P, uint32_t j, uint32_
         for (int i = 0; i < 8; ++i) nxt[i] = s0 + 8 + i < len ? P[(size_t)(s0 + 8 + i) * nl + j] : 0.0f;
         PcKf q[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) q[i] = pc_kf(kf + (float)i, cur[i]);
+        for (int i = 0; i < 8; i += 2)
+            pc_kf2(kf + (pc_f2){(float)i, (float)(i + 1)}, (pc_f2){cur[i], cur[i + 1]}, q[i], q[i + 1]);
         const float mu0 = mu, sig0 = sig;
         bool ok = pc_apx_step(q[0], cur[0], kf == 1.0f, mu, sig);
 #pragma unroll
