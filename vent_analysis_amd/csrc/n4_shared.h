@@ -1157,9 +1157,9 @@ __device__ __forceinline__ bool pc_apx_step(const PcKf &q, float p, bool first, 
     const float t1 = fmaf(-mu, q.r0, q.B);
     const float t = fmaf(-mu, q.rl, t1);
     const float E = fmaf(fabsf(t), 0x1p-21f, q.e0);
-    const float ya = mu + (t - E);
-    const bool ok = ya == mu + (t + E);
-    mu = ya;   // = RN(mu + t) whenever ok
+    const pc_f2 y2 = (pc_f2)mu + ((pc_f2)t + (pc_f2){-E, E});   // both ends in two packed adds
+    const bool ok = y2.x == y2.y;
+    mu = y2.x;   // = RN(mu + t) whenever ok
     return ok;
 }
 // a lane's block in phase A: groups of 8 steps without guards; a group with an uncertified step is
