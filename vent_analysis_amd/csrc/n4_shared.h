@@ -1118,7 +1118,7 @@ __device__ void pc_serial(PcShared<NL> &S, const PcMap &m, const float *P) {
 // round (scripts/dev/pc_sim.c: 12 A + 1.2 B rounds on the bench studies, against 13 exact rounds).
 // consts of one step for phase A
 struct PcKf {
-    float r0, rl, B, ch, cl, e0;
+    float r0, rl, B, ch, cl;
 };
 __device__ __forceinline__ PcKf pc_kf(float k, float p) {
     PcKf q;
@@ -1127,7 +1127,6 @@ __device__ __forceinline__ PcKf pc_kf(float k, float p) {
     q.B = fmaf(p, q.r0, p * q.rl);
     q.ch = 1.0f - q.r0;
     q.cl = ((-q.r0) - (q.ch - 1.0f)) - q.rl;
-    q.e0 = fmaf(q.r0, 0x1p-40f, 0x1p-44f);   // >= 2^-22 |mu rl| + 2^-46 |mu| for mu < 4 (see below)
     return q;
 }
 // the same constants for two steps at once (packed FP32: v_pk_fma / v_pk_mul / v_pk_add issue two
@@ -1139,12 +1138,12 @@ __device__ __forceinline__ void pc_kf2(pc_f2 k, pc_f2 p, PcKf &qa, PcKf &qb) {
     const pc_f2 B = __builtin_elementwise_fma(p, r0, p * rl);
     const pc_f2 ch = 1.0f - r0;
     const pc_f2 cl = ((-r0) - (ch - 1.0f)) - rl;
-    const pc_f2 e0 = __builtin_elementwise_fma(r0, (pc_f2)0x1p-40f, (pc_f2)0x1p-44f);
-    qa = PcKf{r0.x, rl.x, B.x, ch.x, cl.x, e0.x};
-    qb = PcKf{r0.y, rl.y, B.y, ch.y, cl.y, e0.y};
+    qa = PcKf{r0.x, rl.x, B.x, ch.x, cl.x};
+    qb = PcKf{r0.y, rl.y, B.y, ch.y, cl.y};
 }
 // one phase-A step; returns false when the mu step is not certified (the state is then approximate)
-__device__ __forceinline__ bool pc_apx_step(const PcKf &q, float p, bool first, float &mu, float &sig) {
+// e0 >= r0 2^-40 + 2^-44 >= 2^-22 |mu rl| + 2^-46 |mu| for mu < 4 (one bound per block: r0 <= 1/k0)
+__device__ __forceinline__ bool pc_apx_step(const PcKf &q, float e0, float p, bool first, float &mu, float &sig) {
     if (!first) {
         const float d = p - mu, q2 = d * d;
         const float y = fmaf(q2, q.ch, sig);
@@ -1156,7 +1155,7 @@ __device__ __forceinline__ bool pc_apx_step(const PcKf &q, float p, bool first, 
     // them): a larger mu only makes a step uncertified-but-wrong, which phase B then corrects
     const float t1 = fmaf(-mu, q.r0, q.B);
     const float t = fmaf(-mu, q.rl, t1);
-    const float E = fmaf(fabsf(t), 0x1p-21f, q.e0);
+    const float E = fmaf(fabsf(t), 0x1p-21f, e0);
     const pc_f2 y2 = (pc_f2)mu + ((pc_f2)t + (pc_f2){-E, E});   // both ends in two packed adds
     const bool ok = y2.x == y2.y;
     mu = y2.x;   // = RN(mu + t) whenever ok
@@ -1171,6 +1170,7 @@ __device__ __forceinline__ void pc_block_apx(const float *P, uint32_t j, uint32_
 #pragma unroll
     for (int i = 0; i < 8; ++i) cur[i] = (uint32_t)i < len ? P[(size_t)i * nl + j] : 0.0f;
     float kf = (float)k0;
+    const float e0 = fmaf(__builtin_amdgcn_rcpf(kf), 0x1p-39f, 0x1p-44f);   // covers every step's r0
     uint32_t s0 = 0;
     for (; s0 + 8 <= len; s0 += 8) {
 #pragma unroll
@@ -1180,9 +1180,9 @@ __device__ __forceinline__ void pc_block_apx(const float *P, uint32_t j, uint32_
         for (int i = 0; i < 8; i += 2)
             pc_kf2(kf + (pc_f2){(float)i, (float)(i + 1)}, (pc_f2){cur[i], cur[i + 1]}, q[i], q[i + 1]);
         const float mu0 = mu, sig0 = sig;
-        bool ok = pc_apx_step(q[0], cur[0], kf == 1.0f, mu, sig);
+        bool ok = pc_apx_step(q[0], e0, cur[0], kf == 1.0f, mu, sig);
 #pragma unroll
-        for (int i = 1; i < 8; ++i) ok &= pc_apx_step(q[i], cur[i], false, mu, sig);
+        for (int i = 1; i < 8; ++i) ok &= pc_apx_step(q[i], e0, cur[i], false, mu, sig);
         if (!ok) {   // redo the group exactly
             mu = mu0;
             sig = sig0;
