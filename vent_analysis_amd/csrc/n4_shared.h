@@ -1143,8 +1143,9 @@ __device__ __forceinline__ void pc_kf2(pc_f2 k, pc_f2 p, PcKf &qa, PcKf &qb) {
 }
 // one phase-A step; returns false when the mu step is not certified (the state is then approximate)
 // e0 >= r0 2^-40 + 2^-44 >= 2^-22 |mu rl| + 2^-46 |mu| for mu < 4 (one bound per block: r0 <= 1/k0)
+template <bool SIG = true>
 __device__ __forceinline__ bool pc_apx_step(const PcKf &q, float e0, float p, bool first, float &mu, float &sig) {
-    if (!first) {
+    if (SIG && !first) {
         const float d = p - mu, q2 = d * d;
         const float y = fmaf(q2, q.ch, sig);
         const float rho = fmaf(q2, q.ch, sig - y);
@@ -1163,9 +1164,11 @@ __device__ __forceinline__ bool pc_apx_step(const PcKf &q, float e0, float p, bo
 }
 // a lane's block in phase A: groups of 8 steps without guards; a group with an uncertified step is
 // redone with the exact steps (rare: the wave branches only when one of its lanes needs it)
-template <int NL>
+// SIG = false: the mu recurrence alone (mu never reads sig; sig is returned unchanged)
+template <int NL, bool SIG = true>
 __device__ __forceinline__ void pc_block_apx(const float *P, uint32_t j, uint32_t len, uint32_t k0,
                                              float &mu, float &sig, uint32_t nl = NL) {
+    const float sig_in = sig;
     float cur[8], nxt[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) cur[i] = (uint32_t)i < len ? P[(size_t)i * nl + j] : 0.0f;
@@ -1180,9 +1183,9 @@ __device__ __forceinline__ void pc_block_apx(const float *P, uint32_t j, uint32_
         for (int i = 0; i < 8; i += 2)
             pc_kf2(kf + (pc_f2){(float)i, (float)(i + 1)}, (pc_f2){cur[i], cur[i + 1]}, q[i], q[i + 1]);
         const float mu0 = mu, sig0 = sig;
-        bool ok = pc_apx_step(q[0], e0, cur[0], kf == 1.0f, mu, sig);
+        bool ok = pc_apx_step<SIG>(q[0], e0, cur[0], kf == 1.0f, mu, sig);
 #pragma unroll
-        for (int i = 1; i < 8; ++i) ok &= pc_apx_step(q[i], e0, cur[i], false, mu, sig);
+        for (int i = 1; i < 8; ++i) ok &= pc_apx_step<SIG>(q[i], e0, cur[i], false, mu, sig);
         if (!ok) {   // redo the group exactly
             mu = mu0;
             sig = sig0;
@@ -1201,6 +1204,7 @@ __device__ __forceinline__ void pc_block_apx(const float *P, uint32_t j, uint32_
             pc_step(kd, cur[i], mu, sig);
             kd += 1.0;
         }
+    if (!SIG) sig = sig_in;
 }
 
 // ---- all-wave PC helpers (NL = threads of the workgroup, one block per thread) -----------------
@@ -1264,7 +1268,7 @@ __device__ void pcw_guess(PcShared<NL> &S, const PcMap &m) {
 // first failing transition; else the next guesses.  Ends with the caller's barrier.
 template <int NL>
 __device__ void pcw_update(PcShared<NL> &S, const PcMap &m, int round, int req, bool at_cap,
-                           bool cap_fallback) {
+                           bool cap_fallback, bool use_sig = true) {
     const int j = threadIdx.x, lane = j & 63, w = j >> 6;
     const int nbe = m.L ? NL : (int)m.rem;
     double a = 1.0, bm = 0.0, bs = 0.0;
@@ -1275,9 +1279,10 @@ __device__ void pcw_update(PcShared<NL> &S, const PcMap &m, int round, int req, 
         const float gn = S.b[j + 1].gmu, gsn = S.b[j + 1].gsig;
         em = B.emu;
         es = B.esig;
-        mm = __float_as_uint(B.emu) != __float_as_uint(gn) || __float_as_uint(B.esig) != __float_as_uint(gsn);
+        mm = __float_as_uint(B.emu) != __float_as_uint(gn) ||
+             (use_sig && __float_as_uint(B.esig) != __float_as_uint(gsn));
         bm = (double)B.emu - (double)gn;
-        bs = (double)B.esig - (double)gsn;
+        bs = use_sig ? (double)B.esig - (double)gsn : 0.0;
         const uint32_t k0 = pc_k0(m, j), k1 = k0 + pc_len(m, j) - 1u;
         // model slopes (deterministic float arithmetic; they only steer the guesses)
         float af = (float)(k0 - 1u) * __builtin_amdgcn_rcpf((float)k1);
@@ -1314,7 +1319,7 @@ __device__ void pcw_update(PcShared<NL> &S, const PcMap &m, int round, int req, 
     }
     if (j < nbe - 1) {
         S.b[j + 1].gmu = dm == 0.0 ? em : (float)((double)em + a * dm);
-        S.b[j + 1].gsig = ds == 0.0 ? es : (float)((double)es + ds);
+        if (use_sig) S.b[j + 1].gsig = ds == 0.0 ? es : (float)((double)es + ds);
     }
 }
 
@@ -1368,43 +1373,49 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
     c1 = clock64();
 #endif
     int round = 0;
-    // phase A: certified float rounds to their fixed point.  A thread whose start did not change
+    // phase A: certified float rounds to their fixed point, first on mu alone (mu never reads sig:
+    // a third fewer instructions per step), then on both.  A thread whose start did not change
     // keeps its end; a wave whose threads all kept theirs skips the round.
-    float lg = __int_as_float(0x7fc00000), ls = lg, le = 0.0f, les = 0.0f;
 #ifdef PC_PROF
     unsigned long long cblk = 0;
 #endif
-    for (int ra0 = 0; ra0 < PC_AMAX; ++ra0, ++round) {
+    for (int pass = 0; pass < 2; ++pass) {
+        // done / fallback flags carry a tag per call and stage (no reset between stages: a wave
+        // still reading the flag of the stage before must not see it cleared)
+        const int tag = 4 * req + pass;
+        float lg = __int_as_float(0x7fc00000), ls = lg, le = 0.0f, les = 0.0f;
+        for (int ra0 = 0; ra0 < PC_AMAX; ++ra0, ++round) {
 #ifdef PC_PROF
-        const unsigned long long cq = clock64();
+            const unsigned long long cq = clock64();
 #endif
-        const float g = S.b[j].gmu, gs = S.b[j].gsig;
-        const bool same = __float_as_uint(g) == __float_as_uint(lg) && __float_as_uint(gs) == __float_as_uint(ls);
-        if (__ballot(!same) != 0ull && !same) {
-            float mu = g, sig = gs;
-            pc_block_apx<PC_TPB>(P, j, len, k0, mu, sig);
-            lg = g;
-            ls = gs;
-            le = mu;
-            les = sig;
+            const float g = S.b[j].gmu, gs = S.b[j].gsig;
+            const bool same = __float_as_uint(g) == __float_as_uint(lg) && __float_as_uint(gs) == __float_as_uint(ls);
+            if (__ballot(!same) != 0ull && !same) {
+                float mu = g, sig = gs;
+                if (pass == 0) pc_block_apx<PC_TPB, false>(P, j, len, k0, mu, sig);
+                else pc_block_apx<PC_TPB, true>(P, j, len, k0, mu, sig);
+                lg = g;
+                ls = gs;
+                le = mu;
+                les = sig;
+            }
+            S.b[j].emu = le;
+            S.b[j].esig = les;
+            __syncthreads();
+#ifdef PC_PROF
+            cblk += clock64() - cq;
+#endif
+            pcw_update<PC_TPB>(S, m, round, tag, ra0 == PC_AMAX - 1, false, pass == 1);
+            __syncthreads();
+            if (S.done == tag) break;
         }
-        S.b[j].emu = le;
-        S.b[j].esig = les;
-        __syncthreads();
-#ifdef PC_PROF
-        cblk += clock64() - cq;
-#endif
-        pcw_update<PC_TPB>(S, m, round, req, ra0 == PC_AMAX - 1, false);
-        __syncthreads();
-        if (S.done == req) break;
     }
 #ifdef PC_PROF
     ra = round + 1;
     c2 = clock64();
 #endif
     // phase B: exact rounds (the verification; usually one)
-    if (tid == 0) S.done = 0;
-    __syncthreads();
+    const int tagb = 4 * req + 2;
     for (int rb = 0; rb < PC_RMAX; ++rb) {
         ++round;
         float mu = S.b[j].gmu, sig = S.b[j].gsig;
@@ -1412,10 +1423,10 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
         S.b[j].emu = mu;
         S.b[j].esig = sig;
         __syncthreads();
-        pcw_update<PC_TPB>(S, m, round, req, rb == PC_RMAX - 1, true);
+        pcw_update<PC_TPB>(S, m, round, tagb, rb == PC_RMAX - 1, true);
         __syncthreads();
-        if (S.done == req) break;
-        if (S.fallback == req) {
+        if (S.done == tagb) break;
+        if (S.fallback == tagb) {
             if (tid == 0) pc_serial<PC_TPB>(S, m, P);
             __syncthreads();
             break;
@@ -1428,7 +1439,7 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
 #ifdef PC_PROF
         if (blockIdx.x == 0)
             printf("PCW_PROF n %lld roundsA %d roundsB %d fallback %d pass0 %llu A %llu (blocks %llu) B %llu\n",
-                   (long long)n, ra, S.rounds - ra + 0, S.fallback == req, c1 - c0, c2 - c1, cblk, clock64() - c2);
+                   (long long)n, ra, S.rounds - ra + 0, S.fallback == tagb, c1 - c0, c2 - c1, cblk, clock64() - c2);
 #endif
     }
 }
