@@ -1331,6 +1331,10 @@ __device__ void pcw_update(PcShared<NL> &S, const PcMap &m, int round, int req, 
 // p = exp(d) into P in block layout (one wave-wide load per step afterwards) and the block sums;
 // then phase A (certified float rounds) and phase B (exact rounds, the verification); after
 // PC_RMAX exact rounds the rest runs serially from the first failing block.  ch.conv = result.
+#ifndef PC_APASS
+#define PC_APASS 2   // phase-A stages; 1 = mu alone, then straight to the exact rounds (measured 7.56k
+                     // against 8.02k vol/s: sig then takes several of the dearer exact rounds)
+#endif
 #ifndef PC_AMAX
 #define PC_AMAX 40
 #endif
@@ -1379,7 +1383,7 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
 #ifdef PC_PROF
     unsigned long long cblk = 0;
 #endif
-    for (int pass = 0; pass < 2; ++pass) {
+    for (int pass = 0; pass < PC_APASS; ++pass) {
         // done / fallback flags carry a tag per call and stage (no reset between stages: a wave
         // still reading the flag of the stage before must not see it cleared)
         const int tag = 4 * req + pass;
