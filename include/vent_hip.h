@@ -17,6 +17,7 @@
  *   vh_ci        CI.calculate_CI + Vent_Analysis.calculate_CI CI.py:107-145, Vent_Analysis.py:265-271
  *   vh_overlay   Vent_Analysis.exportDICOM (pixel data)       Vent_Analysis.py:381-428
  *   vh_montage   Vent_Analysis.screenShot (montage array)     Vent_Analysis.py:458-520
+ *   vh_recon     Vent_Analysis.process_RAW (k-space -> image) Vent_Analysis.py:537-540
  *   vh_batch_*   the same pipeline over a device-resident batch of studies (build-defined)
  *   vh_pipe_*    the batch pipeline fed from host memory with overlapped transfers (build-defined)
  *   vh_comm_*    cohort histogram all-reduce over RCCL (build-defined, BASELINE config 4)
@@ -30,7 +31,7 @@
 extern "C" {
 #endif
 
-#define VH_ABI_VERSION 3
+#define VH_ABI_VERSION 4
 
 /* status codes */
 #define VH_OK 0
@@ -175,6 +176,13 @@ int vh_montage(vh_ctx *ctx, int64_t R, int64_t C, int64_t Z, const void *proton,
                const void *hp, int hp_is64, const float *n4, const uint8_t *mask_border,
                const uint8_t *defect, const double *ci, const double *parula, int64_t prow,
                const int64_t crop[6], uint8_t *image);
+
+/* ---- TWIX raw reconstruction --------------------------------------- */
+/* process_RAW's image from raw k-space (Vent_Analysis.py:537-540): for every slice k,
+ * fftshift(fft2(fftshift(K[:, :, k]))) in complex128, then np.transpose(., (1, 0, 2))[:, ::-1, :].
+ * k: complex128 as interleaved (re, im) doubles, C order [n0][n1][nz]; out: complex128 [n1][n0][nz].
+ * (The twix file parse, mapvbvd at :532-536, stays on the host.)  1 <= n0, n1 <= 5120. */
+int vh_recon(vh_ctx *ctx, const double *k, int64_t n0, int64_t n1, int64_t nz, double *out);
 
 /* ---- host-to-host pipeline ------------------------------------------------------------------ */
 /* Streams n host-resident studies through `slots` device batches of `sub` volumes each (one HIP

@@ -30,10 +30,11 @@
  *          denominator weights w^2 with p = 1.  phi = (float)(num / den), lattice += phi.
  *      S6  evaluation: P1 = sum_k wz lat (double), T = (float) sum_j wy P1 (double), B = float
  *          sum_i wx T (4 products, left to right); U = L0 - B.
- *      S7  convergence: d = expm1c(B_old - B_new) (float; degree-5 polynomial for |x| < 1/16,
- *          else (float)expm1((double)x)); CoV from sum d, sum d^2 in double (the only reduction
- *          whose order is not fixed: it moves the iteration count only if CoV is within ~1e-15
- *          relative of the threshold).
+ *      S7  convergence (conv_mode 0): ITK's float convergence measure over d = B_old - B_new in
+ *          raster order, RealType = float throughout -- the counter N too (N += 1.0 is exact up to
+ *          2^24 and then frozen) -- with ITK's separate double roundings of every right-hand side
+ *          (conv_welford below).  conv_mode 1 (S7x): the exact coefficient of variation from
+ *          sum d', sum d'^2 in double, d' = expm1c(d).
  *      S8  level change: exact cubic subdivision (spans doubled per axis), axis by axis.
  *      S9  output: B at every voxel per S6, I / (float)exp((double)B).
  *
@@ -441,28 +442,33 @@ static inline float eval_B(const float *T, const axis_t *ax, int ncx, int64_t x,
  *   if (N > 1.0) sigma = sigma + sqr(pixel - mu) * (N - 1.0) / N;
  *   mu = mu * (1.0 - 1.0 / N) + pixel / N;
  *   sigma = std::sqrt(sigma / (N - 1.0)); return sigma / mu;
- * with float state and the double literals promoting each right-hand side to double.  The build
- * spec evaluates each right-hand side as ONE double fma rounded to float:
- *   mu  <- (float)fma((double)mu, 1 - 1/N, (double)(p / N))
- *   sig <- (float)fma((double)((p - mu)^2), (N - 1)/N, (double)sig)
- * (ITK rounds the product and the sum separately; the two agree unless the double result lies within
- * ~2^-52 of a float rounding boundary, p ~ 2^-28 per step).  p = (float)exp((double)d).  The state is a
- * serial float recurrence (the float running mean drifts): it must be evaluated in raster order. */
+ * with float state (mu, sigma, N) and the double literals promoting each right-hand side to double,
+ * evaluated left to right with a rounding after every operation:
+ *   N   <- (float)(N + 1.0)                       exact below 2^24; 2^24 + 1 rounds back to 2^24
+ *   sig <- (float)(sig + RN(RN(sqr(p - mu) * (N - 1)) / N))   (the product is exact: 24 x 24 bits)
+ *   mu  <- (float)(RN(mu * RN(1 - RN(1 / N))) + (double)(p / N))   (p / N a float division)
+ * p = (float)exp((double)d) (correctly rounded).  The state is a serial float recurrence (the float
+ * running mean drifts): it must be evaluated in raster order.  This is exactly the S7 of the ITK-float
+ * restatement n4_oracle_itk below (which takes expf instead). */
 static float conv_welford(const float *d, int64_t n)
 {
-    float mu = 0.0f, sig = 0.0f;
+    float mu = 0.0f, sig = 0.0f, N = 0.0f;
     for (int64_t k = 1; k <= n; ++k) {
         const float p = expf_cr(d[k - 1]);
-        const double kd = (double)k;
-        if (k > 1) {
+        N = (float)((double)N + 1.0);
+        const double Nd = (double)N;
+        if (Nd > 1.0) {
             const float q = p - mu;
-            sig = (float)fma((double)(q * q), (kd - 1.0) / kd, (double)sig);
+            sig = (float)((double)sig + ((double)(q * q) * (Nd - 1.0)) / Nd);
         }
-        mu = (float)fma((double)mu, 1.0 - 1.0 / kd, (double)(p / (float)k));
+        mu = (float)((double)mu * (1.0 - 1.0 / Nd) + (double)(p / N));
     }
-    const float s = (float)sqrt((double)sig / ((double)n - 1.0));
+    const float s = (float)sqrt((double)sig / ((double)N - 1.0));
     return s / mu;
 }
+
+/* S7 alone (tests/test_n4_oracle.py) */
+float n4o_conv_welford(const float *d, int64_t n) { return conv_welford(d, n); }
 
 /* S7x (conv_mode 1): the coefficient of variation ITK intends, evaluated exactly enough that
  * order does not matter: d' = expm1c(d), CoV from sum d', sum d'^2 in double */
@@ -786,4 +792,38 @@ done:
     free(L0); free(B); free(lat); free(tmp); free(tmp2); free(delta); free(omega);
     free(H); free(hv); free(E);
     return rc;
+}
+
+/* ---- lemma check (tests/test_n4_oracle.py): the exact sig step of the GPU's PC (n4_shared.h pc_div)
+ * takes RN(Q / N) as Markstein's correction RN(y + r (Q - N y)), y = RN(Q r), r = RN(1 / N), for
+ * Q = sqr(p - mu) (N - 1) (exact in double).  Returns the number of cases, out of `count`
+ * pseudo-random (q2 float, N integer in [2, 2^24]) pairs and the edge N values, whose corrected
+ * quotient differs from the IEEE division. */
+static uint64_t xs64(uint64_t *s) { *s ^= *s << 13; *s ^= *s >> 7; *s ^= *s << 17; return *s; }
+int64_t markstein_check(int64_t count, uint64_t seed)
+{
+    uint64_t st = seed ? seed : 88172645463325252ull;
+    int64_t bad = 0;
+    for (int64_t i = 0; i < count; ++i) {
+        const uint64_t u = xs64(&st);
+        double N;
+        switch (i & 7) {
+        case 0: N = (double)(1u << (1 + (u >> 59) % 24)); break;                 /* powers of two */
+        case 1: N = (double)(1u << (1 + (u >> 59) % 24)) - 1.0; break;
+        case 2: N = (double)((1u << (1 + (u >> 59) % 23)) + 1u); break;
+        case 3: N = 16777216.0 - (double)(u >> 60); break;                         /* near 2^24 */
+        default: N = 2.0 + (double)(u % 16777215u); break;
+        }
+        if (N < 2.0) N = 2.0;
+        const uint32_t bits = (uint32_t)(xs64(&st) >> 32);
+        const int ex = (int)(xs64(&st) % 80) - 70;
+        const float q2 = ldexpf(1.0f + (float)(bits & 0x7fffff) * 0x1p-23f, ex);
+        const double Q = (double)q2 * (N - 1.0);
+        const double r = 1.0 / N;
+        const double y = Q * r;
+        const double e = fma(-N, y, Q);
+        const double t = fma(e, r, y);
+        if (t != Q / N) ++bad;
+    }
+    return bad;
 }

@@ -412,6 +412,47 @@ def test_full_size_batch_properties():
     assert np.array_equal(h1, exp)
 
 
+def test_bench_workload_vs_oracle():
+    """The exact batch bench.py times at N=1 (256 x 128x128x24, 64 distinct studies with per-study
+    lung geometry, masked voxels +-20 %: synth_batch(..., unique=64, vary=True)) through the default
+    path (k_n4_study with PC).  Every distinct study against the C oracle: per-level iterations,
+    identical float32 convergence values, N4HPvent within 1 ulp; the post-N4 chain bit-exact against
+    the numpy oracle applied to the GPU's N4HPvent; the repeated studies identical to their first
+    copy wherever they sit in the batch."""
+    import bench
+    from concurrent.futures import ThreadPoolExecutor
+    nb, R, C, Z = 256, 128, 128, 24
+    vox = (1.5, 1.5, 10.0)
+    hp, mk = synth_batch(R, C, Z, nb, base_seed=bench.shard_seed(0), unique=bench.BENCH_UNIQUE,
+                         vary=True)
+    B = _lib.Batch(R, C, Z, nb)
+    B.upload(hp, mk)
+    B.run(B.options(do_n4=True, vox=vox, do_cohort=True))
+    n4, d, bo, lb, res = B.download(n4=True)
+    B.close()
+    u = bench.BENCH_UNIQUE
+    for b in range(u, nb):
+        assert np.array_equal(n4[b], n4[b % u]) and np.array_equal(d[b], d[b % u])
+        assert list(res[b].n4_iters[:4]) == list(res[b % u].n4_iters[:4])
+    with ThreadPoolExecutor(16) as ex:   # ctypes drops the GIL: the oracle runs in parallel
+        refs = list(ex.map(lambda b: native.n4(hp[b], mk[b]), range(u)))
+    nmask = [int((mk[b] == 1).sum()) for b in range(u)]
+    assert max(nmask) > 1.15 * min(nmask)   # the heterogeneous batch, not 64 copies of one geometry
+    for b in range(u):
+        ref, its_ref, conv_ref = refs[b]
+        assert_n4_matches(n4[b], res[b].n4_iters[:4], res[b].n4_conv[:4], ref, its_ref, conv_ref,
+                          0, ("bench", b))
+        o = O.calculate_vdp(n4[b], mk[b].astype(np.float64), vox, HP=hp[b])
+        assert np.array_equal(d[b], o["defectArray"]), b
+        assert np.array_equal(bo[b] == 1, o["defectBorder"]), b
+        assert np.array_equal(lb[b], o["defectArrayLB"]), b
+        assert res[b].vdp == o["VDP"] and res[b].vdp_lb == o["VDP_lb"], b
+        assert np.float32(res[b].mean_anchor) == o["mean_anchor"], b
+        assert np.float32(res[b].p99) == o["p99"], b
+        assert res[b].n_km0 * 100 / mk[b].sum() == pytest.approx(o["VDP_km"], abs=0), b
+        assert rel(np.float32(res[b].snr), o["SNR"]) < 1e-5, b
+
+
 # ---- BASELINE configs 2 and 5 --------------------------------------------------------------------
 @pytest.mark.parametrize("shape,seed", [((64, 64, 16), 0), ((37, 45, 7), 3), ((48, 48, 48), 4)])
 def test_vdp_chain_morph3d_vs_oracle(shape, seed):

@@ -81,3 +81,46 @@ def test_deterministic():
     a = native.n4(X, M)[0]
     b = native.n4(X, M)[0]
     assert np.array_equal(a, b)
+
+
+def test_markstein_division_lemma():
+    """The GPU's exact sig step (n4_shared.h pc_div) takes ITK's RN(sqr(p - mu) (N - 1) / N) as
+    Markstein's correction from RN(1/N); it must equal the IEEE double division (N in [2, 2^24],
+    including powers of two and their neighbours)."""
+    import ctypes as ct
+    f = native.lib().markstein_check
+    f.restype = ct.c_int64
+    assert f(ct.c_int64(4_000_000), ct.c_uint64(12345)) == 0
+
+
+def itk_convergence_py(d):
+    """ITK's CalculateConvergenceMeasurement with RealType = float, restated step by step in numpy
+    scalars (itkN4BiasFieldCorrectionImageFilter: N += 1.0; if (N > 1.0) sigma = sigma +
+    sqr(pixel - mu) * (N - 1.0) / N; mu = mu * (1.0 - 1.0 / N) + pixel / N; each right-hand side
+    in double, assigned to float)."""
+    f32, f64 = np.float32, np.float64
+    mu = sig = N = f32(0.0)
+    for x in d:
+        p = f32(np.exp(f64(x)))
+        N = f32(f64(N) + 1.0)
+        if f64(N) > 1.0:
+            q = f32(p - mu)
+            sig = f32(f64(sig) + (f64(f32(q * q)) * (f64(N) - 1.0)) / f64(N))
+        mu = f32(f64(mu) * (1.0 - 1.0 / f64(N)) + f64(f32(p / N)))
+    s = f32(np.sqrt(f64(sig) / (f64(N) - 1.0)))
+    return f32(s / mu)
+
+
+def test_conv_welford_follows_itk_roundings():
+    """S7 of the build spec (oracle conv_welford, which the GPU matches bit for bit) equals ITK's
+    float recurrence with its separate double roundings, on field differences of the N4 scale."""
+    import ctypes as ct
+    f = native.lib().n4o_conv_welford
+    f.restype = ct.c_float
+    rng = np.random.default_rng(3)
+    for n, scale in ((2, 1e-2), (37, 3e-3), (5000, 2e-3), (20000, 1e-3)):
+        d = (rng.standard_normal(n) * scale).astype(np.float32)
+        got = f(d.ctypes.data_as(ct.POINTER(ct.c_float)), ct.c_int64(n))
+        assert np.float32(got) == itk_convergence_py(d), n
+    # the float counter stops at 2^24 (2^24 + 1 rounds to even), which conv_welford shares
+    assert np.float32(np.float64(np.float32(2.0 ** 24)) + 1.0) == np.float32(2.0 ** 24)

@@ -359,9 +359,25 @@ class Vent_Analysis:
             print(f'\033[32mScreenshot saved to {path}\033[37m')
         return img
 
-    def process_RAW(self, *a, **k):
-        raise NotImplementedError("TWIX recon (Vent_Analysis.py:522-540) is disabled in the "
-                                  "reference GUI (SURVEY §8f rank 4)")
+    def process_RAW(self, filepath=None, raw_K=None):
+        """TWIX reconstruction (Vent_Analysis.py:522-540): raw_HPvent = transpose(fftshift(fft2(
+        fftshift(raw_K[:, :, k]))), (1, 0, 2))[:, ::-1, :] in complex128, on the GPU (vh_recon).
+        The twix parse (mapvbvd.mapVBVD, :532-536) needs mapvbvd, which is not installed here: pass
+        the squeezed k-space array as raw_K instead (what ``twix.image['']`` returns)."""
+        if raw_K is None:
+            try:
+                import mapvbvd  # noqa: F401  (not in the reference's requirements either)
+            except ImportError as e:
+                raise ImportError("process_RAW: reading a twix file needs mapvbvd; pass raw_K= "
+                                  "(the squeezed k-space array) instead") from e
+            twix = mapvbvd.mapVBVD(filepath)
+            self.raw_twix = twix
+            self.metadata['TWIXscanDateTime'] = twix.hdr.Config['PrepareTimestamp']
+            self.metadata['TWIXprotocolName'] = twix.hdr.Meas['tProtocolName']
+            twix.image.squeeze = True
+            raw_K = twix.image['']
+        self.raw_K = np.asarray(raw_K)
+        self.raw_HPvent = _lib.recon(self.raw_K)
 
     def __repr__(self):
         s = f'\033[35mVent_Analysis\033[37m class object version \033[94m{self.version}\033[37m\n'

@@ -80,6 +80,7 @@ _SIGS = {
     "vh_overlay": ([_P, _P, _P, _I64, _I64, _I64, _I64, _P], ct.c_int),
     "vh_montage": ([_P, _I64, _I64, _I64, _P, ct.c_int, _P, ct.c_int, _P, _P, _P, _P, _P, _I64, _P,
                     _P], ct.c_int),
+    "vh_recon": ([_P, _P, _I64, _I64, _I64, _P], ct.c_int),
     "vh_pipe_create": ([_P, _I64, _I64, _I64, _I64, ct.c_int, ct.POINTER(_P)], ct.c_int),
     "vh_pipe_run": ([_P, _P, _P, _I64, ct.POINTER(RunOpts), _P, _P, _P, _P, _P], ct.c_int),
     "vh_pipe_destroy": ([_P], ct.c_int),
@@ -310,6 +311,22 @@ def montage(proton, hp, n4, mask_border, defect, ci, parula, crop, device=0):
     c.check(c.L.vh_montage(c.h, R, C, Z, _ptr(p), p64, _ptr(h), h64, _ptr(n), _ptr(mb), _ptr(df),
                            _ptr(ci64), _ptr(pal), pal.shape[0], _ptr(cr), _ptr(img)), "vh_montage")
     return img
+
+
+def recon(raw_k, device=0):
+    """process_RAW's image (vh_recon, Vent_Analysis.py:537-540): complex k-space [n0][n1][nz] ->
+    complex128 [n1][n0][nz] = transpose(fftshift(fft2(fftshift(slice))), (1, 0, 2))[:, ::-1, :].
+    The transform runs in complex128 whatever the input precision (numpy 1.23, the reference pin,
+    computes every FFT in double)."""
+    c = context(device)
+    k = np.asarray(raw_k)
+    if k.ndim != 3:
+        raise ValueError(f"raw k-space must be 3-D (cols, lines, slices), got shape {k.shape}")
+    k = np.ascontiguousarray(k, dtype=np.complex128)
+    n0, n1, nz = k.shape
+    out = np.empty((n1, n0, nz), np.complex128)
+    c.check(c.L.vh_recon(c.h, _ptr(k), n0, n1, nz, _ptr(out)), "vh_recon")
+    return out
 
 
 class Batch:

@@ -54,7 +54,10 @@ static void resolve_timers(vh_batch *b) {
 // helpers
 // ---------------------------------------------------------------------------------------------
 static int fail(vh_ctx *c, int code, const std::string &msg) {
-    if (c) c->last_error = msg;
+    if (c) {
+        std::lock_guard<std::mutex> g(c->err_mu);
+        c->last_error = msg;
+    }
     return code;
 }
 
@@ -364,11 +367,19 @@ int vh_destroy(vh_ctx *ctx) {
     }
     if (ctx->comm) ncclCommDestroy((ncclComm_t)ctx->comm);
     if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
+    if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
+    if (ctx->recon_buf) (void)hipFree(ctx->recon_buf);
     delete ctx;
     return VH_OK;
 }
 
-const char *vh_last_error(const vh_ctx *ctx) { return ctx ? ctx->last_error.c_str() : ""; }
+const char *vh_last_error(const vh_ctx *ctx) {
+    static thread_local std::string copy;   // stable until this thread's next call
+    if (!ctx) return "";
+    std::lock_guard<std::mutex> g(ctx->err_mu);
+    copy = ctx->last_error;
+    return copy.c_str();
+}
 
 int vh_synchronize(vh_ctx *ctx) {
     API_TRY(ctx, {
@@ -616,6 +627,33 @@ int vh_montage(vh_ctx *ctx, int64_t R, int64_t C, int64_t Z, const void *proton,
         vh_batch *b = scratch_batch(ctx, R, C, Z, 1);
         vh_montage_run(b->stream, R, C, Z, proton, proton_is64, hp, hp_is64, n4, mask_border, defect,
                        ci, parula, prow, crop, image);
+    })
+}
+
+// ---- TWIX recon (recon.hip) -------------------------------------------------------------------
+int vh_recon(vh_ctx *ctx, const double *k, int64_t n0, int64_t n1, int64_t nz, double *out) {
+    API_TRY(ctx, {
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        if (!k || !out) throw VhError{VH_ERR_ARG, "recon: null buffer"};
+        if (n0 < 1 || n1 < 1 || nz < 1 || n0 > 5120 || n1 > 5120 || n0 * n1 * nz >= ((int64_t)1 << 31))
+            throw VhError{VH_ERR_ARG, "recon: dims must be 1 <= n0, n1 <= 5120, n0 n1 nz < 2^31"};
+        HIP_TRY(hipSetDevice(ctx->device));
+        if (!ctx->aux) HIP_TRY(hipStreamCreateWithFlags(&ctx->aux, hipStreamNonBlocking));
+        const size_t NV = (size_t)(n0 * n1 * nz), bytes = sizeof(double2) * (3 * NV + n0 + n1);
+        if (bytes > ctx->recon_cap) {
+            if (ctx->recon_buf) HIP_TRY(hipFree(ctx->recon_buf));
+            ctx->recon_buf = nullptr;
+            ctx->recon_cap = 0;
+            HIP_TRY(hipMalloc(&ctx->recon_buf, bytes));
+            ctx->recon_cap = bytes;
+        }
+        double2 *d_in = (double2 *)ctx->recon_buf, *d_tmp = d_in + NV, *d_out = d_tmp + NV,
+                *d_tw0 = d_out + NV, *d_tw1 = d_tw0 + n0;
+        hipStream_t st = ctx->aux;
+        HIP_TRY(hipMemcpyAsync(d_in, k, sizeof(double2) * NV, hipMemcpyHostToDevice, st));
+        vh_recon_run(st, d_in, d_tmp, d_out, d_tw0, d_tw1, n0, n1, nz);
+        HIP_TRY(hipMemcpyAsync(out, d_out, sizeof(double2) * NV, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
     })
 }
 

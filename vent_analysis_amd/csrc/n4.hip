@@ -1234,11 +1234,13 @@ __device__ void pcg_scan(const PcgArgs &A, PcgLds &L, cooperative_groups::grid_g
         A.agF[blockIdx.x] = f;
     }
     grid.sync();
-    if (w == 0) {   // the workgroups before this one (ordered: lane l folds [4l, 4l + 4)), and the grid's first failure
+    if (w == 0) {   // the workgroups before this one (ordered: lane l folds [per l, per l + per)), and
+        // the grid's first failure; any grid size (per = ceil(G / 64) aggregates per lane)
         double Al = 1.0, Bl = 0.0, Sl = 0.0;
         int f = NB;
-        for (int i = 0; i < 4; ++i) {
-            const int u = 4 * lane + i;
+        const int per = (G + 63) / 64;
+        for (int i = 0; i < per; ++i) {
+            const int u = per * lane + i;
             if (u < G) {
                 f = min(f, A.agF[u]);
                 if (u < (int)blockIdx.x) {
@@ -1366,10 +1368,7 @@ __global__ void __launch_bounds__(PC_TPB) k_n4_pcg(PcgArgs A) {
             pcg_scan(A, L, grid, a, bm, bsv, mm, dm, ds, first);
             if (first == NB) {   // every block end matched its successor's guess
                 if (phase == 0) break;   // phase A's fixed point (sig steps uncertified): verify it exactly
-                if (j == (uint32_t)(nbe - 1)) {
-                    const float sd = (float)sqrt((double)sig / ((double)n - 1.0));
-                    A.st[A.b].conv_w = sd / mu;
-                }
+                if (j == (uint32_t)(nbe - 1)) A.st[A.b].conv_w = itk_conv(mu, sig, n);
                 done = true;
                 break;
             }
@@ -1389,8 +1388,7 @@ __global__ void __launch_bounds__(PC_TPB) k_n4_pcg(PcgArgs A) {
             double kd = (double)pc_k0(m, jb);
             for (uint32_t s = 0; s < l; ++s, kd += 1.0) pc_step(kd, A.P[(size_t)s * NB + jb], mu, sig);
         }
-        const float sd = (float)sqrt((double)sig / ((double)n - 1.0));
-        A.st[A.b].conv_w = sd / mu;
+        A.st[A.b].conv_w = itk_conv(mu, sig, n);
     }
 }
 

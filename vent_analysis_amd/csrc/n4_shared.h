@@ -459,24 +459,40 @@ __device__ __forceinline__ bool r3_bin_min(const Range3 &r, const float *u, int 
 }
 
 // ---------------------------------------------------------------------------------------------
-// S7 convergence (conv_mode 0): ITK's float Welford recurrence over the masked voxels in raster
-// order, d_k = B_old - B_new read from a raster-ordered buffer.  Three waves of one workgroup:
-//   producers (C, several waves): per block of 64 steps, all lanes compute p = (float)exp((double)d),
-//     1/k, the mu step constants (1 - 1/k, p/k) and (k-1)/k into the block's LDS slot;
-//   wave A (mu): lane 0 runs (pipelined, chain_block64)
-//       mu <- (float)fma((double)mu, 1 - 1/k, (double)(p / k))      (one step per voxel)
-//     recording mu before each step for wave B.
-//   wave B (sig): per block, all lanes form s = (p - mu_prev)^2 (float); lane 0 runs
-//       sig <- (float)fma((double)s, (k-1)/k, (double)sig)          (k >= 2)
-// The recurrences are inherently serial (the float running mean drifts); the slot ring and three
-// LDS counters let the three waves overlap (A and B then do nothing but their steps).  Result: conv = (float)sqrt(sig / (n-1)) / mu.
+// S7 convergence (conv_mode 0): ITK's convergence measure (itkN4BiasFieldCorrectionImageFilter
+// CalculateConvergenceMeasurement, RealType = float) over the masked voxels in raster order,
+// d_k = B_old - B_new:
+//   N += 1.0                                   float counter: exact up to 2^24, then frozen (itk_Nd)
+//   p = (float)exp((double)d)
+//   sig <- (float)((double)sig + ((double)sqr(p - mu) * (N - 1.0)) / N)      (N > 1)
+//   mu  <- (float)((double)mu * (1.0 - 1.0 / N) + (double)(p / N))           (p / N: float division)
+//   conv = (float)sqrt((double)sig / (N - 1.0)) / mu
+// every right-hand side in double with ITK's separate roundings (oracle/n4_oracle.c conv_welford).
+// The state is a serial float recurrence (the float running mean drifts) that must be evaluated in
+// raster order.  It is run either by PC (guess and verify, below: the default) or by this serial
+// chain (ST_PC 0 / VH_N4_SERIAL_CHAIN, A/B and the equivalence test): waves of one workgroup over a
+// ring of 64-step blocks:
+//   producers (several waves): per block, all lanes compute p, a = RN(1 - RN(1/N)),
+//     b = RN_f(p / N) and N into the block's LDS slot;
+//   wave A (mu): the 64 steps mu <- (float)(RN(mu a) + b), systolic (chain_sys64), recording mu
+//     before each step for wave B;
+//   wave B (sig): lanes form t = RN(RN(sqr(p - mu_prev) (N - 1)) / N) in parallel (the product is
+//     exact: 24 x 24 bits), then the 64 steps sig <- (float)(sig + t), systolic.
 // ---------------------------------------------------------------------------------------------
+#define ITK_NMAX 16777216.0   // 2^24: float N += 1.0 stops growing there (2^24 + 1 rounds to 2^24)
+__device__ __forceinline__ double itk_Nd(double k) { return fmin(k, ITK_NMAX); }
+// the measure from the final state after n steps
+__device__ __forceinline__ float itk_conv(float mu, float sig, int64_t n) {
+    const float sd = (float)sqrt((double)sig / (itk_Nd((double)n) - 1.0));
+    return sd / mu;
+}
+
 #ifndef CH_SLOTS
 #define CH_SLOTS 16
 #endif
 struct ChainSlot {
-    double2 ab[64];    // (1 - 1/k, p / k) for wave A; (1, 0) past the end (a no-op step)
-    double2 cs[64];    // ((k - 1) / k, (double)(p - mu_prev)^2): c by the producer, s by wave B
+    double2 ab[64];    // (RN(1 - RN(1/N)), RN_f(p / N)) for wave A; (1, 0) past the end (a no-op step)
+    double nd[64];     // N of the step (double)
     float p[64];
     float mu[64];      // mu before step k
     int ready;         // block + 1 once a producer has filled the slot for that block
@@ -489,15 +505,9 @@ struct ChainSlot {
 // SIMD w % 4), and a producer's VALU instruction in flight on wave A's SIMD delays A's next
 // dependent step however A is prioritised.  So wave 0 (A) and wave 1 (B) keep SIMDs 0 and 1 to
 // themselves and the producers are the waves on SIMDs 2 and 3.  Producer index of wave w, or -1.
-#ifndef CH_SIMD_ROLES
-#define CH_SIMD_ROLES 1
-#endif
-__device__ __forceinline__ int chain_prod_id(int w) {
-    if (!CH_SIMD_ROLES) return w >= 2 ? w - 2 : -1;
-    return (w & 3) >= 2 ? (w >> 2) * 2 + (w & 1) : -1;
-}
+__device__ __forceinline__ int chain_prod_id(int w) { return (w & 3) >= 2 ? (w >> 2) * 2 + (w & 1) : -1; }
 // waves a workgroup needs for np producers
-constexpr int chain_waves(int np) { return CH_SIMD_ROLES ? 4 * ((np + 1) / 2) : 2 + np; }
+constexpr int chain_waves(int np) { return 4 * ((np + 1) / 2); }
 struct ChainState {
     int a_done, b_done, c_done;   // blocks finished by wave A / wave B / the producer
     float mu, conv;
@@ -531,138 +541,11 @@ __device__ __forceinline__ void lds_store_rel(int *p, int v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-// ---- the 64 serial steps of one block on lane 0, software-pipelined -------------------------
-// The step operands are 64 double2 in LDS; they are read in groups of 8 (ds_read_b128), group g+1
-// issued before group g's steps, with an explicit lgkmcnt wait tied to the group's registers (the
-// compiler otherwise batches all reads behind one full wait: ~31 -> ~53 cycles per step measured,
-// scripts/microbench/chain_fast.hip).  MU: x <- (float)fma(x, q.x, q.y), recording x before each
-// step as float (two b128 writes per group at mbase); SIG: x <- (float)fma(q.y, q.x, x).
-// LDS addresses are the low 32 bits of the generic address of a __shared__ object.  The read
-// outputs are early-clobber: a data register that doubled as the address would be overwritten by
-// an early return while later reads of the same statement still use it (seen in n4_study).
-typedef double ch_d2 __attribute__((ext_vector_type(2)));
-typedef float ch_f4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ uint32_t lds_addr(const void *p) { return (uint32_t)(uintptr_t)p; }
-
-#define CH_RD8(q, base, g)                                                                         \
-    asm volatile("ds_read_b128 %0, %8 offset:%9\n\t"                                               \
-                 "ds_read_b128 %1, %8 offset:%10\n\t"                                              \
-                 "ds_read_b128 %2, %8 offset:%11\n\t"                                              \
-                 "ds_read_b128 %3, %8 offset:%12\n\t"                                              \
-                 "ds_read_b128 %4, %8 offset:%13\n\t"                                              \
-                 "ds_read_b128 %5, %8 offset:%14\n\t"                                              \
-                 "ds_read_b128 %6, %8 offset:%15\n\t"                                              \
-                 "ds_read_b128 %7, %8 offset:%16"                                                  \
-                 : "=&v"(q[0]), "=&v"(q[1]), "=&v"(q[2]), "=&v"(q[3]), "=&v"(q[4]),               \
-                   "=&v"(q[5]), "=&v"(q[6]), "=&v"(q[7])                                           \
-                 : "v"(base), "i"(128 * (g)), "i"(128 * (g) + 16), "i"(128 * (g) + 32),             \
-                   "i"(128 * (g) + 48), "i"(128 * (g) + 64), "i"(128 * (g) + 80),                   \
-                   "i"(128 * (g) + 96), "i"(128 * (g) + 112)                                      \
-                 : "memory")
-
-#define CH_RD4(q, base, off)                                                                       \
-    asm volatile("ds_read_b128 %0, %4 offset:%5\n\t"                                               \
-                 "ds_read_b128 %1, %4 offset:%6\n\t"                                              \
-                 "ds_read_b128 %2, %4 offset:%7\n\t"                                              \
-                 "ds_read_b128 %3, %4 offset:%8"                                                    \
-                 : "=&v"(q[0]), "=&v"(q[1]), "=&v"(q[2]), "=&v"(q[3])                              \
-                 : "v"(base), "i"(off), "i"((off) + 16), "i"((off) + 32), "i"((off) + 48)           \
-                 : "memory")
-
-template <int N>
-__device__ __forceinline__ void ch_wait(ch_d2 *q) {   // N LDS ops may still be in flight
-    asm volatile("s_waitcnt lgkmcnt(%8)"
-                 : "+v"(q[0]), "+v"(q[1]), "+v"(q[2]), "+v"(q[3]), "+v"(q[4]), "+v"(q[5]),
-                   "+v"(q[6]), "+v"(q[7])
-                 : "i"(N)
-                 : "memory");
-}
-template <int N>
-__device__ __forceinline__ void ch_wait4(ch_d2 *q) {
-    asm volatile("s_waitcnt lgkmcnt(%4)"
-                 : "+v"(q[0]), "+v"(q[1]), "+v"(q[2]), "+v"(q[3])
-                 : "i"(N)
-                 : "memory");
-}
-
-// GS = 8: groups of 8 steps (64 VGPRs of operands in flight); GS = 4: groups of 4 (32 VGPRs),
-// for the volume-resident kernel whose register budget would otherwise spill inside the loop.
-template <bool MU, int GS, int G>
-__device__ __forceinline__ void ch_group(uint32_t base, uint32_t mbase, double &x, ch_d2 *cur,
-                                         ch_d2 *nxt) {
-    constexpr int NG = 64 / GS;
-    // MU writes 8 / GS b128 records per group (one per 4 steps)
-    constexpr int WPG = MU ? GS / 4 : 0;
-    if constexpr (G < NG - 1) {
-        if constexpr (GS == 8) {
-            CH_RD8(nxt, base, G + 1);
-            ch_wait<G == 0 ? 8 : 8 + WPG>(cur);
-        } else {
-            CH_RD4(nxt, base, 64 * (G + 1));
-            ch_wait4<G == 0 ? 4 : 4 + WPG>(cur);
-        }
-    } else {
-        if constexpr (GS == 8) ch_wait<WPG>(cur);
-        else ch_wait4<WPG>(cur);
-    }
-    if constexpr (MU) {
-        float mr[GS];
-#pragma unroll
-        for (int i = 0; i < GS; ++i) {
-            mr[i] = (float)x;
-            x = (double)(float)fma(x, cur[i].x, cur[i].y);
-        }
-#pragma unroll
-        for (int h = 0; h < GS / 4; ++h) {
-            const ch_f4 w = {mr[4 * h], mr[4 * h + 1], mr[4 * h + 2], mr[4 * h + 3]};
-            asm volatile("ds_write_b128 %0, %1 offset:%2"
-                         :
-                         : "v"(mbase), "v"(w), "i"(4 * GS * G + 16 * h)
-                         : "memory");
-        }
-    } else {
-#pragma unroll
-        for (int i = 0; i < GS; ++i) x = (double)(float)fma(cur[i].y, cur[i].x, x);
-    }
-    if constexpr (G < NG - 1) ch_group<MU, GS, G + 1>(base, mbase, x, nxt, cur);
-}
-
-#ifndef CH_ASM
-#define CH_ASM 1
-#endif
-template <bool MU, int GS = 8>
-__device__ __forceinline__ double chain_block64(const double2 *q, float *murec, double x) {
-    if constexpr (!CH_ASM) {   // reference form (A/B builds)
-#pragma unroll 4
-        for (int l = 0; l < 64; ++l) {
-            const double2 v = q[l];
-            if (MU) {
-                murec[l] = (float)x;
-                x = (double)(float)fma(x, v.x, v.y);
-            } else {
-                x = (double)(float)fma(v.y, v.x, x);
-            }
-        }
-        return x;
-    }
-    const uint32_t base = lds_addr(q), mbase = MU ? lds_addr(murec) : 0u;
-    ch_d2 qa[GS], qb[GS];
-    if constexpr (GS == 8) CH_RD8(qa, base, 0);
-    else CH_RD4(qa, base, 0);
-    ch_group<MU, GS, 0>(base, mbase, x, qa, qb);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    return x;
-}
-
-// Producer wave (C): per block of 64 steps, all lanes compute p = (float)exp((double)d), 1/k,
-// the mu step constants (1 - 1/k, p / k) and (k - 1) / k into the block's LDS slot, up to CH_SLOTS
-// blocks ahead of wave B.  The n d values are in raster order: Dr[k] (perm == nullptr), else
-// Dr[perm[k]]; a block's values are loaded CH_PF blocks ahead (its perm entries 2 CH_PF ahead).
-// np producer waves share the blocks round-robin (producer pid takes blk = pid mod np): one wave
-// took ~3.3k cycles per block (its global loads wait at every hand-off), several keep the serial
-// waves fed.  Each prefetches its next block's d (and perm entries two blocks ahead) while it
-// processes the current one.
+// Producer wave: per block of 64 steps, all lanes compute p = (float)exp((double)d), the mu step
+// constants (a, b) and N into the block's LDS slot, up to CH_SLOTS blocks ahead of wave B.  The n
+// d values are in raster order: Dr[k] (perm == nullptr), else Dr[perm[k]].  np producer waves
+// share the blocks round-robin (producer pid takes blk = pid mod np); each prefetches its next
+// block's d (and perm entries two blocks ahead) while it processes the current one.
 template <int NS = CH_SLOTS>
 __device__ void chain_wave_prod(const float *Dr, const int32_t *perm, int64_t n, ChainSlot *slots,
                                 ChainState *cs, int pid, int np) {
@@ -690,15 +573,14 @@ __device__ void chain_wave_prod(const float *Dr, const int32_t *perm, int64_t n,
         p1 = ld_perm(blk + 2 * np);
         const bool ok = j < n;
         const float p = expf_cr(d);
-        const double kd = (double)(j + 1);
-        const double r = 1.0 / kd;
-        const double2 ab = ok ? make_double2(1.0 - r, (double)(float)((double)p * r))   // p / k, div_r form
+        const double N = itk_Nd((double)(j + 1));
+        const double r = 1.0 / N;
+        const double2 ab = ok ? make_double2(1.0 - r, (double)(float)((double)p * r))   // p / N, div_r form
                               : make_double2(1.0, 0.0);
-        const double c = (kd - 1.0) / kd;
         if (blk >= NS + bseen)
             CH_WAIT(wt, while ((bseen = lds_load_acq(&cs->b_done)) <= (int)(blk - NS)) __builtin_amdgcn_s_sleep(1));
         S.ab[lane] = ab;
-        S.cs[lane] = make_double2(c, 0.0);
+        S.nd[lane] = N;
         S.p[lane] = p;
         wave_lds_order();
         if (lane == 0) lds_store_rel(&S.ready, (int)(blk + 1));
@@ -718,18 +600,15 @@ __device__ __forceinline__ void chain_reset(ChainSlot *slots, ChainState *cs, in
     }
 }
 
-// ---- the 64 serial steps of one block, systolic (CH_SYS, the default) ---------------------------
+// ---- the 64 serial steps of one block, systolic ------------------------------------------------
 // Lane j holds step j's constants (one LDS read of the block by all lanes).  Every tick all lanes
 // take the float x of lane j - 1 (DPP wave_shr:1; lane 0, which has no source lane, keeps the
 // carried-in x) and apply their own step.  After tick t lanes 0..t hold the chain's values and keep
 // them (their inputs no longer change), so after 64 ticks lane j holds x after step j, and the
-// shifted copy holds x before it.  4 VALU per step (DPP move, cvt, fma, cvt) and no LDS access:
-// the lane-0 form above needs an LDS read per step, which the other waves' LDS traffic delays.
-// MU: x <- (float)fma(x, q0, q1); SIG: x <- (float)fma(q1, q0, x).  xin is wave-uniform; returns
-// lane 63's x (wave-uniform); rec = x before the lane's step.
-#ifndef CH_SYS
-#define CH_SYS 1
-#endif
+// shifted copy holds x before it.  No LDS access on the chain.
+// MU: x <- (float)(RN(x q0) + q1) (mul, add: ITK's two roundings); SIG: x <- (float)(x + q1) (q0
+// is 1, or 0 with q1 = 0 for a no-op step: fma(q1, q0, x) is then the plain sum).  xin is
+// wave-uniform; returns lane 63's x (wave-uniform); rec = x before the lane's step.
 template <bool MU>
 __device__ __forceinline__ float chain_sys64(double q0, double q1, float xin, float &rec) {
     float xf = xin, xs = xin;
@@ -739,7 +618,8 @@ __device__ __forceinline__ float chain_sys64(double q0, double q1, float xin, fl
                      "s_nop 1\n\t"   // VALU write -> DPP read: 2 wait states
                      "v_mov_b32_dpp %1, %0 wave_shr:1 row_mask:0xf bank_mask:0xf\n\t"
                      "v_cvt_f64_f32 %2, %1\n\t"
-                     "v_fma_f64 %2, %2, %3, %4\n\t"
+                     "v_mul_f64 %2, %2, %3\n\t"
+                     "v_add_f64 %2, %2, %4\n\t"
                      "v_cvt_f32_f64 %0, %2\n\t"
                      ".endr"
                      : "+v"(xf), "+v"(xs), "=&v"(x)
@@ -757,57 +637,6 @@ __device__ __forceinline__ float chain_sys64(double q0, double q1, float xin, fl
     rec = xs;
     return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xf), 63));
 }
-
-// (A fused form -- the shift riding on v_cvt_f64_f32_dpp wave_shr:1, 3 VALU per step -- does not
-// assemble: gfx950's DP-ALU DPP accepts only row_newbcast.)
-// Row form (CH_SYS 2): the 64 steps as 4 rows of 16 lanes taken one after the other (EXEC = the
-// row).  Inside a row the move rides on the cvt (DPP row_newbcast:k gives every lane of the row
-// lane k's x: 3 VALU per step); the first step of a row takes lane 15 of the row before
-// (row_bcast:15) or, in row 0, the carried-in x.  Lanes outside the row keep their values.
-#define CH_ROW_TICKS(FMA)                                                                          \
-    "s_nop 4\n\t"                                                                               \
-    "v_cvt_f64_f32 %2, %1\n\t" FMA "v_cvt_f32_f64 %0, %2\n\t"                                  \
-    ".irp k, 0,1,2,3,4,5,6,7,8,9,10,11,12,13,14\n\t"                                            \
-    "s_nop 1\n\t"                                                                               \
-    "v_cvt_f64_f32_dpp %2, %0 row_newbcast:\\k row_mask:0xf bank_mask:0xf\n\t" FMA             \
-    "v_cvt_f32_f64 %0, %2\n\t"                                                                   \
-    ".endr\n\t"
-#define CH_ROWS(FMA)                                                                               \
-    "s_mov_b64 %3, exec\n\t"                                                                     \
-    "s_mov_b32 exec_lo, 0xffff\n\t"                                                              \
-    "s_mov_b32 exec_hi, 0\n\t" CH_ROW_TICKS(FMA)                                                  \
-    "s_mov_b32 exec_lo, 0xffff0000\n\t"                                                          \
-    "s_nop 4\n\t"                                                                               \
-    "v_mov_b32_dpp %1, %0 row_bcast:15 row_mask:0xf bank_mask:0xf\n\t" CH_ROW_TICKS(FMA)         \
-    "s_mov_b32 exec_lo, 0\n\t"                                                                   \
-    "s_mov_b32 exec_hi, 0xffff\n\t"                                                              \
-    "s_nop 4\n\t"                                                                               \
-    "v_mov_b32_dpp %1, %0 row_bcast:15 row_mask:0xf bank_mask:0xf\n\t" CH_ROW_TICKS(FMA)         \
-    "s_mov_b32 exec_hi, 0xffff0000\n\t"                                                          \
-    "s_nop 4\n\t"                                                                               \
-    "v_mov_b32_dpp %1, %0 row_bcast:15 row_mask:0xf bank_mask:0xf\n\t" CH_ROW_TICKS(FMA)         \
-    "s_mov_b64 exec, %3\n\t"
-template <bool MU>
-__device__ __forceinline__ float chain_rows64(double q0, double q1, float xin, float &rec) {
-    float xf = xin, xs = xin;
-    double x;
-    uint64_t sv;
-    if (MU)
-        asm volatile(CH_ROWS("v_fma_f64 %2, %2, %4, %5\n\t")
-                     : "+v"(xf), "+v"(xs), "=&v"(x), "=&s"(sv)
-                     : "v"(q0), "v"(q1));
-    else
-        asm volatile(CH_ROWS("v_fma_f64 %2, %5, %4, %2\n\t")
-                     : "+v"(xf), "+v"(xs), "=&v"(x), "=&s"(sv)
-                     : "v"(q0), "v"(q1));
-    // x before each lane's step: lane j - 1's x (lane 0: the carried-in x)
-    float r = xin;
-    asm volatile("s_nop 1\n\tv_mov_b32_dpp %0, %1 wave_shr:1 row_mask:0xf bank_mask:0xf"
-                 : "+v"(r) : "v"(xf));
-    rec = r;
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xf), 63));
-}
-
 // ---- S7 by guess and verify ("PC") ------------------------------------------------------------
 // The recurrence is serial, but one step is cheap to *check*: given the float state before a step,
 // the state after it is a pure function of that state and the step's inputs.  So the n steps are cut
@@ -823,10 +652,12 @@ __device__ __forceinline__ float chain_rows64(double q0, double q1, float xin, f
 // so the exact prefix grows every round; after PC_RMAX rounds the rest runs serially from the
 // first mismatch.  Measured on the bench studies' d sequences: 6 - 21 rounds (scripts/dev/pc_sim.c).
 //
-// Step arithmetic is that of the serial chain (chain_wave_prod / _mu / _sig) with the two divisions
-// replaced by exact equivalents: r = RN(1/k) by rcp and two Newton steps (pc_rcp), and
-// c = RN((k-1)/k) = RN(1 - 1/k) from r, the exact residual 1 - k r and Fast2Sum(1, -r) (pc_step).
-// Both were checked bit-exact against IEEE division for every k < 2^25 (scripts/microbench/recip_exact.hip).
+// Step arithmetic is that of the serial chain (chain_wave_prod / _mu / _sig, ITK's roundings) with
+// the two divisions replaced by exact equivalents: r = RN(1/N) by rcp and two Newton steps
+// (pc_rcp, checked bit-exact against IEEE division for every N < 2^25 by
+// scripts/microbench/recip_exact.hip), and RN(Q / N) by Markstein's correction y + r (Q - N y)
+// from y = RN(Q r) (pc_div: y is faithful and r correctly rounded, so the corrected quotient is
+// the correctly rounded one; tests/test_n4_oracle.py checks it against IEEE division).
 //
 // Layout of the step inputs: block j holds steps [k0_j, k0_j + len_j) (1-based), len_j = L + (j < rem),
 // L = n / NL, rem = n % NL; step s of block j lives at s NL + j, so one wave-wide load reads 64
@@ -870,7 +701,7 @@ __device__ __forceinline__ uint32_t pc_addr(uint32_t r, const PcMap &m) {
 __device__ __forceinline__ uint32_t pc_len(const PcMap &m, uint32_t j) { return m.L + (j < m.rem ? 1u : 0u); }
 __device__ __forceinline__ uint32_t pc_k0(const PcMap &m, uint32_t j) { return j * m.L + min(j, m.rem) + 1u; }
 
-// RN(1 / k) for an integer k < 2^25: rcp, then two Newton steps with exact fma residuals
+// RN(1 / N) for an integer N < 2^25: rcp, then two Newton steps with exact fma residuals
 __device__ __forceinline__ double pc_rcp(double kd) {
     double y = __builtin_amdgcn_rcp(kd);
     double e = fma(-kd, y, 1.0);
@@ -878,28 +709,34 @@ __device__ __forceinline__ double pc_rcp(double kd) {
     e = fma(-kd, y, 1.0);
     return fma(y, e, y);
 }
-// the constants of step k (= kd): A = 1 - 1/k and B = p / k as chain_wave_prod forms them (div_r
-// form, r = RN(1/k)), c = RN((k - 1) / k) = RN(1 - 1/k)
+// RN(Q / N) from r = RN(1 / N) (Markstein): y = RN(Q r) is within an ulp of Q / N, the residual
+// Q - N y is exact by fma, and RN(y + r (Q - N y)) is the correctly rounded quotient
+__device__ __forceinline__ double pc_div(double Q, double N, double r) {
+    const double y = Q * r;
+    const double e = fma(-N, y, Q);
+    return fma(e, r, y);
+}
+// the constants of step k (kd = k, N = itk_Nd(k)): A = RN(1 - RN(1/N)) and B = RN_f(p / N) as
+// chain_wave_prod forms them (div_r form, r = RN(1/N)), and N, r for sig's RN(Q / N)
 struct PcK {
-    double A, B, c;
+    double A, B, N, r;
 };
 __device__ __forceinline__ PcK pc_consts(double kd, float p) {
     PcK q;
-    const double r = pc_rcp(kd);
-    q.A = 1.0 - r;
-    q.B = (double)(float)((double)p * r);
-    const double z = q.A - 1.0, err = -r - z;   // 1 - r = A + err exactly (Fast2Sum)
-    const double res = fma(-kd, r, 1.0);        // 1 - k r exactly: 1/k = r + res / k
-    q.c = q.A + fma(-res, r, err);
+    q.N = itk_Nd(kd);
+    q.r = pc_rcp(q.N);
+    q.A = 1.0 - q.r;
+    q.B = (double)(float)((double)p * q.r);
     return q;
 }
-// one step on the float state (mu, sig); sig is untouched at k = 1 (ITK's N > 1 test)
+// one step on the float state (mu, sig) with ITK's roundings; sig is untouched at k = 1 (N > 1);
+// the sig product sqr(p - mu) (N - 1) is exact in double (24-bit by at most 24-bit integers)
 __device__ __forceinline__ void pc_apply(const PcK &q, float p, bool first, float &mu, float &sig) {
     if (!first) {
         const float d = p - mu;
-        sig = (float)fma((double)(d * d), q.c, (double)sig);
+        sig = (float)__dadd_rn((double)sig, pc_div((double)(d * d) * (q.N - 1.0), q.N, q.r));
     }
-    mu = (float)fma((double)mu, q.A, q.B);
+    mu = (float)__dadd_rn(__dmul_rn((double)mu, q.A), q.B);
 }
 __device__ __forceinline__ void pc_step(double kd, float p, float &mu, float &sig) {
     pc_apply(pc_consts(kd, p), p, kd == 1.0, mu, sig);
@@ -1172,7 +1009,8 @@ __device__ __forceinline__ void pc_block_apx(const float *P, uint32_t j, uint32_
     float cur[8], nxt[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) cur[i] = (uint32_t)i < len ? P[(size_t)i * nl + j] : 0.0f;
-    float kf = (float)k0;
+    // N of the group's first step: min(k, 2^24), exact in float (ITK's frozen float counter)
+    float kf = fminf((float)k0, (float)ITK_NMAX);
     const float e0 = fmaf(__builtin_amdgcn_rcpf(kf), 0x1p-39f, 0x1p-44f);   // covers every step's r0
     uint32_t s0 = 0;
     for (; s0 + 8 <= len; s0 += 8) {
@@ -1181,7 +1019,8 @@ __device__ __forceinline__ void pc_block_apx(const float *P, uint32_t j, uint32_
         PcKf q[8];
 #pragma unroll
         for (int i = 0; i < 8; i += 2)
-            pc_kf2(kf + (pc_f2){(float)i, (float)(i + 1)}, (pc_f2){cur[i], cur[i + 1]}, q[i], q[i + 1]);
+            pc_kf2(__builtin_elementwise_min(kf + (pc_f2){(float)i, (float)(i + 1)}, (pc_f2)(float)ITK_NMAX),
+                   (pc_f2){cur[i], cur[i + 1]}, q[i], q[i + 1]);
         const float mu0 = mu, sig0 = sig;
         bool ok = pc_apx_step<SIG>(q[0], e0, cur[0], kf == 1.0f, mu, sig);
 #pragma unroll
@@ -1193,11 +1032,11 @@ __device__ __forceinline__ void pc_block_apx(const float *P, uint32_t j, uint32_
 #pragma unroll 1
             for (int i = 0; i < 8; ++i, kd += 1.0) pc_step(kd, cur[i], mu, sig);
         }
-        kf += 8.0f;
+        kf = fminf(kf + 8.0f, (float)ITK_NMAX);   // exact below 2^24, clamped above
 #pragma unroll
         for (int i = 0; i < 8; ++i) cur[i] = nxt[i];
     }
-    double kd = (double)kf;
+    double kd = (double)kf;   // = N of the next step (pc_step clamps again past 2^24)
 #pragma unroll
     for (int i = 0; i < 7; ++i)   // the tail: exact steps
         if (s0 + i < len) {
@@ -1335,6 +1174,8 @@ __device__ void pcw_update(PcShared<NL> &S, const PcMap &m, int round, int req, 
 #define PC_APASS 2   // phase-A stages; 1 = mu alone, then straight to the exact rounds (measured 7.56k
                      // against 8.02k vol/s: sig then takes several of the dearer exact rounds)
 #endif
+// the done / fallback tags are 4 req + stage: phase-A stages 0 .. PC_APASS - 1, phase B 2
+static_assert(PC_APASS >= 1 && PC_APASS <= 2, "PC_APASS: 1 or 2 phase-A stages (tag 2 is phase B's)");
 #ifndef PC_AMAX
 #define PC_AMAX 40
 #endif
@@ -1437,9 +1278,8 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
         }
     }
     if (tid == 0) {
-        const float sd = (float)sqrt((double)S.sig / ((double)n - 1.0));
         ch.mu = S.mu;
-        ch.conv = sd / S.mu;
+        ch.conv = itk_conv(S.mu, S.sig, n);
 #ifdef PC_PROF
         if (blockIdx.x == 0)
             printf("PCW_PROF n %lld roundsA %d roundsB %d fallback %d pass0 %llu A %llu (blocks %llu) B %llu\n",
@@ -1449,97 +1289,25 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
 }
 
 
-// ---- block steps that skip work the float arithmetic makes redundant (CH_SKIP) -----------------
-// mu: late in a chain the float running mean mostly stays put (|p - mu| / k below half an ulp: in
-// the bench studies' last 20 iterations 4-13 % of the steps change it).  Every lane evaluates its
-// step from the current mu exactly (the spec's fma and roundings); the first lane whose result
-// differs is the next change, the lanes before it leave mu as it is.  One dependent round per
-// change instead of one per step; a block whose predecessor changed mu more than CH_SKIP_MAX times
-// takes the systolic form.  Bit-identical by construction (every step is the exact step applied to
-// the exact state).  rec = mu before the lane's step.  Measured on the 256-study bench (serial
-// chains, ST_PC 0): mu skip 60.7 ms, sig blocks 66.2 ms, both 69.7 ms against 54.1 ms systolic --
-// one skip round (convert, f64 fma, convert, compare, ballot, find-first, readlane) is a dependent
-// chain about twice a systolic step, and too few steps stagnate on whole blocks; kept opt-in.
-#ifndef CH_SKIP
-#define CH_SKIP 0   // bit 0: mu skip, bit 1: sig block (opt-in: measured slower, see above)
-#endif
-#ifndef CH_SKIP_MAX
-#define CH_SKIP_MAX 24
-#endif
-__device__ __forceinline__ float chain_mu_skip(double q0, double q1, float m, float &rec, int &changes) {
-    const int lane = threadIdx.x & 63;
-    uint64_t pending = ~0ull;
-    changes = 0;
-    for (;;) {
-        const float cand = (float)fma((double)m, q0, q1);
-        const uint64_t chg = __ballot(cand != m) & pending;
-        if (!chg) {
-            if ((pending >> lane) & 1ull) rec = m;
-            return m;
-        }
-        const int j0 = __ffsll((unsigned long long)chg) - 1;
-        const uint64_t upto = (j0 == 63) ? ~0ull : ((2ull << j0) - 1ull);
-        if (((pending & upto) >> lane) & 1ull) rec = m;
-        m = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cand), j0));
-        pending &= ~upto;
-        ++changes;
-        if (!pending) return m;
-    }
-}
-// sig: inside one binade [2^e, 2^(e+1)) a float step adds RN(sig + t) - sig, the same amount for
-// every sig of the binade (the double rounding of sig + t is anchored on sig's own grid, whose low
-// 29 bits are zero; only an exact float tie would depend on sig's last bit).  So the block's 64
-// increments are taken from the block's first state sig0 in parallel and summed exactly (multiples
-// of ulp(sig0)).  Valid when sig0 > 0, no step lands on an exact tie, and the sum stays in sig0's
-// binade (the steps only add); otherwise the caller runs the block serially.  Returns false then.
-__device__ __forceinline__ bool chain_sig_block(double q0, double q1, float sig0, float &sig_end) {
-    if (!(sig0 > 0.0f)) return false;
-    const double y = fma(q1, q0, (double)sig0);           // q1 = s (or 0), q0 = (k - 1) / k (or 0)
-    const uint64_t yb = (uint64_t)__double_as_longlong(y);
-    const bool tie = (yb & 0x1fffffffull) == 0x10000000ull;
-    const float inc = (float)y - sig0;                     // exact: same binade (checked below)
-    double sum = (double)inc;
-    for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off, 64);
-    if (__ballot(tie) != 0ull) return false;
-    const double e = (double)sig0 + sum;
-    const float ef = (float)e;
-    const int b0 = (__float_as_int(sig0) >> 23) & 0xff, b1 = (__float_as_int(ef) >> 23) & 0xff;
-    if (b0 != b1 || (double)ef != e) return false;
-    sig_end = ef;
-    return true;
-}
-
 // wave A: the mu recurrence, block by block as the producers fill them.
-template <int GS = 8, int NS = CH_SLOTS>
+template <int NS = CH_SLOTS>
 __device__ void chain_wave_mu(int64_t n, ChainSlot *slots, ChainState *cs) {
     const int lane = threadIdx.x & 63;
-    double mu = 0.0;
     const int64_t nblk = (n + 63) / 64;
     unsigned long long wt = 0;
     __builtin_amdgcn_s_setprio(CH_PRIO);   // the serial waves win issue arbitration on their SIMD
     CH_T0();
     float muf = 0.0f;
-    int last_changes = 64;   // the first block (k from 1) moves mu at nearly every step
     for (int64_t blk = 0; blk < nblk; ++blk) {
         ChainSlot &S = slots[blk % NS];
         CH_WAIT(wt, while (lds_load_acq(&S.ready) != (int)(blk + 1)) __builtin_amdgcn_s_sleep(1));
-        if (CH_SYS) {
-            const double2 q = S.ab[lane];
-            float rec;
-            if ((CH_SKIP & 1) && last_changes <= CH_SKIP_MAX)
-                muf = chain_mu_skip(q.x, q.y, muf, rec, last_changes);
-            else {
-                muf = CH_SYS == 2 ? chain_rows64<true>(q.x, q.y, muf, rec) : chain_sys64<true>(q.x, q.y, muf, rec);
-                last_changes = __popcll(__ballot(rec != __shfl_down(rec, 1, 64)));   // changes seen
-            }
-            S.mu[lane] = rec;
-            mu = (double)muf;
-        } else if (lane == 0) {
-            mu = chain_block64<true, GS>(S.ab, S.mu, mu);
-        }
+        const double2 q = S.ab[lane];
+        float rec;
+        muf = chain_sys64<true>(q.x, q.y, muf, rec);
+        S.mu[lane] = rec;
         wave_lds_order();
         if (lane == 0) {
-            if (blk == nblk - 1) cs->mu = (float)mu;   // published by the release below
+            if (blk == nblk - 1) cs->mu = muf;   // published by the release below
             lds_store_rel(&cs->a_done, (int)(blk + 1));
         }
     }
@@ -1548,10 +1316,10 @@ __device__ void chain_wave_mu(int64_t n, ChainSlot *slots, ChainState *cs) {
 }
 
 // wave B.  Returns conv in cs->conv.
-template <int GS = 8, int NS = CH_SLOTS>
+template <int NS = CH_SLOTS>
 __device__ void chain_wave_sig(int64_t n, ChainSlot *slots, ChainState *cs) {
     const int lane = threadIdx.x & 63;
-    double sig = 0.0;
+    float sig = 0.0f;
     const int64_t nblk = (n + 63) / 64;
     unsigned long long wt = 0;
     __builtin_amdgcn_s_setprio(CH_PRIO);
@@ -1561,24 +1329,13 @@ __device__ void chain_wave_sig(int64_t n, ChainSlot *slots, ChainState *cs) {
         const int64_t j = blk * 64 + lane;
         CH_WAIT(wt, while (lds_load_acq(&cs->a_done) <= (int)blk) __builtin_amdgcn_s_sleep(1));
         const float q = S.p[lane] - S.mu[lane];
+        const double N = S.nd[lane];
+        const double t = ((double)(q * q) * (N - 1.0)) / N;   // IEEE double division
         // k = 1 adds nothing (ITK's N > 1 test), nor do the steps past the end: (0, 0) is a no-op
         const bool ok = j < n && j > 0;
-        if (CH_SYS) {
-            const double c = S.cs[lane].x;
-            float rec;
-            const double q0 = ok ? c : 0.0, q1 = ok ? (double)(q * q) : 0.0;
-            float se;
-            if ((CH_SKIP & 2) && chain_sig_block(q0, q1, (float)sig, se))
-                sig = (double)se;
-            else
-                sig = (double)(CH_SYS == 2 ? chain_rows64<false>(q0, q1, (float)sig, rec)
-                                           : chain_sys64<false>(q0, q1, (float)sig, rec));
-            (void)rec;
-        } else {
-            S.cs[lane] = ok ? make_double2(S.cs[lane].x, (double)(q * q)) : make_double2(0.0, 0.0);
-            wave_lds_order();
-            if (lane == 0) sig = chain_block64<false, GS>(S.cs, nullptr, sig);
-        }
+        float rec;
+        sig = chain_sys64<false>(ok ? 1.0 : 0.0, ok ? t : 0.0, sig, rec);
+        (void)rec;
         wave_lds_order();
         if (lane == 0) lds_store_rel(&cs->b_done, (int)(blk + 1));
     }
@@ -1586,8 +1343,6 @@ __device__ void chain_wave_sig(int64_t n, ChainSlot *slots, ChainState *cs) {
     __builtin_amdgcn_s_setprio(0);
     if (lane == 0) {
         while (lds_load_acq(&cs->a_done) < (int)nblk) __builtin_amdgcn_s_sleep(1);
-        const float mu = cs->mu;
-        const float s = (float)sqrt(sig / ((double)n - 1.0));
-        cs->conv = s / mu;
+        cs->conv = itk_conv(cs->mu, sig, n);
     }
 }

@@ -72,9 +72,6 @@ static_assert(ST_CG == 0 || ST_DEPTH == 1, "compute waves on SIMDs 2 and 3 only 
 constexpr int ST_NG = ST_DEPTH;             // chain groups
 constexpr int ST_CWT = ST_NG * ST_CW;       // chain waves in all
 constexpr int ST_NB = ST_DEPTH + 1;         // U / D ring buffers
-#ifndef ST_CH_GS
-#define ST_CH_GS 8   // convergence-chain group size here (n4_shared.h ch_group): 8 measured 135M vs 167M cycles for 4
-#endif
 
 // ST_PROF builds (scripts/dev/phase_ab.sh): block 0 prints shader cycles per phase at the end
 #ifdef ST_PROF
@@ -768,9 +765,9 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                 if (M.go_op[cg]) break;   // level end
                 const float *const Dk = a.D + M.go_d[cg] * a.half + b * a.VS;
                 if (wl == 0) {
-                    chain_wave_mu<ST_CH_GS, ST_CH_NS>(n, gslots, &M.ch[cg]);
+                    chain_wave_mu<ST_CH_NS>(n, gslots, &M.ch[cg]);
                 } else if (wl == 1) {
-                    chain_wave_sig<ST_CH_GS, ST_CH_NS>(n, gslots, &M.ch[cg]);
+                    chain_wave_sig<ST_CH_NS>(n, gslots, &M.ch[cg]);
                     wave_lds_order();
                     if (lane == 0) lds_store_rel(&M.ch_seq[cg], req);   // after ch.conv
                 } else {

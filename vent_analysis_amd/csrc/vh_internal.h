@@ -112,6 +112,14 @@ struct vh_ctx {
     // context; mu serialises them, so a context may be used from several host threads
     vh_batch *scratch = nullptr;
     std::mutex mu;
+    // last_error is written by any failing entry point (several host threads may fail at once on
+    // one context, and vh_pipe_run does not hold mu): its own lock, and vh_last_error hands out a
+    // per-thread copy
+    mutable std::mutex err_mu;
+    // vh_recon: its own stream and a cached device buffer (input, line transforms, output, twiddles)
+    hipStream_t aux = nullptr;
+    void *recon_buf = nullptr;
+    size_t recon_cap = 0;
 };
 
 struct vh_pipe {
@@ -319,6 +327,8 @@ __device__ inline void snr_block_write(double (&acc)[4], double (*s_red)[VH_TPB 
 // export.hip (rendering after the hot path)
 void vh_overlay_launch(hipStream_t s, const float *d_n4, const uint8_t *d_def, int64_t R, int64_t C,
                        int64_t Z, int64_t nb, uint32_t *d_mm, uint8_t *d_rgb);
+void vh_recon_run(hipStream_t st, const double2 *d_in, double2 *d_tmp, double2 *d_out, double2 *d_tw0,
+                  double2 *d_tw1, int64_t n0, int64_t n1, int64_t nz);
 void vh_montage_run(hipStream_t s, int64_t R, int64_t C, int64_t Z, const void *proton, int p64,
                     const void *hp, int h64, const float *n4, const uint8_t *mborder,
                     const uint8_t *def, const double *ci, const double *parula, int64_t prow,
