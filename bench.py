@@ -336,6 +336,12 @@ def main():
         dt = max_over_ranks(dt, dist)
 
     _, _, _, _, res = Bt.download(n4=False, maps=False)
+    st_us = Bt.study_times()   # per-study wall time of the last step's one-workgroup-per-study N4
+    tail = None
+    if st_us.max() > 0:
+        tail = {"min_us": round(float(st_us.min()), 1), "mean_us": round(float(st_us.mean()), 1),
+                "max_us": round(float(st_us.max()), 1),
+                "max_over_mean": round(float(st_us.max() / st_us.mean()), 4)}
     used_study = args.n4_mode == "study" or (args.n4_mode == "auto" and nb >= 16)
     kernels = {}
     if not args.no_profile:
@@ -391,6 +397,7 @@ def main():
                    "n4_iterations_mean": float(its.sum(axis=1).mean()) if its.size else 0.0},
         "roofline": roof,
         "cpu_baseline": cpu,
+        "n4_study_times": tail,
         "host_to_host_vol_s": round(world * h2h["volumes"] / h2h["seconds"], 2) if h2h else None,
         "host_to_host": h2h,
     }

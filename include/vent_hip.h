@@ -159,6 +159,11 @@ int vh_batch_reset_timers(vh_batch *b);
 int vh_batch_kernel_time(vh_batch *b, const char *name, double *total_ms, int64_t *launches,
                          double *bytes_per_launch);
 
+/* Per-study wall time (microseconds, device wall clock) of the last vh_batch_run's volume-resident
+ * N4 kernel (one workgroup per study: the slowest study bounds the launch); zeros when that run did
+ * not use it.  us[batch]. */
+int vh_batch_study_times(vh_batch *b, double *us);
+
 /* ---- rendering after the hot path ---------------------------------- */
 /* exportDICOM's pixel data (Vent_Analysis.py:387-393): BW = uint8(normalize(|N4HPvent|) * 255) in
  * float32, RGB = (BW*(defect==0) + 255*(defect==1), BW*(defect==0), BW*(defect==0)).  n4 float32

@@ -6,9 +6,11 @@ exception the reference raises at the same point (SURVEY.md §8b "Errors").
 """
 from __future__ import annotations
 
+import atexit
 import ctypes as ct
 import os
 import threading
+import weakref
 
 import numpy as np
 
@@ -77,6 +79,7 @@ _SIGS = {
     "vh_batch_reset_timers": ([_P], ct.c_int),
     "vh_batch_kernel_time": ([_P, ct.c_char_p, ct.POINTER(ct.c_double), ct.POINTER(ct.c_int64),
                               ct.POINTER(ct.c_double)], ct.c_int),
+    "vh_batch_study_times": ([_P, _P], ct.c_int),
     "vh_overlay": ([_P, _P, _P, _I64, _I64, _I64, _I64, _P], ct.c_int),
     "vh_montage": ([_P, _I64, _I64, _I64, _P, ct.c_int, _P, ct.c_int, _P, _P, _P, _P, _P, _I64, _P,
                     _P], ct.c_int),
@@ -158,6 +161,27 @@ class Context:
 
 
 _ctx = {}
+_live = weakref.WeakSet()   # open Batch / Pipe objects
+
+
+@atexit.register
+def _shutdown():
+    """Destroy the cached contexts (their scratch batches, streams and device buffers) while the HIP
+    runtime -- and a profiler attached to it -- is still fully up.  Left to interpreter teardown,
+    vh_destroy ran in no defined order, possibly after C-level exit handlers had started taking the
+    runtime and rocprofv3 down (SIGSEGV in exit() after profiled cooperative launches)."""
+    with _lock:
+        for o in list(_live):   # batches and pipes first: they hold their context
+            try:
+                o.close()
+            except Exception:
+                pass
+        for c in list(_ctx.values()):
+            try:
+                c.close()
+            except Exception:
+                pass
+        _ctx.clear()
 
 
 def context(device: int = 0) -> Context:
@@ -341,6 +365,7 @@ class Batch:
         self.ctx.check(self.L.vh_batch_create(self.ctx.h, R, C, Z, n, ct.byref(h)),
                        "vh_batch_create")
         self.h = h
+        _live.add(self)
 
     def close(self):
         if getattr(self, "h", None):
@@ -408,6 +433,12 @@ class Batch:
     def reset_timers(self):
         self.ctx.check(self.L.vh_batch_reset_timers(self.h), "vh_batch_reset_timers")
 
+    def study_times(self):
+        """Per-study wall time (us) of the last run's one-workgroup-per-study N4 kernel."""
+        us = np.zeros(self.shape[0], np.float64)
+        self.ctx.check(self.L.vh_batch_study_times(self.h, _ptr(us)), "vh_batch_study_times")
+        return us
+
     def kernel_time(self, name):
         ms, n, by = ct.c_double(0), ct.c_int64(0), ct.c_double(0)
         self.ctx.check(self.L.vh_batch_kernel_time(self.h, name.encode(), ct.byref(ms),
@@ -428,6 +459,7 @@ class Pipe:
         self.ctx.check(self.L.vh_pipe_create(self.ctx.h, R, C, Z, sub, slots, ct.byref(h)),
                        "vh_pipe_create")
         self.h = h
+        _live.add(self)
 
     def close(self):
         if getattr(self, "h", None):

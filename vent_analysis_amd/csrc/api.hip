@@ -4,8 +4,13 @@
 // message for vh_last_error().
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstring>
 #include <stdexcept>
+
+#ifndef VH_COPY_THREADS
+#define VH_COPY_THREADS 8   // host threads per staging copy (each pipe slot copies on its own)
+#endif
 
 #include "vh_internal.h"
 
@@ -594,6 +599,22 @@ int vh_batch_kernel_time(vh_batch *b, const char *name, double *total_ms, int64_
     })
 }
 
+int vh_batch_study_times(vh_batch *b, double *us) {
+    API_TRY(b->ctx, {
+        if (!us) throw VhError{VH_ERR_ARG, "null buffer"};
+        HIP_TRY(hipStreamSynchronize(b->stream));
+        for (int64_t i = 0; i < b->nb; ++i) us[i] = 0.0;
+        if (!b->have_result || !b->opts.do_n4 || !b->n4_used_study) return VH_OK;
+        std::vector<N4State> st(b->nb);
+        HIP_TRY(hipMemcpy(st.data(), b->d_st, sizeof(N4State) * b->nb, hipMemcpyDeviceToHost));
+        int rate_khz = 0;
+        HIP_TRY(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, b->ctx->device));
+        if (rate_khz <= 0) throw VhError{VH_ERR_HIP, "no device wall clock rate"};
+        for (int64_t i = 0; i < b->nb; ++i)
+            us[i] = (double)(st[i].t_end - st[i].t_start) * 1000.0 / (double)rate_khz;
+    })
+}
+
 // ---- rendering (export.hip) ------------------------------------------------------------------
 int vh_overlay(vh_ctx *ctx, const float *n4, const uint8_t *defect, int64_t R, int64_t C, int64_t Z,
                int64_t batch, uint8_t *rgb) {
@@ -657,7 +678,27 @@ int vh_recon(vh_ctx *ctx, const double *k, int64_t n0, int64_t n1, int64_t nz, d
     })
 }
 
-// ---- host-to-host pipeline -------------------------------------------------------------------
+// ---- host-to-host pipeline -----
+// pageable <-> pinned staging copies split over host threads: one thread's memcpy (~5-10 GB/s) bounded
+// the whole pipeline at about half the device-resident rate; the copy engines and the
+// PCIe link are far from busy at that rate
+static void par_memcpy(void *dst, const void *src, size_t bytes) {
+    const size_t chunk = (size_t)16 << 20;   // 16 MiB per task
+    const int want = (int)std::min<size_t>(VH_COPY_THREADS, (bytes + chunk - 1) / chunk);
+    if (want <= 1) {
+        memcpy(dst, src, bytes);
+        return;
+    }
+    std::vector<std::thread> th;
+    const size_t per = (bytes + want - 1) / want;
+    for (int i = 1; i < want; ++i) {
+        const size_t o = per * i, n = std::min(per, bytes - o);
+        th.emplace_back([=] { memcpy((char *)dst + o, (const char *)src + o, n); });
+    }
+    memcpy(dst, src, std::min(per, bytes));
+    for (auto &t : th) t.join();
+}
+
 // One host thread per slot; slot s owns batch b[s] (its own stream) and pinned staging, and takes
 // sub-batches s, s + slots, ...  Within a slot the steps are serial (stage in -> H2D -> pipeline ->
 // D2H -> stage out); across slots they overlap, so the copy engines, the host memcpys and the
@@ -708,8 +749,8 @@ int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, con
                     const int64_t v0 = k * sub, cnt = std::min(sub, n - v0);
                     uint8_t *qm = q.u8, *qd = q.u8 + sub * V, *qb = q.u8 + 2 * sub * V,
                             *ql = q.u8 + 3 * sub * V;
-                    memcpy(q.hp, hp + v0 * V, sizeof(float) * cnt * V);
-                    memcpy(qm, mask + v0 * V, cnt * V);
+                    par_memcpy(q.hp, hp + v0 * V, sizeof(float) * cnt * V);
+                    par_memcpy(qm, mask + v0 * V, cnt * V);
                     for (int64_t i = cnt; i < sub; ++i) {   // ragged tail: repeat the last study
                         memcpy(q.hp + i * V, hp + (v0 + cnt - 1) * V, sizeof(float) * V);
                         memcpy(qm + i * V, mask + (v0 + cnt - 1) * V, V);
@@ -727,10 +768,10 @@ int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, con
                         fill_results(b, q.res.data());
                         memcpy(res + v0, q.res.data(), sizeof(vh_vdp_result) * cnt);
                     }
-                    if (n4) memcpy(n4 + v0 * V, q.n4, sizeof(float) * cnt * V);
-                    if (defect) memcpy(defect + v0 * V, qd, cnt * V);
-                    if (defect_border) memcpy(defect_border + v0 * V, qb, cnt * V);
-                    if (lb) memcpy(lb + v0 * V, ql, cnt * V);
+                    if (n4) par_memcpy(n4 + v0 * V, q.n4, sizeof(float) * cnt * V);
+                    if (defect) par_memcpy(defect + v0 * V, qd, cnt * V);
+                    if (defect_border) par_memcpy(defect_border + v0 * V, qb, cnt * V);
+                    if (lb) par_memcpy(lb + v0 * V, ql, cnt * V);
                 }
             } catch (const VhError &e) {
                 err[s] = e;

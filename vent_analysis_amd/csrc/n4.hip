@@ -1162,7 +1162,9 @@ __global__ void __launch_bounds__(PC_TPB) k_n4_pcw(const float *D, const int32_t
     __shared__ ChainState ch;
     const float *const Db = D + b * VS;
     const int32_t *const pb = perm + b * VS;
-    pcw_run([=](int64_t r) { return Db[pb[r]]; }, Pbuf + b * VS, sc[b].n_mask1, S, ch, 1);
+    // D[b] (compact d) is free once pass 0 has read it: PCX's stored increments
+    pcw_run([=](int64_t r) { return Db[pb[r]]; }, Pbuf + b * VS, sc[b].n_mask1, S, ch, 1,
+            reinterpret_cast<double *>(const_cast<float *>(Db)), (int)(VS / 2));
     if (threadIdx.x == 0) st[b].conv_w = ch.conv;
 }
 

@@ -792,6 +792,8 @@ struct PcShared {
     // all-wave update (pcw_*): per-wave aggregates of the block transitions
     double agA[NL / 64], agB[NL / 64], agS[NL / 64];
     int agFirst[NL / 64];
+    // exact sig after stage 0 (pcx_*): t-slot allocator, result tag, walks taken
+    int xslots, xdone, xwalks, xslow;
     // pass-0 block sums of p - 1 and (p - 1)^2 (double, 16-aligned pair over gmu_o .. sp1: those
     // fields are written by round 0 before they are next read)
     __device__ double &s1(int j) { return *reinterpret_cast<double *>(&b[j].gmu_o); }
@@ -982,6 +984,10 @@ __device__ __forceinline__ void pc_kf2(pc_f2 k, pc_f2 p, PcKf &qa, PcKf &qb) {
 // e0 >= r0 2^-40 + 2^-44 >= 2^-22 |mu rl| + 2^-46 |mu| for mu < 4 (one bound per block: r0 <= 1/k0)
 template <bool SIG = true>
 __device__ __forceinline__ bool pc_apx_step(const PcKf &q, float e0, float p, bool first, float &mu, float &sig) {
+    if (!SIG && !first) {   // mu alone: sig carries sum (p - mu)^2 along the block (PCX's binade estimate)
+        const float dq = p - mu;
+        sig = fmaf(dq, dq, sig);
+    }
     if (SIG && !first) {
         const float d = p - mu, q2 = d * d;
         const float y = fmaf(q2, q.ch, sig);
@@ -1001,11 +1007,12 @@ __device__ __forceinline__ bool pc_apx_step(const PcKf &q, float e0, float p, bo
 }
 // a lane's block in phase A: groups of 8 steps without guards; a group with an uncertified step is
 // redone with the exact steps (rare: the wave branches only when one of its lanes needs it)
-// SIG = false: the mu recurrence alone (mu never reads sig; sig is returned unchanged)
+// SIG = false: the mu recurrence alone (mu never reads sig); sig returns sum (p - mu)^2 over the
+// block (approximate: the exact redo and tail steps add their sig increments instead)
 template <int NL, bool SIG = true>
 __device__ __forceinline__ void pc_block_apx(const float *P, uint32_t j, uint32_t len, uint32_t k0,
                                              float &mu, float &sig, uint32_t nl = NL) {
-    const float sig_in = sig;
+    if (!SIG) sig = 0.0f;
     float cur[8], nxt[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) cur[i] = (uint32_t)i < len ? P[(size_t)i * nl + j] : 0.0f;
@@ -1043,7 +1050,6 @@ __device__ __forceinline__ void pc_block_apx(const float *P, uint32_t j, uint32_
             pc_step(kd, cur[i], mu, sig);
             kd += 1.0;
         }
-    if (!SIG) sig = sig_in;
 }
 
 // ---- all-wave PC helpers (NL = threads of the workgroup, one block per thread) -----------------
@@ -1162,6 +1168,259 @@ __device__ void pcw_update(PcShared<NL> &S, const PcMap &m, int round, int req, 
     }
 }
 
+// ---- exact sig after stage 0 ("PCX") --------------------------------------------------------------
+// Once stage 0 has made every block's mu start exact, sig needs no rounds: with mu exact, every
+// step's increment t_k = RN(RN(sqr(p - mu) (N - 1)) / N) is a known double, and sig is the float
+// accumulation sig <- (float)(sig + t_k), non-decreasing.  Inside one binade [2^e, 2^(e+1)) that
+// accumulation is an integer sum: sig + t rounds first to the double grid 2^(e-52) and then to the
+// float grid 2^(e-23), both anchored on sig's own grid, so a step adds
+//   c_k(e) = RN(RN(t 2^(52-e)) / 2^29)    whole float ulps (ties to even: a remainder of exactly
+// 2^28 depends on sig's last bit -- flagged), independent of sig as long as sig + t stays below
+// 2^(e+1).  So:
+//   estimate (all threads): sig at every block start from the prefix over the blocks of
+//     sum (p - mu)^2 along stage 0's last trajectories (within ~1e-4 of the float sig; the pass-0
+//     variance guess misses the float mean's drift, up to a factor 2.2);
+//   T pass (all threads): each block runs its steps from its stage-0 start with the exact mu step
+//     (verifying stage 0: its end must be the next block's start) and forms t_k.  A block whose
+//     estimated start and end lie in one binade e sums c_k(e); a block whose estimate crosses a
+//     binade (with a 2^-10 margin), block 0 and the last block store their t_k in tbuf instead;
+//   scan (one wave): from sig = 0, runs of blocks that stay in the current binade are integer prefix
+//     sums (64 blocks per step, DPP scan); a crossing block is walked from its exact start over its
+//     stored t_k, again as integer prefix sums in the current binade up to the step that crosses or
+//     holds a tie, which is evaluated exactly as one float step.
+// Every step is the spec's step evaluated exactly, so the result is the serial recurrence bit for bit
+// (no verification round needed).  A block the estimate misplaced is walked by recomputing its mu
+// trajectory (systolic); stage 0 not verified falls back to the stage-1 / exact rounds below.
+// scripts/dev/pc_sim2.c (GPX=1) emulates this on oracle d sequences: ~20 walks per iteration, all
+// predicted, every result exact.
+struct PcX {                 // overlays (gmu_o, emu_o, sp0, sp1) once stage 0 is over
+    int32_t c;               // sum of c_k(e) over the block (saturated at 2^30)
+    int32_t e;               // binade of the block's estimated start (-200: none)
+    int32_t flags;           // bit 0: tie inside; bit 1: candidate (t_k stored)
+    int32_t slot;            // tbuf slot of a candidate, -1 when none
+};
+#define PCX_TIEF 1
+#define PCX_CANDF 2
+template <int NL>
+__device__ __forceinline__ PcX &pcx_of(PcShared<NL> &S, int j) {
+    return *reinterpret_cast<PcX *>(&S.b[j].gmu_o);
+}
+// binade e of a positive normal float (2^e <= f < 2^(e+1)); -200 for 0, subnormals, inf / NaN
+__device__ __forceinline__ int pcx_binade(float f) {
+    const int be = (__float_as_int(f) >> 23) & 0xff;
+    return (f > 0.0f && be > 0 && be < 255) ? be - 127 : -200;
+}
+// c(e) of one increment: t 2^(52 - e) rounded to an integer (the double grid), then to whole floats
+// (2^29 double ulps, ties flagged)
+__device__ __forceinline__ double pcx_c(double t, int e, bool &tie) {
+    const double Y = rint(ldexp(t, 52 - e));
+    const double hi = floor(Y * 0x1p-29);
+    const double rem = fma(-hi, 0x1p29, Y);
+    tie = rem == 0x1p28;
+    return hi + (rem > 0x1p28 ? 1.0 : 0.0);
+}
+// inclusive prefix sum over the wave's 64 lanes (int32), DPP row shifts and row broadcasts (gfx9)
+__device__ __forceinline__ int pcx_iscan(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);   // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);   // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);   // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);   // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);   // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);   // row_bcast:31 -> rows 2, 3
+    return v;
+}
+
+// T pass: this thread's block from its stage-0 start (S.b[j].gmu) with exact steps; sest / snext =
+// the sig estimate at its start / end
+template <int NL>
+__device__ void pcx_tpass(PcShared<NL> &S, const PcMap &m, const float *P, uint32_t j, uint32_t len,
+                          uint32_t k0, double sest, double snext, double *tbuf, int tcap) {
+    const int nbe = m.L ? NL : (int)m.rem;
+    const int e = pcx_binade((float)sest);
+    const bool cand = (int)j == 0 || (int)j >= nbe - 1 || e < -125 ||
+                      e != pcx_binade((float)(snext * (1.0 + 0x1p-10))) ||
+                      e != pcx_binade((float)(sest * (1.0 - 0x1p-10)));
+    int slot = -1;
+    if (cand && (int)j < nbe) {
+        const int sl = atomicAdd(&S.xslots, 1);
+        if ((sl + 1) * (int)(m.L + 1) <= tcap) slot = sl;
+    }
+    double C = 0.0;
+    bool tie = false;
+    float mu = S.b[j].gmu;
+    double kd = (double)k0;
+    double *const tb = tbuf + (size_t)(slot >= 0 ? slot : 0) * (m.L + 1);
+    for (uint32_t s0 = 0; s0 < len; s0 += 8) {
+        float pv[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) pv[i] = s0 + i < len ? P[(size_t)(s0 + i) * NL + j] : 1.0f;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            if (s0 + i >= len) break;
+            const PcK q = pc_consts(kd, pv[i]);
+            double t = 0.0;
+            if (kd != 1.0) {
+                const float d = pv[i] - mu;
+                t = pc_div((double)(d * d) * (q.N - 1.0), q.N, q.r);
+            }
+            if (slot >= 0) {
+                tb[s0 + i] = t;
+            } else if (!cand) {
+                bool ti;
+                C += pcx_c(t, e, ti);
+                tie |= ti;
+            }
+            mu = (float)__dadd_rn(__dmul_rn((double)mu, q.A), q.B);
+            kd += 1.0;
+        }
+    }
+    S.b[j].emu = mu;
+    PcX &x = pcx_of(S, j);
+    x.c = (int32_t)fmin(C, 1073741824.0);
+    x.e = e;
+    x.flags = (tie ? PCX_TIEF : 0) | (cand ? PCX_CANDF : 0);
+    x.slot = slot;
+}
+
+// Walk block j from its exact start s over its stored increments t (tb[0 .. len)): per 64-step piece,
+// integer prefix sums in the current binade up to the first step that crosses (or comes within an ulp
+// of) the binade's end or holds a tie; that step is one exact float step; repeat.
+// t0 / t1: the first two pieces, loaded ahead by the caller (global latency off the serial path)
+__device__ float pcx_walk_t(const double *tb, uint32_t len, float s, double t0, double t1) {
+    const int lane = threadIdx.x & 63;
+    for (uint32_t s0 = 0; s0 < len; s0 += 64) {
+        const bool in = s0 + lane < len;
+        const double t = !in ? 0.0 : s0 == 0 ? t0 : s0 == 64 ? t1 : tb[s0 + lane];
+        int from = 0;   // lanes below are done
+        while (from < 64) {
+            const int e = pcx_binade(s);
+            bool tie = false;
+            double c = 0.0;
+            if (e >= -125 && in && lane >= from) c = pcx_c(t, e, tie);
+            const bool big = c >= 0x1p23;   // one step past a whole binade: crosses
+            const int pre = pcx_iscan((in && lane >= from && !big) ? (int)c : 0);
+            const double ulp = ldexp(1.0, e - 23), lim = ldexp(1.0, e + 1) - ulp;
+            const double val = (double)s + (double)pre * ulp;
+            const bool bad = in && lane >= from && (e < -125 || tie || big || !(val < lim));
+            const uint64_t bb = __ballot(bad);
+            if (!bb) {   // the rest of the piece stays in the binade
+                s = (float)__shfl(val, 63, 64);
+                break;
+            }
+            const int f = (int)__builtin_ctzll(bb);   // exact step f from the value before it
+            const double before = f > from ? __shfl(val, f - 1, 64) : (double)s;
+            const double tf = __shfl(t, f, 64);
+            s = (float)((double)(float)before + tf);
+            from = f + 1;
+        }
+    }
+    return s;
+}
+
+// Walk block j exactly without stored increments (a block the estimate did not flag): the wave
+// recomputes the block's mu trajectory (systolic) and t_k, then the sig steps (systolic)
+template <int NL>
+__device__ float pcx_walk_mu(const PcShared<NL> &S, const PcMap &m, const float *P, int j, float s) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t len = pc_len(m, (uint32_t)j), k0 = pc_k0(m, (uint32_t)j);
+    float mu = S.b[j].gmu;
+    for (uint32_t s0 = 0; s0 < len; s0 += 64) {
+        const bool in = s0 + lane < len;
+        const float p = in ? P[(size_t)(s0 + lane) * NL + j] : 1.0f;
+        const double kd = (double)(k0 + s0 + lane);
+        const PcK q = pc_consts(kd, p);
+        float mprev;   // mu before this lane's step
+        mu = chain_sys64<true>(in ? q.A : 1.0, in ? q.B : 0.0, mu, mprev);
+        double t = 0.0;
+        if (in && kd != 1.0) {
+            const float d = p - mprev;
+            t = pc_div((double)(d * d) * (q.N - 1.0), q.N, q.r);
+        }
+        float rec;
+        s = chain_sys64<false>(in ? 1.0 : 0.0, t, s, rec);
+    }
+    return s;
+}
+
+// The scan (wave 0).  Returns false when stage 0 is not verified (the caller falls back).
+template <int NL>
+__device__ bool pcx_scan(PcShared<NL> &S, const PcMap &m, const float *P, const double *tbuf, float &sig_out,
+                         int &walks, int &slow) {
+    const int lane = threadIdx.x & 63;
+    const int nbe = m.L ? NL : (int)m.rem;
+    bool bad = false;   // stage 0 verified: every block's exact end is its successor's start
+    for (int j = lane; j < nbe - 1; j += 64)
+        bad |= __float_as_uint(S.b[j].emu) != __float_as_uint(S.b[j + 1].gmu);
+    if (__ballot(bad)) return false;
+    float s = 0.0f;   // exact sig at the start of block j
+    int j = 0;
+    walks = slow = 0;
+    // the next candidate block at or after `from` and its first two pieces of t, loaded ahead
+    int nxt = -1;
+    double pf0 = 0.0, pf1 = 0.0;
+    auto prefetch = [&](int from) {
+        nxt = nbe;
+        for (int c0 = from; c0 < nbe; c0 += 64) {
+            const bool cnd = c0 + lane < nbe && (pcx_of(S, c0 + lane).flags & PCX_CANDF);
+            const uint64_t bl = __ballot(cnd);
+            if (bl) {
+                nxt = c0 + (int)__builtin_ctzll(bl);
+                break;
+            }
+        }
+        if (nxt < nbe) {
+            const PcX x = pcx_of(S, nxt);
+            const uint32_t len = pc_len(m, (uint32_t)nxt);
+            const double *tb = tbuf + (size_t)(x.slot >= 0 ? x.slot : 0) * (m.L + 1);
+            pf0 = (x.slot >= 0 && (uint32_t)lane < len) ? tb[lane] : 0.0;
+            pf1 = (x.slot >= 0 && (uint32_t)lane + 64 < len) ? tb[lane + 64] : 0.0;
+        }
+    };
+    prefetch(0);
+    while (j < nbe) {
+        const int jj = j + lane;
+        const bool have = jj < nbe;
+        const int e = pcx_binade(s);   // wave-uniform
+        bool ok = false;
+        int inc = 0;
+        if (have && e >= -125) {
+            const PcX x = pcx_of(S, jj);
+            ok = x.flags == 0 && x.e == e && x.c < (1 << 23);
+            inc = ok ? x.c : 0;
+        }
+        const int pre = pcx_iscan(inc);
+        const double ulp = ldexp(1.0, e - 23), lim = ldexp(1.0, e + 1) - ulp;
+        const double end = (double)s + (double)pre * ulp;
+        ok = ok && end < lim;
+        const uint64_t fail = ~__ballot(ok || !have);
+        const int first = fail ? (int)__builtin_ctzll(fail) : 64;   // first block that cannot be summed
+        if (first > 0) {   // blocks j .. j + first - 1 stay in the binade: exact integer sums
+            const int last = min(first, nbe - j) - 1;
+            s = (float)__shfl(end, last, 64);
+            j += last + 1;
+            continue;
+        }
+        const PcX x = pcx_of(S, j);   // block j: walked exactly
+        if ((x.flags & PCX_CANDF) && x.slot >= 0) {
+            const double a0 = j == nxt ? pf0 : 0.0, a1 = j == nxt ? pf1 : 0.0;
+            const bool mine = j == nxt;
+            if (mine) prefetch(j + 1);   // the next candidate's loads fly during this walk
+            const double *tb = tbuf + (size_t)x.slot * (m.L + 1);
+            const uint32_t len = pc_len(m, (uint32_t)j);
+            s = mine ? pcx_walk_t(tb, len, s, a0, a1)
+                     : pcx_walk_t(tb, len, s, (uint32_t)lane < len ? tb[lane] : 0.0,
+                                  (uint32_t)lane + 64 < len ? tb[lane + 64] : 0.0);
+        } else {
+            s = pcx_walk_mu<NL>(S, m, P, j, s);
+            ++slow;
+        }
+        ++walks;
+        ++j;
+    }
+    sig_out = s;
+    return true;
+}
+
 #define PC_TPB 1024
 // The recurrence of one iteration on a whole 1024-thread workgroup (one block per thread), shared by
 // the study kernel (ST_PC 2) and the sweep driver (k_n4_pcw).  ld(r) returns d at raster rank r
@@ -1179,9 +1438,12 @@ static_assert(PC_APASS >= 1 && PC_APASS <= 2, "PC_APASS: 1 or 2 phase-A stages (
 #ifndef PC_AMAX
 #define PC_AMAX 40
 #endif
+#ifndef PC_XSIG
+#define PC_XSIG 1   // exact sig after stage 0 (PCX above); 0: stage 1 and the exact rounds always
+#endif
 template <class LoadD>
 __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n, PcShared<PC_TPB> &S,
-                                                  ChainState &ch, int req) {
+                                                  ChainState &ch, int req, double *tbuf, int tcap) {
     const int tid = threadIdx.x;
     const PcMap m = pc_map(n, PC_TPB);
     const uint32_t j = (uint32_t)tid, len = pc_len(m, j), k0 = pc_k0(m, j);
@@ -1190,9 +1452,10 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
     unsigned long long c1 = 0, c2 = 0;
     int ra = 0;
 #endif
-    if (tid == 0) {
+    if (tid == 0) {   // flags from an earlier call (or other phases' use of this LDS) must not match
         S.done = 0;
         S.fallback = 0;
+        S.xdone = 0;
     }
     double s1 = 0.0, s2 = 0.0;
     for (uint32_t s0 = 0; s0 < len; s0 += 8) {
@@ -1222,9 +1485,57 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
     // a third fewer instructions per step), then on both.  A thread whose start did not change
     // keeps its end; a wave whose threads all kept theirs skips the round.
 #ifdef PC_PROF
-    unsigned long long cblk = 0;
+    unsigned long long cblk = 0, cst[2] = {0, 0}, cbs[2] = {0, 0};
+    int rst[2] = {0, 0};
 #endif
+    bool xs = false;   // sig finished exactly by PCX: no stage 1, no exact rounds
     for (int pass = 0; pass < PC_APASS; ++pass) {
+        if (pass == 1 && PC_XSIG && S.done == 4 * req) {   // stage 0 reached its fixed point
+#ifdef PC_PROF
+            const unsigned long long cx0 = clock64();
+#endif
+            const bool real = j < (uint32_t)(m.L ? PC_TPB : m.rem);
+            const double own = real ? (double)S.b[j].esig : 0.0;   // stage 0's sum (p - mu)^2
+            double sest, dummy;   // sig estimate at the block start: the prefix of those sums
+            pcw_scan<PC_TPB>(S, 1.0, own, 0.0, sest, dummy);
+            if (tid == 0) S.xslots = 0;
+            __syncthreads();
+#ifdef PC_PROF
+            const unsigned long long cxt = clock64();
+#endif
+            pcx_tpass<PC_TPB>(S, m, P, j, len, k0, sest, sest + own, tbuf, tcap);
+            __syncthreads();
+#ifdef PC_PROF
+            cbs[1] = clock64() - cxt;   // T pass (reported as stage1 blocks)
+#endif
+            if (tid < 64) {
+                float sg = 0.0f;
+                int w = 0, slow = 0;
+                const bool ok = pcx_scan<PC_TPB>(S, m, P, tbuf, sg, w, slow);
+                if (tid == 0) {
+                    const int nbe = m.L ? PC_TPB : (int)m.rem;
+                    if (ok) {
+                        S.mu = S.b[nbe - 1].emu;
+                        S.sig = sg;
+                        S.rounds = round + 1;
+                        S.xdone = 4 * req + 3;
+                    }
+                    S.xwalks = ok ? w : -1;
+                    S.xslow = slow;
+                }
+            }
+            __syncthreads();
+#ifdef PC_PROF
+            cst[1] = clock64() - cx0;
+#endif
+            if (S.xdone == 4 * req + 3) {
+                xs = true;
+                break;
+            }
+        }
+#ifdef PC_PROF
+        const unsigned long long cs0 = clock64(), cb0 = cblk;
+#endif
         // done / fallback flags carry a tag per call and stage (no reset between stages: a wave
         // still reading the flag of the stage before must not see it cleared)
         const int tag = 4 * req + pass;
@@ -1252,8 +1563,15 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
 #endif
             pcw_update<PC_TPB>(S, m, round, tag, ra0 == PC_AMAX - 1, false, pass == 1);
             __syncthreads();
+#ifdef PC_PROF
+            rst[pass]++;
+#endif
             if (S.done == tag) break;
         }
+#ifdef PC_PROF
+        cst[pass] = clock64() - cs0;
+        cbs[pass] = cblk - cb0;
+#endif
     }
 #ifdef PC_PROF
     ra = round + 1;
@@ -1261,7 +1579,7 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
 #endif
     // phase B: exact rounds (the verification; usually one)
     const int tagb = 4 * req + 2;
-    for (int rb = 0; rb < PC_RMAX; ++rb) {
+    for (int rb = 0; rb < PC_RMAX && !xs; ++rb) {
         ++round;
         float mu = S.b[j].gmu, sig = S.b[j].gsig;
         pc_block<PC_TPB>(P, j, len, k0, mu, sig);
@@ -1282,8 +1600,10 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
         ch.conv = itk_conv(S.mu, S.sig, n);
 #ifdef PC_PROF
         if (blockIdx.x == 0)
-            printf("PCW_PROF n %lld roundsA %d roundsB %d fallback %d pass0 %llu A %llu (blocks %llu) B %llu\n",
-                   (long long)n, ra, S.rounds - ra + 0, S.fallback == tagb, c1 - c0, c2 - c1, cblk, clock64() - c2);
+            printf("PCW_PROF n %lld roundsA %d roundsB %d fallback %d pass0 %llu A %llu (blocks %llu) B %llu"
+                   " | stage0 %d rounds %llu cyc (blocks %llu) stage1 %d rounds %llu cyc (blocks %llu) xsig %d walks %d\n",
+                   (long long)n, ra, S.rounds - ra + 0, S.fallback == tagb, c1 - c0, c2 - c1, cblk, clock64() - c2,
+                   rst[0], cst[0], cbs[0], rst[1], cst[1], cbs[1], (int)xs, S.xwalks * 1000 + S.xslow);
 #endif
     }
 }

@@ -591,6 +591,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
 
     const int64_t n = a.sc[b].n_mask1;
     N4State *stb = a.st + b;
+    if (t == 0) stb->t_start = wall_clock64();   // per-study durations (vh_batch_study_times)
     const DevLevel &lvl = a.lvs->lv[a.nlev - 1];
     const int p1last = lvl.ax[0].ncp * lvl.ax[1].ncp * a.Z;
     if (n < 2) {   // no fit: zero field (output = input), no iterations
@@ -599,6 +600,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
             stb->iters_level[t] = 0;
             stb->conv_level[t] = 0.0f;
         }
+        if (t == 0) stb->t_end = wall_clock64();
         return;
     }
     // Waves.  conv_mode 0: waves [0, ST_CW) run ITK's float Welford recurrence (S7) of each kept
@@ -1089,7 +1091,9 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                 } else if (a.conv_mode == 0) {   // S7 on the whole workgroup (ST_PC 2)
                     PcShared<ST_TPB> &PW = *reinterpret_cast<PcShared<ST_TPB> *>(smem + a.o_scr);
                     const float *const Dr = a.D + b * a.VS;
-                    pcw_run([=](int64_t r) { return Dr[r]; }, a.D + a.half + b * a.VS, n, PW, M.ch[0], itk);
+                    // the raster d buffer is free once pass 0 has read it: PCX's stored increments
+                    pcw_run([=](int64_t r) { return Dr[r]; }, a.D + a.half + b * a.VS, n, PW, M.ch[0], itk,
+                            reinterpret_cast<double *>(a.D + b * a.VS), (int)(a.VS / 2));
                     if (t == 0) M.conv = (double)M.ch[0].conv;
                 } else if (g.w == 0) {   // S7x: item partials in item order
                     double sd = 0.0, sd2 = 0.0;
@@ -1151,6 +1155,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
     if (t == 0) {
         stb->conv = M.conv;
         stb->active = M.wd ? -2 : 0;
+        stb->t_end = wall_clock64();
     }
 }
 

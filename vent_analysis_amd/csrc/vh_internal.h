@@ -84,6 +84,7 @@ struct N4State {
     double conv;
     int32_t iters_level[VH_MAX_LEVELS];
     float conv_level[VH_MAX_LEVELS];
+    uint64_t t_start, t_end;   // k_n4_study: device wall clock (wall_clock64) at the workgroup's start / end
 };
 
 // Per-axis, per-level B-spline tables (host-built, identical to oracle/n4_oracle.c).
