@@ -110,8 +110,10 @@ def algorithmic_bytes(name, hp, mk, res, R, C, Z, study=True, conv_mode=0):
         return float(B * (V / 8.0 + 12.0 * R * tiles) + (0.0 if study else np.sum(16.0 * vm)))
     if name == "n4_final":       # read I, write N4HPvent (every voxel) + the sort keys (masked)
         return float(B * 8.0 * V + np.sum(4.0 * vm))
-    if name == "classify":       # read N4 + mask, write defect, border, LB      every voxel
-        return float(B * 8.0 * V)
+    if name == "classify":       # write defect, border, LB at every voxel; read N4 + mask only in
+        return float(np.sum(3.0 * V + 5.0 * vr))   # the columns' masked row ranges (k_plane skips the rest)
+    if name == "mean":           # numpy-order chunk sums + p99: read the sorted masked keys
+        return float(np.sum(4.0 * (m != 0).sum(axis=(1, 2))))
     if name == "sort":           # digit histograms (read) + 4 LSD passes (read + write), masked
         return float(np.sum(36.0 * vm))
     if name == "gather":
@@ -160,25 +162,28 @@ def max_over_ranks(dt, dist):
 
 
 def host_to_host(R, C, Z, nb, args, device, opts, seed):
-    """Volumes/s from host memory to host memory: args.h2h_batches sub-batches of nb studies
-    through vh_pipe (3 slots, pinned staging, one stream each), inputs HPvent + mask in, every
-    output the class returns out (N4HPvent, defectArray, defectBorder, defectArrayLB, scalars).
-    The slowest rank's time is what the caller's aggregate uses (ranks run independently)."""
+    """Volumes/s from host memory to host memory: args.h2h_batches x nb studies streamed through
+    vh_pipe in sub-batches of args.h2h_sub studies on args.h2h_slots slots (pinned staging, one
+    stream each: the H2D, compute and D2H of different sub-batches overlap, and the studies of
+    concurrent sub-batches fill the CUs that finished studies free), inputs HPvent + mask in,
+    every output the class returns out (N4HPvent, defectArray, defectBorder, defectArrayLB,
+    scalars).  The slowest rank's time is what the caller's aggregate uses (ranks run
+    independently)."""
     from vent_analysis_amd import _lib
     from vent_analysis_amd.synth import synth_batch
-    slots = 3
+    slots, sub = args.h2h_slots, min(args.h2h_sub, nb)
     n = max(1, args.h2h_batches) * nb
     hp, mk = synth_batch(R, C, Z, n, base_seed=seed, unique=BENCH_UNIQUE, vary=True)
-    P = _lib.Pipe(R, C, Z, nb, slots=slots, device=device)
+    P = _lib.Pipe(R, C, Z, sub, slots=slots, device=device)
     out = (np.empty(hp.shape, np.float32), np.empty(hp.shape, np.uint8),
            np.empty(hp.shape, np.uint8), np.empty(hp.shape, np.uint8))
-    P.run(hp[:slots * nb], mk[:slots * nb], opts,
-          out=tuple(a[:slots * nb] for a in out))          # warm: every slot's workspaces
+    P.run(hp[:slots * sub], mk[:slots * sub], opts,
+          out=tuple(a[:slots * sub] for a in out))          # warm: every slot's workspaces
     t = time.perf_counter()
     P.run(hp, mk, opts, out=out)
     dt = time.perf_counter() - t
     P.close()
-    return {"volumes": n, "seconds": round(dt, 4), "sub_batch": nb, "slots": slots,
+    return {"volumes": n, "seconds": round(dt, 4), "sub_batch": sub, "slots": slots,
             "includes": "H2D of HPvent f32 + mask u8, the full pipeline, D2H of N4HPvent f32 + "
                         "defect / border / LB u8 + per-study scalars, host staging memcpys",
             "bytes_per_volume": int(R * C * Z * (4 + 1 + 4 + 3))}
@@ -261,7 +266,11 @@ def main():
     ap.add_argument("--no-h2h", action="store_true",
                     help="skip the host-to-host pipeline measurement (host_to_host_vol_s)")
     ap.add_argument("--h2h-batches", type=int, default=6,
-                    help="host-to-host sample: this many sub-batches of --batch volumes")
+                    help="host-to-host sample: this many x --batch volumes")
+    ap.add_argument("--h2h-sub", type=int, default=64,
+                    help="host-to-host: studies per pipeline sub-batch")
+    ap.add_argument("--h2h-slots", type=int, default=6,
+                    help="host-to-host: pipeline slots (sub-batches in flight, <= 8)")
     ap.add_argument("--workload", default="vdp", choices=["vdp", "ci"],
                     help="vdp: the BASELINE metric (default); ci: the cluster-index line")
     ap.add_argument("--conv-threshold", type=float, default=0.001,

@@ -648,8 +648,12 @@ static float itk_eval(const float *lat, const axis_t *ax, const axis_t *ay, cons
     return s;
 }
 
+/* spec: ablation mask -- bit k replaces ITK's float form of stage Sk by the build spec's (S1 log,
+ * S3 histogram, S5 fit, S6 evaluation, S7 exp, S9 output), so scripts/n4_itk_distance.py can tell
+ * which stage puts the spec where it is relative to ITK's float arithmetic (0 = pure ITK-float). */
+#define ABL(k) ((spec >> (k)) & 1)
 int n4_oracle_itk(const float *I, const uint8_t *mask, int64_t R, int64_t C, int64_t Z,
-                  const n4o_params *prm, int nonpos_raw, int nthreads, float *out,
+                  const n4o_params *prm, int nonpos_raw, int nthreads, int spec, float *out,
                   int32_t *iters_out, float *conv_out)
 {
     /* nthreads > 1: ITK's BSplineScatteredDataPointSetToImageFilter splits the points into
@@ -662,6 +666,7 @@ int n4_oracle_itk(const float *I, const uint8_t *mask, int64_t R, int64_t C, int
     const int bins = prm->n_bins;
     float *L0 = calloc((size_t)V, sizeof(float));
     float *B = calloc((size_t)V, sizeof(float));
+    float *rv = calloc((size_t)V, sizeof(float));
     int ncp[3] = {prm->ncp[0], prm->ncp[1], prm->ncp[2]};
     int mx = ncp[0] > ncp[1] ? ncp[0] : ncp[1];
     mx = mx > ncp[2] ? mx : ncp[2];
@@ -672,7 +677,12 @@ int n4_oracle_itk(const float *I, const uint8_t *mask, int64_t R, int64_t C, int
     float *tmp2 = calloc(latmax, sizeof(float));
     float *delta = calloc(latmax * (size_t)(nthreads < 1 ? 1 : nthreads), sizeof(float));
     float *omega = calloc(latmax * (size_t)(nthreads < 1 ? 1 : nthreads), sizeof(float));
+    i128 *num = calloc(latmax, sizeof(i128));
+    i128 *denf = calloc(latmax, sizeof(i128));
+    double *P1 = calloc((size_t)maxcp * maxcp * Z, sizeof(double));
+    float *T = calloc((size_t)CZ * maxcp, sizeof(float));
     float *H = malloc(sizeof(float) * bins);
+    uint64_t *Hi = malloc(sizeof(uint64_t) * bins);
     double *hv = malloc(sizeof(double) * bins);
     float *E = malloc(sizeof(float) * bins);
     cpx tw[FFT_P / 2];
@@ -682,7 +692,8 @@ int n4_oracle_itk(const float *I, const uint8_t *mask, int64_t R, int64_t C, int
     int64_t nmask = 0;
     for (int64_t v = 0; v < V; ++v)
         if (mask[v] == 1) {
-            L0[v] = I[v] > 0.0f ? logf(I[v]) : (nonpos_raw ? I[v] : 0.0f);
+            L0[v] = I[v] > 0.0f ? (ABL(1) ? (float)log((double)I[v]) : logf(I[v]))
+                                : (nonpos_raw ? I[v] : 0.0f);
             ++nmask;
         }
     int rc = 0;
@@ -697,6 +708,11 @@ int n4_oracle_itk(const float *I, const uint8_t *mask, int64_t R, int64_t C, int
         axis_build(&az, (int)Z, ncp[2], eps);
         have_axes = 1;
         const size_t nl = (size_t)ncp[0] * ncp[1] * ncp[2];
+        const geom_t g = {R, C, Z, CZ, mask, &ax, &ay, &az};
+        if (ABL(5)) {
+            memset(denf, 0, nl * sizeof(i128));
+            fit_items(&g, 2, NULL, denf);
+        }
         int it = 0;
         float conv = INFINITY;
         while (it++ < prm->max_iters[level] && conv > prm->conv_threshold) {
@@ -708,63 +724,97 @@ int n4_oracle_itk(const float *I, const uint8_t *mask, int64_t R, int64_t C, int
                 else if (u < bmin) bmin = u;
             }
             const float slope = (bmax - bmin) / (float)(bins - 1);
-            for (int n = 0; n < bins; ++n) H[n] = 0.0f;
-            for (int64_t v = 0; v < V; ++v) {
-                if (mask[v] != 1) continue;
-                const float cidx = ((L0[v] - B[v]) - bmin) / slope;
-                const int idx = (int)floorf(cidx);
-                const float o = cidx - (float)idx;
-                if (o == 0.0f) {
-                    if (idx >= 0 && idx < bins) H[idx] += 1.0f;
-                } else if (idx >= 0 && idx < bins - 1) {
-                    H[idx] += 1.0f - o;
-                    H[idx + 1] += o;
+            if (ABL(3)) {   /* S3 spec: exact packed integer weights */
+                memset(Hi, 0, sizeof(uint64_t) * bins);
+                for (int64_t v = 0; v < V; ++v) {
+                    if (mask[v] != 1) continue;
+                    const float cidx = ((L0[v] - B[v]) - bmin) / slope;
+                    if (!(cidx >= 0.0f) || !(cidx < (float)bins)) continue;
+                    const int idx = (int)floorf(cidx);
+                    const float o = cidx - (float)idx;
+                    if (idx == bins - 1 && o > 0.0f) continue;
+                    const uint64_t a1 = (uint64_t)(uint32_t)(o * 16777216.0f);
+                    Hi[idx] += (uint64_t)16777216 - a1;
+                    if (a1) Hi[idx + 1] += a1;
                 }
-            }
-            for (int n = 0; n < bins; ++n) hv[n] = (double)H[n];
-            emap(hv, bins, bmin, slope, prm->fwhm, prm->wiener_noise, tw, E);
-            memset(delta, 0, nl * nthreads * sizeof(float));
-            memset(omega, 0, nl * nthreads * sizeof(float));
-            int64_t pt = 0;
-            for (int64_t x = 0; x < R; ++x)
-                for (int64_t y = 0; y < C; ++y)
-                    for (int64_t z = 0; z < Z; ++z) {
-                        const int64_t v = (x * C + y) * Z + z;
-                        if (mask[v] != 1) continue;
-                        const float u = L0[v] - B[v];
-                        const float r = u - sharpen(u, bmin, slope, E, bins);
-                        const size_t th = (size_t)((pt++ * nthreads) / nmask) * nl;
-                        float w2s = 0.0f;
-                        for (int a = 0; a < 4; ++a)
-                            for (int b = 0; b < 4; ++b)
-                                for (int c = 0; c < 4; ++c) {
-                                    const float w = ax.w[4 * x + a] * ay.w[4 * y + b] * az.w[4 * z + c];
-                                    w2s += w * w;
-                                }
-                        for (int a = 0; a < 4; ++a)
-                            for (int b = 0; b < 4; ++b)
-                                for (int c = 0; c < 4; ++c) {
-                                    const float w = ax.w[4 * x + a] * ay.w[4 * y + b] * az.w[4 * z + c];
-                                    const size_t e = ((size_t)(ax.base[x] + a) * ncp[1] + ay.base[y] + b) * ncp[2] + az.base[z] + c;
-                                    const float wc = w * w;
-                                    delta[th + e] += wc * (w * r / w2s);
-                                    omega[th + e] += wc;
-                                }
+                for (int n = 0; n < bins; ++n) hv[n] = (double)Hi[n] * (1.0 / HFIX);
+            } else {
+                for (int n = 0; n < bins; ++n) H[n] = 0.0f;
+                for (int64_t v = 0; v < V; ++v) {
+                    if (mask[v] != 1) continue;
+                    const float cidx = ((L0[v] - B[v]) - bmin) / slope;
+                    const int idx = (int)floorf(cidx);
+                    const float o = cidx - (float)idx;
+                    if (o == 0.0f) {
+                        if (idx >= 0 && idx < bins) H[idx] += 1.0f;
+                    } else if (idx >= 0 && idx < bins - 1) {
+                        H[idx] += 1.0f - o;
+                        H[idx + 1] += o;
                     }
-            for (int q = 1; q < nthreads; ++q)
-                for (size_t c = 0; c < nl; ++c) {
-                    delta[c] += delta[q * nl + c];
-                    omega[c] += omega[q * nl + c];
                 }
-            for (size_t c = 0; c < nl; ++c) lat[c] += omega[c] != 0.0f ? delta[c] / omega[c] : 0.0f;
+                for (int n = 0; n < bins; ++n) hv[n] = (double)H[n];
+            }
+            emap(hv, bins, bmin, slope, prm->fwhm, prm->wiener_noise, tw, E);
+            if (ABL(5)) {   /* S5 spec: item-ordered separable fit, fixed point */
+                for (int64_t v = 0; v < V; ++v) {
+                    if (mask[v] != 1) continue;
+                    const float u = L0[v] - B[v];
+                    rv[v] = u - sharpen(u, bmin, slope, E, bins);
+                }
+                memset(num, 0, nl * sizeof(i128));
+                fit_items(&g, 3, rv, num);
+                for (size_t c = 0; c < nl; ++c) {
+                    const double d = fix128_get(denf[c]);
+                    lat[c] += d != 0.0 ? (float)(fix128_get(num[c]) / d) : 0.0f;
+                }
+            } else {
+                memset(delta, 0, nl * nthreads * sizeof(float));
+                memset(omega, 0, nl * nthreads * sizeof(float));
+                int64_t pt = 0;
+                for (int64_t x = 0; x < R; ++x)
+                    for (int64_t y = 0; y < C; ++y)
+                        for (int64_t z = 0; z < Z; ++z) {
+                            const int64_t v = (x * C + y) * Z + z;
+                            if (mask[v] != 1) continue;
+                            const float u = L0[v] - B[v];
+                            const float r = u - sharpen(u, bmin, slope, E, bins);
+                            const size_t th = (size_t)((pt++ * nthreads) / nmask) * nl;
+                            float w2s = 0.0f;
+                            for (int a = 0; a < 4; ++a)
+                                for (int b = 0; b < 4; ++b)
+                                    for (int c = 0; c < 4; ++c) {
+                                        const float w = ax.w[4 * x + a] * ay.w[4 * y + b] * az.w[4 * z + c];
+                                        w2s += w * w;
+                                    }
+                            for (int a = 0; a < 4; ++a)
+                                for (int b = 0; b < 4; ++b)
+                                    for (int c = 0; c < 4; ++c) {
+                                        const float w = ax.w[4 * x + a] * ay.w[4 * y + b] * az.w[4 * z + c];
+                                        const size_t e = ((size_t)(ax.base[x] + a) * ncp[1] + ay.base[y] + b) * ncp[2] + az.base[z] + c;
+                                        const float wc = w * w;
+                                        delta[th + e] += wc * (w * r / w2s);
+                                        omega[th + e] += wc;
+                                    }
+                        }
+                for (int q = 1; q < nthreads; ++q)
+                    for (size_t c = 0; c < nl; ++c) {
+                        delta[c] += delta[q * nl + c];
+                        omega[c] += omega[q * nl + c];
+                    }
+                for (size_t c = 0; c < nl; ++c) lat[c] += omega[c] != 0.0f ? delta[c] / omega[c] : 0.0f;
+            }
+            if (ABL(6)) {
+                eval_P1(lat, &az, ncp[0], ncp[1], Z, P1);
+                eval_T(P1, &ay, ncp[0], C, Z, T);
+            }
             float N = 0.0f, mu = 0.0f, sig = 0.0f;   /* RealType; literals 1.0 are double */
             for (int64_t x = 0; x < R; ++x)
                 for (int64_t y = 0; y < C; ++y)
                     for (int64_t z = 0; z < Z; ++z) {
                         const int64_t v = (x * C + y) * Z + z;
                         if (mask[v] != 1) continue;
-                        const float bn = itk_eval(lat, &ax, &ay, &az, x, y, z);
-                        const float p = expf(B[v] - bn);
+                        const float bn = ABL(6) ? eval_B(T, &ax, ncp[0], x, y * Z + z) : itk_eval(lat, &ax, &ay, &az, x, y, z);
+                        const float p = ABL(7) ? expf_cr(B[v] - bn) : expf(B[v] - bn);
                         N = (float)((double)N + 1.0);
                         if ((double)N > 1.0) {
                             const float q = p - mu;
@@ -780,19 +830,24 @@ int n4_oracle_itk(const float *I, const uint8_t *mask, int64_t R, int64_t C, int
         if (conv_out) conv_out[level] = conv;
         if (level < prm->n_levels - 1) refine(lat, tmp, tmp2, ncp);
     }
+    if (ABL(6)) {
+        eval_P1(lat, &az, ncp[0], ncp[1], Z, P1);
+        eval_T(P1, &ay, ncp[0], C, Z, T);
+    }
     for (int64_t x = 0; x < R; ++x)
         for (int64_t y = 0; y < C; ++y)
             for (int64_t z = 0; z < Z; ++z) {
                 const int64_t v = (x * C + y) * Z + z;
-                out[v] = I[v] / expf(itk_eval(lat, &ax, &ay, &az, x, y, z));
+                const float bb = ABL(6) ? eval_B(T, &ax, ncp[0], x, y * Z + z) : itk_eval(lat, &ax, &ay, &az, x, y, z);
+                out[v] = I[v] / (ABL(9) ? expf_cr(bb) : expf(bb));
             }
-    (void)CZ;
 done:
     if (have_axes) { axis_free(&ax); axis_free(&ay); axis_free(&az); }
-    free(L0); free(B); free(lat); free(tmp); free(tmp2); free(delta); free(omega);
-    free(H); free(hv); free(E);
+    free(L0); free(B); free(rv); free(lat); free(tmp); free(tmp2); free(delta); free(omega);
+    free(num); free(denf); free(P1); free(T); free(H); free(Hi); free(hv); free(E);
     return rc;
 }
+#undef ABL
 
 /* ---- lemma check (tests/test_n4_oracle.py): the exact sig step of the GPU's PC (n4_shared.h pc_div)
  * takes RN(Q / N) as Markstein's correction RN(y + r (Q - N y)), y = RN(Q r), r = RN(1 / N), for

@@ -73,10 +73,11 @@ def n4(I, mask, **kw):
     return out, its, conv
 
 
-def n4_itk(I, mask, nonpos_raw=False, threads=1, **kw):
+def n4_itk(I, mask, nonpos_raw=False, threads=1, spec=0, **kw):
     """n4_oracle.c mode 1: ITK-like float (RealType) arithmetic in raster order, one thread.  Only
     for measuring how far the build spec's precision choices sit from an ITK-like float pipeline
-    (DESIGN.md §6); the GPU is never compared with it bit for bit."""
+    (DESIGN.md §6); the GPU is never compared with it bit for bit.  spec: bit k takes the build
+    spec's form of stage Sk instead (1 log, 3 histogram, 5 fit, 6 evaluation, 7 exp, 9 output)."""
     I = np.ascontiguousarray(I, dtype=np.float32)
     m = np.ascontiguousarray(mask, dtype=np.uint8)
     prm = n4_params(**kw)
@@ -86,7 +87,7 @@ def n4_itk(I, mask, nonpos_raw=False, threads=1, **kw):
     lib().n4_oracle_itk.restype = ct.c_int
     rc = lib().n4_oracle_itk(_ptr(I, ct.c_float), _ptr(m, ct.c_uint8), ct.c_int64(I.shape[0]),
                              ct.c_int64(I.shape[1]), ct.c_int64(I.shape[2]), ct.byref(prm),
-                             ct.c_int(1 if nonpos_raw else 0), ct.c_int(threads),
+                             ct.c_int(1 if nonpos_raw else 0), ct.c_int(threads), ct.c_int(spec),
                              _ptr(out, ct.c_float),
                              _ptr(its, ct.c_int32), _ptr(conv, ct.c_float))
     if rc:

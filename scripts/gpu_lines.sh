@@ -2,10 +2,10 @@
 # GPU-box: the per-config perf lines besides the default bench: config 2
 # (256x256x24, batch 1, sweep driver), config 5 (512^3, batch 1, 3-D morphology), the CI line
 # (defect-voxels/s), and the RCCL path at --gpus 1 (--comm).  Benches first, then rocprofv3 kernel
-# stats for the lines named in PROF (default all).  rocprofv3 7.2 segfaults in its exit path after
-# a run with a cooperative launch (k_n4_pcg: config 2 / 5) although the stats are written, so run
-# those profiles as the LAST step of a call: PROF=config2 or PROF=config5.
-# usage: [PROF="ci comm1"] scripts/gpu_lines.sh TAG
+# stats for the lines named in PROF (default "config2 ci comm1": config 2 first, to show that the
+# exit-time segfault of round 2 under rocprofv3 -- ctypes handles released at interpreter teardown
+# after a cooperative launch -- is gone since the atexit shutdown in _lib.py).
+# usage: [LINES="config2 ci"] [PROF="ci comm1"] scripts/gpu_lines.sh TAG
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -15,13 +15,12 @@ ARGS[config2]="--shape 256 256 24 --batch 1 --steps 10 --warmup 2 --no-cpu-basel
 ARGS[config5]="--shape 512 512 512 --batch 1 --morph3d --steps 2 --warmup 1 --no-cpu-baseline --no-h2h"
 ARGS[ci]="--workload ci --steps 20 --warmup 3"
 ARGS[comm1]="--comm --steps 5 --warmup 1 --no-cpu-baseline --no-h2h"
-if [ -z "${PROF+x}" ]; then
-  for name in config2 config5 ci comm1; do
-    timeout -k 10 600 python3 bench.py ${ARGS[$name]} > gpurun_out/${TAG}_${name}.json 2> gpurun_out/${TAG}_${name}.err
-    rc=$?; echo "$name rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/${TAG}_${name}.err; exit $rc; }
-  done
-  PROF="ci comm1"
-fi
+LINES=${LINES-config2 config5 ci comm1}
+PROF=${PROF-config2 ci comm1}
+for name in $LINES; do
+  timeout -k 10 600 python3 bench.py ${ARGS[$name]} > gpurun_out/${TAG}_${name}.json 2> gpurun_out/${TAG}_${name}.err
+  rc=$?; echo "$name rc=$rc"; [ $rc -eq 0 ] || { tail -5 gpurun_out/${TAG}_${name}.err; exit $rc; }
+done
 for name in $PROF; do
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/${TAG}_${name}_prof -o run -- \
       python3 bench.py ${ARGS[$name]} --no-profile > gpurun_out/${TAG}_${name}_prof.log 2>&1

@@ -354,6 +354,20 @@ def test_large_single_volume_grid_sort_vs_oracle(shape):
     assert np.allclose(list(res[0].km_centres), centres, rtol=1e-12)
 
 
+def test_kmeans_global_tile_prefix_vs_oracle():
+    """A volume with more than 4096 k-means tiles (> 4.19 M masked voxels) takes the multi-workgroup
+    tile sums (k_km_tiles) and the global-memory prefix of k_kmeans: partition and centres against the
+    oracle's Lloyd run on the sorted values; the sorted-list statistics bit-exact."""
+    X, M = synth_volume(336, 336, 192, 43)
+    assert (M > 0).sum() > 4096 * 1024
+    d, bo, lb, res = _lib.vdp(X, M.astype(np.uint8), (1.0, 1.0, 1.0))
+    s = np.sort(X[M > 0].astype(np.float32))
+    counts, centres, _ = O.kmeans_1d_sorted(s)
+    assert int(res[0].n_km0) == int(counts[0])
+    assert np.allclose(list(res[0].km_centres), centres, rtol=1e-12)
+    assert np.float32(res[0].p99) == s[int(len(s) * 0.99)]
+
+
 def test_empty_mask_volume_in_batch():
     """A study with an empty mask must not disturb its neighbours; the class raises IndexError
     like the reference's sorted-list indexing (Vent_Analysis.py:255)."""

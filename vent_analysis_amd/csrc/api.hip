@@ -109,7 +109,7 @@ static void batch_free(vh_batch *b) {
     dfree(b->d_sc); dfree(b->d_part); dfree(b->d_keys0); dfree(b->d_keys1); dfree(b->d_tilecnt);
     dfree(b->d_cohort);
     dfree(b->d_L0); dfree(b->d_lat); dfree(b->d_E);
-    dfree(b->d_numfix); dfree(b->d_rowstart); dfree(b->d_rowmask); dfree(b->d_rrank); dfree(b->d_D); dfree(b->d_perm); dfree(b->d_P1); dfree(b->d_den); dfree(b->d_T);
+    dfree(b->d_numfix); dfree(b->d_rowstart); dfree(b->d_rowmask); dfree(b->d_rrank); dfree(b->d_iscan); dfree(b->d_D); dfree(b->d_perm); dfree(b->d_P1); dfree(b->d_den); dfree(b->d_T);
     dfree(b->d_U); dfree(b->d_ridx); dfree(b->d_cp); dfree(b->d_cvol); dfree(b->d_hpart); dfree(b->d_cpart); dfree(b->d_st); dfree(b->d_nactive); dfree(b->d_tabs); dfree(b->d_twiddle); dfree(b->d_study_lv); dfree(b->d_pcg); dfree(b->d_sortg); dfree(b->d_study_latg);
     dfree(b->d_bitmap); dfree(b->d_ci_list); dfree(b->d_ci_shell); dfree(b->d_ci_hist);
     dfree(b->d_ci_offL); dfree(b->d_ci_bounds); dfree(b->d_ci_radii); dfree(b->d_ci_status);
@@ -572,7 +572,7 @@ int vh_batch_cohort_hist(vh_batch *b, uint64_t *hist) {
 }
 
 const char *vh_batch_kernel_names(void) {
-    return "mask_stats;gather;sort;classify;cohort;kmeans;snr;border;n4_init;n4_den;n4_hist;"
+    return "mask_stats;gather;sort;mean;classify;cohort;kmeans;snr;border;n4_init;n4_den;n4_hist;"
            "n4_fit;n4_contract;n4_eval;n4_welford;n4_pcw;n4_pcg;n4_final;n4_study;ci_walk";
 }
 

@@ -9,6 +9,7 @@
 // Fortran-order linear index L = (i+dx) + (j+dy) s0 + (k+dz) s0 s1 (px2vec, CI.py:65-68), so
 // out-of-range rows/cols alias into neighbouring columns/slices and only 0 <= L < N is required;
 // table rows whose linear offset repeats an earlier row never count (np.intersect1d uniques).
+#include <algorithm>
 #include <climits>
 
 #include "vh_internal.h"
@@ -40,51 +41,73 @@ __global__ void k_ci_bitmap(const uint8_t *__restrict__ defect, int64_t s0, int6
     if (d) list[b * V + (int64_t)(s_base + my)] = (int32_t)v;
 }
 
-__global__ void __launch_bounds__(VH_TPB) k_ci_walk(const uint32_t *__restrict__ bits,
-                                                   const int32_t *__restrict__ list,
-                                                   const unsigned long long *count,
-                                                   const int32_t *__restrict__ offL,
-                                                   const int32_t *__restrict__ bounds, int64_t nbs,
-                                                   int64_t s0, int64_t s1, int64_t s2, int64_t V,
-                                                   int64_t words, int32_t *shell_of,
-                                                   uint32_t *hist, int32_t *status) {
+// One WAVE per defect voxel: the wave walks 64 consecutive table rows per step (lane l probes row
+// r0 + l), the step's hits are one ballot, and the shell boundaries that fall in the step are tested
+// in parallel (lane i takes the i-th boundary in the step: cumulative hits up to row b - 1 are the
+// hits before the step plus a popcount of the ballot's low bits; the first boundary with
+// 2 hits < b stops the walk).  Every probe of the lockstep lane-per-voxel form is made (same rows,
+// same order of boundaries), but a 128x128x24 study's ~6k defect voxels now fill ~6k waves instead
+// of ~93.  The defect bitmap sits in LDS when it fits (48 KiB at 128x128x24).
+#define CIW_TPB 1024
+#define CIW_LDS_WORDS (40 * 1024)   // bitmaps up to 160 KiB in LDS (V <= 1.3 M voxels)
+__global__ void __launch_bounds__(CIW_TPB) k_ci_walk(const uint32_t *__restrict__ bits,
+                                                    const int32_t *__restrict__ list,
+                                                    const unsigned long long *count,
+                                                    const int32_t *__restrict__ offL, int64_t rows,
+                                                    const int32_t *__restrict__ bounds, int64_t nbs,
+                                                    int64_t s0, int64_t s1, int64_t s2, int64_t V,
+                                                    int64_t words, int use_lds, int32_t *shell_of,
+                                                    uint32_t *hist, int32_t *status) {
+    extern __shared__ uint32_t s_bits[];
     const int64_t b = blockIdx.y;
     const int64_t n = (int64_t)count[b];
-    const int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if ((int64_t)blockIdx.x * blockDim.x >= n) return;   // block-uniform exit
-    const bool valid = idx < n;
-    int64_t base = 0;
-    int32_t v = 0;
-    if (valid) {
-        v = list[b * V + idx];
-        const int64_t i = v / (s1 * s2), j = (v / s2) % s1, k = v % s2;
-        base = i + j * s0 + k * s0 * s1;
+    constexpr int W = CIW_TPB / 64;
+    if ((int64_t)blockIdx.x * W >= n) return;   // block-uniform exit
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t *bm = bits + b * words;
+    if (use_lds) {
+        for (int64_t i = threadIdx.x; i < words; i += CIW_TPB) s_bits[i] = bm[i];
+        __syncthreads();
+        bm = s_bits;
     }
     const int64_t N = s0 * s1 * s2;
-    const uint32_t *bm = bits + b * words;
-    bool done = !valid;
-    int32_t qstop = -1;
-    int64_t hits = 0;
-    int64_t row = 0;
-    for (int64_t q = 0; q < nbs; ++q) {
-        if (__all(done)) break;
-        const int64_t bq = bounds[q];
-        for (; row < bq; ++row) {
-            const int32_t off = offL[row];
-            if (!done && off != CI_SENTINEL) {
+    for (int64_t idx = (int64_t)blockIdx.x * W + w; idx < n; idx += (int64_t)gridDim.x * W) {
+        const int32_t v = list[b * V + idx];
+        const int64_t i = v / (s1 * s2), j = (v / s2) % s1, k = v % s2;
+        const int64_t base = i + j * s0 + k * s0 * s1;   // px2vec (Fortran order, CI.py:65-68)
+        int64_t hits = 0, q = 0, row = 0;
+        int32_t qstop = -1;
+        while (q < nbs && row < rows) {
+            const int64_t r = row + lane;
+            bool hit = false;
+            if (r < rows) {
+                const int32_t off = offL[r];
                 const int64_t L = base + off;
-                if (L >= 0 && L < N) hits += (bm[L >> 5] >> (L & 31)) & 1u;
+                hit = off != CI_SENTINEL && L >= 0 && L < N && ((bm[L >> 5] >> (L & 31)) & 1u);
             }
+            const uint64_t bal = __ballot(hit);
+            const int64_t bq = q + lane < nbs ? (int64_t)bounds[q + lane] : INT64_MAX;
+            const bool inc = bq <= row + 64;   // boundaries in (row, row + 64]: a prefix of the lanes
+            bool stop = false;
+            if (inc) {
+                const int pos = (int)(bq - 1 - row);   // 0 .. 63
+                const uint64_t m = pos == 63 ? ~0ull : ((2ull << pos) - 1ull);
+                stop = 2 * (hits + __popcll(bal & m)) < bq;
+            }
+            const uint64_t sb = __ballot(stop);
+            if (sb) {
+                qstop = (int32_t)(q + __builtin_ctzll(sb));
+                break;
+            }
+            q += __popcll(__ballot(inc));
+            hits += __popcll(bal);
+            row += 64;
         }
-        if (!done && 2 * hits < bq) {
-            done = true;
-            qstop = (int32_t)q;
+        if (lane == 0) {
+            shell_of[b * V + v] = qstop;
+            if (qstop >= 0) atomicAdd(&hist[b * nbs + qstop], 1u);
+            else atomicExch(&status[b], 1);
         }
-    }
-    if (valid) {
-        shell_of[b * V + v] = qstop;
-        if (qstop >= 0) atomicAdd(&hist[b * nbs + qstop], 1u);
-        else atomicExch(&status[b], 1);
     }
 }
 
@@ -178,9 +201,15 @@ void vh_ci_run(vh_batch *b, const int16_t *offs, const uint8_t *dup, int64_t row
     VH_CHECK_LAUNCH();
     {
         ScopedKTimer tm(b, "ci_walk", 0.0);
-        k_ci_walk<<<vg, VH_TPB, 0, st>>>(b->d_bitmap, b->d_ci_list, d_count, d_offL, d_bounds, nbs,
-                                         b->R, b->C, b->Z, b->V, words, b->d_ci_shell,
-                                         b->d_ci_hist, d_status);
+        // one wave per defect voxel: up to V waves per volume, 16 per block, grid-strided beyond
+        // 16384 blocks per volume; the block reads the volume's defect count itself
+        const int64_t wg = std::min<int64_t>((b->V + CIW_TPB / 64 - 1) / (CIW_TPB / 64), 16384);
+        const int use_lds = words <= CIW_LDS_WORDS ? 1 : 0;
+        vh_set_max_lds((const void *)k_ci_walk, 160 * 1024);
+        k_ci_walk<<<dim3((unsigned)wg, (unsigned)b->nb), CIW_TPB,
+                    use_lds ? sizeof(uint32_t) * (size_t)words : 0, st>>>(
+            b->d_bitmap, b->d_ci_list, d_count, d_offL, rows, d_bounds, nbs, b->R, b->C, b->Z, b->V,
+            words, use_lds, b->d_ci_shell, b->d_ci_hist, d_status);
         VH_CHECK_LAUNCH();
     }
     k_ci_finish<<<(unsigned)((b->nb + 63) / 64), 64, 0, st>>>(b->d_ci_hist, d_count, d_radii, nbs,

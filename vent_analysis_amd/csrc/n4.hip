@@ -404,6 +404,129 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_rowscan(int32_t *rs, int64_t n) {
     for (int64_t i = s0; i < e0; ++i) { const int32_t v = a[i]; a[i] = (int32_t)run; run += v; }
 }
 
+// ---- the same two scans for large volumes, over the whole GPU (config 5: the one-workgroup forms
+// above took 3.5 + 3.9 ms of a 154 ms study) -------------------------------------------------------
+#define RS_CH 4096   // entries per chunk of the flat row-start scan (16 per thread)
+__device__ __forceinline__ int32_t block_excl_scan_i32(int32_t v, int32_t *s_w, int32_t &total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int32_t inc = v;
+    for (int off = 1; off < 64; off <<= 1) {
+        const int32_t y = __shfl_up(inc, off, 64);
+        if (lane >= off) inc += y;
+    }
+    if (lane == 63) s_w[w] = inc;
+    __syncthreads();
+    int32_t base = 0;
+    total = 0;
+    for (int q = 0; q < VH_TPB / 64; ++q) {
+        if (q < w) base += s_w[q];
+        total += s_w[q];
+    }
+    return base + inc - v;
+}
+// pass 1: chunk sums
+__global__ void __launch_bounds__(VH_TPB) k_n4_rowscan_parts(const int32_t *rs, int64_t n, int32_t *parts,
+                                                            int64_t ncs) {
+    __shared__ int32_t s_w[VH_TPB / 64];
+    const int64_t b = blockIdx.y, c0 = (int64_t)blockIdx.x * RS_CH;
+    const int32_t *a = rs + b * n;
+    int32_t acc = 0;
+    for (int64_t i = c0 + threadIdx.x; i < n && i < c0 + RS_CH; i += VH_TPB) acc += a[i];
+    int32_t tot;
+    (void)block_excl_scan_i32(acc, s_w, tot);
+    if (threadIdx.x == 0) parts[b * ncs + blockIdx.x] = tot;
+}
+// pass 2: exclusive scan of the chunk sums of each volume (in place)
+__global__ void __launch_bounds__(VH_TPB) k_n4_rowscan_top(int32_t *parts, int64_t ncs) {
+    __shared__ int32_t s_w[VH_TPB / 64];
+    int32_t *p = parts + blockIdx.x * ncs;
+    int32_t carry = 0;
+    for (int64_t c0 = 0; c0 < ncs; c0 += VH_TPB) {
+        const int64_t i = c0 + threadIdx.x;
+        const int32_t v = i < ncs ? p[i] : 0;
+        int32_t tot;
+        const int32_t ex = block_excl_scan_i32(v, s_w, tot);
+        if (i < ncs) p[i] = carry + ex;
+        carry += tot;
+        __syncthreads();
+    }
+}
+// pass 3: each chunk's exclusive scan (16 consecutive entries per thread) plus its offset, in place
+__global__ void __launch_bounds__(VH_TPB) k_n4_rowscan_apply(int32_t *rs, int64_t n, const int32_t *parts,
+                                                            int64_t ncs) {
+    __shared__ int32_t s_w[VH_TPB / 64];
+    const int64_t b = blockIdx.y, c0 = (int64_t)blockIdx.x * RS_CH;
+    int32_t *a = rs + b * n;
+    const int64_t i0 = c0 + (int64_t)threadIdx.x * (RS_CH / VH_TPB);
+    int32_t v[RS_CH / VH_TPB];
+    int32_t acc = 0;
+#pragma unroll
+    for (int q = 0; q < RS_CH / VH_TPB; ++q) {
+        v[q] = i0 + q < n ? a[i0 + q] : 0;
+        acc += v[q];
+    }
+    int32_t tot;
+    int32_t run = parts[b * ncs + blockIdx.x] + block_excl_scan_i32(acc, s_w, tot);
+#pragma unroll
+    for (int q = 0; q < RS_CH / VH_TPB; ++q)
+        if (i0 + q < n) {
+            a[i0 + q] = run;
+            run += v[q];
+        }
+}
+// raster ranks, pass 1: per (chunk of 64 tiles, volume) and row, the running count over the chunk's
+// tiles (local) and the chunk's total per row (rows across threads: coalesced)
+#define RR_CH 64
+__global__ void __launch_bounds__(VH_TPB) k_n4_rr_chunk(const uint64_t *rowmask, int64_t R, int64_t ntiles,
+                                                       int32_t *rrank, int32_t *ctot, int64_t nrc) {
+    const int64_t b = blockIdx.y, t0 = (int64_t)blockIdx.x * RR_CH;
+    const int64_t t1 = t0 + RR_CH < ntiles ? t0 + RR_CH : ntiles;
+    const uint64_t *rm = rowmask + b * ntiles * R;
+    int32_t *rr = rrank + b * ntiles * R;
+    for (int64_t x = threadIdx.x; x < R; x += VH_TPB) {
+        int32_t run = 0;
+        for (int64_t t = t0; t < t1; ++t) {
+            rr[t * R + x] = run;
+            run += __popcll(rm[t * R + x]);
+        }
+        ctot[(b * (nrc + 1) + blockIdx.x) * R + x] = run;
+    }
+}
+// pass 2 (one block per volume): per row, exclusive prefix over the chunks (in place); the row
+// totals' exclusive prefix over the rows into the extra chunk row nrc
+__global__ void __launch_bounds__(VH_TPB) k_n4_rr_top(int32_t *ctot, int64_t R, int64_t nrc) {
+    __shared__ int32_t s_w[VH_TPB / 64];
+    int32_t *c = ctot + blockIdx.x * (nrc + 1) * R;
+    int32_t carry = 0;
+    for (int64_t x0 = 0; x0 < R; x0 += VH_TPB) {
+        const int64_t x = x0 + threadIdx.x;
+        int32_t run = 0;
+        if (x < R)
+            for (int64_t q = 0; q < nrc; ++q) {
+                const int32_t v = c[q * R + x];
+                c[q * R + x] = run;
+                run += v;
+            }
+        int32_t tot;
+        const int32_t ex = block_excl_scan_i32(x < R ? run : 0, s_w, tot);
+        if (x < R) c[nrc * R + x] = carry + ex;
+        carry += tot;
+        __syncthreads();
+    }
+}
+// pass 3: the chunk offset and the row base added to every (tile, row)
+__global__ void __launch_bounds__(VH_TPB) k_n4_rr_apply(int64_t R, int64_t ntiles, int32_t *rrank,
+                                                       const int32_t *ctot, int64_t nrc) {
+    const int64_t b = blockIdx.y, t0 = (int64_t)blockIdx.x * RR_CH;
+    const int64_t t1 = t0 + RR_CH < ntiles ? t0 + RR_CH : ntiles;
+    const int32_t *c = ctot + b * (nrc + 1) * R;
+    int32_t *rr = rrank + b * ntiles * R;
+    for (int64_t x = threadIdx.x; x < R; x += VH_TPB) {
+        const int32_t off = c[blockIdx.x * R + x] + c[nrc * R + x];
+        for (int64_t t = t0; t < t1; ++t) rr[t * R + x] += off;
+    }
+}
+
 // Raster rank of the first masked voxel of every (tile, row): masked voxels before row x plus
 // those of row x in tiles before t -- the position of the voxel in ITK's raster-order scans (the
 // convergence recurrence S7).  One block per volume; dynamic LDS holds the R row totals.
@@ -1788,12 +1911,38 @@ void vh_launch_n4(vh_batch *b, const vh_n4_params &prm) {
         k_n4_rowcount<<<dim3((unsigned)ntiles, (unsigned)b->nb), 64, 0, st>>>(
             b->d_colbits, b->R, b->CZ, ntiles, b->d_rowstart, b->d_rowmask);
         VH_CHECK_LAUNCH();
-        k_n4_rowscan<<<(unsigned)b->nb, VH_TPB, 0, st>>>(b->d_rowstart, ntiles * b->R);
-        VH_CHECK_LAUNCH();
-        if (b->R > 16384) throw VhError{VH_ERR_ARG, "N4: more than 16384 rows"};
-        k_n4_rrank<<<(unsigned)b->nb, VH_TPB, sizeof(int32_t) * (size_t)b->R, st>>>(
-            b->d_rowmask, b->d_rowstart, b->R, ntiles, b->VS, b->d_rrank, b->d_perm);
-        VH_CHECK_LAUNCH();
+        const int64_t nrs = ntiles * b->R;
+        if (nrs <= ((int64_t)1 << 16)) {   // small volumes (the bench): one workgroup per volume
+            k_n4_rowscan<<<(unsigned)b->nb, VH_TPB, 0, st>>>(b->d_rowstart, nrs);
+            VH_CHECK_LAUNCH();
+            if (b->R > 16384) throw VhError{VH_ERR_ARG, "N4: more than 16384 rows"};
+            k_n4_rrank<<<(unsigned)b->nb, VH_TPB, sizeof(int32_t) * (size_t)b->R, st>>>(
+                b->d_rowmask, b->d_rowstart, b->R, ntiles, b->VS, b->d_rrank, b->d_perm);
+            VH_CHECK_LAUNCH();
+        } else {   // large volumes: chunked scans over the GPU
+            const int64_t ncs = (nrs + RS_CH - 1) / RS_CH, nrc = (ntiles + RR_CH - 1) / RR_CH;
+            const int64_t need = b->nb * std::max(ncs, (nrc + 1) * b->R);
+            if (need > b->iscan_cap) {
+                if (b->d_iscan) HIP_TRY(hipFree(b->d_iscan));
+                b->d_iscan = nullptr;
+                b->iscan_cap = 0;
+                HIP_TRY(hipMalloc(&b->d_iscan, sizeof(int32_t) * need));
+                b->iscan_cap = need;
+            }
+            const dim3 gs((unsigned)ncs, (unsigned)b->nb), gr((unsigned)nrc, (unsigned)b->nb);
+            k_n4_rowscan_parts<<<gs, VH_TPB, 0, st>>>(b->d_rowstart, nrs, b->d_iscan, ncs);
+            VH_CHECK_LAUNCH();
+            k_n4_rowscan_top<<<(unsigned)b->nb, VH_TPB, 0, st>>>(b->d_iscan, ncs);
+            VH_CHECK_LAUNCH();
+            k_n4_rowscan_apply<<<gs, VH_TPB, 0, st>>>(b->d_rowstart, nrs, b->d_iscan, ncs);
+            VH_CHECK_LAUNCH();
+            k_n4_rr_chunk<<<gr, VH_TPB, 0, st>>>(b->d_rowmask, b->R, ntiles, b->d_rrank, b->d_iscan, nrc);
+            VH_CHECK_LAUNCH();
+            k_n4_rr_top<<<(unsigned)b->nb, VH_TPB, 0, st>>>(b->d_iscan, b->R, nrc);
+            VH_CHECK_LAUNCH();
+            k_n4_rr_apply<<<gr, VH_TPB, 0, st>>>(b->R, ntiles, b->d_rrank, b->d_iscan, nrc);
+            VH_CHECK_LAUNCH();
+        }
         const int64_t pairs = ntiles * b->R;
         k_n4_perm<<<dim3((unsigned)((pairs + VH_TPB / 64 - 1) / (VH_TPB / 64)), (unsigned)b->nb), VH_TPB, 0, st>>>(
             b->d_rowmask, b->d_rowstart, b->d_rrank, b->R, ntiles, b->VS, b->d_perm);

@@ -794,6 +794,10 @@ struct PcShared {
     int agFirst[NL / 64];
     // exact sig after stage 0 (pcx_*): t-slot allocator, result tag, walks taken
     int xslots, xdone, xwalks, xslow;
+#ifdef PC_PROF
+    int pchg[32], pwav[32];   // stage-0 rounds: blocks whose start changed, waves that ran
+    unsigned long long xwcyc, xscyc;   // PCX scan: cycles in walks, whole scan
+#endif
     // pass-0 block sums of p - 1 and (p - 1)^2 (double, 16-aligned pair over gmu_o .. sp1: those
     // fields are written by round 0 before they are next read)
     __device__ double &s1(int j) { return *reinterpret_cast<double *>(&b[j].gmu_o); }
@@ -1057,35 +1061,61 @@ __device__ __forceinline__ void pc_block_apx(const float *P, uint32_t j, uint32_
 // scan (shuffles), per-wave aggregates in LDS, then each wave composes the aggregates before it.
 // Fixed order, so deterministic; exact zeros stay exact zeros (the property the convergence proof
 // uses: a block whose predecessors all matched gets the exact predecessor end).
+// a double from the DPP source lane (CTRL / RMASK as __builtin_amdgcn_update_dpp); lanes with no
+// source, or in rows the mask leaves out, get `id`
+template <int CTRL, int RMASK>
+__device__ __forceinline__ double dpp_d(double v, double id) {
+    const long long x = __double_as_longlong(v), y = __double_as_longlong(id);
+    const int lo = __builtin_amdgcn_update_dpp((int)y, (int)x, CTRL, RMASK, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(y >> 32), (int)(x >> 32), CTRL, RMASK, 0xf, false);
+    return __longlong_as_double(((long long)hi << 32) | (long long)(uint32_t)lo);
+}
+// one Hillis-Steele step of the affine scan: (A, B) <- (A, B) o (lane source's (A, B)); Bs sums
+template <int CTRL, int RMASK>
+__device__ __forceinline__ void aff_step(double &A, double &B, double &Bs) {
+    const double ya = dpp_d<CTRL, RMASK>(A, 1.0), yb = dpp_d<CTRL, RMASK>(B, 0.0), ys = dpp_d<CTRL, RMASK>(Bs, 0.0);
+    B = A * yb + B;
+    A = A * ya;
+    Bs = ys + Bs;
+}
 template <int NL>
 __device__ __forceinline__ void pcw_scan(PcShared<NL> &S, double a, double b, double bs, double &dm,
                                          double &ds) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     double A = a, B = b, Bs = bs;
-    for (int off = 1; off < 64; off <<= 1) {
-        const double ya = __shfl_up(A, off, 64), yb = __shfl_up(B, off, 64), ys = __shfl_up(Bs, off, 64);
-        if (lane >= off) {
-            B = A * yb + B;
-            A = A * ya;
-            Bs = ys + Bs;
-        }
-    }
+    // inclusive wave scan with DPP (row shifts, then the row broadcasts of gfx9): VALU moves instead
+    // of 36 dependent ds_bpermute round trips
+    aff_step<0x111, 0xf>(A, B, Bs);   // row_shr:1
+    aff_step<0x112, 0xf>(A, B, Bs);   // row_shr:2
+    aff_step<0x114, 0xf>(A, B, Bs);   // row_shr:4
+    aff_step<0x118, 0xf>(A, B, Bs);   // row_shr:8
+    aff_step<0x142, 0xa>(A, B, Bs);   // row_bcast:15 -> rows 1, 3
+    aff_step<0x143, 0xc>(A, B, Bs);   // row_bcast:31 -> rows 2, 3
     if (lane == 63) {
         S.agA[w] = A;
         S.agB[w] = B;
         S.agS[w] = Bs;
     }
-    double ea = __shfl_up(A, 1, 64), eb = __shfl_up(B, 1, 64), es = __shfl_up(Bs, 1, 64);
-    if (lane == 0) {
-        ea = 1.0;
-        eb = 0.0;
-        es = 0.0;
-    }
+    const double ea = dpp_d<0x138, 0xf>(A, 1.0), eb = dpp_d<0x138, 0xf>(B, 0.0),   // wave_shr:1
+                 es = dpp_d<0x138, 0xf>(Bs, 0.0);
     __syncthreads();
-    double pb = 0.0, ps = 0.0;   // aggregates of the waves before this one, applied to delta = 0
-    for (int v = 0; v < w; ++v) {
-        pb = S.agA[v] * pb + S.agB[v];
-        ps = ps + S.agS[v];
+    // the waves before this one: lanes v < w hold wave v's aggregate, scanned across the row (NL / 64
+    // <= 16 waves: one row), lane w - 1 has their composition applied to delta = 0
+    static_assert(NL / 64 <= 16, "one DPP row of wave aggregates");
+    double gA = 1.0, gB = 0.0, gS = 0.0;
+    if (lane < w) {
+        gA = S.agA[lane];
+        gB = S.agB[lane];
+        gS = S.agS[lane];
+    }
+    aff_step<0x111, 0xf>(gA, gB, gS);
+    aff_step<0x112, 0xf>(gA, gB, gS);
+    aff_step<0x114, 0xf>(gA, gB, gS);
+    aff_step<0x118, 0xf>(gA, gB, gS);
+    double pb = 0.0, ps = 0.0;
+    if (w > 0) {
+        pb = __shfl(gB, w - 1, 64);
+        ps = __shfl(gS, w - 1, 64);
     }
     dm = ea * pb + eb;
     ds = ps + es;
@@ -1401,6 +1431,9 @@ __device__ bool pcx_scan(PcShared<NL> &S, const PcMap &m, const float *P, const 
             continue;
         }
         const PcX x = pcx_of(S, j);   // block j: walked exactly
+#ifdef PC_PROF
+        const unsigned long long cw0 = clock64();
+#endif
         if ((x.flags & PCX_CANDF) && x.slot >= 0) {
             const double a0 = j == nxt ? pf0 : 0.0, a1 = j == nxt ? pf1 : 0.0;
             const bool mine = j == nxt;
@@ -1414,6 +1447,9 @@ __device__ bool pcx_scan(PcShared<NL> &S, const PcMap &m, const float *P, const 
             s = pcx_walk_mu<NL>(S, m, P, j, s);
             ++slow;
         }
+#ifdef PC_PROF
+        if (lane == 0) S.xwcyc += clock64() - cw0;
+#endif
         ++walks;
         ++j;
     }
@@ -1452,26 +1488,42 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
     unsigned long long c1 = 0, c2 = 0;
     int ra = 0;
 #endif
+    // pass 0: p = exp(d) from raster order into block layout (P[s NL + j]) and the block sums.  A
+    // block's d values are consecutive in raster order, so one thread reading its own block touched
+    // 64 cache lines per wave-wide load; instead the workgroup loads each group of PC_G0 steps of
+    // all blocks together (8 lanes per block: 32-byte runs) and transposes it through LDS (the
+    // PcShared area, rewritten after this pass; rows padded by 8 floats against bank conflicts).
+    constexpr int G0 = 8, TS = PC_TPB + 8;
+    static_assert(sizeof(float) * G0 * TS <= sizeof(PcShared<PC_TPB>), "pass-0 transpose buffer");
+    float *const T0 = reinterpret_cast<float *>(&S);
+    const uint32_t lmax = m.L + (m.rem ? 1u : 0u);
+    double s1 = 0.0, s2 = 0.0;
+    for (uint32_t g0 = 0; g0 < lmax; g0 += G0) {
+        for (int e = tid; e < G0 * PC_TPB; e += PC_TPB) {
+            const uint32_t jb = (uint32_t)e / G0, i = (uint32_t)e % G0;
+            const uint32_t lb = pc_len(m, jb);
+            T0[i * TS + jb] = g0 + i < lb ? ld((int64_t)(pc_k0(m, jb) - 1u + g0 + i)) : 0.0f;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < G0; ++i)
+            if (g0 + i < len) {
+                const float p = expf_cr(T0[i * TS + j]);
+                P[(size_t)(g0 + i) * PC_TPB + j] = p;
+                const double e = (double)p - 1.0;
+                s1 += e;
+                s2 = fma(e, e, s2);
+            }
+        __syncthreads();
+    }
     if (tid == 0) {   // flags from an earlier call (or other phases' use of this LDS) must not match
         S.done = 0;
         S.fallback = 0;
         S.xdone = 0;
     }
-    double s1 = 0.0, s2 = 0.0;
-    for (uint32_t s0 = 0; s0 < len; s0 += 8) {
-        float v[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = s0 + i < len ? ld((int64_t)(k0 - 1u + s0 + i)) : 0.0f;
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-            if (s0 + i < len) {
-                const float p = expf_cr(v[i]);
-                P[(size_t)(s0 + i) * PC_TPB + j] = p;
-                const double e = (double)p - 1.0;
-                s1 += e;
-                s2 = fma(e, e, s2);
-            }
-    }
+#ifdef PC_PROF
+    if (tid < 32) S.pchg[tid] = S.pwav[tid] = 0;
+#endif
     S.s1(j) = s1;
     S.s2(j) = s2;
     __syncthreads();
@@ -1509,6 +1561,10 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
             cbs[1] = clock64() - cxt;   // T pass (reported as stage1 blocks)
 #endif
             if (tid < 64) {
+#ifdef PC_PROF
+                if (tid == 0) S.xwcyc = 0;
+                const unsigned long long csc = clock64();
+#endif
                 float sg = 0.0f;
                 int w = 0, slow = 0;
                 const bool ok = pcx_scan<PC_TPB>(S, m, P, tbuf, sg, w, slow);
@@ -1522,6 +1578,9 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
                     }
                     S.xwalks = ok ? w : -1;
                     S.xslow = slow;
+#ifdef PC_PROF
+                    S.xscyc = clock64() - csc;
+#endif
                 }
             }
             __syncthreads();
@@ -1546,6 +1605,13 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
 #endif
             const float g = S.b[j].gmu, gs = S.b[j].gsig;
             const bool same = __float_as_uint(g) == __float_as_uint(lg) && __float_as_uint(gs) == __float_as_uint(ls);
+#ifdef PC_PROF
+            if (pass == 0 && ra0 < 32 && (tid & 63) == 0) {
+                const uint64_t bq = __ballot(!same);
+                atomicAdd(&S.pchg[ra0], __popcll(bq));
+                atomicAdd(&S.pwav[ra0], bq != 0ull);
+            }
+#endif
             if (__ballot(!same) != 0ull && !same) {
                 float mu = g, sig = gs;
                 if (pass == 0) pc_block_apx<PC_TPB, false>(P, j, len, k0, mu, sig);
@@ -1604,6 +1670,9 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
                    " | stage0 %d rounds %llu cyc (blocks %llu) stage1 %d rounds %llu cyc (blocks %llu) xsig %d walks %d\n",
                    (long long)n, ra, S.rounds - ra + 0, S.fallback == tagb, c1 - c0, c2 - c1, cblk, clock64() - c2,
                    rst[0], cst[0], cbs[0], rst[1], cst[1], cbs[1], (int)xs, S.xwalks * 1000 + S.xslow);
+        if (blockIdx.x == 0)
+            for (int r = 0; r < rst[0] && r < 32; ++r) printf("PCW_RND %d chg %d waves %d\n", r, S.pchg[r], S.pwav[r]);
+        if (blockIdx.x == 0 && xs) printf("PCW_X scan %llu walks %llu\n", S.xscyc, S.xwcyc);
 #endif
     }
 }

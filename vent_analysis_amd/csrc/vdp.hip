@@ -1416,8 +1416,26 @@ __device__ __forceinline__ int64_t km_boundary(const uint32_t *k, int64_t n, dou
     return lo + (__ffsll((long long)__ballot(pr)) - 1);
 }
 
-// One block (4 waves) per volume.  Cluster sums: head partial tile + whole-tile sums + tail
-// partial tile, in tile order (deterministic).
+// Tile sums of a volume too large for the LDS prefix (more than KM_LDS_TILES tiles: e.g. one 512^3
+// study, 27k tiles), over the whole GPU: one wave per tile (the same km_tile_sum arithmetic), into
+// the volume's global tile array; k_kmeans then prefixes it once.  (One workgroup summing every tile
+// took 16 ms of config 5's 154 ms.)
+__global__ void __launch_bounds__(KM_TPB) k_km_tiles(const uint32_t *__restrict__ keys, int64_t V,
+                                                    double *tile_scratch, int64_t max_ktiles,
+                                                    const VolScalars *sc) {
+    const int64_t b = blockIdx.y;
+    const int64_t n = sc[b].n_mask;
+    const int64_t nt = (n + KM_TILE - 1) / KM_TILE;
+    if (nt <= KM_LDS_TILES) return;   // k_kmeans sums these itself, in LDS
+    const int64_t tt = (int64_t)blockIdx.x * (KM_TPB / 64) + (threadIdx.x >> 6);
+    if (tt >= nt) return;
+    const double ts = km_tile_sum(keys + b * V, tt, 0, n);
+    if ((threadIdx.x & 63) == 0) tile_scratch[b * (max_ktiles + 1) + tt] = ts;
+}
+
+// One block (16 waves) per volume.  Cluster sums: head partial tile + whole tiles (a difference of
+// the exclusive prefix of the tile sums, in LDS or -- large volumes, tile sums from k_km_tiles -- in
+// global memory) + tail partial tile (deterministic: fixed orders throughout).
 __global__ void __launch_bounds__(KM_TPB) k_kmeans(const uint32_t *__restrict__ keys,
                                                   int64_t V, double *tile_scratch,
                                                   int64_t max_ktiles, VolScalars *sc) {
@@ -1433,15 +1451,13 @@ __global__ void __launch_bounds__(KM_TPB) k_kmeans(const uint32_t *__restrict__ 
     const uint32_t *k = keys + b * V;
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     const int64_t nt = (n + KM_TILE - 1) / KM_TILE;
-    double *gt = tile_scratch + b * max_ktiles;
+    double *gt = tile_scratch + b * (max_ktiles + 1);   // [nt + 1]: tile sums -> their exclusive prefix
     const bool in_lds = nt <= KM_LDS_TILES;
-    for (int64_t tt = w; tt < nt; tt += KM_TPB / 64) {
-        const double ts = km_tile_sum(k, tt, 0, n);
-        if (lane == 0) {
-            if (in_lds) s_tiles[tt] = ts;
-            else gt[tt] = ts;
+    if (in_lds)
+        for (int64_t tt = w; tt < nt; tt += KM_TPB / 64) {
+            const double ts = km_tile_sum(k, tt, 0, n);
+            if (lane == 0) s_tiles[tt] = ts;
         }
-    }
     const int64_t stride = n <= (int64_t)KM_SAMPLES * 64 ? 64 : (n + KM_SAMPLES - 1) / KM_SAMPLES;
     const int64_t ns = (n - 1) / stride + 1;   // samples at 0, stride, 2 stride, ... < n
     for (int64_t j = t; j < ns; j += KM_TPB) s_samp[j] = key2f(k[j * stride]);
@@ -1464,6 +1480,24 @@ __global__ void __launch_bounds__(KM_TPB) k_kmeans(const uint32_t *__restrict__ 
         for (int ww = 0; ww < w; ++ww) run += s_wtot[ww];
         for (int64_t tt = t0; tt < t1; ++tt) { s_tiles[tt] = run; run += tv[tt - t0]; }
         if (t1 == nt && t0 < t1) s_tiles[nt] = run;
+    } else {   // the same fixed-order prefix over k_km_tiles' sums, in place in global memory
+        const int64_t per = (nt + KM_TPB - 1) / KM_TPB;
+        const int64_t t0 = (int64_t)t * per, t1 = t0 + per < nt ? t0 + per : nt;
+        double mine = 0.0;
+        for (int64_t tt = t0; tt < t1; ++tt) mine += gt[tt];
+        double inc = mine;
+        for (int off = 1; off < 64; off <<= 1) {
+            const double o = __shfl_up(inc, off, 64);
+            if (lane >= off) inc += o;
+        }
+        double run = __shfl_up(inc, 1, 64);
+        if (lane == 0) run = 0.0;
+        if (lane == 63) s_wtot[w] = inc;
+        __syncthreads();
+        for (int ww = 0; ww < w; ++ww) run += s_wtot[ww];
+        for (int64_t tt = t0; tt < t1; ++tt) { const double v = gt[tt]; gt[tt] = run; run += v; }
+        if (t1 == nt && t0 < t1) gt[nt] = run;
+        __threadfence_block();
     }
     if (t < KM_K) s_c[t] = (double)key2f(k[(n * (2 * t + 1)) / (2 * KM_K)]);
     if (t == 0) { s_cut[0] = -1; s_done = 0; }
@@ -1493,18 +1527,9 @@ __global__ void __launch_bounds__(KM_TPB) k_kmeans(const uint32_t *__restrict__ 
                 const int64_t ta = a / KM_TILE, te = (e - 1) / KM_TILE;
                 double head, tail;
                 km_tile_sum2(k, ta, te, a, e, head, tail);
-                double mid = 0.0;   // tiles held in global memory (large volumes): the wave sums them
-                if (!in_lds) {      // in a fixed order (lane-strided partials, shuffle tree)
-                    for (int64_t tt = ta + 1 + lane; tt < te; tt += 64) mid += gt[tt];
-                    for (int off = 32; off > 0; off >>= 1) mid += __shfl_down(mid, off, 64);
-                }
                 if (lane == 0) {
                     double sum = head;
-                    if (in_lds) {
-                        if (te > ta + 1) sum += s_tiles[te] - s_tiles[ta + 1];
-                    } else {
-                        sum += mid;
-                    }
+                    if (te > ta + 1) sum += in_lds ? s_tiles[te] - s_tiles[ta + 1] : gt[te] - gt[ta + 1];
                     if (te != ta) sum += tail;
                     s_c[w] = sum / (double)(e - a);
                 }
@@ -1717,6 +1742,7 @@ void vh_launch_vdp_chain(vh_batch *b, const float *d_n4, const vh_run_opts &o) {
         }
     }
     {
+        ScopedKTimer tm(b, "mean", 0.0);
         const int64_t max_chunks = (b->V + 8191) / 8192;
         float *chunk = reinterpret_cast<float *>(b->d_part);   // part holds >= nb*max_chunks floats
         k_chunk_sums<<<dim3((unsigned)((max_chunks + VH_TPB / 64 - 1) / (VH_TPB / 64)), (unsigned)b->nb),
@@ -1765,7 +1791,13 @@ void vh_launch_vdp_chain(vh_batch *b, const float *d_n4, const vh_run_opts &o) {
     if (o.do_kmeans) {
         ScopedKTimer tm(b, "kmeans", 0.0);
         const int64_t max_ktiles = (b->V + KM_TILE - 1) / KM_TILE;
-        double *scratch = reinterpret_cast<double *>(b->d_keys1);   // free after the sort (4V >= 8V/1024 B)
+        // free after the sort: 4V bytes per volume >= 8 (V / 1024 + 1)
+        double *scratch = reinterpret_cast<double *>(b->d_keys1);
+        if (max_ktiles > KM_LDS_TILES) {
+            k_km_tiles<<<dim3((unsigned)((max_ktiles + KM_TPB / 64 - 1) / (KM_TPB / 64)), (unsigned)b->nb),
+                         KM_TPB, 0, st>>>(b->d_keys0, b->V, scratch, max_ktiles, b->d_sc);
+            VH_CHECK_LAUNCH();
+        }
         k_kmeans<<<(unsigned)b->nb, KM_TPB, 0, st>>>(b->d_keys0, b->V, scratch, max_ktiles, b->d_sc);
         VH_CHECK_LAUNCH();
     }

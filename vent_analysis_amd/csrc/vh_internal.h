@@ -170,6 +170,8 @@ struct vh_batch {
     int32_t *d_rowstart = nullptr;   // [nb][tiles][R] compact offset of each (64-column tile, row)
     uint64_t *d_rowmask = nullptr;   // [nb][tiles][R] mask == 1 lanes of each (tile, row)
     int32_t *d_rrank = nullptr;      // [nb][tiles][R] raster rank of the first masked voxel of (tile, row)
+    int32_t *d_iscan = nullptr;      // large volumes: chunk sums of the row-start / raster-rank scans
+    int64_t iscan_cap = 0;
     float *d_D = nullptr;            // [nb][VS] B_old - B_new (S7 input): compact order (n4), raster order (n4_study)
     int32_t *d_perm = nullptr;       // [nb][VS] raster rank -> compact index of the mask == 1 voxels (n4)
     // compact N4 state: mask==1 voxels in tile-row order, volume stride VS
