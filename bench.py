@@ -218,16 +218,33 @@ def main_ci(args):
         d = d.astype(np.uint8)
         for _ in range(max(1, args.warmup)):
             ci, sc, shell = _lib.ci(d, table, float(np.min(vox)))
+        if not args.no_profile:
+            _lib.ctx_profile(True)
         t = time.perf_counter()
         for _ in range(args.steps):
             ci, sc, shell = _lib.ci(d, table, float(np.min(vox)))
         dt = (time.perf_counter() - t) / args.steps
+        kms, kn = _lib.ctx_kernel_time("ci_walk") if not args.no_profile else (0.0, 0)
+        _lib.ctx_profile(False)
         nd = int((d > 0).sum())
         probes = int(np.sum(table.bounds[shell[0][d > 0]].astype(np.int64)))
         cases[name] = {"defect_voxels": nd, "seconds_per_map": round(dt, 6),
                        "defect_voxels_per_s": round(nd / dt, 1), "sphere_probes_per_s": round(probes / dt, 1),
-                       "sphere_probes": probes, "CI": float(sc[0])}
+                       "sphere_probes": probes, "CI": float(sc[0]),
+                       "ci_walk_us": round(kms / kn * 1e3, 2) if kn else None}
     head = cases["seed0_pipeline"]   # 5917 defects, CI 22.5: the study BASELINE.md timed
+    roof = None
+    if head["ci_walk_us"]:
+        # k_ci_walk is bound by LDS bit tests, not HBM: each sphere probe is one
+        # ds_read_b32 of the LDS-staged defect bitmap (4 B); peak = 128 B/clk/CU (ds_read_b32,
+        # MI355X_MICROARCH.md LDS table) x 256 CUs x 2.4 GHz
+        lds_peak = 128.0 * 256 * 2.4e9 / 1e9
+        ach = head["sphere_probes"] * 4.0 / (head["ci_walk_us"] * 1e-6) / 1e9
+        roof = {"bound": "lds", "kernel": "ci_walk", "achieved": round(ach, 1), "peak": lds_peak,
+                "unit": "GB/s", "frac": round(ach / lds_peak, 4), "traffic": None,
+                "avg_launch_us": head["ci_walk_us"],
+                "probes_per_s_kernel": round(head["sphere_probes"] / (head["ci_walk_us"] * 1e-6), 1),
+                "alg_bytes_per_launch": head["sphere_probes"] * 4.0}
     line = {"metric": "CI defect-voxels/s (cluster-index map, 128x128x24, host-to-host)",
             "value": head["defect_voxels_per_s"], "unit": "defect-voxels/s", "n_gpus": 1,
             "steps": args.steps, "warmup": args.warmup,
@@ -236,7 +253,7 @@ def main_ci(args):
             "dtype": "u8/f64", "data": "synthetic",
             "config": {"workload": "CI.calculate_CI + the 95th-percentile CI on one 128x128x24 "
                                    "study, Rmax 50, vox [1.5, 1.5, 10]", "cases": cases},
-            "roofline": None, "cpu_baseline": None,
+            "roofline": roof, "cpu_baseline": None,
             "baseline_note": "reference: 5917 clustered defect voxels in 44.4 s (BASELINE.md)"}
     print(json.dumps(line))
 

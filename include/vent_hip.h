@@ -159,6 +159,12 @@ int vh_batch_reset_timers(vh_batch *b);
 int vh_batch_kernel_time(vh_batch *b, const char *name, double *total_ms, int64_t *launches,
                          double *bytes_per_launch);
 
+/* Kernel-class timing of the host-buffer entry points (vh_ci, vh_vdp, ...): on = 1 makes them time
+ * their kernel classes with HIP events on the context's scratch batch (timings accumulate; setting
+ * the switch discards them); vh_ctx_kernel_time reads them like vh_batch_kernel_time. */
+int vh_ctx_profile(vh_ctx *ctx, int on);
+int vh_ctx_kernel_time(vh_ctx *ctx, const char *name, double *total_ms, int64_t *launches);
+
 /* Per-study wall time (microseconds, device wall clock) of the last vh_batch_run's volume-resident
  * N4 kernel (one workgroup per study: the slowest study bounds the launch); zeros when that run did
  * not use it.  us[batch]. */

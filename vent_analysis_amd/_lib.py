@@ -80,6 +80,9 @@ _SIGS = {
     "vh_batch_kernel_time": ([_P, ct.c_char_p, ct.POINTER(ct.c_double), ct.POINTER(ct.c_int64),
                               ct.POINTER(ct.c_double)], ct.c_int),
     "vh_batch_study_times": ([_P, _P], ct.c_int),
+    "vh_ctx_profile": ([_P, ct.c_int], ct.c_int),
+    "vh_ctx_kernel_time": ([_P, ct.c_char_p, ct.POINTER(ct.c_double), ct.POINTER(ct.c_int64)],
+                           ct.c_int),
     "vh_overlay": ([_P, _P, _P, _I64, _I64, _I64, _I64, _P], ct.c_int),
     "vh_montage": ([_P, _I64, _I64, _I64, _P, ct.c_int, _P, ct.c_int, _P, _P, _P, _P, _P, _I64, _P,
                     _P], ct.c_int),
@@ -296,6 +299,21 @@ def ci(defect, table, minvox, device=0):
                       _ptr(table.bounds), _ptr(table.radii), table.bounds.shape[0],
                       ct.c_double(minvox), _ptr(out), _ptr(sc), _ptr(shell)), "vh_ci")
     return out, sc, shell
+
+
+def ctx_profile(on, device=0):
+    """Time the kernel classes of the host-buffer entry points (vh_ci, ...) on this device's
+    context (vh_ctx_profile); switching discards earlier timings."""
+    c = context(device)
+    c.check(c.L.vh_ctx_profile(c.h, 1 if on else 0), "vh_ctx_profile")
+
+
+def ctx_kernel_time(name, device=0):
+    """(total ms, launches) of a kernel class timed since ctx_profile(True)."""
+    c = context(device)
+    ms, n = ct.c_double(), ct.c_int64()
+    c.check(c.L.vh_ctx_kernel_time(c.h, name.encode(), ct.byref(ms), ct.byref(n)), "vh_ctx_kernel_time")
+    return ms.value, n.value
 
 
 def overlay(n4, defect, device=0):

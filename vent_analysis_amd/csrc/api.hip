@@ -505,7 +505,7 @@ int vh_ci(vh_ctx *ctx, const uint8_t *defect, int64_t R, int64_t C, int64_t Z, i
                 throw VhError{VH_ERR_ARG, "sphere table bounds must be increasing in [1, rows]"};
         vh_batch *b = scratch_batch(ctx, R, C, Z, batch);
         HIP_TRY(hipSetDevice(ctx->device));
-        b->profile = false;
+        b->profile = ctx->profile != 0;
         const size_t NV = (size_t)batch * b->V;
         HIP_TRY(hipMemcpyAsync(b->d_defect, defect, NV, hipMemcpyHostToDevice, b->stream));
         if (ci_array && !b->d_ci_map) HIP_TRY(hipMalloc(&b->d_ci_map, sizeof(double) * NV));
@@ -595,6 +595,34 @@ int vh_batch_kernel_time(vh_batch *b, const char *name, double *total_ms, int64_
             *total_ms = it->second.total_ms;
             *launches = it->second.launches;
             if (bytes_per_launch) *bytes_per_launch = it->second.bytes_per_launch;
+        }
+    })
+}
+
+int vh_ctx_profile(vh_ctx *ctx, int on) {
+    API_TRY(ctx, {
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        ctx->profile = on ? 1 : 0;
+        if (ctx->scratch) {
+            HIP_TRY(hipStreamSynchronize(ctx->scratch->stream));
+            clear_timers(ctx->scratch);
+        }
+    })
+}
+
+int vh_ctx_kernel_time(vh_ctx *ctx, const char *name, double *total_ms, int64_t *launches) {
+    API_TRY(ctx, {
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        if (!name || !total_ms || !launches) throw VhError{VH_ERR_ARG, "null argument"};
+        *total_ms = 0;
+        *launches = 0;
+        if (ctx->scratch) {
+            resolve_timers(ctx->scratch);
+            auto it = ctx->scratch->timers.find(name);
+            if (it != ctx->scratch->timers.end()) {
+                *total_ms = it->second.total_ms;
+                *launches = it->second.launches;
+            }
         }
     })
 }

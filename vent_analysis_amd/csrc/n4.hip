@@ -1460,7 +1460,7 @@ __global__ void __launch_bounds__(PC_TPB) k_n4_pcg(PcgArgs A) {
             } else {
                 const bool same = __float_as_uint(g) == __float_as_uint(lg) && __float_as_uint(gs) == __float_as_uint(ls);
                 if (__ballot(!same) != 0ull && !same) {
-                    pc_block_apx<0>(A.P, j, len, k0, mu, sig, NB);
+                    pc_block_apx<0>(A.P, j, len, k0, mu, sig, (uint32_t)NB, (m.L + 1u) * (uint32_t)NB);
                     lg = g;
                     ls = gs;
                     le = mu;

@@ -1013,47 +1013,98 @@ __device__ __forceinline__ bool pc_apx_step(const PcKf &q, float e0, float p, bo
 // redone with the exact steps (rare: the wave branches only when one of its lanes needs it)
 // SIG = false: the mu recurrence alone (mu never reads sig); sig returns sum (p - mu)^2 over the
 // block (approximate: the exact redo and tail steps add their sig increments instead)
-template <int NL, bool SIG = true>
-__device__ __forceinline__ void pc_block_apx(const float *P, uint32_t j, uint32_t len, uint32_t k0,
-                                             float &mu, float &sig, uint32_t nl = NL) {
-    if (!SIG) sig = 0.0f;
-    float cur[8], nxt[8];
+// P is read through a buffer resource of np floats (np = (L + 1) nl, the block layout's extent): the
+// step rows are loaded unguarded with the row offset in an SGPR (soffset), and rows past a block's
+// end (or past np) cost nothing but a load whose value is never used (0 beyond np)
+// one group of 8 phase-A steps from N = kf (the float counter); a group with an uncertified step is
+// redone with the exact steps.  CLAMP: some step of the block may pass 2^24 (ITK's frozen counter).
+template <bool SIG, bool CLAMP>
+__device__ __forceinline__ void pc_apx_group(const float (&c)[8], float kf, float e0, float &mu, float &sig) {
+    PcKf q[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) cur[i] = (uint32_t)i < len ? P[(size_t)i * nl + j] : 0.0f;
+    for (int i = 0; i < 8; i += 2) {
+        pc_f2 kk = kf + (pc_f2){(float)i, (float)(i + 1)};
+        if (CLAMP) kk = __builtin_elementwise_min(kk, (pc_f2)(float)ITK_NMAX);
+        pc_kf2(kk, (pc_f2){c[i], c[i + 1]}, q[i], q[i + 1]);
+    }
+    const float mu0 = mu, sig0 = sig;
+    bool ok = pc_apx_step<SIG>(q[0], e0, c[0], kf == 1.0f, mu, sig);
+#pragma unroll
+    for (int i = 1; i < 8; ++i) ok &= pc_apx_step<SIG>(q[i], e0, c[i], false, mu, sig);
+    if (!ok) {   // redo the group exactly
+        mu = mu0;
+        sig = sig0;
+        double kd = (double)kf;
+#pragma unroll 1
+        for (int i = 0; i < 8; ++i, kd += 1.0) pc_step(kd, c[i], mu, sig);
+    }
+}
+// a lane's block in phase A: groups of 8 steps without guards, two groups per trip (the loads of
+// one group in flight while the other computes, no register rotation); the tail by exact steps.
+// SIG = false: the mu recurrence alone (mu never reads sig); sig returns sum (p - mu)^2 over the
+// block (approximate: the exact redo and tail steps add their sig increments instead)
+// P is read through a buffer resource of np floats (np = (L + 1) nl, the block layout's extent): the
+// step rows are loaded unguarded with the row offset in an SGPR (soffset), and rows past a block's
+// end (or past np) cost nothing but a load whose value is never used (0 beyond np)
+template <bool SIG, bool CLAMP>
+__device__ __forceinline__ void pc_block_apx_t(const __amdgpu_buffer_rsrc_t rs, int voff, int rstride,
+                                               uint32_t len, uint32_t k0, float &mu, float &sig) {
+    auto ld = [&](uint32_t s) {
+        return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, voff, (int)s * rstride, 0));
+    };
+    // after the loop s0 differs between lanes whose lengths straddle a 16-step boundary: the row
+    // offset goes in the lane's voffset there (an SGPR soffset would need a waterfall)
+    auto ldv = [&](uint32_t s) {
+        return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, voff + (int)s * rstride, 0, 0));
+    };
+    auto adv = [](float kf) { return CLAMP ? fminf(kf + 8.0f, (float)ITK_NMAX) : kf + 8.0f; };
+    float a[8], b[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = ld((uint32_t)i);
     // N of the group's first step: min(k, 2^24), exact in float (ITK's frozen float counter)
-    float kf = fminf((float)k0, (float)ITK_NMAX);
+    float kf = CLAMP ? fminf((float)k0, (float)ITK_NMAX) : (float)k0;
     const float e0 = fmaf(__builtin_amdgcn_rcpf(kf), 0x1p-39f, 0x1p-44f);   // covers every step's r0
     uint32_t s0 = 0;
-    for (; s0 + 8 <= len; s0 += 8) {
+    for (; s0 + 16 <= len; s0 += 16) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) nxt[i] = s0 + 8 + i < len ? P[(size_t)(s0 + 8 + i) * nl + j] : 0.0f;
-        PcKf q[8];
+        for (int i = 0; i < 8; ++i) b[i] = ld(s0 + 8 + (uint32_t)i);
+        pc_apx_group<SIG, CLAMP>(a, kf, e0, mu, sig);
+        kf = adv(kf);
 #pragma unroll
-        for (int i = 0; i < 8; i += 2)
-            pc_kf2(__builtin_elementwise_min(kf + (pc_f2){(float)i, (float)(i + 1)}, (pc_f2)(float)ITK_NMAX),
-                   (pc_f2){cur[i], cur[i + 1]}, q[i], q[i + 1]);
-        const float mu0 = mu, sig0 = sig;
-        bool ok = pc_apx_step<SIG>(q[0], e0, cur[0], kf == 1.0f, mu, sig);
+        for (int i = 0; i < 8; ++i) a[i] = ld(s0 + 16 + (uint32_t)i);
+        pc_apx_group<SIG, CLAMP>(b, kf, e0, mu, sig);
+        kf = adv(kf);
+    }
+    if (s0 + 8 <= len) {
 #pragma unroll
-        for (int i = 1; i < 8; ++i) ok &= pc_apx_step<SIG>(q[i], e0, cur[i], false, mu, sig);
-        if (!ok) {   // redo the group exactly
-            mu = mu0;
-            sig = sig0;
-            double kd = (double)kf;
-#pragma unroll 1
-            for (int i = 0; i < 8; ++i, kd += 1.0) pc_step(kd, cur[i], mu, sig);
-        }
-        kf = fminf(kf + 8.0f, (float)ITK_NMAX);   // exact below 2^24, clamped above
+        for (int i = 0; i < 8; ++i) b[i] = ldv(s0 + 8 + (uint32_t)i);
+        pc_apx_group<SIG, CLAMP>(a, kf, e0, mu, sig);
+        kf = adv(kf);
+        s0 += 8;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) cur[i] = nxt[i];
+        for (int i = 0; i < 8; ++i) a[i] = b[i];
     }
     double kd = (double)kf;   // = N of the next step (pc_step clamps again past 2^24)
 #pragma unroll
     for (int i = 0; i < 7; ++i)   // the tail: exact steps
         if (s0 + i < len) {
-            pc_step(kd, cur[i], mu, sig);
+            pc_step(kd, a[i], mu, sig);
             kd += 1.0;
         }
+}
+template <int NL, bool SIG = true>
+__device__ __forceinline__ void pc_block_apx(const float *P, uint32_t j, uint32_t len, uint32_t k0,
+                                             float &mu, float &sig, uint32_t nl, uint32_t np) {
+    if (!SIG) sig = 0.0f;
+    // P, nl and np are uniform (one study per workgroup / grid): scalar registers, no waterfall
+    const uint64_t pa = (uint64_t)P;
+    const uint32_t plo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)pa),
+                   phi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(pa >> 32));
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)(((uint64_t)phi << 32) | plo), 0, __builtin_amdgcn_readfirstlane((int)(np * 4u)), 0x00020000);
+    const int voff = (int)(j * 4u), rstride = __builtin_amdgcn_readfirstlane((int)(nl * 4u));
+    if ((uint64_t)k0 + len <= (uint64_t)ITK_NMAX) pc_block_apx_t<SIG, false>(rs, voff, rstride, len, k0, mu, sig);
+    else pc_block_apx_t<SIG, true>(rs, voff, rstride, len, k0, mu, sig);
 }
 
 // ---- all-wave PC helpers (NL = threads of the workgroup, one block per thread) -----------------
@@ -1614,8 +1665,8 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
 #endif
             if (__ballot(!same) != 0ull && !same) {
                 float mu = g, sig = gs;
-                if (pass == 0) pc_block_apx<PC_TPB, false>(P, j, len, k0, mu, sig);
-                else pc_block_apx<PC_TPB, true>(P, j, len, k0, mu, sig);
+                if (pass == 0) pc_block_apx<PC_TPB, false>(P, j, len, k0, mu, sig, PC_TPB, (m.L + 1u) * PC_TPB);
+                else pc_block_apx<PC_TPB, true>(P, j, len, k0, mu, sig, PC_TPB, (m.L + 1u) * PC_TPB);
                 lg = g;
                 ls = gs;
                 le = mu;

@@ -112,6 +112,7 @@ struct vh_ctx {
     // the host-buffer entry points (vh_n4, vh_vdp, ...) share one cached scratch batch per
     // context; mu serialises them, so a context may be used from several host threads
     vh_batch *scratch = nullptr;
+    int profile = 0;                // vh_ctx_profile: time the scratch batch's kernel classes
     std::mutex mu;
     // last_error is written by any failing entry point (several host threads may fail at once on
     // one context, and vh_pipe_run does not hold mu): its own lock, and vh_last_error hands out a
