@@ -161,6 +161,20 @@ def max_over_ranks(dt, dist):
     return float(t.item())
 
 
+class stdout_to_stderr:
+    """RCCL's communicator setup prints a version banner on stdout; rank 0's stdout must carry the
+    one JSON line only (the driver parses it), so fd 1 points at fd 2 while the block runs."""
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 def host_to_host(R, C, Z, nb, args, device, opts, seed):
     """Volumes/s from host memory to host memory: args.h2h_batches x nb studies streamed through
     vh_pipe in sub-batches of args.h2h_sub studies on args.h2h_slots slots (pinned staging, one
@@ -319,11 +333,12 @@ def main():
     Bt = _lib.Batch(R, C, Z, nb, device=local)
     Bt.upload(hp, mk)
     use_comm = world > 1 or args.comm
-    if world > 1:
-        uid = broadcast_uid(_lib.comm_unique_id() if rank == 0 else None, dist)
-        _lib.comm_init(world, rank, uid, device=local)
-    elif args.comm:
-        _lib.comm_init(1, 0, _lib.comm_unique_id(), device=local)
+    with stdout_to_stderr():
+        if world > 1:
+            uid = broadcast_uid(_lib.comm_unique_id() if rank == 0 else None, dist)
+            _lib.comm_init(world, rank, uid, device=local)
+        elif args.comm:
+            _lib.comm_init(1, 0, _lib.comm_unique_id(), device=local)
     vox = (1.5, 1.5, 10.0)
     opts = Bt.options(do_n4=not args.no_n4, vox=vox, do_cohort=True,
                       profile=not args.no_profile, n4_subbatch=args.subbatch,
@@ -428,13 +443,17 @@ def main():
         "host_to_host": h2h,
     }
     if rank == 0:
-        print(json.dumps(line))
+        print(json.dumps(line), flush=True)
     Bt.close()
     if use_comm:
-        _lib.comm_destroy(device=local)
+        with stdout_to_stderr():
+            _lib.comm_destroy(device=local)
     if dist:
         dist.destroy_process_group()
 
 
 if __name__ == "__main__":
+    if os.environ.get("VH_DUMP_MAPS"):   # symbolising exit-time faults (scripts/dev): the mappings
+        import atexit                     # as they stand when Python's exit handlers run
+        atexit.register(lambda: open(os.environ["VH_DUMP_MAPS"], "w").write(open("/proc/self/maps").read()))
     main()

@@ -470,6 +470,39 @@ static float conv_welford(const float *d, int64_t n)
 /* S7 alone (tests/test_n4_oracle.py) */
 float n4o_conv_welford(const float *d, int64_t n) { return conv_welford(d, n); }
 
+/* The lower bound of the float sig that PC's certified decision uses (vent_analysis_amd/csrc/
+ * n4_shared.h pcw_run, after stage 0): nb blocks of consecutive steps, block j's float sum
+ * B_j = fma(q, q, B_j) of q = (float)(p - mu) along the exact mu trajectory, weighted by
+ * 1 - 1/min(k0_j, 2^24), summed in double in block order, times 1 - (n + L + 8) 2^-24.  Returns the
+ * true float sig of the recurrence in *sig and the bound in *lo (tests/test_n4_oracle.py checks
+ * lo <= sig on oracle d sequences). */
+void n4o_pc_sig_bound(const float *d, int64_t n, int nb, double *lo, float *sig_out, float *mu_out)
+{
+    float mu = 0.0f, sig = 0.0f, N = 0.0f;
+    const int64_t L = n / nb, rem = n % nb;
+    double tot = 0.0;
+    int64_t k = 1;
+    for (int j = 0; j < nb; ++j) {
+        const int64_t len = L + (j < rem ? 1 : 0), k0 = k;
+        float B = 0.0f;
+        for (int64_t s = 0; s < len; ++s, ++k) {
+            const float p = expf_cr(d[k - 1]);
+            N = (float)((double)N + 1.0);
+            const double Nd = (double)N;
+            if (Nd > 1.0) {
+                const float q = p - mu;
+                B = fmaf(q, q, B);
+                sig = (float)((double)sig + ((double)(q * q) * (Nd - 1.0)) / Nd);
+            }
+            mu = (float)((double)mu * (1.0 - 1.0 / Nd) + (double)(p / N));
+        }
+        if (k0 > 1) tot += (double)B * (1.0 - 1.0 / fmin((double)k0, 16777216.0));
+    }
+    *lo = tot * (1.0 - ((double)n + (double)L + 8.0) * 0x1p-24);
+    *sig_out = sig;
+    *mu_out = mu;
+}
+
 /* S7x (conv_mode 1): the coefficient of variation ITK intends, evaluated exactly enough that
  * order does not matter: d' = expm1c(d), CoV from sum d', sum d'^2 in double */
 static double conv_exact(const float *d, int64_t n)

@@ -124,3 +124,42 @@ def test_conv_welford_follows_itk_roundings():
         assert np.float32(got) == itk_convergence_py(d), n
     # the float counter stops at 2^24 (2^24 + 1 rounds to even), which conv_welford shares
     assert np.float32(np.float64(np.float32(2.0 ** 24)) + 1.0) == np.float32(2.0 ** 24)
+
+
+def _conv(mu, sig, n):
+    """ITK's measure from the float state (n4_shared.h itk_conv): float sqrt of sig / (N - 1) over mu."""
+    sd = np.float32(np.sqrt(np.float64(sig) / (min(float(n), 2.0 ** 24) - 1.0)))
+    return np.float32(sd / np.float32(mu))
+
+
+@pytest.mark.parametrize("shape,seed,nb", [((64, 64, 16), 0, 1024), ((96, 80, 12), 3, 1024),
+                                           ((40, 36, 9), 5, 64)])
+def test_pc_sig_lower_bound(tmp_path, monkeypatch, shape, seed, nb):
+    """PC's certified decision (n4_shared.h pcw_run): the bound from stage 0's block sums never
+    exceeds the float sig of ITK's recurrence, on every iteration's d sequence of an oracle N4 run,
+    so a measure above the threshold at the bound (and mu one float up) proves the true one is."""
+    import ctypes as ct
+    dump = tmp_path / "d.bin"
+    monkeypatch.setenv("N4_DUMP_D", str(dump))
+    X, M = synth_volume(*shape, seed)
+    native.n4(X, M)
+    raw = dump.read_bytes()
+    L = native.lib()
+    L.n4o_pc_sig_bound.restype = None
+    off = its = 0
+    while off < len(raw):
+        n = int(np.frombuffer(raw, np.int64, 1, off)[0])
+        d = np.frombuffer(raw, np.float32, n, off + 8).copy()
+        off += 8 + 4 * n
+        lo, sig, mu = ct.c_double(), ct.c_float(), ct.c_float()
+        L.n4o_pc_sig_bound(d.ctypes.data_as(ct.POINTER(ct.c_float)), ct.c_int64(n), ct.c_int(nb),
+                           ct.byref(lo), ct.byref(sig), ct.byref(mu))
+        assert 0.0 < lo.value <= sig.value, (its, lo.value, sig.value)
+        sl = np.float32(lo.value)
+        if np.float64(sl) > lo.value:
+            sl = np.nextafter(sl, np.float32(0))
+        muh = np.nextafter(np.float32(mu.value), np.float32(np.inf))
+        assert _conv(muh, sl, n) <= _conv(mu.value, sig.value, n)
+        assert lo.value > 0.95 * sig.value          # tight enough to decide most iterations
+        its += 1
+    assert its >= 4

@@ -759,6 +759,53 @@ int vh_pipe_create(vh_ctx *ctx, int64_t R, int64_t C, int64_t Z, int64_t sub, in
     })
 }
 
+// Host buffers the copy engines may read / write in place: hipHostRegister pins the caller's pages
+// (the page tables only; measured ~0.4-0.5 TB/s on the box, scripts/dev/h2h_probe.py) and the DMA
+// then runs at the link rate with no staging memcpy on a host thread.  A buffer that cannot be
+// registered (e.g. pages already registered, or VH_PIPE_STAGE=1) goes through the pinned staging.
+// First touch of a caller's output pages on several host threads (hipHostRegister would otherwise
+// fault in and zero every untouched page on the calling thread: measured 3.8k vs 5.1k vol/s staged)
+static void par_touch(void *dst, size_t bytes) {
+    const size_t page = 4096, chunk = (size_t)64 << 20;
+    const int want = (int)std::min<size_t>(2 * VH_COPY_THREADS, (bytes + chunk - 1) / chunk);
+    auto touch = [=](size_t o, size_t n) {
+        volatile char *q = (volatile char *)dst + o;
+        for (size_t i = 0; i < n; i += page) q[i] = q[i];
+    };
+    if (want <= 1) {
+        touch(0, bytes);
+        return;
+    }
+    std::vector<std::thread> th;
+    const size_t per = ((bytes + want - 1) / want + page - 1) / page * page;
+    for (int i = 1; i < want; ++i) {
+        const size_t o = per * i;
+        if (o < bytes) th.emplace_back(touch, o, std::min(per, bytes - o));
+    }
+    touch(0, std::min(per, bytes));
+    for (auto &t : th) t.join();
+}
+
+struct HostPin {
+    void *p = nullptr;
+    HostPin() = default;
+    HostPin(const HostPin &) = delete;
+    HostPin &operator=(const HostPin &) = delete;
+    bool pin(const void *ptr, size_t bytes, bool touch = false) {
+        if (!ptr || !bytes || getenv("VH_PIPE_STAGE")) return false;
+        if (touch) par_touch(const_cast<void *>(ptr), bytes);
+        if (hipHostRegister(const_cast<void *>(ptr), bytes, hipHostRegisterDefault) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        p = const_cast<void *>(ptr);
+        return true;
+    }
+    ~HostPin() {
+        if (p) (void)hipHostUnregister(p);
+    }
+};
+
 int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, const vh_run_opts *opts,
                 float *n4, uint8_t *defect, uint8_t *defect_border, uint8_t *lb, vh_vdp_result *res) {
     API_TRY(p->ctx, {
@@ -766,6 +813,12 @@ int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, con
         const int64_t V = p->R * p->C * p->Z, sub = p->sub;
         const int64_t nchunk = (n + sub - 1) / sub;
         const int slots = (int)p->slot.size();
+        HIP_TRY(hipSetDevice(p->ctx->device));
+        const size_t NV = (size_t)n * V;
+        HostPin g_hp, g_mk, g_n4, g_d, g_b, g_l;
+        const bool d_hp = g_hp.pin(hp, sizeof(float) * NV), d_mk = g_mk.pin(mask, NV),
+                   d_n4 = g_n4.pin(n4, sizeof(float) * NV, true), d_d = g_d.pin(defect, NV, true),
+                   d_b = g_b.pin(defect_border, NV, true), d_l = g_l.pin(lb, NV, true);
         std::vector<VhError> err(slots);
         std::vector<int> failed(slots, 0);
         auto work = [&](int s) {
@@ -777,29 +830,40 @@ int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, con
                     const int64_t v0 = k * sub, cnt = std::min(sub, n - v0);
                     uint8_t *qm = q.u8, *qd = q.u8 + sub * V, *qb = q.u8 + 2 * sub * V,
                             *ql = q.u8 + 3 * sub * V;
-                    par_memcpy(q.hp, hp + v0 * V, sizeof(float) * cnt * V);
-                    par_memcpy(qm, mask + v0 * V, cnt * V);
-                    for (int64_t i = cnt; i < sub; ++i) {   // ragged tail: repeat the last study
-                        memcpy(q.hp + i * V, hp + (v0 + cnt - 1) * V, sizeof(float) * V);
-                        memcpy(qm + i * V, mask + (v0 + cnt - 1) * V, V);
+                    const hipMemcpyKind H2D = hipMemcpyHostToDevice, D2H = hipMemcpyDeviceToHost;
+                    if (d_hp) {
+                        HIP_TRY(hipMemcpyAsync(b->d_hp, hp + v0 * V, sizeof(float) * cnt * V, H2D, b->stream));
+                    } else {
+                        par_memcpy(q.hp, hp + v0 * V, sizeof(float) * cnt * V);
+                        HIP_TRY(hipMemcpyAsync(b->d_hp, q.hp, sizeof(float) * cnt * V, H2D, b->stream));
                     }
-                    HIP_TRY(hipMemcpyAsync(b->d_hp, q.hp, sizeof(float) * sub * V, hipMemcpyHostToDevice, b->stream));
-                    HIP_TRY(hipMemcpyAsync(b->d_mask, qm, sub * V, hipMemcpyHostToDevice, b->stream));
+                    if (d_mk) {
+                        HIP_TRY(hipMemcpyAsync(b->d_mask, mask + v0 * V, cnt * V, H2D, b->stream));
+                    } else {
+                        par_memcpy(qm, mask + v0 * V, cnt * V);
+                        HIP_TRY(hipMemcpyAsync(b->d_mask, qm, cnt * V, H2D, b->stream));
+                    }
+                    for (int64_t i = cnt; i < sub; ++i) {   // ragged tail: repeat the last study
+                        HIP_TRY(hipMemcpyAsync(b->d_hp + i * V, b->d_hp + (cnt - 1) * V, sizeof(float) * V,
+                                               hipMemcpyDeviceToDevice, b->stream));
+                        HIP_TRY(hipMemcpyAsync(b->d_mask + i * V, b->d_mask + (cnt - 1) * V, V,
+                                               hipMemcpyDeviceToDevice, b->stream));
+                    }
                     batch_run(b, *opts, opts->do_n4 ? 0 : 1);
                     const float *dn4 = opts->do_n4 ? b->d_n4 : b->d_hp;
-                    if (n4) HIP_TRY(hipMemcpyAsync(q.n4, dn4, sizeof(float) * cnt * V, hipMemcpyDeviceToHost, b->stream));
-                    if (defect) HIP_TRY(hipMemcpyAsync(qd, b->d_defect, cnt * V, hipMemcpyDeviceToHost, b->stream));
-                    if (defect_border) HIP_TRY(hipMemcpyAsync(qb, b->d_border, cnt * V, hipMemcpyDeviceToHost, b->stream));
-                    if (lb) HIP_TRY(hipMemcpyAsync(ql, b->d_lb, cnt * V, hipMemcpyDeviceToHost, b->stream));
+                    if (n4) HIP_TRY(hipMemcpyAsync(d_n4 ? n4 + v0 * V : q.n4, dn4, sizeof(float) * cnt * V, D2H, b->stream));
+                    if (defect) HIP_TRY(hipMemcpyAsync(d_d ? defect + v0 * V : qd, b->d_defect, cnt * V, D2H, b->stream));
+                    if (defect_border) HIP_TRY(hipMemcpyAsync(d_b ? defect_border + v0 * V : qb, b->d_border, cnt * V, D2H, b->stream));
+                    if (lb) HIP_TRY(hipMemcpyAsync(d_l ? lb + v0 * V : ql, b->d_lb, cnt * V, D2H, b->stream));
                     HIP_TRY(hipStreamSynchronize(b->stream));
                     if (res) {
                         fill_results(b, q.res.data());
                         memcpy(res + v0, q.res.data(), sizeof(vh_vdp_result) * cnt);
                     }
-                    if (n4) par_memcpy(n4 + v0 * V, q.n4, sizeof(float) * cnt * V);
-                    if (defect) par_memcpy(defect + v0 * V, qd, cnt * V);
-                    if (defect_border) par_memcpy(defect_border + v0 * V, qb, cnt * V);
-                    if (lb) par_memcpy(lb + v0 * V, ql, cnt * V);
+                    if (n4 && !d_n4) par_memcpy(n4 + v0 * V, q.n4, sizeof(float) * cnt * V);
+                    if (defect && !d_d) par_memcpy(defect + v0 * V, qd, cnt * V);
+                    if (defect_border && !d_b) par_memcpy(defect_border + v0 * V, qb, cnt * V);
+                    if (lb && !d_l) par_memcpy(lb + v0 * V, ql, cnt * V);
                 }
             } catch (const VhError &e) {
                 err[s] = e;
@@ -813,6 +877,8 @@ int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, con
         for (int s = 1; s < slots; ++s) th.emplace_back(work, s);
         work(0);
         for (auto &t : th) t.join();
+        for (int s = 0; s < slots; ++s)   // no copy may still touch a pinned buffer when it is released
+            (void)hipStreamSynchronize(p->slot[s].b->stream);
         for (int s = 0; s < slots; ++s)
             if (failed[s]) throw err[s];
     })

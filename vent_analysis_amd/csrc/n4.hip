@@ -1277,7 +1277,7 @@ __global__ void __launch_bounds__(WF_TPB) k_n4_welford(const float *D, const int
 // replaces the serial chain's n dependent steps (~30 cycles each) by ~13 parallel rounds.
 __global__ void __launch_bounds__(PC_TPB) k_n4_pcw(const float *D, const int32_t *perm, float *Pbuf,
                                                    int64_t VS, const VolScalars *sc, N4State *st,
-                                                   int64_t vol0) {
+                                                   int64_t vol0, float skip_thresh) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int64_t b = vol0 + blockIdx.x;
     if (!st[b].active) return;
@@ -1285,9 +1285,10 @@ __global__ void __launch_bounds__(PC_TPB) k_n4_pcw(const float *D, const int32_t
     __shared__ ChainState ch;
     const float *const Db = D + b * VS;
     const int32_t *const pb = perm + b * VS;
-    // D[b] (compact d) is free once pass 0 has read it: PCX's stored increments
+    // D[b] (compact d) is free once pass 0 has read it: PCX's stored increments.  skip_thresh:
+    // the certified "above the threshold" decision of pcw_run (0 at the level's last iteration)
     pcw_run([=](int64_t r) { return Db[pb[r]]; }, Pbuf + b * VS, sc[b].n_mask1, S, ch, 1,
-            reinterpret_cast<double *>(const_cast<float *>(Db)), (int)(VS / 2));
+            reinterpret_cast<double *>(const_cast<float *>(Db)), (int)(VS / 2), skip_thresh);
     if (threadIdx.x == 0) st[b].conv_w = ch.conv;
 }
 
@@ -1871,7 +1872,8 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
                 } else if (cm == 0) {
                     ScopedKTimer tm(b, "n4_pcw", 0.0);
                     k_n4_pcw<<<(unsigned)ns, PC_TPB, sizeof(PcShared<PC_TPB>), st>>>(
-                        b->d_D, b->d_perm, b->d_D + b->nb * b->VS, b->VS, b->d_sc, b->d_st, vol0);
+                        b->d_D, b->d_perm, b->d_D + b->nb * b->VS, b->VS, b->d_sc, b->d_st, vol0,
+                        it + 1 < prm.max_iters[L] ? prm.conv_threshold : 0.0f);
                     VH_CHECK_LAUNCH();
                 }
                 if (getenv("VH_N4_TRACE")) n4_trace(b, vol0, L, it);

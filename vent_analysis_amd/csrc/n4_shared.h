@@ -1018,8 +1018,10 @@ __device__ __forceinline__ bool pc_apx_step(const PcKf &q, float e0, float p, bo
 // end (or past np) cost nothing but a load whose value is never used (0 beyond np)
 // one group of 8 phase-A steps from N = kf (the float counter); a group with an uncertified step is
 // redone with the exact steps.  CLAMP: some step of the block may pass 2^24 (ITK's frozen counter).
-template <bool SIG, bool CLAMP>
-__device__ __forceinline__ void pc_apx_group(const float (&c)[8], float kf, float e0, float &mu, float &sig) {
+// PART: only the first cnt (< 8) steps (a block's tail; lanes differ by at most one step there)
+template <bool SIG, bool CLAMP, bool PART = false>
+__device__ __forceinline__ void pc_apx_group(const float (&c)[8], float kf, float e0, float &mu, float &sig,
+                                             int cnt = 8) {
     PcKf q[8];
 #pragma unroll
     for (int i = 0; i < 8; i += 2) {
@@ -1028,15 +1030,16 @@ __device__ __forceinline__ void pc_apx_group(const float (&c)[8], float kf, floa
         pc_kf2(kk, (pc_f2){c[i], c[i + 1]}, q[i], q[i + 1]);
     }
     const float mu0 = mu, sig0 = sig;
-    bool ok = pc_apx_step<SIG>(q[0], e0, c[0], kf == 1.0f, mu, sig);
+    bool ok = !PART || cnt > 0 ? pc_apx_step<SIG>(q[0], e0, c[0], kf == 1.0f, mu, sig) : true;
 #pragma unroll
-    for (int i = 1; i < 8; ++i) ok &= pc_apx_step<SIG>(q[i], e0, c[i], false, mu, sig);
+    for (int i = 1; i < 8; ++i)
+        if (!PART || i < cnt) ok &= pc_apx_step<SIG>(q[i], e0, c[i], false, mu, sig);
     if (!ok) {   // redo the group exactly
         mu = mu0;
         sig = sig0;
         double kd = (double)kf;
 #pragma unroll 1
-        for (int i = 0; i < 8; ++i, kd += 1.0) pc_step(kd, c[i], mu, sig);
+        for (int i = 0; i < (PART ? cnt : 8); ++i, kd += 1.0) pc_step(kd, c[i], mu, sig);
     }
 }
 // a lane's block in phase A: groups of 8 steps without guards, two groups per trip (the loads of
@@ -1084,13 +1087,7 @@ __device__ __forceinline__ void pc_block_apx_t(const __amdgpu_buffer_rsrc_t rs, 
 #pragma unroll
         for (int i = 0; i < 8; ++i) a[i] = b[i];
     }
-    double kd = (double)kf;   // = N of the next step (pc_step clamps again past 2^24)
-#pragma unroll
-    for (int i = 0; i < 7; ++i)   // the tail: exact steps
-        if (s0 + i < len) {
-            pc_step(kd, a[i], mu, sig);
-            kd += 1.0;
-        }
+    if (s0 < len) pc_apx_group<SIG, CLAMP, true>(a, kf, e0, mu, sig, (int)(len - s0));   // the tail
 }
 template <int NL, bool SIG = true>
 __device__ __forceinline__ void pc_block_apx(const float *P, uint32_t j, uint32_t len, uint32_t k0,
@@ -1530,7 +1527,8 @@ static_assert(PC_APASS >= 1 && PC_APASS <= 2, "PC_APASS: 1 or 2 phase-A stages (
 #endif
 template <class LoadD>
 __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n, PcShared<PC_TPB> &S,
-                                                  ChainState &ch, int req, double *tbuf, int tcap) {
+                                                  ChainState &ch, int req, double *tbuf, int tcap,
+                                                  float skip_thresh = 0.0f) {
     const int tid = threadIdx.x;
     const PcMap m = pc_map(n, PC_TPB);
     const uint32_t j = (uint32_t)tid, len = pc_len(m, j), k0 = pc_k0(m, j);
@@ -1549,13 +1547,23 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
     float *const T0 = reinterpret_cast<float *>(&S);
     const uint32_t lmax = m.L + (m.rem ? 1u : 0u);
     double s1 = 0.0, s2 = 0.0;
-    for (uint32_t g0 = 0; g0 < lmax; g0 += G0) {
-        for (int e = tid; e < G0 * PC_TPB; e += PC_TPB) {
-            const uint32_t jb = (uint32_t)e / G0, i = (uint32_t)e % G0;
-            const uint32_t lb = pc_len(m, jb);
-            T0[i * TS + jb] = g0 + i < lb ? ld((int64_t)(pc_k0(m, jb) - 1u + g0 + i)) : 0.0f;
+    // thread tid loads step i = tid % G0 of blocks tid / G0 + (PC_TPB / G0) q; the next group's
+    // loads are in flight while this group's exp runs
+    float v[G0];
+    auto fetch = [&](uint32_t g0) {
+#pragma unroll
+        for (int q = 0; q < G0; ++q) {
+            const uint32_t jb = (uint32_t)tid / G0 + (uint32_t)(PC_TPB / G0) * q, i = (uint32_t)tid % G0;
+            v[q] = g0 + i < pc_len(m, jb) ? ld((int64_t)(pc_k0(m, jb) - 1u + g0 + i)) : 0.0f;
         }
+    };
+    fetch(0);
+    for (uint32_t g0 = 0; g0 < lmax; g0 += G0) {
+#pragma unroll
+        for (int q = 0; q < G0; ++q)
+            T0[(tid % G0) * TS + tid / G0 + (PC_TPB / G0) * q] = v[q];
         __syncthreads();
+        if (g0 + G0 < lmax) fetch(g0 + G0);
 #pragma unroll
         for (int i = 0; i < G0; ++i)
             if (g0 + i < len) {
@@ -1599,10 +1607,42 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
 #endif
             const bool real = j < (uint32_t)(m.L ? PC_TPB : m.rem);
             const double own = real ? (double)S.b[j].esig : 0.0;   // stage 0's sum (p - mu)^2
-            double sest, dummy;   // sig estimate at the block start: the prefix of those sums
-            pcw_scan<PC_TPB>(S, 1.0, own, 0.0, sest, dummy);
+            // the same sums weighted by the smallest (N - 1) / N of the block: their total bounds
+            // the float sig from below (the certified decision below)
+            const double wown = (real && k0 > 1u) ? own * (1.0 - 1.0 / fmin((double)k0, ITK_NMAX)) : 0.0;
+            double sest, wpre;   // sig estimate at the block start: the prefix of those sums
+            pcw_scan<PC_TPB>(S, 1.0, own, wown, sest, wpre);
+            // Certified decision (skip_thresh > 0: this iteration's measure is only compared with the
+            // threshold, never reported): with mu exact after stage 0, every float sig step is
+            // t_k = RN(RN(RN_f(q q) (N - 1)) / N) >= q^2 (1 - 1/N)(1 - 2^-24)(1 - 2^-52)^2, the float
+            // accumulation keeps S >= (1 - n 2^-24) sum t_k, and a block's stage-0 float sum B of
+            // fma(q, q, .) over its <= L + 1 steps has sum q^2 >= B (1 - (L + 1) 2^-24).  So
+            // S >= lo = (sum of the weighted B) (1 - (n + L + 8) 2^-24), and since ITK's measure
+            // sqrt(S / (N - 1)) / mu is monotone in S under round-to-nearest, a measure above the
+            // threshold at sig = RD(lo) proves the true one is above it too: the iteration goes on
+            // and the exact sig (PCX below) is not needed.  Otherwise, or when the measure is the
+            // level's reported one (skip_thresh = 0), PCX computes it exactly.
+            if (tid == PC_TPB - 1 && skip_thresh > 0.0f) {
+                const double f = 1.0 - ((double)n + (double)m.L + 8.0) * 0x1p-24;
+                const double lo = (wpre + wown) * f;
+                float sl = (float)lo;
+                if ((double)sl > lo && sl > 0.0f) sl = __uint_as_float(__float_as_uint(sl) - 1u);
+                const int nbe = m.L ? PC_TPB : (int)m.rem;
+                const float mue = S.b[nbe - 1].emu;   // (one float up: a margin that costs nothing)
+                const float muh = __uint_as_float(__float_as_uint(mue) + 1u);
+                if (f > 0.5 && lo > 0.0 && mue > 0.0f && itk_conv(muh, sl, n) > skip_thresh) {
+                    S.mu = mue;
+                    S.sig = sl;
+                    S.rounds = round + 1;
+                    S.xdone = 4 * req + 3;
+                }
+            }
             if (tid == 0) S.xslots = 0;
             __syncthreads();
+            if (S.xdone == 4 * req + 3) {   // decided: no PCX, no exact rounds
+                xs = true;
+                break;
+            }
 #ifdef PC_PROF
             const unsigned long long cxt = clock64();
 #endif

@@ -350,20 +350,37 @@ __device__ void eval_item(const Item &it, int item, int Z, const TabV &Tn, const
 #pragma unroll 1
         for (;;) {
             const int rb = min(it.xe, Tn.xst[wbn + 1] - 1);
-#pragma unroll 1
-            for (int xb = x; xb <= rb; xb += FIT_G) {
-                uint32_t offs[FIT_G];
-                int rrs[FIT_G];
-                float la[FIT_G];
+            // groups of FIT_G rows, two per trip: the next group's L0 loads are in flight while
+            // this group's voxels are evaluated (the span's rows only: the window moves after it)
+            uint32_t oA[FIT_G], oB[FIT_G];
+            int rA[FIT_G], rB[FIT_G];
+            float lA[FIT_G], lB[FIT_G];
+            auto issue = [&](int xb, uint32_t (&o)[FIT_G], int (&r)[FIT_G], float (&l)[FIT_G]) {
 #pragma unroll
                 for (int g = 0; g < FIT_G; ++g) {
                     const int xg = xb + g;
-                    offs[g] = item_off(it, xg <= rb ? xg : rb, xg <= rb, CM == 0 ? &rrs[g] : nullptr);
-                    la[g] = st_load(rL, offs[g]);
+                    o[g] = item_off(it, xg <= rb ? xg : rb, xg <= rb, CM == 0 ? &r[g] : nullptr);
+                    l[g] = st_load(rL, o[g]);
                 }
+            };
+            auto run = [&](int xb, const uint32_t (&o)[FIT_G], const int (&r)[FIT_G], const float (&l)[FIT_G]) {
 #pragma unroll
                 for (int g = 0; g < FIT_G; ++g)
-                    if (offs[g] != VH_OOB) voxel(offs[g], CM == 0 ? rrs[g] : 0, la[g], xb + g);
+                    if (o[g] != VH_OOB) voxel(o[g], CM == 0 ? r[g] : 0, l[g], xb + g);
+            };
+            if (x <= rb) {
+                issue(x, oA, rA, lA);
+#pragma unroll 1
+                for (int xb = x;; xb += 2 * FIT_G) {
+                    const bool hb = xb + FIT_G <= rb;
+                    if (hb) issue(xb + FIT_G, oB, rB, lB);
+                    run(xb, oA, rA, lA);
+                    if (!hb) break;
+                    const bool ha = xb + 2 * FIT_G <= rb;
+                    if (ha) issue(xb + 2 * FIT_G, oA, rA, lA);
+                    run(xb + FIT_G, oB, rB, lB);
+                    if (!ha) break;
+                }
             }
             x = rb + 1 > x ? rb + 1 : x;
             if (x > it.xe) break;
@@ -1092,8 +1109,11 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                     PcShared<ST_TPB> &PW = *reinterpret_cast<PcShared<ST_TPB> *>(smem + a.o_scr);
                     const float *const Dr = a.D + b * a.VS;
                     // the raster d buffer is free once pass 0 has read it: PCX's stored increments
+                    // below the iteration cap this iteration's measure only decides whether the
+                    // level goes on: PC may certify "above the threshold" without the exact sig
                     pcw_run([=](int64_t r) { return Dr[r]; }, a.D + a.half + b * a.VS, n, PW, M.ch[0], itk,
-                            reinterpret_cast<double *>(a.D + b * a.VS), (int)(a.VS / 2));
+                            reinterpret_cast<double *>(a.D + b * a.VS), (int)(a.VS / 2),
+                            itk < a.lvs->max_iters[L] ? a.thresh : 0.0f);
                     if (t == 0) M.conv = (double)M.ch[0].conv;
                 } else if (g.w == 0) {   // S7x: item partials in item order
                     double sd = 0.0, sd2 = 0.0;
