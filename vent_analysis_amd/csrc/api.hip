@@ -5,6 +5,8 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <stdexcept>
 
@@ -814,13 +816,27 @@ int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, con
         const int64_t nchunk = (n + sub - 1) / sub;
         const int slots = (int)p->slot.size();
         HIP_TRY(hipSetDevice(p->ctx->device));
-        const size_t NV = (size_t)n * V;
-        HostPin g_hp, g_mk, g_n4, g_d, g_b, g_l;
-        const bool d_hp = g_hp.pin(hp, sizeof(float) * NV), d_mk = g_mk.pin(mask, NV),
-                   d_n4 = g_n4.pin(n4, sizeof(float) * NV, true), d_d = g_d.pin(defect, NV, true),
-                   d_b = g_b.pin(defect_border, NV, true), d_l = g_l.pin(lb, NV, true);
         std::vector<VhError> err(slots);
         std::vector<int> failed(slots, 0);
+        // VH_PIPE_TRACE=1: per chunk, host times (ms from the start) of the input pin + H2D enqueue, the
+        // pipeline enqueue, the output pin, the sync, and device times of H2D / compute / D2H ends (stderr)
+        struct Mark {
+            int64_t k;
+            double h[5];
+            hipEvent_t e[3];
+        };
+        const bool trace = getenv("VH_PIPE_TRACE") != nullptr;
+        std::vector<std::vector<Mark>> marks(slots);
+        hipEvent_t ev0 = nullptr;
+        const auto c0 = std::chrono::steady_clock::now();
+        auto now_ms = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - c0).count(); };
+        if (trace) {
+            HIP_TRY(hipEventCreate(&ev0));
+            HIP_TRY(hipEventRecord(ev0, p->slot[0].b->stream));
+        }
+        auto mark_ev = [&](Mark &m, int i, hipStream_t st) {
+            if (trace && hipEventCreate(&m.e[i]) == hipSuccess) (void)hipEventRecord(m.e[i], st);
+        };
         auto work = [&](int s) {
             vh_pipe::Slot &q = p->slot[s];
             vh_batch *b = q.b;
@@ -828,42 +844,66 @@ int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, con
                 HIP_TRY(hipSetDevice(p->ctx->device));
                 for (int64_t k = s; k < nchunk; k += slots) {
                     const int64_t v0 = k * sub, cnt = std::min(sub, n - v0);
+                    const size_t CV = (size_t)cnt * V;
                     uint8_t *qm = q.u8, *qd = q.u8 + sub * V, *qb = q.u8 + 2 * sub * V,
                             *ql = q.u8 + 3 * sub * V;
                     const hipMemcpyKind H2D = hipMemcpyHostToDevice, D2H = hipMemcpyDeviceToHost;
-                    if (d_hp) {
-                        HIP_TRY(hipMemcpyAsync(b->d_hp, hp + v0 * V, sizeof(float) * cnt * V, H2D, b->stream));
-                    } else {
-                        par_memcpy(q.hp, hp + v0 * V, sizeof(float) * cnt * V);
-                        HIP_TRY(hipMemcpyAsync(b->d_hp, q.hp, sizeof(float) * cnt * V, H2D, b->stream));
+                    // this chunk's caller buffers, pinned in place while its copies run (a chunk
+                    // whose pages another chunk holds, or VH_PIPE_STAGE=1, goes through the staging)
+                    HostPin g_hp, g_mk, g_n4, g_d, g_b, g_l;
+                    Mark mk_{k, {now_ms(), 0, 0, 0, 0}, {nullptr, nullptr, nullptr}};
+                    try {
+                        const bool d_hp = g_hp.pin(hp + v0 * V, sizeof(float) * CV), d_mk = g_mk.pin(mask + v0 * V, CV);
+                        if (d_hp) {
+                            HIP_TRY(hipMemcpyAsync(b->d_hp, hp + v0 * V, sizeof(float) * CV, H2D, b->stream));
+                        } else {
+                            par_memcpy(q.hp, hp + v0 * V, sizeof(float) * CV);
+                            HIP_TRY(hipMemcpyAsync(b->d_hp, q.hp, sizeof(float) * CV, H2D, b->stream));
+                        }
+                        if (d_mk) {
+                            HIP_TRY(hipMemcpyAsync(b->d_mask, mask + v0 * V, CV, H2D, b->stream));
+                        } else {
+                            par_memcpy(qm, mask + v0 * V, CV);
+                            HIP_TRY(hipMemcpyAsync(b->d_mask, qm, CV, H2D, b->stream));
+                        }
+                        for (int64_t i = cnt; i < sub; ++i) {   // ragged tail: repeat the last study
+                            HIP_TRY(hipMemcpyAsync(b->d_hp + i * V, b->d_hp + (cnt - 1) * V, sizeof(float) * V,
+                                                   hipMemcpyDeviceToDevice, b->stream));
+                            HIP_TRY(hipMemcpyAsync(b->d_mask + i * V, b->d_mask + (cnt - 1) * V, V,
+                                                   hipMemcpyDeviceToDevice, b->stream));
+                        }
+                        mark_ev(mk_, 0, b->stream);
+                        mk_.h[1] = now_ms();
+                        batch_run(b, *opts, opts->do_n4 ? 0 : 1);
+                        mark_ev(mk_, 1, b->stream);
+                        mk_.h[2] = now_ms();
+                        // while the chunk computes: first touch + pin of its output ranges
+                        const bool d_n4 = g_n4.pin(n4 ? n4 + v0 * V : nullptr, sizeof(float) * CV, true),
+                                   d_d = g_d.pin(defect ? defect + v0 * V : nullptr, CV, true),
+                                   d_b = g_b.pin(defect_border ? defect_border + v0 * V : nullptr, CV, true),
+                                   d_l = g_l.pin(lb ? lb + v0 * V : nullptr, CV, true);
+                        const float *dn4 = opts->do_n4 ? b->d_n4 : b->d_hp;
+                        if (n4) HIP_TRY(hipMemcpyAsync(d_n4 ? n4 + v0 * V : q.n4, dn4, sizeof(float) * CV, D2H, b->stream));
+                        if (defect) HIP_TRY(hipMemcpyAsync(d_d ? defect + v0 * V : qd, b->d_defect, CV, D2H, b->stream));
+                        if (defect_border) HIP_TRY(hipMemcpyAsync(d_b ? defect_border + v0 * V : qb, b->d_border, CV, D2H, b->stream));
+                        if (lb) HIP_TRY(hipMemcpyAsync(d_l ? lb + v0 * V : ql, b->d_lb, CV, D2H, b->stream));
+                        mark_ev(mk_, 2, b->stream);
+                        mk_.h[3] = now_ms();
+                        HIP_TRY(hipStreamSynchronize(b->stream));
+                        mk_.h[4] = now_ms();
+                        if (trace) marks[s].push_back(mk_);
+                        if (res) {
+                            fill_results(b, q.res.data());
+                            memcpy(res + v0, q.res.data(), sizeof(vh_vdp_result) * cnt);
+                        }
+                        if (n4 && !d_n4) par_memcpy(n4 + v0 * V, q.n4, sizeof(float) * CV);
+                        if (defect && !d_d) par_memcpy(defect + v0 * V, qd, CV);
+                        if (defect_border && !d_b) par_memcpy(defect_border + v0 * V, qb, CV);
+                        if (lb && !d_l) par_memcpy(lb + v0 * V, ql, CV);
+                    } catch (...) {   // no copy may still touch a pinned range when it is released
+                        (void)hipStreamSynchronize(b->stream);
+                        throw;
                     }
-                    if (d_mk) {
-                        HIP_TRY(hipMemcpyAsync(b->d_mask, mask + v0 * V, cnt * V, H2D, b->stream));
-                    } else {
-                        par_memcpy(qm, mask + v0 * V, cnt * V);
-                        HIP_TRY(hipMemcpyAsync(b->d_mask, qm, cnt * V, H2D, b->stream));
-                    }
-                    for (int64_t i = cnt; i < sub; ++i) {   // ragged tail: repeat the last study
-                        HIP_TRY(hipMemcpyAsync(b->d_hp + i * V, b->d_hp + (cnt - 1) * V, sizeof(float) * V,
-                                               hipMemcpyDeviceToDevice, b->stream));
-                        HIP_TRY(hipMemcpyAsync(b->d_mask + i * V, b->d_mask + (cnt - 1) * V, V,
-                                               hipMemcpyDeviceToDevice, b->stream));
-                    }
-                    batch_run(b, *opts, opts->do_n4 ? 0 : 1);
-                    const float *dn4 = opts->do_n4 ? b->d_n4 : b->d_hp;
-                    if (n4) HIP_TRY(hipMemcpyAsync(d_n4 ? n4 + v0 * V : q.n4, dn4, sizeof(float) * cnt * V, D2H, b->stream));
-                    if (defect) HIP_TRY(hipMemcpyAsync(d_d ? defect + v0 * V : qd, b->d_defect, cnt * V, D2H, b->stream));
-                    if (defect_border) HIP_TRY(hipMemcpyAsync(d_b ? defect_border + v0 * V : qb, b->d_border, cnt * V, D2H, b->stream));
-                    if (lb) HIP_TRY(hipMemcpyAsync(d_l ? lb + v0 * V : ql, b->d_lb, cnt * V, D2H, b->stream));
-                    HIP_TRY(hipStreamSynchronize(b->stream));
-                    if (res) {
-                        fill_results(b, q.res.data());
-                        memcpy(res + v0, q.res.data(), sizeof(vh_vdp_result) * cnt);
-                    }
-                    if (n4 && !d_n4) par_memcpy(n4 + v0 * V, q.n4, sizeof(float) * cnt * V);
-                    if (defect && !d_d) par_memcpy(defect + v0 * V, qd, cnt * V);
-                    if (defect_border && !d_b) par_memcpy(defect_border + v0 * V, qb, cnt * V);
-                    if (lb && !d_l) par_memcpy(lb + v0 * V, ql, cnt * V);
                 }
             } catch (const VhError &e) {
                 err[s] = e;
@@ -879,6 +919,21 @@ int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, con
         for (auto &t : th) t.join();
         for (int s = 0; s < slots; ++s)   // no copy may still touch a pinned buffer when it is released
             (void)hipStreamSynchronize(p->slot[s].b->stream);
+        if (trace) {
+            fprintf(stderr, "pipe_trace total_ms %.2f\n", now_ms());
+            for (int s = 0; s < slots; ++s)
+                for (Mark &m : marks[s]) {
+                    float d[3] = {-1, -1, -1};
+                    for (int i = 0; i < 3; ++i)
+                        if (m.e[i]) {
+                            (void)hipEventElapsedTime(&d[i], ev0, m.e[i]);
+                            (void)hipEventDestroy(m.e[i]);
+                        }
+                    fprintf(stderr, "pipe_trace slot %d chunk %lld host %.2f %.2f %.2f %.2f %.2f dev %.2f %.2f %.2f\n", s,
+                            (long long)m.k, m.h[0], m.h[1], m.h[2], m.h[3], m.h[4], d[0], d[1], d[2]);
+                }
+            (void)hipEventDestroy(ev0);
+        }
         for (int s = 0; s < slots; ++s)
             if (failed[s]) throw err[s];
     })

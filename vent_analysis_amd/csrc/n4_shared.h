@@ -355,19 +355,26 @@ __device__ void fit_item(const Item &it, const TabV &T, const double *Wk, const 
     for (;;) {
         if (x <= it.xe) {   // rows of control span wb: the window does not move
             const int rb = min(it.xe, T.xst[wb + 1] - 1);
-#pragma unroll 1
-            for (int xb = x; xb <= rb; xb += FIT_G) {
-                uint32_t offs[FIT_G];
-                float u[FIT_G];
+            // groups of FIT_G rows, two per trip: the next group's U loads are in flight while this
+            // group's rows are added (the chains still take the rows in order)
+            uint32_t oA[FIT_G], oB[FIT_G];
+            float uA[FIT_G], uB[FIT_G];
+            auto issue = [&](int xb, uint32_t (&o)[FIT_G], float (&u)[FIT_G]) {
 #pragma unroll
                 for (int g = 0; g < FIT_G; ++g) {
                     const int xg = xb + g;
-                    offs[g] = item_off(it, xg <= rb ? xg : rb, xg <= rb);
-                    if (MODE == 0) u[g] = st_load(rU, offs[g]);
+                    o[g] = item_off(it, xg <= rb ? xg : rb, xg <= rb);
+#ifdef AB_FIT_NOLOAD   // A/B builds only (fixed iteration counts): the fit without its U loads
+                    if (MODE == 0) u[g] = 0.5f + 0.01f * (float)g;
+#else
+                    if (MODE == 0) u[g] = st_load(rU, o[g]);
+#endif
                 }
+            };
+            auto run = [&](int xb, const uint32_t (&o)[FIT_G], const float (&u)[FIT_G]) {
 #pragma unroll
                 for (int g = 0; g < FIT_G; ++g) {
-                    if (offs[g] == VH_OOB) continue;
+                    if (o[g] == VH_OOB) continue;
                     const int xg = xb + g;
                     const double2 wa = Wx[2 * xg], wc = Wx[2 * xg + 1];
                     if (MODE == 0) {
@@ -383,6 +390,20 @@ __device__ void fit_item(const Item &it, const TabV &T, const double *Wk, const 
                         acc2 += wc.x;
                         acc3 += wc.y;
                     }
+                }
+            };
+            if (x <= rb) {
+                issue(x, oA, uA);
+#pragma unroll 1
+                for (int xb = x;; xb += 2 * FIT_G) {
+                    const bool hb = xb + FIT_G <= rb;
+                    if (hb) issue(xb + FIT_G, oB, uB);
+                    run(xb, oA, uA);
+                    if (!hb) break;
+                    const bool ha = xb + 2 * FIT_G <= rb;
+                    if (ha) issue(xb + 2 * FIT_G, oA, uA);
+                    run(xb + FIT_G, oB, uB);
+                    if (!ha) break;
                 }
             }
             x = rb + 1 > x ? rb + 1 : x;

@@ -335,9 +335,15 @@ __device__ void eval_item(const Item &it, int item, int Z, const TabV &Tn, const
             bo = ((wo.x * to0 + wo.y * to1) + wo.z * to2) + wo.w * to3;
         }
         const float u = la - bn;
+#ifndef AB_EVAL_NOSTORE   // A/B builds only: the phase without its U / d stores
         st_store(rU, off, u);
+#endif
         if (CM == 0) {
+#ifndef AB_EVAL_NOSTORE
             st_store(rD, (uint32_t)rr * 4u, bo - bn);
+#else
+            if (bo - bn == 12345.0f) st_store(rD, (uint32_t)rr * 4u, u);
+#endif
         } else {
             const double d = (double)expm1c(bo - bn);
             sd += d;
@@ -360,7 +366,11 @@ __device__ void eval_item(const Item &it, int item, int Z, const TabV &Tn, const
                 for (int g = 0; g < FIT_G; ++g) {
                     const int xg = xb + g;
                     o[g] = item_off(it, xg <= rb ? xg : rb, xg <= rb, CM == 0 ? &r[g] : nullptr);
+#ifdef AB_EVAL_NOLOAD   // A/B builds only (fixed iteration counts): the phase without its L0 loads
+                    l[g] = 1.0f + (float)g;
+#else
                     l[g] = st_load(rL, o[g]);
+#endif
                 }
             };
             auto run = [&](int xb, const uint32_t (&o)[FIT_G], const int (&r)[FIT_G], const float (&l)[FIT_G]) {
@@ -719,7 +729,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
         for (int e = t; e < nl0; e += ST_TPB) lat[e] = 0.0f;
     }
 #ifdef ST_PROF
-    unsigned long long st_prof[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_t0 = clock64();
+    unsigned long long st_prof[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_t0 = clock64();
 #endif
     int ch_seen = 0;   // chain waves: the last request taken
     for (int L = 0; L < a.nlev; ++L) {
@@ -951,8 +961,10 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                     }
                     if (g.t < P / 2) TW[g.t] = twv;
                     gsync(g, M);
+                    ST_MARK(11);
                     if (g.w < 2) wave_fft_lds(g.w ? F : V, TW, false, FftId(), FftId());
                     gsync(g, M);
+                    ST_MARK(12);
                     if (g.w == 0) {   // Wiener filter (first pass), inverse, clamp and the moment series (last pass)
                         const double noise = (double)a.noise;
                         wave_fft_lds(V, TW, true,
@@ -970,6 +982,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                             });
                     }
                     gsync(g, M);
+                    ST_MARK(13);
                     if (g.w < 2) {   // each series: forward, times the kernel's transform (last pass), inverse
                         double2 *x = g.w ? DEN : V;
                         wave_fft_lds(x, TW, false, FftId(), [=](int i, double2 v) {
@@ -980,6 +993,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                         wave_fft_lds(x, TW, true, FftId(), FftId());
                     }
                     gsync(g, M);
+                    ST_MARK(14);
                     for (int i = g.t; i < bins; i += g.n) {
                         const double d = DEN[fpad(i + off)].x;
                         sE[i] = d != 0.0 ? (float)(V[fpad(i + off)].x / d) : 0.0f;
@@ -1166,8 +1180,10 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
 #ifdef ST_PROF
     if (t == st_pt && blockIdx.x == 0)
         printf("ST_PROF den %llu ctrl %llu hist %llu emap %llu fit %llu latP1 %llu eval %llu "
-               "wait %llu level %llu exact %llu top %llu\n", st_prof[0], st_prof[1], st_prof[2], st_prof[3],
-               st_prof[4], st_prof[5], st_prof[6], st_prof[7], st_prof[8], st_prof[9], st_prof[10]);
+               "wait %llu level %llu exact %llu top %llu | emap: series %llu fwd %llu filter %llu conv %llu div %llu\n",
+               st_prof[0], st_prof[1], st_prof[2], st_prof[3],
+               st_prof[4], st_prof[5], st_prof[6], st_prof[7], st_prof[8], st_prof[9], st_prof[10],
+               st_prof[11], st_prof[12], st_prof[13], st_prof[14], st_prof[3]);
 #endif
     // final field's P1 for k_n4_final
     const double *P1f = M.cur ? P1b1 : P1b0;
