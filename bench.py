@@ -298,9 +298,9 @@ def main():
                     help="skip the host-to-host pipeline measurement (host_to_host_vol_s)")
     ap.add_argument("--h2h-batches", type=int, default=6,
                     help="host-to-host sample: this many x --batch volumes")
-    ap.add_argument("--h2h-sub", type=int, default=64,
+    ap.add_argument("--h2h-sub", type=int, default=128,
                     help="host-to-host: studies per pipeline sub-batch")
-    ap.add_argument("--h2h-slots", type=int, default=6,
+    ap.add_argument("--h2h-slots", type=int, default=4,
                     help="host-to-host: pipeline slots (sub-batches in flight, <= 8)")
     ap.add_argument("--workload", default="vdp", choices=["vdp", "ci"],
                     help="vdp: the BASELINE metric (default); ci: the cluster-index line")

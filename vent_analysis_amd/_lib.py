@@ -469,7 +469,7 @@ class Pipe:
     """Host-to-host pipeline (vh_pipe): n host-resident studies streamed through `slots` device
     batches of `sub` volumes, transfers of one sub-batch overlapping the compute of another."""
 
-    def __init__(self, R, C, Z, sub, slots=3, device=0):
+    def __init__(self, R, C, Z, sub, slots=4, device=0):
         self.ctx = context(device)
         self.L = self.ctx.L
         self.vshape = (int(R), int(C), int(Z))

@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <memory>
 #include <cstdio>
 #include <cstring>
 #include <stdexcept>
@@ -218,15 +219,30 @@ static void check_n4_watchdog(const N4State *st, int64_t nb) {
         if (st[i].active == -2) throw VhError{VH_ERR_HIP, "N4 study kernel: a synchronisation wait timed out"};
 }
 
+// small device -> host copy ordered on the batch's own stream: a synchronous hipMemcpy goes through
+// the null stream, whose hardware queue is shared with one of the pipe slots' streams once there are
+// more streams than queues (GPU_MAX_HW_QUEUES), so it waited for that slot's queued work
+static void d2h_on_stream(vh_batch *b, void *dst, const void *src, size_t bytes) {
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, b->stream));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+}
+
+static void fill_results_from(const vh_batch *b, const VolScalars *sc, const N4State *st, vh_vdp_result *res);
+
 static void fill_results(vh_batch *b, vh_vdp_result *res) {
     std::vector<VolScalars> sc(b->nb);
-    HIP_TRY(hipMemcpy(sc.data(), b->d_sc, sizeof(VolScalars) * b->nb, hipMemcpyDeviceToHost));
+    d2h_on_stream(b, sc.data(), b->d_sc, sizeof(VolScalars) * b->nb);
     std::vector<N4State> st;
     if (b->opts.do_n4) {
         st.resize(b->nb);
-        HIP_TRY(hipMemcpy(st.data(), b->d_st, sizeof(N4State) * b->nb, hipMemcpyDeviceToHost));
-        check_n4_watchdog(st.data(), b->nb);
+        d2h_on_stream(b, st.data(), b->d_st, sizeof(N4State) * b->nb);
     }
+    fill_results_from(b, sc.data(), st.data(), res);
+}
+
+// per-study results from host copies of the scalars (and N4 states when the batch ran N4)
+static void fill_results_from(const vh_batch *b, const VolScalars *sc, const N4State *st, vh_vdp_result *res) {
+    if (b->opts.do_n4) check_n4_watchdog(st, b->nb);
     const double *vox = b->opts.vox;
     // np.prod(np.divide(vox, 10)): sequential multiply (Vent_Analysis.py:166, 252)
     const double pv = ((vox[0] / 10.0) * (vox[1] / 10.0)) * (vox[2] / 10.0);
@@ -278,6 +294,9 @@ static void pipe_free(vh_pipe *p) {
         if (q.hp) (void)hipHostFree(q.hp);
         if (q.n4) (void)hipHostFree(q.n4);
         if (q.u8) (void)hipHostFree(q.u8);
+        if (q.done) (void)hipEventDestroy(q.done);
+        if (q.sc) (void)hipHostFree(q.sc);
+        if (q.st) (void)hipHostFree(q.st);
     }
     delete p;
 }
@@ -751,6 +770,9 @@ int vh_pipe_create(vh_ctx *ctx, int64_t R, int64_t C, int64_t Z, int64_t sub, in
                 HIP_TRY(hipHostMalloc((void **)&q.hp, sizeof(float) * NV));
                 HIP_TRY(hipHostMalloc((void **)&q.n4, sizeof(float) * NV));
                 HIP_TRY(hipHostMalloc((void **)&q.u8, 4 * NV));   // mask, defect, border, lb
+                HIP_TRY(hipEventCreateWithFlags(&q.done, hipEventDisableTiming));
+                HIP_TRY(hipHostMalloc((void **)&q.sc, sizeof(VolScalars) * sub));
+                HIP_TRY(hipHostMalloc((void **)&q.st, sizeof(N4State) * sub));
                 q.res.resize(sub);
             }
         } catch (...) {
@@ -808,6 +830,67 @@ struct HostPin {
     }
 };
 
+// One caller range of a pipe chunk.  Only its whole pages are pinned (and DMA'd in place): a page
+// it shares with the neighbouring chunk or another buffer must never be registered twice or
+// unregistered under another range's copy, so the head and tail fragments (< 1 page each) go
+// through the slot's pinned staging at the same offsets.  A range that cannot be pinned is staged.
+struct PipeAbort {};   // a pipe slot stopped because another slot failed
+
+struct PipeSpan {
+    char *p = nullptr;
+    size_t n = 0, h = 0, t = 0;
+    bool direct = false;
+    HostPin pin;
+    void plan(const void *ptr, size_t bytes, bool touch) {
+        p = (char *)ptr;
+        n = ptr ? bytes : 0;
+        if (!n) return;
+        const uintptr_t pg = 4096, s0 = (uintptr_t)p, e0 = s0 + n;
+        const uintptr_t a = (s0 + pg - 1) / pg * pg, e = e0 / pg * pg;
+        if (e <= a || e - a < ((size_t)1 << 20)) return;   // small: staged
+        if (!pin.pin((void *)a, e - a, touch)) return;
+        h = a - s0;
+        t = e0 - e;
+        direct = true;
+    }
+    void h2d(char *dst, char *stage, hipStream_t st) {
+        if (!n) return;
+        if (!direct) {
+            par_memcpy(stage, p, n);
+            HIP_TRY(hipMemcpyAsync(dst, stage, n, hipMemcpyHostToDevice, st));
+            return;
+        }
+        if (h) {
+            memcpy(stage, p, h);
+            HIP_TRY(hipMemcpyAsync(dst, stage, h, hipMemcpyHostToDevice, st));
+        }
+        HIP_TRY(hipMemcpyAsync(dst + h, p + h, n - h - t, hipMemcpyHostToDevice, st));
+        if (t) {
+            memcpy(stage + n - t, p + n - t, t);
+            HIP_TRY(hipMemcpyAsync(dst + n - t, stage + n - t, t, hipMemcpyHostToDevice, st));
+        }
+    }
+    void d2h(const char *src, char *stage, hipStream_t st) {
+        if (!n) return;
+        if (!direct) {
+            HIP_TRY(hipMemcpyAsync(stage, src, n, hipMemcpyDeviceToHost, st));
+            return;
+        }
+        if (h) HIP_TRY(hipMemcpyAsync(stage, src, h, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(p + h, src + h, n - h - t, hipMemcpyDeviceToHost, st));
+        if (t) HIP_TRY(hipMemcpyAsync(stage + n - t, src + n - t, t, hipMemcpyDeviceToHost, st));
+    }
+    void d2h_finish(const char *stage) {   // after the stream sync
+        if (!n) return;
+        if (!direct) {
+            par_memcpy(p, stage, n);
+            return;
+        }
+        if (h) memcpy(p, stage, h);
+        if (t) memcpy(p + n - t, stage + n - t, t);
+    }
+};
+
 int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, const vh_run_opts *opts,
                 float *n4, uint8_t *defect, uint8_t *defect_border, uint8_t *lb, vh_vdp_result *res) {
     API_TRY(p->ctx, {
@@ -826,6 +909,7 @@ int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, con
             hipEvent_t e[3];
         };
         const bool trace = getenv("VH_PIPE_TRACE") != nullptr;
+        std::vector<std::vector<std::unique_ptr<PipeSpan[]>>> keep(slots);
         std::vector<std::vector<Mark>> marks(slots);
         hipEvent_t ev0 = nullptr;
         const auto c0 = std::chrono::steady_clock::now();
@@ -837,6 +921,39 @@ int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, con
         auto mark_ev = [&](Mark &m, int i, hipStream_t st) {
             if (trace && hipEventCreate(&m.e[i]) == hipSuccess) (void)hipEventRecord(m.e[i], st);
         };
+        // Chunk k's pipeline waits on the device for chunk k - lag's (lag = the chunks that fill the
+        // CUs, VH_PIPE_LAG overrides; 0 = no ordering).  Without it the slots ran in lockstep: all
+        // computing together, then all copying out / in together with the GPU idle (~60% of the
+        // device rate, VH_PIPE_TRACE); with it the computes are staggered and each chunk's copies
+        // overlap the next chunks' compute.  Enqueues happen in chunk order (host-side ticket).
+        int cus = 256;
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, p->ctx->device);
+        int lag = (int)std::max<int64_t>(1, (cus + sub - 1) / sub);
+        if (const char *e = getenv("VH_PIPE_LAG")) lag = atoi(e);
+        lag = std::min(lag, slots);
+        std::mutex tk_mu;
+        std::condition_variable tk_cv;
+        int64_t tk_next = 0;   // the chunk whose pipeline is enqueued next
+        bool tk_abort = false;
+        auto ticket_wait = [&](int64_t k) {
+            std::unique_lock<std::mutex> lk(tk_mu);
+            tk_cv.wait(lk, [&] { return tk_next == k || tk_abort; });
+            if (tk_abort && tk_next != k) throw PipeAbort{};
+        };
+        auto ticket_pass = [&](int64_t k) {
+            {
+                std::lock_guard<std::mutex> lk(tk_mu);
+                if (tk_next == k) tk_next = k + 1;
+            }
+            tk_cv.notify_all();
+        };
+        auto ticket_abort = [&] {
+            {
+                std::lock_guard<std::mutex> lk(tk_mu);
+                tk_abort = true;
+            }
+            tk_cv.notify_all();
+        };
         auto work = [&](int s) {
             vh_pipe::Slot &q = p->slot[s];
             vh_batch *b = q.b;
@@ -847,25 +964,19 @@ int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, con
                     const size_t CV = (size_t)cnt * V;
                     uint8_t *qm = q.u8, *qd = q.u8 + sub * V, *qb = q.u8 + 2 * sub * V,
                             *ql = q.u8 + 3 * sub * V;
-                    const hipMemcpyKind H2D = hipMemcpyHostToDevice, D2H = hipMemcpyDeviceToHost;
-                    // this chunk's caller buffers, pinned in place while its copies run (a chunk
-                    // whose pages another chunk holds, or VH_PIPE_STAGE=1, goes through the staging)
-                    HostPin g_hp, g_mk, g_n4, g_d, g_b, g_l;
+                    // this chunk's caller ranges: whole pages pinned in place while its copies run,
+                    // fragments (and everything under VH_PIPE_STAGE=1) through the slot's staging
+                    // the spans' pins are released only after the whole run (hipHostUnregister waits
+                    // for the device: released per chunk, it lined every slot up behind the others)
+                    keep[s].emplace_back(new PipeSpan[6]);
+                    PipeSpan *sp = keep[s].back().get();
+                    PipeSpan &s_hp = sp[0], &s_mk = sp[1], &s_n4 = sp[2], &s_d = sp[3], &s_b = sp[4], &s_l = sp[5];
                     Mark mk_{k, {now_ms(), 0, 0, 0, 0}, {nullptr, nullptr, nullptr}};
                     try {
-                        const bool d_hp = g_hp.pin(hp + v0 * V, sizeof(float) * CV), d_mk = g_mk.pin(mask + v0 * V, CV);
-                        if (d_hp) {
-                            HIP_TRY(hipMemcpyAsync(b->d_hp, hp + v0 * V, sizeof(float) * CV, H2D, b->stream));
-                        } else {
-                            par_memcpy(q.hp, hp + v0 * V, sizeof(float) * CV);
-                            HIP_TRY(hipMemcpyAsync(b->d_hp, q.hp, sizeof(float) * CV, H2D, b->stream));
-                        }
-                        if (d_mk) {
-                            HIP_TRY(hipMemcpyAsync(b->d_mask, mask + v0 * V, CV, H2D, b->stream));
-                        } else {
-                            par_memcpy(qm, mask + v0 * V, CV);
-                            HIP_TRY(hipMemcpyAsync(b->d_mask, qm, CV, H2D, b->stream));
-                        }
+                        s_hp.plan(hp + v0 * V, sizeof(float) * CV, false);
+                        s_mk.plan(mask + v0 * V, CV, false);
+                        s_hp.h2d((char *)b->d_hp, (char *)q.hp, b->stream);
+                        s_mk.h2d((char *)b->d_mask, (char *)qm, b->stream);
                         for (int64_t i = cnt; i < sub; ++i) {   // ragged tail: repeat the last study
                             HIP_TRY(hipMemcpyAsync(b->d_hp + i * V, b->d_hp + (cnt - 1) * V, sizeof(float) * V,
                                                    hipMemcpyDeviceToDevice, b->stream));
@@ -873,44 +984,63 @@ int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, con
                                                    hipMemcpyDeviceToDevice, b->stream));
                         }
                         mark_ev(mk_, 0, b->stream);
+                        ticket_wait(k);
                         mk_.h[1] = now_ms();
-                        batch_run(b, *opts, opts->do_n4 ? 0 : 1);
+                        try {
+                            if (lag > 0 && k >= lag)
+                                HIP_TRY(hipStreamWaitEvent(b->stream, p->slot[(k - lag) % slots].done, 0));
+                            batch_run(b, *opts, opts->do_n4 ? 0 : 1);
+                            HIP_TRY(hipEventRecord(q.done, b->stream));
+                        } catch (...) {
+                            ticket_pass(k);
+                            throw;
+                        }
+                        ticket_pass(k);
                         mark_ev(mk_, 1, b->stream);
                         mk_.h[2] = now_ms();
                         // while the chunk computes: first touch + pin of its output ranges
-                        const bool d_n4 = g_n4.pin(n4 ? n4 + v0 * V : nullptr, sizeof(float) * CV, true),
-                                   d_d = g_d.pin(defect ? defect + v0 * V : nullptr, CV, true),
-                                   d_b = g_b.pin(defect_border ? defect_border + v0 * V : nullptr, CV, true),
-                                   d_l = g_l.pin(lb ? lb + v0 * V : nullptr, CV, true);
+                        s_n4.plan(n4 ? n4 + v0 * V : nullptr, sizeof(float) * CV, true);
+                        s_d.plan(defect ? defect + v0 * V : nullptr, CV, true);
+                        s_b.plan(defect_border ? defect_border + v0 * V : nullptr, CV, true);
+                        s_l.plan(lb ? lb + v0 * V : nullptr, CV, true);
                         const float *dn4 = opts->do_n4 ? b->d_n4 : b->d_hp;
-                        if (n4) HIP_TRY(hipMemcpyAsync(d_n4 ? n4 + v0 * V : q.n4, dn4, sizeof(float) * CV, D2H, b->stream));
-                        if (defect) HIP_TRY(hipMemcpyAsync(d_d ? defect + v0 * V : qd, b->d_defect, CV, D2H, b->stream));
-                        if (defect_border) HIP_TRY(hipMemcpyAsync(d_b ? defect_border + v0 * V : qb, b->d_border, CV, D2H, b->stream));
-                        if (lb) HIP_TRY(hipMemcpyAsync(d_l ? lb + v0 * V : ql, b->d_lb, CV, D2H, b->stream));
+                        s_n4.d2h((const char *)dn4, (char *)q.n4, b->stream);
+                        s_d.d2h((const char *)b->d_defect, (char *)qd, b->stream);
+                        s_b.d2h((const char *)b->d_border, (char *)qb, b->stream);
+                        s_l.d2h((const char *)b->d_lb, (char *)ql, b->stream);
+                        if (res) {   // the scalars ride the same stream into pinned slot memory
+                            HIP_TRY(hipMemcpyAsync(q.sc, b->d_sc, sizeof(VolScalars) * sub, hipMemcpyDeviceToHost, b->stream));
+                            if (opts->do_n4)
+                                HIP_TRY(hipMemcpyAsync(q.st, b->d_st, sizeof(N4State) * sub, hipMemcpyDeviceToHost, b->stream));
+                        }
                         mark_ev(mk_, 2, b->stream);
                         mk_.h[3] = now_ms();
                         HIP_TRY(hipStreamSynchronize(b->stream));
                         mk_.h[4] = now_ms();
                         if (trace) marks[s].push_back(mk_);
                         if (res) {
-                            fill_results(b, q.res.data());
+                            fill_results_from(b, q.sc, q.st, q.res.data());
                             memcpy(res + v0, q.res.data(), sizeof(vh_vdp_result) * cnt);
                         }
-                        if (n4 && !d_n4) par_memcpy(n4 + v0 * V, q.n4, sizeof(float) * CV);
-                        if (defect && !d_d) par_memcpy(defect + v0 * V, qd, CV);
-                        if (defect_border && !d_b) par_memcpy(defect_border + v0 * V, qb, CV);
-                        if (lb && !d_l) par_memcpy(lb + v0 * V, ql, CV);
+                        s_n4.d2h_finish((const char *)q.n4);
+                        s_d.d2h_finish((const char *)qd);
+                        s_b.d2h_finish((const char *)qb);
+                        s_l.d2h_finish((const char *)ql);
                     } catch (...) {   // no copy may still touch a pinned range when it is released
                         (void)hipStreamSynchronize(b->stream);
                         throw;
                     }
                 }
+            } catch (const PipeAbort &) {   // another slot's failure is the one reported
+                failed[s] = 2;
             } catch (const VhError &e) {
                 err[s] = e;
                 failed[s] = 1;
+                ticket_abort();
             } catch (const std::exception &e) {
                 err[s] = VhError{VH_ERR_HIP, e.what()};
                 failed[s] = 1;
+                ticket_abort();
             }
         };
         std::vector<std::thread> th;
@@ -919,6 +1049,7 @@ int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, con
         for (auto &t : th) t.join();
         for (int s = 0; s < slots; ++s)   // no copy may still touch a pinned buffer when it is released
             (void)hipStreamSynchronize(p->slot[s].b->stream);
+        keep.clear();
         if (trace) {
             fprintf(stderr, "pipe_trace total_ms %.2f\n", now_ms());
             for (int s = 0; s < slots; ++s)
@@ -935,7 +1066,7 @@ int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, con
             (void)hipEventDestroy(ev0);
         }
         for (int s = 0; s < slots; ++s)
-            if (failed[s]) throw err[s];
+            if (failed[s] == 1) throw err[s];
     })
 }
 

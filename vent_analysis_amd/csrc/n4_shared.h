@@ -77,11 +77,18 @@ __device__ __forceinline__ float expm1c(float x) {
 __device__ __forceinline__ float div_r(float c, double rinv) { return (float)((double)c * rinv); }
 
 // S3 sharpen value E(u)
-__device__ __forceinline__ float sharpen_r(float u, float bmin, double rinv, const float *E, int bins) {
+__device__ __forceinline__ float sharpen_r(float u, float bmin, double rinv, const float *E, int bins,
+                                           float fbins, float elast) {
     const float cidx = div_r(u - bmin, rinv);
-    const int idx = (cidx >= 0.0f && cidx < (float)bins) ? (int)floorf(cidx) : bins;
-    if (idx < bins - 1) return E[idx] + (E[idx + 1] - E[idx]) * (cidx - (float)idx);
-    return E[bins - 1];
+    const int idx = (cidx >= 0.0f && cidx < fbins) ? (int)floorf(cidx) : bins;
+    // branch-free (a divergent branch here split the fit's row groups): both table reads always
+    // happen, at a clamped index when the value takes the last bin's E (= elast, fbins = bins)
+    const bool in = idx < bins - 1;
+    const int j = in ? idx : bins - 2;
+    const float e0 = E[j], e1 = E[j + 1];
+    float lin = e0 + (e1 - e0) * (cidx - (float)idx);
+    __asm__ volatile("" : "+v"(lin));   // keeps the select a select (not a branch round the reads)
+    return in ? lin : elast;
 }
 
 // S3 Parzen histogram contribution of one U value, packed as (1 << 44) | trunc(o * 2^24) on bin
@@ -149,6 +156,15 @@ struct TabV {
 // ---------------------------------------------------------------------------------------------
 // work item = (64-column tile, 64-row slot) of one study: the wave's view of its rows
 // ---------------------------------------------------------------------------------------------
+// a wave-uniform value moved to an SGPR (values read from LDS or shuffled are VGPRs to the
+// compiler; row loops indexed by them then pay a readfirstlane + wait states per row)
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ float uni(float v) { return __int_as_float(uni(__float_as_int(v))); }
+__device__ __forceinline__ double uni(double v) {
+    const long long b = __double_as_longlong(v);
+    return __longlong_as_double(((long long)(uint32_t)uni((int)(b >> 32)) << 32) | (uint32_t)uni((int)b));
+}
+
 struct Item {
     int tile, x0, xs, xe;     // wave-uniform: tile, slot's first row, first / last non-empty row
     uint64_t mreg;            // lane l: mask == 1 lanes of row x0 + l
@@ -164,6 +180,7 @@ __device__ __forceinline__ bool item_begin(Item &it, const uint64_t *rowmask, co
                                            const int32_t *rrank, int R, int C, int Z, int CZ,
                                            int nslots, int item) {
     const int lane = threadIdx.x & 63;
+    item = uni(item);
     it.tile = item / nslots;
     it.x0 = (item % nslots) * SLOT_R;
     const int64_t rbase = (int64_t)it.tile * R;
@@ -200,8 +217,10 @@ __device__ __forceinline__ uint32_t item_off(const Item &it, int x, bool valid, 
     const uint32_t mhi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(it.mreg >> 32), xl);
     const uint64_t m = ((uint64_t)mhi << 32) | mlo;
     const int r0 = __builtin_amdgcn_readlane(it.rsreg, xl);
-    const bool on = valid && ((m >> lane) & 1ull);
+    // lane's own bit from two lane counts (bits 0..lane minus bits below lane): no per-lane
+    // (1 << lane) mask pair to keep in VGPRs across the row loops
     const int below = lanes_below(m);
+    const bool on = valid && lanes_below(m >> 1) + (int)(m & 1ull) != below;
     if (rr) *rr = __builtin_amdgcn_readlane(it.rrreg, xl) + below;
     return on ? (uint32_t)(r0 + below) * 4u : VH_OOB;
 }
@@ -346,15 +365,18 @@ __device__ void fit_item(const Item &it, const TabV &T, const double *Wk, const 
                          unsigned long long *numfix) {
     constexpr int P = MODE == 0 ? 3 : 2;
     const __amdgpu_buffer_rsrc_t rU = st_rsrc(Ub, n);
+    bmin = uni(bmin);   // SGPRs: as VGPRs they were spilled and reloaded once per voxel
+    rinv = uni(rinv);
+    const float fbins = uni((float)bins), elast = MODE == 0 ? uni(sE[bins - 1]) : 0.0f;
     const double isyz = MODE == 0 ? T.iy[it.y] * T.iz[it.z] : 1.0;
-    int wb = T.bx[it.xs];
+    int wb = uni(T.bx[it.xs]);
     double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0, acc3 = 0.0;
     int x = it.xs, tail = 0;
     fit_ring_begin<INPLACE>(rg, it, T, Z, nb_ring);
 #pragma unroll 1
     for (;;) {
         if (x <= it.xe) {   // rows of control span wb: the window does not move
-            const int rb = min(it.xe, T.xst[wb + 1] - 1);
+            const int rb = uni(min(it.xe, T.xst[wb + 1] - 1));
             // groups of FIT_G rows, two per trip: the next group's U loads are in flight while this
             // group's rows are added (the chains still take the rows in order)
             uint32_t oA[FIT_G], oB[FIT_G];
@@ -374,21 +396,23 @@ __device__ void fit_item(const Item &it, const TabV &T, const double *Wk, const 
             auto run = [&](int xb, const uint32_t (&o)[FIT_G], const float (&u)[FIT_G]) {
 #pragma unroll
                 for (int g = 0; g < FIT_G; ++g) {
-                    if (o[g] == VH_OOB) continue;
-                    const int xg = xb + g;
+                    // branch-free: a masked-out lane / row past the span adds exact zeros (its U load
+                    // returned 0, so every operand is finite) -- see eval_item for why
+                    const bool on = o[g] != VH_OOB;
+                    const int xg = xb + g <= rb ? xb + g : rb;
                     const double2 wa = Wx[2 * xg], wc = Wx[2 * xg + 1];
                     if (MODE == 0) {
-                        const float rv = u[g] - sharpen_r(u[g], bmin, rinv, sE, bins);
-                        const double p = (double)rv * isyz;
+                        const float rv = u[g] - sharpen_r(u[g], bmin, rinv, sE, bins, fbins, elast);
+                        const double p = on ? (double)rv * isyz : 0.0;
                         acc0 = fma(wa.x, p, acc0);
                         acc1 = fma(wa.y, p, acc1);
                         acc2 = fma(wc.x, p, acc2);
                         acc3 = fma(wc.y, p, acc3);
                     } else {
-                        acc0 += wa.x;
-                        acc1 += wa.y;
-                        acc2 += wc.x;
-                        acc3 += wc.y;
+                        acc0 += on ? wa.x : 0.0;
+                        acc1 += on ? wa.y : 0.0;
+                        acc2 += on ? wc.x : 0.0;
+                        acc3 += on ? wc.y : 0.0;
                     }
                 }
             };
@@ -396,14 +420,14 @@ __device__ void fit_item(const Item &it, const TabV &T, const double *Wk, const 
                 issue(x, oA, uA);
 #pragma unroll 1
                 for (int xb = x;; xb += 2 * FIT_G) {
-                    const bool hb = xb + FIT_G <= rb;
-                    if (hb) issue(xb + FIT_G, oB, uB);
+                    // the next group is issued unconditionally (rows past rb load nothing): a branch
+                    // round the issue makes its loads maybe-pending at the join
+                    issue(xb + FIT_G, oB, uB);
                     run(xb, oA, uA);
-                    if (!hb) break;
-                    const bool ha = xb + 2 * FIT_G <= rb;
-                    if (ha) issue(xb + 2 * FIT_G, oA, uA);
+                    if (xb + FIT_G > rb) break;
+                    issue(xb + 2 * FIT_G, oA, uA);
                     run(xb + FIT_G, oB, uB);
-                    if (!ha) break;
+                    if (xb + 2 * FIT_G > rb) break;
                 }
             }
             x = rb + 1 > x ? rb + 1 : x;

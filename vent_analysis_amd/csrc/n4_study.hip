@@ -311,7 +311,7 @@ __device__ void eval_item(const Item &it, int item, int Z, const TabV &Tn, const
     const float4 wyn = it.colok ? Tn.wy[it.y] : make_float4(0.f, 0.f, 0.f, 0.f);
     const float4 wyo = it.colok ? To.wy[it.y] : make_float4(0.f, 0.f, 0.f, 0.f);
     const int byn = Tn.by[it.y], byo = To.by[it.y];
-    int wbn = Tn.bx[it.xs], wbo = To.bx[it.xs];
+    int wbn = uni(Tn.bx[it.xs]), wbo = uni(To.bx[it.xs]);
     float tn0 = col_T_lds(P1n, wbn, ncyn, Z, byn, wyn, it.z);
     float tn1 = col_T_lds(P1n, wbn + 1, ncyn, Z, byn, wyn, it.z);
     float tn2 = col_T_lds(P1n, wbn + 2, ncyn, Z, byn, wyn, it.z);
@@ -326,7 +326,13 @@ __device__ void eval_item(const Item &it, int item, int Z, const TabV &Tn, const
     double sd = 0.0, sd2 = 0.0;
     Range3 rg;
     r3_init(rg);
-    auto voxel = [&](uint32_t off, int rr, float la, int x) {
+    // one voxel; off / roff are VH_OOB for a masked-out lane or a row past the span: its stores are
+    // dropped by the buffer range check and its values are replaced by neutral ones (the current max /
+    // third smallest for the range, 0 for the sums), so the row groups below run without branches (a branch per voxel
+    // made every load of the group a maybe-pending one at the joins, and the waits for them undid
+    // the next group's prefetch)
+    auto voxel = [&](uint32_t off, uint32_t roff, float la, int x) {
+        const bool on = off != VH_OOB;
         const float4 w = Tn.wx[x];
         const float bn = ((w.x * tn0 + w.y * tn1) + w.z * tn2) + w.w * tn3;
         float bo = 0.0f;
@@ -340,22 +346,24 @@ __device__ void eval_item(const Item &it, int item, int Z, const TabV &Tn, const
 #endif
         if (CM == 0) {
 #ifndef AB_EVAL_NOSTORE
-            st_store(rD, (uint32_t)rr * 4u, bo - bn);
+            st_store(rD, roff, bo - bn);
 #else
-            if (bo - bn == 12345.0f) st_store(rD, (uint32_t)rr * 4u, u);
+            if (bo - bn == 12345.0f) st_store(rD, roff, u);
 #endif
         } else {
-            const double d = (double)expm1c(bo - bn);
+            const double d = on ? (double)expm1c(bo - bn) : 0.0;
             sd += d;
             sd2 = fma(d, d, sd2);
         }
-        r3_add(rg, u);
+        const float um = on ? u : rg.mx, un = on ? u : rg.m3;   // neutral: max(mx, mx), ins(m3)
+        rg.mx = fmaxf(rg.mx, um);
+        r3_ins(rg, un);
     };
     if (SAME) {
         int x = it.xs;
 #pragma unroll 1
         for (;;) {
-            const int rb = min(it.xe, Tn.xst[wbn + 1] - 1);
+            const int rb = uni(min(it.xe, Tn.xst[wbn + 1] - 1));
             // groups of FIT_G rows, two per trip: the next group's L0 loads are in flight while
             // this group's voxels are evaluated (the span's rows only: the window moves after it)
             uint32_t oA[FIT_G], oB[FIT_G];
@@ -365,7 +373,9 @@ __device__ void eval_item(const Item &it, int item, int Z, const TabV &Tn, const
 #pragma unroll
                 for (int g = 0; g < FIT_G; ++g) {
                     const int xg = xb + g;
-                    o[g] = item_off(it, xg <= rb ? xg : rb, xg <= rb, CM == 0 ? &r[g] : nullptr);
+                    int rr = 0;
+                    o[g] = item_off(it, xg <= rb ? xg : rb, xg <= rb, CM == 0 ? &rr : nullptr);
+                    r[g] = o[g] == VH_OOB ? (int)VH_OOB : rr * 4;
 #ifdef AB_EVAL_NOLOAD   // A/B builds only (fixed iteration counts): the phase without its L0 loads
                     l[g] = 1.0f + (float)g;
 #else
@@ -376,20 +386,18 @@ __device__ void eval_item(const Item &it, int item, int Z, const TabV &Tn, const
             auto run = [&](int xb, const uint32_t (&o)[FIT_G], const int (&r)[FIT_G], const float (&l)[FIT_G]) {
 #pragma unroll
                 for (int g = 0; g < FIT_G; ++g)
-                    if (o[g] != VH_OOB) voxel(o[g], CM == 0 ? r[g] : 0, l[g], xb + g);
+                    voxel(o[g], CM == 0 ? (uint32_t)r[g] : VH_OOB, l[g], xb + g <= rb ? xb + g : rb);
             };
             if (x <= rb) {
                 issue(x, oA, rA, lA);
 #pragma unroll 1
                 for (int xb = x;; xb += 2 * FIT_G) {
-                    const bool hb = xb + FIT_G <= rb;
-                    if (hb) issue(xb + FIT_G, oB, rB, lB);
+                    issue(xb + FIT_G, oB, rB, lB);   // unconditional, as in fit_item
                     run(xb, oA, rA, lA);
-                    if (!hb) break;
-                    const bool ha = xb + 2 * FIT_G <= rb;
-                    if (ha) issue(xb + 2 * FIT_G, oA, rA, lA);
+                    if (xb + FIT_G > rb) break;
+                    issue(xb + 2 * FIT_G, oA, rA, lA);
                     run(xb + FIT_G, oB, rB, lB);
-                    if (!ha) break;
+                    if (xb + 2 * FIT_G > rb) break;
                 }
             }
             x = rb + 1 > x ? rb + 1 : x;
@@ -406,13 +414,13 @@ __device__ void eval_item(const Item &it, int item, int Z, const TabV &Tn, const
     } else {
 #pragma unroll 1
         for (int x = it.xs; x <= it.xe; ++x) {
-            const int bxn = Tn.bx[x];
+            const int bxn = uni(Tn.bx[x]);
             while (bxn > wbn) {
                 ++wbn;
                 tn0 = tn1; tn1 = tn2; tn2 = tn3;
                 tn3 = col_T_lds(P1n, wbn + 3, ncyn, Z, byn, wyn, it.z);
             }
-            const int bxo = To.bx[x];
+            const int bxo = uni(To.bx[x]);
             while (bxo > wbo) {
                 ++wbo;
                 to0 = to1; to1 = to2; to2 = to3;
@@ -420,7 +428,7 @@ __device__ void eval_item(const Item &it, int item, int Z, const TabV &Tn, const
             }
             int rr = 0;
             const uint32_t off = item_off(it, x, true, CM == 0 ? &rr : nullptr);
-            if (off != VH_OOB) voxel(off, rr, st_load(rL, off), x);
+            if (off != VH_OOB) voxel(off, (uint32_t)rr * 4u, st_load(rL, off), x);
         }
     }
     if (CM != 0) {
@@ -594,8 +602,8 @@ __device__ void refine_axis_st(const float *in, float *out, int d0, int d1, int 
 __device__ __forceinline__ int next_item(StudyMisc &M, const int32_t *ordr, int nitems) {
     int item = 0;
     if ((threadIdx.x & 63) == 0) item = atomicAdd(&M.item_ctr, 1);
-    item = __shfl(item, 0, 64);
-    return item >= nitems ? -1 : ordr[item];
+    item = uni(__shfl(item, 0, 64));
+    return item >= nitems ? -1 : uni(ordr[item]);
 }
 
 // ---------------------------------------------------------------------------------------------

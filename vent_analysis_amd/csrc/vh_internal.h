@@ -6,6 +6,7 @@
 #include <cstdio>
 #include <map>
 #include <set>
+#include <condition_variable>
 #include <mutex>
 #include <thread>
 #include <string>
@@ -129,6 +130,9 @@ struct vh_pipe {
         vh_batch *b = nullptr;
         float *hp = nullptr, *n4 = nullptr;   // pinned staging [sub][V]
         uint8_t *u8 = nullptr;                // pinned: mask, defect, border, lb ([4][sub][V])
+        hipEvent_t done = nullptr;            // recorded after the slot's current chunk's pipeline
+        VolScalars *sc = nullptr;             // pinned per-study scalars / N4 states of the chunk
+        N4State *st = nullptr;
         std::vector<vh_vdp_result> res;
     };
     vh_ctx *ctx = nullptr;
