@@ -874,11 +874,38 @@ __device__ void lds_fft2(double2 *x, double2 *y, double2 *tx, double2 *ty, const
 }
 
 
+// Slice sums of a study's chunk histograms for studies with many chunks (a 512^3 study has ~7k:
+// one emap block summing them alone took ~0.4 ms per iteration).  Block (s, b) adds chunks
+// ca + s*per .. of study b per bin, counts and o-weight sums apart (integer sums: exact, order-free);
+// k_n4_emap then adds the N4_HSL slices.
+#define N4_HSL 64
+__global__ void __launch_bounds__(VH_TPB) k_n4_hred(const uint64_t *hpart, const int32_t *cp,
+                                                   const N4State *st, int bins, uint64_t *hred,
+                                                   int64_t vol0) {
+    const int64_t b = vol0 + blockIdx.y;
+    if (!st[b].active) return;
+    const int32_t ca = cp[b], ce = cp[b + 1];
+    const int32_t per = (ce - ca + N4_HSL - 1) / N4_HSL, c0 = ca + (int32_t)blockIdx.x * per,
+                  c1 = min(ce, c0 + per);
+    uint64_t *out = hred + ((int64_t)blockIdx.y * N4_HSL + blockIdx.x) * 2 * VH_MAX_BINS;
+    for (int h = threadIdx.x; h < bins; h += VH_TPB) {
+        uint64_t cs = 0ull, os = 0ull;
+#pragma unroll 8
+        for (int32_t c = c0; c < c1; ++c) {
+            const uint64_t w = hpart[(int64_t)c * VH_MAX_BINS + h];
+            cs += hist_count(w);
+            os += hist_osum(w);
+        }
+        out[h] = cs;
+        out[VH_MAX_BINS + h] = os;
+    }
+}
+
 // E(u|v) map (Wiener deconvolution of the histogram by the bias Gaussian), one block per volume.
 __global__ void __launch_bounds__(VH_TPB) k_n4_emap(const uint64_t *hpart, const int32_t *cp,
                                                    const double2 *tw, int bins, float fwhm,
                                                    float noise, const N4State *st, float *Eout,
-                                                   int64_t vol0) {
+                                                   int64_t vol0, const uint64_t *hred) {
     __shared__ double2 V[VH_FFT_P], F[VH_FFT_P], U[VH_FFT_P], NUM[VH_FFT_P], DEN[VH_FFT_P],
         TMP[VH_FFT_P], TMP2[VH_FFT_P], TW[VH_FFT_P / 2];
     const int64_t b = vol0 + blockIdx.x;
@@ -897,13 +924,22 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_emap(const uint64_t *hpart, const
         const int h = t & 255, sl = t >> 8;
         const int32_t per = (ce - ca + NSL - 1) / NSL, c0 = ca + sl * per, c1 = min(ce, c0 + per);
         uint64_t cs = 0ull, os = 0ull;
-        if (h < bins)
+        if (hred) {   // k_n4_hred's slices of this study
+            const uint64_t *r = hred + (int64_t)blockIdx.x * N4_HSL * 2 * VH_MAX_BINS;
+            if (h < bins && sl == 0)
+#pragma unroll 8
+                for (int q = 0; q < N4_HSL; ++q) {
+                    cs += r[(int64_t)q * 2 * VH_MAX_BINS + h];
+                    os += r[(int64_t)q * 2 * VH_MAX_BINS + VH_MAX_BINS + h];
+                }
+        } else if (h < bins) {
 #pragma unroll 8
             for (int32_t c = c0; c < c1; ++c) {
                 const uint64_t w = hpart[(int64_t)c * VH_MAX_BINS + h];
                 cs += hist_count(w);
                 os += hist_osum(w);
             }
+        }
         pc[sl * 256 + h] = cs;
         po[sl * 256 + h] = os;
     }
@@ -1725,6 +1761,21 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
     std::vector<int> ev_slot;   // iteration slot (d_nactive / h_flags index) behind each event
     if (!b->h_flags) HIP_TRY(hipHostMalloc((void **)&b->h_flags, sizeof(int32_t) * 1024));
     int32_t *hflag = b->h_flags;
+    // studies with many chunks: their chunk histograms are summed in slices first (k_n4_hred)
+    int32_t max_ch = 0;
+    for (int64_t v = vol0; v < vol0 + ns; ++v) max_ch = std::max(max_ch, hcp[v + 1] - hcp[v]);
+    uint64_t *hred = nullptr;
+    if (max_ch >= 4 * N4_HSL) {
+        const size_t need = sizeof(uint64_t) * (size_t)ns * N4_HSL * 2 * VH_MAX_BINS;
+        if (need > b->hred_cap) {
+            if (b->d_hred) HIP_TRY(hipFree(b->d_hred));
+            b->d_hred = nullptr;
+            b->hred_cap = 0;
+            HIP_TRY(hipMalloc(&b->d_hred, need));
+            b->hred_cap = need;
+        }
+        hred = b->d_hred;
+    }
     int total_iters = 0;
     for (int L = 0; L < prm.n_levels; ++L) total_iters += prm.max_iters[L];
     HIP_TRY(hipMemsetAsync(b->d_nactive, 0, sizeof(int32_t) * (total_iters + 1), st));
@@ -1818,9 +1869,14 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
                                                                 bins, b->d_st, b->d_hpart, ch0);
                     VH_CHECK_LAUNCH();
                 }
+                if (hred) {
+                    k_n4_hred<<<dim3(N4_HSL, (unsigned)ns), VH_TPB, 0, st>>>(b->d_hpart, b->d_cp, b->d_st,
+                                                                             bins, hred, vol0);
+                    VH_CHECK_LAUNCH();
+                }
                 k_n4_emap<<<(unsigned)ns, VH_TPB, 0, st>>>(b->d_hpart, b->d_cp, b->d_twiddle, bins,
                                                            prm.fwhm, prm.wiener_noise, b->d_st,
-                                                           b->d_E, vol0);
+                                                           b->d_E, vol0, hred);
                 VH_CHECK_LAUNCH();
                 {
                     ScopedKTimer tm(b, "n4_fit", 0.0);

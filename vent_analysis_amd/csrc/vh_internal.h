@@ -188,6 +188,8 @@ struct vh_batch {
     int32_t *d_cp = nullptr;         // [nb + 1] chunk prefix (N4_CH voxels per chunk)
     int32_t *d_cvol = nullptr;       // [chunks] owning volume
     uint64_t *d_hpart = nullptr;     // [chunks][VH_MAX_BINS] per-chunk histograms
+    uint64_t *d_hred = nullptr;      // [studies][N4_HSL][2][VH_MAX_BINS] slice sums (k_n4_hred)
+    size_t hred_cap = 0;
     double *d_cpart = nullptr;       // [chunks][2] per-chunk convergence sums
     int64_t n4_tiles = 0;
     std::vector<size_t> lvx_off;     // per level: xst / wk3 / wk2 offsets in d_tabs
