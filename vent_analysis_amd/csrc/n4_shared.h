@@ -362,7 +362,16 @@ template <int MODE, bool INPLACE>
 __device__ void fit_item(const Item &it, const TabV &T, const double *Wk, const double2 *Wx,
                          int ncy, int ncz, int Z, int bins, const float *Ub, int64_t n,
                          const float *sE, float bmin, double rinv, FitRing &rg, int nb_ring,
-                         unsigned long long *numfix) {
+                         unsigned long long *numfix, unsigned long long *fprof = nullptr) {
+    // fprof (profiling builds): lane 0 adds the cycles of the row loops / pushes / contraction
+    unsigned long long fpc = fprof ? clock64() : 0ull;
+    auto fpm = [&](int k) {
+        if (fprof && (threadIdx.x & 63) == 0) {
+            const unsigned long long c = clock64();
+            fprof[k] += c - fpc;
+            fpc = c;
+        }
+    };
     constexpr int P = MODE == 0 ? 3 : 2;
     const __amdgpu_buffer_rsrc_t rU = st_rsrc(Ub, n);
     bmin = uni(bmin);   // SGPRs: as VGPRs they were spilled and reloaded once per voxel
@@ -432,12 +441,16 @@ __device__ void fit_item(const Item &it, const TabV &T, const double *Wk, const 
             }
             x = rb + 1 > x ? rb + 1 : x;
         }
+        fpm(0);
         fit_push<P, INPLACE>(rg, acc0, wb, it, T, Wk, ncy, ncz, Z, numfix);   // control row wb is done
+        fpm(1);
         acc0 = acc1; acc1 = acc2; acc2 = acc3; acc3 = 0.0;
         ++wb;
         if (x > it.xe && ++tail == 4) break;
     }
     fit_contract<P, INPLACE>(rg, it, T, Wk, ncy, ncz, Z, numfix);
+    fpm(2);
+    if (fprof && (threadIdx.x & 63) == 0) fprof[3] += 1;
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -126,6 +126,9 @@ struct StudyMisc {
     int32_t rx[ST_NFIRST], rc[ST_NFIRST];   // their (row, column)
     float fu[ST_NFIRST];   // their values in the current field (ctrl wave)
     float bin_min, slope, bmax, pad;
+#ifdef ST_PROF
+    unsigned long long fprof[4];   // wave of thread st_pt: fit rows / push / contract / items
+#endif
     double sd, sd2, conv;
     int32_t nc[2][3];
     ChainState ch[ST_NG];
@@ -738,6 +741,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
     }
 #ifdef ST_PROF
     unsigned long long st_prof[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_t0 = clock64();
+    if (t == 0) M.fprof[0] = M.fprof[1] = M.fprof[2] = M.fprof[3] = 0ull;
 #endif
     int ch_seen = 0;   // chain waves: the last request taken
     for (int L = 0; L < a.nlev; ++L) {
@@ -1019,7 +1023,11 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                     Item it;
                     if (!study_item(it, a, b, item)) continue;
                     fit_item<0, true>(it, T, Wk3, Wx3, ncy, ncz, a.Z, bins, Ub, n, sE, bmin, rinv, ring,
-                                      a.nb_ring, numfix);
+                                      a.nb_ring, numfix
+#ifdef ST_PROF
+                                      , (t >> 6) == (st_pt >> 6) ? M.fprof : nullptr
+#endif
+                                      );
                 }
                 gsync(g, M);
                 ST_MARK(4);
@@ -1192,6 +1200,11 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                st_prof[0], st_prof[1], st_prof[2], st_prof[3],
                st_prof[4], st_prof[5], st_prof[6], st_prof[7], st_prof[8], st_prof[9], st_prof[10],
                st_prof[11], st_prof[12], st_prof[13], st_prof[14], st_prof[3]);
+#ifdef ST_PROF
+    if (t == st_pt && blockIdx.x == 0)
+        printf("ST_PROF fit: rows %llu push %llu contract %llu items %llu\n", M.fprof[0], M.fprof[1],
+               M.fprof[2], M.fprof[3]);
+#endif
 #endif
     // final field's P1 for k_n4_final
     const double *P1f = M.cur ? P1b1 : P1b0;
