@@ -61,3 +61,42 @@ for size in (256 << 20, 1 << 30):
     td = time.perf_counter() - t
     print(f"pinned {size / GB:.2f} GB: one-thread memcpy {size / GB / tc:.1f} GB/s, H2D {size / GB / th:.1f} GB/s, "
           f"D2H {size / GB / td:.1f} GB/s")
+
+
+# both directions at once (two streams), registered (4 KiB pages) vs hipHostMalloc memory
+hip.hipStreamCreate.argtypes = [ct.POINTER(ct.c_void_p)]
+hip.hipMemcpyAsync.argtypes = [ct.c_void_p, ct.c_void_p, ct.c_size_t, ct.c_int, ct.c_void_p]
+hip.hipStreamSynchronize.argtypes = [ct.c_void_p]
+s1, s2 = ct.c_void_p(), ct.c_void_p()
+ok(hip.hipStreamCreate(ct.byref(s1)), "stream")
+ok(hip.hipStreamCreate(ct.byref(s2)), "stream")
+size = 1 << 30
+d1, d2 = ct.c_void_p(), ct.c_void_p()
+ok(hip.hipMalloc(ct.byref(d1), size), "hipMalloc")
+ok(hip.hipMalloc(ct.byref(d2), size), "hipMalloc")
+a = np.ones(size // 4, np.float32)
+b = np.ones(size // 4, np.float32)
+ok(hip.hipHostRegister(a.ctypes.data, size, 0), "reg")
+ok(hip.hipHostRegister(b.ctypes.data, size, 0), "reg")
+for label, src, dst in (("registered", a.ctypes.data, b.ctypes.data),):
+    for _ in range(2):
+        t = time.perf_counter()
+        ok(hip.hipMemcpyAsync(d1, src, size, H2D, s1), "h2d")
+        ok(hip.hipMemcpyAsync(dst, d2, size, D2H, s2), "d2h")
+        ok(hip.hipStreamSynchronize(s1), "sync")
+        ok(hip.hipStreamSynchronize(s2), "sync")
+        dt = time.perf_counter() - t
+    print(f"bidirectional {label} 1 GB each way: {2 * size / GB / dt:.1f} GB/s combined")
+ok(hip.hipHostUnregister(a.ctypes.data), "unreg")
+ok(hip.hipHostUnregister(b.ctypes.data), "unreg")
+p1, p2 = ct.c_void_p(), ct.c_void_p()
+ok(hip.hipHostMalloc(ct.byref(p1), size, 0), "hm")
+ok(hip.hipHostMalloc(ct.byref(p2), size, 0), "hm")
+for _ in range(2):
+    t = time.perf_counter()
+    ok(hip.hipMemcpyAsync(d1, p1, size, H2D, s1), "h2d")
+    ok(hip.hipMemcpyAsync(p2, d2, size, D2H, s2), "d2h")
+    ok(hip.hipStreamSynchronize(s1), "sync")
+    ok(hip.hipStreamSynchronize(s2), "sync")
+    dt = time.perf_counter() - t
+print(f"bidirectional hipHostMalloc 1 GB each way: {2 * size / GB / dt:.1f} GB/s combined")

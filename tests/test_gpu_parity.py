@@ -196,18 +196,27 @@ def test_rccl_cohort_allreduce_one_rank():
         _lib.comm_destroy()
 
 
-def test_pipe_host_to_host_equals_batch():
-    """vh_pipe (3 slots x 4-volume sub-batches, ragged last sub-batch) returns exactly what one
-    device-resident batch returns for the same 10 studies."""
-    hp, mk = synth_batch(64, 64, 16, 10, base_seed=77)
+@pytest.mark.parametrize("shape,n,sub,slots,twos", [((64, 64, 16), 10, 4, 3, False),
+                                                    ((64, 64, 16), 10, 4, 3, True),
+                                                    ((128, 128, 24), 21, 8, 4, False)])
+def test_pipe_host_to_host_equals_batch(shape, n, sub, slots, twos):
+    """vh_pipe (slots x sub-volume sub-batches, ragged last sub-batch) returns exactly what one
+    device-resident batch returns for the same studies: the mask crossing PCIe as bits (or as bytes
+    when it holds values other than 0 / 1: twos), the output maps packed into one byte, the
+    caller's whole pages pinned in place (the 128x128x24 case) and the chunk computes staggered."""
+    R, C, Z = shape
+    hp, mk = synth_batch(R, C, Z, n, base_seed=77)
+    if twos:   # a mask value 2 somewhere outside the lung: the byte path must carry it as is
+        mk = mk.copy()
+        mk[:, 0, 0, :] = 2
     vox = (1.5, 1.5, 10.0)
-    B = _lib.Batch(64, 64, 16, 10)
+    B = _lib.Batch(R, C, Z, n)
     B.upload(hp, mk)
     o = B.options(do_n4=True, vox=vox)
     B.run(o)
     ref = B.download(n4=True)
     B.close()
-    P = _lib.Pipe(64, 64, 16, 4, slots=3)
+    P = _lib.Pipe(R, C, Z, sub, slots=slots)
     got = P.run(hp, mk, o)
     P.close()
     for a, b in zip(got[:4], ref[:4]):

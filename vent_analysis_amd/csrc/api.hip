@@ -292,9 +292,12 @@ static void pipe_free(vh_pipe *p) {
             batch_free(q.b);
         }
         if (q.hp) (void)hipHostFree(q.hp);
+        if (q.d_pack) (void)hipFree(q.d_pack);
+        if (q.mb) (void)hipHostFree(q.mb);
         if (q.n4) (void)hipHostFree(q.n4);
         if (q.u8) (void)hipHostFree(q.u8);
         if (q.done) (void)hipEventDestroy(q.done);
+        if (q.h2d) (void)hipEventDestroy(q.h2d);
         if (q.sc) (void)hipHostFree(q.sc);
         if (q.st) (void)hipHostFree(q.st);
     }
@@ -731,6 +734,108 @@ int vh_recon(vh_ctx *ctx, const double *k, int64_t n0, int64_t n1, int64_t nz, d
 // pageable <-> pinned staging copies split over host threads: one thread's memcpy (~5-10 GB/s) bounded
 // the whole pipeline at about half the device-resident rate; the copy engines and the
 // PCIe link are far from busy at that rate
+// The three u8 maps of a pipe chunk leave the GPU as one byte per voxel, defect | border << 1 |
+// LB class << 2 (0/1, 0/1, 0..6): PCIe carries H2D and D2H together at ~53 GB/s on the box
+// (scripts/dev/h2h_probe.py, both directions at once), so the host-to-host rate is link-bound
+// near the device rate; this takes 12 -> 10 bytes per voxel.  The slot's host threads unpack.
+__global__ void k_pack_maps(const uint8_t *__restrict__ d, const uint8_t *__restrict__ b,
+                            const uint8_t *__restrict__ l, uint8_t *__restrict__ out, int64_t n) {
+    const int64_t n16 = n / 16;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint4 vd = reinterpret_cast<const uint4 *>(d)[i], vb = reinterpret_cast<const uint4 *>(b)[i],
+                    vl = reinterpret_cast<const uint4 *>(l)[i];
+        uint4 o;   // bytes pack lane-wise: no carries (defect, border <= 1, class <= 6)
+        o.x = vd.x | (vb.x << 1) | (vl.x << 2);
+        o.y = vd.y | (vb.y << 1) | (vl.y << 2);
+        o.z = vd.z | (vb.z << 1) | (vl.z << 2);
+        o.w = vd.w | (vb.w << 1) | (vl.w << 2);
+        reinterpret_cast<uint4 *>(out)[i] = o;
+    }
+    for (int64_t i = n16 * 16 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        out[i] = (uint8_t)(d[i] | (b[i] << 1) | (l[i] << 2));
+}
+
+static void par_memcpy(void *dst, const void *src, size_t bytes);
+
+// The mask crosses PCIe as one bit per voxel (bit i % 8 of byte i / 8); k_unpack_mask restores the
+// bytes on the device.  par_pack_mask returns false (nothing usable) if a byte is not 0 / 1.
+__global__ void k_unpack_mask(const uint8_t *__restrict__ bits, uint8_t *__restrict__ mask, int64_t n) {
+    const int64_t nb = (n + 7) / 8;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t v = bits[i];
+        if (i * 8 + 8 <= n) {
+            uint64_t w = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) w |= (uint64_t)((v >> k) & 1u) << (8 * k);
+            memcpy(mask + i * 8, &w, 8);
+        } else {
+            for (int64_t k = 0; i * 8 + k < n; ++k) mask[i * 8 + k] = (uint8_t)((v >> k) & 1u);
+        }
+    }
+}
+
+static bool par_pack_mask(const uint8_t *src, uint8_t *dst, size_t n) {
+    const size_t chunk = (size_t)8 << 20;   // bytes of mask per task (a multiple of 8)
+    const int want = (int)std::max<size_t>(1, std::min<size_t>(VH_COPY_THREADS, (n + chunk - 1) / chunk));
+    std::vector<int> bad(want, 0);
+    auto run = [&](int t, size_t o, size_t m) {   // [o, o + m), o a multiple of 8
+        uint64_t hi = 0;
+        size_t i = o;
+        for (; i + 8 <= o + m; i += 8) {
+            uint64_t w;
+            memcpy(&w, src + i, 8);
+            hi |= w;
+            dst[i / 8] = (uint8_t)((w * 0x0102040810204080ull) >> 56);   // byte k's bit 0 -> bit k
+        }
+        if (i < o + m) {
+            uint8_t v = 0;
+            for (size_t k = 0; i + k < o + m; ++k) {
+                hi |= src[i + k];
+                v |= (uint8_t)((src[i + k] & 1u) << k);
+            }
+            dst[i / 8] = v;
+        }
+        bad[t] = (hi & 0xFEFEFEFEFEFEFEFEull) != 0;
+    };
+    const size_t per = ((n + want - 1) / want + 7) / 8 * 8;
+    std::vector<std::thread> th;
+    for (int t = 1; t < want; ++t) {
+        const size_t o = per * t;
+        if (o < n) th.emplace_back(run, t, o, std::min(per, n - o));
+    }
+    run(0, 0, std::min(per, n));
+    for (auto &x : th) x.join();
+    for (int t = 0; t < want; ++t)
+        if (bad[t]) return false;
+    return true;
+}
+
+// the caller's maps from the packed bytes (any of d / b / l may be null), on host threads
+static void par_unpack_maps(const uint8_t *src, uint8_t *d, uint8_t *b, uint8_t *l, size_t n) {
+    const size_t chunk = (size_t)8 << 20;
+    const int want = (int)std::min<size_t>(VH_COPY_THREADS, (n + chunk - 1) / chunk);
+    auto run = [=](size_t o, size_t m) {
+        for (size_t i = o; i < o + m; ++i) {
+            const uint8_t v = src[i];
+            if (d) d[i] = v & 1u;
+            if (b) b[i] = (v >> 1) & 1u;
+            if (l) l[i] = v >> 2;
+        }
+    };
+    if (want <= 1) {
+        run(0, n);
+        return;
+    }
+    std::vector<std::thread> th;
+    const size_t per = (n + want - 1) / want;
+    for (int i = 1; i < want; ++i) {
+        const size_t o = per * i;
+        if (o < n) th.emplace_back(run, o, std::min(per, n - o));
+    }
+    run(0, std::min(per, n));
+    for (auto &t : th) t.join();
+}
+
 static void par_memcpy(void *dst, const void *src, size_t bytes) {
     const size_t chunk = (size_t)16 << 20;   // 16 MiB per task
     const int want = (int)std::min<size_t>(VH_COPY_THREADS, (bytes + chunk - 1) / chunk);
@@ -769,8 +874,12 @@ int vh_pipe_create(vh_ctx *ctx, int64_t R, int64_t C, int64_t Z, int64_t sub, in
                 q.b = batch_new(ctx, R, C, Z, sub);
                 HIP_TRY(hipHostMalloc((void **)&q.hp, sizeof(float) * NV));
                 HIP_TRY(hipHostMalloc((void **)&q.n4, sizeof(float) * NV));
-                HIP_TRY(hipHostMalloc((void **)&q.u8, 4 * NV));   // mask, defect, border, lb
+                HIP_TRY(hipHostMalloc((void **)&q.u8, 2 * NV));   // mask in, packed maps out
                 HIP_TRY(hipEventCreateWithFlags(&q.done, hipEventDisableTiming));
+                HIP_TRY(hipEventCreateWithFlags(&q.h2d, hipEventDisableTiming));
+                HIP_TRY(hipMalloc((void **)&q.d_pack, (size_t)NV));
+                q.mb_half = ((size_t)NV / 8 + 1 + 63) / 64 * 64;
+                HIP_TRY(hipHostMalloc((void **)&q.mb, 2 * q.mb_half));
                 HIP_TRY(hipHostMalloc((void **)&q.sc, sizeof(VolScalars) * sub));
                 HIP_TRY(hipHostMalloc((void **)&q.st, sizeof(N4State) * sub));
                 q.res.resize(sub);
@@ -830,12 +939,14 @@ struct HostPin {
     }
 };
 
+struct PipeAbort {   // a pipe slot stopped because another slot failed
+    int slot = -1;
+};
+
 // One caller range of a pipe chunk.  Only its whole pages are pinned (and DMA'd in place): a page
 // it shares with the neighbouring chunk or another buffer must never be registered twice or
 // unregistered under another range's copy, so the head and tail fragments (< 1 page each) go
 // through the slot's pinned staging at the same offsets.  A range that cannot be pinned is staged.
-struct PipeAbort {};   // a pipe slot stopped because another slot failed
-
 struct PipeSpan {
     char *p = nullptr;
     size_t n = 0, h = 0, t = 0;
@@ -954,78 +1065,128 @@ int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, con
             }
             tk_cv.notify_all();
         };
+        // Per slot, chunk by chunk: prep (host: pin the input pages, pack the mask bits) -> front
+        // (enqueue H2D, the pipeline behind its ticket and lag event, the map packing) -> back
+        // (first-touch + pin the n4 output pages, enqueue the D2Hs) -> sync -> finish (results,
+        // fragments, map unpacking).  The next chunk's prep runs before this chunk's sync and its
+        // front right after it, so the host work of finish overlaps the next chunk's H2D and
+        // compute (its D2H is enqueued after finish: the staging it writes is free by then).
+        struct Chunk {
+            int64_t k = -1, v0 = 0, cnt = 0;
+            size_t CV = 0;
+            PipeSpan *sp = nullptr;
+            bool mbits = false;
+            uint8_t *mb = nullptr;
+            Mark mk{};
+        };
+        const bool maps = defect || defect_border || lb;
         auto work = [&](int s) {
             vh_pipe::Slot &q = p->slot[s];
             vh_batch *b = q.b;
+            uint8_t *qm = q.u8, *qd = q.u8 + sub * V;   // mask bytes in (fallback), packed maps out
+            auto prep = [&](Chunk &c, int64_t k) {
+                c.k = k;
+                c.v0 = k * sub;
+                c.cnt = std::min(sub, n - c.v0);
+                c.CV = (size_t)c.cnt * V;
+                c.mk = Mark{k, {now_ms(), 0, 0, 0, 0}, {nullptr, nullptr, nullptr}};
+                // the spans' pins are released only after the whole run (hipHostUnregister waits
+                // for the device: released per chunk, it lined every slot up behind the others)
+                keep[s].emplace_back(new PipeSpan[3]);
+                c.sp = keep[s].back().get();
+                c.sp[0].plan(hp + c.v0 * V, sizeof(float) * c.CV, false);
+                c.mb = q.mb + ((k / slots) & 1) * q.mb_half;   // bits double-buffered across chunks
+                c.mbits = !getenv("VH_PIPE_STAGE") && par_pack_mask(mask + c.v0 * V, c.mb, c.CV);
+                if (!c.mbits) c.sp[1].plan(mask + c.v0 * V, c.CV, false);
+            };
+            auto front = [&](Chunk &c) {
+                const size_t CV = c.CV;
+                // enqueues in chunk order; the H2Ds also run in chunk order (each waits for the one
+                // before): at the start the first chunks' inputs get the whole link instead of
+                // every slot's sharing it
+                ticket_wait(c.k);
+                try {
+                if (c.k > 0) HIP_TRY(hipStreamWaitEvent(b->stream, p->slot[(c.k - 1) % slots].h2d, 0));
+                c.sp[0].h2d((char *)b->d_hp, (char *)q.hp, b->stream);
+                if (c.mbits) {
+                    HIP_TRY(hipMemcpyAsync(q.d_pack, c.mb, (CV + 7) / 8, hipMemcpyHostToDevice, b->stream));
+                    k_unpack_mask<<<(unsigned)std::min<int64_t>(4096, ((int64_t)(CV + 7) / 8 + 255) / 256), 256, 0,
+                                    b->stream>>>(q.d_pack, b->d_mask, (int64_t)CV);
+                    HIP_TRY(hipGetLastError());
+                } else {
+                    c.sp[1].h2d((char *)b->d_mask, (char *)qm, b->stream);
+                }
+                for (int64_t i = c.cnt; i < sub; ++i) {   // ragged tail: repeat the last study
+                    HIP_TRY(hipMemcpyAsync(b->d_hp + i * V, b->d_hp + (c.cnt - 1) * V, sizeof(float) * V,
+                                           hipMemcpyDeviceToDevice, b->stream));
+                    HIP_TRY(hipMemcpyAsync(b->d_mask + i * V, b->d_mask + (c.cnt - 1) * V, V,
+                                           hipMemcpyDeviceToDevice, b->stream));
+                }
+                HIP_TRY(hipEventRecord(q.h2d, b->stream));
+                mark_ev(c.mk, 0, b->stream);
+                c.mk.h[1] = now_ms();
+                if (lag > 0 && c.k >= lag)
+                    HIP_TRY(hipStreamWaitEvent(b->stream, p->slot[(c.k - lag) % slots].done, 0));
+                batch_run(b, *opts, opts->do_n4 ? 0 : 1);
+                HIP_TRY(hipEventRecord(q.done, b->stream));
+                } catch (...) {
+                    ticket_pass(c.k);
+                    throw;
+                }
+                ticket_pass(c.k);
+                mark_ev(c.mk, 1, b->stream);
+                c.mk.h[2] = now_ms();
+                if (maps) {   // the three maps packed into one byte per voxel (k_pack_maps)
+                    k_pack_maps<<<(unsigned)std::min<int64_t>(4096, ((int64_t)CV / 16 + 255) / 256 + 1), 256, 0,
+                                  b->stream>>>(b->d_defect, b->d_border, b->d_lb, q.d_pack, (int64_t)CV);
+                    HIP_TRY(hipGetLastError());
+                }
+            };
+            auto back = [&](Chunk &c) {
+                // while the chunk computes: first touch + pin of its output pages
+                c.sp[2].plan(n4 ? n4 + c.v0 * V : nullptr, sizeof(float) * c.CV, true);
+                const float *dn4 = opts->do_n4 ? b->d_n4 : b->d_hp;
+                c.sp[2].d2h((const char *)dn4, (char *)q.n4, b->stream);
+                if (maps) HIP_TRY(hipMemcpyAsync(qd, q.d_pack, c.CV, hipMemcpyDeviceToHost, b->stream));
+                if (res) {   // the scalars ride the same stream into pinned slot memory
+                    HIP_TRY(hipMemcpyAsync(q.sc, b->d_sc, sizeof(VolScalars) * sub, hipMemcpyDeviceToHost, b->stream));
+                    if (opts->do_n4)
+                        HIP_TRY(hipMemcpyAsync(q.st, b->d_st, sizeof(N4State) * sub, hipMemcpyDeviceToHost, b->stream));
+                }
+                mark_ev(c.mk, 2, b->stream);
+                c.mk.h[3] = now_ms();
+            };
+            auto finish = [&](Chunk &c) {
+                if (res) {
+                    fill_results_from(b, q.sc, q.st, q.res.data());
+                    memcpy(res + c.v0, q.res.data(), sizeof(vh_vdp_result) * c.cnt);
+                }
+                c.sp[2].d2h_finish((const char *)q.n4);
+                if (maps)
+                    par_unpack_maps(qd, defect ? defect + c.v0 * V : nullptr,
+                                    defect_border ? defect_border + c.v0 * V : nullptr,
+                                    lb ? lb + c.v0 * V : nullptr, c.CV);
+                if (trace) marks[s].push_back(c.mk);
+            };
             try {
                 HIP_TRY(hipSetDevice(p->ctx->device));
-                for (int64_t k = s; k < nchunk; k += slots) {
-                    const int64_t v0 = k * sub, cnt = std::min(sub, n - v0);
-                    const size_t CV = (size_t)cnt * V;
-                    uint8_t *qm = q.u8, *qd = q.u8 + sub * V, *qb = q.u8 + 2 * sub * V,
-                            *ql = q.u8 + 3 * sub * V;
-                    // this chunk's caller ranges: whole pages pinned in place while its copies run,
-                    // fragments (and everything under VH_PIPE_STAGE=1) through the slot's staging
-                    // the spans' pins are released only after the whole run (hipHostUnregister waits
-                    // for the device: released per chunk, it lined every slot up behind the others)
-                    keep[s].emplace_back(new PipeSpan[6]);
-                    PipeSpan *sp = keep[s].back().get();
-                    PipeSpan &s_hp = sp[0], &s_mk = sp[1], &s_n4 = sp[2], &s_d = sp[3], &s_b = sp[4], &s_l = sp[5];
-                    Mark mk_{k, {now_ms(), 0, 0, 0, 0}, {nullptr, nullptr, nullptr}};
+                Chunk cur, nxt;
+                if (s < nchunk) {
                     try {
-                        s_hp.plan(hp + v0 * V, sizeof(float) * CV, false);
-                        s_mk.plan(mask + v0 * V, CV, false);
-                        s_hp.h2d((char *)b->d_hp, (char *)q.hp, b->stream);
-                        s_mk.h2d((char *)b->d_mask, (char *)qm, b->stream);
-                        for (int64_t i = cnt; i < sub; ++i) {   // ragged tail: repeat the last study
-                            HIP_TRY(hipMemcpyAsync(b->d_hp + i * V, b->d_hp + (cnt - 1) * V, sizeof(float) * V,
-                                                   hipMemcpyDeviceToDevice, b->stream));
-                            HIP_TRY(hipMemcpyAsync(b->d_mask + i * V, b->d_mask + (cnt - 1) * V, V,
-                                                   hipMemcpyDeviceToDevice, b->stream));
+                        prep(cur, s);
+                        front(cur);
+                        back(cur);
+                        for (;;) {
+                            const int64_t kn = cur.k + slots;
+                            if (kn < nchunk) prep(nxt, kn);   // host work while the GPU has cur
+                            HIP_TRY(hipStreamSynchronize(b->stream));
+                            cur.mk.h[4] = now_ms();
+                            if (kn < nchunk) front(nxt);      // the next chunk's H2D + compute first
+                            finish(cur);                      // then this chunk's host side
+                            if (kn >= nchunk) break;
+                            back(nxt);
+                            cur = nxt;
                         }
-                        mark_ev(mk_, 0, b->stream);
-                        ticket_wait(k);
-                        mk_.h[1] = now_ms();
-                        try {
-                            if (lag > 0 && k >= lag)
-                                HIP_TRY(hipStreamWaitEvent(b->stream, p->slot[(k - lag) % slots].done, 0));
-                            batch_run(b, *opts, opts->do_n4 ? 0 : 1);
-                            HIP_TRY(hipEventRecord(q.done, b->stream));
-                        } catch (...) {
-                            ticket_pass(k);
-                            throw;
-                        }
-                        ticket_pass(k);
-                        mark_ev(mk_, 1, b->stream);
-                        mk_.h[2] = now_ms();
-                        // while the chunk computes: first touch + pin of its output ranges
-                        s_n4.plan(n4 ? n4 + v0 * V : nullptr, sizeof(float) * CV, true);
-                        s_d.plan(defect ? defect + v0 * V : nullptr, CV, true);
-                        s_b.plan(defect_border ? defect_border + v0 * V : nullptr, CV, true);
-                        s_l.plan(lb ? lb + v0 * V : nullptr, CV, true);
-                        const float *dn4 = opts->do_n4 ? b->d_n4 : b->d_hp;
-                        s_n4.d2h((const char *)dn4, (char *)q.n4, b->stream);
-                        s_d.d2h((const char *)b->d_defect, (char *)qd, b->stream);
-                        s_b.d2h((const char *)b->d_border, (char *)qb, b->stream);
-                        s_l.d2h((const char *)b->d_lb, (char *)ql, b->stream);
-                        if (res) {   // the scalars ride the same stream into pinned slot memory
-                            HIP_TRY(hipMemcpyAsync(q.sc, b->d_sc, sizeof(VolScalars) * sub, hipMemcpyDeviceToHost, b->stream));
-                            if (opts->do_n4)
-                                HIP_TRY(hipMemcpyAsync(q.st, b->d_st, sizeof(N4State) * sub, hipMemcpyDeviceToHost, b->stream));
-                        }
-                        mark_ev(mk_, 2, b->stream);
-                        mk_.h[3] = now_ms();
-                        HIP_TRY(hipStreamSynchronize(b->stream));
-                        mk_.h[4] = now_ms();
-                        if (trace) marks[s].push_back(mk_);
-                        if (res) {
-                            fill_results_from(b, q.sc, q.st, q.res.data());
-                            memcpy(res + v0, q.res.data(), sizeof(vh_vdp_result) * cnt);
-                        }
-                        s_n4.d2h_finish((const char *)q.n4);
-                        s_d.d2h_finish((const char *)qd);
-                        s_b.d2h_finish((const char *)qb);
-                        s_l.d2h_finish((const char *)ql);
                     } catch (...) {   // no copy may still touch a pinned range when it is released
                         (void)hipStreamSynchronize(b->stream);
                         throw;

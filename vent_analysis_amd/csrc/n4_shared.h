@@ -211,7 +211,6 @@ __device__ __forceinline__ bool item_begin(Item &it, const uint64_t *rowmask, co
 // wave-uniform and inside the item's slot.  With rr != nullptr also the voxel's raster rank (index
 // among the study's masked voxels in raster order: the order of ITK's convergence scan).
 __device__ __forceinline__ uint32_t item_off(const Item &it, int x, bool valid, int *rr = nullptr) {
-    const int lane = threadIdx.x & 63;
     const int xl = x - it.x0;
     const uint32_t mlo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)it.mreg, xl);
     const uint32_t mhi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(it.mreg >> 32), xl);
