@@ -203,8 +203,11 @@ def host_to_host(R, C, Z, nb, args, device, opts, seed):
     return {"volumes": n, "seconds": round(dt, 4), "runs_seconds": [round(r, 4) for r in runs],
             "statistic": "median of 3 passes", "sub_batch": sub, "slots": slots,
             "includes": "H2D of HPvent f32 + mask u8, the full pipeline, D2H of N4HPvent f32 + "
-                        "defect / border / LB u8 + per-study scalars, host staging memcpys",
-            "bytes_per_volume": int(R * C * Z * (4 + 1 + 4 + 3))}
+                        "defect / border / LB u8 + per-study scalars, host staging memcpys; over "
+                        "PCIe the mask travels as bits and the three maps as one packed byte "
+                        "(packed / unpacked on host threads inside the timed region)",
+            "bytes_per_volume": int(R * C * Z * (4 + 1 + 4 + 3)),
+            "pcie_bytes_per_volume": int(R * C * Z * (4 + 0.125 + 4 + 1))}
 
 
 def main_ci(args):
