@@ -1080,6 +1080,12 @@ int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, con
             Mark mk{};
         };
         const bool maps = defect || defect_border || lb;
+        // A/B switches (VH_PIPE_H2D_ORDER, VH_PIPE_D2H_LATE: 0 / 1) for the copy ordering below
+        auto env_flag = [](const char *name, bool dflt) {
+            const char *e = getenv(name);
+            return e ? atoi(e) != 0 : dflt;
+        };
+        const bool h2d_order = env_flag("VH_PIPE_H2D_ORDER", true), d2h_late = env_flag("VH_PIPE_D2H_LATE", false);
         auto work = [&](int s) {
             vh_pipe::Slot &q = p->slot[s];
             vh_batch *b = q.b;
@@ -1106,7 +1112,7 @@ int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, con
                 // every slot's sharing it
                 ticket_wait(c.k);
                 try {
-                if (c.k > 0) HIP_TRY(hipStreamWaitEvent(b->stream, p->slot[(c.k - 1) % slots].h2d, 0));
+                if (h2d_order && c.k > 0) HIP_TRY(hipStreamWaitEvent(b->stream, p->slot[(c.k - 1) % slots].h2d, 0));
                 c.sp[0].h2d((char *)b->d_hp, (char *)q.hp, b->stream);
                 if (c.mbits) {
                     HIP_TRY(hipMemcpyAsync(q.d_pack, c.mb, (CV + 7) / 8, hipMemcpyHostToDevice, b->stream));
@@ -1142,9 +1148,10 @@ int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, con
                     HIP_TRY(hipGetLastError());
                 }
             };
-            auto back = [&](Chunk &c) {
-                // while the chunk computes: first touch + pin of its output pages
+            auto back_pin = [&](Chunk &c) {   // while the chunk computes: first touch + pin of its output pages
                 c.sp[2].plan(n4 ? n4 + c.v0 * V : nullptr, sizeof(float) * c.CV, true);
+            };
+            auto back = [&](Chunk &c) {
                 const float *dn4 = opts->do_n4 ? b->d_n4 : b->d_hp;
                 c.sp[2].d2h((const char *)dn4, (char *)q.n4, b->stream);
                 if (maps) HIP_TRY(hipMemcpyAsync(qd, q.d_pack, c.CV, hipMemcpyDeviceToHost, b->stream));
@@ -1175,16 +1182,19 @@ int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, con
                     try {
                         prep(cur, s);
                         front(cur);
-                        back(cur);
                         for (;;) {
                             const int64_t kn = cur.k + slots;
                             if (kn < nchunk) prep(nxt, kn);   // host work while the GPU has cur
+                            back_pin(cur);
+                            // VH_PIPE_D2H_LATE=1 enqueues the D2Hs only once the compute has
+                            // finished (A/B: neutral to -2 % on the boxes measured, r3q3; off)
+                            if (d2h_late) HIP_TRY(hipEventSynchronize(q.done));
+                            back(cur);
                             HIP_TRY(hipStreamSynchronize(b->stream));
                             cur.mk.h[4] = now_ms();
                             if (kn < nchunk) front(nxt);      // the next chunk's H2D + compute first
                             finish(cur);                      // then this chunk's host side
                             if (kn >= nchunk) break;
-                            back(nxt);
                             cur = nxt;
                         }
                     } catch (...) {   // no copy may still touch a pinned range when it is released
