@@ -1,0 +1,10 @@
+# expf_tab (LDS table) in PC pass 0: parity, pass-0 profile, bench
+cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out; export TMPDIR=/tmp
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/ -k "n4 or pc or vdp or bench or config or ragged" > gpurun_out/r3v3_tests.log 2>&1 || { tail -5 gpurun_out/r3v3_tests.log; exit 1; }
+tail -1 gpurun_out/r3v3_tests.log
+VH_LIB_PATH=$PWD/scratch_libs/pcp.so timeout -k 10 200 python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-h2h > gpurun_out/r3v3_pcprof.log 2>&1 || exit 2
+grep PCW_P0 gpurun_out/r3v3_pcprof.log | head -4
+for i in 1 2; do
+timeout -k 10 300 python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-h2h > gpurun_out/r3v3_bench$i.json 2> gpurun_out/r3v3_bench$i.err || exit 3
+python3 -c "import json;d=json.loads(open('gpurun_out/r3v3_bench$i.json').read());print(d['value'], d['roofline']['kernel_ms_per_step']['n4_study'])"
+done

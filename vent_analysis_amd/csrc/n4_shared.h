@@ -1615,11 +1615,19 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
         }
     };
     fetch(0);
+#ifdef PC_PROF
+    unsigned long long p0t[4] = {0, 0, 0, 0}, p0c = clock64();
+#define P0M(k) do { const unsigned long long _c = clock64(); p0t[k] += _c - p0c; p0c = _c; } while (0)
+#else
+#define P0M(k) do { } while (0)
+#endif
     for (uint32_t g0 = 0; g0 < lmax; g0 += G0) {
 #pragma unroll
         for (int q = 0; q < G0; ++q)
             T0[(tid % G0) * TS + tid / G0 + (PC_TPB / G0) * q] = v[q];
+        P0M(0);   // (profiling) the group's loads arrived and went to LDS
         __syncthreads();
+        P0M(1);   // first barrier
         if (g0 + G0 < lmax) fetch(g0 + G0);
 #pragma unroll
         for (int i = 0; i < G0; ++i)
@@ -1630,8 +1638,15 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
                 s1 += e;
                 s2 = fma(e, e, s2);
             }
+        P0M(2);   // exp, stores and sums
         __syncthreads();
+        P0M(3);   // second barrier
     }
+#undef P0M
+#ifdef PC_PROF
+    if (blockIdx.x == 0 && tid == 0)
+        printf("PCW_P0 loads %llu bar1 %llu work %llu bar2 %llu\n", p0t[0], p0t[1], p0t[2], p0t[3]);
+#endif
     if (tid == 0) {   // flags from an earlier call (or other phases' use of this LDS) must not match
         S.done = 0;
         S.fallback = 0;
