@@ -1582,7 +1582,8 @@ static_assert(PC_APASS >= 1 && PC_APASS <= 2, "PC_APASS: 1 or 2 phase-A stages (
 #ifndef PC_XSIG
 #define PC_XSIG 1   // exact sig after stage 0 (PCX above); 0: stage 1 and the exact rounds always
 #endif
-template <class LoadD>
+// PEXP: ld returns p = expf_cr(d) already (the study kernel's eval stored it, ST_EVAL_EXP)
+template <bool PEXP = false, class LoadD>
 __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n, PcShared<PC_TPB> &S,
                                                   ChainState &ch, int req, double *tbuf, int tcap,
                                                   float skip_thresh = 0.0f) {
@@ -1632,7 +1633,7 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
 #pragma unroll
         for (int i = 0; i < G0; ++i)
             if (g0 + i < len) {
-                const float p = expf_cr(T0[i * TS + j]);
+                const float p = PEXP ? T0[i * TS + j] : expf_cr(T0[i * TS + j]);
                 P[(size_t)(g0 + i) * PC_TPB + j] = p;
                 const double e = (double)p - 1.0;
                 s1 += e;

@@ -47,6 +47,9 @@ static_assert(ST_CW == 4, "a chain group is 4 waves, one per SIMD (mu, sig, 2 pr
 // (heterogeneous studies): 2 33.1 ms, 0 depth 1 53.7 ms, 0 depth 2 48.8 ms.  (Before the bin
 // minimum stopped falling back to the raster scan, r3_bin_min, the compute waves spent that scan's
 // time beside the serial chain and 0 came out ahead: 45.8 vs 49-50 ms.)
+#ifndef ST_EVAL_EXP
+#define ST_EVAL_EXP 0   // 1: eval stores p = expf_cr(d) for PC (its pass 0 then skips the exp)
+#endif
 #ifndef ST_PC
 #define ST_PC 2
 #endif
@@ -349,7 +352,7 @@ __device__ void eval_item(const Item &it, int item, int Z, const TabV &Tn, const
 #endif
         if (CM == 0) {
 #ifndef AB_EVAL_NOSTORE
-            st_store(rD, roff, bo - bn);
+            st_store(rD, roff, (ST_EVAL_EXP && !ST_SPLIT) ? expf_cr(bo - bn) : bo - bn);
 #else
             if (bo - bn == 12345.0f) st_store(rD, roff, u);
 #endif
@@ -1141,7 +1144,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                     // the raster d buffer is free once pass 0 has read it: PCX's stored increments
                     // below the iteration cap this iteration's measure only decides whether the
                     // level goes on: PC may certify "above the threshold" without the exact sig
-                    pcw_run([=](int64_t r) { return Dr[r]; }, a.D + a.half + b * a.VS, n, PW, M.ch[0], itk,
+                    pcw_run<ST_EVAL_EXP && !ST_SPLIT>([=](int64_t r) { return Dr[r]; }, a.D + a.half + b * a.VS, n, PW, M.ch[0], itk,
                             reinterpret_cast<double *>(a.D + b * a.VS), (int)(a.VS / 2),
                             itk < a.lvs->max_iters[L] ? a.thresh : 0.0f);
                     if (t == 0) M.conv = (double)M.ch[0].conv;
