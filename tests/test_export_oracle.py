@@ -2,6 +2,7 @@
 against properties that follow from the cited reference lines by hand."""
 import os
 
+import pytest
 import numpy as np
 
 from oracle import export_oracle as E
@@ -68,3 +69,33 @@ def test_screenshot_layout_and_panels():
         raise AssertionError("expected IndexError")
     except IndexError:
         pass
+
+
+def test_screenshot_annotations_drawn_like_the_reference():
+    """screenShot's text (Vent_Analysis.py:500-518) on the saved PNG: every line is drawn in white
+    on the montage, the CI line only once the CI is numeric (the reference's try/except), and the
+    slice numbers under the N4 row.  Fonts: arial.ttf when installed, else PIL's default at the
+    same size, so only where text lands is checked here (pixel parity unpinned)."""
+    pytest.importorskip("PIL")
+    from types import SimpleNamespace
+    from PIL import Image
+    from vent_analysis_amd.Vent_Analysis import Vent_Analysis
+    md = {'PatientName': 'P1', 'PatientAge': '40', 'PatientSex': 'F', 'Disease': 'CF',
+          'StudyDate': '20240101', 'visit': '1', 'treatment': 'none', 'LungVolume': 3.2,
+          'DefectVolume': 0.4, 'DE': '', 'FEV1': '', 'VDP': 12.34, 'CI': '', 'analysisUser': 'u'}
+    obj = SimpleNamespace(metadata=md, version='241007_vent')
+    h0, w0, ss = 40, 48, range(2, 10)
+    width = w0 * len(ss)
+    base = np.zeros((7 * h0, width, 3), np.uint8)
+    img = Image.fromarray(base.copy())
+    Vent_Analysis._annotate_screenshot(obj, img, h0, w0, ss, width)
+    a = np.asarray(img)
+    assert a.shape == base.shape and (a > 0).any()
+    assert (a[:, :, 0] == a[:, :, 1]).all() and (a[:, :, 1] == a[:, :, 2]).all()   # white text only
+    assert a[int(h0 * 1.8):int(h0 * 1.8) + 30].any()                              # slice numbers
+    md2 = dict(md, CI=22.5)
+    img2 = Image.fromarray(base.copy())
+    Vent_Analysis._annotate_screenshot(SimpleNamespace(metadata=md2, version='v'), img2, h0, w0, ss, width)
+    b = np.asarray(img2)
+    x0 = int(round(width * .50))
+    assert b[int(h0 * 1.0):int(h0 * 1.0) + 35, x0:].sum() > a[int(h0 * 1.0):int(h0 * 1.0) + 35, x0:].sum()

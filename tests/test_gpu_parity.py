@@ -784,3 +784,8 @@ def test_export_class_methods(tmp_path):
     exp = E.screenshot_image(v.proton, v.HPvent, v.N4HPvent, v.mask, v.mask_border, v.defectArray,
                              None, pal)
     assert np.array_equal(img, exp) and (tmp_path / "shot.png").exists()
+    from PIL import Image   # the PNG: the montage plus the reference's white text
+    png = np.asarray(Image.open(tmp_path / "shot.png").convert("RGB"))
+    assert png.shape == img.shape and (png != img).any()
+    diff = (png != img).any(axis=2)
+    assert (png[diff] >= img[diff]).all()

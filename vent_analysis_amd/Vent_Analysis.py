@@ -338,9 +338,12 @@ class Vent_Analysis:
         """Vent_Analysis.py:458-520: the 7-row montage (blank, blank, proton, HPvent, N4 + mask
         border, N4 + defects, N4 + parula CI) over cropToData(mask, border=5), rendered on the
         GPU (vh_montage) as the uint8(IMAGE * 255) array, returned and -- when PIL is present --
-        saved as PNG.  parula: the 64 x 3 colour table the reference loads from
-        'C:\\PIRL\\data\\parula.np.npy' (same default path).  The text annotations need the
-        reference's arial.ttf and are not drawn."""
+        saved as PNG with the reference's text annotations (:500-518: slice numbers, patient,
+        disease, dates, volumes, DE / FEV1 / VDP / CI, version, user and date; same positions,
+        strings and sizes).  The reference draws them in arial.ttf; where that font is missing
+        PIL's default font at the same size stands in (text pixels then differ: parity unpinned).
+        parula: the 64 x 3 colour table the reference loads from 'C:\\PIRL\\data\\parula.np.npy'
+        (same default path).  The returned array is the montage without the text."""
         if parula is None:
             parula = np.load('C:\\PIRL\\data\\parula.np.npy', allow_pickle=False)
         _, rr, cc, ss = self.cropToData(self.mask, border=5)
@@ -355,9 +358,49 @@ class Vent_Analysis:
         except ImportError:
             return img
         if path:
-            Image.fromarray(img).save(path, 'PNG')
+            image = Image.fromarray(img)
+            self._annotate_screenshot(image, len(rr), len(cc), ss, img.shape[1])
+            image.save(path, 'PNG')
             print(f'\033[32mScreenshot saved to {path}\033[37m')
         return img
+
+    def _annotate_screenshot(self, image, h0, w0, ss, width):
+        """The text of Vent_Analysis.py:500-518 on the montage; h0, w0 = the cropped volume's rows
+        and columns (the reference's N4.shape[0], N4.shape[1]), width = the montage's width."""
+        import datetime
+        from PIL import ImageDraw, ImageFont
+
+        def font(size):
+            try:
+                return ImageFont.truetype('arial.ttf', size=size)
+            except OSError:   # the reference's font is not installed: PIL's default, same size
+                return ImageFont.load_default(size=size)
+
+        md, white = self.metadata, (255, 255, 255)
+        draw = ImageDraw.Draw(image)
+        for k in ss:
+            draw.text((k * w0 - w0 / 2, h0 * 1.8), f"{k + 1}", fill=white, font=font(30))
+        draw.text((10, h0 * 0.10), f"Patient: {md['PatientName']} ({md['PatientAge']}/{md['PatientSex']})",
+                  fill=white, font=font(40))
+        draw.text((10, h0 * 0.40), f"Disease: {md['Disease']}", fill=white, font=font(35))
+        draw.text((10, h0 * 0.70), f"StudyDate: {md['StudyDate']}", fill=white, font=font(35))
+        draw.text((10, h0 * 1.00), f"Visit#: {md['visit']}", fill=white, font=font(35))
+        draw.text((10, h0 * 1.30), f"Treatment: {md['treatment']}", fill=white, font=font(35))
+        draw.text((np.round(width * .25), h0 * 0.10), f"Lung Volume: {np.round(md['LungVolume'] * 1000)} mL",
+                  fill=white, font=font(35))
+        draw.text((np.round(width * .25), h0 * 0.40), f"Defect Volume: {np.round(md['DefectVolume'] * 1000)} mL",
+                  fill=white, font=font(35))
+        draw.text((np.round(width * .50), h0 * 0.10), f"DE: {md['DE']} mL", fill=white, font=font(35))
+        draw.text((np.round(width * .50), h0 * 0.40), f"FEV1: {md['FEV1']} %", fill=white, font=font(35))
+        draw.text((np.round(width * .50), h0 * 0.70), f"VDP: {np.round(md['VDP'], 1)} %", fill=white, font=font(35))
+        try:   # as the reference: no CI line when the CI is not numeric yet
+            draw.text((np.round(width * .50), h0 * 1.00), f"CI: {np.round(md['CI'])} %", fill=white, font=font(35))
+        except Exception:
+            pass
+        draw.text((np.round(width * .75), h0 * 0.25), f'Analysis Version: {self.version}', fill=white, font=font(35))
+        draw.text((np.round(width * .75), h0 * 0.50),
+                  f"Analyzed by: {md['analysisUser']} on {str(datetime.datetime.today()).split()[0]}",
+                  fill=white, font=font(35))
 
     def process_RAW(self, filepath=None, raw_K=None):
         """TWIX reconstruction (Vent_Analysis.py:522-540): raw_HPvent = transpose(fftshift(fft2(
