@@ -1085,7 +1085,11 @@ int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, con
             const char *e = getenv(name);
             return e ? atoi(e) != 0 : dflt;
         };
-        const bool h2d_order = env_flag("VH_PIPE_H2D_ORDER", true), d2h_late = env_flag("VH_PIPE_D2H_LATE", false);
+        // H2D order: 0 none, 1 device-side (the H2D waits on the previous chunk's H2D event),
+        // 2 host-side (the enqueuing thread waits for that event first)
+        const char *ho = getenv("VH_PIPE_H2D_ORDER");
+        const int h2d_order = ho ? atoi(ho) : 1;
+        const bool d2h_late = env_flag("VH_PIPE_D2H_LATE", false);
         auto work = [&](int s) {
             vh_pipe::Slot &q = p->slot[s];
             vh_batch *b = q.b;
@@ -1112,7 +1116,9 @@ int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, con
                 // every slot's sharing it
                 ticket_wait(c.k);
                 try {
-                if (h2d_order && c.k > 0) HIP_TRY(hipStreamWaitEvent(b->stream, p->slot[(c.k - 1) % slots].h2d, 0));
+                if (h2d_order == 1 && c.k > 0)
+                    HIP_TRY(hipStreamWaitEvent(b->stream, p->slot[(c.k - 1) % slots].h2d, 0));
+                if (h2d_order == 2 && c.k > 0) HIP_TRY(hipEventSynchronize(p->slot[(c.k - 1) % slots].h2d));
                 c.sp[0].h2d((char *)b->d_hp, (char *)q.hp, b->stream);
                 if (c.mbits) {
                     HIP_TRY(hipMemcpyAsync(q.d_pack, c.mb, (CV + 7) / 8, hipMemcpyHostToDevice, b->stream));
