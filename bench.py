@@ -37,36 +37,69 @@ def _cpu_one(args):
     R, C, Z, seed = args
     from oracle import native, vdp_oracle as O
     from vent_analysis_amd.synth import synth_volume
-    X, M = synth_volume(R, C, Z, seed)
+    X, M = synth_volume(R, C, Z, seed, True)   # the GPU line's heterogeneous studies (vary=True)
     t = time.perf_counter()
     n4, _, _ = native.n4(X, M)
     O.calculate_vdp(n4, M, (1.5, 1.5, 10.0), HP=X)
     return time.perf_counter() - t
 
 
-def cpu_baseline(R, C, Z, seconds=15.0, procs=16):
+def host_cpu_share():
+    """(CPUs this process may use, why).  os.cpu_count() is the whole machine; the affinity mask,
+    a cgroup CPU quota and the pool's per-GPU share (OMP_NUM_THREADS, 16 on the GPU boxes, which
+    also cap worker pools at that many processes) can each be smaller."""
+    n, why = os.cpu_count() or 1, "os.cpu_count()"
+    try:
+        a = len(os.sched_getaffinity(0))
+        if a < n:
+            n, why = a, "sched_getaffinity"
+    except (AttributeError, OSError):
+        pass
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max" and int(q) // int(per) < n:
+            n, why = max(1, int(q) // int(per)), "cgroup cpu.max"
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and 0 < int(omp) < n:
+        n, why = int(omp), "OMP_NUM_THREADS (the box's CPU share per GPU)"
+    return n, why
+
+
+def cpu_baseline(R, C, Z, seconds=15.0, procs=None, base_seed=0, unique=64):
+    """The CPU restatement (C N4 + numpy chain) over the same heterogeneous studies the GPU line
+    times (seeds base_seed + i % unique, vary=True), one process per usable host core
+    (host_cpu_share), before any GPU initialisation.  Reports per-core throughput and its
+    extrapolation to every CPU of the host next to the measured value."""
     import multiprocessing as mp
     from oracle import native
     native.build()
-    procs = max(1, min(procs, os.cpu_count() or 1))
+    share, why = host_cpu_share()
+    procs = max(1, min(procs or share, share))
     ctx = mp.get_context("spawn")
     done = 0
     busy = 0.0
     with ctx.Pool(procs) as pool:
-        pool.map(_cpu_one, [(R, C, Z, 1000 + i) for i in range(procs)])   # warm imports
+        pool.map(_cpu_one, [(R, C, Z, base_seed + i % unique) for i in range(procs)])   # warm imports
         t0 = time.perf_counter()
-        seed = 0
+        i = 0
         while time.perf_counter() - t0 < seconds:
-            ts = pool.map(_cpu_one, [(R, C, Z, seed + i) for i in range(procs)])
-            seed += procs
+            ts = pool.map(_cpu_one, [(R, C, Z, base_seed + (i + j) % unique) for j in range(procs)])
+            i += procs
             done += len(ts)
             busy += sum(ts)
         wall = time.perf_counter() - t0
-    return {"value": done / wall, "unit": "volumes/s", "cores": procs, "host_cpus": os.cpu_count(),
+    host = os.cpu_count() or procs
+    per_core = done / wall / procs
+    return {"value": done / wall, "unit": "volumes/s", "cores": procs, "host_cpus": host,
+            "cores_reason": why, "per_core_vol_s": round(per_core, 3),
+            "full_host_extrapolated_vol_s": round(per_core * host, 1),
             "kind": "port",
-            "sample": f"{done} synthetic {R}x{C}x{Z} volumes (oracle/n4_oracle.c N4, conv_mode 0 = "
-                      f"ITK float Welford, + oracle/vdp_oracle.py chain), {procs} processes of "
-                      f"{os.cpu_count()} host CPUs, {wall:.1f} s wall, "
+            "sample": f"{done} synthetic {R}x{C}x{Z} volumes, the GPU line's heterogeneous studies "
+                      f"(synth_volume vary=True, seeds {base_seed}+i%{unique}; oracle/n4_oracle.c N4, "
+                      f"conv_mode 0 = ITK float Welford, + oracle/vdp_oracle.py chain), {procs} "
+                      f"processes ({why}) of {host} host CPUs, {wall:.1f} s wall, "
                       f"{busy / max(done, 1):.3f} s per volume per core"}
 
 
@@ -279,6 +312,92 @@ def main_ci(args):
     print(json.dumps(line))
 
 
+def free_port():
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(args, argv):
+    """``--gpus N`` (N > 1) without a launcher's WORLD_SIZE: start N rank processes of this script
+    (one per GPU, RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set as torchrun sets
+    them) before this process touches any GPU, pass rank 0's stdout (the one JSON line) through,
+    and exit non-zero if any rank fails (the others are then stopped).  This process never
+    initialises the GPU, so nothing is exec'd from a GPU process."""
+    import subprocess
+    n = args.gpus
+    port = os.environ.get("MASTER_PORT") or str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=None if r == 0 else sys.stderr))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 1
+                print(f"bench.py: rank {procs.index(p)} exited with {c}; stopping the other ranks",
+                      file=sys.stderr)
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def main_dry(args, rank, world, dist):
+    """--dry-run (CPU, gloo): the multi-rank skeleton of the GPU line without libventhip -- shard
+    seeds, the unique-id broadcast, the barrier-bracketed max-over-ranks timing and the cohort
+    histogram sum -- with a numpy stand-in for the step (tests/test_dist_gloo.py)."""
+    import torch
+    from vent_analysis_amd.synth import synth_batch
+    R, C, Z = args.shape
+    hp, mk = synth_batch(R, C, Z, args.batch, base_seed=shard_seed(rank), unique=BENCH_UNIQUE, vary=True)
+    uid = broadcast_uid(bytes(range(128)) if rank == 0 else None, dist)
+    if os.environ.get("VH_DRY_FAIL_RANK") == str(rank):   # tests: a failing rank fails the job
+        raise SystemExit(3)
+
+    def step():   # per-rank cohort rows (numpy stand-in for k_cohort_*), summed over the ranks
+        h = np.zeros(1024, np.int64)
+        for x, m in zip(hp, mk):
+            s = np.sort(x[m > 0])
+            nv = (x / np.float32(s[int(len(s) * 0.99)])).astype(np.float32)[m > 0]
+            nv = nv[(nv >= 0) & (nv < np.float32(1.5))]
+            h += np.bincount(np.minimum((nv * np.float32(1024 / 1.5)).astype(np.int64), 1023),
+                             minlength=1024)
+        t = torch.from_numpy(h)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return t.numpy()
+
+    for _ in range(args.warmup):
+        step()
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        hist = step()
+    dist.barrier()
+    dt = max_over_ranks(time.perf_counter() - t0, dist)
+    line = {"metric": METRIC, "value": round(world * args.batch * args.steps / dt, 2),
+            "unit": "volumes/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": "dry run (CPU, no GPU work)", "volumes_per_gpu": args.batch,
+                       "shape": [R, C, Z], "parallelism": f"dp{world}"},
+            "dry_run": {"uid_ok": uid == bytes(range(128)), "cohort_hist": hist.tolist(),
+                        "rank_seeds": [shard_seed(r) for r in range(world)]}}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -309,8 +428,14 @@ def main():
                     help="host-to-host: studies per pipeline sub-batch")
     ap.add_argument("--h2h-slots", type=int, default=4,
                     help="host-to-host: pipeline slots (sub-batches in flight, <= 8)")
+    ap.add_argument("--h2h-keep-batch", action="store_true",
+                    help="A/B: keep the device-resident batch (and its stream) open during the "
+                         "host-to-host measurement (round-3 behaviour)")
     ap.add_argument("--workload", default="vdp", choices=["vdp", "ci"],
                     help="vdp: the BASELINE metric (default); ci: the cluster-index line")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="multi-rank skeleton on the CPU (gloo, no GPU): launcher, uid broadcast, "
+                         "timing and cohort sum (tests)")
     ap.add_argument("--conv-threshold", type=float, default=0.001,
                     help="N4 convergence threshold (SimpleITK default 0.001; 0 = fixed 4x50 "
                          "iterations, for kernel A/B runs at constant work)")
@@ -318,20 +443,28 @@ def main():
     if args.workload == "ci":
         return main_ci(args)
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:   # python bench.py --gpus N: N ranks
+        sys.exit(launch_ranks(args, sys.argv[1:]))
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE {world} but --gpus {args.gpus} (one rank per GPU)")
     R, C, Z = args.shape
     nb = args.batch
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(R, C, Z, seconds=args.cpu_seconds)   # before any GPU initialisation
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.dry_run:
+        cpu = cpu_baseline(R, C, Z, seconds=args.cpu_seconds, base_seed=shard_seed(0),
+                           unique=BENCH_UNIQUE)   # before any GPU initialisation
 
     dist = None
-    if world > 1:
+    if world > 1 or args.dry_run:
         import torch.distributed as dist
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        with stdout_to_stderr():   # gloo prints its connection banner on fd 1
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+    if args.dry_run:
+        return main_dry(args, rank, world, dist)
 
     from vent_analysis_amd import _lib
     from vent_analysis_amd.synth import synth_batch
@@ -363,7 +496,11 @@ def main():
 
     try:
         import torch
-        sync_dev = torch.cuda.synchronize if torch.cuda.is_available() else (lambda: None)
+        if torch.cuda.is_available():   # this rank's GPU (torch's current device is 0 otherwise)
+            torch.cuda.set_device(local)
+            sync_dev = torch.cuda.synchronize
+        else:
+            sync_dev = lambda: None  # noqa: E731
     except Exception:   # torch is plumbing only; the library syncs its own stream
         sync_dev = lambda: None  # noqa: E731
 
@@ -418,6 +555,10 @@ def main():
                 "kernel_us_per_launch": {n: round(v["ms_total"] / v["launches"] * 1e3, 2)
                                          for n, v in kernels.items()}}
     its = np.array([list(r.n4_iters[:4]) for r in res])
+    if not args.h2h_keep_batch:
+        # the device-resident batch (its stream, 1.5 GB of HBM) is done: the pipe's slot streams
+        # then have the GPU_MAX_HW_QUEUES (4) hardware queues to themselves
+        Bt.close()
     h2h = None
     if not args.no_h2h:
         if dist:   # every rank streams at once (host memory and PCIe shared as in a cohort run)
@@ -456,7 +597,8 @@ def main():
     }
     if rank == 0:
         print(json.dumps(line), flush=True)
-    Bt.close()
+    if args.h2h_keep_batch:
+        Bt.close()
     if use_comm:
         with stdout_to_stderr():
             _lib.comm_destroy(device=local)

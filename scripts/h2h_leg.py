@@ -1,0 +1,40 @@
+"""The host-to-host leg of bench.py alone (for rocprofv3 --kernel-trace --memory-copy-trace and
+VH_PIPE_TRACE runs): n = batches x 256 heterogeneous studies streamed through vh_pipe.
+
+  python3 scripts/h2h_leg.py [--slots 4] [--sub 128] [--batches 6] [--keep-batch]
+
+--keep-batch also holds a 256-study device batch (and its stream) open, as bench.py did in
+round 3 while it measured this leg."""
+import argparse
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, HERE)
+
+import bench  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--slots", type=int, default=4)
+    ap.add_argument("--sub", type=int, default=128)
+    ap.add_argument("--batches", type=int, default=6)
+    ap.add_argument("--keep-batch", action="store_true")
+    a = ap.parse_args()
+    from vent_analysis_amd import _lib
+    R, C, Z, nb = 128, 128, 24, 256
+    Bt = _lib.Batch(R, C, Z, nb) if a.keep_batch else None
+    opts = _lib.Batch.options(do_n4=True, vox=(1.5, 1.5, 10.0), do_cohort=True, profile=False)
+    args = argparse.Namespace(h2h_slots=a.slots, h2h_sub=a.sub, h2h_batches=a.batches)
+    h = bench.host_to_host(R, C, Z, nb, args, 0, opts, 500)
+    h["vol_s"] = round(h["volumes"] / h["seconds"], 1)
+    h["keep_batch"] = a.keep_batch
+    print(json.dumps(h), flush=True)
+    if Bt:
+        Bt.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -71,3 +71,58 @@ def test_two_rank_shards_uid_timing_and_cohort():
     Xb, Mb = synth_batch(*SHAPE, PER_RANK, base_seed=bench.shard_seed(1))
     whole = cohort_hist(np.concatenate([Xa, Xb]), np.concatenate([Ma, Mb]))
     assert np.array_equal(h0, whole)
+
+
+def _bench(cmd, env=None, timeout=300):
+    import subprocess
+    import sys
+    e = dict(os.environ, **(env or {}))
+    return subprocess.run([sys.executable] + cmd, cwd=bench.HERE, env=e, capture_output=True,
+                          text=True, timeout=timeout)
+
+
+DRY = ["--dry-run", "--steps", "2", "--warmup", "1", "--batch", str(PER_RANK), "--shape",
+       *map(str, SHAPE), "--no-h2h"]
+
+
+def _check_dry_line(out, world):
+    import json
+    lines = [ln for ln in out.splitlines() if ln.strip()]
+    assert len(lines) == 1, out          # rank 0's one JSON line, nothing else on stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == world and line["config"]["parallelism"] == f"dp{world}"
+    assert line["dry_run"]["uid_ok"]
+    X, M = [], []
+    for r in range(world):
+        x, m = synth_batch(*SHAPE, PER_RANK, base_seed=bench.shard_seed(r), vary=True)
+        X.append(x)
+        M.append(m)
+    whole = cohort_hist(np.concatenate(X), np.concatenate(M))
+    assert np.array_equal(np.array(line["dry_run"]["cohort_hist"]), whole)
+    return line
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_gpus_n_launches_n_ranks(world):
+    """python bench.py --gpus N (no WORLD_SIZE, the driver's N = 1 command form) starts N ranks
+    itself: rank 0's single JSON line carries n_gpus = N, dpN, and the cohort sum of all shards."""
+    r = _bench(["bench.py", "--gpus", str(world)] + DRY)
+    assert r.returncode == 0, r.stderr[-2000:]
+    _check_dry_line(r.stdout, world)
+
+
+def test_bench_under_torchrun():
+    """The torchrun form (WORLD_SIZE from the launcher) gives the same line."""
+    r = _bench(["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
+                "--gpus", "2"] + DRY)
+    assert r.returncode == 0, r.stderr[-2000:]
+    _check_dry_line(r.stdout, 2)
+
+
+def test_bench_rank_failure_and_world_mismatch():
+    r = _bench(["bench.py", "--gpus", "2"] + DRY, env={"VH_DRY_FAIL_RANK": "1"})
+    assert r.returncode != 0
+    assert not r.stdout.strip()
+    r = _bench(["bench.py", "--gpus", "2"] + DRY, env={"WORLD_SIZE": "1", "RANK": "0"})
+    assert r.returncode != 0 and "WORLD_SIZE 1 but --gpus 2" in r.stderr
