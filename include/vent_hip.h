@@ -15,6 +15,8 @@
  *   vh_border    Vent_Analysis.calculateBorder               Vent_Analysis.py:225-231
  *   vh_vdp       Vent_Analysis.calculate_VDP (post-N4 part)  Vent_Analysis.py:239-263
  *   vh_ci        CI.calculate_CI + Vent_Analysis.calculate_CI CI.py:107-145, Vent_Analysis.py:265-271
+ *   vh_ci_table_* / vh_ci_tab  the same with the sphere table resident in HBM (CI.getSpherePix's
+ *                cached table, CI.py:33-63, uploaded once)
  *   vh_overlay   Vent_Analysis.exportDICOM (pixel data)       Vent_Analysis.py:381-428
  *   vh_montage   Vent_Analysis.screenShot (montage array)     Vent_Analysis.py:458-520
  *   vh_recon     Vent_Analysis.process_RAW (k-space -> image) Vent_Analysis.py:537-540
@@ -31,7 +33,7 @@
 extern "C" {
 #endif
 
-#define VH_ABI_VERSION 4
+#define VH_ABI_VERSION 5
 
 /* status codes */
 #define VH_OK 0
@@ -46,6 +48,7 @@ extern "C" {
 
 typedef struct vh_ctx vh_ctx;
 typedef struct vh_batch vh_batch;
+typedef struct vh_ci_table vh_ci_table;
 
 /* N4 parameters; vh_n4_default_params() fills the SimpleITK 2.3.1 defaults the reference runs with
  * (Vent_Analysis.py:330: no setter is called).  ncp is given per numpy axis (rows, cols, slices). */
@@ -141,6 +144,15 @@ int vh_ci(vh_ctx *ctx, const uint8_t *defect, int64_t R, int64_t C, int64_t Z, i
           const int16_t *offs, const uint8_t *dup, int64_t rows, const int32_t *bounds,
           const double *radii, int64_t nb, double minvox, double *ci_array, double *ci_scalar,
           int32_t *shell);
+/* The sphere table uploaded once for volumes of R rows and C columns (the px2vec stride of
+ * CI.py:65-68): the same arrays as vh_ci; it stays in HBM until vh_ci_table_destroy.  vh_ci_tab is
+ * vh_ci with such a table (ci_array and shell nullable): no per-call table work or upload. */
+int vh_ci_table_create(vh_ctx *ctx, int64_t R, int64_t C, const int16_t *offs, const uint8_t *dup,
+                       int64_t rows, const int32_t *bounds, const double *radii, int64_t nb,
+                       vh_ci_table **out);
+int vh_ci_table_destroy(vh_ci_table *t);
+int vh_ci_tab(vh_ctx *ctx, const uint8_t *defect, int64_t R, int64_t C, int64_t Z, int64_t batch,
+              const vh_ci_table *t, double minvox, double *ci_array, double *ci_scalar, int32_t *shell);
 
 /* ---- device-resident batch pipeline ---------------------------------------------------------- */
 int vh_batch_create(vh_ctx *ctx, int64_t R, int64_t C, int64_t Z, int64_t batch, vh_batch **out);
@@ -208,6 +220,10 @@ int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, con
                 float *n4, uint8_t *defect, uint8_t *defect_border, uint8_t *lb,
                 vh_vdp_result *res);
 int vh_pipe_destroy(vh_pipe *p);
+/* The last vh_pipe_run's peak of caller memory pinned in place (bytes) and the caller ranges that
+ * went through the pinned staging instead (not registrable, or past the VH_PIPE_PIN_CAP budget,
+ * default 32 GiB: a long cohort run never page-locks more than that at once). */
+int vh_pipe_stats(vh_pipe *p, int64_t *pinned_peak_bytes, int64_t *staged_spans);
 
 /* ---- multi-GPU (RCCL over xGMI) -------------------------------------------------------------- */
 #define VH_COMM_ID_BYTES 128

@@ -270,6 +270,37 @@ def calculate_vdp(N4: np.ndarray, mask: np.ndarray, vox, thresh: float = 0.6, HP
     return out
 
 
+def calculate_vdp_literal(N4: np.ndarray, mask: np.ndarray, vox, thresh: float = 0.6):
+    """Vent_Analysis.calculate_VDP after N4 (Vent_Analysis.py:245-257) line by line, for ANY
+    numeric mask (e.g. 0/255 mask DICOMs): the signal is ``mask > 0`` (:245), the per-slice
+    threshold map is multiplied by the mask itself and filtered by scipy's own ``medfilt2d``
+    (the reference's third-party call, :248-249), the LB classes are multiplied by the mask
+    (:256) and every scalar is the reference's expression on those arrays.  Slow (scipy per
+    slice); for small cases.  Equal to calculate_vdp for 0/1 masks
+    (tests/test_oracle_golden.py)."""
+    from scipy.signal import medfilt2d
+    N4 = np.asarray(N4, dtype=F32)
+    mask = np.asarray(mask)
+    sig = np.sort(N4[mask > 0], kind="stable")                          # :245 sorted(...)
+    m = mean_f32(sig)                                                   # :246 np.mean
+    mn = np.divide(N4, m)
+    defect = np.zeros(mn.shape)
+    for k in range(mask.shape[2]):                                      # :247-249
+        defect[:, :, k] = medfilt2d((mn[:, :, k] < F32(thresh)) * mask[:, :, k])
+    border = calculate_border(defect) == 1                              # :250
+    msum = np.sum(mask)
+    out = dict(defectArray=defect, defectBorder=border, mean_anchor=m)
+    out["VDP"] = 100 * np.sum(defect) / msum                            # :251
+    out["DefectVolume"] = volume_litres(np.sum(defect == 1), vox)       # :252
+    p99 = sig[int(len(sig) * .99)]                                      # :255
+    nv = np.divide(N4, p99)
+    lb = lb_classes(nv).astype(np.int64) * mask                         # :256 (int * mask)
+    out["defectArrayLB"] = lb
+    out["p99"] = p99
+    out["VDP_lb"] = 100 * np.sum((lb == 1) * 1 + (lb == 2) * 1) / msum  # :257
+    return out
+
+
 def ci_scalar(ci_values: np.ndarray) -> float:
     """Vent_Analysis.calculate_CI tail (Vent_Analysis.py:268-270): 95th-pct order statistic."""
     s = np.sort(ci_values)

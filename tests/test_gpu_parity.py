@@ -18,6 +18,12 @@ pytestmark = pytest.mark.gpu
 GOLD = golden_files()
 
 
+def parula():
+    """tests/golden/parula.npy: the reference's colour table (/root/reference/parula.npy, a data
+    file it ships; screenShot loads it at Vent_Analysis.py:466), loaded without pickle."""
+    return np.load(os.path.join(os.path.dirname(__file__), "golden", "parula.npy"), allow_pickle=False)
+
+
 def rel(a, b):
     a = np.asarray(a, np.float64)
     b = np.asarray(b, np.float64)
@@ -104,6 +110,50 @@ def test_ci_errors():
         _lib.ci(np.ones((40, 40, 24), np.uint8), table, 1.5)
     with pytest.raises(ValueError):
         native.ci(np.ones((40, 40, 24), np.uint8), table, (1.5, 1.5, 10.0))
+
+
+def test_ci_table_api_equals_per_call_table():
+    """vh_ci_tab with the HBM-resident table (vh_ci_table_create, reused across calls and batch
+    sizes) equals vh_ci, which uploads the table per call; a table built for another (R, C) is
+    refused; shells, maps and scalars bit-identical; shell=None skips that copy."""
+    import ctypes as ct
+    rng = np.random.default_rng(5)
+    shape = (70, 90, 12)
+    i, j, k = np.meshgrid(*[np.arange(s) for s in shape], indexing="ij")
+    ds = []
+    for _ in range(3):
+        d = np.zeros(shape, bool)
+        for _ in range(6):
+            c = [rng.uniform(0, 1) * s for s in shape]
+            r = rng.uniform(3, 10)
+            d |= (i - c[0]) ** 2 + (j - c[1]) ** 2 + ((k - c[2]) * 3) ** 2 <= r * r
+        ds.append(d.astype(np.uint8))
+    vox = (1.5, 1.5, 10.0)
+    table = compact_table(sphere_pix(vox, 50), shape)
+    c = _lib.context(0)
+    L = c.L
+    for b in (1, 3):
+        dd = np.ascontiguousarray(np.stack(ds[:b]))
+        ci0 = np.empty(dd.shape, np.float64)
+        sh0 = np.empty(dd.shape, np.int32)
+        sc0 = np.zeros(b)
+        c.check(L.vh_ci(c.h, _lib._ptr(dd), *shape, b, _lib._ptr(table.offsets), _lib._ptr(table.dup),
+                        table.rows, _lib._ptr(table.bounds), _lib._ptr(table.radii),
+                        table.bounds.shape[0], ct.c_double(1.5), _lib._ptr(ci0), _lib._ptr(sc0),
+                        _lib._ptr(sh0)), "vh_ci")
+        for _ in range(2):   # the second call reuses the device table
+            ci1, sc1, sh1 = _lib.ci(dd, table, 1.5)
+            assert np.array_equal(ci1, ci0) and np.array_equal(sc1, sc0) and np.array_equal(sh1, sh0)
+        ci2, sc2, sh2 = _lib.ci(dd, table, 1.5, shell=False)
+        assert sh2 is None and np.array_equal(ci2, ci0) and np.array_equal(sc2, sc0)
+        for q in range(b):
+            ref, _ = native.ci(ds[q], table, vox)
+            assert np.array_equal(ci0[q], ref)
+    th = c.ci_table(table, shape[0], shape[1])
+    other = np.zeros((60, 90, 12), np.uint8)
+    other[30, 40, 5] = 1
+    rc = L.vh_ci_tab(c.h, _lib._ptr(other), 60, 90, 12, 1, th, ct.c_double(1.5), None, None, None)
+    assert rc == _lib.VH_ERR_ARG
 
 
 def ulps(a, b):
@@ -228,6 +278,29 @@ def test_pipe_host_to_host_equals_batch(shape, n, sub, slots, twos):
                               [q.vdp, q.vdp_lb, q.n_km0, q.snr] + list(q.n4_iters[:4]), equal_nan=True)
 
 
+def test_pipe_pin_budget_stages_the_rest(monkeypatch):
+    """VH_PIPE_PIN_CAP bounds the caller memory a run pins in place: past it the
+    ranges go through the pinned staging, are counted (vh_pipe_stats) and the results are the same."""
+    R, C, Z = 128, 128, 24
+    n, sub, slots = 12, 4, 3
+    hp, mk = synth_batch(R, C, Z, n, base_seed=91)
+    o = _lib.Batch.options(do_n4=True, vox=(1.5, 1.5, 10.0))
+    P = _lib.Pipe(R, C, Z, sub, slots=slots)
+    ref = P.run(hp, mk, o)
+    peak0, staged0 = P.stats()
+    P.close()
+    assert peak0 > 0 and staged0 == 0
+    cap = 3 * sub * R * C * Z * 4   # about three chunks' inputs
+    monkeypatch.setenv("VH_PIPE_PIN_CAP", str(cap))
+    P = _lib.Pipe(R, C, Z, sub, slots=slots)
+    got = P.run(hp, mk, o)
+    peak, staged = P.stats()
+    P.close()
+    assert 0 < peak <= cap and staged > 0
+    for a, b in zip(got[:4], ref[:4]):
+        assert np.array_equal(a, b)
+
+
 def test_batch_equals_single():
     hp, mk = synth_batch(64, 64, 16, 4, base_seed=3)
     B = _lib.Batch(64, 64, 16, 4)
@@ -288,6 +361,96 @@ def test_class_full_pipeline_with_n4():
     n4b = v.N4_bias_correction(X, M)
     assert np.array_equal(n4b, v.N4HPvent)
 
+
+
+@pytest.mark.parametrize("v", [255, 2])
+def test_class_single_value_mask_vs_reference(v):
+    """A 0/v mask (mask DICOM folders often hold 0/255): with N4 := identity, as the
+    goldens were made, the class gives the reference's expressions on the v-scaled maps
+    (oracle.calculate_vdp_literal: scipy's medfilt2d on (mn < thresh) * mask, LB * mask) and the
+    golden VDP / SNR / CI."""
+    from vent_analysis_amd import Vent_Analysis
+    for path in GOLD:
+        X, M, vox, exp, name = load_case(path)
+        Mv = M * v
+        va = Vent_Analysis(xenon_array=X, mask_array=Mv, vox=vox)
+        va.N4_bias_correction = lambda H, Mk: H.astype(np.float32)
+        va.calculate_VDP()
+        o = O.calculate_vdp_literal(X, Mv, vox)
+        assert va.defectArray.dtype == np.float64 and va.defectArrayLB.dtype == np.float64, name
+        assert np.array_equal(va.defectArray, o["defectArray"]), name
+        assert np.array_equal(va.defectArray, exp["defect"] * np.float64(v)), name
+        assert np.array_equal(va.defectBorder, exp["defect_border"]), name
+        assert np.array_equal(va.defectArrayLB, o["defectArrayLB"]), name
+        for k in ("VDP", "VDP_lb", "DefectVolume"):
+            assert va.metadata[k] == o[k], (name, k)
+        assert va.metadata["VDP"] == exp["VDP"], name
+        assert va.metadata["LungVolume"] == 0.0   # np.sum(mask == 1) (:166)
+        assert rel(va.metadata["SNR"], exp["SNR"]) < 1e-5
+        if "CI" in exp:
+            va.calculate_CI()
+            assert va.metadata["CI"] == exp["CI"]
+            assert np.array_equal(va.CIarray[exp["defect"] > 0], exp["ci_values"])
+
+
+def test_class_255_mask_full_pipeline():
+    """Without an N4 override: a 0/255 mask has no voxel of SimpleITK N4's label 1 (the mask is
+    cast to UInt8, MaskLabel 1), so N4HPvent is HPvent itself (parity unpinned, see
+    Vent_Analysis.calculate_VDP) and the chain equals the literal oracle on it."""
+    from vent_analysis_amd import Vent_Analysis
+    X, M = synth_volume(128, 128, 24, 0)
+    va = Vent_Analysis(xenon_array=X, mask_array=M * 255.0, vox=(1.5, 1.5, 10.0))
+    va.calculate_VDP()
+    assert va.N4HPvent.dtype == np.float32 and np.array_equal(va.N4HPvent, X)
+    assert va.n4_iterations == [0, 0, 0, 0]
+    o = O.calculate_vdp_literal(X, M * 255.0, (1.5, 1.5, 10.0))
+    assert np.array_equal(va.defectArray, o["defectArray"])
+    assert np.array_equal(va.defectArrayLB, o["defectArrayLB"])
+    for k in ("VDP", "VDP_lb", "DefectVolume"):
+        assert va.metadata[k] == o[k], k
+    assert va.metadata["VDP_lb"] == 0.0 and va.metadata["DefectVolume"] == 0.0
+    assert rel(va.metadata["SNR"], O.calculate_snr(X, M)) < 1e-5
+    assert np.array_equal(va.N4_bias_correction(X, M * 255.0), X)
+    with pytest.raises(ValueError):   # several nonzero values: a median over mixed values
+        Vent_Analysis(xenon_array=X, mask_array=M * (1 + (np.arange(M.shape[2]) % 2)),
+                      vox=(1.5, 1.5, 10.0)).calculate_VDP()
+
+
+def test_pickle_and_nifti_of_gpu_study(tmp_path):
+    """SURVEY 8(f) rank 2 on device outputs: a GPU-computed study (calculate_VDP with N4 +
+    calculate_CI) through pickleMe -> Vent_Analysis(pickle_path=) keeps every array bit for bit
+    with the reference's dtypes (defectArray f64, defectBorder bool, defectArrayLB
+    f64, CIarray f64, N4HPvent f32, SNR f32), and exportNifti's six channels are those arrays
+    (Vent_Analysis.py:273-313, 542-559)."""
+    from vent_analysis_amd import Vent_Analysis, nifti
+    X, M = synth_volume(128, 128, 24, 0)
+    P = (X * 0.5 + 3).astype(np.float32)
+    va = Vent_Analysis(xenon_array=X, mask_array=M, proton_array=P, vox=(1.5, 1.5, 10.0))
+    va.calculate_VDP()
+    va.calculate_CI()
+    va.metadata["PatientName"] = "Test^Pickle"
+    pk = str(tmp_path / "study.pkl")
+    va.pickleMe(pk)
+    vb = Vent_Analysis(pickle_path=pk)
+    dtypes = {"defectArray": np.float64, "defectBorder": np.bool_, "defectArrayLB": np.float64,
+              "CIarray": np.float64, "N4HPvent": np.float32, "mask_border": np.float64}
+    for k, dt in dtypes.items():
+        a, b = getattr(va, k), getattr(vb, k)
+        assert b.dtype == dt, (k, b.dtype)
+        assert np.array_equal(a, b), k
+    for k in ("HPvent", "mask", "proton"):
+        assert np.array_equal(getattr(va, k), getattr(vb, k)), k
+    assert isinstance(vb.metadata["SNR"], np.float32)
+    for k, val in va.metadata.items():
+        assert vb.metadata[k] == val or (val != val and vb.metadata[k] != vb.metadata[k]), k
+    assert vb.vox == va.vox and vb.version == va.version
+    o = O.calculate_vdp(vb.N4HPvent, M, (1.5, 1.5, 10.0), HP=X)
+    assert np.array_equal(vb.defectArray, o["defectArray"]) and vb.metadata["VDP"] == o["VDP"]
+    vb.exportNifti(str(tmp_path), "study")
+    data, _, _ = nifti.load(str(tmp_path / "study_dataArray.nii"))
+    assert data.shape == X.shape + (6,) and data.dtype == np.float32
+    for ch, a in enumerate((P, X, M, vb.N4HPvent, vb.defectArray, vb.CIarray)):
+        assert np.array_equal(data[..., ch], np.asarray(a, np.float32)), ch
 
 # ---- ragged / degenerate shapes and full-size properties -------------------------------------
 RAGGED = [((37, 45, 7), 11), ((12, 70, 9), 12), ((12, 70, 9), 13), ((130, 20, 3), 13),
@@ -756,7 +919,7 @@ def test_overlay_vs_oracle(shape, seed):
 def test_montage_vs_oracle(shape, seed):
     from oracle import export_oracle as E
     mask, n4, defect, hp, proton, mb, ci = _render_case(*shape, seed)
-    pal = np.linspace(0.0, 1.0, 64 * 3).reshape(64, 3)
+    pal = parula()   # the reference's own 64 x 3 table (parula.npy, read by screenShot :466)
     rr, cc, ss = E.crop_to_data(mask, border=5)
     crop = (rr[0], len(rr), cc[0], len(cc), ss[0], len(ss))
     for c in (ci, None):
@@ -779,7 +942,7 @@ def test_export_class_methods(tmp_path):
     v.exportDICOM(ds, save_dir=str(tmp_path), forPACS=False)
     back = dicom.dcmread(tmp_path / f"{v.metadata['PatientName']}_defectDICOM.dcm")
     assert back.Rows == 48 and back.NumberOfFrames == 8 and back["PixelData"].value == rgb.tobytes()
-    pal = np.linspace(0.0, 1.0, 64 * 3).reshape(64, 3)
+    pal = parula()   # the reference's own 64 x 3 table (parula.npy, read by screenShot :466)
     img = v.screenShot(path=str(tmp_path / "shot.png"), parula=pal)
     exp = E.screenshot_image(v.proton, v.HPvent, v.N4HPvent, v.mask, v.mask_border, v.defectArray,
                              None, pal)

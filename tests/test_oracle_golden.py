@@ -121,3 +121,34 @@ def test_border3d_matches_np_gradient():
     one = np.zeros((5, 5, 1))
     one[2, 2, 0] = 1
     assert np.array_equal(O.calculate_border3d(one), O.calculate_border(one))
+
+
+@pytest.mark.parametrize("path", GOLD, ids=lambda p: p.split("/")[-1])
+def test_literal_oracle_vs_reference(path):
+    """calculate_vdp_literal (scipy's medfilt2d, the reference's expressions on any mask) gives
+    the reference's outputs on every golden case."""
+    X, M, vox, exp, _ = load_case(path)
+    r = O.calculate_vdp_literal(X, M, vox)
+    assert np.array_equal(r["defectArray"], exp["defect"])
+    assert np.array_equal(r["defectBorder"], exp["defect_border"])
+    assert np.array_equal(r["defectArrayLB"], exp["lb"])
+    for k in ("VDP", "VDP_lb", "DefectVolume", "mean_anchor", "p99"):
+        assert r[k] == exp[k], k
+
+
+@pytest.mark.parametrize("v", [255, 2, 1.5])
+def test_literal_oracle_single_value_mask(v):
+    """A 0/v mask (mask DICOM folders often hold 0/255): the maps scale by v, VDP is unchanged,
+    and the reference's `== 1` / `== 2` tests change DefectVolume and VDP_lb."""
+    path = [p for p in GOLD if "vdp_edge" in p][0]
+    X, M, vox, exp, _ = load_case(path)
+    r = O.calculate_vdp_literal(X, M * v, vox)
+    assert np.array_equal(r["defectArray"], exp["defect"] * np.float64(v))
+    assert np.array_equal(r["defectBorder"], exp["defect_border"])
+    assert np.array_equal(r["defectArrayLB"], exp["lb"] * np.float64(v))
+    assert r["VDP"] == exp["VDP"]
+    assert r["DefectVolume"] == (exp["DefectVolume"] if v == 1 else 0.0)
+    lb = exp["lb"] * np.float64(v)
+    assert r["VDP_lb"] == 100 * np.sum((lb == 1) * 1 + (lb == 2) * 1) / np.sum(M * v)
+    if v == 255:
+        assert r["VDP_lb"] == 0.0

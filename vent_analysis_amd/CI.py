@@ -10,7 +10,7 @@ from __future__ import annotations
 import numpy as np
 
 from . import _lib
-from .sphere import compact_table, radii_indices, sphere_pix
+from .sphere import compact_table, compact_table_for, radii_indices, sphere_pix
 
 __all__ = ["multi_which", "getSpherePix", "px2vec", "vec2px", "getRadiiIndices", "calculate_CV",
            "calculate_CI", "calculate_CI_with_index"]
@@ -53,8 +53,8 @@ def calculate_CI_with_index(defectArray, vox=(1, 1, 1), Rmax=50, device=0):
     """GPU cluster-index map plus the 95th-percentile CI of Vent_Analysis.calculate_CI
     (Vent_Analysis.py:268-270), from one kernel pass.  Returns (CIarray float64, CI float64)."""
     d = np.asarray(defectArray)
-    table = compact_table(sphere_pix(vox, Rmax), d.shape)
-    ci, scal, _ = _lib.ci(d, table, float(np.min(vox)), device=device)
+    table = compact_table_for(vox, Rmax, d.shape)
+    ci, scal, _ = _lib.ci(d, table, float(np.min(vox)), device=device, shell=False)
     return ci[0], np.float64(scal[0])
 
 

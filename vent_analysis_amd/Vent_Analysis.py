@@ -37,6 +37,32 @@ def _binary_u8(A, what):
     return u8
 
 
+def _mask_value(A, what='mask'):
+    """(mask != 0 as uint8 0/1, v) for a mask whose nonzero voxels all hold one positive value v
+    (0/1, 0/255, ...: what mask DICOM folders hold).  The reference works on any such mask:
+    ``mask > 0`` selects the signal (Vent_Analysis.py:245, :340), the defect and LB maps are
+    multiplied by the mask (:249, :256) and VDP divides by ``np.sum(mask)`` (:251, :257), so v
+    scales the maps and cancels in VDP.  Masks with several nonzero values (a median over mixed
+    values) or negative values raise ValueError."""
+    a = np.asarray(A)
+    if a.dtype == np.uint8 and a.max(initial=0) <= 1:
+        return np.ascontiguousarray(a), 1
+    nz = a != 0
+    vals = np.unique(a[nz]) if nz.any() else np.array([1])
+    if vals.size != 1 or not vals[0] > 0:
+        raise ValueError(f"{what}: the GPU path implements the reference's behaviour for masks "
+                         f"whose nonzero voxels share one positive value (got {vals[:4]}...)")
+    v = vals[0].item()
+    return nz.astype(np.uint8), (1 if v == 1 else v)
+
+
+def _n4_label(v):
+    """Whether N4 sees the mask voxels: the reference casts the mask to float32 and then to
+    sitk.UInt8 (Vent_Analysis.py:323-327, truncation) and SimpleITK's N4 uses label 1 only
+    (MaskLabel 1, UseMaskLabel true: SURVEY A.2).  A 0/255 mask therefore has no N4 voxels."""
+    return int(np.float32(v)) == 1
+
+
 class Vent_Analysis:
     """Complete VDP analysis: N4 bias correction, normalisation, defect maps, VDPs, CI.
     See the reference docstring (Vent_Analysis.py:27-57) for the attribute list."""
@@ -154,8 +180,16 @@ class Vent_Analysis:
 
     def calculate_VDP(self, thresh=0.6):
         """Vent_Analysis.py:239-263 as one GPU pipeline: SNR, N4, sorted masked list -> numpy-order
-        mean anchor, threshold + 3x3 median + border, 99th-pct linear binning, k-means, volumes."""
-        mask_u8 = _binary_u8(self.mask, 'mask')
+        mean anchor, threshold + 3x3 median + border, 99th-pct linear binning, k-means, volumes.
+
+        A mask of one nonzero value v != 1 (e.g. 0/255) runs the kernels on mask != 0 and scales
+        the maps by v as ``* self.mask`` does; VDP, VDP_lb and DefectVolume then follow the
+        reference's expressions on the scaled maps (v cancels in VDP; ``== 1`` tests find no
+        voxel for v = 255).  Such a mask has no voxel of N4's label 1 (_n4_label), and ITK's N4
+        on an empty label set leaves the image as it is (no histogram, an all-zero B-spline fit,
+        a NaN convergence measure that ends every level after one iteration): N4HPvent = HPvent,
+        parity unpinned (SimpleITK absent)."""
+        mask_u8, v = _mask_value(self.mask)
         hp = np.asarray(self.HPvent)
         vox = np.asarray(self.vox, dtype=np.float64)
         if self._n4_overridden():
@@ -165,10 +199,11 @@ class Vent_Analysis:
             d, bo, lb, res = _lib.vdp(self.N4HPvent, mask_u8, vox, hp=None, thresh=thresh,
                                       device=self.device)
         else:
+            do_n4 = _n4_label(v)
             B = _lib.Batch(*hp.shape, 1, device=self.device)
             try:
                 B.upload(hp.astype(np.float32)[None], mask_u8[None])
-                B.run(B.options(do_n4=True, thresh=thresh, vox=vox))
+                B.run(B.options(do_n4=do_n4, thresh=thresh, vox=vox))
                 n4, d, bo, lb, res = B.download(n4=True)
             finally:
                 B.close()
@@ -177,13 +212,22 @@ class Vent_Analysis:
             self.N4HPvent = n4[0]
             self.metadata['SNR'] = self._snr_dtype(res[0].snr, hp)
         r = res[0]
-        self.defectArray = d[0].astype(np.float64)
+        msum = np.sum(self.mask)
         self.defectBorder = bo[0] == 1
-        self.metadata['VDP'] = 100 * np.float64(r.n_defect) / np.sum(self.mask)
-        self.metadata['DefectVolume'] = r.n_defect * np.prod(np.divide(self.vox, 10)) / 1000
         self.defectArrayLB = lb[0].astype(np.float64) * np.asarray(self.mask)
-        self.metadata['VDP_lb'] = 100 * np.float64(r.n_lb12) / np.sum(self.mask)
-        self.metadata['VDP_km'] = 100 * np.float64(r.n_km0) / np.sum(self.mask)
+        if v == 1:
+            self.defectArray = d[0].astype(np.float64)
+            self.metadata['VDP'] = 100 * np.float64(r.n_defect) / msum
+            self.metadata['DefectVolume'] = r.n_defect * np.prod(np.divide(self.vox, 10)) / 1000
+            self.metadata['VDP_lb'] = 100 * np.float64(r.n_lb12) / msum
+        else:   # the reference's expressions on the v-scaled maps (:249-257)
+            self.defectArray = d[0].astype(np.float64) * v
+            self.metadata['VDP'] = 100 * np.sum(self.defectArray) / msum
+            self.metadata['DefectVolume'] = (np.sum(self.defectArray == 1)
+                                             * np.prod(np.divide(self.vox, 10)) / 1000)
+            self.metadata['VDP_lb'] = 100 * np.sum((self.defectArrayLB == 1) * 1
+                                                   + (self.defectArrayLB == 2) * 1) / msum
+        self.metadata['VDP_km'] = 100 * np.float64(r.n_km0) / np.float64(r.n_mask)
         self.n4_iterations = list(r.n4_iters)[:4]
         print('\033[32mcalculate_VDP ran successfully\033[37m')
 
@@ -203,7 +247,11 @@ class Vent_Analysis:
     def N4_bias_correction(self, HPvent, mask):
         """Vent_Analysis.py:316-334: N4 with the SimpleITK 2.3.1 defaults, on the GPU.
         Returns float32 like sitk.GetArrayFromImage."""
-        m = (np.asarray(mask) == 1).astype(np.uint8)
+        m = np.asarray(mask).astype(np.float32)
+        m = ((m >= 1) & (m < 2)).astype(np.uint8)   # sitk.Cast(..., UInt8) == label 1 (:323-327)
+        if not m.any():   # empty label set: ITK's N4 leaves the image unchanged (calculate_VDP)
+            self.n4_iterations = [0, 0, 0, 0]
+            return np.asarray(HPvent, dtype=np.float32).copy()
         out, its, _ = _lib.n4(np.asarray(HPvent, dtype=np.float32), m, device=self.device)
         self.n4_iterations = list(its[0])
         return out[0]
@@ -214,7 +262,7 @@ class Vent_Analysis:
         if manualNoise:
             raise UnboundLocalError("cannot access local variable 'noise' (manualNoise branch is "
                                     "empty in the reference, Vent_Analysis.py:353-355)")
-        m = _binary_u8(self.mask, 'mask')
+        m, _ = _mask_value(self.mask)
         v = _lib.snr(np.asarray(A, dtype=np.float32), m, device=self.device)[0]
         return self._snr_dtype(v, A)
 
@@ -374,7 +422,10 @@ class Vent_Analysis:
             try:
                 return ImageFont.truetype('arial.ttf', size=size)
             except OSError:   # the reference's font is not installed: PIL's default, same size
-                return ImageFont.load_default(size=size)
+                try:
+                    return ImageFont.load_default(size=size)
+                except TypeError:   # Pillow < 10.1 (the reference pins 10.0.0): no size argument
+                    return ImageFont.load_default()
 
         md, white = self.metadata, (255, 255, 255)
         draw = ImageDraw.Draw(image)

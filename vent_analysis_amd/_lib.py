@@ -68,6 +68,9 @@ _SIGS = {
     "vh_vdp": ([_P, _P, _P, _P, _I64, _I64, _I64, _I64, ct.c_float, _P, _P, _P, _P, _P], ct.c_int),
     "vh_ci": ([_P, _P, _I64, _I64, _I64, _I64, _P, _P, _I64, _P, _P, _I64, ct.c_double, _P, _P,
                _P], ct.c_int),
+    "vh_ci_table_create": ([_P, _I64, _I64, _P, _P, _I64, _P, _P, _I64, ct.POINTER(_P)], ct.c_int),
+    "vh_ci_table_destroy": ([_P], ct.c_int),
+    "vh_ci_tab": ([_P, _P, _I64, _I64, _I64, _I64, _P, ct.c_double, _P, _P, _P], ct.c_int),
     "vh_batch_create": ([_P, _I64, _I64, _I64, _I64, ct.POINTER(_P)], ct.c_int),
     "vh_batch_destroy": ([_P], ct.c_int),
     "vh_batch_upload": ([_P, _P, _P], ct.c_int),
@@ -90,6 +93,7 @@ _SIGS = {
     "vh_pipe_create": ([_P, _I64, _I64, _I64, _I64, ct.c_int, ct.POINTER(_P)], ct.c_int),
     "vh_pipe_run": ([_P, _P, _P, _I64, ct.POINTER(RunOpts), _P, _P, _P, _P, _P], ct.c_int),
     "vh_pipe_destroy": ([_P], ct.c_int),
+    "vh_pipe_stats": ([_P, ct.POINTER(ct.c_int64), ct.POINTER(ct.c_int64)], ct.c_int),
     "vh_comm_unique_id": ([_P], ct.c_int),
     "vh_comm_init": ([_P, ct.c_int, ct.c_int, _P], ct.c_int),
     "vh_batch_cohort_allreduce": ([_P], ct.c_int),
@@ -135,9 +139,31 @@ class Context:
                                f"{self.L.vh_status_string(rc).decode()}")
         self.h = h
         self.device = device
+        self.ci_tables = {}   # id(SphereTable) -> (table, vh_ci_table handle): tables stay in HBM
+
+    def ci_table(self, table, R, C):
+        """The device copy of a compact sphere table for (R, C) volumes (vh_ci_table_create, once
+        per table object; the reference caches the table file the same way, CI.py:43-61)."""
+        key = (id(table), int(R), int(C))
+        hit = self.ci_tables.get(key)
+        if hit is not None and hit[0] is table:
+            return hit[1]
+        if len(self.ci_tables) >= 8:   # drop the oldest
+            k0 = next(iter(self.ci_tables))
+            self.L.vh_ci_table_destroy(self.ci_tables.pop(k0)[1])
+        h = _P()
+        self.check(self.L.vh_ci_table_create(self.h, int(R), int(C), _ptr(table.offsets),
+                                             _ptr(table.dup), table.rows, _ptr(table.bounds),
+                                             _ptr(table.radii), table.bounds.shape[0], ct.byref(h)),
+                   "vh_ci_table_create")
+        self.ci_tables[key] = (table, h)
+        return h
 
     def close(self):
         if getattr(self, "h", None):
+            for _, th in self.ci_tables.values():
+                self.L.vh_ci_table_destroy(th)
+            self.ci_tables.clear()
             self.L.vh_destroy(self.h)
             self.h = None
 
@@ -286,19 +312,19 @@ def vdp(n4v, mask, vox, hp=None, thresh=0.6, device=0):
     return defect, bord, lb, list(res)
 
 
-def ci(defect, table, minvox, device=0):
-    """table: vent_analysis_amd.sphere.SphereTable for this shape.  Returns (ci f64, scalar[B],
-    shell int32)."""
+def ci(defect, table, minvox, device=0, shell=True):
+    """table: vent_analysis_amd.sphere.SphereTable for this shape (kept in HBM per context after
+    the first call).  Returns (ci f64, scalar[B], shell int32 or None)."""
     c = context(device)
     d = as_batch(np.asarray(defect) != 0, np.uint8)
     B, R, C, Z = d.shape
     out = np.empty((B, R, C, Z), np.float64)
-    shell = np.empty((B, R, C, Z), np.int32)
+    sh = np.empty((B, R, C, Z), np.int32) if shell else None
     sc = np.zeros(B, np.float64)
-    c.check(c.L.vh_ci(c.h, _ptr(d), R, C, Z, B, _ptr(table.offsets), _ptr(table.dup), table.rows,
-                      _ptr(table.bounds), _ptr(table.radii), table.bounds.shape[0],
-                      ct.c_double(minvox), _ptr(out), _ptr(sc), _ptr(shell)), "vh_ci")
-    return out, sc, shell
+    th = c.ci_table(table, R, C)
+    c.check(c.L.vh_ci_tab(c.h, _ptr(d), R, C, Z, B, th, ct.c_double(minvox), _ptr(out), _ptr(sc),
+                          _ptr(sh)), "vh_ci_tab")
+    return out, sc, sh
 
 
 def ctx_profile(on, device=0):
@@ -508,6 +534,13 @@ class Pipe:
                                           *[_ptr(a) for a in out], ct.cast(res, ct.c_void_p)),
                        "vh_pipe_run")
         return (*out, list(res))
+
+    def stats(self):
+        """(peak bytes of caller memory pinned in place, caller ranges staged instead) of the last
+        run (vh_pipe_stats)."""
+        pk, st = ct.c_int64(), ct.c_int64()
+        self.ctx.check(self.L.vh_pipe_stats(self.h, ct.byref(pk), ct.byref(st)), "vh_pipe_stats")
+        return int(pk.value), int(st.value)
 
 
 def comm_unique_id() -> bytes:

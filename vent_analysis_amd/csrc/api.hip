@@ -115,7 +115,7 @@ static void batch_free(vh_batch *b) {
     dfree(b->d_numfix); dfree(b->d_rowstart); dfree(b->d_rowmask); dfree(b->d_rrank); dfree(b->d_iscan); dfree(b->d_D); dfree(b->d_perm); dfree(b->d_P1); dfree(b->d_den); dfree(b->d_T);
     dfree(b->d_U); dfree(b->d_ridx); dfree(b->d_cp); dfree(b->d_cvol); dfree(b->d_hpart); dfree(b->d_hred); dfree(b->d_cpart); dfree(b->d_st); dfree(b->d_nactive); dfree(b->d_tabs); dfree(b->d_twiddle); dfree(b->d_study_lv); dfree(b->d_pcg); dfree(b->d_sortg); dfree(b->d_study_latg);
     dfree(b->d_bitmap); dfree(b->d_ci_list); dfree(b->d_ci_shell); dfree(b->d_ci_hist);
-    dfree(b->d_ci_offL); dfree(b->d_ci_bounds); dfree(b->d_ci_radii); dfree(b->d_ci_status);
+    dfree(b->d_ci_status);
     dfree(b->d_ci_count); dfree(b->d_ci_map);
     if (b->stream) (void)hipStreamDestroy(b->stream);
     if (b->h_flags) (void)hipHostFree(b->h_flags);
@@ -516,35 +516,66 @@ int vh_vdp(vh_ctx *ctx, const float *hp, const float *n4, const uint8_t *mask, i
     })
 }
 
+// CI on host buffers through a device-resident table; shared by vh_ci and vh_ci_tab
+static void ci_host(vh_ctx *ctx, const uint8_t *defect, int64_t R, int64_t C, int64_t Z, int64_t batch,
+                    const vh_ci_table *t, double minvox, double *ci_array, double *ci_scalar, int32_t *shell) {
+    if (!defect || !t) throw VhError{VH_ERR_ARG, "null defect map / table"};
+    if (t->ctx != ctx) throw VhError{VH_ERR_ARG, "sphere table of another context"};
+    vh_batch *b = scratch_batch(ctx, R, C, Z, batch);
+    HIP_TRY(hipSetDevice(ctx->device));
+    b->profile = ctx->profile != 0;
+    const size_t NV = (size_t)batch * b->V;
+    HIP_TRY(hipMemcpyAsync(b->d_defect, defect, NV, hipMemcpyHostToDevice, b->stream));
+    if (ci_array && !b->d_ci_map) HIP_TRY(hipMalloc(&b->d_ci_map, sizeof(double) * NV));
+    vh_ci_run(b, t, minvox, ci_array ? b->d_ci_map : nullptr);
+    // every copy on the batch's stream, one sync at the end
+    if (ci_array) HIP_TRY(hipMemcpyAsync(ci_array, b->d_ci_map, sizeof(double) * NV, hipMemcpyDeviceToHost, b->stream));
+    if (shell) HIP_TRY(hipMemcpyAsync(shell, b->d_ci_shell, sizeof(int32_t) * NV, hipMemcpyDeviceToHost, b->stream));
+    std::vector<VolScalars> sc(batch);
+    HIP_TRY(hipMemcpyAsync(sc.data(), b->d_sc, sizeof(VolScalars) * batch, hipMemcpyDeviceToHost, b->stream));
+    HIP_TRY(hipStreamSynchronize(b->stream));
+    for (int64_t i = 0; i < batch; ++i) {
+        if (ci_scalar) ci_scalar[i] = sc[i].ci_scalar;
+        if (sc[i].ci_status == VH_ERR_MAXRADIUS)
+            throw VhError{VH_ERR_MAXRADIUS, "--MAX RADIUS REACHED-- (CI.py:101-103)"};
+        if (sc[i].ci_status == VH_ERR_EMPTY)
+            throw VhError{VH_ERR_EMPTY, "no defect voxels (Vent_Analysis.py:270 IndexError)"};
+    }
+}
+
 int vh_ci(vh_ctx *ctx, const uint8_t *defect, int64_t R, int64_t C, int64_t Z, int64_t batch,
           const int16_t *offs, const uint8_t *dup, int64_t rows, const int32_t *bounds,
           const double *radii, int64_t nb, double minvox, double *ci_array, double *ci_scalar,
           int32_t *shell) {
     API_TRY(ctx, {
         std::lock_guard<std::mutex> lock(ctx->mu);
-        if (!defect || !offs || !dup || !bounds || !radii || rows < 1 || nb < 1)
-            throw VhError{VH_ERR_ARG, "null buffer / empty table"};
-        for (int64_t q = 0; q < nb; ++q)
-            if (bounds[q] < 1 || bounds[q] > rows || (q && bounds[q] <= bounds[q - 1]))
-                throw VhError{VH_ERR_ARG, "sphere table bounds must be increasing in [1, rows]"};
-        vh_batch *b = scratch_batch(ctx, R, C, Z, batch);
-        HIP_TRY(hipSetDevice(ctx->device));
-        b->profile = ctx->profile != 0;
-        const size_t NV = (size_t)batch * b->V;
-        HIP_TRY(hipMemcpyAsync(b->d_defect, defect, NV, hipMemcpyHostToDevice, b->stream));
-        if (ci_array && !b->d_ci_map) HIP_TRY(hipMalloc(&b->d_ci_map, sizeof(double) * NV));
-        vh_ci_run(b, offs, dup, rows, bounds, radii, nb, minvox, ci_array ? b->d_ci_map : nullptr);
-        if (ci_array) HIP_TRY(hipMemcpy(ci_array, b->d_ci_map, sizeof(double) * NV, hipMemcpyDeviceToHost));
-        if (shell) HIP_TRY(hipMemcpy(shell, b->d_ci_shell, sizeof(int32_t) * NV, hipMemcpyDeviceToHost));
-        std::vector<VolScalars> sc(batch);
-        HIP_TRY(hipMemcpy(sc.data(), b->d_sc, sizeof(VolScalars) * batch, hipMemcpyDeviceToHost));
-        for (int64_t i = 0; i < batch; ++i) {
-            if (ci_scalar) ci_scalar[i] = sc[i].ci_scalar;
-            if (sc[i].ci_status == VH_ERR_MAXRADIUS)
-                throw VhError{VH_ERR_MAXRADIUS, "--MAX RADIUS REACHED-- (CI.py:101-103)"};
-            if (sc[i].ci_status == VH_ERR_EMPTY)
-                throw VhError{VH_ERR_EMPTY, "no defect voxels (Vent_Analysis.py:270 IndexError)"};
-        }
+        std::unique_ptr<vh_ci_table, void (*)(vh_ci_table *)> t(
+            vh_ci_table_build(ctx, R, C, offs, dup, rows, bounds, radii, nb), vh_ci_table_free);
+        ci_host(ctx, defect, R, C, Z, batch, t.get(), minvox, ci_array, ci_scalar, shell);
+    })
+}
+
+int vh_ci_table_create(vh_ctx *ctx, int64_t R, int64_t C, const int16_t *offs, const uint8_t *dup,
+                       int64_t rows, const int32_t *bounds, const double *radii, int64_t nb,
+                       vh_ci_table **out) {
+    if (out) *out = nullptr;
+    API_TRY(ctx, {
+        if (!out) throw VhError{VH_ERR_ARG, "null out"};
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        *out = vh_ci_table_build(ctx, R, C, offs, dup, rows, bounds, radii, nb);
+    })
+}
+
+int vh_ci_table_destroy(vh_ci_table *t) {
+    vh_ci_table_free(t);
+    return VH_OK;
+}
+
+int vh_ci_tab(vh_ctx *ctx, const uint8_t *defect, int64_t R, int64_t C, int64_t Z, int64_t batch,
+              const vh_ci_table *t, double minvox, double *ci_array, double *ci_scalar, int32_t *shell) {
+    API_TRY(ctx, {
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        ci_host(ctx, defect, R, C, Z, batch, t, minvox, ci_array, ci_scalar, shell);
     })
 }
 
@@ -658,7 +689,7 @@ int vh_batch_study_times(vh_batch *b, double *us) {
         for (int64_t i = 0; i < b->nb; ++i) us[i] = 0.0;
         if (!b->have_result || !b->opts.do_n4 || !b->n4_used_study) return VH_OK;
         std::vector<N4State> st(b->nb);
-        HIP_TRY(hipMemcpy(st.data(), b->d_st, sizeof(N4State) * b->nb, hipMemcpyDeviceToHost));
+        d2h_on_stream(b, st.data(), b->d_st, sizeof(N4State) * b->nb);
         int rate_khz = 0;
         HIP_TRY(hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, b->ctx->device));
         if (rate_khz <= 0) throw VhError{VH_ERR_HIP, "no device wall clock rate"};
@@ -866,6 +897,8 @@ int vh_pipe_create(vh_ctx *ctx, int64_t R, int64_t C, int64_t Z, int64_t sub, in
         vh_pipe *p = new vh_pipe;
         p->ctx = ctx;
         p->R = R; p->C = C; p->Z = Z; p->sub = sub;
+        p->pin_cap = (int64_t)32 << 30;
+        if (const char *e = getenv("VH_PIPE_PIN_CAP")) p->pin_cap = atoll(e);
         const size_t NV = (size_t)sub * R * C * Z;
         try {
             for (int s = 0; s < slots; ++s) {
@@ -921,21 +954,39 @@ static void par_touch(void *dst, size_t bytes) {
 
 struct HostPin {
     void *p = nullptr;
+    size_t n = 0;
+    vh_pipe *owner = nullptr;   // the pipe whose pin budget this registration counts against
     HostPin() = default;
     HostPin(const HostPin &) = delete;
     HostPin &operator=(const HostPin &) = delete;
-    bool pin(const void *ptr, size_t bytes, bool touch = false) {
+    bool pin(const void *ptr, size_t bytes, bool touch, vh_pipe *pp) {
         if (!ptr || !bytes || getenv("VH_PIPE_STAGE")) return false;
+        // the budget first: a run over more than pin_cap bytes of caller memory stages the rest
+        // rather than page-locking all of it (counted in staged_spans, vh_pipe_stats)
+        const int64_t now = pp->pinned.fetch_add((int64_t)bytes) + (int64_t)bytes;
+        if (now > pp->pin_cap) {
+            pp->pinned.fetch_sub((int64_t)bytes);
+            return false;
+        }
+        int64_t pk = pp->pinned_peak.load();
+        while (now > pk && !pp->pinned_peak.compare_exchange_weak(pk, now)) {
+        }
         if (touch) par_touch(const_cast<void *>(ptr), bytes);
         if (hipHostRegister(const_cast<void *>(ptr), bytes, hipHostRegisterDefault) != hipSuccess) {
             (void)hipGetLastError();
+            pp->pinned.fetch_sub((int64_t)bytes);
             return false;
         }
         p = const_cast<void *>(ptr);
+        n = bytes;
+        owner = pp;
         return true;
     }
     ~HostPin() {
-        if (p) (void)hipHostUnregister(p);
+        if (p) {
+            (void)hipHostUnregister(p);
+            owner->pinned.fetch_sub((int64_t)n);
+        }
     }
 };
 
@@ -952,14 +1003,17 @@ struct PipeSpan {
     size_t n = 0, h = 0, t = 0;
     bool direct = false;
     HostPin pin;
-    void plan(const void *ptr, size_t bytes, bool touch) {
+    void plan(const void *ptr, size_t bytes, bool touch, vh_pipe *pp) {
         p = (char *)ptr;
         n = ptr ? bytes : 0;
         if (!n) return;
         const uintptr_t pg = 4096, s0 = (uintptr_t)p, e0 = s0 + n;
         const uintptr_t a = (s0 + pg - 1) / pg * pg, e = e0 / pg * pg;
         if (e <= a || e - a < ((size_t)1 << 20)) return;   // small: staged
-        if (!pin.pin((void *)a, e - a, touch)) return;
+        if (!pin.pin((void *)a, e - a, touch, pp)) {
+            pp->staged_spans.fetch_add(1);
+            return;
+        }
         h = a - s0;
         t = e0 - e;
         direct = true;
@@ -1020,6 +1074,8 @@ int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, con
             hipEvent_t e[3];
         };
         const bool trace = getenv("VH_PIPE_TRACE") != nullptr;
+        p->pinned_peak = 0;
+        p->staged_spans = 0;
         std::vector<std::vector<std::unique_ptr<PipeSpan[]>>> keep(slots);
         std::vector<std::vector<Mark>> marks(slots);
         hipEvent_t ev0 = nullptr;
@@ -1104,10 +1160,10 @@ int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, con
                 // for the device: released per chunk, it lined every slot up behind the others)
                 keep[s].emplace_back(new PipeSpan[3]);
                 c.sp = keep[s].back().get();
-                c.sp[0].plan(hp + c.v0 * V, sizeof(float) * c.CV, false);
+                c.sp[0].plan(hp + c.v0 * V, sizeof(float) * c.CV, false, p);
                 c.mb = q.mb + ((k / slots) & 1) * q.mb_half;   // bits double-buffered across chunks
                 c.mbits = !getenv("VH_PIPE_STAGE") && par_pack_mask(mask + c.v0 * V, c.mb, c.CV);
-                if (!c.mbits) c.sp[1].plan(mask + c.v0 * V, c.CV, false);
+                if (!c.mbits) c.sp[1].plan(mask + c.v0 * V, c.CV, false, p);
             };
             auto front = [&](Chunk &c) {
                 const size_t CV = c.CV;
@@ -1155,7 +1211,7 @@ int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, con
                 }
             };
             auto back_pin = [&](Chunk &c) {   // while the chunk computes: first touch + pin of its output pages
-                c.sp[2].plan(n4 ? n4 + c.v0 * V : nullptr, sizeof(float) * c.CV, true);
+                c.sp[2].plan(n4 ? n4 + c.v0 * V : nullptr, sizeof(float) * c.CV, true, p);
             };
             auto back = [&](Chunk &c) {
                 const float *dn4 = opts->do_n4 ? b->d_n4 : b->d_hp;
@@ -1245,6 +1301,13 @@ int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, con
         for (int s = 0; s < slots; ++s)
             if (failed[s] == 1) throw err[s];
     })
+}
+
+int vh_pipe_stats(vh_pipe *p, int64_t *pinned_peak_bytes, int64_t *staged_spans) {
+    if (!p) return VH_ERR_ARG;
+    if (pinned_peak_bytes) *pinned_peak_bytes = p->pinned_peak.load();
+    if (staged_spans) *staged_spans = p->staged_spans.load();
+    return VH_OK;
 }
 
 int vh_pipe_destroy(vh_pipe *p) {

@@ -1,10 +1,9 @@
 // ci.hip -- cluster-index map on gfx950 (CI.calculate_CI, CI.py:107-145, and the 95th-percentile
 // tail of Vent_Analysis.calculate_CI, Vent_Analysis.py:265-271).
 //
-// One lane per defect voxel.  The lanes of a wave walk the sphere table in LOCKSTEP (row index is
-// wave-uniform, so the table's row offset is one broadcast load per row for the whole wave), each
-// lane testing one bit of the volume's defect bitmap per row.  At every shell boundary b the lane
-// stops at the first b with 2*hits < b (C = hits/b < 0.5, CI.py:97) and records the shell.
+// One wave per defect voxel (k_ci_walk): the wave's lanes test consecutive rows of the sphere table
+// against the volume's defect bitmap and stop at the first shell boundary b with 2*hits < b
+// (C = hits/b < 0.5, CI.py:97), recording the shell.
 // Semantics restated in oracle/ci_oracle.c: the bitmap is indexed by the
 // Fortran-order linear index L = (i+dx) + (j+dy) s0 + (k+dz) s0 s1 (px2vec, CI.py:65-68), so
 // out-of-range rows/cols alias into neighbouring columns/slices and only 0 <= L < N is required;
@@ -41,35 +40,50 @@ __global__ void k_ci_bitmap(const uint8_t *__restrict__ defect, int64_t s0, int6
     if (d) list[b * V + (int64_t)(s_base + my)] = (int32_t)v;
 }
 
-// One WAVE per defect voxel: the wave walks 64 consecutive table rows per step (lane l probes row
-// r0 + l), the step's hits are one ballot, and the shell boundaries that fall in the step are tested
-// in parallel (lane i takes the i-th boundary in the step: cumulative hits up to row b - 1 are the
-// hits before the step plus a popcount of the ballot's low bits; the first boundary with
-// 2 hits < b stops the walk).  Every probe of the lockstep lane-per-voxel form is made (same rows,
-// same order of boundaries), but a 128x128x24 study's ~6k defect voxels now fill ~6k waves instead
-// of ~93.  The defect bitmap sits in LDS when it fits (48 KiB at 128x128x24).
+// One WAVE per defect voxel: the wave probes CIW_U x 64 consecutive table rows per step (lane l
+// tests rows r0 + 64 u + l, u < CIW_U: the CIW_U loads are independent, so one step pays one memory
+// latency for 256 rows), the step's hits are CIW_U ballots, and the shell boundaries that fall in
+// the step are tested in parallel, 64 at a time (lane i takes the i-th boundary: cumulative hits up
+// to row b - 1 are the hits before the step plus popcounts of the ballots below b's); the first
+// boundary with 2 hits < b stops the walk.  Every probe of the lane-per-voxel form is made (same rows,
+// same order of boundaries; rows past the stop in the last step are probed and ignored).  LDS holds
+// the Fortran-order defect bitmap (48 KiB at 128x128x24) and the first CIW_ROWS rows of linear
+// offsets and CIW_NBS boundaries (every walk shorter than r ~ 23 at [1.5, 1.5, 10] stays in LDS);
+// later rows come from L2.  A block takes voxels blockIdx.x, blockIdx.x + gridDim.x, ... (16 waves
+// each) and exits before staging anything when the volume has fewer defect voxels than its first.
 #define CIW_TPB 1024
-#define CIW_LDS_WORDS (40 * 1024)   // bitmaps up to 160 KiB in LDS (V <= 1.3 M voxels)
+#define CIW_U 4
+#define CIW_ROWS 8192
+#define CIW_NBS 1024
+#define CIW_LDS_MAX (160 * 1024)
 __global__ void __launch_bounds__(CIW_TPB) k_ci_walk(const uint32_t *__restrict__ bits,
                                                     const int32_t *__restrict__ list,
                                                     const unsigned long long *count,
                                                     const int32_t *__restrict__ offL, int64_t rows,
                                                     const int32_t *__restrict__ bounds, int64_t nbs,
                                                     int64_t s0, int64_t s1, int64_t s2, int64_t V,
-                                                    int64_t words, int use_lds, int32_t *shell_of,
+                                                    int64_t words, int stage_bits, int32_t *shell_of,
                                                     uint32_t *hist, int32_t *status) {
-    extern __shared__ uint32_t s_bits[];
+    extern __shared__ uint32_t s_lds[];
     const int64_t b = blockIdx.y;
     const int64_t n = (int64_t)count[b];
     constexpr int W = CIW_TPB / 64;
-    if ((int64_t)blockIdx.x * W >= n) return;   // block-uniform exit
+    if ((int64_t)blockIdx.x * W >= n) return;   // block-uniform exit, before any staging
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    // LDS: offsets [CIW_ROWS], boundaries [CIW_NBS], then the bitmap (stage_bits)
+    int32_t *s_off = reinterpret_cast<int32_t *>(s_lds), *s_bnd = s_off + CIW_ROWS;
+    const int lrows = (int)(rows < CIW_ROWS ? rows : CIW_ROWS), lnbs = (int)(nbs < CIW_NBS ? nbs : CIW_NBS);
+    for (int i = threadIdx.x; i < lrows; i += CIW_TPB) s_off[i] = offL[i];
+    for (int i = threadIdx.x; i < lnbs; i += CIW_TPB) s_bnd[i] = bounds[i];
     const uint32_t *bm = bits + b * words;
-    if (use_lds) {
+    if (stage_bits) {
+        uint32_t *s_bits = reinterpret_cast<uint32_t *>(s_bnd + CIW_NBS);
         for (int64_t i = threadIdx.x; i < words; i += CIW_TPB) s_bits[i] = bm[i];
-        __syncthreads();
         bm = s_bits;
     }
+    __syncthreads();
+    auto off_at = [&](int64_t r) { return r < lrows ? s_off[r] : offL[r]; };
+    auto bnd_at = [&](int64_t q) { return q < lnbs ? (int64_t)s_bnd[q] : (int64_t)bounds[q]; };
     const int64_t N = s0 * s1 * s2;
     for (int64_t idx = (int64_t)blockIdx.x * W + w; idx < n; idx += (int64_t)gridDim.x * W) {
         const int32_t v = list[b * V + idx];
@@ -78,30 +92,49 @@ __global__ void __launch_bounds__(CIW_TPB) k_ci_walk(const uint32_t *__restrict_
         int64_t hits = 0, q = 0, row = 0;
         int32_t qstop = -1;
         while (q < nbs && row < rows) {
-            const int64_t r = row + lane;
-            bool hit = false;
-            if (r < rows) {
-                const int32_t off = offL[r];
-                const int64_t L = base + off;
-                hit = off != CI_SENTINEL && L >= 0 && L < N && ((bm[L >> 5] >> (L & 31)) & 1u);
+            uint64_t bal[CIW_U];
+            int32_t off[CIW_U];
+#pragma unroll
+            for (int u = 0; u < CIW_U; ++u) {
+                const int64_t r = row + 64 * u + lane;
+                off[u] = r < rows ? off_at(r) : CI_SENTINEL;
             }
-            const uint64_t bal = __ballot(hit);
-            const int64_t bq = q + lane < nbs ? (int64_t)bounds[q + lane] : INT64_MAX;
-            const bool inc = bq <= row + 64;   // boundaries in (row, row + 64]: a prefix of the lanes
-            bool stop = false;
-            if (inc) {
-                const int pos = (int)(bq - 1 - row);   // 0 .. 63
-                const uint64_t m = pos == 63 ? ~0ull : ((2ull << pos) - 1ull);
-                stop = 2 * (hits + __popcll(bal & m)) < bq;
+#pragma unroll
+            for (int u = 0; u < CIW_U; ++u) {
+                const int64_t L = base + off[u];
+                const bool hit = off[u] != CI_SENTINEL && L >= 0 && L < N && ((bm[L >> 5] >> (L & 31)) & 1u);
+                bal[u] = __ballot(hit);
             }
-            const uint64_t sb = __ballot(stop);
-            if (sb) {
-                qstop = (int32_t)(q + __builtin_ctzll(sb));
-                break;
+            const int64_t rend = row + 64 * CIW_U;
+            // boundaries in (row, rend], 64 per pass, in order
+            bool stopped = false;
+            for (;;) {
+                const int64_t bq = q + lane < nbs ? bnd_at(q + lane) : INT64_MAX;
+                const bool inc = bq <= rend;
+                bool stop = false;
+                if (inc) {
+                    const int pos = (int)(bq - 1 - row);   // 0 .. 64 CIW_U - 1
+                    const int u = pos >> 6, pb = pos & 63;
+                    int64_t c = hits;
+#pragma unroll
+                    for (int uu = 0; uu < CIW_U; ++uu)
+                        c += uu < u ? __popcll(bal[uu]) : uu == u ? __popcll(bal[uu] & (pb == 63 ? ~0ull : ((2ull << pb) - 1ull))) : 0;
+                    stop = 2 * c < bq;
+                }
+                const uint64_t sb = __ballot(stop);
+                if (sb) {
+                    qstop = (int32_t)(q + __builtin_ctzll(sb));
+                    stopped = true;
+                    break;
+                }
+                const int ninc = __popcll(__ballot(inc));
+                q += ninc;
+                if (ninc < 64 || q >= nbs) break;
             }
-            q += __popcll(__ballot(inc));
-            hits += __popcll(bal);
-            row += 64;
+            if (stopped) break;
+#pragma unroll
+            for (int u = 0; u < CIW_U; ++u) hits += __popcll(bal[u]);
+            row = rend;
         }
         if (lane == 0) {
             shell_of[b * V + v] = qstop;
@@ -142,31 +175,62 @@ __global__ void k_ci_scatter(const int32_t *shell_of, const uint8_t *defect, con
     ci[b * V + v] = r;
 }
 
-// host: offs/dup/bounds/radii are host arrays; results stay on device (d_ci_shell, d_sc) and the
-// float64 CI map goes to ci_dev (caller-provided device buffer, nb*V doubles).
-void vh_ci_run(vh_batch *b, const int16_t *offs, const uint8_t *dup, int64_t rows,
-               const int32_t *bounds, const double *radii, int64_t nbs, double minvox,
-               double *d_ci) {
-    hipStream_t st = b->stream;
-    const int64_t words = (b->V + 31) / 32;
-    // px2vec strides (CI.py:65-68): s0 = R (rows), s1 = C (cols): L = i + j R + k R C
+// host: a compact sphere table uploaded once (vh_ci_table_create): the linear px2vec offsets of
+// its rows for one (R, C) -- the stride of L = i + j R + k R C, CI.py:65-68 -- with duplicates
+// marked, the shell boundaries and radii, all resident in HBM until vh_ci_table_destroy.
+vh_ci_table *vh_ci_table_build(vh_ctx *ctx, int64_t R, int64_t C, const int16_t *offs, const uint8_t *dup,
+                               int64_t rows, const int32_t *bounds, const double *radii, int64_t nbs) {
+    if (!offs || !dup || !bounds || !radii || rows < 1 || nbs < 1 || R < 1 || C < 1)
+        throw VhError{VH_ERR_ARG, "null buffer / empty table"};
+    for (int64_t q = 0; q < nbs; ++q)
+        if (bounds[q] < 1 || bounds[q] > rows || (q && bounds[q] <= bounds[q - 1]))
+            throw VhError{VH_ERR_ARG, "sphere table bounds must be increasing in [1, rows]"};
     std::vector<int32_t> offL(rows);
     for (int64_t r = 0; r < rows; ++r)
         offL[r] = dup[r] ? CI_SENTINEL
-                         : (int32_t)(offs[3 * r] + (int64_t)offs[3 * r + 1] * b->R +
-                                     (int64_t)offs[3 * r + 2] * b->R * b->C);
-    // workspace owned by the batch (freed with it): no allocation, and nothing to leak, per call
-    if (rows > b->ci_rows_cap) {
-        if (b->d_ci_offL) HIP_TRY(hipFree(b->d_ci_offL));
-        b->d_ci_offL = nullptr;
-        HIP_TRY(hipMalloc(&b->d_ci_offL, sizeof(int32_t) * rows));
-        b->ci_rows_cap = rows;
+                         : (int32_t)(offs[3 * r] + (int64_t)offs[3 * r + 1] * R + (int64_t)offs[3 * r + 2] * R * C);
+    HIP_TRY(hipSetDevice(ctx->device));
+    vh_ci_table *t = new vh_ci_table;
+    t->ctx = ctx;
+    t->R = R;
+    t->C = C;
+    t->rows = rows;
+    t->nbs = nbs;
+    try {
+        HIP_TRY(hipMalloc(&t->d_offL, sizeof(int32_t) * rows));
+        HIP_TRY(hipMalloc(&t->d_bounds, sizeof(int32_t) * nbs));
+        HIP_TRY(hipMalloc(&t->d_radii, sizeof(double) * nbs));
+        HIP_TRY(hipMemcpy(t->d_offL, offL.data(), sizeof(int32_t) * rows, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(t->d_bounds, bounds, sizeof(int32_t) * nbs, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(t->d_radii, radii, sizeof(double) * nbs, hipMemcpyHostToDevice));
+    } catch (...) {
+        vh_ci_table_free(t);
+        throw;
     }
+    return t;
+}
+
+void vh_ci_table_free(vh_ci_table *t) {
+    if (!t) return;
+    (void)hipSetDevice(t->ctx->device);
+    if (t->d_offL) (void)hipFree(t->d_offL);
+    if (t->d_bounds) (void)hipFree(t->d_bounds);
+    if (t->d_radii) (void)hipFree(t->d_radii);
+    delete t;
+}
+
+// results stay on device (d_ci_shell, d_sc); the float64 CI map goes to d_ci (nb*V doubles) when
+// given.  Enqueued on the batch's stream; the caller synchronises.
+void vh_ci_run(vh_batch *b, const vh_ci_table *t, double minvox, double *d_ci) {
+    if (t->R != b->R || t->C != b->C) throw VhError{VH_ERR_ARG, "sphere table built for another (R, C)"};
+    hipStream_t st = b->stream;
+    const int64_t words = (b->V + 31) / 32, rows = t->rows, nbs = t->nbs;
+    // workspace owned by the batch (freed with it): no allocation, and nothing to leak, per call
     if (!b->d_ci_status) {
         HIP_TRY(hipMalloc(&b->d_ci_status, sizeof(int32_t) * b->nb));
         HIP_TRY(hipMalloc(&b->d_ci_count, sizeof(unsigned long long) * b->nb));
     }
-    int32_t *d_offL = b->d_ci_offL, *d_status = b->d_ci_status;
+    int32_t *d_status = b->d_ci_status;
     unsigned long long *d_count = b->d_ci_count;
     if (!b->d_bitmap) {
         HIP_TRY(hipMalloc(&b->d_bitmap, sizeof(uint32_t) * b->nb * words));
@@ -175,22 +239,11 @@ void vh_ci_run(vh_batch *b, const int16_t *offs, const uint8_t *dup, int64_t row
     }
     if (nbs > b->ci_nb_cap) {
         if (b->d_ci_hist) HIP_TRY(hipFree(b->d_ci_hist));
-        if (b->d_ci_bounds) HIP_TRY(hipFree(b->d_ci_bounds));
-        if (b->d_ci_radii) HIP_TRY(hipFree(b->d_ci_radii));
         b->d_ci_hist = nullptr;
-        b->d_ci_bounds = nullptr;
-        b->d_ci_radii = nullptr;
         b->ci_nb_cap = 0;
         HIP_TRY(hipMalloc(&b->d_ci_hist, sizeof(uint32_t) * b->nb * nbs));
-        HIP_TRY(hipMalloc(&b->d_ci_bounds, sizeof(int32_t) * nbs));
-        HIP_TRY(hipMalloc(&b->d_ci_radii, sizeof(double) * nbs));
         b->ci_nb_cap = nbs;
     }
-    int32_t *d_bounds = b->d_ci_bounds;
-    double *d_radii = b->d_ci_radii;
-    HIP_TRY(hipMemcpyAsync(d_offL, offL.data(), sizeof(int32_t) * rows, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(d_bounds, bounds, sizeof(int32_t) * nbs, hipMemcpyHostToDevice, st));
-    HIP_TRY(hipMemcpyAsync(d_radii, radii, sizeof(double) * nbs, hipMemcpyHostToDevice, st));
     HIP_TRY(hipMemsetAsync(d_status, 0, sizeof(int32_t) * b->nb, st));
     HIP_TRY(hipMemsetAsync(d_count, 0, sizeof(unsigned long long) * b->nb, st));
     HIP_TRY(hipMemsetAsync(b->d_bitmap, 0, sizeof(uint32_t) * b->nb * words, st));
@@ -201,23 +254,23 @@ void vh_ci_run(vh_batch *b, const int16_t *offs, const uint8_t *dup, int64_t row
     VH_CHECK_LAUNCH();
     {
         ScopedKTimer tm(b, "ci_walk", 0.0);
-        // one wave per defect voxel: up to V waves per volume, 16 per block, grid-strided beyond
-        // 16384 blocks per volume; the block reads the volume's defect count itself
-        const int64_t wg = std::min<int64_t>((b->V + CIW_TPB / 64 - 1) / (CIW_TPB / 64), 16384);
-        const int use_lds = words <= CIW_LDS_WORDS ? 1 : 0;
-        vh_set_max_lds((const void *)k_ci_walk, 160 * 1024);
+        // one wave per defect voxel, 16 per block; blocks stride over the defect list past 512 per
+        // volume (two per CU), and a block past the volume's defect count exits before staging
+        const int64_t wg = std::min<int64_t>((b->V + CIW_TPB / 64 - 1) / (CIW_TPB / 64), 512);
+        const size_t fixed = sizeof(int32_t) * (CIW_ROWS + CIW_NBS);
+        const int stage_bits = fixed + sizeof(uint32_t) * (size_t)words <= CIW_LDS_MAX ? 1 : 0;
+        vh_set_max_lds((const void *)k_ci_walk, CIW_LDS_MAX);
         k_ci_walk<<<dim3((unsigned)wg, (unsigned)b->nb), CIW_TPB,
-                    use_lds ? sizeof(uint32_t) * (size_t)words : 0, st>>>(
-            b->d_bitmap, b->d_ci_list, d_count, d_offL, rows, d_bounds, nbs, b->R, b->C, b->Z, b->V,
-            words, use_lds, b->d_ci_shell, b->d_ci_hist, d_status);
+                    fixed + (stage_bits ? sizeof(uint32_t) * (size_t)words : 0), st>>>(
+            b->d_bitmap, b->d_ci_list, d_count, t->d_offL, rows, t->d_bounds, nbs, b->R, b->C, b->Z, b->V,
+            words, stage_bits, b->d_ci_shell, b->d_ci_hist, d_status);
         VH_CHECK_LAUNCH();
     }
-    k_ci_finish<<<(unsigned)((b->nb + 63) / 64), 64, 0, st>>>(b->d_ci_hist, d_count, d_radii, nbs,
+    k_ci_finish<<<(unsigned)((b->nb + 63) / 64), 64, 0, st>>>(b->d_ci_hist, d_count, t->d_radii, nbs,
                                                               minvox, b->nb, d_status, b->d_sc);
     VH_CHECK_LAUNCH();
     if (d_ci) {
-        k_ci_scatter<<<vg, VH_TPB, 0, st>>>(b->d_ci_shell, b->d_defect, d_radii, minvox, b->V, d_ci);
+        k_ci_scatter<<<vg, VH_TPB, 0, st>>>(b->d_ci_shell, b->d_defect, t->d_radii, minvox, b->V, d_ci);
         VH_CHECK_LAUNCH();
     }
-    HIP_TRY(hipStreamSynchronize(st));
 }

@@ -1197,17 +1197,23 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
         }
     }
 #ifdef ST_PROF
-    if (t == st_pt && blockIdx.x == 0)
-        printf("ST_PROF den %llu ctrl %llu hist %llu emap %llu fit %llu latP1 %llu eval %llu "
-               "wait %llu level %llu exact %llu top %llu | emap: series %llu fwd %llu filter %llu conv %llu div %llu\n",
-               st_prof[0], st_prof[1], st_prof[2], st_prof[3],
-               st_prof[4], st_prof[5], st_prof[6], st_prof[7], st_prof[8], st_prof[9], st_prof[10],
-               st_prof[11], st_prof[12], st_prof[13], st_prof[14], st_prof[3]);
-#ifdef ST_PROF
-    if (t == st_pt && blockIdx.x == 0)
-        printf("ST_PROF fit: rows %llu push %llu contract %llu items %llu\n", M.fprof[0], M.fprof[1],
-               M.fprof[2], M.fprof[3]);
+    // ST_PROF_ALL: one line per study (per-study phase split against n and the iteration count)
+#ifndef ST_PROF_ALL
+#define ST_PROF_ALL 0
 #endif
+    __syncthreads();
+    if (t == st_pt && (ST_PROF_ALL || blockIdx.x == 0)) {
+        int its = 0;
+        for (int q = 0; q < a.nlev; ++q) its += stb->iters_level[q];
+        printf("ST_PROF b %lld n %lld its %d den %llu ctrl %llu hist %llu emap %llu fit %llu latP1 %llu "
+               "eval %llu wait %llu level %llu exact %llu top %llu | emap: series %llu fwd %llu "
+               "filter %llu conv %llu div %llu | fit: rows %llu push %llu contract %llu items %llu\n",
+               (long long)b, (long long)n, its, st_prof[0], st_prof[1], st_prof[2],
+               st_prof[3] + st_prof[11] + st_prof[12] + st_prof[13] + st_prof[14],
+               st_prof[4], st_prof[5], st_prof[6], st_prof[7], st_prof[8], st_prof[9], st_prof[10],
+               st_prof[11], st_prof[12], st_prof[13], st_prof[14], st_prof[3], M.fprof[0], M.fprof[1],
+               M.fprof[2], M.fprof[3]);
+    }
 #endif
     // final field's P1 for k_n4_final
     const double *P1f = M.cur ? P1b1 : P1b0;

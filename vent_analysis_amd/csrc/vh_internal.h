@@ -4,6 +4,7 @@
 
 #include <cstdint>
 #include <cstdio>
+#include <atomic>
 #include <map>
 #include <set>
 #include <condition_variable>
@@ -142,6 +143,10 @@ struct vh_pipe {
     vh_ctx *ctx = nullptr;
     int64_t R = 0, C = 0, Z = 0, sub = 0;
     std::vector<Slot> slot;
+    // caller pages pinned in place during a run (released at its end), capped at pin_cap bytes
+    // (VH_PIPE_PIN_CAP, default 32 GiB): past the cap a range goes through the pinned staging
+    int64_t pin_cap = 0;
+    std::atomic<int64_t> pinned{0}, pinned_peak{0}, staged_spans{0};
 };
 
 struct vh_batch {
@@ -221,10 +226,6 @@ struct vh_batch {
     int32_t *d_ci_shell = nullptr;   // [nb][V]
     uint32_t *d_ci_hist = nullptr;   // [nb][ci_nb]
     int64_t ci_nb_cap = 0;
-    int32_t *d_ci_offL = nullptr;    // [ci_rows_cap] linear sphere-table offsets
-    int64_t ci_rows_cap = 0;
-    int32_t *d_ci_bounds = nullptr;  // [ci_nb_cap]
-    double *d_ci_radii = nullptr;    // [ci_nb_cap]
     int32_t *d_ci_status = nullptr;  // [nb]
     unsigned long long *d_ci_count = nullptr;   // [nb]
     double *d_ci_map = nullptr;      // [nb][V] float64 CI map (vh_ci)
@@ -237,6 +238,15 @@ struct vh_batch {
     // last run options
     vh_run_opts opts{};
     bool have_result = false;
+};
+
+// a compact sphere table resident in HBM (vh_ci_table_create): linear offsets for one (R, C)
+struct vh_ci_table {
+    vh_ctx *ctx = nullptr;
+    int64_t R = 0, C = 0, rows = 0, nbs = 0;
+    int32_t *d_offL = nullptr;       // [rows] px2vec offsets, CI_SENTINEL for duplicate rows
+    int32_t *d_bounds = nullptr;     // [nbs] shell prefix lengths
+    double *d_radii = nullptr;       // [nbs] r[b - 1]
 };
 
 // ---- timing helper ----------------------------------------------------------------------------
@@ -255,9 +265,10 @@ void vh_launch_snr(vh_batch *b);
 void vh_launch_border(vh_batch *b, const uint8_t *d_in, uint8_t *d_out);
 void vh_launch_n4(vh_batch *b, const vh_n4_params &prm);
 void vh_n4_prepare_tables(vh_batch *b, const vh_n4_params &prm);
-void vh_ci_run(vh_batch *b, const int16_t *offs, const uint8_t *dup, int64_t rows,
-               const int32_t *bounds, const double *radii, int64_t nb_shell, double minvox,
-               double *d_ci);
+vh_ci_table *vh_ci_table_build(vh_ctx *ctx, int64_t R, int64_t C, const int16_t *offs, const uint8_t *dup,
+                               int64_t rows, const int32_t *bounds, const double *radii, int64_t nbs);
+void vh_ci_table_free(vh_ci_table *t);
+void vh_ci_run(vh_batch *b, const vh_ci_table *t, double minvox, double *d_ci);
 void vh_ensure_n4_workspace(vh_batch *b, const vh_n4_params &prm);
 
 // ---- shared host helpers ----------------------------------------------------------------------

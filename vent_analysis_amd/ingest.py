@@ -15,10 +15,11 @@ Restates the reference's loaders (Vent_Analysis.py:169-223) on top of ``vent_ana
 * ``load_study`` / ``load_batch`` -- one study or many into the (B, R, C, Z) float32 / uint8
   arrays ``_lib.Batch.upload`` takes, plus vox and the metadata; files are parsed on a thread pool.
 
-The mask must be binary (0/1, as ``Vent_Analysis._binary_u8`` demands for the class path) and
-non-empty; it is handed to the device as uint8.  Other label values raise ValueError rather than
-silently becoming an empty study (the reference's chain selects mask > 0 at :245 while N4 uses
-MaskLabel 1 -- the two agree only for binary masks, the case the GPU path implements).
+The mask must be binary (0/1) and non-empty; it is handed to the device as uint8.  Other label
+values raise ValueError rather than silently becoming an empty study: the reference's chain
+selects mask > 0 (:245) while N4 uses MaskLabel 1, so a 0/255 mask has no N4 voxels.  The class
+path (``Vent_Analysis._mask_value``) implements that case per study (N4 := identity, maps scaled
+by the mask value); a batch runs one N4 setting for all its studies, so it takes 0/1 masks only.
 """
 from __future__ import annotations
 

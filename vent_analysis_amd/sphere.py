@@ -88,6 +88,17 @@ class SphereTable:
         return int(self.offsets.shape[0])
 
 
+@functools.lru_cache(maxsize=16)
+def _compact_cached(vox_key: tuple, radius: int, shape: tuple) -> SphereTable:
+    return compact_table(_sphere_pix_cached(vox_key, radius), shape)
+
+
+def compact_table_for(vox, radius, shape) -> SphereTable:
+    """compact_table(sphere_pix(vox, radius), shape), built once per (vox, radius, shape): the
+    same object each call, so its device copy (_lib Context.ci_table) is uploaded once."""
+    return _compact_cached(tuple(float(v) for v in vox), int(radius), tuple(int(s) for s in shape))
+
+
 def compact_table(table: np.ndarray, shape) -> SphereTable:
     s0, s1, _ = (int(s) for s in shape)
     offs = table[:, 1:4].astype(np.int64)
