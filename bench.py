@@ -208,7 +208,7 @@ class stdout_to_stderr:
         os.close(self.saved)
 
 
-def host_to_host(R, C, Z, nb, args, device, opts, seed):
+def host_to_host(R, C, Z, nb, args, device, opts, seed, aligned=True):
     """Volumes/s from host memory to host memory: args.h2h_batches x nb studies streamed through
     vh_pipe in sub-batches of args.h2h_sub studies on args.h2h_slots slots (pinned staging, one
     stream each: the H2D, compute and D2H of different sub-batches overlap, and the studies of
@@ -220,10 +220,15 @@ def host_to_host(R, C, Z, nb, args, device, opts, seed):
     from vent_analysis_amd.synth import synth_batch
     slots, sub = args.h2h_slots, min(args.h2h_sub, nb)
     n = max(1, args.h2h_batches) * nb
-    hp, mk = synth_batch(R, C, Z, n, base_seed=seed, unique=BENCH_UNIQUE, vary=True)
+    hp0, mk0 = synth_batch(R, C, Z, n, base_seed=seed, unique=BENCH_UNIQUE, vary=True)
+    # page-aligned host arrays (as ingest.load_batch allocates them): whole chunks DMA in place
+    alloc = _lib.empty_aligned if aligned else (lambda shape, t: np.empty(shape, t))
+    hp, mk = alloc(hp0.shape, np.float32), alloc(mk0.shape, np.uint8)
+    hp[...] = hp0
+    mk[...] = mk0
+    del hp0, mk0
     P = _lib.Pipe(R, C, Z, sub, slots=slots, device=device)
-    out = (np.empty(hp.shape, np.float32), np.empty(hp.shape, np.uint8),
-           np.empty(hp.shape, np.uint8), np.empty(hp.shape, np.uint8))
+    out = tuple(alloc(hp.shape, t) for t in (np.float32, np.uint8, np.uint8, np.uint8))
     P.run(hp[:slots * sub], mk[:slots * sub], opts,
           out=tuple(a[:slots * sub] for a in out))          # warm: every slot's workspaces
     runs = []

@@ -10,12 +10,12 @@ TAG=${1:-h2h}
 timeout -k 10 300 python bench.py --steps 10 --warmup 2 > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err
 rc=$?; echo "bench rc=$rc"; cat gpurun_out/${TAG}_bench.json; [ $rc -eq 0 ] || exit $rc
 for i in 1 2; do
-  for kb in "" "--keep-batch"; do
+  for kb in "" "--unaligned"; do
     timeout -k 10 120 python scripts/h2h_leg.py $kb >> gpurun_out/${TAG}_ab.jsonl 2>> gpurun_out/${TAG}_ab.err
     rc=$?; [ $rc -eq 0 ] || { echo "h2h_leg $kb rc=$rc"; exit $rc; }
   done
 done
-cat gpurun_out/${TAG}_ab.jsonl | python -c "import sys,json; [print(d['keep_batch'], d['vol_s'], d['runs_seconds']) for d in map(json.loads, sys.stdin)]"
+cat gpurun_out/${TAG}_ab.jsonl | python -c "import sys,json; [print('aligned', d['aligned'], d['vol_s'], d['runs_seconds']) for d in map(json.loads, sys.stdin)]"
 VH_PIPE_TRACE=1 timeout -k 10 120 python scripts/h2h_leg.py > gpurun_out/${TAG}_trace.json 2> gpurun_out/${TAG}_pipe_trace.txt
 rc=$?; echo "trace rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats --output-format csv \

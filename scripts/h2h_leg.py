@@ -22,15 +22,17 @@ def main():
     ap.add_argument("--sub", type=int, default=128)
     ap.add_argument("--batches", type=int, default=6)
     ap.add_argument("--keep-batch", action="store_true")
+    ap.add_argument("--unaligned", action="store_true", help="plain np.empty host arrays")
     a = ap.parse_args()
     from vent_analysis_amd import _lib
     R, C, Z, nb = 128, 128, 24, 256
     Bt = _lib.Batch(R, C, Z, nb) if a.keep_batch else None
     opts = _lib.Batch.options(do_n4=True, vox=(1.5, 1.5, 10.0), do_cohort=True, profile=False)
     args = argparse.Namespace(h2h_slots=a.slots, h2h_sub=a.sub, h2h_batches=a.batches)
-    h = bench.host_to_host(R, C, Z, nb, args, 0, opts, 500)
+    h = bench.host_to_host(R, C, Z, nb, args, 0, opts, 500, aligned=not a.unaligned)
     h["vol_s"] = round(h["volumes"] / h["seconds"], 1)
     h["keep_batch"] = a.keep_batch
+    h["aligned"] = not a.unaligned
     print(json.dumps(h), flush=True)
     if Bt:
         Bt.close()

@@ -837,6 +837,32 @@ def test_n4_study_empty_mask_in_batch():
 
 
 # ---- sorted-list statistics on adversarial value distributions ------------------------------------
+def test_mean_anchor_partial_chunk_lengths():
+    """k_chunk_sums: numpy's pairwise tree of the last, partial 8192-chunk of each volume (built
+    level by level in LDS) for masked counts around every leaf / split edge (< 8, 8, 128, 129,
+    130, 255, 256, 1000, 8191, 8192, 8193, 16385, 33000): mean anchor bit-exact to np.mean of the
+    sorted list (oracle mean_f32, pinned to numpy)."""
+    rng = np.random.default_rng(11)
+    shape = (64, 64, 12)
+    counts = [1, 5, 8, 9, 127, 128, 129, 130, 255, 256, 1000, 4097, 8191, 8192, 8193, 16385, 33000,
+              49151]
+    B = _lib.Batch(*shape, len(counts))
+    X = np.zeros((len(counts),) + shape, np.float32)
+    M = np.zeros((len(counts),) + shape, np.uint8)
+    for b, n in enumerate(counts):
+        idx = rng.choice(X[b].size, n, replace=False)
+        M[b].flat[idx] = 1
+        X[b].flat[idx] = (rng.gamma(2.0, 50.0, n) + 1).astype(np.float32)
+    B.upload(X, M)
+    B.run(B.options(do_n4=False, vox=(1.5, 1.5, 10.0)))
+    _, _, _, _, res = B.download(maps=False)
+    B.close()
+    for b, n in enumerate(counts):
+        s_ = np.sort(X[b][M[b] > 0])
+        assert np.float32(res[b].mean_anchor) == O.mean_f32(s_) == np.mean(s_), n
+        assert np.float32(res[b].p99) == s_[int(n * 0.99)], n
+
+
 @pytest.mark.parametrize("kind", ["constant", "two_values", "negative", "ulp_range", "decades"])
 def test_sorted_statistics_adversarial(kind):
     """The per-volume radix sort (k_sort_vol), the numpy-order mean anchor, p99, k-means and the

@@ -123,6 +123,18 @@ def lib():
     return _lib
 
 
+def empty_aligned(shape, dtype, align=4096):
+    """np.empty whose data starts on a page boundary.  vh_pipe DMAs caller arrays in place, chunk
+    by chunk; when every chunk boundary is page aligned (a study is 384 pages at 128x128x24 float32)
+    no chunk needs the sub-page head / tail copies through staging, which run as blit kernels that
+    wait for a free CU behind the N4 kernel."""
+    dtype = np.dtype(dtype)
+    n = int(np.prod(shape)) * dtype.itemsize
+    buf = np.empty(n + align, np.uint8)
+    off = (-buf.ctypes.data) % align
+    return buf[off:off + n].view(dtype).reshape(shape)
+
+
 def _ptr(a):
     return None if a is None else ct.c_void_p(a.ctypes.data)
 
@@ -525,10 +537,10 @@ class Pipe:
         if h.shape[1:] != self.vshape or m.shape != h.shape:
             raise ValueError(f"pipe expects (n,) + {self.vshape}")
         if out is None:
-            out = (np.empty(h.shape, np.float32) if n4 else None,
-                   np.empty(h.shape, np.uint8) if maps else None,
-                   np.empty(h.shape, np.uint8) if maps else None,
-                   np.empty(h.shape, np.uint8) if maps else None)
+            out = (empty_aligned(h.shape, np.float32) if n4 else None,
+                   empty_aligned(h.shape, np.uint8) if maps else None,
+                   empty_aligned(h.shape, np.uint8) if maps else None,
+                   empty_aligned(h.shape, np.uint8) if maps else None)
         res = (VdpResult * n)()
         self.ctx.check(self.L.vh_pipe_run(self.h, _ptr(h), _ptr(m), n, ct.byref(opts),
                                           *[_ptr(a) for a in out], ct.cast(res, ct.c_void_p)),

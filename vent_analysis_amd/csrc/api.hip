@@ -298,8 +298,7 @@ static void pipe_free(vh_pipe *p) {
         if (q.u8) (void)hipHostFree(q.u8);
         if (q.done) (void)hipEventDestroy(q.done);
         if (q.h2d) (void)hipEventDestroy(q.h2d);
-        if (q.sc) (void)hipHostFree(q.sc);
-        if (q.st) (void)hipHostFree(q.st);
+
     }
     delete p;
 }
@@ -770,7 +769,13 @@ int vh_recon(vh_ctx *ctx, const double *k, int64_t n0, int64_t n1, int64_t nz, d
 // (scripts/dev/h2h_probe.py, both directions at once), so the host-to-host rate is link-bound
 // near the device rate; this takes 12 -> 10 bytes per voxel.  The slot's host threads unpack.
 __global__ void k_pack_maps(const uint8_t *__restrict__ d, const uint8_t *__restrict__ b,
-                            const uint8_t *__restrict__ l, uint8_t *__restrict__ out, int64_t n) {
+                            const uint8_t *__restrict__ l, uint8_t *__restrict__ out, int64_t n,
+                            const uint32_t *__restrict__ sc, int64_t sc_words,
+                            const uint32_t *__restrict__ st, int64_t st_words, uint32_t *__restrict__ scal) {
+    // the chunk's scalars and N4 states ahead of the maps (the D2H block's head)
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < sc_words + st_words;
+         i += (int64_t)gridDim.x * blockDim.x)
+        scal[i] = i < sc_words ? sc[i] : st[i - sc_words];
     const int64_t n16 = n / 16;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x) {
         const uint4 vd = reinterpret_cast<const uint4 *>(d)[i], vb = reinterpret_cast<const uint4 *>(b)[i],
@@ -907,14 +912,20 @@ int vh_pipe_create(vh_ctx *ctx, int64_t R, int64_t C, int64_t Z, int64_t sub, in
                 q.b = batch_new(ctx, R, C, Z, sub);
                 HIP_TRY(hipHostMalloc((void **)&q.hp, sizeof(float) * NV));
                 HIP_TRY(hipHostMalloc((void **)&q.n4, sizeof(float) * NV));
-                HIP_TRY(hipHostMalloc((void **)&q.u8, 2 * NV));   // mask in, packed maps out
+                // the chunk's outputs leave the GPU as ONE copy: the per-study scalars and N4 states,
+                // then the packed maps.  Small copies (the scalars were two of ~20 / 11 KiB) run as
+                // blit kernels (__amd_rocclr_copyBuffer), which wait for a CU like any kernel -- for
+                // milliseconds while k_n4_study holds every CU's LDS (r4a trace); one large copy
+                // goes to the SDMA engines.
+                q.scal = (sizeof(VolScalars) * sub + sizeof(N4State) * sub + 4095) / 4096 * 4096;
+                HIP_TRY(hipHostMalloc((void **)&q.u8, 2 * NV + q.scal));   // mask in | scalars + maps out
                 HIP_TRY(hipEventCreateWithFlags(&q.done, hipEventDisableTiming));
                 HIP_TRY(hipEventCreateWithFlags(&q.h2d, hipEventDisableTiming));
-                HIP_TRY(hipMalloc((void **)&q.d_pack, (size_t)NV));
+                HIP_TRY(hipMalloc((void **)&q.d_pack, (size_t)NV + q.scal));
                 q.mb_half = ((size_t)NV / 8 + 1 + 63) / 64 * 64;
                 HIP_TRY(hipHostMalloc((void **)&q.mb, 2 * q.mb_half));
-                HIP_TRY(hipHostMalloc((void **)&q.sc, sizeof(VolScalars) * sub));
-                HIP_TRY(hipHostMalloc((void **)&q.st, sizeof(N4State) * sub));
+                q.sc = reinterpret_cast<VolScalars *>(q.u8 + NV);
+                q.st = reinterpret_cast<N4State *>(q.u8 + NV + sizeof(VolScalars) * sub);
                 q.res.resize(sub);
             }
         } catch (...) {
@@ -1149,7 +1160,8 @@ int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, con
         auto work = [&](int s) {
             vh_pipe::Slot &q = p->slot[s];
             vh_batch *b = q.b;
-            uint8_t *qm = q.u8, *qd = q.u8 + sub * V;   // mask bytes in (fallback), packed maps out
+            // mask bytes in (fallback); the D2H block: scalars / states, then the packed maps
+            uint8_t *qm = q.u8, *qd = q.u8 + sub * V + q.scal;
             auto prep = [&](Chunk &c, int64_t k) {
                 c.k = k;
                 c.v0 = k * sub;
@@ -1204,9 +1216,15 @@ int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, con
                 ticket_pass(c.k);
                 mark_ev(c.mk, 1, b->stream);
                 c.mk.h[2] = now_ms();
-                if (maps) {   // the three maps packed into one byte per voxel (k_pack_maps)
-                    k_pack_maps<<<(unsigned)std::min<int64_t>(4096, ((int64_t)CV / 16 + 255) / 256 + 1), 256, 0,
-                                  b->stream>>>(b->d_defect, b->d_border, b->d_lb, q.d_pack, (int64_t)CV);
+                if (maps || res) {   // scalars + the three maps packed into one byte per voxel
+                    const int64_t cvm = maps ? (int64_t)CV : 0;
+                    const int64_t scw = (int64_t)(sizeof(VolScalars) * sub / 4);
+                    const int64_t stw = opts->do_n4 ? (int64_t)(sizeof(N4State) * sub / 4) : 0;
+                    k_pack_maps<<<(unsigned)std::min<int64_t>(4096, (cvm / 16 + 255) / 256 + 1), 256, 0,
+                                  b->stream>>>(b->d_defect, b->d_border, b->d_lb, q.d_pack + q.scal, cvm,
+                                               reinterpret_cast<const uint32_t *>(b->d_sc), scw,
+                                               reinterpret_cast<const uint32_t *>(b->d_st), stw,
+                                               reinterpret_cast<uint32_t *>(q.d_pack));
                     HIP_TRY(hipGetLastError());
                 }
             };
@@ -1216,12 +1234,9 @@ int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, con
             auto back = [&](Chunk &c) {
                 const float *dn4 = opts->do_n4 ? b->d_n4 : b->d_hp;
                 c.sp[2].d2h((const char *)dn4, (char *)q.n4, b->stream);
-                if (maps) HIP_TRY(hipMemcpyAsync(qd, q.d_pack, c.CV, hipMemcpyDeviceToHost, b->stream));
-                if (res) {   // the scalars ride the same stream into pinned slot memory
-                    HIP_TRY(hipMemcpyAsync(q.sc, b->d_sc, sizeof(VolScalars) * sub, hipMemcpyDeviceToHost, b->stream));
-                    if (opts->do_n4)
-                        HIP_TRY(hipMemcpyAsync(q.st, b->d_st, sizeof(N4State) * sub, hipMemcpyDeviceToHost, b->stream));
-                }
+                if (maps || res)   // one D2H: the scalars / states block, then the packed maps
+                    HIP_TRY(hipMemcpyAsync(q.u8 + sub * V, q.d_pack, q.scal + (maps ? c.CV : 0),
+                                           hipMemcpyDeviceToHost, b->stream));
                 mark_ev(c.mk, 2, b->stream);
                 c.mk.h[3] = now_ms();
             };

@@ -528,186 +528,77 @@ __global__ void __launch_bounds__(VS_TPB) k_sortg_scatter(const uint32_t *__rest
 // =============================================================================================
 // mean anchor (Vent_Analysis.py:246): np.mean of the sorted float32 list is
 //   float32( float64( serial float32 sum over 8192-chunks of numpy pairwise_sum(chunk) ) / n ).
-// One thread per chunk evaluates numpy's pairwise recursion exactly (explicit stack), then one
-// thread per volume adds the chunk sums in order.  p99 (Vent_Analysis.py:255) is the order
+// One wave per chunk evaluates numpy's pairwise recursion exactly (k_chunk_sums: leaves of <= 128
+// values on 8 lanes each, then the tree's left + right combines), then one thread per volume adds
+// the chunk sums in order (pairwise_sum's leaf: 8 stride-8 accumulators combined as
+// ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)), then the n % 8 tail; fewer than 8 values: a plain loop).  p99 (Vent_Analysis.py:255) is the order
 // statistic sorted[int(n * 0.99)].
 // =============================================================================================
-__device__ float pw_leaf(const uint32_t *a, int64_t n) {
-    if (n < 8) {
-        float res = 0.0f;
-        for (int64_t i = 0; i < n; ++i) res = res + key2f(a[i]);
-        return res;
-    }
-    float r0 = key2f(a[0]), r1 = key2f(a[1]), r2 = key2f(a[2]), r3 = key2f(a[3]);
-    float r4 = key2f(a[4]), r5 = key2f(a[5]), r6 = key2f(a[6]), r7 = key2f(a[7]);
-    int64_t i = 8;
-    const int64_t lim = n - (n % 8);
-    for (; i < lim; i += 8) {
-        r0 = r0 + key2f(a[i + 0]); r1 = r1 + key2f(a[i + 1]);
-        r2 = r2 + key2f(a[i + 2]); r3 = r3 + key2f(a[i + 3]);
-        r4 = r4 + key2f(a[i + 4]); r5 = r5 + key2f(a[i + 5]);
-        r6 = r6 + key2f(a[i + 6]); r7 = r7 + key2f(a[i + 7]);
-    }
-    float res = ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7));
-    for (; i < n; ++i) res = res + key2f(a[i]);
-    return res;
-}
-
-__device__ float pw_sum(const uint32_t *a, int64_t n) {
-    // iterative post-order walk of numpy's pairwise_sum recursion (depth <= 8 for n <= 8192)
-    int64_t st_s[12], st_n[12];
-    float st_left[12];
-    int st_stage[12];
-    int sp = 0;
-    st_s[0] = 0; st_n[0] = n; st_stage[0] = 0;
-    for (;;) {
-        if (st_n[sp] <= 128) {
-            float ret = pw_leaf(a + st_s[sp], st_n[sp]);
-            for (;;) {
-                if (sp == 0) return ret;
-                --sp;
-                const int64_t n2 = (st_n[sp] / 2) - ((st_n[sp] / 2) % 8);
-                if (st_stage[sp] == 1) {
-                    st_left[sp] = ret;
-                    st_stage[sp] = 2;
-                    ++sp;
-                    st_s[sp] = st_s[sp - 1] + n2;
-                    st_n[sp] = st_n[sp - 1] - n2;
-                    st_stage[sp] = 0;
-                    break;
-                }
-                ret = st_left[sp] + ret;   // stage 2: left + right
-            }
-        } else {
-            const int64_t n2 = (st_n[sp] / 2) - ((st_n[sp] / 2) % 8);
-            st_stage[sp] = 1;
-            ++sp;
-            st_s[sp] = st_s[sp - 1];
-            st_n[sp] = n2;
-            st_stage[sp] = 0;
-        }
-    }
-}
-
-// One wave per 8192-chunk: the recursion's leaves (blocks of <= 128 values) are enumerated in
-// order by every lane (uniform walk), lane l sums leaf l with pw_leaf, then lane 0 replays the
-// recursion combining the leaf sums in the same left + right order.  Same additions in the same
-// order as pw_sum, so the same float; the leaf sums (the 128-term chains) run in parallel.
 #define PW_MAX_LEAVES 64   // 8192 / 128
-__device__ __forceinline__ int pw_leaves(int64_t n, int want, int64_t &my_s, int64_t &my_n) {
-    int64_t st_s[12], st_n[12];
-    int sp = 0, nl = 0;
-    st_s[0] = 0; st_n[0] = n;
-    my_s = 0; my_n = 0;
-    while (sp >= 0) {   // pre-order with the left child on top: leaves come out in order
-        const int64_t s = st_s[sp], m = st_n[sp];
-        --sp;
-        if (m <= 128) {
-            if (nl == want) { my_s = s; my_n = m; }
-            ++nl;
-        } else {
-            const int64_t n2 = (m / 2) - ((m / 2) % 8);
-            ++sp; st_s[sp] = s + n2; st_n[sp] = m - n2;   // right (popped second)
-            ++sp; st_s[sp] = s; st_n[sp] = n2;            // left
-        }
-    }
-    return nl;
-}
 
-__device__ float pw_combine(int64_t n, const float *leaf) {
-    // pw_sum's post-order walk with leaf values taken in order from leaf[]
-    int64_t st_n[12];
-    float st_left[12];
-    int st_stage[12];
-    int sp = 0, li = 0;
-    st_n[0] = n; st_stage[0] = 0;
-    for (;;) {
-        if (st_n[sp] <= 128) {
-            float ret = leaf[li++];
-            for (;;) {
-                if (sp == 0) return ret;
-                --sp;
-                const int64_t n2 = (st_n[sp] / 2) - ((st_n[sp] / 2) % 8);
-                if (st_stage[sp] == 1) {
-                    st_left[sp] = ret;
-                    st_stage[sp] = 2;
-                    ++sp;
-                    st_n[sp] = st_n[sp - 1] - n2;
-                    st_stage[sp] = 0;
-                    break;
-                }
-                ret = st_left[sp] + ret;
-            }
-        } else {
-            const int64_t n2 = (st_n[sp] / 2) - ((st_n[sp] / 2) % 8);
-            st_stage[sp] = 1;
-            ++sp;
-            st_n[sp] = n2;
-            st_stage[sp] = 0;
-        }
-    }
-}
+// A partial chunk's pairwise tree (numpy's split n2 = n/2 - (n/2) % 8 down to leaves of <= 128)
+// built level by level by the whole wave in LDS (no per-lane stack: a dynamically indexed private
+// array lives in scratch memory, and the one-lane recursion walk plus its replay took ~0.25 ms of a
+// step), the leaves summed 8 lanes each, then the internal nodes combined bottom-up, left + right.
+#define PW_NODES 256   // nodes of one chunk's tree (<= 128 leaves of >= 64 values)
+struct PwTree {
+    int32_t s[PW_NODES], n[PW_NODES], child[PW_NODES];   // child: first child's index, -1 = leaf
+    float sum[PW_NODES];
+    int32_t lvl[14];                                     // level starts (lvl[L] .. lvl[L + 1])
+};
 
-__global__ void __launch_bounds__(VH_TPB) k_chunk_sums(const uint32_t *__restrict__ keys,
-                                                      const VolScalars *sc, int64_t V,
-                                                      int64_t max_chunks, float *chunk) {
-    __shared__ float s_leaf[VH_TPB / 64][PW_MAX_LEAVES];
-    __shared__ int32_t s_ls[VH_TPB / 64][PW_MAX_LEAVES], s_ln[VH_TPB / 64][PW_MAX_LEAVES];
-    const int64_t b = blockIdx.y;
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int64_t c = blockIdx.x * (int64_t)(VH_TPB / 64) + w;
-    const int64_t n = sc[b].n_mask;
-    const int64_t s = c * 8192;
-    if (s >= n) return;   // wave-uniform
-    const int64_t m = n - s < 8192 ? n - s : 8192;
-    const uint32_t *a = keys + b * V + s;
-    // leaves 8 at a time: lane = (leaf, accumulator j) -- pw_leaf's 8 stride-8 accumulators run
-    // on 8 lanes (loads of a leaf row are 8 consecutive keys), then its fixed combine tree by
-    // xor shuffles (a + b == b + a bitwise), then the n % 8 tail adds on the leaf's lane 0
-    int64_t my_s, my_n;
-    const bool full = m == 8192;   // 64 leaves of 128, no recursion walk needed
-    int nl = 64;
-    if (!full) {   // a partial chunk: lane 0 walks the recursion once, listing the leaves in order
-        if (lane == 0) {   // (every lane walking it per group of 8 leaves took 0.9 ms a step)
-            int64_t st_s[12], st_n[12];
-            int sp = 0, k = 0;
-            st_s[0] = 0; st_n[0] = m;
-            while (sp >= 0) {
-                const int64_t s0 = st_s[sp], m0 = st_n[sp];
-                --sp;
-                if (m0 <= 128) {
-                    s_ls[w][k] = (int32_t)s0;
-                    s_ln[w][k] = (int32_t)m0;
-                    ++k;
-                } else {
-                    const int64_t n2 = (m0 / 2) - ((m0 / 2) % 8);
-                    ++sp; st_s[sp] = s0 + n2; st_n[sp] = m0 - n2;
-                    ++sp; st_s[sp] = s0; st_n[sp] = n2;
-                }
-            }
-            s_leaf[w][0] = __int_as_float(k);
-        }
+__device__ float pw_tree_sum(const uint32_t *a, int m, PwTree &T) {
+    const int lane = threadIdx.x & 63;
+    auto wsync = [] {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        nl = __float_as_int(s_leaf[w][0]);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // read before the leaf sums land
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    if (lane == 0) {
+        T.s[0] = 0;
+        T.n[0] = m;
+        T.lvl[0] = 0;
+        T.lvl[1] = 1;
     }
-    for (int g = 0; g * 8 < nl; ++g) {
-        const int leaf = g * 8 + (lane >> 3), j = lane & 7;
-        if (full) { my_s = 128 * leaf; my_n = 128; }
-        else if (leaf < nl) { my_s = s_ls[w][leaf]; my_n = s_ln[w][leaf]; }
-        else { my_s = 0; my_n = 0; }
-        const bool has = leaf < nl;
-        const uint32_t *p = a + my_s;
-        const int64_t ln = has ? my_n : 0;
-        const int64_t lim = ln - ln % 8;
+    wsync();
+    int nlev = 1, total = 1;
+    for (int L = 0; L < 11; ++L) {   // children of level L's nodes become level L + 1
+        const int ls = T.lvl[L], le = T.lvl[L + 1];
+        if (ls == le) break;
+        int next = le;
+        for (int base = ls; base < le; base += 64) {
+            const int i = base + lane;
+            const bool in = i < le;
+            const int nn = in ? T.n[i] : 0;
+            const bool split = in && nn > 128;
+            const uint64_t bal = __ballot(split);
+            const int pos = next + 2 * __popcll(bal & ((1ull << lane) - 1ull));
+            if (in) T.child[i] = split ? pos : -1;
+            if (split) {
+                const int n2 = nn / 2 - (nn / 2) % 8;
+                T.s[pos] = T.s[i];
+                T.n[pos] = n2;
+                T.s[pos + 1] = T.s[i] + n2;
+                T.n[pos + 1] = nn - n2;
+            }
+            next += 2 * __popcll(bal);
+        }
+        if (lane == 0) T.lvl[L + 2] = next;
+        total = next;
+        nlev = L + 2;
+        wsync();
+    }
+    // leaves: 8 lanes each (pw_leaf's 8 stride-8 accumulators), 8 leaves per pass over the nodes
+    for (int g = 0; g * 8 < total; ++g) {
+        const int node = g * 8 + (lane >> 3), j = lane & 7;
+        const bool has = node < total && T.child[node] < 0;
+        const int ln = has ? T.n[node] : 0;
+        const uint32_t *p = a + (has ? T.s[node] : 0);
+        const int lim = ln - ln % 8;
         float v[16];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) {   // all loads first
-            const int64_t i = 8 * q + j;
+        for (int q = 0; q < 16; ++q) {
+            const int i = 8 * q + j;
             v[q] = i < lim ? key2f(p[i]) : 0.0f;
         }
         float r = v[0];
@@ -719,20 +610,64 @@ __global__ void __launch_bounds__(VH_TPB) k_chunk_sums(const uint32_t *__restric
         r = r + __shfl_xor(r, 4, 64);
         if (has && j == 0) {
             float res = ln < 8 ? 0.0f : r;
-            for (int64_t i = lim; i < ln; ++i) res = res + key2f(p[i]);
-            s_leaf[w][leaf] = res;
+            for (int i = lim; i < ln; ++i) res = res + key2f(p[i]);
+            T.sum[node] = res;
         }
+    }
+    wsync();
+    // internal nodes bottom-up: sum = left + right (pairwise_sum's return expression)
+    for (int L = nlev - 2; L >= 0; --L) {
+        for (int i = T.lvl[L] + lane; i < T.lvl[L + 1]; i += 64) {
+            const int c = T.child[i];
+            if (c >= 0) T.sum[i] = T.sum[c] + T.sum[c + 1];
+        }
+        wsync();
+    }
+    return T.sum[0];
+}
+
+__global__ void __launch_bounds__(VH_TPB) k_chunk_sums(const uint32_t *__restrict__ keys,
+                                                      const VolScalars *sc, int64_t V,
+                                                      int64_t max_chunks, float *chunk) {
+    __shared__ float s_leaf[VH_TPB / 64][PW_MAX_LEAVES];
+    __shared__ PwTree s_tree;   // the volume's partial chunk (one per volume, so one per block)
+    const int64_t b = blockIdx.y;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int64_t c = blockIdx.x * (int64_t)(VH_TPB / 64) + w;
+    const int64_t n = sc[b].n_mask;
+    const int64_t s = c * 8192;
+    if (s >= n) return;   // wave-uniform
+    const int64_t m = n - s < 8192 ? n - s : 8192;
+    const uint32_t *a = keys + b * V + s;
+    if (m < 8192) {   // the last chunk of the volume: its own tree
+        const float r = pw_tree_sum(a, (int)m, s_tree);
+        if (lane == 0) chunk[b * max_chunks + c] = r;
+        return;
+    }
+    // full chunk: 64 leaves of 128, 8 at a time: lane = (leaf, accumulator j) -- pw_leaf's 8
+    // stride-8 accumulators run on 8 lanes (loads of a leaf row are 8 consecutive keys), then its
+    // fixed combine tree by xor shuffles (a + b == b + a bitwise)
+    for (int g = 0; g < 8; ++g) {
+        const int leaf = g * 8 + (lane >> 3), j = lane & 7;
+        const uint32_t *p = a + 128 * leaf;
+        float v[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) v[q] = key2f(p[8 * q + j]);
+        float r = v[0];
+#pragma unroll
+        for (int q = 1; q < 16; ++q) r = r + v[q];
+        r = r + __shfl_xor(r, 1, 64);
+        r = r + __shfl_xor(r, 2, 64);
+        r = r + __shfl_xor(r, 4, 64);
+        if (j == 0) s_leaf[w][leaf] = r;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (full) {   // perfect binary tree over the 64 leaves: xor shuffles, same pairs and order
-        float r = s_leaf[w][lane];
-        for (int off = 1; off < 64; off <<= 1) r = r + __shfl_xor(r, off, 64);
-        if (lane == 0) chunk[b * max_chunks + c] = r;
-    } else if (lane == 0) {
-        chunk[b * max_chunks + c] = pw_combine(m, s_leaf[w]);
-    }
+    // perfect binary tree over the 64 leaves: xor shuffles, same pairs and order
+    float r = s_leaf[w][lane];
+    for (int off = 1; off < 64; off <<= 1) r = r + __shfl_xor(r, off, 64);
+    if (lane == 0) chunk[b * max_chunks + c] = r;
 }
 
 __global__ void k_mean_p99(const uint32_t *__restrict__ keys, const float *chunk,

@@ -130,13 +130,14 @@ struct vh_pipe {
     struct Slot {
         vh_batch *b = nullptr;
         float *hp = nullptr, *n4 = nullptr;   // pinned staging [sub][V]
-        uint8_t *u8 = nullptr;                // pinned: mask in, packed maps out ([2][sub][V])
+        uint8_t *u8 = nullptr;                // pinned: mask in [sub][V], then the D2H block (scal + [sub][V])
         hipEvent_t done = nullptr;            // recorded after the slot's current chunk's pipeline
         hipEvent_t h2d = nullptr;             // recorded after the slot's current chunk's H2D
-        uint8_t *d_pack = nullptr;            // device: the chunk's packed maps ([sub][V] bytes)
+        uint8_t *d_pack = nullptr;            // device: the chunk's D2H block: scalars (scal bytes), packed maps
+        size_t scal = 0;                      // bytes of the per-study scalars + N4 states block (4 KiB multiple)
         uint8_t *mb = nullptr;                // pinned: mask bits, two chunks' worth (double buffer)
         size_t mb_half = 0;
-        VolScalars *sc = nullptr;             // pinned per-study scalars / N4 states of the chunk
+        VolScalars *sc = nullptr;             // the chunk's per-study scalars / N4 states: views into u8
         N4State *st = nullptr;
         std::vector<vh_vdp_result> res;
     };

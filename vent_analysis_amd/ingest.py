@@ -148,8 +148,9 @@ def load_batch(studies, workers=8):
     for s in loaded:
         if s.hp.shape != shape:
             raise ValueError(f"load_batch: {s.path} has shape {s.hp.shape}, batch shape {shape}")
-    hp = np.empty((len(loaded),) + shape, np.float32)
-    mk = np.empty((len(loaded),) + shape, np.uint8)
+    from ._lib import empty_aligned   # page-aligned: _lib.Pipe DMAs whole chunks in place
+    hp = empty_aligned((len(loaded),) + shape, np.float32)
+    mk = empty_aligned((len(loaded),) + shape, np.uint8)
     for b, s in enumerate(loaded):
         hp[b] = s.hp
         mk[b] = s.mask
