@@ -438,6 +438,9 @@ def main():
                     help="host-to-host: studies per pipeline sub-batch")
     ap.add_argument("--h2h-slots", type=int, default=4,
                     help="host-to-host: pipeline slots (sub-batches in flight, <= 8)")
+    ap.add_argument("--inflight", type=int, default=1,
+                    help="device batches in flight: steps of consecutive batches overlap on their own "
+                         "streams (a cohort stream); 1 = one batch, synchronised every step")
     ap.add_argument("--h2h-keep-batch", action="store_true",
                     help="A/B: keep the device-resident batch (and its stream) open during the "
                          "host-to-host measurement (round-3 behaviour)")
@@ -479,9 +482,20 @@ def main():
     from vent_analysis_amd import _lib
     from vent_analysis_amd.synth import synth_batch
 
-    hp, mk = synth_batch(R, C, Z, nb, base_seed=shard_seed(rank), unique=BENCH_UNIQUE, vary=True)
-    Bt = _lib.Batch(R, C, Z, nb, device=local)
-    Bt.upload(hp, mk)
+    # --inflight I: I device batches (distinct studies) whose steps are enqueued back to back on
+    # their own streams, so batch i + 1's N4 workgroups take the CUs that batch i's short studies
+    # free (a cohort stream); I = 1 is one batch, synchronised every step
+    ninf = max(1, args.inflight)
+    data, batches = [], []
+    for i in range(ninf):
+        h_, m_ = synth_batch(R, C, Z, nb, base_seed=shard_seed(rank) + BENCH_UNIQUE * i,
+                             unique=BENCH_UNIQUE, vary=True)
+        b_ = _lib.Batch(R, C, Z, nb, device=local)
+        b_.upload(h_, m_)
+        data.append((h_, m_))
+        batches.append(b_)
+    hp, mk = data[0]
+    Bt = batches[0]
     use_comm = world > 1 or args.comm
     with stdout_to_stderr():
         if world > 1:
@@ -498,11 +512,17 @@ def main():
                       n4_subbatch=args.subbatch, conv_threshold=args.conv_threshold,
                       morph3d=args.morph3d, n4_mode=args.n4_mode, conv_mode=args.conv_mode)
 
-    def step(o):
-        Bt.run(o)
+    def step(o, i=0):
+        b_ = batches[i % ninf]
+        b_.run(o)
         if use_comm:
-            Bt.cohort_allreduce()
-        Bt.sync()
+            b_.cohort_allreduce()
+        if ninf == 1:
+            b_.sync()
+
+    def sync_all():
+        for b_ in batches:
+            b_.sync()
 
     try:
         import torch
@@ -514,21 +534,30 @@ def main():
     except Exception:   # torch is plumbing only; the library syncs its own stream
         sync_dev = lambda: None  # noqa: E731
 
-    for _ in range(args.warmup):
-        step(warm)
-    Bt.reset_timers()
+    for i in range(args.warmup):
+        step(warm, i)
+    sync_all()
+    for b_ in batches:
+        b_.reset_timers()
     if dist:
         dist.barrier()
     sync_dev()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(opts)
+    for i in range(args.steps):
+        step(opts, i)
+    sync_all()
     sync_dev()
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
     if dist:
         dt = max_over_ranks(dt, dist)
+    batch_latency_ms = None
+    if ninf > 1:   # one batch alone (untimed above): the latency a single batch sees
+        t1 = time.perf_counter()
+        step(warm, 0)
+        sync_all()
+        batch_latency_ms = round((time.perf_counter() - t1) * 1e3, 3)
 
     _, _, _, _, res = Bt.download(n4=False, maps=False)
     st_us = Bt.study_times()   # per-study wall time of the last step's one-workgroup-per-study N4
@@ -540,13 +569,19 @@ def main():
     used_study = args.n4_mode == "study" or (args.n4_mode == "auto" and nb >= 16)
     kernels = {}
     if not args.no_profile:
+        results = [res] + [b_.download(n4=False, maps=False)[4] for b_ in batches[1:]]
         for name in _lib.lib().vh_batch_kernel_names().decode().split(";"):
-            ms, n, _ = Bt.kernel_time(name)
-            if n:
-                kernels[name] = {"ms_total": ms, "launches": n,
-                                 "alg_bytes": algorithmic_bytes(name, hp, mk, res, R, C, Z,
-                                                                study=used_study,
-                                                                conv_mode=args.conv_mode) * args.steps}
+            tot_ms, tot_n, tot_b = 0.0, 0, 0.0
+            for i, b_ in enumerate(batches):
+                ms, n, _ = b_.kernel_time(name)
+                runs = len(range(i, args.steps, ninf))   # timed steps batch i ran
+                tot_ms += ms
+                tot_n += n
+                if n:
+                    tot_b += algorithmic_bytes(name, data[i][0], data[i][1], results[i], R, C, Z,
+                                               study=used_study, conv_mode=args.conv_mode) * runs
+            if tot_n:
+                kernels[name] = {"ms_total": tot_ms, "launches": tot_n, "alg_bytes": tot_b}
     roof = None
     if kernels:
         dom = max(kernels, key=lambda k: kernels[k]["ms_total"])
@@ -566,9 +601,10 @@ def main():
                                          for n, v in kernels.items()}}
     its = np.array([list(r.n4_iters[:4]) for r in res])
     if not args.h2h_keep_batch:
-        # the device-resident batch (its stream, 1.5 GB of HBM) is done: the pipe's slot streams
-        # then have the GPU_MAX_HW_QUEUES (4) hardware queues to themselves
-        Bt.close()
+        # the device-resident batches (their streams, 1.5 GB of HBM each) are done: the pipe's slot
+        # streams then have the GPU_MAX_HW_QUEUES (4) hardware queues to themselves
+        for b_ in batches:
+            b_.close()
     h2h = None
     if not args.no_h2h:
         if dist:   # every rank streams at once (host memory and PCIe shared as in a cohort run)
@@ -596,19 +632,22 @@ def main():
                                "mean-anchored + linear-binning + k-means VDP + defect border + "
                                "SNR + cohort histogram" + (" (N4 skipped)" if args.no_n4 else ""),
                    "volumes_per_gpu": nb, "shape": [R, C, Z],
-                   "distinct_studies_per_gpu": min(nb, BENCH_UNIQUE), "lung_geometry": "per study",
+                   "distinct_studies_per_gpu": min(nb, BENCH_UNIQUE) * ninf, "lung_geometry": "per study",
                    "parallelism": f"dp{world}", "n4_subbatch": args.subbatch or nb,
+                   "batches_in_flight": ninf,
                    "n4_iterations_mean": float(its.sum(axis=1).mean()) if its.size else 0.0},
         "roofline": roof,
         "cpu_baseline": cpu,
         "n4_study_times": tail,
+        "batch_latency_ms": batch_latency_ms if ninf > 1 else round(dt / args.steps * 1e3, 3),
         "host_to_host_vol_s": round(world * h2h["volumes"] / h2h["seconds"], 2) if h2h else None,
         "host_to_host": h2h,
     }
     if rank == 0:
         print(json.dumps(line), flush=True)
     if args.h2h_keep_batch:
-        Bt.close()
+        for b_ in batches:
+            b_.close()
     if use_comm:
         with stdout_to_stderr():
             _lib.comm_destroy(device=local)

@@ -23,7 +23,12 @@ def main():
     ap.add_argument("--batches", type=int, default=6)
     ap.add_argument("--keep-batch", action="store_true")
     ap.add_argument("--unaligned", action="store_true", help="plain np.empty host arrays")
+    ap.add_argument("--torch", action="store_true", help="initialise torch's HIP context first (as bench.py does)")
     a = ap.parse_args()
+    if a.torch:
+        import torch
+        torch.cuda.set_device(0)
+        torch.cuda.synchronize()
     from vent_analysis_amd import _lib
     R, C, Z, nb = 128, 128, 24, 256
     Bt = _lib.Batch(R, C, Z, nb) if a.keep_batch else None
@@ -33,6 +38,8 @@ def main():
     h["vol_s"] = round(h["volumes"] / h["seconds"], 1)
     h["keep_batch"] = a.keep_batch
     h["aligned"] = not a.unaligned
+    h["torch"] = a.torch
+    h["d2h_late"] = os.environ.get("VH_PIPE_D2H_LATE", "0")
     print(json.dumps(h), flush=True)
     if Bt:
         Bt.close()

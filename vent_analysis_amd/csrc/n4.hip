@@ -1964,6 +1964,16 @@ void vh_launch_n4(vh_batch *b, const vh_n4_params &prm) {
     HIP_TRY(hipMemsetAsync(b->d_lat, 0, sizeof(float) * b->nb * b->lat_cap, st));
     k_n4_state_init<<<(unsigned)((b->nb + 255) / 256), 256, 0, st>>>(b->d_st, b->nb);
     VH_CHECK_LAUNCH();
+    // driver: volume-resident (one workgroup per study) when the batch has studies for the CUs
+    // and a study's state fits in LDS, else per-iteration sweeps over the whole batch
+    int mode = b->n4_mode;
+    if (const char *e = getenv("VH_N4_MODE")) mode = atoi(e);
+    size_t study_lds = 0;
+    const bool fits = vh_n4_study_eligible(b, prm, &study_lds);
+    if (getenv("VH_N4_DEBUG"))
+        fprintf(stderr, "N4 study driver: %s, %zu B LDS\n", fits ? "eligible" : "not eligible", study_lds);
+    if (mode == 2 && !fits) throw VhError{VH_ERR_ARG, "n4_mode=2: study state exceeds the LDS budget"};
+    b->n4_used_study = mode == 2 || (mode == 0 && fits && b->nb >= 16);
     {
         ScopedKTimer tm(b, "n4_init", 0.0);
         k_n4_rowcount<<<dim3((unsigned)ntiles, (unsigned)b->nb), 64, 0, st>>>(
@@ -2001,21 +2011,14 @@ void vh_launch_n4(vh_batch *b, const vh_n4_params &prm) {
             k_n4_rr_apply<<<gr, VH_TPB, 0, st>>>(b->R, ntiles, b->d_rrank, b->d_iscan, nrc);
             VH_CHECK_LAUNCH();
         }
-        const int64_t pairs = ntiles * b->R;
-        k_n4_perm<<<dim3((unsigned)((pairs + VH_TPB / 64 - 1) / (VH_TPB / 64)), (unsigned)b->nb), VH_TPB, 0, st>>>(
-            b->d_rowmask, b->d_rowstart, b->d_rrank, b->R, ntiles, b->VS, b->d_perm);
-        VH_CHECK_LAUNCH();
+        if (!b->n4_used_study) {   // raster rank -> compact index: the sweep driver's S7 walk only
+            // (the study kernel writes d at its raster rank itself; 0.155 ms of the bench step)
+            const int64_t pairs = ntiles * b->R;
+            k_n4_perm<<<dim3((unsigned)((pairs + VH_TPB / 64 - 1) / (VH_TPB / 64)), (unsigned)b->nb), VH_TPB, 0, st>>>(
+                b->d_rowmask, b->d_rowstart, b->d_rrank, b->R, ntiles, b->VS, b->d_perm);
+            VH_CHECK_LAUNCH();
+        }
     }
-    // driver: volume-resident (one workgroup per study) when the batch has studies for the CUs
-    // and a study's state fits in LDS, else per-iteration sweeps over the whole batch
-    int mode = b->n4_mode;
-    if (const char *e = getenv("VH_N4_MODE")) mode = atoi(e);
-    size_t study_lds = 0;
-    const bool fits = vh_n4_study_eligible(b, prm, &study_lds);
-    if (getenv("VH_N4_DEBUG"))
-        fprintf(stderr, "N4 study driver: %s, %zu B LDS\n", fits ? "eligible" : "not eligible", study_lds);
-    if (mode == 2 && !fits) throw VhError{VH_ERR_ARG, "n4_mode=2: study state exceeds the LDS budget"};
-    b->n4_used_study = mode == 2 || (mode == 0 && fits && b->nb >= 16);
     if (!b->n4_used_study) {   // the study kernel computes L0 / U itself
         ScopedKTimer tm(b, "n4_init", 0.0);
         const dim3 sg((unsigned)((ntiles + 3) / 4), (unsigned)((b->R + SEG_R - 1) / SEG_R),

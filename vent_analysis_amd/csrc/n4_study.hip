@@ -1197,21 +1197,19 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
         }
     }
 #ifdef ST_PROF
-    // ST_PROF_ALL: one line per study (per-study phase split against n and the iteration count)
-#ifndef ST_PROF_ALL
-#define ST_PROF_ALL 0
+    // ST_PROF_B: the study whose phase cycles are printed (one study: a printf in every workgroup
+    // made the instrumented kernel ~50x slower)
+#ifndef ST_PROF_B
+#define ST_PROF_B 0
 #endif
-    __syncthreads();
-    if (t == st_pt && (ST_PROF_ALL || blockIdx.x == 0)) {
-        int its = 0;
-        for (int q = 0; q < a.nlev; ++q) its += stb->iters_level[q];
-        printf("ST_PROF b %lld n %lld its %d den %llu ctrl %llu hist %llu emap %llu fit %llu latP1 %llu "
-               "eval %llu wait %llu level %llu exact %llu top %llu | emap: series %llu fwd %llu "
-               "filter %llu conv %llu div %llu | fit: rows %llu push %llu contract %llu items %llu\n",
-               (long long)b, (long long)n, its, st_prof[0], st_prof[1], st_prof[2],
+    if (t == st_pt && blockIdx.x == ST_PROF_B) {
+        printf("ST_PROF b %d n %lld den %llu ctrl %llu hist %llu emap %llu fit %llu latP1 %llu eval %llu "
+               "wait %llu level %llu exact %llu top %llu | emap: series %llu fwd %llu filter %llu conv %llu div %llu\n",
+               ST_PROF_B, (long long)n, st_prof[0], st_prof[1], st_prof[2],
                st_prof[3] + st_prof[11] + st_prof[12] + st_prof[13] + st_prof[14],
                st_prof[4], st_prof[5], st_prof[6], st_prof[7], st_prof[8], st_prof[9], st_prof[10],
-               st_prof[11], st_prof[12], st_prof[13], st_prof[14], st_prof[3], M.fprof[0], M.fprof[1],
+               st_prof[11], st_prof[12], st_prof[13], st_prof[14], st_prof[3]);
+        printf("ST_PROF fit: rows %llu push %llu contract %llu items %llu\n", M.fprof[0], M.fprof[1],
                M.fprof[2], M.fprof[3]);
     }
 #endif

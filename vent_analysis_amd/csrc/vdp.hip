@@ -243,7 +243,9 @@ __global__ void __launch_bounds__(VH_TPB) k_gather(const float *__restrict__ n4,
 // =============================================================================================
 #define VS_TPB 1024
 #define VS_WAVES (VS_TPB / 64)
+#ifndef VS_KPT
 #define VS_KPT 8                       // keys per lane per chunk
+#endif
 #define VS_CHUNK (VS_TPB * VS_KPT)
 
 // peers of this lane's digit among the wave's valid lanes (8 ballots)
@@ -1256,6 +1258,8 @@ void vh_launch_border(vh_batch *b, const uint8_t *d_in, uint8_t *d_out) {
 #define KM_LDS_TILES 4096
 #define KM_SAMPLES 4096   // LDS sample of the sorted values for the boundary searches
 #define KM_TPB 1024
+#define KM_WT 4        // tiles of LDS window per inner cut
+#define KM_WSLOTS 14   // 3 windows of KM_WT tiles, tile 0, the last tile
 
 // wave-cooperative sum of sorted values k[i], i in tile t intersected with [a, e): lane l adds
 // elements t*1024 + j*64 + l for j = 0..15 in order, then a fixed shuffle tree (deterministic)
@@ -1276,15 +1280,16 @@ __device__ __forceinline__ double km_tile_sum(const uint32_t *k, int64_t t, int6
 
 // head and tail partial tiles of a cluster together: both tiles' loads are issued before either
 // reduction (one memory round trip instead of two); same per-tile arithmetic as km_tile_sum
-__device__ __forceinline__ void km_tile_sum2(const uint32_t *k, int64_t t0, int64_t t1, int64_t a,
+template <class KV>
+__device__ __forceinline__ void km_tile_sum2(const KV &kv, int64_t t0, int64_t t1, int64_t a,
                                              int64_t e, double &s0, double &s1) {
     const int lane = threadIdx.x & 63;
     float v0[16], v1[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         const int64_t i0 = t0 * KM_TILE + j * 64 + lane, i1 = t1 * KM_TILE + j * 64 + lane;
-        v0[j] = (i0 >= a && i0 < e) ? key2f(k[i0]) : 0.0f;
-        v1[j] = (i1 >= a && i1 < e) ? key2f(k[i1]) : 0.0f;
+        v0[j] = (i0 >= a && i0 < e) ? kv(i0) : 0.0f;
+        v1[j] = (i1 >= a && i1 < e) ? kv(i1) : 0.0f;
     }
     double acc0 = 0.0, acc1 = 0.0;
 #pragma unroll
@@ -1305,7 +1310,8 @@ __device__ __forceinline__ bool km_closer(double x, double clo, double chi) {
     return fabs(x - chi) < fabs(x - clo);
 }
 
-__device__ __forceinline__ int64_t km_boundary(const uint32_t *k, int64_t n, double clo, double chi,
+template <class KV>
+__device__ __forceinline__ int64_t km_boundary(const KV &kv, int64_t n, double clo, double chi,
                                                const float *samp, int64_t ns, int64_t stride) {
     const int lane = threadIdx.x & 63;
     // sample: first sample index js with the predicate true (ns if none)
@@ -1335,7 +1341,7 @@ __device__ __forceinline__ int64_t km_boundary(const uint32_t *k, int64_t n, dou
     while (hi - lo > 64) {
         const int64_t span = hi - lo;
         const int64_t p = lo + (span * (lane + 1)) / 65;
-        const uint64_t m = __ballot(km_closer((double)key2f(k[p]), clo, chi));
+        const uint64_t m = __ballot(km_closer((double)kv(p), clo, chi));
         if (m == 0ull) {
             lo = lo + (span * 64) / 65 + 1;
         } else {
@@ -1347,7 +1353,7 @@ __device__ __forceinline__ int64_t km_boundary(const uint32_t *k, int64_t n, dou
         }
     }
     const int64_t p = lo + lane;
-    const bool pr = p < hi ? km_closer((double)key2f(k[p]), clo, chi) : true;
+    const bool pr = p < hi ? km_closer((double)kv(p), clo, chi) : true;
     return lo + (__ffsll((long long)__ballot(pr)) - 1);
 }
 
@@ -1380,6 +1386,12 @@ __global__ void __launch_bounds__(KM_TPB) k_kmeans(const uint32_t *__restrict__ 
     __shared__ double s_c[KM_K];
     __shared__ int64_t s_cut[KM_K + 1], s_new[KM_K + 1];
     __shared__ int s_done;
+    // LDS tile cache: tile 0 (slot 12), the last tile (slot 13) and 4 tiles around each inner cut
+    // (slots 4 j .. 4 j + 3 from tile s_wb[j]).  Once the cuts settle, every boundary search and
+    // every partial-tile sum of an iteration reads LDS only (two dependent global round trips per
+    // iteration before: ~8 us of k_kmeans' ~30 iterations per study).
+    __shared__ float s_win[KM_WSLOTS][KM_TILE];
+    __shared__ int64_t s_wb[KM_K - 1];
     const int64_t b = blockIdx.x;
     const int64_t n = sc[b].n_mask;
     if (n <= 0) return;
@@ -1436,11 +1448,27 @@ __global__ void __launch_bounds__(KM_TPB) k_kmeans(const uint32_t *__restrict__ 
     }
     if (t < KM_K) s_c[t] = (double)key2f(k[(n * (2 * t + 1)) / (2 * KM_K)]);
     if (t == 0) { s_cut[0] = -1; s_done = 0; }
+    if (t < KM_K - 1) s_wb[t] = -KM_WT - 1;   // no window yet
+    const int64_t tl = nt - 1;
+    for (int i = t; i < KM_TILE; i += KM_TPB) {   // tile 0 and the last tile, once
+        s_win[12][i] = i < n ? key2f(k[i]) : 0.0f;
+        s_win[13][i] = tl * KM_TILE + i < n ? key2f(k[tl * KM_TILE + i]) : 0.0f;
+    }
     __syncthreads();
+    auto kv = [&](int64_t i) -> float {   // key i from the LDS tile cache, else global memory
+        const int64_t ti = i / KM_TILE;
+        int slot = ti == 0 ? 12 : ti == tl ? 13 : -1;
+#pragma unroll
+        for (int j = 0; j < KM_K - 1; ++j) {
+            const int64_t d = ti - s_wb[j];
+            if (d >= 0 && d < KM_WT) slot = 4 * j + (int)d;
+        }
+        return slot >= 0 ? s_win[slot][i - ti * KM_TILE] : key2f(k[i]);
+    };
     int it = 0;
     for (it = 1; it <= 300; ++it) {
         if (w < KM_K - 1) {
-            const int64_t c = km_boundary(k, n, s_c[w], s_c[w + 1], s_samp, ns, stride);
+            const int64_t c = km_boundary(kv, n, s_c[w], s_c[w + 1], s_samp, ns, stride);
             if (lane == 0) s_new[w + 1] = c;
         }
         __syncthreads();
@@ -1456,12 +1484,41 @@ __global__ void __launch_bounds__(KM_TPB) k_kmeans(const uint32_t *__restrict__ 
         }
         __syncthreads();
         if (s_done) break;
+        {   // windows: tiles base .. base + 3 around each inner cut (base = tile of the cut - 1),
+            // reloaded only when a cut leaves its window's middle two tiles
+            bool moved = false;
+#pragma unroll
+            for (int j = 0; j < KM_K - 1; ++j) {
+                const int64_t ct = s_cut[j + 1] / KM_TILE;
+                moved |= ct - s_wb[j] < 1 || ct - s_wb[j] > 2;
+            }
+            if (moved) {   // block-uniform
+                int64_t nb_[KM_K - 1];
+#pragma unroll
+                for (int j = 0; j < KM_K - 1; ++j) {
+                    const int64_t ct = s_cut[j + 1] / KM_TILE;
+                    nb_[j] = (ct - s_wb[j] < 1 || ct - s_wb[j] > 2) ? ct - 1 : s_wb[j];
+                }
+                __syncthreads();   // every reader of the old bases is past them
+#pragma unroll
+                for (int j = 0; j < KM_K - 1; ++j) {
+                    if (nb_[j] == s_wb[j]) continue;
+                    for (int i = t; i < KM_WT * KM_TILE; i += KM_TPB) {
+                        const int64_t g = nb_[j] * KM_TILE + i;
+                        s_win[4 * j + i / KM_TILE][i % KM_TILE] = (g >= 0 && g < n) ? key2f(k[g]) : 0.0f;
+                    }
+                }
+                __syncthreads();
+                if (t < KM_K - 1) s_wb[t] = nb_[t];
+                __syncthreads();
+            }
+        }
         if (w < KM_K) {   // wave w updates centre w: head + whole tiles (prefix) + tail
             const int64_t a = s_cut[w], e = s_cut[w + 1];
             if (e > a) {
                 const int64_t ta = a / KM_TILE, te = (e - 1) / KM_TILE;
                 double head, tail;
-                km_tile_sum2(k, ta, te, a, e, head, tail);
+                km_tile_sum2(kv, ta, te, a, e, head, tail);
                 if (lane == 0) {
                     double sum = head;
                     if (te > ta + 1) sum += in_lds ? s_tiles[te] - s_tiles[ta + 1] : gt[te] - gt[ta + 1];
