@@ -438,7 +438,7 @@ def main():
                     help="host-to-host: studies per pipeline sub-batch")
     ap.add_argument("--h2h-slots", type=int, default=4,
                     help="host-to-host: pipeline slots (sub-batches in flight, <= 8)")
-    ap.add_argument("--inflight", type=int, default=1,
+    ap.add_argument("--inflight", type=int, default=2,
                     help="device batches in flight: steps of consecutive batches overlap on their own "
                          "streams (a cohort stream); 1 = one batch, synchronised every step")
     ap.add_argument("--h2h-keep-batch", action="store_true",
@@ -552,13 +552,6 @@ def main():
     dt = time.perf_counter() - t0
     if dist:
         dt = max_over_ranks(dt, dist)
-    batch_latency_ms = None
-    if ninf > 1:   # one batch alone (untimed above): the latency a single batch sees
-        t1 = time.perf_counter()
-        step(warm, 0)
-        sync_all()
-        batch_latency_ms = round((time.perf_counter() - t1) * 1e3, 3)
-
     _, _, _, _, res = Bt.download(n4=False, maps=False)
     st_us = Bt.study_times()   # per-study wall time of the last step's one-workgroup-per-study N4
     tail = None
@@ -599,6 +592,31 @@ def main():
                                                           key=lambda kv: -kv[1]["ms_total"])},
                 "kernel_us_per_launch": {n: round(v["ms_total"] / v["launches"] * 1e3, 2)
                                          for n, v in kernels.items()}}
+    batch_latency_ms = None
+    iso_kernels = {}
+    if ninf > 1:   # one batch alone (untimed above): the latency a single batch sees, and its
+        # kernels' launch durations without another batch's workgroups on the CUs
+        Bt.reset_timers()
+        t1 = time.perf_counter()
+        step(opts, 0)
+        sync_all()
+        batch_latency_ms = round((time.perf_counter() - t1) * 1e3, 3)
+        if not args.no_profile:
+            for name in _lib.lib().vh_batch_kernel_names().decode().split(";"):
+                ms, n, _ = Bt.kernel_time(name)
+                if n:
+                    iso_kernels[name] = ms / n
+
+    if roof and iso_kernels.get(roof["kernel"]):
+        # the same launch class alone on the GPU: its duration without the other batch's workgroups
+        iso_us = iso_kernels[roof["kernel"]] * 1e3
+        b0 = algorithmic_bytes(roof["kernel"], hp, mk, res, R, C, Z, study=used_study,
+                               conv_mode=args.conv_mode)   # batch 0's bytes per launch
+        ach_iso = b0 / (iso_us * 1e-6) / 1e9
+        roof["isolated"] = {"avg_launch_us": round(iso_us, 2), "achieved": round(ach_iso, 1),
+                            "frac": round(ach_iso / HBM_PEAK_GBS, 4),
+                            "note": "one batch alone (batch_latency run): no other batch's "
+                                    "workgroups on the CUs"}
     its = np.array([list(r.n4_iters[:4]) for r in res])
     if not args.h2h_keep_batch:
         # the device-resident batches (their streams, 1.5 GB of HBM each) are done: the pipe's slot

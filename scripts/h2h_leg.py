@@ -24,14 +24,31 @@ def main():
     ap.add_argument("--keep-batch", action="store_true")
     ap.add_argument("--unaligned", action="store_true", help="plain np.empty host arrays")
     ap.add_argument("--torch", action="store_true", help="initialise torch's HIP context first (as bench.py does)")
+    ap.add_argument("--warm-device", type=int, default=0,
+                    help="run this many 256-study device-resident steps first (as bench.py does)")
+    ap.add_argument("--cpu-load", type=float, default=0.0,
+                    help="run bench.py's CPU baseline for this many seconds first")
     a = ap.parse_args()
+    if a.cpu_load > 0:
+        bench.cpu_baseline(128, 128, 24, seconds=a.cpu_load)
     if a.torch:
         import torch
         torch.cuda.set_device(0)
         torch.cuda.synchronize()
     from vent_analysis_amd import _lib
     R, C, Z, nb = 128, 128, 24, 256
-    Bt = _lib.Batch(R, C, Z, nb) if a.keep_batch else None
+    Bt = _lib.Batch(R, C, Z, nb) if (a.keep_batch or a.warm_device) else None
+    if a.warm_device:
+        from vent_analysis_amd.synth import synth_batch
+        hw, mw = synth_batch(R, C, Z, nb, base_seed=0, unique=64, vary=True)
+        Bt.upload(hw, mw)
+        o = _lib.Batch.options(do_n4=True, vox=(1.5, 1.5, 10.0), do_cohort=True)
+        for _ in range(a.warm_device):
+            Bt.run(o)
+        Bt.sync()
+        if not a.keep_batch:
+            Bt.close()
+            Bt = None
     opts = _lib.Batch.options(do_n4=True, vox=(1.5, 1.5, 10.0), do_cohort=True, profile=False)
     args = argparse.Namespace(h2h_slots=a.slots, h2h_sub=a.sub, h2h_batches=a.batches)
     h = bench.host_to_host(R, C, Z, nb, args, 0, opts, 500, aligned=not a.unaligned)
@@ -39,6 +56,8 @@ def main():
     h["keep_batch"] = a.keep_batch
     h["aligned"] = not a.unaligned
     h["torch"] = a.torch
+    h["warm_device"] = a.warm_device
+    h["cpu_load"] = a.cpu_load
     h["d2h_late"] = os.environ.get("VH_PIPE_D2H_LATE", "0")
     print(json.dumps(h), flush=True)
     if Bt:

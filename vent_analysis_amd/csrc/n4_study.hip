@@ -99,6 +99,7 @@ struct StudyArgs {
     const uint64_t *rmask;
     const int32_t *rrs;
     const VolScalars *sc;
+    const int32_t *order;   // workgroup -> study (largest first; null: identity)
     N4State *st;
     double *P1out;
     int64_t q2cap;
@@ -617,7 +618,7 @@ __device__ __forceinline__ int next_item(StudyMisc &M, const int32_t *ordr, int 
 // ---------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int64_t b = a.vol0 + blockIdx.x;
+    const int64_t b = a.vol0 + (a.order ? a.order[blockIdx.x] : (int32_t)blockIdx.x);
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     StudyMisc &M = *reinterpret_cast<StudyMisc *>(smem + a.o_misc);
     float *sE = reinterpret_cast<float *>(smem + a.o_E);
@@ -1202,7 +1203,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
 #ifndef ST_PROF_B
 #define ST_PROF_B 0
 #endif
-    if (t == st_pt && blockIdx.x == ST_PROF_B) {
+    if (t == st_pt && b == ST_PROF_B) {
         printf("ST_PROF b %d n %lld den %llu ctrl %llu hist %llu emap %llu fit %llu latP1 %llu eval %llu "
                "wait %llu level %llu exact %llu top %llu | emap: series %llu fwd %llu filter %llu conv %llu div %llu\n",
                ST_PROF_B, (long long)n, st_prof[0], st_prof[1], st_prof[2],
@@ -1220,6 +1221,22 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
         stb->conv = M.conv;
         stb->active = M.wd ? -2 : 0;
         stb->t_end = wall_clock64();
+    }
+}
+
+// Workgroup -> study, the largest study (most mask == 1 voxels, the best a-priori proxy of its
+// cost) first, ties by index: the dispatcher starts workgroups in order, so when the CUs are
+// shared with another batch's launch (batches in flight) the long studies start first and the
+// launch's tail is its short studies.  One workgroup, rank by counting (nb <= 4096).
+__global__ void __launch_bounds__(1024) k_study_order(const VolScalars *sc, int64_t nb, int32_t *order) {
+    for (int64_t i = threadIdx.x; i < nb; i += blockDim.x) {
+        const int64_t ni = sc[i].n_mask1;
+        int32_t r = 0;
+        for (int64_t j = 0; j < nb; ++j) {
+            const int64_t nj = sc[j].n_mask1;
+            r += (nj > ni) || (nj == ni && j < i);
+        }
+        order[r] = (int32_t)i;
     }
 }
 
@@ -1352,6 +1369,13 @@ void vh_launch_n4_study(vh_batch *b, const vh_n4_params &prm) {
                            b->stream));
     a.lvs = (const StudyLevels *)b->d_study_lv;
     a.vol0 = 0;
+    a.order = nullptr;
+    if (b->nb > 1 && b->nb <= 4096) {
+        if (!b->d_study_order) HIP_TRY(hipMalloc(&b->d_study_order, sizeof(int32_t) * b->nb));
+        k_study_order<<<1, 1024, 0, b->stream>>>(b->d_sc, b->nb, b->d_study_order);
+        VH_CHECK_LAUNCH();
+        a.order = b->d_study_order;
+    }
     a.latg = nullptr;
     if (prm.conv_mode == 0 && ST_SPLIT && ST_DEPTH == 2) {   // the two lattice saves per study
         const size_t need = sizeof(float) * 2 * (size_t)a.lat_cap * (size_t)b->nb;

@@ -237,14 +237,14 @@ __global__ void __launch_bounds__(VH_TPB) k_gather(const float *__restrict__ n4,
 // Stable LSD radix sort (4 x 8-bit digits) of each volume's masked keys, ONE workgroup (1024
 // threads) per volume: a volume's keys
 // (~330 KB at 128x128x24) stay in L2 / MALL, the four digit histograms come from one read pass
-// (digit counts do not depend on order), and each pass ranks chunks of 8192 keys in order
+// (digit counts do not depend on order), and each pass ranks chunks of VS_CHUNK keys in order
 // (wave ballots within a wave, wave prefixes per digit across waves, running digit offsets
 // across chunks) -- one launch for the whole sort instead of 12, all volumes in parallel.
 // =============================================================================================
 #define VS_TPB 1024
 #define VS_WAVES (VS_TPB / 64)
 #ifndef VS_KPT
-#define VS_KPT 8                       // keys per lane per chunk
+#define VS_KPT 16   // keys per lane per chunk (8: 0.51 ms per bench step, 16: 0.47, r4c)
 #endif
 #define VS_CHUNK (VS_TPB * VS_KPT)
 
@@ -321,7 +321,7 @@ __global__ void __launch_bounds__(VS_TPB) k_sort_vol(uint32_t *__restrict__ k0,
                 key[r] = idx < n ? kin[idx] : 0u;
             }
 #pragma unroll
-            for (int r = 0; r < VS_KPT; ++r) {   // wave w owns keys [c0 + w*512, c0 + (w+1)*512)
+            for (int r = 0; r < VS_KPT; ++r) {   // wave w owns keys [c0 + 64 VS_KPT w, c0 + 64 VS_KPT (w + 1))
                 const int64_t idx = c0 + (int64_t)w * (VS_KPT * 64) + r * 64 + lane;
                 const bool valid = idx < n;
                 const uint32_t kk = key[r];
@@ -389,11 +389,11 @@ __global__ void __launch_bounds__(VS_TPB) k_sort_vol(uint32_t *__restrict__ k0,
 
 // ---------------------------------------------------------------------------------------------
 // The same stable LSD sort over the whole GPU for ONE large volume (config 5: ~28 M keys, where the
-// one-workgroup sort took 118 ms).  Per 8-bit pass: k_sortg_count (one workgroup per 8192-key chunk:
+// one-workgroup sort took 118 ms).  Per 8-bit pass: k_sortg_count (one workgroup per VS_CHUNK-key chunk:
 // the chunk's digit counts), k_sortg_offsets (one workgroup: per digit, the exclusive prefix over
 // chunks in chunk order plus the digit's base), k_sortg_scatter (one workgroup per chunk: the
 // chunk ranked exactly as k_sort_vol ranks it, written at its chunk's digit offsets).  Chunk c of
-// every pass holds keys [8192 c, 8192 (c + 1)), so the order of equal digits is the input order:
+// every pass holds keys [VS_CHUNK c, VS_CHUNK (c + 1)), so the order of equal digits is the input order:
 // stable, and the result is the same array k_sort_vol produces.
 // ---------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(VS_TPB) k_sortg_count(const uint32_t *__restrict__ kin,
@@ -474,7 +474,7 @@ __global__ void __launch_bounds__(VS_TPB) k_sortg_scatter(const uint32_t *__rest
         key[r] = idx < n ? kin[idx] : 0u;
     }
 #pragma unroll
-    for (int r = 0; r < VS_KPT; ++r) {   // as k_sort_vol: wave w owns keys [c0 + 512 w, c0 + 512 (w + 1))
+    for (int r = 0; r < VS_KPT; ++r) {   // as k_sort_vol: wave w owns keys [c0 + 64 VS_KPT w, c0 + 64 VS_KPT (w + 1))
         const int64_t idx = c0 + (int64_t)w * (VS_KPT * 64) + r * 64 + lane;
         const bool valid = idx < n;
         const uint32_t kk = key[r];
@@ -1258,8 +1258,6 @@ void vh_launch_border(vh_batch *b, const uint8_t *d_in, uint8_t *d_out) {
 #define KM_LDS_TILES 4096
 #define KM_SAMPLES 4096   // LDS sample of the sorted values for the boundary searches
 #define KM_TPB 1024
-#define KM_WT 4        // tiles of LDS window per inner cut
-#define KM_WSLOTS 14   // 3 windows of KM_WT tiles, tile 0, the last tile
 
 // wave-cooperative sum of sorted values k[i], i in tile t intersected with [a, e): lane l adds
 // elements t*1024 + j*64 + l for j = 0..15 in order, then a fixed shuffle tree (deterministic)
@@ -1280,16 +1278,15 @@ __device__ __forceinline__ double km_tile_sum(const uint32_t *k, int64_t t, int6
 
 // head and tail partial tiles of a cluster together: both tiles' loads are issued before either
 // reduction (one memory round trip instead of two); same per-tile arithmetic as km_tile_sum
-template <class KV>
-__device__ __forceinline__ void km_tile_sum2(const KV &kv, int64_t t0, int64_t t1, int64_t a,
+__device__ __forceinline__ void km_tile_sum2(const uint32_t *k, int64_t t0, int64_t t1, int64_t a,
                                              int64_t e, double &s0, double &s1) {
     const int lane = threadIdx.x & 63;
     float v0[16], v1[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         const int64_t i0 = t0 * KM_TILE + j * 64 + lane, i1 = t1 * KM_TILE + j * 64 + lane;
-        v0[j] = (i0 >= a && i0 < e) ? kv(i0) : 0.0f;
-        v1[j] = (i1 >= a && i1 < e) ? kv(i1) : 0.0f;
+        v0[j] = (i0 >= a && i0 < e) ? key2f(k[i0]) : 0.0f;
+        v1[j] = (i1 >= a && i1 < e) ? key2f(k[i1]) : 0.0f;
     }
     double acc0 = 0.0, acc1 = 0.0;
 #pragma unroll
@@ -1310,8 +1307,7 @@ __device__ __forceinline__ bool km_closer(double x, double clo, double chi) {
     return fabs(x - chi) < fabs(x - clo);
 }
 
-template <class KV>
-__device__ __forceinline__ int64_t km_boundary(const KV &kv, int64_t n, double clo, double chi,
+__device__ __forceinline__ int64_t km_boundary(const uint32_t *k, int64_t n, double clo, double chi,
                                                const float *samp, int64_t ns, int64_t stride) {
     const int lane = threadIdx.x & 63;
     // sample: first sample index js with the predicate true (ns if none)
@@ -1341,7 +1337,7 @@ __device__ __forceinline__ int64_t km_boundary(const KV &kv, int64_t n, double c
     while (hi - lo > 64) {
         const int64_t span = hi - lo;
         const int64_t p = lo + (span * (lane + 1)) / 65;
-        const uint64_t m = __ballot(km_closer((double)kv(p), clo, chi));
+        const uint64_t m = __ballot(km_closer((double)key2f(k[p]), clo, chi));
         if (m == 0ull) {
             lo = lo + (span * 64) / 65 + 1;
         } else {
@@ -1353,7 +1349,7 @@ __device__ __forceinline__ int64_t km_boundary(const KV &kv, int64_t n, double c
         }
     }
     const int64_t p = lo + lane;
-    const bool pr = p < hi ? km_closer((double)kv(p), clo, chi) : true;
+    const bool pr = p < hi ? km_closer((double)key2f(k[p]), clo, chi) : true;
     return lo + (__ffsll((long long)__ballot(pr)) - 1);
 }
 
@@ -1386,12 +1382,6 @@ __global__ void __launch_bounds__(KM_TPB) k_kmeans(const uint32_t *__restrict__ 
     __shared__ double s_c[KM_K];
     __shared__ int64_t s_cut[KM_K + 1], s_new[KM_K + 1];
     __shared__ int s_done;
-    // LDS tile cache: tile 0 (slot 12), the last tile (slot 13) and 4 tiles around each inner cut
-    // (slots 4 j .. 4 j + 3 from tile s_wb[j]).  Once the cuts settle, every boundary search and
-    // every partial-tile sum of an iteration reads LDS only (two dependent global round trips per
-    // iteration before: ~8 us of k_kmeans' ~30 iterations per study).
-    __shared__ float s_win[KM_WSLOTS][KM_TILE];
-    __shared__ int64_t s_wb[KM_K - 1];
     const int64_t b = blockIdx.x;
     const int64_t n = sc[b].n_mask;
     if (n <= 0) return;
@@ -1448,27 +1438,11 @@ __global__ void __launch_bounds__(KM_TPB) k_kmeans(const uint32_t *__restrict__ 
     }
     if (t < KM_K) s_c[t] = (double)key2f(k[(n * (2 * t + 1)) / (2 * KM_K)]);
     if (t == 0) { s_cut[0] = -1; s_done = 0; }
-    if (t < KM_K - 1) s_wb[t] = -KM_WT - 1;   // no window yet
-    const int64_t tl = nt - 1;
-    for (int i = t; i < KM_TILE; i += KM_TPB) {   // tile 0 and the last tile, once
-        s_win[12][i] = i < n ? key2f(k[i]) : 0.0f;
-        s_win[13][i] = tl * KM_TILE + i < n ? key2f(k[tl * KM_TILE + i]) : 0.0f;
-    }
     __syncthreads();
-    auto kv = [&](int64_t i) -> float {   // key i from the LDS tile cache, else global memory
-        const int64_t ti = i / KM_TILE;
-        int slot = ti == 0 ? 12 : ti == tl ? 13 : -1;
-#pragma unroll
-        for (int j = 0; j < KM_K - 1; ++j) {
-            const int64_t d = ti - s_wb[j];
-            if (d >= 0 && d < KM_WT) slot = 4 * j + (int)d;
-        }
-        return slot >= 0 ? s_win[slot][i - ti * KM_TILE] : key2f(k[i]);
-    };
     int it = 0;
     for (it = 1; it <= 300; ++it) {
         if (w < KM_K - 1) {
-            const int64_t c = km_boundary(kv, n, s_c[w], s_c[w + 1], s_samp, ns, stride);
+            const int64_t c = km_boundary(k, n, s_c[w], s_c[w + 1], s_samp, ns, stride);
             if (lane == 0) s_new[w + 1] = c;
         }
         __syncthreads();
@@ -1484,41 +1458,12 @@ __global__ void __launch_bounds__(KM_TPB) k_kmeans(const uint32_t *__restrict__ 
         }
         __syncthreads();
         if (s_done) break;
-        {   // windows: tiles base .. base + 3 around each inner cut (base = tile of the cut - 1),
-            // reloaded only when a cut leaves its window's middle two tiles
-            bool moved = false;
-#pragma unroll
-            for (int j = 0; j < KM_K - 1; ++j) {
-                const int64_t ct = s_cut[j + 1] / KM_TILE;
-                moved |= ct - s_wb[j] < 1 || ct - s_wb[j] > 2;
-            }
-            if (moved) {   // block-uniform
-                int64_t nb_[KM_K - 1];
-#pragma unroll
-                for (int j = 0; j < KM_K - 1; ++j) {
-                    const int64_t ct = s_cut[j + 1] / KM_TILE;
-                    nb_[j] = (ct - s_wb[j] < 1 || ct - s_wb[j] > 2) ? ct - 1 : s_wb[j];
-                }
-                __syncthreads();   // every reader of the old bases is past them
-#pragma unroll
-                for (int j = 0; j < KM_K - 1; ++j) {
-                    if (nb_[j] == s_wb[j]) continue;
-                    for (int i = t; i < KM_WT * KM_TILE; i += KM_TPB) {
-                        const int64_t g = nb_[j] * KM_TILE + i;
-                        s_win[4 * j + i / KM_TILE][i % KM_TILE] = (g >= 0 && g < n) ? key2f(k[g]) : 0.0f;
-                    }
-                }
-                __syncthreads();
-                if (t < KM_K - 1) s_wb[t] = nb_[t];
-                __syncthreads();
-            }
-        }
         if (w < KM_K) {   // wave w updates centre w: head + whole tiles (prefix) + tail
             const int64_t a = s_cut[w], e = s_cut[w + 1];
             if (e > a) {
                 const int64_t ta = a / KM_TILE, te = (e - 1) / KM_TILE;
                 double head, tail;
-                km_tile_sum2(kv, ta, te, a, e, head, tail);
+                km_tile_sum2(k, ta, te, a, e, head, tail);
                 if (lane == 0) {
                     double sum = head;
                     if (te > ta + 1) sum += in_lds ? s_tiles[te] - s_tiles[ta + 1] : gt[te] - gt[ta + 1];

@@ -215,6 +215,7 @@ struct vh_batch {
     bool tabs_valid = false;
     double2 *d_twiddle = nullptr;    // FFT twiddles (host-computed)
     void *d_study_lv = nullptr;      // n4_study.hip: per-level table pointers + iteration caps
+    int32_t *d_study_order = nullptr;   // n4_study.hip: workgroup -> study, largest study first
     void *d_pcg = nullptr;           // n4.hip k_n4_pcg: per-block guesses / ends / sums, aggregates
     void *d_study_latg = nullptr;    // n4_study.hip depth 2: the lattice before the last two updates
     size_t study_latg_cap = 0;
