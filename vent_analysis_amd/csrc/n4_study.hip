@@ -132,6 +132,7 @@ struct StudyMisc {
     float bin_min, slope, bmax, pad;
 #ifdef ST_PROF
     unsigned long long fprof[4];   // wave of thread st_pt: fit rows / push / contract / items
+    unsigned long long sprof[4];   // emap series of thread 300 (h in range): total, hist sums, kernel exp, twiddle
 #endif
     double sd, sd2, conv;
     int32_t nc[2][3];
@@ -746,6 +747,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
 #ifdef ST_PROF
     unsigned long long st_prof[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_t0 = clock64();
     if (t == 0) M.fprof[0] = M.fprof[1] = M.fprof[2] = M.fprof[3] = 0ull;
+    if (t == 0) M.sprof[0] = M.sprof[1] = M.sprof[2] = M.sprof[3] = 0ull;
 #endif
     int ch_seen = 0;   // chain waves: the last request taken
     for (int L = 0; L < a.nlev; ++L) {
@@ -953,6 +955,9 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                     const float ef = (float)(4.0 * LN2 / (double)(sFWHM * sFWHM));
                     const float sf = (float)(2.0 * sqrt(LN2 / PI_D) / (double)sFWHM);
                     // one twiddle per thread: P / 2 <= g.n (ST_TPB - 64 ST_CW)
+#ifdef ST_PROF
+                    const unsigned long long sp0 = clock64();
+#endif
                     const double2 twv = g.t < P / 2 ? a.tw[g.t] : make_double2(0.0, 0.0);   // in flight
                     for (int i = g.t; i < P; i += g.n) {   // histogram series and Gaussian kernel
                         const int h = i - off;
@@ -964,6 +969,10 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                                 if (h > 0) s += hist_osum(Hc[q * VH_MAX_BINS + h - 1]);
                             }
                         V[fpad(i)] = make_double2((double)s * (1.0 / 16777216.0), 0.0);
+#ifdef ST_PROF
+                        const unsigned long long sp1 = clock64();
+                        if (g.t == 300) M.sprof[1] += sp1 - sp0;
+#endif
                         double fx;
                         if (i == 0) {
                             fx = (double)sf;
@@ -974,8 +983,18 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                             fx = (double)(sf * expf_cr(-(nf * nf) * ef));
                         }
                         F[fpad(i)] = make_double2(fx, 0.0);
+#ifdef ST_PROF
+                        if (g.t == 300) M.sprof[2] += clock64() - sp1;
+#endif
                     }
+#ifdef ST_PROF
+                    const unsigned long long sp2 = clock64();
+#endif
                     if (g.t < P / 2) TW[g.t] = twv;
+#ifdef ST_PROF
+                    if (g.t == 300) M.sprof[0] += clock64() - sp0;
+                    if (g.t == 200) M.sprof[3] += clock64() - sp2;
+#endif
                     gsync(g, M);
                     ST_MARK(11);
                     if (g.w < 2) wave_fft_lds(g.w ? F : V, TW, false, FftId(), FftId());
@@ -1204,14 +1223,17 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
 #define ST_PROF_B 0
 #endif
     if (t == st_pt && b == ST_PROF_B) {
-        printf("ST_PROF b %d n %lld den %llu ctrl %llu hist %llu emap %llu fit %llu latP1 %llu eval %llu "
+        int its = 0;   // (st_pt is thread 0, the writer of iters_level, when no chain waves split off)
+        for (int q = 0; q < a.nlev; ++q) its += stb->iters_level[q];
+        printf("ST_PROF b %d n %lld its %d den %llu ctrl %llu hist %llu emap %llu fit %llu latP1 %llu eval %llu "
                "wait %llu level %llu exact %llu top %llu | emap: series %llu fwd %llu filter %llu conv %llu div %llu\n",
-               ST_PROF_B, (long long)n, st_prof[0], st_prof[1], st_prof[2],
+               ST_PROF_B, (long long)n, its, st_prof[0], st_prof[1], st_prof[2],
                st_prof[3] + st_prof[11] + st_prof[12] + st_prof[13] + st_prof[14],
                st_prof[4], st_prof[5], st_prof[6], st_prof[7], st_prof[8], st_prof[9], st_prof[10],
                st_prof[11], st_prof[12], st_prof[13], st_prof[14], st_prof[3]);
-        printf("ST_PROF fit: rows %llu push %llu contract %llu items %llu\n", M.fprof[0], M.fprof[1],
-               M.fprof[2], M.fprof[3]);
+        printf("ST_PROF fit: rows %llu push %llu contract %llu items %llu | series thread 300: total %llu "
+               "hist %llu kernel-exp %llu; thread 200 twiddle %llu\n", M.fprof[0], M.fprof[1],
+               M.fprof[2], M.fprof[3], M.sprof[0], M.sprof[1], M.sprof[2], M.sprof[3]);
     }
 #endif
     // final field's P1 for k_n4_final
