@@ -298,6 +298,7 @@ static void pipe_free(vh_pipe *p) {
         if (q.u8) (void)hipHostFree(q.u8);
         if (q.done) (void)hipEventDestroy(q.done);
         if (q.h2d) (void)hipEventDestroy(q.h2d);
+        if (q.packed) (void)hipEventDestroy(q.packed);
 
     }
     delete p;
@@ -793,6 +794,18 @@ __global__ void k_pack_maps(const uint8_t *__restrict__ d, const uint8_t *__rest
 
 static void par_memcpy(void *dst, const void *src, size_t bytes);
 
+// studies cnt .. sub - 1 of a ragged pipe chunk := study cnt - 1 (image and mask)
+__global__ void k_repeat_last(float *hp, uint8_t *mask, int64_t V, int64_t cnt, int64_t sub) {
+    const int64_t n = (sub - cnt) * V;
+    const float *sh = hp + (cnt - 1) * V;
+    const uint8_t *sm = mask + (cnt - 1) * V;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t v = i % V;
+        hp[cnt * V + i] = sh[v];
+        mask[cnt * V + i] = sm[v];
+    }
+}
+
 // The mask crosses PCIe as one bit per voxel (bit i % 8 of byte i / 8); k_unpack_mask restores the
 // bytes on the device.  par_pack_mask returns false (nothing usable) if a byte is not 0 / 1.
 __global__ void k_unpack_mask(const uint8_t *__restrict__ bits, uint8_t *__restrict__ mask, int64_t n) {
@@ -921,6 +934,7 @@ int vh_pipe_create(vh_ctx *ctx, int64_t R, int64_t C, int64_t Z, int64_t sub, in
                 HIP_TRY(hipHostMalloc((void **)&q.u8, 2 * NV + q.scal));   // mask in | scalars + maps out
                 HIP_TRY(hipEventCreateWithFlags(&q.done, hipEventDisableTiming));
                 HIP_TRY(hipEventCreateWithFlags(&q.h2d, hipEventDisableTiming));
+                HIP_TRY(hipEventCreateWithFlags(&q.packed, hipEventDisableTiming));
                 HIP_TRY(hipMalloc((void **)&q.d_pack, (size_t)NV + q.scal));
                 q.mb_half = ((size_t)NV / 8 + 1 + 63) / 64 * 64;
                 HIP_TRY(hipHostMalloc((void **)&q.mb, 2 * q.mb_half));
@@ -1155,8 +1169,13 @@ int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, con
         // H2D order: 0 none, 1 device-side (the H2D waits on the previous chunk's H2D event),
         // 2 host-side (the enqueuing thread waits for that event first)
         const char *ho = getenv("VH_PIPE_H2D_ORDER");
-        const int h2d_order = ho ? atoi(ho) : 1;
-        const bool d2h_late = env_flag("VH_PIPE_D2H_LATE", false);
+        const int h2d_order = ho ? atoi(ho) : 2;
+        // No copy is enqueued before what it depends on has finished (host-side waits): a copy
+        // enqueued behind unfinished work waits on the DMA engine's queue and holds back every
+        // later copy of that engine -- an H2D stuck behind another chunk's D2H that waits for a
+        // kernel which waits for a CU (r4b trace: 30 ms stalls).  The D2H waits for the chunk's
+        // packing kernel (not just the pipeline: the packing may itself wait for a free CU).
+        const bool d2h_late = env_flag("VH_PIPE_D2H_LATE", true);
         auto work = [&](int s) {
             vh_pipe::Slot &q = p->slot[s];
             vh_batch *b = q.b;
@@ -1187,22 +1206,22 @@ int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, con
                 if (h2d_order == 1 && c.k > 0)
                     HIP_TRY(hipStreamWaitEvent(b->stream, p->slot[(c.k - 1) % slots].h2d, 0));
                 if (h2d_order == 2 && c.k > 0) HIP_TRY(hipEventSynchronize(p->slot[(c.k - 1) % slots].h2d));
+                // the copies first (the event marks their end: the next chunk's H2D waits for it
+                // on the host), then the kernels that consume them
                 c.sp[0].h2d((char *)b->d_hp, (char *)q.hp, b->stream);
+                if (c.mbits) HIP_TRY(hipMemcpyAsync(q.d_pack, c.mb, (CV + 7) / 8, hipMemcpyHostToDevice, b->stream));
+                else c.sp[1].h2d((char *)b->d_mask, (char *)qm, b->stream);
+                HIP_TRY(hipEventRecord(q.h2d, b->stream));
                 if (c.mbits) {
-                    HIP_TRY(hipMemcpyAsync(q.d_pack, c.mb, (CV + 7) / 8, hipMemcpyHostToDevice, b->stream));
                     k_unpack_mask<<<(unsigned)std::min<int64_t>(4096, ((int64_t)(CV + 7) / 8 + 255) / 256), 256, 0,
                                     b->stream>>>(q.d_pack, b->d_mask, (int64_t)CV);
                     HIP_TRY(hipGetLastError());
-                } else {
-                    c.sp[1].h2d((char *)b->d_mask, (char *)qm, b->stream);
                 }
-                for (int64_t i = c.cnt; i < sub; ++i) {   // ragged tail: repeat the last study
-                    HIP_TRY(hipMemcpyAsync(b->d_hp + i * V, b->d_hp + (c.cnt - 1) * V, sizeof(float) * V,
-                                           hipMemcpyDeviceToDevice, b->stream));
-                    HIP_TRY(hipMemcpyAsync(b->d_mask + i * V, b->d_mask + (c.cnt - 1) * V, V,
-                                           hipMemcpyDeviceToDevice, b->stream));
+                if (c.cnt < sub) {   // ragged tail: repeat the last study (a kernel, not DMA copies)
+                    k_repeat_last<<<(unsigned)std::min<int64_t>(4096, (sub - c.cnt) * (V / 4 + 255) / 256 + 1), 256, 0,
+                                    b->stream>>>(b->d_hp, b->d_mask, V, c.cnt, sub);
+                    HIP_TRY(hipGetLastError());
                 }
-                HIP_TRY(hipEventRecord(q.h2d, b->stream));
                 mark_ev(c.mk, 0, b->stream);
                 c.mk.h[1] = now_ms();
                 if (lag > 0 && c.k >= lag)
@@ -1227,6 +1246,7 @@ int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, con
                                                reinterpret_cast<uint32_t *>(q.d_pack));
                     HIP_TRY(hipGetLastError());
                 }
+                HIP_TRY(hipEventRecord(q.packed, b->stream));
             };
             auto back_pin = [&](Chunk &c) {   // while the chunk computes: first touch + pin of its output pages
                 c.sp[2].plan(n4 ? n4 + c.v0 * V : nullptr, sizeof(float) * c.CV, true, p);
@@ -1265,7 +1285,7 @@ int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, con
                             back_pin(cur);
                             // VH_PIPE_D2H_LATE=1 enqueues the D2Hs only once the compute has
                             // finished (A/B: neutral to -2 % on the boxes measured, r3q3; off)
-                            if (d2h_late) HIP_TRY(hipEventSynchronize(q.done));
+                            if (d2h_late) HIP_TRY(hipEventSynchronize(q.packed));
                             back(cur);
                             HIP_TRY(hipStreamSynchronize(b->stream));
                             cur.mk.h[4] = now_ms();

@@ -1323,7 +1323,7 @@ __global__ void __launch_bounds__(PC_TPB) k_n4_pcw(const float *D, const int32_t
     const int32_t *const pb = perm + b * VS;
     // D[b] (compact d) is free once pass 0 has read it: PCX's stored increments.  skip_thresh:
     // the certified "above the threshold" decision of pcw_run (0 at the level's last iteration)
-    pcw_run([=](int64_t r) { return Db[pb[r]]; }, Pbuf + b * VS, sc[b].n_mask1, S, ch, 1,
+    pcw_run<PC_TPB>([=](int64_t r) { return Db[pb[r]]; }, Pbuf + b * VS, sc[b].n_mask1, S, ch, 1,
             reinterpret_cast<double *>(const_cast<float *>(Db)), (int)(VS / 2), skip_thresh);
     if (threadIdx.x == 0) st[b].conv_w = ch.conv;
 }

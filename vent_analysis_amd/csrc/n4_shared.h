@@ -1563,7 +1563,7 @@ __device__ bool pcx_scan(PcShared<NL> &S, const PcMap &m, const float *P, const 
 }
 
 #define PC_TPB 1024
-// The recurrence of one iteration on a whole 1024-thread workgroup (one block per thread), shared by
+// The recurrence of one iteration on a whole NL-thread workgroup (one block per thread), shared by
 // the study kernel (ST_PC 2) and the sweep driver (k_n4_pcw).  ld(r) returns d at raster rank r
 // (the study's raster-ordered stores, or the sweep's compact d through the raster permutation);
 // pass 0 reads each block's run of it, writes
@@ -1583,12 +1583,12 @@ static_assert(PC_APASS >= 1 && PC_APASS <= 2, "PC_APASS: 1 or 2 phase-A stages (
 #define PC_XSIG 1   // exact sig after stage 0 (PCX above); 0: stage 1 and the exact rounds always
 #endif
 // PEXP: ld returns p = expf_cr(d) already (the study kernel's eval stored it, ST_EVAL_EXP)
-template <bool PEXP = false, class LoadD>
-__device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n, PcShared<PC_TPB> &S,
+template <int NL, bool PEXP = false, class LoadD>
+__device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n, PcShared<NL> &S,
                                                   ChainState &ch, int req, double *tbuf, int tcap,
                                                   float skip_thresh = 0.0f) {
     const int tid = threadIdx.x;
-    const PcMap m = pc_map(n, PC_TPB);
+    const PcMap m = pc_map(n, NL);
     const uint32_t j = (uint32_t)tid, len = pc_len(m, j), k0 = pc_k0(m, j);
 #ifdef PC_PROF
     const unsigned long long c0 = clock64();
@@ -1600,18 +1600,18 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
     // 64 cache lines per wave-wide load; instead the workgroup loads each group of PC_G0 steps of
     // all blocks together (8 lanes per block: 32-byte runs) and transposes it through LDS (the
     // PcShared area, rewritten after this pass; rows padded by 8 floats against bank conflicts).
-    constexpr int G0 = 8, TS = PC_TPB + 8;
-    static_assert(sizeof(float) * G0 * TS <= sizeof(PcShared<PC_TPB>), "pass-0 transpose buffer");
+    constexpr int G0 = 8, TS = NL + 8;
+    static_assert(sizeof(float) * G0 * TS <= sizeof(PcShared<NL>), "pass-0 transpose buffer");
     float *const T0 = reinterpret_cast<float *>(&S);
     const uint32_t lmax = m.L + (m.rem ? 1u : 0u);
     double s1 = 0.0, s2 = 0.0;
-    // thread tid loads step i = tid % G0 of blocks tid / G0 + (PC_TPB / G0) q; the next group's
+    // thread tid loads step i = tid % G0 of blocks tid / G0 + (NL / G0) q; the next group's
     // loads are in flight while this group's exp runs
     float v[G0];
     auto fetch = [&](uint32_t g0) {
 #pragma unroll
         for (int q = 0; q < G0; ++q) {
-            const uint32_t jb = (uint32_t)tid / G0 + (uint32_t)(PC_TPB / G0) * q, i = (uint32_t)tid % G0;
+            const uint32_t jb = (uint32_t)tid / G0 + (uint32_t)(NL / G0) * q, i = (uint32_t)tid % G0;
             v[q] = g0 + i < pc_len(m, jb) ? ld((int64_t)(pc_k0(m, jb) - 1u + g0 + i)) : 0.0f;
         }
     };
@@ -1625,7 +1625,7 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
     for (uint32_t g0 = 0; g0 < lmax; g0 += G0) {
 #pragma unroll
         for (int q = 0; q < G0; ++q)
-            T0[(tid % G0) * TS + tid / G0 + (PC_TPB / G0) * q] = v[q];
+            T0[(tid % G0) * TS + tid / G0 + (NL / G0) * q] = v[q];
         P0M(0);   // (profiling) the group's loads arrived and went to LDS
         __syncthreads();
         P0M(1);   // first barrier
@@ -1634,7 +1634,7 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
         for (int i = 0; i < G0; ++i)
             if (g0 + i < len) {
                 const float p = PEXP ? T0[i * TS + j] : expf_cr(T0[i * TS + j]);
-                P[(size_t)(g0 + i) * PC_TPB + j] = p;
+                P[(size_t)(g0 + i) * NL + j] = p;
                 const double e = (double)p - 1.0;
                 s1 += e;
                 s2 = fma(e, e, s2);
@@ -1659,7 +1659,7 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
     S.s1(j) = s1;
     S.s2(j) = s2;
     __syncthreads();
-    pcw_guess<PC_TPB>(S, m);
+    pcw_guess<NL>(S, m);
     __syncthreads();
 #ifdef PC_PROF
     c1 = clock64();
@@ -1678,13 +1678,13 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
 #ifdef PC_PROF
             const unsigned long long cx0 = clock64();
 #endif
-            const bool real = j < (uint32_t)(m.L ? PC_TPB : m.rem);
+            const bool real = j < (uint32_t)(m.L ? NL : m.rem);
             const double own = real ? (double)S.b[j].esig : 0.0;   // stage 0's sum (p - mu)^2
             // the same sums weighted by the smallest (N - 1) / N of the block: their total bounds
             // the float sig from below (the certified decision below)
             const double wown = (real && k0 > 1u) ? own * (1.0 - 1.0 / fmin((double)k0, ITK_NMAX)) : 0.0;
             double sest, wpre;   // sig estimate at the block start: the prefix of those sums
-            pcw_scan<PC_TPB>(S, 1.0, own, wown, sest, wpre);
+            pcw_scan<NL>(S, 1.0, own, wown, sest, wpre);
             // Certified decision (skip_thresh > 0: this iteration's measure is only compared with the
             // threshold, never reported): with mu exact after stage 0, every float sig step is
             // t_k = RN(RN(RN_f(q q) (N - 1)) / N) >= q^2 (1 - 1/N)(1 - 2^-24)(1 - 2^-52)^2, the float
@@ -1695,12 +1695,12 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
             // threshold at sig = RD(lo) proves the true one is above it too: the iteration goes on
             // and the exact sig (PCX below) is not needed.  Otherwise, or when the measure is the
             // level's reported one (skip_thresh = 0), PCX computes it exactly.
-            if (tid == PC_TPB - 1 && skip_thresh > 0.0f) {
+            if (tid == NL - 1 && skip_thresh > 0.0f) {
                 const double f = 1.0 - ((double)n + (double)m.L + 8.0) * 0x1p-24;
                 const double lo = (wpre + wown) * f;
                 float sl = (float)lo;
                 if ((double)sl > lo && sl > 0.0f) sl = __uint_as_float(__float_as_uint(sl) - 1u);
-                const int nbe = m.L ? PC_TPB : (int)m.rem;
+                const int nbe = m.L ? NL : (int)m.rem;
                 const float mue = S.b[nbe - 1].emu;   // (one float up: a margin that costs nothing)
                 const float muh = __uint_as_float(__float_as_uint(mue) + 1u);
                 if (f > 0.5 && lo > 0.0 && mue > 0.0f && itk_conv(muh, sl, n) > skip_thresh) {
@@ -1719,7 +1719,7 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
 #ifdef PC_PROF
             const unsigned long long cxt = clock64();
 #endif
-            pcx_tpass<PC_TPB>(S, m, P, j, len, k0, sest, sest + own, tbuf, tcap);
+            pcx_tpass<NL>(S, m, P, j, len, k0, sest, sest + own, tbuf, tcap);
             __syncthreads();
 #ifdef PC_PROF
             cbs[1] = clock64() - cxt;   // T pass (reported as stage1 blocks)
@@ -1731,9 +1731,9 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
 #endif
                 float sg = 0.0f;
                 int w = 0, slow = 0;
-                const bool ok = pcx_scan<PC_TPB>(S, m, P, tbuf, sg, w, slow);
+                const bool ok = pcx_scan<NL>(S, m, P, tbuf, sg, w, slow);
                 if (tid == 0) {
-                    const int nbe = m.L ? PC_TPB : (int)m.rem;
+                    const int nbe = m.L ? NL : (int)m.rem;
                     if (ok) {
                         S.mu = S.b[nbe - 1].emu;
                         S.sig = sg;
@@ -1778,8 +1778,8 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
 #endif
             if (__ballot(!same) != 0ull && !same) {
                 float mu = g, sig = gs;
-                if (pass == 0) pc_block_apx<PC_TPB, false>(P, j, len, k0, mu, sig, PC_TPB, (m.L + 1u) * PC_TPB);
-                else pc_block_apx<PC_TPB, true>(P, j, len, k0, mu, sig, PC_TPB, (m.L + 1u) * PC_TPB);
+                if (pass == 0) pc_block_apx<NL, false>(P, j, len, k0, mu, sig, NL, (m.L + 1u) * NL);
+                else pc_block_apx<NL, true>(P, j, len, k0, mu, sig, NL, (m.L + 1u) * NL);
                 lg = g;
                 ls = gs;
                 le = mu;
@@ -1791,7 +1791,7 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
 #ifdef PC_PROF
             cblk += clock64() - cq;
 #endif
-            pcw_update<PC_TPB>(S, m, round, tag, ra0 == PC_AMAX - 1, false, pass == 1);
+            pcw_update<NL>(S, m, round, tag, ra0 == PC_AMAX - 1, false, pass == 1);
             __syncthreads();
 #ifdef PC_PROF
             rst[pass]++;
@@ -1812,15 +1812,15 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
     for (int rb = 0; rb < PC_RMAX && !xs; ++rb) {
         ++round;
         float mu = S.b[j].gmu, sig = S.b[j].gsig;
-        pc_block<PC_TPB>(P, j, len, k0, mu, sig);
+        pc_block<NL>(P, j, len, k0, mu, sig);
         S.b[j].emu = mu;
         S.b[j].esig = sig;
         __syncthreads();
-        pcw_update<PC_TPB>(S, m, round, tagb, rb == PC_RMAX - 1, true);
+        pcw_update<NL>(S, m, round, tagb, rb == PC_RMAX - 1, true);
         __syncthreads();
         if (S.done == tagb) break;
         if (S.fallback == tagb) {
-            if (tid == 0) pc_serial<PC_TPB>(S, m, P);
+            if (tid == 0) pc_serial<NL>(S, m, P);
             __syncthreads();
             break;
         }

@@ -28,7 +28,9 @@
 
 #include "n4_shared.h"
 
+#ifndef ST_TPB
 #define ST_TPB 1024
+#endif
 #define ST_WAVES (ST_TPB / 64)
 #define ST_HC 8        // LDS histogram copies
 #define ST_NFIRST 16   // first masked voxels (raster order) tracked for the bin minimum (n4_shared.h r3_bin_min)
@@ -55,7 +57,7 @@ static_assert(ST_CW == 4, "a chain group is 4 waves, one per SIMD (mu, sig, 2 pr
 #endif
 static_assert(ST_PC == 0 || ST_PC == 2, "ST_PC 0 (serial chains) or 2 (PC on all waves)");
 constexpr bool ST_SPLIT = ST_PC != 2;   // conv_mode 0 runs chain waves beside compute waves
-static_assert(ST_PC != 2 || ST_TPB == PC_TPB, "pcw_run takes the whole 1024-thread workgroup");
+static_assert(ST_TPB == 1024 || ST_TPB == 512, "pcw_run takes the whole workgroup (one block per thread)");
 // Speculation depth of the split mode: the compute waves run up to ST_DEPTH iterations ahead of
 // the last iteration whose recurrence has finished.  Depth 2 keeps two chains in flight (chain
 // group g = iteration & 1, ST_CW waves each), so two serial recurrences overlap each other and the
@@ -1164,7 +1166,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                     // the raster d buffer is free once pass 0 has read it: PCX's stored increments
                     // below the iteration cap this iteration's measure only decides whether the
                     // level goes on: PC may certify "above the threshold" without the exact sig
-                    pcw_run<ST_EVAL_EXP && !ST_SPLIT>([=](int64_t r) { return Dr[r]; }, a.D + a.half + b * a.VS, n, PW, M.ch[0], itk,
+                    pcw_run<ST_TPB, ST_EVAL_EXP && !ST_SPLIT>([=](int64_t r) { return Dr[r]; }, a.D + a.half + b * a.VS, n, PW, M.ch[0], itk,
                             reinterpret_cast<double *>(a.D + b * a.VS), (int)(a.VS / 2),
                             itk < a.lvs->max_iters[L] ? a.thresh : 0.0f);
                     if (t == 0) M.conv = (double)M.ch[0].conv;

@@ -133,6 +133,7 @@ struct vh_pipe {
         uint8_t *u8 = nullptr;                // pinned: mask in [sub][V], then the D2H block (scal + [sub][V])
         hipEvent_t done = nullptr;            // recorded after the slot's current chunk's pipeline
         hipEvent_t h2d = nullptr;             // recorded after the slot's current chunk's H2D
+        hipEvent_t packed = nullptr;          // recorded after the chunk's output packing (its D2H may start)
         uint8_t *d_pack = nullptr;            // device: the chunk's D2H block: scalars (scal bytes), packed maps
         size_t scal = 0;                      // bytes of the per-study scalars + N4 states block (4 KiB multiple)
         uint8_t *mb = nullptr;                // pinned: mask bits, two chunks' worth (double buffer)
