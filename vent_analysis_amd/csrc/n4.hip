@@ -978,7 +978,7 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_emap(const uint64_t *hpart, const
             F[n].x = (double)sf * exp(-0.25 * (double)((float)P * (float)P) * (double)ef);
         } else {
             const float nf = (float)n;
-            const double v = (double)(sf * expf_cr(-(nf * nf) * ef));
+            const double v = (double)(sf * expf_cr_tail(-(nf * nf) * ef));
             F[n].x = v;
             F[P - n].x = v;
         }

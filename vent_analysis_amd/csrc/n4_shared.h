@@ -62,6 +62,10 @@ __device__ __forceinline__ void wave_lds_order() {
 
 // correctly rounded float exp through double (S1/S7/S9)
 __device__ __forceinline__ float expf_cr(float x) { return (float)exp((double)x); }
+// the Wiener kernel's Gaussian tail: (float)exp((double)x) is +0 for every float x < -104
+// (e^-104 < 2^-150, half the smallest float denormal), and the double exp of such an argument
+// took ~30 k cycles a step in the E map (ST_PROF r4e: thread 300's exp 0.96 M cycles per study)
+__device__ __forceinline__ float expf_cr_tail(float x) { return x < -104.0f ? 0.0f : expf_cr(x); }
 
 // S7x (conv_mode 1): expm1 of a float field difference
 __device__ __forceinline__ float expm1c(float x) {

@@ -982,7 +982,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                             fx = (double)sf * exp(-0.25 * (double)((float)P * (float)P) * (double)ef);
                         } else {
                             const float nf = (float)(i < P / 2 ? i : P - i);
-                            fx = (double)(sf * expf_cr(-(nf * nf) * ef));
+                            fx = (double)(sf * expf_cr_tail(-(nf * nf) * ef));
                         }
                         F[fpad(i)] = make_double2(fx, 0.0);
 #ifdef ST_PROF
