@@ -250,6 +250,58 @@ def host_to_host(R, C, Z, nb, args, device, opts, seed, aligned=True):
             "pcie_bytes_per_volume": int(R * C * Z * (4 + 0.125 + 4 + 1))}
 
 
+def link_probe(device, mb=256):
+    """This box's PCIe link with pinned host memory: H2D alone, D2H alone and both at once on two
+    streams (as the pipe's overlapped chunks use it), best of 3 each.  The host-to-host line can
+    not beat link rate / PCIe bytes per volume, whatever the device-resident rate."""
+    import torch
+    n = mb << 20
+    dev = torch.device("cuda", device)
+    h_in = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    h_out = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    d_in = torch.empty(n, dtype=torch.uint8, device=dev)
+    d_out = torch.empty(n, dtype=torch.uint8, device=dev)
+    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
+
+    def h2d():
+        with torch.cuda.stream(s1):
+            d_in.copy_(h_in, non_blocking=True)
+
+    def d2h():
+        with torch.cuda.stream(s2):
+            h_out.copy_(d_out, non_blocking=True)
+
+    def both():
+        h2d()
+        d2h()
+
+    def best(fn):
+        ts = []
+        for _ in range(3):
+            torch.cuda.synchronize(dev)
+            t = time.perf_counter()
+            fn()
+            torch.cuda.synchronize(dev)
+            ts.append(time.perf_counter() - t)
+        return min(ts)
+
+    both()
+    torch.cuda.synchronize(dev)
+    t1, t2, t3 = best(h2d), best(d2h), best(both)
+    del h_in, h_out, d_in, d_out
+    return {"bytes_each_way": n, "h2d_GBps": round(n / t1 / 1e9, 2),
+            "d2h_GBps": round(n / t2 / 1e9, 2), "both_GBps": round(2 * n / t3 / 1e9, 2)}
+
+
+def link_bound(link, R, C, Z):
+    """Upper bound of the host-to-host rate from the link probe: the pipe moves 4.125 bytes per
+    voxel in (HPvent f32, mask bits) and 5 out (N4HPvent f32, one packed map byte)."""
+    v = R * C * Z
+    b_in, b_out = v * 4.125, v * 5.0
+    return min(link["both_GBps"] * 1e9 / (b_in + b_out), link["h2d_GBps"] * 1e9 / b_in,
+               link["d2h_GBps"] * 1e9 / b_out)
+
+
 def main_ci(args):
     """CI line: defect-voxels/s and sphere-probes/s of the cluster-index map
     on 128x128x24 studies, host-to-host through vh_ci (defect map in, float64 CI map out).  Two
@@ -628,6 +680,9 @@ def main():
         if dist:   # every rank streams at once (host memory and PCIe shared as in a cohort run)
             dist.barrier()
         h2h = host_to_host(R, C, Z, nb, args, local, warm, shard_seed(rank) + 500)
+        h2h["link"] = link_probe(local)
+        h2h["link"]["bound_vol_s"] = round(link_bound(h2h["link"], R, C, Z), 1)
+        h2h["link"]["h2h_of_bound"] = round(h2h["volumes"] / h2h["seconds"] / h2h["link"]["bound_vol_s"], 3)
         if dist:   # the aggregate uses the slowest rank's time
             h2h["seconds"] = round(max_over_ranks(h2h["seconds"], dist), 4)
             h2h["seconds_statistic"] = "max over ranks of each rank's median"
