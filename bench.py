@@ -606,6 +606,9 @@ def main():
         dt = max_over_ranks(dt, dist)
     _, _, _, _, res = Bt.download(n4=False, maps=False)
     st_us = Bt.study_times()   # per-study wall time of the last step's one-workgroup-per-study N4
+    if os.environ.get("VH_STUDY_TRACE"):   # the other batches' placements too (A/B runs)
+        for b_ in batches[1:]:
+            b_.study_times()
     tail = None
     if st_us.max() > 0:
         tail = {"min_us": round(float(st_us.min()), 1), "mean_us": round(float(st_us.mean()), 1),

@@ -118,6 +118,9 @@ static void batch_free(vh_batch *b) {
     dfree(b->d_ci_status);
     dfree(b->d_ci_count); dfree(b->d_ci_map);
     if (b->stream) (void)hipStreamDestroy(b->stream);
+    if (b->st_n4) (void)hipStreamDestroy(b->st_n4);
+    if (b->ev_n4_pre) (void)hipEventDestroy(b->ev_n4_pre);
+    if (b->ev_n4_post) (void)hipEventDestroy(b->ev_n4_post);
     if (b->h_flags) (void)hipHostFree(b->h_flags);
     delete b;
 }
@@ -127,9 +130,22 @@ static vh_batch *batch_new(vh_ctx *ctx, int64_t R, int64_t C, int64_t Z, int64_t
     HIP_TRY(hipSetDevice(ctx->device));
     vh_batch *b = new vh_batch;
     b->ctx = ctx;
-    if (hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess) {
+    // VH_PRIO=1: the batch's stream at the highest priority and its study kernel on a second stream
+    // at the lowest, so when CUs free up the dispatcher serves the short kernels of other batches
+    // (their next study launch waits on them) before more studies
+    const char *pe = getenv("VH_PRIO");
+    const bool prio = pe && atoi(pe) != 0;
+    int lo = 0, hi = 0;
+    if (prio) (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+    if ((prio ? hipStreamCreateWithPriority(&b->stream, hipStreamNonBlocking, hi)
+              : hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking)) != hipSuccess ||
+        (prio && (hipStreamCreateWithPriority(&b->st_n4, hipStreamNonBlocking, lo) != hipSuccess ||
+                  hipEventCreateWithFlags(&b->ev_n4_pre, hipEventDisableTiming) != hipSuccess ||
+                  hipEventCreateWithFlags(&b->ev_n4_post, hipEventDisableTiming) != hipSuccess))) {
+        if (b->stream) (void)hipStreamDestroy(b->stream);
+        if (b->st_n4) (void)hipStreamDestroy(b->st_n4);
         delete b;
-        throw VhError{VH_ERR_HIP, "hipStreamCreateWithFlags failed"};
+        throw VhError{VH_ERR_HIP, "batch stream creation failed"};
     }
     b->R = R; b->C = C; b->Z = Z; b->nb = nb;
     b->V = R * C * Z;
@@ -695,6 +711,15 @@ int vh_batch_study_times(vh_batch *b, double *us) {
         if (rate_khz <= 0) throw VhError{VH_ERR_HIP, "no device wall clock rate"};
         for (int64_t i = 0; i < b->nb; ++i)
             us[i] = (double)(st[i].t_end - st[i].t_start) * 1000.0 / (double)rate_khz;
+        if (const char *path = getenv("VH_STUDY_TRACE")) {   // per study: start, end, placement
+            if (FILE *f = fopen(path, "a")) {
+                for (int64_t i = 0; i < b->nb; ++i)
+                    fprintf(f, "%p,%lld,%llu,%llu,%u,%u,%d\n", (void *)b, (long long)i,
+                            (unsigned long long)st[i].t_start, (unsigned long long)st[i].t_end,
+                            st[i].hw_id, st[i].xcc_id, rate_khz);
+                fclose(f);
+            }
+        }
     })
 }
 

@@ -1,12 +1,15 @@
 // n4_study.hip -- volume-resident N4 bias-field correction on gfx950: ONE workgroup (1024 threads,
-// 16 waves) per study runs the whole multi-level iteration loop of
+// 16 waves; ST_TPB=512 builds: 8 waves, two studies per CU) per study runs the whole multi-level
+// iteration loop of
 // sitk.N4BiasFieldCorrectionImageFilter (Vent_Analysis.py:316-334; build spec
 // S1-S9 in oracle/n4_oracle.c, which this kernel matches bit for bit) in a single launch.  Between
-// sweeps the study's small state -- B-spline lattice, fit denominators, the z-contracted lattices
-// P1 (current and previous field), level tables, histogram, FFT buffers, E(u) map -- never leaves
-// LDS, so an iteration costs three streaming passes over the compact masked voxels, workgroup
-// barriers and (conv_mode 0) the serial convergence recurrence, with no kernel launches, no
-// grid-wide dependencies and no host round trips.  A batch of >= one study per CU fills the chip.
+// sweeps the study's small state -- B-spline lattice, level tables, histogram, FFT buffers, E(u)
+// map, the new field's z-contracted lattice P1 -- stays in LDS (70 KB at 128x128x24); the fit
+// denominators and the per-column T windows of the last two fields (the old field's B at every
+// voxel is rebuilt from them) sit in small per-study global buffers that stay in L2.  An
+// iteration costs three streaming passes over the compact masked voxels, workgroup barriers and
+// (conv_mode 0) the convergence recurrence, with no kernel launches, no grid-wide dependencies and
+// no host round trips.  A batch of >= one study per CU fills the chip.
 //
 // Per iteration (all inside the workgroup):
 //   ctrl  convergence of the previous iteration, ITK's while-condition, bin range (S2: max and the
@@ -17,11 +20,22 @@
 //         the row axis contracted in registers by a sliding 4-wide window (S5), finished control
 //         rows contracted over the tile's slices and cols, 128-bit fixed-point LDS atomics
 //   lat   phi = num / den, lattice += phi, P1 = lattice contracted over slices (S6)
-//   eval  column walk again: B_new and B_old from the column's T windows, U = L0 - B_new, the field
+//   eval  column walk again: B_new from the column's T window (from P1, stored for the next
+//         iteration), B_old from the stored window of the previous field, U = L0 - B_new, the field
 //         difference d written in raster order (conv_mode 0) or the exact-CoV sums (conv_mode 1)
-//   conv  (conv_mode 0) two waves run ITK's float Welford recurrence over d in raster order (S7)
+//   conv  (conv_mode 0) ITK's float Welford recurrence over d in raster order (S7) by guess and
+//         verify on all waves (n4_shared.h PC)
 // Work items are taken from an LDS counter; every reduction is either integer (order-free) or in
 // a fixed order, so results are deterministic.
+//
+// Round 4: 153 -> 70 KB of LDS per study (P1 pair, denominators and the second table set out of
+// LDS, 4 histogram copies in the emap's DEN buffer) at unchanged speed, so that ST_TPB=512 builds
+// fit two studies per CU.  Measured: two 512-thread studies on a CU
+// take 1.37x as long as one alone, 1.46x the CU's throughput -- but one alone takes 1.26x as long
+// as a 1024-thread study (128 VGPRs and half the waves for the latency-bound fit and eval walks),
+// and 256-study batches do not keep both slots fed (the next batch's short kernels wait for CUs
+// that two studies fill), so 1024 threads stay the default.  The serial-chain variant of S7 (chain
+// waves beside the compute waves, 46-54 ms per bench step against PC's 33 ms) is gone.
 #include <algorithm>
 #include <cfloat>
 #include <cstring>
@@ -32,51 +46,14 @@
 #define ST_TPB 1024
 #endif
 #define ST_WAVES (ST_TPB / 64)
-#define ST_HC 8        // LDS histogram copies
+#define ST_HC 4        // LDS histogram copies (in the emap's DEN buffer, free until the Wiener pass)
 #define ST_NFIRST 16   // first masked voxels (raster order) tracked for the bin minimum (n4_shared.h r3_bin_min)
 #define ST_MAX_LDS (160 * 1024)
-#ifndef ST_CH_PROD
-#define ST_CH_PROD 2   // producer waves of the convergence chain (n4_shared.h chain_wave_prod)
-#endif
-#define ST_CW (2 + ST_CH_PROD)   // chain waves (conv_mode 0): A, B, producers
-#ifndef ST_CG
-#define ST_CG 0        // conv_mode 0 compute waves: 0 = all the others, 1 = the 6 on SIMDs 2 and 3 (depth 1)
-#endif
-static_assert(ST_CW == 4, "a chain group is 4 waves, one per SIMD (mu, sig, 2 producers)");
-// conv_mode 0, the S7 recurrence: 0 = serial chains on chain waves beside the compute waves, which
-// speculate ST_DEPTH iterations ahead (below); 2 = S7 by guess and verify (n4_shared.h PC) on all
-// 16 waves after each iteration's eval (no speculation).  Measured per 256-study bench step
-// (heterogeneous studies): 2 33.1 ms, 0 depth 1 53.7 ms, 0 depth 2 48.8 ms.  (Before the bin
-// minimum stopped falling back to the raster scan, r3_bin_min, the compute waves spent that scan's
-// time beside the serial chain and 0 came out ahead: 45.8 vs 49-50 ms.)
 #ifndef ST_EVAL_EXP
 #define ST_EVAL_EXP 0   // 1: eval stores p = expf_cr(d) for PC (its pass 0 then skips the exp)
 #endif
-#ifndef ST_PC
-#define ST_PC 2
-#endif
-static_assert(ST_PC == 0 || ST_PC == 2, "ST_PC 0 (serial chains) or 2 (PC on all waves)");
-constexpr bool ST_SPLIT = ST_PC != 2;   // conv_mode 0 runs chain waves beside compute waves
 static_assert(ST_TPB == 1024 || ST_TPB == 512, "pcw_run takes the whole workgroup (one block per thread)");
-// Speculation depth of the split mode: the compute waves run up to ST_DEPTH iterations ahead of
-// the last iteration whose recurrence has finished.  Depth 2 keeps two chains in flight (chain
-// group g = iteration & 1, ST_CW waves each), so two serial recurrences overlap each other and the
-// compute of the next iteration: U / D rings of 3 buffers, the lattice before each of the last two
-// updates saved in global memory, up to two iterations discarded when ITK's while-condition stops.
-#ifndef ST_DEPTH
-#define ST_DEPTH 1
-#endif
-// Depth 2 is bit-exact (all study tests) but measured slower: 57.4 ms against 46.4 per bench step.
-// Its 8 chain waves leave 8 compute waves (compute phases 34.9 M -> 53.6 M cycles of block 0, two
-// iterations discarded per level end) while the waits only halve (70.2 M -> 33.5 M).
-#ifndef ST_CH_NS
-#define ST_CH_NS (ST_DEPTH == 1 ? 4 : 2)   // chain slots per group (depth 1: 4 within 1 % of 16;
-#endif                                      // depth 2: two rings of 2 keep the LDS of one ring of 4)
-static_assert(ST_DEPTH == 1 || ST_DEPTH == 2, "speculation depth 1 or 2");
-static_assert(ST_CG == 0 || ST_DEPTH == 1, "compute waves on SIMDs 2 and 3 only with one chain group");
-constexpr int ST_NG = ST_DEPTH;             // chain groups
-constexpr int ST_CWT = ST_NG * ST_CW;       // chain waves in all
-constexpr int ST_NB = ST_DEPTH + 1;         // U / D ring buffers
+constexpr int ST_NB = 2;   // U buffers: the last computed field's and the one being computed
 
 // ST_PROF builds (scripts/dev/phase_ab.sh): block 0 prints shader cycles per phase at the end
 #ifdef ST_PROF
@@ -112,18 +89,18 @@ struct StudyArgs {
     float thresh, fwhm, noise;
     const StudyLevels *lvs;   // device copy: per-level tables and iteration caps
     // dynamic-LDS carve (byte offsets)
-    int32_t o_E, o_tab0, o_tab1, o_lat, o_den, o_P10, o_P11, o_ipart, o_rpart, o_misc, o_scr, o_wave,
-        o_order;
-    int32_t o_chain, o_latp;   // conv_mode 0: the chain's slot ring; the lattice before the last update
-    int64_t half;              // U and D are double-buffered: second buffer at + half floats
+    int32_t o_E, o_tab, o_lat, o_ipart, o_rpart, o_misc, o_scr, o_wave, o_order;
+    int64_t half;              // U buffers: the second at + half floats (D: PC's p values there)
     int32_t s_cap;   // doubles of a wave's ring row (>= 64, >= ny * KT)
     int32_t nb_ring; // ring rows per wave (<= FIT_NB)
     int32_t o_wx;    // row weights of the current level: Wx[2][R][4] doubles (w^3/sum w^2, w^2)
     int32_t o_wk;    // dense slice weights Wk[2][ncz][Z] (w^3, w^2) of the current level
     int32_t kcap;    // krange entries per table set
     int64_t vol0;
-    float *latg;     // depth 2: [nb][2][lat_cap] the lattice before each of the last two updates
-    int32_t lat_cap;
+    double *den;     // [nb][lat_cap] fit denominators of the current level
+    int64_t lat_cap;
+    float *Tg;       // [nb][2][tcap] T(i, col) of the last two fields, col fastest (stride CZ)
+    int64_t tcap;
 };
 
 struct StudyMisc {
@@ -137,27 +114,9 @@ struct StudyMisc {
     unsigned long long sprof[4];   // emap series of thread 300 (h in range): total, hist sums, kernel exp, twiddle
 #endif
     double sd, sd2, conv;
-    int32_t nc[2][3];
-    ChainState ch[ST_NG];
-    // conv_mode 0 hand-offs between the compute waves and chain group g
-    int32_t go[ST_NG], go_op[ST_NG], go_d[ST_NG];   // request number; op 0 = run the chain on D[go_d], 1 = level end
-    int32_t ch_seq[ST_NG];     // request number of the group's last finished chain (after ch.conv)
-    int32_t gb_cnt, gb_gen;    // the compute waves' barrier
-    int32_t itn, cur, uin;     // iterations of the level, P1 buffer of the last field, U buffer
-    int32_t wd;                // a spin-wait watchdog fired (N4State.active = -2; the host raises)
-    int32_t restore;           // depth 2, at the cap: the last computed iteration is discarded
+    ChainState ch;             // PC's result (conv of the last iteration)
+    int32_t itn, uin;          // iterations of the level, U buffer of the last field
 };
-
-// Spin-wait step with a budget: ~0.5 s of s_sleep, far beyond any legitimate wait (a study's whole
-// N4 takes ~70 ms).  When it is spent the wait gives up and the kernel runs to its end with the
-// watchdog flag set, rather than leaving waves that never finish.
-#define ST_SPIN_MAX (1 << 22)
-__device__ __forceinline__ bool st_spin(int &budget, int32_t *wd) {
-    __builtin_amdgcn_s_sleep(2);
-    if (--budget > 0) return true;
-    *wd = 1;
-    return false;
-}
 
 // One level's axis tables staged in LDS.
 struct TabW {
@@ -309,29 +268,41 @@ __device__ __forceinline__ float col_T_lds(const double *P1, int i, int ncy, int
 }
 
 // eval: B_new, U = L0 - B_new, the field difference d = B_old - B_new (conv_mode 0: stored at the
-// voxel's raster rank; conv_mode 1: exact-CoV sums), U range.  SAME: the previous field uses this
-// level's tables (every iteration but the first of levels > 0), so both T windows move together at
-// the row-span boundaries; otherwise rows are taken one at a time.
+// voxel's raster rank; conv_mode 1: exact-CoV sums), U range.  The lane's column T window of the
+// new field comes from P1 in LDS and is stored to Tgn (the next iteration's old window, the same
+// control rows: the walk is the same); the old field's window is loaded from Tgo (written by the
+// previous iteration's eval with the tables of its level: the same floats a P1 of the old field
+// would give).  SAME: the previous field uses this level's tables (every
+// iteration but the first of levels > 0), so both windows move together at the row-span
+// boundaries (the old window's next row is loaded one span ahead); otherwise rows are taken one
+// at a time (To: the previous level's row tables, in global memory).
 template <bool SAME, int CM>
-__device__ void eval_item(const Item &it, int item, int Z, const TabV &Tn, const TabV &To, int ncyn,
-                          int ncyo, const double *P1n, const double *P1o, bool bo_mode,
-                          const float *Lb, float *Ub, float *Db, int64_t n, double *ipart,
-                          float4 *rpart, const PcMap &pm) {
+__device__ void eval_item(const Item &it, int item, int Z, int CZ, const TabV &Tn, const TabV &To,
+                          int ncxn, int ncyn, int ncxo, const double *P1n, float *Tgn, const float *Tgo,
+                          bool bo_mode, const float *Lb, float *Ub, float *Db, int64_t n,
+                          double *ipart, float4 *rpart, const PcMap &pm) {
     const __amdgpu_buffer_rsrc_t rL = st_rsrc(Lb, n), rU = st_rsrc(Ub, n), rD = st_rsrc(Db, n);
     const float4 wyn = it.colok ? Tn.wy[it.y] : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4 wyo = it.colok ? To.wy[it.y] : make_float4(0.f, 0.f, 0.f, 0.f);
-    const int byn = Tn.by[it.y], byo = To.by[it.y];
+    const int byn = Tn.by[it.y];
+    // T(i, col) at byte offset 4 (i CZ + col) of a buffer resource: 32-bit offsets (no 64-bit
+    // address pairs to keep live), a masked-off lane's store dropped and its load 0 by the range check
+    const __amdgpu_buffer_rsrc_t rTn = st_rsrc(Tgn, (int64_t)ncxn * CZ), rTo = st_rsrc(Tgo, (int64_t)ncxo * CZ);
+    const uint32_t cb = (uint32_t)it.col * 4u, rsz = (uint32_t)uni(CZ * 4);
     int wbn = uni(Tn.bx[it.xs]), wbo = uni(To.bx[it.xs]);
-    float tn0 = col_T_lds(P1n, wbn, ncyn, Z, byn, wyn, it.z);
-    float tn1 = col_T_lds(P1n, wbn + 1, ncyn, Z, byn, wyn, it.z);
-    float tn2 = col_T_lds(P1n, wbn + 2, ncyn, Z, byn, wyn, it.z);
-    float tn3 = col_T_lds(P1n, wbn + 3, ncyn, Z, byn, wyn, it.z);
-    float to0 = 0.f, to1 = 0.f, to2 = 0.f, to3 = 0.f;
+    auto tnew = [&](int i) {
+        const float v = col_T_lds(P1n, i, ncyn, Z, byn, wyn, it.z);
+        st_store(rTn, it.colok ? cb + (uint32_t)i * rsz : VH_OOB, v);
+        return v;
+    };
+    auto told = [&](int i) { return st_load(rTo, it.colok ? cb + (uint32_t)i * rsz : VH_OOB); };
+    float tn0 = tnew(wbn), tn1 = tnew(wbn + 1), tn2 = tnew(wbn + 2), tn3 = tnew(wbn + 3);
+    float to0 = 0.f, to1 = 0.f, to2 = 0.f, to3 = 0.f, to4 = 0.f;
     if (bo_mode) {
-        to0 = col_T_lds(P1o, wbo, ncyo, Z, byo, wyo, it.z);
-        to1 = col_T_lds(P1o, wbo + 1, ncyo, Z, byo, wyo, it.z);
-        to2 = col_T_lds(P1o, wbo + 2, ncyo, Z, byo, wyo, it.z);
-        to3 = col_T_lds(P1o, wbo + 3, ncyo, Z, byo, wyo, it.z);
+        to0 = told(wbo);
+        to1 = told(wbo + 1);
+        to2 = told(wbo + 2);
+        to3 = told(wbo + 3);
+        if (SAME) to4 = told(wbo + 4);   // (past the last control row: 0 from the range check)
     }
     double sd = 0.0, sd2 = 0.0;
     Range3 rg;
@@ -356,7 +327,7 @@ __device__ void eval_item(const Item &it, int item, int Z, const TabV &Tn, const
 #endif
         if (CM == 0) {
 #ifndef AB_EVAL_NOSTORE
-            st_store(rD, roff, (ST_EVAL_EXP && !ST_SPLIT) ? expf_cr(bo - bn) : bo - bn);
+            st_store(rD, roff, ST_EVAL_EXP ? expf_cr(bo - bn) : bo - bn);
 #else
             if (bo - bn == 12345.0f) st_store(rD, roff, u);
 #endif
@@ -414,11 +385,11 @@ __device__ void eval_item(const Item &it, int item, int Z, const TabV &Tn, const
             if (x > it.xe) break;
             ++wbn;   // next span: both windows move one control row
             tn0 = tn1; tn1 = tn2; tn2 = tn3;
-            tn3 = col_T_lds(P1n, wbn + 3, ncyn, Z, byn, wyn, it.z);
+            tn3 = tnew(wbn + 3);
             if (bo_mode) {
                 ++wbo;
-                to0 = to1; to1 = to2; to2 = to3;
-                to3 = col_T_lds(P1o, wbo + 3, ncyo, Z, byo, wyo, it.z);
+                to0 = to1; to1 = to2; to2 = to3; to3 = to4;
+                to4 = told(wbo + 4);
             }
         }
     } else {
@@ -428,13 +399,13 @@ __device__ void eval_item(const Item &it, int item, int Z, const TabV &Tn, const
             while (bxn > wbn) {
                 ++wbn;
                 tn0 = tn1; tn1 = tn2; tn2 = tn3;
-                tn3 = col_T_lds(P1n, wbn + 3, ncyn, Z, byn, wyn, it.z);
+                tn3 = tnew(wbn + 3);
             }
             const int bxo = uni(To.bx[x]);
-            while (bxo > wbo) {
+            while (bo_mode && bxo > wbo) {
                 ++wbo;
                 to0 = to1; to1 = to2; to2 = to3;
-                to3 = col_T_lds(P1o, wbo + 3, ncyo, Z, byo, wyo, it.z);
+                to3 = told(wbo + 3);
             }
             int rr = 0;
             const uint32_t off = item_off(it, x, true, CM == 0 ? &rr : nullptr);
@@ -531,33 +502,11 @@ __device__ void exact_row(const StudyArgs &a, int64_t b, const float *Ub, int x,
     }
 }
 
-// Barrier of the compute waves (conv_mode 0: the chain waves run alongside): one lane per wave
-// counts in at an LDS counter and the last flips the generation.  Workgroup-scope release before
-// (this wave's stores complete) and acquire after, as __syncthreads.
+// The workgroup's barrier (the phases below were once shared with a subset of the waves)
 struct Grp {
     int t, n, w, nw;   // thread / threads, wave / waves of the group
-    bool hw;           // the group is the whole workgroup: __syncthreads
 };
-__device__ __forceinline__ void gsync(const Grp &g, StudyMisc &M) {
-    if (g.hw) {
-        __syncthreads();
-        return;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if ((threadIdx.x & 63) == 0) {
-        const int gen = __hip_atomic_load(&M.gb_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (atomicAdd(&M.gb_cnt, 1) == g.nw - 1) {
-            __hip_atomic_store(&M.gb_cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_store(&M.gb_gen, gen + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        } else {
-            int bud = ST_SPIN_MAX;
-            while (__hip_atomic_load(&M.gb_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == gen &&
-                   st_spin(bud, &M.wd)) {
-            }
-        }
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
+__device__ __forceinline__ void gsync(const Grp &, StudyMisc &) { __syncthreads(); }
 
 __device__ float exact_min_study(const StudyArgs &a, int64_t b, const float *Ub, float *s_cmax,
                                  float *s_min, const Grp &g, StudyMisc &M) {
@@ -619,16 +568,14 @@ __device__ __forceinline__ int next_item(StudyMisc &M, const int32_t *ordr, int 
 // ---------------------------------------------------------------------------------------------
 // the kernel: one workgroup per study
 // ---------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
+// 4 waves per SIMD (<= 128 VGPRs): one 1024-thread workgroup or two 512-thread ones per CU
+__global__ void __launch_bounds__(ST_TPB, 4) k_n4_study(StudyArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int64_t b = a.vol0 + (a.order ? a.order[blockIdx.x] : (int32_t)blockIdx.x);
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     StudyMisc &M = *reinterpret_cast<StudyMisc *>(smem + a.o_misc);
     float *sE = reinterpret_cast<float *>(smem + a.o_E);
     float *lat = reinterpret_cast<float *>(smem + a.o_lat);
-    double *den = reinterpret_cast<double *>(smem + a.o_den);
-    double *const P1b0 = reinterpret_cast<double *>(smem + a.o_P10);
-    double *const P1b1 = reinterpret_cast<double *>(smem + a.o_P11);
     double *ipart = reinterpret_cast<double *>(smem + a.o_ipart);
     float4 *const rpart0 = reinterpret_cast<float4 *>(smem + a.o_rpart);   // [2][nitems]: per U buffer
     int32_t *ordr = reinterpret_cast<int32_t *>(smem + a.o_order);
@@ -636,7 +583,11 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
 
     const int64_t n = a.sc[b].n_mask1;
     N4State *stb = a.st + b;
-    if (t == 0) stb->t_start = wall_clock64();   // per-study durations (vh_batch_study_times)
+    if (t == 0) {   // per-study durations and placement (vh_batch_study_times, VH_STUDY_TRACE)
+        stb->t_start = wall_clock64();
+        stb->hw_id = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID: cu / sh / se
+        stb->xcc_id = __builtin_amdgcn_s_getreg((15 << 11) | 20);  // HW_REG_XCC_ID
+    }
     const DevLevel &lvl = a.lvs->lv[a.nlev - 1];
     const int p1last = lvl.ax[0].ncp * lvl.ax[1].ncp * a.Z;
     if (n < 2) {   // no fit: zero field (output = input), no iterations
@@ -648,64 +599,41 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
         if (t == 0) stb->t_end = wall_clock64();
         return;
     }
-    // Waves.  conv_mode 0: waves [0, ST_CW) run ITK's float Welford recurrence (S7) of each kept
-    // iteration while the other waves already compute the next iteration; ITK's while-condition on
-    // that recurrence's result then keeps the new iteration or discards it (the lattice, the U
-    // buffer and the field buffer of the last kept iteration are still there).  The arithmetic of
-    // every kept iteration is unchanged.  conv_mode 1: all waves compute, no speculation.
-    const bool split = a.conv_mode == 0 && ST_SPLIT;
     Grp g;
-    g.hw = !split;
-    if (!split) {
-        g.w = wv;
-        g.nw = ST_WAVES;
-    } else if (ST_CG == 0) {   // every wave but the chains'
-        g.w = wv - ST_CWT;
-        g.nw = ST_WAVES - ST_CWT;
-    } else {   // only waves on SIMDs 2 and 3 (wave w on SIMD w % 4): A and B keep their SIMDs
-        g.w = (wv >= 4 && (wv & 3) >= 2) ? ((wv >> 2) - 1) * 2 + (wv & 1) : -1;
-        g.nw = 2 * (ST_WAVES / 4 - 1);
-    }
-    g.t = g.w >= 0 ? g.w * 64 + lane : -1;
-    g.n = g.nw * 64;
-    const bool in_g = g.w >= 0;
+    g.w = wv;
+    g.nw = ST_WAVES;
+    g.t = t;
+    g.n = ST_TPB;
     float *Lb = a.L0 + b * a.VS;
     const int64_t fm = a.sc[b].first_masked;
-    // fit / eval scratch: lattice numerator (fixed point), then per-wave Q / S rows of the group
+    // fit scratch: lattice numerator (fixed point), then per-wave Q / S rows; from the lattice
+    // update to the end of eval: the new field's P1
     unsigned long long *numfix = reinterpret_cast<unsigned long long *>(scr);
+    double *const P1 = reinterpret_cast<double *>(scr);
+    double *const den = a.den + b * a.lat_cap;          // this level's fit denominators
+    float *const Tg0 = a.Tg + (size_t)b * 2 * a.tcap;   // T windows of the last two fields
     FitRing ring;
-    ring.q = reinterpret_cast<double *>(scr + a.o_wave) + (size_t)(in_g ? g.w : 0) * a.nb_ring * a.s_cap;
+    ring.q = reinterpret_cast<double *>(scr + a.o_wave) + (size_t)g.w * a.nb_ring * a.s_cap;
     ring.sx = nullptr;
     ring.rowcap = a.s_cap;
     ring.nr = 0;
     double *const Wk3 = reinterpret_cast<double *>(smem + a.o_wk);
-    // emap scratch: V (= U = NUM), F, DEN, twiddles, then the histogram copies
+    // emap scratch: V (= U = NUM), F, DEN, twiddles; the histogram copies in DEN (read by the
+    // series loop, which writes V and F; DEN is written after it)
     double2 *V = reinterpret_cast<double2 *>(scr), *F = V + ST_FFT_N, *DEN = F + ST_FFT_N;
     double2 *TW = DEN + ST_FFT_N;
-    unsigned long long *Hc = reinterpret_cast<unsigned long long *>(TW + VH_FFT_P / 2);
-    ChainSlot *const cslots = reinterpret_cast<ChainSlot *>(smem + a.o_chain);
-    const PcMap pm = pc_map(n, 64 * ST_CW);   // (eval_item's PC layout argument: unused here)
-    float *const latg = a.latg ? a.latg + (size_t)b * 2 * a.lat_cap : nullptr;
-    float *const latp = reinterpret_cast<float *>(smem + a.o_latp);
+    unsigned long long *Hc = reinterpret_cast<unsigned long long *>(DEN);
+    static_assert(sizeof(unsigned long long) * ST_HC * VH_MAX_BINS <= sizeof(double2) * ST_FFT_N,
+                  "histogram copies fit the DEN buffer");
+    const PcMap pm = pc_map(n, 256);   // (eval_item's PC layout argument: unused here)
     const int bins = a.bins;
 #ifdef ST_PROF
-    const int st_pt = split ? (ST_CG == 0 ? 64 * ST_CWT : 6 * 64) : 0;   // first compute thread keeps the marks
+    const int st_pt = 0;   // the thread that keeps the marks
 #endif
 
     if (t == 0) {
         M.item_ctr = 0;
-        for (int q = 0; q < ST_NG; ++q) {
-            M.go[q] = 0;
-            M.go_op[q] = 0;
-            M.go_d[q] = 0;
-            M.ch_seq[q] = 0;
-        }
-        M.restore = 0;
-        M.gb_cnt = 0;
-        M.gb_gen = 0;
-        M.cur = 0;
         M.uin = 0;
-        M.wd = 0;
     }
     if (wv == 0) find_first(a, b, fm, M);
     {   // item schedule: items by row count, largest first (ties by index), so the dynamic item
@@ -751,19 +679,14 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
     if (t == 0) M.fprof[0] = M.fprof[1] = M.fprof[2] = M.fprof[3] = 0ull;
     if (t == 0) M.sprof[0] = M.sprof[1] = M.sprof[2] = M.sprof[3] = 0ull;
 #endif
-    int ch_seen = 0;   // chain waves: the last request taken
+    int tpar = 0;   // Tg buffer of the last computed field's T windows
     for (int L = 0; L < a.nlev; ++L) {
         const DevLevel &lv = a.lvs->lv[L];
-        char *tabp = smem + ((L & 1) ? a.o_tab1 : a.o_tab0);
+        char *tabp = smem + a.o_tab;
         load_tables(tab_w(tabp, a.R, a.C, a.Z, a.kcap), lv, a.R, a.C, a.Z);
         const TabV T = tab_view(tabp, a.R, a.C, a.Z, a.kcap);
         const int ncx = lv.ax[0].ncp, ncy = lv.ax[1].ncp, ncz = lv.ax[2].ncp;
         const int nlat = ncx * ncy * ncz;
-        if (t == 0) {
-            M.nc[L & 1][0] = ncx;
-            M.nc[L & 1][1] = ncy;
-            M.nc[L & 1][2] = ncz;
-        }
         double *const Wk2 = Wk3 + (size_t)ncz * a.Z;
         for (int e = t; e < ncz * a.Z; e += ST_TPB) {   // dense slice weights of this level
             Wk3[e] = lv.wk3[e];
@@ -785,64 +708,22 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
         {
             const int uin = M.uin;
             float *const Ub = a.U + uin * a.half + b * a.VS;
-            if (in_g)
-                for (;;) {
-                    const int item = next_item(M, ordr, a.nitems);
-                    if (item < 0) break;
-                    Item it;
-                    if (!study_item(it, a, b, item)) continue;
-                    fit_item<1, true>(it, T, Wk2, Wx2, ncy, ncz, a.Z, bins, Ub, n, sE, 0.0f, 1.0, ring,
-                                      a.nb_ring, numfix);
-                }
+            for (;;) {
+                const int item = next_item(M, ordr, a.nitems);
+                if (item < 0) break;
+                Item it;
+                if (!study_item(it, a, b, item)) continue;
+                fit_item<1, true>(it, T, Wk2, Wx2, ncy, ncz, a.Z, bins, Ub, n, sE, 0.0f, 1.0, ring,
+                                  a.nb_ring, numfix);
+            }
         }
         __syncthreads();
         ST_MARK(0);
         for (int e = t; e < nlat; e += ST_TPB) den[e] = fix128_get(numfix + 2 * e, numfix + 2 * e + 1);
-        if (split && wv < ST_CWT) {
-            // ---- chain waves: group cg runs the recurrence of the iterations requested of it ----
-            // roles: 0 mu, 1 sig, 2-3 producers.  Wave w runs on SIMD w % 4, and a serial wave is
-            // issue-bound on its SIMD's VALU (4 full-wave VALU per step), so group 1 puts its mu
-            // and sig waves on SIMDs 2 and 3, beside group 0's producers
-            const int cg = wv / ST_CW, wl = (cg == 1) ? (wv % ST_CW + 2) % 4 : wv % ST_CW;
-            ChainSlot *const gslots = cslots + cg * ST_CH_NS;
-            for (;;) {
-                int req, bud = ST_SPIN_MAX;
-                while ((req = lds_load_acq(&M.go[cg])) == ch_seen && st_spin(bud, &M.wd)) {
-                }
-                if (req == ch_seen) break;   // watchdog
-                ch_seen = req;
-                if (M.go_op[cg]) break;   // level end
-                const float *const Dk = a.D + M.go_d[cg] * a.half + b * a.VS;
-                if (wl == 0) {
-                    chain_wave_mu<ST_CH_NS>(n, gslots, &M.ch[cg]);
-                } else if (wl == 1) {
-                    chain_wave_sig<ST_CH_NS>(n, gslots, &M.ch[cg]);
-                    wave_lds_order();
-                    if (lane == 0) lds_store_rel(&M.ch_seq[cg], req);   // after ch.conv
-                } else {
-                    chain_wave_prod<ST_CH_NS>(Dk, nullptr, n, gslots, &M.ch[cg], wl - 2, ST_CH_PROD);
-                }
-            }
-        } else if (in_g) {
-            // ---- the iterations (compute waves) ----
-            int itn = 0;          // iterations computed in this level (split: the last ST_DEPTH undecided)
-            int cur = M.cur;      // P1 buffer of the last computed field
-            int uin = M.uin;      // U buffer (and its rpart row) of the last computed iteration
-            // (thread g.t == 0) the recurrence of iteration j: wait for it / request it of group j % ST_NG
-            auto cwait = [&](int j) -> float {
-                const int q = j % ST_NG;
-                int bud = ST_SPIN_MAX;
-                while (lds_load_acq(&M.ch_seq[q]) != M.go[q] && st_spin(bud, &M.wd)) {
-                }
-                return M.ch[q].conv;
-            };
-            auto creq = [&](int j) {
-                const int q = j % ST_NG;
-                for (int i = 0; i < ST_CH_NS; ++i) chain_reset<ST_CH_NS>(cslots + q * ST_CH_NS, &M.ch[q], i);
-                M.go_op[q] = 0;
-                M.go_d[q] = j % ST_NB;
-                lds_store_rel(&M.go[q], M.go[q] + 1);
-            };
+        {
+            // ---- the iterations ----
+            int itn = 0;       // iterations computed in this level
+            int uin = M.uin;   // U buffer (and its rpart row) of the last computed iteration
             for (;;) {
                 gsync(g, M);
                 ST_MARK(10);
@@ -863,28 +744,9 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                     if (lane == 0) {
                         M.stop = 0;
                         M.exact = 0;
-                        M.restore = 0;
                         if (itn > 0) {
-                            if (split) {
-                                if (itn >= a.lvs->max_iters[L]) {   // no speculation past the cap
-                                    M.stop = 1;
-                                    if (ST_DEPTH == 1 || itn == 1) {
-                                        M.conv = (double)cwait(itn);
-                                    } else {   // iteration itn runs iff conv(itn - 1) > threshold
-                                        const float c1 = cwait(itn - 1);
-                                        const float c2 = cwait(itn);
-                                        if (!(c1 > a.thresh)) {
-                                            M.conv = (double)c1;
-                                            M.restore = 1;
-                                        } else {
-                                            M.conv = (double)c2;
-                                        }
-                                    }
-                                }
-                            } else {
-                                if (a.conv_mode == 1) M.conv = conv_of(M.sd, M.sd2, (double)n);
-                                if (!(M.conv > (double)a.thresh) || itn >= a.lvs->max_iters[L]) M.stop = 1;
-                            }
+                            if (a.conv_mode == 1) M.conv = conv_of(M.sd, M.sd2, (double)n);
+                            if (!(M.conv > (double)a.thresh) || itn >= a.lvs->max_iters[L]) M.stop = 1;
                         }
                         if (!M.stop) {
                             float bmin;
@@ -900,16 +762,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                 }
                 gsync(g, M);
                 ST_MARK(1);
-                if (M.stop) {
-                    if (M.restore) {   // depth 2 at the cap: iteration itn discarded (its field's
-                        // P1 is in buffer cur, the previous one's still in the other)
-                        for (int e = g.t; e < nlat; e += g.n) lat[e] = latg[(size_t)(itn & 1) * a.lat_cap + e];
-                        cur ^= 1;
-                        uin = (uin + ST_NB - 1) % ST_NB;
-                        itn -= 1;
-                    }
-                    break;
-                }
+                if (M.stop) break;
                 if (M.exact) {
                     float *s_cmax = reinterpret_cast<float *>(scr);
                     const float m = exact_min_study(a, b, Ub, s_cmax, s_cmax + g.n, g, M);
@@ -956,7 +809,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                     const float sFWHM = a.fwhm / slope;
                     const float ef = (float)(4.0 * LN2 / (double)(sFWHM * sFWHM));
                     const float sf = (float)(2.0 * sqrt(LN2 / PI_D) / (double)sFWHM);
-                    // one twiddle per thread: P / 2 <= g.n (ST_TPB - 64 ST_CW)
+                    // one twiddle per thread: P / 2 <= g.n
 #ifdef ST_PROF
                     const unsigned long long sp0 = clock64();
 #endif
@@ -1056,42 +909,43 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                 }
                 gsync(g, M);
                 ST_MARK(4);
-                // ---- lattice update (the kept lattice saved first) and P1 ----
+                // ---- lattice update and P1 (in the fit scratch, free from here to the end of eval) ----
                 for (int e = g.t; e < nlat; e += g.n) {
                     const double d = den[e];
                     const double num = fix128_get(numfix + 2 * e, numfix + 2 * e + 1);
                     const float phi = d != 0.0 ? (float)(num / d) : 0.0f;
-                    if (split) {
-                        if (ST_DEPTH == 1) latp[e] = lat[e];
-                        else latg[(size_t)(itk & 1) * a.lat_cap + e] = lat[e];
-                    }
                     lat[e] += phi;
                 }
                 gsync(g, M);
-                double *P1n = cur ? P1b0 : P1b1;
-                double *P1o = cur ? P1b1 : P1b0;
                 for (int e = g.t; e < ncx * ncy * a.Z; e += g.n) {
                     const int ij = e / a.Z, z = e % a.Z;
                     const float4 w = T.wz[z];
                     const float *l = lat + ij * ncz + T.bz[z];
-                    P1n[e] = (double)w.x * (double)l[0] + (double)w.y * (double)l[1] +
-                             (double)w.z * (double)l[2] + (double)w.w * (double)l[3];
+                    P1[e] = (double)w.x * (double)l[0] + (double)w.y * (double)l[1] +
+                            (double)w.z * (double)l[2] + (double)w.w * (double)l[3];
                 }
                 if (g.t == 0) M.item_ctr = 0;
                 gsync(g, M);
                 ST_MARK(5);
-                // ---- eval: U into the other buffer, d into D[itk & 1] ----
+                // ---- eval: U into the other buffer, d into D, this field's T windows into Tg ----
                 {
                     const int uo = (uin + 1) % ST_NB;
                     float *const Uo = a.U + uo * a.half + b * a.VS;
-                    float *const Dw = a.D + (split ? (itk % ST_NB) * a.half : 0) + b * a.VS;
+                    float *const Dw = a.D + b * a.VS;
                     float4 *const rp_out = rpart0 + uo * a.nitems;
                     const bool first_of_level = itk == 1;
                     const bool bo_mode = !(L == 0 && first_of_level);
-                    const int so = (first_of_level && L > 0) ? ((L - 1) & 1) : (L & 1);
-                    const TabV To = tab_view(smem + (so ? a.o_tab1 : a.o_tab0), a.R, a.C, a.Z, a.kcap);
-                    const int ncyo = M.nc[so][1];
-                    const bool same = so == (L & 1);
+                    const bool same = !(first_of_level && L > 0);
+                    TabV To = T;   // first iteration of a level > 0: the old field's row tables
+                    int ncxo = ncx;
+                    if (!same) {
+                        const DevLevel &lo = a.lvs->lv[L - 1];
+                        To.wx = reinterpret_cast<const float4 *>(lo.ax[0].w);
+                        To.bx = lo.ax[0].base;
+                        ncxo = lo.ax[0].ncp;
+                    }
+                    float *const Tgn = Tg0 + (size_t)(tpar ^ 1) * a.tcap;
+                    const float *const Tgo = Tg0 + (size_t)tpar * a.tcap;
                     for (;;) {
                         const int item = next_item(M, ordr, a.nitems);
                         if (item < 0) break;
@@ -1104,72 +958,30 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                             }
                             continue;
                         }
+#define ST_EVAL(S, CM) eval_item<S, CM>(it, item, a.Z, a.CZ, T, To, ncx, ncy, ncxo, P1, Tgn, Tgo, bo_mode, \
+                                        Lb, Uo, Dw, n, ipart, rp_out, pm)
                         if (a.conv_mode == 0) {
-                            if (same)
-                                eval_item<true, 0>(it, item, a.Z, T, To, ncy, ncyo, P1n, P1o, bo_mode, Lb, Uo, Dw, n, ipart, rp_out, pm);
-                            else
-                                eval_item<false, 0>(it, item, a.Z, T, To, ncy, ncyo, P1n, P1o, bo_mode, Lb, Uo, Dw, n, ipart, rp_out, pm);
+                            if (same) ST_EVAL(true, 0);
+                            else ST_EVAL(false, 0);
                         } else {
-                            if (same)
-                                eval_item<true, 1>(it, item, a.Z, T, To, ncy, ncyo, P1n, P1o, bo_mode, Lb, Uo, Dw, n, ipart, rp_out, pm);
-                            else
-                                eval_item<false, 1>(it, item, a.Z, T, To, ncy, ncyo, P1n, P1o, bo_mode, Lb, Uo, Dw, n, ipart, rp_out, pm);
+                            if (same) ST_EVAL(true, 1);
+                            else ST_EVAL(false, 1);
                         }
+#undef ST_EVAL
                     }
                 }
                 gsync(g, M);
                 ST_MARK(6);
-                // ---- keep iteration itk or not ----
-                if (split) {
-                    if (g.t == 0) {
-                        M.stop = 0;
-                        if (ST_DEPTH == 1) {
-                            if (itn > 0) {   // ITK's while-condition on iteration itn's recurrence
-                                const float c = cwait(itn);
-                                M.conv = (double)c;
-                                if (!(c > a.thresh)) M.stop = 1;
-                            }
-                        } else if (itk >= 3) {   // iteration itk - 1 runs iff conv(itk - 2) > threshold
-                            const float c = cwait(itk - 2);
-                            if (!(c > a.thresh)) {
-                                (void)cwait(itk - 1);   // drain the other group
-                                M.conv = (double)c;
-                                M.stop = 1;
-                            }
-                        }
-                        if (!M.stop) creq(itk);   // the recurrence of iteration itk
-                    }
-                    gsync(g, M);
-                    if (M.stop) {
-                        if (ST_DEPTH == 1) {   // discard iteration itk: the kept lattice goes back
-                            for (int e = g.t; e < nlat; e += g.n) lat[e] = latp[e];
-                        } else {   // discard itk - 1 and itk: the lattice before itk - 1's update,
-                            // its P1 recomputed into the buffer of itk - 1's field, U of itk - 2
-                            for (int e = g.t; e < nlat; e += g.n) lat[e] = latg[(size_t)((itk - 1) & 1) * a.lat_cap + e];
-                            gsync(g, M);
-                            for (int e = g.t; e < ncx * ncy * a.Z; e += g.n) {
-                                const int ij = e / a.Z, z = e % a.Z;
-                                const float4 w = T.wz[z];
-                                const float *l = lat + ij * ncz + T.bz[z];
-                                P1o[e] = (double)w.x * (double)l[0] + (double)w.y * (double)l[1] +
-                                         (double)w.z * (double)l[2] + (double)w.w * (double)l[3];
-                            }
-                            uin = (uin + ST_NB - 1) % ST_NB;
-                            itn = itk - 2;
-                            gsync(g, M);
-                        }
-                        break;
-                    }
-                } else if (a.conv_mode == 0) {   // S7 on the whole workgroup (ST_PC 2)
+                if (a.conv_mode == 0) {   // S7 on the whole workgroup by guess and verify
                     PcShared<ST_TPB> &PW = *reinterpret_cast<PcShared<ST_TPB> *>(smem + a.o_scr);
                     const float *const Dr = a.D + b * a.VS;
                     // the raster d buffer is free once pass 0 has read it: PCX's stored increments
                     // below the iteration cap this iteration's measure only decides whether the
                     // level goes on: PC may certify "above the threshold" without the exact sig
-                    pcw_run<ST_TPB, ST_EVAL_EXP && !ST_SPLIT>([=](int64_t r) { return Dr[r]; }, a.D + a.half + b * a.VS, n, PW, M.ch[0], itk,
+                    pcw_run<ST_TPB, ST_EVAL_EXP>([=](int64_t r) { return Dr[r]; }, a.D + a.half + b * a.VS, n, PW, M.ch, itk,
                             reinterpret_cast<double *>(a.D + b * a.VS), (int)(a.VS / 2),
                             itk < a.lvs->max_iters[L] ? a.thresh : 0.0f);
-                    if (t == 0) M.conv = (double)M.ch[0].conv;
+                    if (t == 0) M.conv = (double)M.ch.conv;
                 } else if (g.w == 0) {   // S7x: item partials in item order
                     double sd = 0.0, sd2 = 0.0;
                     for (int i = lane; i < a.nitems; i += 64) {
@@ -1186,19 +998,13 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                     }
                 }
                 ST_MARK(7);
-                cur ^= 1;
+                tpar ^= 1;
                 uin = (uin + 1) % ST_NB;
                 itn = itk;
             }
             if (g.t == 0) {
                 M.itn = itn;
-                M.cur = cur;
                 M.uin = uin;
-                if (split)   // level end: release the chain waves (every requested chain has finished)
-                    for (int q = 0; q < ST_NG; ++q) {
-                        M.go_op[q] = 1;
-                        lds_store_rel(&M.go[q], M.go[q] + 1);
-                    }
             }
         }
         __syncthreads();
@@ -1225,7 +1031,7 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
 #define ST_PROF_B 0
 #endif
     if (t == st_pt && b == ST_PROF_B) {
-        int its = 0;   // (st_pt is thread 0, the writer of iters_level, when no chain waves split off)
+        int its = 0;   // (st_pt is thread 0, the writer of iters_level)
         for (int q = 0; q < a.nlev; ++q) its += stb->iters_level[q];
         printf("ST_PROF b %d n %lld its %d den %llu ctrl %llu hist %llu emap %llu fit %llu latP1 %llu eval %llu "
                "wait %llu level %llu exact %llu top %llu | emap: series %llu fwd %llu filter %llu conv %llu div %llu\n",
@@ -1238,12 +1044,20 @@ __global__ void __launch_bounds__(ST_TPB) k_n4_study(StudyArgs a) {
                M.fprof[2], M.fprof[3], M.sprof[0], M.sprof[1], M.sprof[2], M.sprof[3]);
     }
 #endif
-    // final field's P1 for k_n4_final
-    const double *P1f = M.cur ? P1b1 : P1b0;
-    for (int e = t; e < p1last; e += ST_TPB) a.P1out[b * a.q2cap + e] = P1f[e];
+    {   // final field's P1 for k_n4_final, from the lattice (the last level's tables are loaded)
+        const TabV T = tab_view(smem + a.o_tab, a.R, a.C, a.Z, a.kcap);
+        const int ncz = lvl.ax[2].ncp;
+        for (int e = t; e < p1last; e += ST_TPB) {
+            const int ij = e / a.Z, z = e % a.Z;
+            const float4 w = T.wz[z];
+            const float *l = lat + ij * ncz + T.bz[z];
+            a.P1out[b * a.q2cap + e] = (double)w.x * (double)l[0] + (double)w.y * (double)l[1] +
+                                       (double)w.z * (double)l[2] + (double)w.w * (double)l[3];
+        }
+    }
     if (t == 0) {
         stb->conv = M.conv;
-        stb->active = M.wd ? -2 : 0;
+        stb->active = 0;
         stb->t_end = wall_clock64();
     }
 }
@@ -1296,31 +1110,24 @@ static bool study_layout(const vh_batch *b, const vh_n4_params &prm, StudyLayout
     }
     // refinement temporaries: two lattices of the next level (<= 8x the current)
     const size_t refine = 2 * sizeof(float) * (size_t)nlat_max + 64;
-    const size_t emap = sizeof(double2) * (3 * ST_FFT_N + VH_FFT_P / 2) +
-                        sizeof(unsigned long long) * ST_HC * VH_MAX_BINS;
+    const size_t emap = sizeof(double2) * (3 * ST_FFT_N + VH_FFT_P / 2);   // (histogram copies in DEN)
     const bool geom_ok = s_cap <= 64 * FIT_SO;   // one ring row's stage-1 outputs fit the lanes
     s_cap = std::max(s_cap, 64);
-    // conv_mode 0: ST_CW waves run the recurrence beside the compute waves (own slot ring, the
-    // lattice kept for a discarded iteration); the fit rings are the compute waves' only
-    const bool split = prm.conv_mode == 0 && ST_SPLIT;
-    const int fit_waves = !split ? ST_WAVES : ST_CG == 0 ? ST_WAVES - ST_CWT : 2 * (ST_WAVES / 4 - 1);
-    // ring rows per wave: up to FIT_NB within ~32 KB for the computing waves
+    const int fit_waves = ST_WAVES;
+    // ring rows per wave: up to FIT_NB within ~32 KB
     const int nb_ring = std::max(1, std::min(FIT_NB, (int)(32768 / (fit_waves * 8 * (size_t)s_cap))));
     const size_t fit_num = 2 * sizeof(unsigned long long) * (size_t)nlat_max;
     const size_t fit = ((fit_num + 15) & ~(size_t)15) + sizeof(double) * fit_waves * nb_ring * (size_t)s_cap;
     const size_t exact = sizeof(float) * 2 * ST_TPB;
-    const size_t pcs = (prm.conv_mode == 0 && !ST_SPLIT) ? sizeof(PcShared<ST_TPB>) : 0;
-    const size_t scr = std::max({refine, emap, fit, exact, pcs});
+    const size_t pcs = prm.conv_mode == 0 ? sizeof(PcShared<ST_TPB>) : 0;
+    const size_t p1 = sizeof(double) * (size_t)p1_max;   // the new field's P1, lattice update to eval
+    const size_t scr = std::max({refine, emap, fit, exact, pcs, p1});
     auto A = [](size_t v) { return (v + 15) & ~(size_t)15; };
     size_t o = 0;
     a.o_E = (int32_t)o; o += A(sizeof(float) * VH_MAX_BINS);
     const size_t tb = study_tab_bytes(R, C, Z, kcap);
-    a.o_tab0 = (int32_t)o; o += tb;
-    a.o_tab1 = (int32_t)o; o += tb;
+    a.o_tab = (int32_t)o; o += tb;
     a.o_lat = (int32_t)o; o += A(sizeof(float) * nlat_max);
-    a.o_den = (int32_t)o; o += A(sizeof(double) * nlat_max);
-    a.o_P10 = (int32_t)o; o += A(sizeof(double) * p1_max);
-    a.o_P11 = (int32_t)o; o += A(sizeof(double) * p1_max);
     const int64_t nslots = (b->R + SLOT_R - 1) / SLOT_R;
     const int64_t nitems = b->n4_tiles * nslots;
     a.o_ipart = (int32_t)o; o += A(sizeof(double) * 2 * (size_t)nitems);
@@ -1330,10 +1137,6 @@ static bool study_layout(const vh_batch *b, const vh_n4_params &prm, StudyLayout
     a.o_wk = (int32_t)o; o += A(2 * sizeof(double) * (size_t)kcap * Z);
     a.o_wx = (int32_t)o; o += A(2 * 4 * sizeof(double) * (size_t)R);
     a.o_scr = (int32_t)o; o += A(scr);
-    a.o_chain = (int32_t)o;
-    o += split ? A(sizeof(ChainSlot) * ST_CH_NS * ST_NG) : 0;
-    a.o_latp = (int32_t)o; o += (split && ST_DEPTH == 1) ? A(sizeof(float) * nlat_max) : 0;
-    a.lat_cap = nlat_max;
     a.o_wave = (int32_t)((fit_num + 15) & ~(size_t)15);   // ring offset inside the scratch
     a.s_cap = s_cap;
     a.nb_ring = nb_ring;
@@ -1400,20 +1203,34 @@ void vh_launch_n4_study(vh_batch *b, const vh_n4_params &prm) {
         VH_CHECK_LAUNCH();
         a.order = b->d_study_order;
     }
-    a.latg = nullptr;
-    if (prm.conv_mode == 0 && ST_SPLIT && ST_DEPTH == 2) {   // the two lattice saves per study
-        const size_t need = sizeof(float) * 2 * (size_t)a.lat_cap * (size_t)b->nb;
-        if (need > b->study_latg_cap) {
-            if (b->d_study_latg) HIP_TRY(hipFree(b->d_study_latg));
-            b->d_study_latg = nullptr;
-            b->study_latg_cap = 0;
-            HIP_TRY(hipMalloc(&b->d_study_latg, need));
-            b->study_latg_cap = need;
-        }
-        a.latg = (float *)b->d_study_latg;
+    // global state of the study: the fit denominators and the two T-window buffers (the sweep
+    // driver's d_den / d_T, vh_ensure_n4_workspace)
+    {
+        const int Lf = prm.n_levels - 1;
+        const int64_t cx = vh_level_ncp(prm, Lf, 0);
+        const int64_t nl = cx * vh_level_ncp(prm, Lf, 1) * vh_level_ncp(prm, Lf, 2);
+        if (!b->d_den || !b->d_T || b->lat_cap < nl || b->t_cap < cx * b->CZ)
+            throw VhError{VH_ERR_ARG, "N4 study kernel: workspace not prepared"};
     }
+    a.den = b->d_den;
+    a.lat_cap = b->lat_cap;
+    a.Tg = b->d_T;
+    a.tcap = b->t_cap;
     vh_set_max_lds((const void *)k_n4_study, ST_MAX_LDS);
+    size_t lds = Ly.bytes;
+    if (const char *e = getenv("VH_ST_MIN_LDS"))   // A/B runs: more LDS than needed, fewer studies per CU
+        lds = std::max(lds, std::min((size_t)atoll(e), (size_t)ST_MAX_LDS));
     ScopedKTimer tm(b, "n4_study", 0.0);
-    k_n4_study<<<(unsigned)b->nb, ST_TPB, Ly.bytes, b->stream>>>(a);
+    hipStream_t ks = b->stream;
+    if (b->st_n4) {   // VH_PRIO: the study kernel on the batch's low-priority stream, in order
+        HIP_TRY(hipEventRecord(b->ev_n4_pre, b->stream));
+        HIP_TRY(hipStreamWaitEvent(b->st_n4, b->ev_n4_pre, 0));
+        ks = b->st_n4;
+    }
+    k_n4_study<<<(unsigned)b->nb, ST_TPB, lds, ks>>>(a);
     VH_CHECK_LAUNCH();
+    if (b->st_n4) {
+        HIP_TRY(hipEventRecord(b->ev_n4_post, b->st_n4));
+        HIP_TRY(hipStreamWaitEvent(b->stream, b->ev_n4_post, 0));
+    }
 }

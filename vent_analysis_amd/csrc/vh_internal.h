@@ -87,6 +87,7 @@ struct N4State {
     int32_t iters_level[VH_MAX_LEVELS];
     float conv_level[VH_MAX_LEVELS];
     uint64_t t_start, t_end;   // k_n4_study: device wall clock (wall_clock64) at the workgroup's start / end
+    uint32_t hw_id, xcc_id;    // k_n4_study: where the workgroup ran (HW_REG_HW_ID / HW_REG_XCC_ID)
 };
 
 // Per-axis, per-level B-spline tables (host-built, identical to oracle/n4_oracle.c).
@@ -154,6 +155,8 @@ struct vh_pipe {
 struct vh_batch {
     vh_ctx *ctx = nullptr;
     hipStream_t stream = nullptr;    // every launch and copy of this batch (batches overlap)
+    hipStream_t st_n4 = nullptr;     // VH_PRIO: the study kernel alone on a low-priority stream (the
+    hipEvent_t ev_n4_pre = nullptr, ev_n4_post = nullptr;   // rest on a high-priority one), joined by events
     int32_t *h_flags = nullptr;      // pinned: the sweep driver's per-iteration active counts
     int64_t R = 0, C = 0, Z = 0, V = 0, nb = 0, CZ = 0;
     int64_t max_tiles = 0;
