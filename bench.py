@@ -252,45 +252,12 @@ def host_to_host(R, C, Z, nb, args, device, opts, seed, aligned=True):
 
 def link_probe(device, mb=256):
     """This box's PCIe link with pinned host memory: H2D alone, D2H alone and both at once on two
-    streams (as the pipe's overlapped chunks use it), best of 3 each.  The host-to-host line can
-    not beat link rate / PCIe bytes per volume, whatever the device-resident rate."""
-    import torch
-    n = mb << 20
-    dev = torch.device("cuda", device)
-    h_in = torch.empty(n, dtype=torch.uint8, pin_memory=True)
-    h_out = torch.empty(n, dtype=torch.uint8, pin_memory=True)
-    d_in = torch.empty(n, dtype=torch.uint8, device=dev)
-    d_out = torch.empty(n, dtype=torch.uint8, device=dev)
-    s1, s2 = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
-
-    def h2d():
-        with torch.cuda.stream(s1):
-            d_in.copy_(h_in, non_blocking=True)
-
-    def d2h():
-        with torch.cuda.stream(s2):
-            h_out.copy_(d_out, non_blocking=True)
-
-    def both():
-        h2d()
-        d2h()
-
-    def best(fn):
-        ts = []
-        for _ in range(3):
-            torch.cuda.synchronize(dev)
-            t = time.perf_counter()
-            fn()
-            torch.cuda.synchronize(dev)
-            ts.append(time.perf_counter() - t)
-        return min(ts)
-
-    both()
-    torch.cuda.synchronize(dev)
-    t1, t2, t3 = best(h2d), best(d2h), best(both)
-    del h_in, h_out, d_in, d_out
-    return {"bytes_each_way": n, "h2d_GBps": round(n / t1 / 1e9, 2),
-            "d2h_GBps": round(n / t2 / 1e9, 2), "both_GBps": round(2 * n / t3 / 1e9, 2)}
+    streams (as the pipe's overlapped chunks use it), best of 3 each (vh_link_probe).  The
+    host-to-host line can not beat link rate / PCIe bytes per volume, whatever the device rate."""
+    from vent_analysis_amd import _lib
+    r = _lib.context(device).link_probe(mb << 20)
+    r["bytes_each_way"] = mb << 20
+    return r
 
 
 def link_bound(link, R, C, Z):
@@ -484,11 +451,11 @@ def main():
                          "cohort all-reduce per step)")
     ap.add_argument("--no-h2h", action="store_true",
                     help="skip the host-to-host pipeline measurement (host_to_host_vol_s)")
-    ap.add_argument("--h2h-batches", type=int, default=6,
+    ap.add_argument("--h2h-batches", type=int, default=12,
                     help="host-to-host sample: this many x --batch volumes")
-    ap.add_argument("--h2h-sub", type=int, default=128,
+    ap.add_argument("--h2h-sub", type=int, default=224,
                     help="host-to-host: studies per pipeline sub-batch")
-    ap.add_argument("--h2h-slots", type=int, default=4,
+    ap.add_argument("--h2h-slots", type=int, default=3,
                     help="host-to-host: pipeline slots (sub-batches in flight, <= 8)")
     ap.add_argument("--inflight", type=int, default=2,
                     help="device batches in flight: steps of consecutive batches overlap on their own "

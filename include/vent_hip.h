@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define VH_ABI_VERSION 5
+#define VH_ABI_VERSION 6
 
 /* status codes */
 #define VH_OK 0
@@ -224,6 +224,9 @@ int vh_pipe_destroy(vh_pipe *p);
  * went through the pinned staging instead (not registrable, or past the VH_PIPE_PIN_CAP budget,
  * default 32 GiB: a long cohort run never page-locks more than that at once). */
 int vh_pipe_stats(vh_pipe *p, int64_t *pinned_peak_bytes, int64_t *staged_spans);
+/* This GPU's PCIe link with pinned host memory (bench.py's host-to-host bound): bytes copied H2D
+ * alone, D2H alone and both at once on two streams, best of 3; out_gbps = {h2d, d2h, both}. */
+int vh_link_probe(vh_ctx *ctx, int64_t bytes, double out_gbps[3]);
 
 /* ---- multi-GPU (RCCL over xGMI) -------------------------------------------------------------- */
 #define VH_COMM_ID_BYTES 128

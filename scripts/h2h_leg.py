@@ -1,7 +1,7 @@
 """The host-to-host leg of bench.py alone (for rocprofv3 --kernel-trace --memory-copy-trace and
 VH_PIPE_TRACE runs): n = batches x 256 heterogeneous studies streamed through vh_pipe.
 
-  python3 scripts/h2h_leg.py [--slots 4] [--sub 128] [--batches 6] [--keep-batch]
+  python3 scripts/h2h_leg.py [--slots 3] [--sub 224] [--batches 12] [--keep-batch]
 
 --keep-batch also holds a 256-study device batch (and its stream) open, as bench.py did in
 round 3 while it measured this leg."""
@@ -18,9 +18,9 @@ import bench  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--slots", type=int, default=4)
-    ap.add_argument("--sub", type=int, default=128)
-    ap.add_argument("--batches", type=int, default=6)
+    ap.add_argument("--slots", type=int, default=3)
+    ap.add_argument("--sub", type=int, default=224)
+    ap.add_argument("--batches", type=int, default=12)
     ap.add_argument("--keep-batch", action="store_true")
     ap.add_argument("--unaligned", action="store_true", help="plain np.empty host arrays")
     ap.add_argument("--torch", action="store_true", help="initialise torch's HIP context first (as bench.py does)")

@@ -94,6 +94,7 @@ _SIGS = {
     "vh_pipe_run": ([_P, _P, _P, _I64, ct.POINTER(RunOpts), _P, _P, _P, _P, _P], ct.c_int),
     "vh_pipe_destroy": ([_P], ct.c_int),
     "vh_pipe_stats": ([_P, ct.POINTER(ct.c_int64), ct.POINTER(ct.c_int64)], ct.c_int),
+    "vh_link_probe": ([_P, ct.c_int64, ct.POINTER(ct.c_double)], ct.c_int),
     "vh_comm_unique_id": ([_P], ct.c_int),
     "vh_comm_init": ([_P, ct.c_int, ct.c_int, _P], ct.c_int),
     "vh_batch_cohort_allreduce": ([_P], ct.c_int),
@@ -152,6 +153,13 @@ class Context:
         self.h = h
         self.device = device
         self.ci_tables = {}   # id(SphereTable) -> (table, vh_ci_table handle): tables stay in HBM
+
+    def link_probe(self, nbytes=256 << 20):
+        """PCIe rates of this context's GPU with pinned host memory, GB/s: H2D alone, D2H alone,
+        both at once on two streams (vh_link_probe)."""
+        out = (ct.c_double * 3)()
+        self.check(self.L.vh_link_probe(self.h, int(nbytes), out), "vh_link_probe")
+        return {"h2d_GBps": round(out[0], 2), "d2h_GBps": round(out[1], 2), "both_GBps": round(out[2], 2)}
 
     def ci_table(self, table, R, C):
         """The device copy of a compact sphere table for (R, C) volumes (vh_ci_table_create, once
@@ -507,7 +515,7 @@ class Pipe:
     """Host-to-host pipeline (vh_pipe): n host-resident studies streamed through `slots` device
     batches of `sub` volumes, transfers of one sub-batch overlapping the compute of another."""
 
-    def __init__(self, R, C, Z, sub, slots=4, device=0):
+    def __init__(self, R, C, Z, sub, slots=3, device=0):
         self.ctx = context(device)
         self.L = self.ctx.L
         self.vshape = (int(R), int(C), int(Z))

@@ -130,18 +130,38 @@ static vh_batch *batch_new(vh_ctx *ctx, int64_t R, int64_t C, int64_t Z, int64_t
     HIP_TRY(hipSetDevice(ctx->device));
     vh_batch *b = new vh_batch;
     b->ctx = ctx;
-    // VH_PRIO=1: the batch's stream at the highest priority and its study kernel on a second stream
-    // at the lowest, so when CUs free up the dispatcher serves the short kernels of other batches
-    // (their next study launch waits on them) before more studies
-    const char *pe = getenv("VH_PRIO");
+    // Study-kernel stream (A/B options, off by default).  VH_PRIO=1: the batch's stream at the
+    // highest priority and its study kernel on a second stream at the lowest.  VH_ST_RESERVE=k
+    // (1-4): the study kernel on a second stream whose CU mask leaves k CUs per XCD to the batch's
+    // other kernels (mask bits 33 j + 8 m, j < 8, m < k: one per XCD whether the bits map to XCDs
+    // in blocks of 32 or interleaved), so another batch's short kernels never wait for a CU that
+    // studies hold.
+    const char *pe = getenv("VH_PRIO"), *re = getenv("VH_ST_RESERVE");
     const bool prio = pe && atoi(pe) != 0;
+    const int reserve = re ? std::max(0, std::min(4, atoi(re))) : 0;
     int lo = 0, hi = 0;
     if (prio) (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-    if ((prio ? hipStreamCreateWithPriority(&b->stream, hipStreamNonBlocking, hi)
-              : hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking)) != hipSuccess ||
-        (prio && (hipStreamCreateWithPriority(&b->st_n4, hipStreamNonBlocking, lo) != hipSuccess ||
-                  hipEventCreateWithFlags(&b->ev_n4_pre, hipEventDisableTiming) != hipSuccess ||
-                  hipEventCreateWithFlags(&b->ev_n4_post, hipEventDisableTiming) != hipSuccess))) {
+    hipError_t se = prio ? hipStreamCreateWithPriority(&b->stream, hipStreamNonBlocking, hi)
+                         : hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking);
+    if (se == hipSuccess && reserve > 0) {
+        int ncu = 0;
+        (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, ctx->device);
+        std::vector<uint32_t> mask((size_t)(ncu + 31) / 32, 0xffffffffu);
+        for (int j = 0; j < 8; ++j)
+            for (int m = 0; m < reserve; ++m) {
+                const int i = 33 * j + 8 * m;
+                if (i < ncu) mask[i / 32] &= ~(1u << (i % 32));
+            }
+        se = hipExtStreamCreateWithCUMask(&b->st_n4, (uint32_t)mask.size(), mask.data());
+    } else if (se == hipSuccess && prio) {
+        se = hipStreamCreateWithPriority(&b->st_n4, hipStreamNonBlocking, lo);
+    }
+    if (se == hipSuccess && b->st_n4)
+        se = hipEventCreateWithFlags(&b->ev_n4_pre, hipEventDisableTiming);
+    if (se == hipSuccess && b->st_n4)
+        se = hipEventCreateWithFlags(&b->ev_n4_post, hipEventDisableTiming);
+    if (se != hipSuccess) {
+        if (b->ev_n4_pre) (void)hipEventDestroy(b->ev_n4_pre);
         if (b->stream) (void)hipStreamDestroy(b->stream);
         if (b->st_n4) (void)hipStreamDestroy(b->st_n4);
         delete b;
@@ -1368,6 +1388,59 @@ int vh_pipe_stats(vh_pipe *p, int64_t *pinned_peak_bytes, int64_t *staged_spans)
     if (pinned_peak_bytes) *pinned_peak_bytes = p->pinned_peak.load();
     if (staged_spans) *staged_spans = p->staged_spans.load();
     return VH_OK;
+}
+
+int vh_link_probe(vh_ctx *ctx, int64_t bytes, double out_gbps[3]) {
+    API_TRY(ctx, {
+        std::lock_guard<std::mutex> lock(ctx->mu);
+        if (!out_gbps || bytes <= 0) throw VhError{VH_ERR_ARG, "link probe: bad arguments"};
+        HIP_TRY(hipSetDevice(ctx->device));
+        void *h_in = nullptr, *h_out = nullptr, *d_in = nullptr, *d_out = nullptr;
+        hipStream_t s[2] = {nullptr, nullptr};
+        hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+        auto release = [&]() {
+            for (auto e : ev) if (e) (void)hipEventDestroy(e);
+            for (auto x : s) if (x) (void)hipStreamDestroy(x);
+            if (h_in) (void)hipHostFree(h_in);
+            if (h_out) (void)hipHostFree(h_out);
+            if (d_in) (void)hipFree(d_in);
+            if (d_out) (void)hipFree(d_out);
+        };
+        try {
+            HIP_TRY(hipHostMalloc(&h_in, (size_t)bytes, hipHostMallocDefault));
+            HIP_TRY(hipHostMalloc(&h_out, (size_t)bytes, hipHostMallocDefault));
+            HIP_TRY(hipMalloc(&d_in, (size_t)bytes));
+            HIP_TRY(hipMalloc(&d_out, (size_t)bytes));
+            std::memset(h_in, 1, (size_t)bytes);
+            std::memset(h_out, 2, (size_t)bytes);
+            for (auto &x : s) HIP_TRY(hipStreamCreateWithFlags(&x, hipStreamNonBlocking));
+            for (auto &e : ev) HIP_TRY(hipEventCreate(&e));
+            auto h2d = [&]() { HIP_TRY(hipMemcpyAsync(d_in, h_in, (size_t)bytes, hipMemcpyHostToDevice, s[0])); };
+            auto d2h = [&]() { HIP_TRY(hipMemcpyAsync(h_out, d_out, (size_t)bytes, hipMemcpyDeviceToHost, s[1])); };
+            auto best = [&](int mode) {   // 0 H2D, 1 D2H, 2 both: wall time of the copies, best of 3
+                double b = 1e30;
+                for (int r = 0; r < 4; ++r) {   // the first pass warms up
+                    HIP_TRY(hipDeviceSynchronize());
+                    const auto t0 = std::chrono::steady_clock::now();
+                    if (mode != 1) h2d();
+                    if (mode != 0) d2h();
+                    HIP_TRY(hipStreamSynchronize(s[0]));
+                    HIP_TRY(hipStreamSynchronize(s[1]));
+                    const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+                    if (r > 0) b = std::min(b, dt);
+                }
+                return b;
+            };
+            const double t1 = best(0), t2 = best(1), t3 = best(2);
+            out_gbps[0] = (double)bytes / t1 / 1e9;
+            out_gbps[1] = (double)bytes / t2 / 1e9;
+            out_gbps[2] = 2.0 * (double)bytes / t3 / 1e9;
+        } catch (...) {
+            release();
+            throw;
+        }
+        release();
+    })
 }
 
 int vh_pipe_destroy(vh_pipe *p) {

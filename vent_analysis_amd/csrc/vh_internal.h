@@ -10,6 +10,7 @@
 #include <condition_variable>
 #include <mutex>
 #include <thread>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -36,7 +37,23 @@ struct VhError {
                           std::string(#expr) + ": " + hipGetErrorString(_e)};               \
     } while (0)
 
-#define VH_CHECK_LAUNCH() HIP_TRY(hipGetLastError())
+// VH_SYNC_CHECK=1 (diagnostics): every launch is followed by a device sync, so a kernel fault is
+// reported at the launch that caused it (file:line) instead of at a later API call
+inline bool vh_sync_check() {
+    static const bool on = getenv("VH_SYNC_CHECK") != nullptr;
+    return on;
+}
+#define VH_CHECK_LAUNCH()                                                                   \
+    do {                                                                                    \
+        HIP_TRY(hipGetLastError());                                                         \
+        if (vh_sync_check()) {                                                              \
+            const hipError_t _s = hipDeviceSynchronize();                                   \
+            if (_s != hipSuccess)                                                           \
+                throw VhError{VH_ERR_HIP, std::string("after the launch at ") + __FILE__ + \
+                                              ":" + std::to_string(__LINE__) + ": " +       \
+                                              hipGetErrorString(_s)};                       \
+        }                                                                                   \
+    } while (0)
 
 // hipFuncSetAttribute(MaxDynamicSharedMemorySize) once per (kernel, device): the attribute is
 // per device, and batches of several contexts / pipeline slots launch from several host threads.
