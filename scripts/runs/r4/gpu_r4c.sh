@@ -2,7 +2,7 @@
 # GPU-box (round 4): bench with one / two batches in flight, sort-chunk A/B, per-study phase
 # profiles of studies 1 and 3, and the host-to-host leg's dependence on torch's runtime init and
 # on the late D2H enqueue.  usage: scripts/gpu_r4c.sh TAG
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-r4c}

@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU-box (round 4): batches in flight 1/2/3 with the largest-first study order, and the
 # host-to-host leg after a device-resident warm-up / a CPU load (the bench's order) vs cold.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-r4d}

@@ -2,7 +2,7 @@
 # GPU-box (round 4): the study kernel at 512 threads (8 waves per study, one study per CU: how much
 # slower is a study on half the waves?), its study-driver parity tests, the CI line, and the
 # emap series probes (ST_PROF, study 3).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-r4e}

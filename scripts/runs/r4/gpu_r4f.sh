@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU-box (round 4): the study kernel at 512 threads and <= 80 KB of LDS (two studies per CU):
 # study-driver parity first, then the bench at 1-3 batches in flight, then the whole -m gpu suite.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-r4f}

@@ -2,7 +2,7 @@
 # GPU-box (round 4): why the 512-thread / 70 KB study kernel is slower per study (r4f).  A/B of
 # one vs two studies per CU on the same build (VH_ST_MIN_LDS pads the dynamic LDS past 80 KB), the
 # same layout at 1024 threads, and ST_PROF phase splits of study 3 in both placements.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-r4g}

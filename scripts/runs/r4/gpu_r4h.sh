@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU-box (round 4): where the 512-thread study workgroups run (VH_STUDY_TRACE): one launch of
 # 512 studies, and two 256-study batches in flight.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-r4h}

@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU-box (round 4): feeding two study slots per CU -- batches in flight at 512 threads (placement
 # traces), 512-study batches in flight (the fed upper bound), 1024 threads at 3 in flight.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-r4i}

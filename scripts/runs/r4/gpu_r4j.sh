@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU-box (round 4): batches in flight with more hardware queues per process (GPU_MAX_HW_QUEUES 8:
 # one queue per batch stream, so no two batches' kernels serialise on a shared queue).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-r4j}

@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU-box (round 4): stream priorities for batches in flight (VH_PRIO=1: the study kernel on a
 # low-priority stream, every other kernel of the batch high), 512 and 1024 threads.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-r4k}

@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU-box (round 4): host-to-host sub-batch / slot sweep (the pipe at 128 x 4 behaves like 128-study
 # batches in flight, which run 7.1 k vol/s device-resident, r4i).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-r4n}

@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU-box (round 4): host-to-host sweep over 12 x 256 studies (pipeline fill / drain amortised).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-r4o}

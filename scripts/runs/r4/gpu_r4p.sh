@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU-box (round 4): CUs reserved for the batches' short kernels (VH_ST_RESERVE=k: the study kernel
 # on a stream whose CU mask leaves k CUs per XCD free), device-resident and host-to-host.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-r4p}

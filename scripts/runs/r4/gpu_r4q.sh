@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU-box (round 4): the default bench with the new host-to-host defaults (224 x 3, 12 x 256 studies).
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../../..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 TAG=${1:-r4q}
