@@ -6,7 +6,7 @@ import sys
 
 rows = []
 for line in open(sys.argv[1]):
-    bp, i, t0, t1, hw, xcc, khz = line.strip().split(",")
+    bp, i, t0, t1, hw, xcc, khz = line.strip().split(",")[:7]
     hw = int(hw)
     cu = (int(xcc) & 0xF, (hw >> 13) & 0x7, (hw >> 12) & 1, (hw >> 8) & 0xF)
     rows.append((bp, int(i), int(t0), int(t1), cu, int(khz)))

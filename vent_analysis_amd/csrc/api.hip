@@ -734,9 +734,11 @@ int vh_batch_study_times(vh_batch *b, double *us) {
         if (const char *path = getenv("VH_STUDY_TRACE")) {   // per study: start, end, placement
             if (FILE *f = fopen(path, "a")) {
                 for (int64_t i = 0; i < b->nb; ++i)
-                    fprintf(f, "%p,%lld,%llu,%llu,%u,%u,%d\n", (void *)b, (long long)i,
+                    fprintf(f, "%p,%lld,%llu,%llu,%u,%u,%d,%d,%d,%d\n", (void *)b, (long long)i,
                             (unsigned long long)st[i].t_start, (unsigned long long)st[i].t_end,
-                            st[i].hw_id, st[i].xcc_id, rate_khz);
+                            st[i].hw_id, st[i].xcc_id, rate_khz, st[i].pc_rounds,
+                            st[i].pc_fallbacks, st[i].iters_level[0] + st[i].iters_level[1] +
+                                st[i].iters_level[2] + st[i].iters_level[3]);
                 fclose(f);
             }
         }

@@ -116,6 +116,7 @@ struct StudyMisc {
     double sd, sd2, conv;
     ChainState ch;             // PC's result (conv of the last iteration)
     int32_t itn, uin;          // iterations of the level, U buffer of the last field
+    int32_t pc_rounds, pc_fb;  // S7 by PC: rounds and serial fallbacks over all iterations
 };
 
 // One level's axis tables staged in LDS.
@@ -634,6 +635,8 @@ __global__ void __launch_bounds__(ST_TPB, 4) k_n4_study(StudyArgs a) {
     if (t == 0) {
         M.item_ctr = 0;
         M.uin = 0;
+        M.pc_rounds = 0;
+        M.pc_fb = 0;
     }
     if (wv == 0) find_first(a, b, fm, M);
     {   // item schedule: items by row count, largest first (ties by index), so the dynamic item
@@ -981,7 +984,11 @@ __global__ void __launch_bounds__(ST_TPB, 4) k_n4_study(StudyArgs a) {
                     pcw_run<ST_TPB, ST_EVAL_EXP>([=](int64_t r) { return Dr[r]; }, a.D + a.half + b * a.VS, n, PW, M.ch, itk,
                             reinterpret_cast<double *>(a.D + b * a.VS), (int)(a.VS / 2),
                             itk < a.lvs->max_iters[L] ? a.thresh : 0.0f);
-                    if (t == 0) M.conv = (double)M.ch.conv;
+                    if (t == 0) {
+                        M.conv = (double)M.ch.conv;
+                        M.pc_rounds += PW.rounds;
+                        M.pc_fb += PW.fallback == 4 * itk + 2 ? 1 : 0;   // serial fallbacks of the exact rounds
+                    }
                 } else if (g.w == 0) {   // S7x: item partials in item order
                     double sd = 0.0, sd2 = 0.0;
                     for (int i = lane; i < a.nitems; i += 64) {
@@ -1058,6 +1065,8 @@ __global__ void __launch_bounds__(ST_TPB, 4) k_n4_study(StudyArgs a) {
     if (t == 0) {
         stb->conv = M.conv;
         stb->active = 0;
+        stb->pc_rounds = M.pc_rounds;
+        stb->pc_fallbacks = M.pc_fb;
         stb->t_end = wall_clock64();
     }
 }

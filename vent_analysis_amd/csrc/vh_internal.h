@@ -105,6 +105,7 @@ struct N4State {
     float conv_level[VH_MAX_LEVELS];
     uint64_t t_start, t_end;   // k_n4_study: device wall clock (wall_clock64) at the workgroup's start / end
     uint32_t hw_id, xcc_id;    // k_n4_study: where the workgroup ran (HW_REG_HW_ID / HW_REG_XCC_ID)
+    int32_t pc_rounds, pc_fallbacks;   // k_n4_study: S7 guess-and-verify rounds / serial fallbacks, all iterations
 };
 
 // Per-axis, per-level B-spline tables (host-built, identical to oracle/n4_oracle.c).
