@@ -855,10 +855,15 @@ struct PcShared {
     int agFirst[NL / 64];
     // exact sig after stage 0 (pcx_*): t-slot allocator, result tag, walks taken
     int xslots, xdone, xwalks, xslow;
+    int nfrz;   // pcw_run calls closed by the frozen serial (diagnostics; reset per call)
+    int nfr;    // stage 0 at its cap: blocks past the frontier certified frozen at their guesses
 #ifdef PC_PROF
     int pchg[32], pwav[32];   // stage-0 rounds: blocks whose start changed, waves that ran
     unsigned long long xwcyc, xscyc;   // PCX scan: cycles in walks, whole scan
 #endif
+    // pass 0: per block, the float starts m for which every step of the block leaves mu at m
+    // (pc_mu_serial_frozen; empty for blocks before step PC_FRZ_K0)
+    float4 fz[NL];   // (lo, hi) for starts in (0.5, 1], (lo, hi) for starts in (1, 2)
     // pass-0 block sums of p - 1 and (p - 1)^2 (double, 16-aligned pair over gmu_o .. sp1: those
     // fields are written by round 0 before they are next read)
     __device__ double &s1(int j) { return *reinterpret_cast<double *>(&b[j].gmu_o); }
@@ -1007,6 +1012,79 @@ __device__ void pc_serial(PcShared<NL> &S, const PcMap &m, const float *P) {
     }
     S.mu = mu;
     S.sig = sig;
+}
+
+// ---- frozen mu (stage 0 at its round cap) -------------------------------------------------------
+// Near convergence p = exp(d) ~ 1 and, past N ~ 2e4, most steps' increment (p - mu) / N is below
+// half an ulp: ITK's float mu stops moving for whole blocks (r4u: 782 of 1024 blocks in an
+// iteration of seed 1).  The frozen value sits thousands of ulps from the double running mean that
+// seeds PC's guesses, a frozen block maps any nearby start to itself, so wrong guesses pass the
+// continuity check and only the exact frontier corrects them, a few blocks per round: stage 0 and
+// stage 1 hit their caps and the exact rounds end in the serial fallback (the 32 slowest of 256
+// studies were exactly those with such an iteration).  Certified freeze: with mu' =
+// RN_f(RN_d(m A) + B) = m + (p - m) / N + E, |E| <= 2^-23 / N + 7e-16 (A = RN(1 - RN(1/N)),
+// B = RN_f(p RN(1/N)), m, p < 2), a start m with |p - m| <= N h stays at m when h + |E| is below
+// half the float spacing on both sides of m: h = 0.99 2^-25 for m in (0.5, 1] (spacing 2^-24, and
+// 2^-25 below 1.0), h = 0.99 2^-24 for m in (1, 2) (spacing 2^-23).  Pass 0 intersects those
+// intervals over each block for both h (steps from PC_FRZ_K0 on, where |E| < 3e-11, far inside the
+// 1 % margin), rounded inward to floats.  Checked on the CPU against the exact trajectories of the
+// frozen iterations (every certified block's end equals its start; 734 of 1024 blocks certified in
+// the worst one).
+#define PC_FRZ_H1 (0x1p-25 * 0.99)
+#define PC_FRZ_H2 (0x1p-24 * 0.99)
+#define PC_FRZ_K0 4096u
+__device__ __forceinline__ float f_up(double x) {
+    float f = (float)x;
+    if ((double)f < x) f = __uint_as_float(f >= 0.0f ? __float_as_uint(f) + 1u : __float_as_uint(f) - 1u);
+    return f;
+}
+__device__ __forceinline__ float f_dn(double x) {
+    float f = (float)x;
+    if ((double)f > x) f = __uint_as_float(f > 0.0f ? __float_as_uint(f) - 1u : __float_as_uint(f) + 1u);
+    return f;
+}
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const long long x = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)x, l), hi = __builtin_amdgcn_readlane((int)(x >> 32), l);
+    return __longlong_as_double(((long long)hi << 32) | (long long)(uint32_t)lo);
+}
+__device__ __forceinline__ bool pc_frozen(float4 z, float m) {
+    return m > 0.5f && m < 2.0f && (m <= 1.0f ? (z.x <= m && m <= z.y) : (z.z <= m && m <= z.w));
+}
+// One wave: the exact mu at every block start past the frontier S.first_bad, skipping certified
+// frozen blocks in O(1) and running the others step by step (lane l forms step s0 + l's constants,
+// the chain reads them across lanes; the same exact step as pc_apply), at most PC_FRZ_RUN of them.
+// Returns true when it reached the last block: stage 0's next round then matches everywhere and
+// PCX gives sig.  Otherwise the exact starts it set stay as guesses and stage 1 goes on.
+#ifndef PC_FRZ_RUN
+#define PC_FRZ_RUN 96   // blocks run step by step (~10 k cycles each) before handing back to the rounds
+#endif
+template <int NL>
+__device__ bool pc_mu_serial_frozen(PcShared<NL> &S, const PcMap &m, const float *P) {
+    const int lane = threadIdx.x & 63;
+    const int nbe = m.L ? NL : (int)m.rem;
+    const int f = S.first_bad;
+    float mu = S.b[f].emu;   // block f's start was exact, so is its end
+    int run = 0;
+    for (int jb = f + 1; jb < nbe; ++jb) {
+        if (lane == 0) S.b[jb].gmu = mu;
+        if (pc_frozen(S.fz[jb], mu)) continue;   // end = start
+        if (++run > PC_FRZ_RUN) return false;
+        const uint32_t len = pc_len(m, jb), k0 = pc_k0(m, jb);
+        for (uint32_t s0 = 0; s0 < len; s0 += 64) {
+            const uint32_t s = s0 + (uint32_t)lane;
+            double A = 1.0, B = 0.0;
+            if (s < len) {
+                const PcK q = pc_consts((double)(k0 + s), P[(size_t)s * NL + jb]);
+                A = q.A;
+                B = q.B;
+            }
+            const int cnt = (int)min(64u, len - s0);
+            for (int i = 0; i < cnt; ++i)
+                mu = (float)__dadd_rn(__dmul_rn((double)mu, readlane_d(A, i)), readlane_d(B, i));
+        }
+    }
+    return true;
 }
 
 // ---- PC phase A: certified float steps --------------------------------------------------------
@@ -1609,6 +1687,7 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
     float *const T0 = reinterpret_cast<float *>(&S);
     const uint32_t lmax = m.L + (m.rem ? 1u : 0u);
     double s1 = 0.0, s2 = 0.0;
+    double fa1 = -1e300, fb1 = 1e300, fa2 = -1e300, fb2 = 1e300;   // certified-frozen start intervals
     // thread tid loads step i = tid % G0 of blocks tid / G0 + (NL / G0) q; the next group's
     // loads are in flight while this group's exp runs
     float v[G0];
@@ -1642,6 +1721,11 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
                 const double e = (double)p - 1.0;
                 s1 += e;
                 s2 = fma(e, e, s2);
+                const double nd = itk_Nd((double)(k0 + g0 + i)), nh1 = nd * PC_FRZ_H1, nh2 = nd * PC_FRZ_H2;
+                fa1 = fmax(fa1, (double)p - nh1);
+                fb1 = fmin(fb1, (double)p + nh1);
+                fa2 = fmax(fa2, (double)p - nh2);
+                fb2 = fmin(fb2, (double)p + nh2);
             }
         P0M(2);   // exp, stores and sums
         __syncthreads();
@@ -1656,12 +1740,20 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
         S.done = 0;
         S.fallback = 0;
         S.xdone = 0;
+        S.nfrz = 0;
+        S.nfr = 0;
     }
 #ifdef PC_PROF
     if (tid < 32) S.pchg[tid] = S.pwav[tid] = 0;
 #endif
     S.s1(j) = s1;
     S.s2(j) = s2;
+    {   // empty intervals (lo = +inf) before PC_FRZ_K0 or where the block's p spread is too wide
+        const bool ok = k0 >= PC_FRZ_K0 && len > 0u;
+        const float inf = __int_as_float(0x7f800000);
+        S.fz[j] = make_float4(ok && fa1 <= fb1 ? f_up(fa1) : inf, ok && fa1 <= fb1 ? f_dn(fb1) : -inf,
+                              ok && fa2 <= fb2 ? f_up(fa2) : inf, ok && fa2 <= fb2 ? f_dn(fb2) : -inf);
+    }
     __syncthreads();
     pcw_guess<NL>(S, m);
     __syncthreads();
@@ -1767,7 +1859,9 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
         // still reading the flag of the stage before must not see it cleared)
         const int tag = 4 * req + pass;
         float lg = __int_as_float(0x7fc00000), ls = lg, le = 0.0f, les = 0.0f;
-        for (int ra0 = 0; ra0 < PC_AMAX; ++ra0, ++round) {
+        int amax = PC_AMAX;
+        bool frz = false;   // stage 0 closed by pc_mu_serial_frozen (one more round to confirm)
+        for (int ra0 = 0; ra0 < amax; ++ra0, ++round) {
 #ifdef PC_PROF
             const unsigned long long cq = clock64();
 #endif
@@ -1795,12 +1889,27 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
 #ifdef PC_PROF
             cblk += clock64() - cq;
 #endif
-            pcw_update<NL>(S, m, round, tag, ra0 == PC_AMAX - 1, false, pass == 1);
+            // stage 0 at its cap also reports its frontier (first_bad) and sets fallback = tag
+            pcw_update<NL>(S, m, round, tag, ra0 == amax - 1, pass == 0 && !frz, pass == 1);
             __syncthreads();
 #ifdef PC_PROF
             rst[pass]++;
 #endif
             if (S.done == tag) break;
+            if (pass == 0 && !frz && S.fallback == tag) {
+                // the frozen serial from the frontier; when it stops at its budget, its exact starts
+                // stay as guesses and stage 1's rounds go on as before
+                frz = true;
+                if (tid < 64) {
+                    const bool all = pc_mu_serial_frozen<NL>(S, m, P);
+                    if (tid == 0) {
+                        S.nfr = all ? 1 : 0;
+                        S.nfrz += all ? 1 : 100;
+                    }
+                }
+                __syncthreads();
+                if (S.nfr) amax = ra0 + 2;   // every start past the frontier is exact now
+            }
         }
 #ifdef PC_PROF
         cst[pass] = clock64() - cs0;

@@ -987,7 +987,8 @@ __global__ void __launch_bounds__(ST_TPB, 4) k_n4_study(StudyArgs a) {
                     if (t == 0) {
                         M.conv = (double)M.ch.conv;
                         M.pc_rounds += PW.rounds;
-                        M.pc_fb += PW.fallback == 4 * itk + 2 ? 1 : 0;   // serial fallbacks of the exact rounds
+                        // serial fallbacks of the exact rounds (units), frozen-serial stage-0 closes (thousands)
+                        M.pc_fb += (PW.fallback == 4 * itk + 2 ? 1 : 0) + 1000 * PW.nfrz;
                     }
                 } else if (g.w == 0) {   // S7x: item partials in item order
                     double sd = 0.0, sd2 = 0.0;
