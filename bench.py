@@ -638,7 +638,13 @@ def main():
         roof["isolated"] = {"avg_launch_us": round(iso_us, 2), "achieved": round(ach_iso, 1),
                             "frac": round(ach_iso / HBM_PEAK_GBS, 4),
                             "note": "one batch alone (batch_latency run): no other batch's "
-                                    "workgroups on the CUs"}
+                                    "workgroups on the CUs",
+                            # every class's launch time alone (the overlapped kernel_ms_per_step
+                            # above includes waiting for CUs the other batch's studies hold)
+                            "kernel_us_per_launch": {n: round(v * 1e3, 2) for n, v in
+                                                     sorted(iso_kernels.items(), key=lambda kv: -kv[1])},
+                            "non_n4_us_per_step": round(sum(v for n, v in iso_kernels.items()
+                                                            if not n.startswith("n4_")) * 1e3, 2)}
     its = np.array([list(r.n4_iters[:4]) for r in res])
     if not args.h2h_keep_batch:
         # the device-resident batches (their streams, 1.5 GB of HBM each) are done: the pipe's slot
