@@ -144,21 +144,64 @@ __global__ void __launch_bounds__(CIW_TPB) k_ci_walk(const uint32_t *__restrict_
     }
 }
 
-__global__ void k_ci_finish(const uint32_t *hist, const unsigned long long *count,
-                            const double *radii, int64_t nbs, double minvox, int64_t nb,
-                            const int32_t *status, VolScalars *sc) {
-    const int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (b >= nb) return;
+// the workspace's zeroing in one launch (four hipMemsetAsync blits before: ~4 us each, r4ab)
+__global__ void k_ci_clear(int32_t *status, unsigned long long *count, int64_t nb, uint32_t *bits,
+                           int64_t nbits, uint32_t *hist, int64_t nhist) {
+    const int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x, st = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = i0; i < nbits; i += st) bits[i] = 0u;
+    for (int64_t i = i0; i < nhist; i += st) hist[i] = 0u;
+    for (int64_t i = i0; i < nb; i += st) {
+        status[i] = 0;
+        count[i] = 0ull;
+    }
+}
+
+// The 95th-percentile shell (Vent_Analysis.py:265-271): the first shell q whose cumulative count
+// passes i95, one workgroup per volume -- each thread sums a run of consecutive shells, an
+// exclusive scan of the run sums finds the run holding the crossing, and that run is walked (one
+// thread per volume walked every shell serially: 16 us, r4ab).  Integer sums: order-free.
+#define CIF_TPB 256
+__global__ void __launch_bounds__(CIF_TPB) k_ci_finish(const uint32_t *hist, const unsigned long long *count,
+                                                      const double *radii, int64_t nbs, double minvox,
+                                                      int64_t nb, const int32_t *status, VolScalars *sc) {
+    __shared__ unsigned long long s_sum[CIF_TPB];
+    __shared__ int s_hit;
+    const int64_t b = blockIdx.x;
+    const int t = threadIdx.x;
     const int64_t D = (int64_t)count[b];
-    sc[b].n_ci = D;
-    sc[b].ci_status = status[b] ? VH_ERR_MAXRADIUS : (D == 0 ? VH_ERR_EMPTY : VH_OK);
-    sc[b].ci_scalar = 0.0;
-    if (status[b] || D == 0) return;
-    const int64_t i95 = (int64_t)(0.95 * (double)D);
-    int64_t cum = 0;
-    for (int64_t q = 0; q < nbs; ++q) {
-        cum += hist[b * nbs + q];
-        if (cum > i95) { sc[b].ci_scalar = radii[q] * minvox; return; }
+    if (t == 0) {
+        sc[b].n_ci = D;
+        sc[b].ci_status = status[b] ? VH_ERR_MAXRADIUS : (D == 0 ? VH_ERR_EMPTY : VH_OK);
+        sc[b].ci_scalar = 0.0;
+        s_hit = -1;
+    }
+    if (status[b] || D == 0) return;   // block-uniform
+    const unsigned long long i95 = (unsigned long long)(int64_t)(0.95 * (double)D);
+    const int64_t per = (nbs + CIF_TPB - 1) / CIF_TPB, q0 = t * per, q1 = min(q0 + per, nbs);
+    const uint32_t *h = hist + b * nbs;
+    unsigned long long own = 0;
+    for (int64_t q = q0; q < q1; ++q) own += h[q];
+    s_sum[t] = own;
+    __syncthreads();
+    if (t == 0) {   // exclusive scan of the run sums (256 adds) and the run holding the crossing
+        unsigned long long run = 0;
+        for (int i = 0; i < CIF_TPB; ++i) {
+            const unsigned long long v = s_sum[i];
+            s_sum[i] = run;
+            run += v;
+            if (s_hit < 0 && run > i95) s_hit = i;
+        }
+    }
+    __syncthreads();
+    if (t == s_hit) {
+        unsigned long long cum = s_sum[t];
+        for (int64_t q = q0; q < q1; ++q) {
+            cum += h[q];
+            if (cum > i95) {
+                sc[b].ci_scalar = radii[q] * minvox;
+                break;
+            }
+        }
     }
 }
 
@@ -244,10 +287,12 @@ void vh_ci_run(vh_batch *b, const vh_ci_table *t, double minvox, double *d_ci) {
         HIP_TRY(hipMalloc(&b->d_ci_hist, sizeof(uint32_t) * b->nb * nbs));
         b->ci_nb_cap = nbs;
     }
-    HIP_TRY(hipMemsetAsync(d_status, 0, sizeof(int32_t) * b->nb, st));
-    HIP_TRY(hipMemsetAsync(d_count, 0, sizeof(unsigned long long) * b->nb, st));
-    HIP_TRY(hipMemsetAsync(b->d_bitmap, 0, sizeof(uint32_t) * b->nb * words, st));
-    HIP_TRY(hipMemsetAsync(b->d_ci_hist, 0, sizeof(uint32_t) * b->nb * nbs, st));
+    {
+        const int64_t big = std::max<int64_t>(b->nb * words, b->nb * nbs);
+        k_ci_clear<<<(unsigned)std::min<int64_t>((big + VH_TPB - 1) / VH_TPB, 1024), VH_TPB, 0, st>>>(
+            d_status, d_count, b->nb, b->d_bitmap, b->nb * words, b->d_ci_hist, b->nb * nbs);
+        VH_CHECK_LAUNCH();
+    }
     const dim3 vg((unsigned)((b->V + VH_TPB - 1) / VH_TPB), (unsigned)b->nb);
     k_ci_bitmap<<<vg, VH_TPB, 0, st>>>(b->d_defect, b->R, b->C, b->Z, b->V, words, b->d_bitmap,
                                        b->d_ci_list, d_count);
@@ -266,8 +311,8 @@ void vh_ci_run(vh_batch *b, const vh_ci_table *t, double minvox, double *d_ci) {
             words, stage_bits, b->d_ci_shell, b->d_ci_hist, d_status);
         VH_CHECK_LAUNCH();
     }
-    k_ci_finish<<<(unsigned)((b->nb + 63) / 64), 64, 0, st>>>(b->d_ci_hist, d_count, t->d_radii, nbs,
-                                                              minvox, b->nb, d_status, b->d_sc);
+    k_ci_finish<<<(unsigned)b->nb, CIF_TPB, 0, st>>>(b->d_ci_hist, d_count, t->d_radii, nbs, minvox,
+                                                     b->nb, d_status, b->d_sc);
     VH_CHECK_LAUNCH();
     if (d_ci) {
         k_ci_scatter<<<vg, VH_TPB, 0, st>>>(b->d_ci_shell, b->d_defect, t->d_radii, minvox, b->V, d_ci);

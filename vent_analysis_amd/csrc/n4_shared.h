@@ -1056,6 +1056,9 @@ __device__ __forceinline__ bool pc_frozen(float4 z, float m) {
 // the chain reads them across lanes; the same exact step as pc_apply), at most PC_FRZ_RUN of them.
 // Returns true when it reached the last block: stage 0's next round then matches everywhere and
 // PCX gives sig.  Otherwise the exact starts it set stay as guesses and stage 1 goes on.
+#ifndef PC_AMAX0
+#define PC_AMAX0 40   // stage 0's round cap, where the frozen serial takes over
+#endif
 #ifndef PC_FRZ_RUN
 #define PC_FRZ_RUN 96   // blocks run step by step (~10 k cycles each) before handing back to the rounds
 #endif
@@ -1859,7 +1862,7 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
         // still reading the flag of the stage before must not see it cleared)
         const int tag = 4 * req + pass;
         float lg = __int_as_float(0x7fc00000), ls = lg, le = 0.0f, les = 0.0f;
-        int amax = PC_AMAX;
+        int amax = pass == 0 ? PC_AMAX0 : PC_AMAX;
         bool frz = false;   // stage 0 closed by pc_mu_serial_frozen (one more round to confirm)
         for (int ra0 = 0; ra0 < amax; ++ra0, ++round) {
 #ifdef PC_PROF
