@@ -219,7 +219,8 @@ def host_to_host(R, C, Z, nb, args, device, opts, seed, aligned=True):
     from vent_analysis_amd import _lib
     from vent_analysis_amd.synth import synth_batch
     slots, sub = args.h2h_slots, min(args.h2h_sub, nb)
-    n = max(1, args.h2h_batches) * nb
+    hb = args.h2h_batches or (12 if int(os.environ.get("WORLD_SIZE", "1")) == 1 else 6)
+    n = max(1, hb) * nb
     hp0, mk0 = synth_batch(R, C, Z, n, base_seed=seed, unique=BENCH_UNIQUE, vary=True)
     # page-aligned host arrays (as ingest.load_batch allocates them): whole chunks DMA in place
     alloc = _lib.empty_aligned if aligned else (lambda shape, t: np.empty(shape, t))
@@ -451,8 +452,9 @@ def main():
                          "cohort all-reduce per step)")
     ap.add_argument("--no-h2h", action="store_true",
                     help="skip the host-to-host pipeline measurement (host_to_host_vol_s)")
-    ap.add_argument("--h2h-batches", type=int, default=12,
-                    help="host-to-host sample: this many x --batch volumes")
+    ap.add_argument("--h2h-batches", type=int, default=0,
+                    help="host-to-host sample: this many x --batch volumes (0: 12 at one rank, 6 "
+                         "per rank beyond: ~14 GB of host arrays per rank at 12)")
     ap.add_argument("--h2h-sub", type=int, default=224,
                     help="host-to-host: studies per pipeline sub-batch")
     ap.add_argument("--h2h-slots", type=int, default=3,
