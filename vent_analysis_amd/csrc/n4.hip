@@ -1927,7 +1927,8 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
                                                        dim3(PC_TPB), args, 0, st));
                 } else if (cm == 0) {
                     ScopedKTimer tm(b, "n4_pcw", 0.0);
-                    k_n4_pcw<<<(unsigned)ns, PC_TPB, sizeof(PcShared<PC_TPB>), st>>>(
+                    vh_set_max_lds((const void *)k_n4_pcw, (int)pcw_lds_bytes<PC_TPB>());
+                    k_n4_pcw<<<(unsigned)ns, PC_TPB, pcw_lds_bytes<PC_TPB>(), st>>>(
                         b->d_D, b->d_perm, b->d_D + b->nb * b->VS, b->VS, b->d_sc, b->d_st, vol0,
                         it + 1 < prm.max_iters[L] ? prm.conv_threshold : 0.0f);
                     VH_CHECK_LAUNCH();

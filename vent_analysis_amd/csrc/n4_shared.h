@@ -1668,6 +1668,16 @@ static_assert(PC_APASS >= 1 && PC_APASS <= 2, "PC_APASS: 1 or 2 phase-A stages (
 #define PC_XSIG 1   // exact sig after stage 0 (PCX above); 0: stage 1 and the exact rounds always
 #endif
 // PEXP: ld returns p = expf_cr(d) already (the study kernel's eval stored it, ST_EVAL_EXP)
+// pass 0's transpose groups: PC_G0 steps of every block per two barriers (LDS: PC_G0 (NL + 8) floats
+// over the PcShared area, so the area is the larger of the two)
+#ifndef PC_G0
+#define PC_G0 8
+#endif
+template <int NL>
+__host__ __device__ constexpr size_t pcw_lds_bytes() {
+    return sizeof(PcShared<NL>) > sizeof(float) * PC_G0 * (NL + 8) ? sizeof(PcShared<NL>)
+                                                                    : sizeof(float) * PC_G0 * (NL + 8);
+}
 template <int NL, bool PEXP = false, class LoadD>
 __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n, PcShared<NL> &S,
                                                   ChainState &ch, int req, double *tbuf, int tcap,
@@ -1685,8 +1695,8 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
     // 64 cache lines per wave-wide load; instead the workgroup loads each group of PC_G0 steps of
     // all blocks together (8 lanes per block: 32-byte runs) and transposes it through LDS (the
     // PcShared area, rewritten after this pass; rows padded by 8 floats against bank conflicts).
-    constexpr int G0 = 8, TS = NL + 8;
-    static_assert(sizeof(float) * G0 * TS <= sizeof(PcShared<NL>), "pass-0 transpose buffer");
+    constexpr int G0 = PC_G0, TS = NL + 8;
+    static_assert(sizeof(float) * G0 * TS <= pcw_lds_bytes<NL>(), "pass-0 transpose buffer");
     float *const T0 = reinterpret_cast<float *>(&S);
     const uint32_t lmax = m.L + (m.rem ? 1u : 0u);
     double s1 = 0.0, s2 = 0.0;

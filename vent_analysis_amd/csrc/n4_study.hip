@@ -1129,7 +1129,7 @@ static bool study_layout(const vh_batch *b, const vh_n4_params &prm, StudyLayout
     const size_t fit_num = 2 * sizeof(unsigned long long) * (size_t)nlat_max;
     const size_t fit = ((fit_num + 15) & ~(size_t)15) + sizeof(double) * fit_waves * nb_ring * (size_t)s_cap;
     const size_t exact = sizeof(float) * 2 * ST_TPB;
-    const size_t pcs = prm.conv_mode == 0 ? sizeof(PcShared<ST_TPB>) : 0;
+    const size_t pcs = prm.conv_mode == 0 ? pcw_lds_bytes<ST_TPB>() : 0;
     const size_t p1 = sizeof(double) * (size_t)p1_max;   // the new field's P1, lattice update to eval
     const size_t scr = std::max({refine, emap, fit, exact, pcs, p1});
     auto A = [](size_t v) { return (v + 15) & ~(size_t)15; };
