@@ -459,7 +459,7 @@ def main():
                     help="host-to-host: studies per pipeline sub-batch")
     ap.add_argument("--h2h-slots", type=int, default=3,
                     help="host-to-host: pipeline slots (sub-batches in flight, <= 8)")
-    ap.add_argument("--inflight", type=int, default=2,
+    ap.add_argument("--inflight", type=int, default=3,
                     help="device batches in flight: steps of consecutive batches overlap on their own "
                          "streams (a cohort stream); 1 = one batch, synchronised every step")
     ap.add_argument("--h2h-keep-batch", action="store_true",
