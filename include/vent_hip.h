@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define VH_ABI_VERSION 6
+#define VH_ABI_VERSION 7
 
 /* status codes */
 #define VH_OK 0
@@ -227,6 +227,11 @@ int vh_pipe_stats(vh_pipe *p, int64_t *pinned_peak_bytes, int64_t *staged_spans)
 /* This GPU's PCIe link with pinned host memory (bench.py's host-to-host bound): bytes copied H2D
  * alone, D2H alone and both at once on two streams, best of 3; out_gbps = {h2d, d2h, both}. */
 int vh_link_probe(vh_ctx *ctx, int64_t bytes, double out_gbps[3]);
+/* Page-locked host memory on the context's device (hipHostMalloc) for result arrays the caller
+ * reuses: a D2H into it runs at the link rate with no runtime staging.  vh_host_free takes any
+ * pointer vh_host_alloc returned (also after vh_destroy). */
+int vh_host_alloc(vh_ctx *ctx, int64_t bytes, void **out);
+int vh_host_free(void *p);
 
 /* ---- multi-GPU (RCCL over xGMI) -------------------------------------------------------------- */
 #define VH_COMM_ID_BYTES 128

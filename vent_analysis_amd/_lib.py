@@ -95,6 +95,8 @@ _SIGS = {
     "vh_pipe_destroy": ([_P], ct.c_int),
     "vh_pipe_stats": ([_P, ct.POINTER(ct.c_int64), ct.POINTER(ct.c_int64)], ct.c_int),
     "vh_link_probe": ([_P, ct.c_int64, ct.POINTER(ct.c_double)], ct.c_int),
+    "vh_host_alloc": ([_P, ct.c_int64, ct.POINTER(_P)], ct.c_int),
+    "vh_host_free": ([_P], ct.c_int),
     "vh_comm_unique_id": ([_P], ct.c_int),
     "vh_comm_init": ([_P, ct.c_int, ct.c_int, _P], ct.c_int),
     "vh_batch_cohort_allreduce": ([_P], ct.c_int),
@@ -140,6 +142,48 @@ def _ptr(a):
     return None if a is None else ct.c_void_p(a.ctypes.data)
 
 
+class _PinnedPool:
+    """Page-locked host buffers (vh_host_alloc) for the arrays an entry point returns: their D2H
+    runs at the link rate with no runtime staging.  A returned array's buffer goes back to the pool
+    when the last view of it is gone (a finalizer on the ctypes buffer numpy holds as its base); the
+    pool keeps at most ``keep`` idle buffers per size.  r4: the CI line's dense f64 map."""
+
+    def __init__(self, ctx, keep=4):
+        self.ctx = ctx
+        self.keep = keep
+        self.idle = {}
+        self.lock = threading.Lock()
+
+    def array(self, shape, dtype):
+        dtype = np.dtype(dtype)
+        n = int(np.prod(shape)) * dtype.itemsize
+        with self.lock:
+            ptrs = self.idle.get(n)
+            ptr = ptrs.pop() if ptrs else None
+        if ptr is None:
+            h = _P()
+            self.ctx.check(self.ctx.L.vh_host_alloc(self.ctx.h, n, ct.byref(h)), "vh_host_alloc")
+            ptr = h.value
+        buf = (ct.c_char * n).from_address(ptr)
+        weakref.finalize(buf, self._release, n, ptr)
+        return np.frombuffer(buf, dtype).reshape(shape)
+
+    def _release(self, n, ptr):
+        with self.lock:
+            ptrs = self.idle.setdefault(n, [])
+            if self.ctx.h is not None and len(ptrs) < self.keep:
+                ptrs.append(ptr)
+                return
+        lib().vh_host_free(ct.c_void_p(ptr))
+
+    def close(self):
+        with self.lock:
+            for ptrs in self.idle.values():
+                for p in ptrs:
+                    lib().vh_host_free(ct.c_void_p(p))
+            self.idle.clear()
+
+
 class Context:
     """One device + one HIP stream (vh_ctx)."""
 
@@ -153,6 +197,7 @@ class Context:
         self.h = h
         self.device = device
         self.ci_tables = {}   # id(SphereTable) -> (table, vh_ci_table handle): tables stay in HBM
+        self.pinned = _PinnedPool(self)
 
     def link_probe(self, nbytes=256 << 20):
         """PCIe rates of this context's GPU with pinned host memory, GB/s: H2D alone, D2H alone,
@@ -181,6 +226,7 @@ class Context:
 
     def close(self):
         if getattr(self, "h", None):
+            self.pinned.close()
             for _, th in self.ci_tables.values():
                 self.L.vh_ci_table_destroy(th)
             self.ci_tables.clear()
@@ -336,9 +382,14 @@ def ci(defect, table, minvox, device=0, shell=True):
     """table: vent_analysis_amd.sphere.SphereTable for this shape (kept in HBM per context after
     the first call).  Returns (ci f64, scalar[B], shell int32 or None)."""
     c = context(device)
-    d = as_batch(np.asarray(defect) != 0, np.uint8)
+    d = np.asarray(defect)
+    if d.dtype == np.bool_:
+        d = d.view(np.uint8)   # (no copy: the kernels test != 0)
+    elif d.dtype != np.uint8:
+        d = d != 0
+    d = as_batch(d, np.uint8)   # a u8 map goes in as it is (nonzero = defect, CI.py:37)
     B, R, C, Z = d.shape
-    out = np.empty((B, R, C, Z), np.float64)
+    out = c.pinned.array((B, R, C, Z), np.float64)   # page-locked: the map's D2H at the link rate
     sh = np.empty((B, R, C, Z), np.int32) if shell else None
     sc = np.zeros(B, np.float64)
     th = c.ci_table(table, R, C)

@@ -1446,6 +1446,20 @@ int vh_link_probe(vh_ctx *ctx, int64_t bytes, double out_gbps[3]) {
     })
 }
 
+int vh_host_alloc(vh_ctx *ctx, int64_t bytes, void **out) {
+    if (out) *out = nullptr;
+    API_TRY(ctx, {
+        if (!out || bytes <= 0) throw VhError{VH_ERR_ARG, "host alloc: bad arguments"};
+        HIP_TRY(hipSetDevice(ctx->device));
+        HIP_TRY(hipHostMalloc(out, (size_t)bytes, hipHostMallocDefault));
+    })
+}
+
+int vh_host_free(void *p) {
+    if (p) (void)hipHostFree(p);
+    return VH_OK;
+}
+
 int vh_pipe_destroy(vh_pipe *p) {
     if (p) {
         (void)hipSetDevice(p->ctx->device);

@@ -161,6 +161,7 @@ __global__ void k_ci_clear(int32_t *status, unsigned long long *count, int64_t n
 // exclusive scan of the run sums finds the run holding the crossing, and that run is walked (one
 // thread per volume walked every shell serially: 16 us, r4ab).  Integer sums: order-free.
 #define CIF_TPB 256
+#define CIF_LDS 16384   // shells staged in LDS (64 KiB)
 __global__ void __launch_bounds__(CIF_TPB) k_ci_finish(const uint32_t *hist, const unsigned long long *count,
                                                       const double *radii, int64_t nbs, double minvox,
                                                       int64_t nb, const int32_t *status, VolScalars *sc) {
@@ -178,7 +179,15 @@ __global__ void __launch_bounds__(CIF_TPB) k_ci_finish(const uint32_t *hist, con
     if (status[b] || D == 0) return;   // block-uniform
     const unsigned long long i95 = (unsigned long long)(int64_t)(0.95 * (double)D);
     const int64_t per = (nbs + CIF_TPB - 1) / CIF_TPB, q0 = t * per, q1 = min(q0 + per, nbs);
+    // the histogram staged through LDS by coalesced loads first (one thread's run of dependent-
+    // address loads took ~16 us, r4al), when it fits
+    extern __shared__ uint32_t s_h[];
     const uint32_t *h = hist + b * nbs;
+    if (nbs <= CIF_LDS) {
+        for (int64_t q = t; q < nbs; q += CIF_TPB) s_h[q] = h[q];
+        __syncthreads();
+        h = s_h;
+    }
     unsigned long long own = 0;
     for (int64_t q = q0; q < q1; ++q) own += h[q];
     s_sum[t] = own;
@@ -311,8 +320,9 @@ void vh_ci_run(vh_batch *b, const vh_ci_table *t, double minvox, double *d_ci) {
             words, stage_bits, b->d_ci_shell, b->d_ci_hist, d_status);
         VH_CHECK_LAUNCH();
     }
-    k_ci_finish<<<(unsigned)b->nb, CIF_TPB, 0, st>>>(b->d_ci_hist, d_count, t->d_radii, nbs, minvox,
-                                                     b->nb, d_status, b->d_sc);
+    vh_set_max_lds((const void *)k_ci_finish, (int)(sizeof(uint32_t) * CIF_LDS + 4096));
+    k_ci_finish<<<(unsigned)b->nb, CIF_TPB, nbs <= CIF_LDS ? sizeof(uint32_t) * (size_t)nbs : 0, st>>>(
+        b->d_ci_hist, d_count, t->d_radii, nbs, minvox, b->nb, d_status, b->d_sc);
     VH_CHECK_LAUNCH();
     if (d_ci) {
         k_ci_scatter<<<vg, VH_TPB, 0, st>>>(b->d_ci_shell, b->d_defect, t->d_radii, minvox, b->V, d_ci);
