@@ -121,6 +121,8 @@ static void batch_free(vh_batch *b) {
     if (b->st_n4) (void)hipStreamDestroy(b->st_n4);
     if (b->ev_n4_pre) (void)hipEventDestroy(b->ev_n4_pre);
     if (b->ev_n4_post) (void)hipEventDestroy(b->ev_n4_post);
+    if (b->ev_cpre) (void)hipEventDestroy(b->ev_cpre);
+    if (b->ev_cpost) (void)hipEventDestroy(b->ev_cpost);
     if (b->h_flags) (void)hipHostFree(b->h_flags);
     delete b;
 }
@@ -433,6 +435,7 @@ int vh_destroy(vh_ctx *ctx) {
     if (ctx->comm) ncclCommDestroy((ncclComm_t)ctx->comm);
     if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
     if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
+    if (ctx->comm_st) (void)hipStreamDestroy(ctx->comm_st);
     if (ctx->recon_buf) (void)hipFree(ctx->recon_buf);
     delete ctx;
     return VH_OK;
@@ -1494,9 +1497,19 @@ int vh_batch_cohort_allreduce(vh_batch *b) {
     API_TRY(b->ctx, {
         vh_ctx *c = b->ctx;
         if (!c->comm) throw VhError{VH_ERR_ARG, "vh_comm_init has not been called"};
+        HIP_TRY(hipSetDevice(c->device));
+        if (!c->comm_st) HIP_TRY(hipStreamCreateWithFlags(&c->comm_st, hipStreamNonBlocking));
+        if (!b->ev_cpre) HIP_TRY(hipEventCreateWithFlags(&b->ev_cpre, hipEventDisableTiming));
+        if (!b->ev_cpost) HIP_TRY(hipEventCreateWithFlags(&b->ev_cpost, hipEventDisableTiming));
+        // after this batch's work, on the communicator's stream (program order across batches),
+        // and the batch's later work after it
+        HIP_TRY(hipEventRecord(b->ev_cpre, b->stream));
+        HIP_TRY(hipStreamWaitEvent(c->comm_st, b->ev_cpre, 0));
         ncclResult_t r = ncclAllReduce(b->d_cohort, b->d_cohort, VH_COHORT_BINS, ncclUint64, ncclSum,
-                                       (ncclComm_t)c->comm, b->stream);
+                                       (ncclComm_t)c->comm, c->comm_st);
         if (r != ncclSuccess) throw VhError{VH_ERR_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r)};
+        HIP_TRY(hipEventRecord(b->ev_cpost, c->comm_st));
+        HIP_TRY(hipStreamWaitEvent(b->stream, b->ev_cpost, 0));
     })
 }
 

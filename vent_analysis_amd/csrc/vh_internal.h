@@ -141,6 +141,10 @@ struct vh_ctx {
     mutable std::mutex err_mu;
     // vh_recon: its own stream and a cached device buffer (input, line transforms, output, twiddles)
     hipStream_t aux = nullptr;
+    // RCCL: every collective of the communicator on this one stream, in program order (batches in
+    // flight would otherwise issue them on their own streams, which the GPU may run in a different
+    // order than another rank does: a deadlock)
+    hipStream_t comm_st = nullptr;
     void *recon_buf = nullptr;
     size_t recon_cap = 0;
 };
@@ -175,6 +179,7 @@ struct vh_batch {
     hipStream_t stream = nullptr;    // every launch and copy of this batch (batches overlap)
     hipStream_t st_n4 = nullptr;     // VH_PRIO: the study kernel alone on a low-priority stream (the
     hipEvent_t ev_n4_pre = nullptr, ev_n4_post = nullptr;   // rest on a high-priority one), joined by events
+    hipEvent_t ev_cpre = nullptr, ev_cpost = nullptr;      // the cohort all-reduce on vh_ctx::comm_st
     int32_t *h_flags = nullptr;      // pinned: the sweep driver's per-iteration active counts
     int64_t R = 0, C = 0, Z = 0, V = 0, nb = 0, CZ = 0;
     int64_t max_tiles = 0;
