@@ -115,7 +115,8 @@ def test_ci_errors():
 def test_ci_table_api_equals_per_call_table():
     """vh_ci_tab with the HBM-resident table (vh_ci_table_create, reused across calls and batch
     sizes) equals vh_ci, which uploads the table per call; a table built for another (R, C) is
-    refused; shells, maps and scalars bit-identical; shell=None skips that copy."""
+    refused; shells, maps and scalars bit-identical; shell=None skips that copy; a caller's own
+    output array gets the same map."""
     import ctypes as ct
     rng = np.random.default_rng(5)
     shape = (70, 90, 12)
@@ -146,6 +147,10 @@ def test_ci_table_api_equals_per_call_table():
             assert np.array_equal(ci1, ci0) and np.array_equal(sc1, sc0) and np.array_equal(sh1, sh0)
         ci2, sc2, sh2 = _lib.ci(dd, table, 1.5, shell=False)
         assert sh2 is None and np.array_equal(ci2, ci0) and np.array_equal(sc2, sc0)
+        # the map into a caller's pageable array (device map + copy) equals the device-mapped
+        # pooled buffer the scatter writes directly
+        ci3, sc3, _ = _lib.ci(dd, table, 1.5, shell=False, out=np.full(dd.shape, np.nan))
+        assert np.array_equal(ci3, ci0) and np.array_equal(sc3, sc0)
         for q in range(b):
             ref, _ = native.ci(ds[q], table, vox)
             assert np.array_equal(ci0[q], ref)

@@ -378,9 +378,11 @@ def vdp(n4v, mask, vox, hp=None, thresh=0.6, device=0):
     return defect, bord, lb, list(res)
 
 
-def ci(defect, table, minvox, device=0, shell=True):
+def ci(defect, table, minvox, device=0, shell=True, out=None):
     """table: vent_analysis_amd.sphere.SphereTable for this shape (kept in HBM per context after
-    the first call).  Returns (ci f64, scalar[B], shell int32 or None)."""
+    the first call).  Returns (ci f64, scalar[B], shell int32 or None).  The map goes into a pooled
+    page-locked buffer the scatter kernel writes directly (vh_host_alloc), or into ``out`` (a
+    C-contiguous f64 array of the batch's shape: then through a device map and one copy)."""
     c = context(device)
     d = np.asarray(defect)
     if d.dtype == np.bool_:
@@ -389,7 +391,10 @@ def ci(defect, table, minvox, device=0, shell=True):
         d = d != 0
     d = as_batch(d, np.uint8)   # a u8 map goes in as it is (nonzero = defect, CI.py:37)
     B, R, C, Z = d.shape
-    out = c.pinned.array((B, R, C, Z), np.float64)   # page-locked: the map's D2H at the link rate
+    if out is None:
+        out = c.pinned.array((B, R, C, Z), np.float64)   # page-locked, device-mapped: no copy
+    elif out.dtype != np.float64 or out.size != B * R * C * Z or not out.flags.c_contiguous:
+        raise ValueError("ci: out must be a C-contiguous float64 array of the batch's size")
     sh = np.empty((B, R, C, Z), np.int32) if shell else None
     sc = np.zeros(B, np.float64)
     th = c.ci_table(table, R, C)

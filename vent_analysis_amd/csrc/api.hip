@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <map>
 #include <memory>
 #include <cstdio>
 #include <cstring>
@@ -419,7 +420,6 @@ int vh_create(int device, vh_ctx **out) {
     c->device = device;
     API_TRY(c, {
         HIP_TRY(hipSetDevice(device));
-        HIP_TRY(hipHostMalloc((void **)&c->h_pinned, sizeof(int32_t) * 1024));
         *out = c;
     })
 }
@@ -433,7 +433,7 @@ int vh_destroy(vh_ctx *ctx) {
         ctx->scratch = nullptr;
     }
     if (ctx->comm) ncclCommDestroy((ncclComm_t)ctx->comm);
-    if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
+    if (ctx->h_ci_sc) (void)hipHostFree(ctx->h_ci_sc);
     if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
     if (ctx->comm_st) (void)hipStreamDestroy(ctx->comm_st);
     if (ctx->recon_buf) (void)hipFree(ctx->recon_buf);
@@ -555,6 +555,21 @@ int vh_vdp(vh_ctx *ctx, const float *hp, const float *n4, const uint8_t *mask, i
     })
 }
 
+// page-locked host buffers handed out by vh_host_alloc, by base address: a CI map destined for one
+// is written there by the scatter kernel directly (device-mapped), with no staging copy
+static std::mutex g_host_mu;
+static std::map<uintptr_t, std::pair<size_t, void *>> g_host;   // base -> (bytes, device pointer)
+
+static void *host_mapped(const void *p, size_t bytes) {
+    std::lock_guard<std::mutex> lock(g_host_mu);
+    const uintptr_t a = (uintptr_t)p;
+    auto it = g_host.upper_bound(a);
+    if (it == g_host.begin()) return nullptr;
+    --it;
+    if (a + bytes > it->first + it->second.first) return nullptr;
+    return (char *)it->second.second + (a - it->first);
+}
+
 // CI on host buffers through a device-resident table; shared by vh_ci and vh_ci_tab
 static void ci_host(vh_ctx *ctx, const uint8_t *defect, int64_t R, int64_t C, int64_t Z, int64_t batch,
                     const vh_ci_table *t, double minvox, double *ci_array, double *ci_scalar, int32_t *shell) {
@@ -565,15 +580,30 @@ static void ci_host(vh_ctx *ctx, const uint8_t *defect, int64_t R, int64_t C, in
     b->profile = ctx->profile != 0;
     const size_t NV = (size_t)batch * b->V;
     HIP_TRY(hipMemcpyAsync(b->d_defect, defect, NV, hipMemcpyHostToDevice, b->stream));
-    if (ci_array && !b->d_ci_map) HIP_TRY(hipMalloc(&b->d_ci_map, sizeof(double) * NV));
-    vh_ci_run(b, t, minvox, ci_array ? b->d_ci_map : nullptr);
-    // every copy on the batch's stream, one sync at the end (the dense f64 map pinned in place for
-    // its DMA measured slower than the runtime's pageable path: 0.25 vs 0.23 ms per map, r4ac)
-    if (ci_array) HIP_TRY(hipMemcpyAsync(ci_array, b->d_ci_map, sizeof(double) * NV, hipMemcpyDeviceToHost, b->stream));
+    // the map straight into the caller's buffer when it is one of vh_host_alloc's (the scatter's
+    // stores cross the link; no device map, no copy), else a device map and one D2H
+    double *d_map = ci_array ? (double *)host_mapped(ci_array, sizeof(double) * NV) : nullptr;
+    if (ci_array && !d_map) {
+        if (!b->d_ci_map) HIP_TRY(hipMalloc(&b->d_ci_map, sizeof(double) * NV));
+        d_map = b->d_ci_map;
+    }
+    // the scalars likewise, into the context's device-mapped page-locked array (a small D2H runs as
+    // a blit kernel, r4al: 4.7 us plus its gap)
+    if (ctx->h_ci_sc_cap < batch) {
+        if (ctx->h_ci_sc) HIP_TRY(hipHostFree(ctx->h_ci_sc));
+        ctx->h_ci_sc = nullptr;
+        ctx->h_ci_sc_cap = 0;
+        HIP_TRY(hipHostMalloc((void **)&ctx->h_ci_sc, sizeof(VolScalars) * batch, hipHostMallocDefault));
+        ctx->h_ci_sc_cap = batch;
+    }
+    VolScalars *d_hsc = nullptr;
+    HIP_TRY(hipHostGetDevicePointer((void **)&d_hsc, ctx->h_ci_sc, 0));
+    vh_ci_run(b, t, minvox, d_map, d_hsc);
+    if (ci_array && d_map == b->d_ci_map)
+        HIP_TRY(hipMemcpyAsync(ci_array, b->d_ci_map, sizeof(double) * NV, hipMemcpyDeviceToHost, b->stream));
     if (shell) HIP_TRY(hipMemcpyAsync(shell, b->d_ci_shell, sizeof(int32_t) * NV, hipMemcpyDeviceToHost, b->stream));
-    std::vector<VolScalars> sc(batch);
-    HIP_TRY(hipMemcpyAsync(sc.data(), b->d_sc, sizeof(VolScalars) * batch, hipMemcpyDeviceToHost, b->stream));
     HIP_TRY(hipStreamSynchronize(b->stream));
+    const VolScalars *sc = ctx->h_ci_sc;
     for (int64_t i = 0; i < batch; ++i) {
         if (ci_scalar) ci_scalar[i] = sc[i].ci_scalar;
         if (sc[i].ci_status == VH_ERR_MAXRADIUS)
@@ -1455,11 +1485,26 @@ int vh_host_alloc(vh_ctx *ctx, int64_t bytes, void **out) {
         if (!out || bytes <= 0) throw VhError{VH_ERR_ARG, "host alloc: bad arguments"};
         HIP_TRY(hipSetDevice(ctx->device));
         HIP_TRY(hipHostMalloc(out, (size_t)bytes, hipHostMallocDefault));
+        void *dp = nullptr;
+        if (hipHostGetDevicePointer(&dp, *out, 0) != hipSuccess || !dp) {
+            (void)hipGetLastError();
+            dp = nullptr;
+        }
+        if (dp) {
+            std::lock_guard<std::mutex> lock(g_host_mu);
+            g_host[(uintptr_t)*out] = {(size_t)bytes, dp};
+        }
     })
 }
 
 int vh_host_free(void *p) {
-    if (p) (void)hipHostFree(p);
+    if (p) {
+        {
+            std::lock_guard<std::mutex> lock(g_host_mu);
+            g_host.erase((uintptr_t)p);
+        }
+        (void)hipHostFree(p);
+    }
     return VH_OK;
 }
 

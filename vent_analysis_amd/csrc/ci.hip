@@ -164,16 +164,23 @@ __global__ void k_ci_clear(int32_t *status, unsigned long long *count, int64_t n
 #define CIF_LDS 16384   // shells staged in LDS (64 KiB)
 __global__ void __launch_bounds__(CIF_TPB) k_ci_finish(const uint32_t *hist, const unsigned long long *count,
                                                       const double *radii, int64_t nbs, double minvox,
-                                                      int64_t nb, const int32_t *status, VolScalars *sc) {
+                                                      int64_t nb, const int32_t *status, VolScalars *sc,
+                                                      VolScalars *hsc) {
     __shared__ unsigned long long s_sum[CIF_TPB];
     __shared__ int s_hit;
     const int64_t b = blockIdx.x;
     const int t = threadIdx.x;
     const int64_t D = (int64_t)count[b];
     if (t == 0) {
+        const int32_t cs = status[b] ? VH_ERR_MAXRADIUS : (D == 0 ? VH_ERR_EMPTY : VH_OK);
         sc[b].n_ci = D;
-        sc[b].ci_status = status[b] ? VH_ERR_MAXRADIUS : (D == 0 ? VH_ERR_EMPTY : VH_OK);
+        sc[b].ci_status = cs;
         sc[b].ci_scalar = 0.0;
+        if (hsc) {   // the host's page-locked copy (vector stores over the link)
+            hsc[b].n_ci = D;
+            hsc[b].ci_status = cs;
+            hsc[b].ci_scalar = 0.0;
+        }
         s_hit = -1;
     }
     if (status[b] || D == 0) return;   // block-uniform
@@ -208,6 +215,7 @@ __global__ void __launch_bounds__(CIF_TPB) k_ci_finish(const uint32_t *hist, con
             cum += h[q];
             if (cum > i95) {
                 sc[b].ci_scalar = radii[q] * minvox;
+                if (hsc) hsc[b].ci_scalar = radii[q] * minvox;
                 break;
             }
         }
@@ -272,8 +280,10 @@ void vh_ci_table_free(vh_ci_table *t) {
 }
 
 // results stay on device (d_ci_shell, d_sc); the float64 CI map goes to d_ci (nb*V doubles) when
-// given.  Enqueued on the batch's stream; the caller synchronises.
-void vh_ci_run(vh_batch *b, const vh_ci_table *t, double minvox, double *d_ci) {
+// given -- device memory, or a device-mapped page-locked host buffer the scatter writes across the
+// link -- and the CI scalars also to h_sc (device-mapped host memory) when given.  Enqueued on the
+// batch's stream; the caller synchronises.
+void vh_ci_run(vh_batch *b, const vh_ci_table *t, double minvox, double *d_ci, VolScalars *h_sc) {
     if (t->R != b->R || t->C != b->C) throw VhError{VH_ERR_ARG, "sphere table built for another (R, C)"};
     hipStream_t st = b->stream;
     const int64_t words = (b->V + 31) / 32, rows = t->rows, nbs = t->nbs;
@@ -322,7 +332,7 @@ void vh_ci_run(vh_batch *b, const vh_ci_table *t, double minvox, double *d_ci) {
     }
     vh_set_max_lds((const void *)k_ci_finish, (int)(sizeof(uint32_t) * CIF_LDS + 4096));
     k_ci_finish<<<(unsigned)b->nb, CIF_TPB, nbs <= CIF_LDS ? sizeof(uint32_t) * (size_t)nbs : 0, st>>>(
-        b->d_ci_hist, d_count, t->d_radii, nbs, minvox, b->nb, d_status, b->d_sc);
+        b->d_ci_hist, d_count, t->d_radii, nbs, minvox, b->nb, d_status, b->d_sc, h_sc);
     VH_CHECK_LAUNCH();
     if (d_ci) {
         k_ci_scatter<<<vg, VH_TPB, 0, st>>>(b->d_ci_shell, b->d_defect, t->d_radii, minvox, b->V, d_ci);

@@ -128,8 +128,9 @@ struct vh_ctx {
     std::string last_error;
     void *comm = nullptr;           // ncclComm_t
     int nranks = 1, rank = 0;
-    // pinned scratch for small readbacks
-    int32_t *h_pinned = nullptr;
+    // page-locked, device-mapped CI scalars (k_ci_finish stores them there: no readback copy)
+    VolScalars *h_ci_sc = nullptr;
+    int64_t h_ci_sc_cap = 0;
     // the host-buffer entry points (vh_n4, vh_vdp, ...) share one cached scratch batch per
     // context; mu serialises them, so a context may be used from several host threads
     vh_batch *scratch = nullptr;
@@ -297,7 +298,7 @@ void vh_n4_prepare_tables(vh_batch *b, const vh_n4_params &prm);
 vh_ci_table *vh_ci_table_build(vh_ctx *ctx, int64_t R, int64_t C, const int16_t *offs, const uint8_t *dup,
                                int64_t rows, const int32_t *bounds, const double *radii, int64_t nbs);
 void vh_ci_table_free(vh_ci_table *t);
-void vh_ci_run(vh_batch *b, const vh_ci_table *t, double minvox, double *d_ci);
+void vh_ci_run(vh_batch *b, const vh_ci_table *t, double minvox, double *d_ci, VolScalars *h_sc = nullptr);
 void vh_ensure_n4_workspace(vh_batch *b, const vh_n4_params &prm);
 
 // ---- shared host helpers ----------------------------------------------------------------------
