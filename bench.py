@@ -576,7 +576,7 @@ def main():
     _, _, _, _, res = Bt.download(n4=False, maps=False)
     st_us = Bt.study_times()   # per-study wall time of the last step's one-workgroup-per-study N4
     if os.environ.get("VH_STUDY_TRACE"):   # the other batches' placements too (A/B runs)
-        for b_ in batches[1:]:
+        for b_ in batches[1:args.steps]:
             b_.study_times()
     tail = None
     if st_us.max() > 0:
@@ -586,7 +586,9 @@ def main():
     used_study = args.n4_mode == "study" or (args.n4_mode == "auto" and nb >= 16)
     kernels = {}
     if not args.no_profile:
-        results = [res] + [b_.download(n4=False, maps=False)[4] for b_ in batches[1:]]
+        # (a batch the timed steps never reached -- steps < batches in flight -- has no results)
+        results = [res] + [b_.download(n4=False, maps=False)[4] if i < args.steps else None
+                           for i, b_ in enumerate(batches[1:], 1)]
         for name in _lib.lib().vh_batch_kernel_names().decode().split(";"):
             tot_ms, tot_n, tot_b = 0.0, 0, 0.0
             for i, b_ in enumerate(batches):
