@@ -1312,15 +1312,19 @@ __device__ __forceinline__ void pcw_scan(PcShared<NL> &S, double a, double b, do
 }
 
 // initial guesses (all threads): running mean / variance sum in double from the pass-0 block sums
+// gd: the double running mean at the block start; dr: the float trajectory's offset from it at the
+// previous call (PC_DRIFT), 0 without one
 template <int NL>
-__device__ void pcw_guess(PcShared<NL> &S, const PcMap &m) {
+__device__ void pcw_guess(PcShared<NL> &S, const PcMap &m, double &gd, float dr = 0.0f) {
     const uint32_t j = threadIdx.x;
     double dm, ds;
     pcw_scan<NL>(S, 1.0, S.s1(j), S.s2(j), dm, ds);   // exclusive sums of s1 (dm) and s2 (ds)
     const double K = (double)(pc_k0(m, j) - 1u);
     float g = 0.0f, gs = 0.0f;
+    gd = 0.0;
     if (K > 0.0) {
-        g = (float)(1.0 + dm / K);
+        gd = 1.0 + dm / K;
+        g = (float)(gd + (double)dr);
         const double v = ds - dm * (dm / K);
         gs = (float)(v > 0.0 ? v : 0.0);
     }
@@ -1684,10 +1688,14 @@ __host__ __device__ constexpr size_t pcw_lds_bytes() {
 template <int NL, bool PEXP = false, class LoadD>
 __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n, PcShared<NL> &S,
                                                   ChainState &ch, int req, double *tbuf, int tcap,
-                                                  float skip_thresh = 0.0f) {
+                                                  float skip_thresh = 0.0f, float *drift = nullptr,
+                                                  bool drift_in = false) {
     const int tid = threadIdx.x;
     const PcMap m = pc_map(n, NL);
     const uint32_t j = (uint32_t)tid, len = pc_len(m, j), k0 = pc_k0(m, j);
+    // the previous call's offsets of the exact block starts from the double running mean (the float
+    // mean's drift changes little from one iteration to the next): added to this call's guesses
+    const float dr = drift && drift_in ? drift[j] : 0.0f;
 #ifdef PC_PROF
     const unsigned long long c0 = clock64();
     unsigned long long c1 = 0, c2 = 0;
@@ -1785,7 +1793,8 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
                               ok && fa2 <= fb2 ? f_up(fa2) : inf, ok && fa2 <= fb2 ? f_dn(fb2) : -inf);
     }
     __syncthreads();
-    pcw_guess<NL>(S, m);
+    double gd;
+    pcw_guess<NL>(S, m, gd, dr);
     __syncthreads();
 #ifdef PC_PROF
     c1 = clock64();
@@ -1968,6 +1977,8 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
             break;
         }
     }
+    // stage 0 reached its fixed point (xs): the block starts are the exact float trajectory's
+    if (drift && xs) drift[j] = (float)((double)S.b[j].gmu - gd);
     if (tid == 0) {
         ch.mu = S.mu;
         ch.conv = itk_conv(S.mu, S.sig, n);

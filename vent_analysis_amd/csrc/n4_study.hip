@@ -49,6 +49,9 @@
 #define ST_HC 4        // LDS histogram copies (in the emap's DEN buffer, free until the Wiener pass)
 #define ST_NFIRST 16   // first masked voxels (raster order) tracked for the bin minimum (n4_shared.h r3_bin_min)
 #define ST_MAX_LDS (160 * 1024)
+#ifndef PC_DRIFT
+#define PC_DRIFT 1   // PC's first guesses carry the previous iteration's drift (pcw_run; r4at: 18.89 -> 18.63 ms)
+#endif
 #ifndef ST_EVAL_EXP
 #define ST_EVAL_EXP 0   // 1: eval stores p = expf_cr(d) for PC (its pass 0 then skips the exp)
 #endif
@@ -100,6 +103,7 @@ struct StudyArgs {
     double *den;     // [nb][lat_cap] fit denominators of the current level
     int64_t lat_cap;
     float *Tg;       // [nb][2][tcap] T(i, col) of the last two fields, col fastest (stride CZ)
+    float *pcdrift;  // [nb][ST_TPB] PC: the last call's block-start offsets (PC_DRIFT), or null
     int64_t tcap;
 };
 
@@ -983,7 +987,8 @@ __global__ void __launch_bounds__(ST_TPB, 4) k_n4_study(StudyArgs a) {
                     // level goes on: PC may certify "above the threshold" without the exact sig
                     pcw_run<ST_TPB, ST_EVAL_EXP>([=](int64_t r) { return Dr[r]; }, a.D + a.half + b * a.VS, n, PW, M.ch, itk,
                             reinterpret_cast<double *>(a.D + b * a.VS), (int)(a.VS / 2),
-                            itk < a.lvs->max_iters[L] ? a.thresh : 0.0f);
+                            itk < a.lvs->max_iters[L] ? a.thresh : 0.0f,
+                            a.pcdrift ? a.pcdrift + (size_t)b * ST_TPB : nullptr, !(L == 0 && itk == 1));
                     if (t == 0) {
                         M.conv = (double)M.ch.conv;
                         M.pc_rounds += PW.rounds;
@@ -1226,6 +1231,11 @@ void vh_launch_n4_study(vh_batch *b, const vh_n4_params &prm) {
     a.lat_cap = b->lat_cap;
     a.Tg = b->d_T;
     a.tcap = b->t_cap;
+    a.pcdrift = nullptr;
+    if (PC_DRIFT) {
+        if (!b->d_pcdrift) HIP_TRY(hipMalloc(&b->d_pcdrift, sizeof(float) * ST_TPB * b->nb));
+        a.pcdrift = b->d_pcdrift;
+    }
     vh_set_max_lds((const void *)k_n4_study, ST_MAX_LDS);
     size_t lds = Ly.bytes;
     if (const char *e = getenv("VH_ST_MIN_LDS"))   // A/B runs: more LDS than needed, fewer studies per CU

@@ -232,6 +232,7 @@ struct vh_batch {
     int64_t n4_tiles = 0;
     std::vector<size_t> lvx_off;     // per level: xst / wk3 / wk2 offsets in d_tabs
     double *d_P1 = nullptr, *d_den = nullptr;
+    float *d_pcdrift = nullptr;      // [nb][1024] the study kernel's PC guess offsets (PC_DRIFT)
     float *d_T = nullptr;            // [2][nb][CZ][ncx] per-column lattice contraction (new / previous field)
     int64_t t_cap = 0;
     N4State *d_st = nullptr;
