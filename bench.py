@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import re
 import os
 import sys
 import time
@@ -162,7 +163,10 @@ def pmc_traffic(kernel):
     """Per-launch HBM-side bytes of ``kernel`` from the newest committed PMC summary
     (profiles/r*_pmc_traffic.json, written by scripts/pmc_summary.py), or None."""
     import glob
-    files = sorted(glob.glob(os.path.join(HERE, "profiles", "r*_pmc_traffic.json")))
+    def run_order(f):   # r<round><tag>: tags run a..z, then aa..az, ... (r4z before r4av)
+        m = re.match(r"r(\d+)([a-z]*)", os.path.basename(f))
+        return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
+    files = sorted(glob.glob(os.path.join(HERE, "profiles", "r*_pmc_traffic.json")), key=run_order)
     if not files:
         return None, None
     k = json.load(open(files[-1]))["kernels"].get(kernel)
