@@ -5,6 +5,7 @@
 // every iteration.
 #pragma once
 #include "vh_internal.h"
+#include "expf_small.h"
 #include <cfloat>
 
 struct DevAxis {
@@ -62,6 +63,10 @@ __device__ __forceinline__ void wave_lds_order() {
 
 // correctly rounded float exp through double (S1/S7/S9)
 __device__ __forceinline__ float expf_cr(float x) { return (float)exp((double)x); }
+// the same floats, by a short double polynomial when |x| <= 2^-5 (expf_small.h; PC pass 0)
+__device__ __forceinline__ float expf_crs(float x) {
+    return vh_expf_small(x, [](float v) { return expf_cr(v); });
+}
 // the Wiener kernel's Gaussian tail: (float)exp((double)x) is +0 for every float x < -104
 // (e^-104 < 2^-150, half the smallest float denormal), and the double exp of such an argument
 // took ~30 k cycles a step in the E map (ST_PROF r4e: thread 300's exp 0.96 M cycles per study)
@@ -1677,6 +1682,9 @@ static_assert(PC_APASS >= 1 && PC_APASS <= 2, "PC_APASS: 1 or 2 phase-A stages (
 #ifndef PC_G0
 #define PC_G0 8
 #endif
+#ifndef PC_EXPS
+#define PC_EXPS 0   // pass 0's exp by expf_crs (the same floats)
+#endif
 #ifndef PC_S12F
 #define PC_S12F 1   // the guesses' block sums in float (r4ar: 18.87 vs 18.93 ms per isolated launch)
 #endif
@@ -1748,7 +1756,11 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
 #pragma unroll
         for (int i = 0; i < G0; ++i)
             if (g0 + i < len) {
-                const float p = PEXP ? T0[i * TS + j] : expf_cr(T0[i * TS + j]);
+#ifdef AB_P0_FASTEXP   // A/B probe only (results not the spec's): pass 0 without the double exp
+                const float p = PEXP ? T0[i * TS + j] : __expf(T0[i * TS + j]);
+#else
+                const float p = PEXP ? T0[i * TS + j] : PC_EXPS ? expf_crs(T0[i * TS + j]) : expf_cr(T0[i * TS + j]);
+#endif
                 P[(size_t)(g0 + i) * NL + j] = p;
 #if PC_S12F
                 const float e = p - 1.0f;
