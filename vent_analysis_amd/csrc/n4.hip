@@ -1462,7 +1462,7 @@ __global__ void __launch_bounds__(PC_TPB) k_n4_pcg(PcgArgs A) {
 #pragma unroll
         for (int i = 0; i < 8; ++i)
             if (s0 + i < len) {
-                const float p = expf_cr(v[i]);
+                const float p = expf_crs(v[i]);
                 A.P[(size_t)(s0 + i) * NB + j] = p;
                 const double e = (double)p - 1.0;
                 s1 += e;

@@ -638,7 +638,7 @@ __device__ void chain_wave_prod(const float *Dr, const int32_t *perm, int64_t n,
         dnext = ld_d(blk + np, p1);
         p1 = ld_perm(blk + 2 * np);
         const bool ok = j < n;
-        const float p = expf_cr(d);
+        const float p = expf_crs(d);
         const double N = itk_Nd((double)(j + 1));
         const double r = 1.0 / N;
         const double2 ab = ok ? make_double2(1.0 - r, (double)(float)((double)p * r))   // p / N, div_r form
@@ -1683,7 +1683,7 @@ static_assert(PC_APASS >= 1 && PC_APASS <= 2, "PC_APASS: 1 or 2 phase-A stages (
 #define PC_G0 8
 #endif
 #ifndef PC_EXPS
-#define PC_EXPS 0   // pass 0's exp by expf_crs (the same floats)
+#define PC_EXPS 1   // pass 0's exp by expf_crs (the same floats; r4ax: 18.62 -> 18.44 ms per isolated launch)
 #endif
 #ifndef PC_S12F
 #define PC_S12F 1   // the guesses' block sums in float (r4ar: 18.87 vs 18.93 ms per isolated launch)
