@@ -32,3 +32,4 @@ float vh_expf_small(float x, FullExp full) {
     if (dm > -256 && dm < 256) return full(x);
     return (float)p;
 }
+
