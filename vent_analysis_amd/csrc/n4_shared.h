@@ -1065,7 +1065,7 @@ __device__ __forceinline__ bool pc_frozen(float4 z, float m) {
 // Returns true when it reached the last block: stage 0's next round then matches everywhere and
 // PCX gives sig.  Otherwise the exact starts it set stay as guesses and stage 1 goes on.
 #ifndef PC_AMAX0
-#define PC_AMAX0 40   // stage 0's round cap, where the frozen serial takes over
+#define PC_AMAX0 28   // stage 0's round cap, where the frozen serial takes over (r4ba / r4bb: 20 / 24 / 28 / 40 / 56 -> 18.72 / 18.42 / 18.34 / 18.43 / 18.51 ms with the drift-seeded guesses)
 #endif
 #ifndef PC_FRZ_RUN
 #define PC_FRZ_RUN 96   // blocks run step by step (~10 k cycles each) before handing back to the rounds
