@@ -254,7 +254,9 @@ __device__ __forceinline__ void st_store(__amdgpu_buffer_rsrc_t r, uint32_t voff
 // ---------------------------------------------------------------------------------------------
 #define FIT_NB 4        // finished control rows per contraction batch (max)
 #define FIT_SO 4        // stage-1 outputs per lane per chunk
-#define FIT_G 8         // rows per lane with loads in flight together
+#ifndef FIT_G
+#define FIT_G 6         // rows per lane with loads in flight together (r4bf / r4bg: 4 / 5 / 6 / 7 / 8 / 12 -> 17.97 / 18.00 / 17.89 / 18.15 / 18.27 / 22.2 ms isolated)
+#endif
 
 struct FitRing {
     double *q;        // [nbmax][rowcap] this wave's rows
