@@ -198,6 +198,27 @@ def max_over_ranks(dt, dist):
     return float(t.item())
 
 
+def check_cohort(local, reduced, dist):
+    """N > 1 self-check of the cohort all-reduce: the histogram the communicator summed must equal
+    the per-rank histograms summed over gloo (an independent path).  Every rank learns the verdict
+    (MIN over ranks), so a mismatch on any rank fails every rank."""
+    import torch
+    g = torch.from_numpy(np.ascontiguousarray(local, dtype=np.int64))
+    dist.all_reduce(g, op=dist.ReduceOp.SUM)
+    mine = int(np.array_equal(np.asarray(reduced, dtype=np.int64), g.numpy()))
+    ok = torch.tensor([mine], dtype=torch.int64)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    return bool(ok.item()), int(g.numpy().sum())
+
+
+def per_rank(value, dist):
+    """Every rank's value of a per-rank quantity, in rank order (gloo all_gather)."""
+    import torch
+    out = [torch.zeros(1, dtype=torch.float64) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, torch.tensor([float(value)], dtype=torch.float64))
+    return [float(t.item()) for t in out]
+
+
 class stdout_to_stderr:
     """RCCL's communicator setup prints a version banner on stdout; rank 0's stdout must carry the
     one JSON line only (the driver parses it), so fd 1 points at fd 2 while the block runs."""
@@ -399,7 +420,7 @@ def main_dry(args, rank, world, dist):
     if os.environ.get("VH_DRY_FAIL_RANK") == str(rank):   # tests: a failing rank fails the job
         raise SystemExit(3)
 
-    def step():   # per-rank cohort rows (numpy stand-in for k_cohort_*), summed over the ranks
+    def local_rows():   # per-rank cohort rows (numpy stand-in for k_cohort_*)
         h = np.zeros(1024, np.int64)
         for x, m in zip(hp, mk):
             s = np.sort(x[m > 0])
@@ -407,7 +428,10 @@ def main_dry(args, rank, world, dist):
             nv = nv[(nv >= 0) & (nv < np.float32(1.5))]
             h += np.bincount(np.minimum((nv * np.float32(1024 / 1.5)).astype(np.int64), 1023),
                              minlength=1024)
-        t = torch.from_numpy(h)
+        return h
+
+    def step():   # the stand-in communicator's all-reduce (RCCL's on the GPU)
+        t = torch.from_numpy(local_rows())
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         return t.numpy()
 
@@ -415,21 +439,35 @@ def main_dry(args, rank, world, dist):
         step()
     dist.barrier()
     t0 = time.perf_counter()
+    t_local = None
     for _ in range(args.steps):
         hist = step()
+    t_local = time.perf_counter() - t0
     dist.barrier()
     dt = max_over_ranks(time.perf_counter() - t0, dist)
+    # the GPU line's self-check with the stand-in communicator: local rows, the communicator's sum,
+    # the gloo sum of the per-rank rows
+    loc = local_rows()
+    if os.environ.get("VH_DRY_BAD_SUM") == str(rank):   # tests: a wrong all-reduce is caught
+        loc = loc + 1
+    ok, total_rows = check_cohort(loc, hist, dist)
+    rates = per_rank(args.batch * args.steps / t_local, dist)
     line = {"metric": METRIC, "value": round(world * args.batch * args.steps / dt, 2),
             "unit": "volumes/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": "dry run (CPU, no GPU work)", "volumes_per_gpu": args.batch,
                        "shape": [R, C, Z], "parallelism": f"dp{world}"},
+            "comm": {"kind": "gloo stand-in (dry run)", "rccl_ranks": dist.get_world_size(),
+                     "allreduce_ok": ok, "cohort_total": total_rows},
+            "per_rank_vol_s": [round(r, 2) for r in rates],
             "dry_run": {"uid_ok": uid == bytes(range(128)), "cohort_hist": hist.tolist(),
                         "rank_seeds": [shard_seed(r) for r in range(world)]}}
     if rank == 0:
         print(json.dumps(line), flush=True)
     dist.destroy_process_group()
+    if not ok:
+        sys.exit("bench.py: the cohort all-reduce differs from the sum of the per-rank histograms")
 
 
 def main():
@@ -522,12 +560,18 @@ def main():
     hp, mk = data[0]
     Bt = batches[0]
     use_comm = world > 1 or args.comm
+    comm = None
     with stdout_to_stderr():
         if world > 1:
             uid = broadcast_uid(_lib.comm_unique_id() if rank == 0 else None, dist)
             _lib.comm_init(world, rank, uid, device=local)
         elif args.comm:
             _lib.comm_init(1, 0, _lib.comm_unique_id(), device=local)
+        if use_comm:   # what RCCL itself reports (ncclCommCount / ncclCommUserRank)
+            n_rccl, r_rccl = _lib.comm_info(device=local)
+            comm = {"kind": "rccl", "rccl_ranks": n_rccl, "rccl_rank": r_rccl}
+            if n_rccl != world or r_rccl != rank:
+                sys.exit(f"bench.py: RCCL reports rank {r_rccl} of {n_rccl}, expected {rank} of {world}")
     vox = (1.5, 1.5, 10.0)
     opts = Bt.options(do_n4=not args.no_n4, vox=vox, do_cohort=True,
                       profile=not args.no_profile, n4_subbatch=args.subbatch,
@@ -572,11 +616,27 @@ def main():
         step(opts, i)
     sync_all()
     sync_dev()
+    t_local = time.perf_counter() - t0
     if dist:
         dist.barrier()
     dt = time.perf_counter() - t0
+    rates = None
     if dist:
         dt = max_over_ranks(dt, dist)
+        rates = per_rank(nb * args.steps / t_local, dist)
+    if use_comm:
+        # after the timed region: one step of batch 0 without the collective, its local histogram,
+        # then RCCL's sum of it checked against the per-rank histograms summed over gloo
+        Bt.run(warm)
+        Bt.sync()
+        loc = Bt.cohort_hist()
+        Bt.cohort_allreduce()
+        Bt.sync()
+        red = Bt.cohort_hist()
+        if dist:
+            comm["allreduce_ok"], comm["cohort_total"] = check_cohort(loc, red, dist)
+        else:   # one rank: the sum over one rank is the local histogram
+            comm["allreduce_ok"], comm["cohort_total"] = bool(np.array_equal(loc, red)), int(loc.sum())
     _, _, _, _, res = Bt.download(n4=False, maps=False)
     st_us = Bt.study_times()   # per-study wall time of the last step's one-workgroup-per-study N4
     if os.environ.get("VH_STUDY_TRACE"):   # the other batches' placements too (A/B runs)
@@ -700,8 +760,14 @@ def main():
         "host_to_host_vol_s": round(world * h2h["volumes"] / h2h["seconds"], 2) if h2h else None,
         "host_to_host": h2h,
     }
+    if comm:
+        line["comm"] = comm
+    if rates:
+        line["per_rank_vol_s"] = [round(r, 2) for r in rates]
     if rank == 0:
         print(json.dumps(line), flush=True)
+    if comm and not comm["allreduce_ok"]:
+        sys.exit("bench.py: the RCCL cohort all-reduce differs from the sum of the per-rank histograms")
     if args.h2h_keep_batch:
         for b_ in batches:
             b_.close()

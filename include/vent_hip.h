@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define VH_ABI_VERSION 7
+#define VH_ABI_VERSION 8
 
 /* status codes */
 #define VH_OK 0
@@ -222,7 +222,8 @@ int vh_pipe_run(vh_pipe *p, const float *hp, const uint8_t *mask, int64_t n, con
 int vh_pipe_destroy(vh_pipe *p);
 /* The last vh_pipe_run's peak of caller memory pinned in place (bytes) and the caller ranges that
  * went through the pinned staging instead (not registrable, or past the VH_PIPE_PIN_CAP budget,
- * default 32 GiB: a long cohort run never page-locks more than that at once). */
+ * default 32 GiB per node divided by LOCAL_WORLD_SIZE: a long cohort run never page-locks more than
+ * that at once). */
 int vh_pipe_stats(vh_pipe *p, int64_t *pinned_peak_bytes, int64_t *staged_spans);
 /* This GPU's PCIe link with pinned host memory (bench.py's host-to-host bound): bytes copied H2D
  * alone, D2H alone and both at once on two streams, best of 3; out_gbps = {h2d, d2h, both}. */
@@ -239,6 +240,9 @@ int vh_comm_unique_id(uint8_t id[VH_COMM_ID_BYTES]);
 int vh_comm_init(vh_ctx *ctx, int nranks, int rank, const uint8_t id[VH_COMM_ID_BYTES]);
 /* Sum the batch's device cohort histogram over all ranks of the context's communicator. */
 int vh_batch_cohort_allreduce(vh_batch *b);
+/* The communicator as RCCL sees it: its rank count (ncclCommCount) and this context's rank
+ * (ncclCommUserRank).  bench.py's N > 1 line reports both (ABI 8). */
+int vh_comm_info(vh_ctx *ctx, int *nranks, int *rank);
 int vh_comm_destroy(vh_ctx *ctx);
 
 #ifdef __cplusplus

@@ -193,12 +193,46 @@ def volume_litres(count, vox) -> float:
     return count * np.prod(np.divide(vox, 10)) / 1000
 
 
+def _km_boundary(x, clo, chi):
+    """First index of sorted x whose value is strictly closer to chi than to clo (clo < chi): the
+    predicate is monotone over sorted x; numpy's searchsorted bisection order."""
+    lo, hi = 0, x.shape[0]
+    while lo < hi:
+        mid = lo + ((hi - lo) >> 1)
+        if not (abs(x[mid] - chi) < abs(x[mid] - clo)):
+            lo = mid + 1
+        else:
+            hi = mid
+    return lo
+
+
 def kmeans_1d_sorted(s: np.ndarray, k: int = 4, max_iter: int = 300):
     """Build-defined k-means VDP (the reference only imports KMeans,
-    Vent_Analysis.py:19, 259-261).  Lloyd on sorted 1-D float32 data: centres start at the
-    order statistics s[floor(n (2j+1) / 2k)]; a value joins the nearest centre (ties -> lower
-    index); centres are float64 means.  Iterate until the partition stops changing.
-    Returns (counts[k], centres[k], iterations)."""
+    Vent_Analysis.py:19, and leaves the k-means VDP commented out, :259-261).  Lloyd on sorted 1-D
+    float32 data (float64 arithmetic), k = 4, centres kept sorted:
+
+    * start: the order statistics c_j = s[floor(n (2j + 1) / 2k)];
+    * assign: a value joins its nearest centre; equal centres -> the lowest index (a duplicate
+      centre gets no points), a value exactly between two centres -> the lower one.  Over sorted
+      centres the clusters are intervals: cut_{j+1} = the first value strictly closer to the next
+      larger centre value than to c_j (n when c_j is the largest);
+    * stop when the cuts repeat;
+    * update: c_j = the mean of cluster j.  A cluster left empty takes the value farthest from its
+      own cluster's centre among clusters of >= 2 values (a cluster's farthest values are its two
+      ends; ties -> the lowest index; a value at distance 0 is never taken), which leaves its
+      donor's sum -- scikit-learn's empty-cluster relocation (_relocate_empty_clusters_dense) with
+      its tie order fixed; an empty cluster with nothing to take keeps its centre.  Then the
+      centres are sorted.
+
+    On data with two or three distinct values every value ends in a cluster of its own, as in
+    scikit-learn 1.7.2's Lloyd from the same centres (tests/test_kmeans_oracle.py pins this);
+    with four or more distinct values and empty clusters, which Lloyd local minimum is reached
+    depends on the relocation tie order (scikit-learn's comes from np.argpartition), so there the
+    result is build-defined.  On non-degenerate data (distinct increasing centres, no empty
+    cluster) the steps reduce to plain Lloyd.
+
+    Returns (counts[k], centres[k] sorted, iterations).  VDP_km counts the lowest non-empty
+    cluster (:func:`kmeans_low_count`)."""
     n = s.shape[0]
     x = s.astype(np.float64)
     c = np.array([x[(n * (2 * j + 1)) // (2 * k)] for j in range(k)])
@@ -206,32 +240,52 @@ def kmeans_1d_sorted(s: np.ndarray, k: int = 4, max_iter: int = 300):
     cuts = None
     it = 0
     for it in range(1, max_iter + 1):
-        # boundary between j and j+1: first index whose value is strictly closer to c[j+1]
         newcuts = np.empty(k + 1, np.int64)
         newcuts[0], newcuts[k] = 0, n
         for j in range(k - 1):
-            # np.searchsorted((|x - c[j+1]| < |x - c[j]|).astype(int8), 1, side="left"), with the
-            # predicate evaluated only at the midpoints numpy's binary search visits (same result,
-            # O(log n) instead of two full passes per boundary)
-            lo_c, hi_c = c[j], c[j + 1]
-            lo, hi = 0, n
-            while lo < hi:
-                mid = lo + ((hi - lo) >> 1)
-                if not (abs(x[mid] - hi_c) < abs(x[mid] - lo_c)):
-                    lo = mid + 1
-                else:
-                    hi = mid
-            newcuts[j + 1] = lo
+            up = c[j + 1:][c[j + 1:] > c[j]]
+            newcuts[j + 1] = _km_boundary(x, c[j], up[0]) if up.size else n
         newcuts[1:k] = np.maximum.accumulate(newcuts[1:k])
         if cuts is not None and np.array_equal(newcuts, cuts):
             break
         cuts = newcuts
+        old = c.copy()
+        cnt = np.diff(cuts).astype(np.int64)
+        sums = np.array([cum[cuts[j + 1]] - cum[cuts[j]] for j in range(k)])
+        win = [[int(cuts[j]), int(cuts[j + 1])] for j in range(k)]
+        newc = c.copy()
         for j in range(k):
-            a, b = cuts[j], cuts[j + 1]
-            if b > a:
-                c[j] = (cum[b] - cum[a]) / (b - a)
+            if np.diff(cuts)[j] > 0:
+                continue
+            best, bi, bq = 0.0, -1, -1
+            for q in range(k):
+                a, e = win[q]
+                if e - a < 2:
+                    continue
+                for i in (a, e - 1):
+                    dd = abs(x[i] - old[q])
+                    if dd > best or (dd == best and dd > 0.0 and i < bi):
+                        best, bi, bq = dd, i, q
+            if bi >= 0:
+                newc[j] = x[bi]
+                sums[bq] -= x[bi]
+                cnt[bq] -= 1
+                if bi == win[bq][0]:
+                    win[bq][0] += 1
+                else:
+                    win[bq][1] -= 1
+        for j in range(k):
+            if cuts[j + 1] > cuts[j]:
+                newc[j] = sums[j] / cnt[j]
+        c = np.sort(newc)
     counts = np.diff(cuts)
     return counts, c, it
+
+
+def kmeans_low_count(counts) -> int:
+    """Voxels in the lowest non-empty k-means cluster (VDP_km's numerator)."""
+    nz = np.flatnonzero(np.asarray(counts) > 0)
+    return int(counts[nz[0]]) if nz.size else 0
 
 
 def calculate_vdp(N4: np.ndarray, mask: np.ndarray, vox, thresh: float = 0.6, HP=None,
@@ -263,7 +317,7 @@ def calculate_vdp(N4: np.ndarray, mask: np.ndarray, vox, thresh: float = 0.6, HP
     out["p99"] = p99
     out["VDP_lb"] = 100 * np.sum((lb == 1) * 1 + (lb == 2) * 1) / msum  # :257
     counts, centres, _ = kmeans_1d_sorted(sig)
-    out["VDP_km"] = 100 * counts[0] / msum
+    out["VDP_km"] = 100 * kmeans_low_count(counts) / msum
     out["km_centres"] = centres
     if HP is not None:
         out["SNR"] = calculate_snr(HP, mask)

@@ -30,7 +30,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_status_strings():
     L = _lib.lib()
-    assert L.vh_abi_version() == 7
+    assert L.vh_abi_version() == 8
     assert L.vh_status_string(0) == b"ok"
     assert b"maximum radius" in L.vh_status_string(_lib.VH_ERR_MAXRADIUS)
 

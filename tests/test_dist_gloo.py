@@ -99,6 +99,12 @@ def _check_dry_line(out, world):
         M.append(m)
     whole = cohort_hist(np.concatenate(X), np.concatenate(M))
     assert np.array_equal(np.array(line["dry_run"]["cohort_hist"]), whole)
+    # the self-check fields the GPU line carries: the communicator's rank
+    # count, the all-reduce checked against the gloo sum of per-rank rows, a rate per rank
+    assert line["comm"]["rccl_ranks"] == world
+    assert line["comm"]["allreduce_ok"] is True
+    assert line["comm"]["cohort_total"] == int(whole.sum())
+    assert len(line["per_rank_vol_s"]) == world and min(line["per_rank_vol_s"]) > 0
     return line
 
 
@@ -126,3 +132,10 @@ def test_bench_rank_failure_and_world_mismatch():
     assert not r.stdout.strip()
     r = _bench(["bench.py", "--gpus", "2"] + DRY, env={"WORLD_SIZE": "1", "RANK": "0"})
     assert r.returncode != 0 and "WORLD_SIZE 1 but --gpus 2" in r.stderr
+
+
+def test_bench_cohort_mismatch_fails():
+    """A rank whose all-reduced histogram differs from the per-rank sum fails the whole job."""
+    r = _bench(["bench.py", "--gpus", "2"] + DRY, env={"VH_DRY_BAD_SUM": "1"})
+    assert r.returncode != 0
+    assert "differs from the sum" in r.stderr

@@ -161,6 +161,42 @@ def test_ci_table_api_equals_per_call_table():
     assert rc == _lib.VH_ERR_ARG
 
 
+def test_ci_threads_many_tables():
+    """Several threads run CI on studies of 20 distinct voxel sizes (more than the 16 device
+    tables a context keeps: evictions happen while other threads hold handles).  Every map equals
+    the single-threaded oracle's (the table cache was unlocked, keyed by id())."""
+    import threading
+    from vent_analysis_amd import CI
+    shape = (40, 36, 9)
+    rng = np.random.default_rng(11)
+    d = (rng.random(shape) < 0.2).astype(np.uint8)
+    voxes = [(1.5, 1.5, 3.0 + 0.5 * i) for i in range(20)]
+    refs = {}
+    for vox in voxes:
+        ref, _ = native.ci(d, compact_table(sphere_pix(vox, 12), shape), vox)
+        refs[vox] = ref
+    errors = []
+
+    def worker(t):
+        try:
+            order = voxes[t:] + voxes[:t]
+            for vox in order + order[::-1]:
+                ci, _ = CI.calculate_CI_with_index(d, vox, Rmax=12)
+                if not np.array_equal(ci, refs[vox]):
+                    errors.append((t, vox))
+        except Exception as e:   # noqa: BLE001 -- reported below
+            errors.append((t, repr(e)))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors[:4]
+    c = _lib.context(0)
+    assert len(c.ci_tables) <= c.CI_TABLES_KEPT
+
+
 def ulps(a, b):
     """Distance in float32 units in the last place (same-sign values)."""
     ia = np.ascontiguousarray(a, np.float32).view(np.int32).astype(np.int64)
@@ -237,6 +273,7 @@ def test_rccl_cohort_allreduce_one_rank():
     assert len(uid) == _lib.COMM_ID_BYTES
     _lib.comm_init(1, 0, uid)
     try:
+        assert _lib.comm_info() == (1, 0)   # RCCL's own rank count and rank (ncclCommCount)
         hp, mk = synth_batch(128, 128, 24, 256, base_seed=4000, unique=16)
         B = _lib.Batch(128, 128, 24, 256)
         B.upload(hp, mk)
@@ -868,7 +905,8 @@ def test_mean_anchor_partial_chunk_lengths():
         assert np.float32(res[b].p99) == s_[int(n * 0.99)], n
 
 
-@pytest.mark.parametrize("kind", ["constant", "two_values", "negative", "ulp_range", "decades"])
+@pytest.mark.parametrize("kind", ["constant", "two_values", "three_values", "negative", "ulp_range",
+                                  "decades"])
 def test_sorted_statistics_adversarial(kind):
     """The per-volume radix sort (k_sort_vol), the numpy-order mean anchor, p99, k-means and the
     cohort rows on value distributions the synthetic generator never makes: a single value (every
@@ -884,6 +922,8 @@ def test_sorted_statistics_adversarial(kind):
         v = np.full(n, 3.25, np.float32)
     elif kind == "two_values":
         v = rng.choice(np.float32([1.5, 2.5]), n)
+    elif kind == "three_values":   # 5 % / 15 % / 80 %: equal initial centres, a mixed first cluster
+        v = rng.choice(np.float32([1.0, 2.0, 10.0]), n, p=[0.05, 0.15, 0.8])
     elif kind == "negative":
         v = rng.normal(-150.0, 50.0, n).astype(np.float32)
     elif kind == "ulp_range":
@@ -906,11 +946,12 @@ def test_sorted_statistics_adversarial(kind):
         assert np.float32(res[b].p99) == o["p99"]
         assert np.array_equal(d[b], o["defectArray"])
         assert np.array_equal(lb[b], o["defectArrayLB"])
-        if kind != "two_values":
-            # two values leave clusters 1-3 empty after one Lloyd step with their stale centres
-            # out of order; the build-defined boundary rule (Appendix B.8, oracle
-            # kmeans_1d_sorted) assumes ordered centres, so VDP_km has no defined value there
-            assert res[b].n_km0 * 100 / MM.sum() == pytest.approx(o["VDP_km"], abs=0)
+        # degenerate inputs included: empty clusters take the farthest value
+        # (oracle kmeans_1d_sorted, pinned to scikit-learn in tests/test_kmeans_oracle.py)
+        assert res[b].n_km0 * 100 / MM.sum() == pytest.approx(o["VDP_km"], abs=0)
+        assert np.allclose(list(res[b].km_centres), o["km_centres"], rtol=1e-12, atol=0)
+        if kind in ("two_values", "three_values"):   # every value a cluster of its own
+            assert res[b].n_km0 == int((XX[MM > 0] == XX[MM > 0].min()).sum())
         nv = (XX / np.float32(res[b].p99)).astype(np.float32)[MM > 0]
         sel = (nv >= 0) & (nv < np.float32(1.5))
         bi = np.minimum((nv[sel] * np.float32(_lib.COHORT_BINS / 1.5)).astype(np.int64), 1023)

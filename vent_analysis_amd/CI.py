@@ -55,7 +55,9 @@ def calculate_CI_with_index(defectArray, vox=(1, 1, 1), Rmax=50, device=0):
     d = np.asarray(defectArray)
     table = compact_table_for(vox, Rmax, d.shape)
     ci, scal, _ = _lib.ci(d, table, float(np.min(vox)), device=device, shell=False)
-    return ci[0], np.float64(scal[0])
+    # the map is kept for the object's life (Vent_Analysis.CIarray): copied out of the pooled
+    # page-locked buffer, which then goes back to the pool (no pinned memory per study)
+    return np.array(ci[0]), np.float64(scal[0])
 
 
 def calculate_CI(defectArray, vox=[1, 1, 1], Rmax=50, type='fast'):   # noqa: A002 (reference name)

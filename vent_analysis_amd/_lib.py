@@ -100,6 +100,7 @@ _SIGS = {
     "vh_comm_unique_id": ([_P], ct.c_int),
     "vh_comm_init": ([_P, ct.c_int, ct.c_int, _P], ct.c_int),
     "vh_batch_cohort_allreduce": ([_P], ct.c_int),
+    "vh_comm_info": ([_P, ct.POINTER(ct.c_int), ct.POINTER(ct.c_int)], ct.c_int),
     "vh_comm_destroy": ([_P], ct.c_int),
 }
 EXPORTED = tuple(_SIGS)
@@ -196,7 +197,11 @@ class Context:
                                f"{self.L.vh_status_string(rc).decode()}")
         self.h = h
         self.device = device
-        self.ci_tables = {}   # id(SphereTable) -> (table, vh_ci_table handle): tables stay in HBM
+        # (table key, R, C) -> (table, vh_ci_table handle), least recently used first: tables stay
+        # in HBM.  ci_lock covers the lookup, any eviction and the vh_ci_tab call that uses the
+        # handle, so no thread's handle is destroyed under it
+        self.ci_tables = {}
+        self.ci_lock = threading.RLock()
         self.pinned = _PinnedPool(self)
 
     def link_probe(self, nbytes=256 << 20):
@@ -206,16 +211,24 @@ class Context:
         self.check(self.L.vh_link_probe(self.h, int(nbytes), out), "vh_link_probe")
         return {"h2d_GBps": round(out[0], 2), "d2h_GBps": round(out[1], 2), "both_GBps": round(out[2], 2)}
 
+    CI_TABLES_KEPT = 16
+
     def ci_table(self, table, R, C):
         """The device copy of a compact sphere table for (R, C) volumes (vh_ci_table_create, once
-        per table object; the reference caches the table file the same way, CI.py:43-61)."""
-        key = (id(table), int(R), int(C))
-        hit = self.ci_tables.get(key)
-        if hit is not None and hit[0] is table:
+        per table content; the reference caches the table file the same way, CI.py:43-61).  Keyed
+        by ``table.key`` -- (vox, Rmax, R, C) for sphere.compact_table_for's tables -- or by the
+        object for ad-hoc tables.  Call with ``ci_lock`` held for as long as the handle is used."""
+        tk = getattr(table, "key", None)
+        key = (tk if tk is not None else ("obj", id(table)), int(R), int(C))
+        hit = self.ci_tables.pop(key, None)
+        if hit is not None and (tk is not None or hit[0] is table):
+            self.ci_tables[key] = hit   # most recently used last
             return hit[1]
-        if len(self.ci_tables) >= 8:   # drop the oldest
+        if hit is not None:   # an ad-hoc table whose id was reused
+            self.L.vh_ci_table_destroy(hit[1])
+        while len(self.ci_tables) >= self.CI_TABLES_KEPT:   # drop the least recently used
             k0 = next(iter(self.ci_tables))
-            self.L.vh_ci_table_destroy(self.ci_tables.pop(k0)[1])
+            self.L.vh_ci_table_destroy(self.ci_tables.pop(k0)[1])   # locks ctx->mu, drains
         h = _P()
         self.check(self.L.vh_ci_table_create(self.h, int(R), int(C), _ptr(table.offsets),
                                              _ptr(table.dup), table.rows, _ptr(table.bounds),
@@ -227,9 +240,10 @@ class Context:
     def close(self):
         if getattr(self, "h", None):
             self.pinned.close()
-            for _, th in self.ci_tables.values():
-                self.L.vh_ci_table_destroy(th)
-            self.ci_tables.clear()
+            with self.ci_lock:
+                for _, th in self.ci_tables.values():
+                    self.L.vh_ci_table_destroy(th)
+                self.ci_tables.clear()
             self.L.vh_destroy(self.h)
             self.h = None
 
@@ -397,9 +411,10 @@ def ci(defect, table, minvox, device=0, shell=True, out=None):
         raise ValueError("ci: out must be a C-contiguous float64 array of the batch's size")
     sh = np.empty((B, R, C, Z), np.int32) if shell else None
     sc = np.zeros(B, np.float64)
-    th = c.ci_table(table, R, C)
-    c.check(c.L.vh_ci_tab(c.h, _ptr(d), R, C, Z, B, th, ct.c_double(minvox), _ptr(out), _ptr(sc),
-                          _ptr(sh)), "vh_ci_tab")
+    with c.ci_lock:
+        th = c.ci_table(table, R, C)
+        c.check(c.L.vh_ci_tab(c.h, _ptr(d), R, C, Z, B, th, ct.c_double(minvox), _ptr(out), _ptr(sc),
+                              _ptr(sh)), "vh_ci_tab")
     return out, sc, sh
 
 
@@ -631,6 +646,14 @@ def comm_init(nranks: int, rank: int, uid: bytes, device=0):
     c = context(device)
     buf = np.frombuffer(uid, np.uint8).copy()
     c.check(c.L.vh_comm_init(c.h, nranks, rank, _ptr(buf)), "vh_comm_init")
+
+
+def comm_info(device=0):
+    """(ranks, rank) of the context's RCCL communicator as RCCL reports them (vh_comm_info)."""
+    c = context(device)
+    n, r = ct.c_int(0), ct.c_int(-1)
+    c.check(c.L.vh_comm_info(c.h, ct.byref(n), ct.byref(r)), "vh_comm_info")
+    return n.value, r.value
 
 
 def comm_destroy(device=0):

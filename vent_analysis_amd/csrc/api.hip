@@ -603,6 +603,7 @@ static void ci_host(vh_ctx *ctx, const uint8_t *defect, int64_t R, int64_t C, in
         HIP_TRY(hipMemcpyAsync(ci_array, b->d_ci_map, sizeof(double) * NV, hipMemcpyDeviceToHost, b->stream));
     if (shell) HIP_TRY(hipMemcpyAsync(shell, b->d_ci_shell, sizeof(int32_t) * NV, hipMemcpyDeviceToHost, b->stream));
     HIP_TRY(hipStreamSynchronize(b->stream));
+    vh_ci_debug_check();
     const VolScalars *sc = ctx->h_ci_sc;
     for (int64_t i = 0; i < batch; ++i) {
         if (ci_scalar) ci_scalar[i] = sc[i].ci_scalar;
@@ -636,7 +637,15 @@ int vh_ci_table_create(vh_ctx *ctx, int64_t R, int64_t C, const int16_t *offs, c
     })
 }
 
+// Tables are used only by ci_host on the context's scratch stream, under ctx->mu: taking the lock
+// waits for a CI call of another thread, and the scratch stream is drained before the hipFrees, so
+// no kernel can read a freed table (the destroy ran with neither).
 int vh_ci_table_destroy(vh_ci_table *t) {
+    if (!t) return VH_OK;
+    vh_ctx *ctx = t->ctx;
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    (void)hipSetDevice(ctx->device);
+    if (ctx->scratch) (void)hipStreamSynchronize(ctx->scratch->stream);
     vh_ci_table_free(t);
     return VH_OK;
 }
@@ -996,7 +1005,11 @@ int vh_pipe_create(vh_ctx *ctx, int64_t R, int64_t C, int64_t Z, int64_t sub, in
         vh_pipe *p = new vh_pipe;
         p->ctx = ctx;
         p->R = R; p->C = C; p->Z = Z; p->sub = sub;
-        p->pin_cap = (int64_t)32 << 30;
+        // a per-node budget of 32 GiB page-locked, shared by the node's ranks (LOCAL_WORLD_SIZE, as
+        // torchrun and bench.py set it): 8 ranks pin at most 4 GiB each
+        int64_t local_ranks = 1;
+        if (const char *e = getenv("LOCAL_WORLD_SIZE")) local_ranks = std::max<int64_t>(1, atoll(e));
+        p->pin_cap = ((int64_t)32 << 30) / local_ranks;
         if (const char *e = getenv("VH_PIPE_PIN_CAP")) p->pin_cap = atoll(e);
         const size_t NV = (size_t)sub * R * C * Z;
         try {
@@ -1555,6 +1568,20 @@ int vh_batch_cohort_allreduce(vh_batch *b) {
         if (r != ncclSuccess) throw VhError{VH_ERR_RCCL, std::string("ncclAllReduce: ") + ncclGetErrorString(r)};
         HIP_TRY(hipEventRecord(b->ev_cpost, c->comm_st));
         HIP_TRY(hipStreamWaitEvent(b->stream, b->ev_cpost, 0));
+    })
+}
+
+int vh_comm_info(vh_ctx *ctx, int *nranks, int *rank) {
+    API_TRY(ctx, {
+        if (!nranks || !rank) throw VhError{VH_ERR_ARG, "null out"};
+        if (!ctx->comm) throw VhError{VH_ERR_ARG, "vh_comm_init has not been called"};
+        int n = 0, r = -1;
+        ncclResult_t e = ncclCommCount((ncclComm_t)ctx->comm, &n);
+        if (e != ncclSuccess) throw VhError{VH_ERR_RCCL, std::string("ncclCommCount: ") + ncclGetErrorString(e)};
+        e = ncclCommUserRank((ncclComm_t)ctx->comm, &r);
+        if (e != ncclSuccess) throw VhError{VH_ERR_RCCL, std::string("ncclCommUserRank: ") + ncclGetErrorString(e)};
+        *nranks = n;
+        *rank = r;
     })
 }
 

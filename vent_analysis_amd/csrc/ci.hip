@@ -15,6 +15,25 @@
 
 #define CI_SENTINEL INT32_MIN
 
+// VH_DEBUG_BOUNDS builds (make DEBUG_BOUNDS=1 -> libventhip_dbg.so): every index the CI kernels
+// derive from data (defect list slots, table rows, shells, bitmap words) is checked against its
+// buffer's extent before the access; a violation skips the access and records (site, index, extent)
+// in g_ci_dbg, which ci_debug_check() reads after the call's stream sync and raises as VH_ERR_HIP.
+// Release builds compile the checks away (CI_OK(c, ...) == c is never evaluated as a guard).
+#ifdef VH_DEBUG_BOUNDS
+static __device__ unsigned long long g_ci_dbg[4];
+__device__ __forceinline__ bool ci_ok(bool c, int site, int64_t idx, int64_t ext) {
+    if (!c && atomicCAS(&g_ci_dbg[0], 0ull, (unsigned long long)site) == 0ull) {
+        atomicExch(&g_ci_dbg[1], (unsigned long long)idx);
+        atomicExch(&g_ci_dbg[2], (unsigned long long)ext);
+    }
+    return c;
+}
+#define CI_OK(c, site, idx, ext) ci_ok((c), (site), (int64_t)(idx), (int64_t)(ext))
+#else
+#define CI_OK(c, site, idx, ext) true
+#endif
+
 __global__ void k_ci_bitmap(const uint8_t *__restrict__ defect, int64_t s0, int64_t s1,
                             int64_t s2, int64_t V, int64_t words, uint32_t *bits,
                             int32_t *list, unsigned long long *count) {
@@ -30,14 +49,15 @@ __global__ void k_ci_bitmap(const uint8_t *__restrict__ defect, int64_t s0, int6
         if (d) {
             const int64_t i = v / (s1 * s2), j = (v / s2) % s1, k = v % s2;
             const int64_t L = i + j * s0 + k * s0 * s1;
-            atomicOr(&bits[b * words + (L >> 5)], 1u << (L & 31));
+            if (CI_OK((L >> 5) < words, 1, L, words))
+                atomicOr(&bits[b * words + (L >> 5)], 1u << (L & 31));
             my = atomicAdd(&s_cnt, 1ull);
         }
     }
     __syncthreads();
     if (threadIdx.x == 0) s_base = s_cnt ? atomicAdd(&count[b], s_cnt) : 0ull;
     __syncthreads();
-    if (d) list[b * V + (int64_t)(s_base + my)] = (int32_t)v;
+    if (d && CI_OK((int64_t)(s_base + my) < V, 2, s_base + my, V)) list[b * V + (int64_t)(s_base + my)] = (int32_t)v;
 }
 
 // One WAVE per defect voxel: the wave probes CIW_U x 64 consecutive table rows per step (lane l
@@ -68,6 +88,7 @@ __global__ void __launch_bounds__(CIW_TPB) k_ci_walk(const uint32_t *__restrict_
     const int64_t b = blockIdx.y;
     const int64_t n = (int64_t)count[b];
     constexpr int W = CIW_TPB / 64;
+    if (!CI_OK(n <= V, 3, n, V)) return;
     if ((int64_t)blockIdx.x * W >= n) return;   // block-uniform exit, before any staging
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     // LDS: offsets [CIW_ROWS], boundaries [CIW_NBS], then the bitmap (stage_bits)
@@ -82,11 +103,18 @@ __global__ void __launch_bounds__(CIW_TPB) k_ci_walk(const uint32_t *__restrict_
         bm = s_bits;
     }
     __syncthreads();
-    auto off_at = [&](int64_t r) { return r < lrows ? s_off[r] : offL[r]; };
-    auto bnd_at = [&](int64_t q) { return q < lnbs ? (int64_t)s_bnd[q] : (int64_t)bounds[q]; };
+    auto off_at = [&](int64_t r) {
+        if (!CI_OK(r >= 0 && r < rows, 4, r, rows)) return (int32_t)CI_SENTINEL;
+        return r < lrows ? s_off[r] : offL[r];
+    };
+    auto bnd_at = [&](int64_t q) {
+        if (!CI_OK(q >= 0 && q < nbs, 5, q, nbs)) return (int64_t)INT64_MAX;
+        return q < lnbs ? (int64_t)s_bnd[q] : (int64_t)bounds[q];
+    };
     const int64_t N = s0 * s1 * s2;
     for (int64_t idx = (int64_t)blockIdx.x * W + w; idx < n; idx += (int64_t)gridDim.x * W) {
         const int32_t v = list[b * V + idx];
+        if (!CI_OK(v >= 0 && v < V, 6, v, V)) continue;
         const int64_t i = v / (s1 * s2), j = (v / s2) % s1, k = v % s2;
         const int64_t base = i + j * s0 + k * s0 * s1;   // px2vec (Fortran order, CI.py:65-68)
         int64_t hits = 0, q = 0, row = 0;
@@ -102,7 +130,8 @@ __global__ void __launch_bounds__(CIW_TPB) k_ci_walk(const uint32_t *__restrict_
 #pragma unroll
             for (int u = 0; u < CIW_U; ++u) {
                 const int64_t L = base + off[u];
-                const bool hit = off[u] != CI_SENTINEL && L >= 0 && L < N && ((bm[L >> 5] >> (L & 31)) & 1u);
+                const bool hit = off[u] != CI_SENTINEL && L >= 0 && L < N && CI_OK((L >> 5) < words, 7, L, words) &&
+                                 ((bm[L >> 5] >> (L & 31)) & 1u);
                 bal[u] = __ballot(hit);
             }
             const int64_t rend = row + 64 * CIW_U;
@@ -113,7 +142,8 @@ __global__ void __launch_bounds__(CIW_TPB) k_ci_walk(const uint32_t *__restrict_
                 const bool inc = bq <= rend;
                 bool stop = false;
                 if (inc) {
-                    const int pos = (int)(bq - 1 - row);   // 0 .. 64 CIW_U - 1
+                    int pos = (int)(bq - 1 - row);   // 0 .. 64 CIW_U - 1
+                    if (!CI_OK(pos >= 0 && pos < 64 * CIW_U, 8, pos, 64 * CIW_U)) pos = 0;
                     const int u = pos >> 6, pb = pos & 63;
                     int64_t c = hits;
 #pragma unroll
@@ -138,7 +168,7 @@ __global__ void __launch_bounds__(CIW_TPB) k_ci_walk(const uint32_t *__restrict_
         }
         if (lane == 0) {
             shell_of[b * V + v] = qstop;
-            if (qstop >= 0) atomicAdd(&hist[b * nbs + qstop], 1u);
+            if (qstop >= 0 && CI_OK(qstop < nbs, 9, qstop, nbs)) atomicAdd(&hist[b * nbs + qstop], 1u);
             else atomicExch(&status[b], 1);
         }
     }
@@ -214,6 +244,7 @@ __global__ void __launch_bounds__(CIF_TPB) k_ci_finish(const uint32_t *hist, con
         for (int64_t q = q0; q < q1; ++q) {
             cum += h[q];
             if (cum > i95) {
+                if (!CI_OK(q < nbs, 10, q, nbs)) break;
                 sc[b].ci_scalar = radii[q] * minvox;
                 if (hsc) hsc[b].ci_scalar = radii[q] * minvox;
                 break;
@@ -223,14 +254,14 @@ __global__ void __launch_bounds__(CIF_TPB) k_ci_finish(const uint32_t *hist, con
 }
 
 __global__ void k_ci_scatter(const int32_t *shell_of, const uint8_t *defect, const double *radii,
-                             double minvox, int64_t V, double *ci) {
+                             int64_t nbs, double minvox, int64_t V, double *ci) {
     const int64_t b = blockIdx.y;
     const int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (v >= V) return;
     double r = 0.0;
     if (defect[b * V + v]) {
         const int32_t q = shell_of[b * V + v];
-        r = q >= 0 ? radii[q] * minvox : 0.0;
+        r = q >= 0 && CI_OK(q < nbs, 11, q, nbs) ? radii[q] * minvox : 0.0;
     }
     ci[b * V + v] = r;
 }
@@ -335,7 +366,22 @@ void vh_ci_run(vh_batch *b, const vh_ci_table *t, double minvox, double *d_ci, V
         b->d_ci_hist, d_count, t->d_radii, nbs, minvox, b->nb, d_status, b->d_sc, h_sc);
     VH_CHECK_LAUNCH();
     if (d_ci) {
-        k_ci_scatter<<<vg, VH_TPB, 0, st>>>(b->d_ci_shell, b->d_defect, t->d_radii, minvox, b->V, d_ci);
+        k_ci_scatter<<<vg, VH_TPB, 0, st>>>(b->d_ci_shell, b->d_defect, t->d_radii, nbs, minvox, b->V, d_ci);
         VH_CHECK_LAUNCH();
     }
+}
+
+// VH_DEBUG_BOUNDS: the first recorded violation of the CI kernels since the last check, raised
+// (after the caller's stream sync); a no-op in release builds
+void vh_ci_debug_check() {
+#ifdef VH_DEBUG_BOUNDS
+    unsigned long long h[4] = {0, 0, 0, 0};
+    HIP_TRY(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_ci_dbg), sizeof h, 0, hipMemcpyDeviceToHost));
+    if (h[0]) {
+        const unsigned long long z[4] = {0, 0, 0, 0};
+        HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_ci_dbg), z, sizeof z, 0, hipMemcpyHostToDevice));
+        throw VhError{VH_ERR_HIP, "CI bounds check: site " + std::to_string(h[0]) + " index " +
+                                      std::to_string((long long)h[1]) + " extent " + std::to_string((long long)h[2])};
+    }
+#endif
 }

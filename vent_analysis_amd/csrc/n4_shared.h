@@ -1995,7 +1995,9 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
         }
     }
     // stage 0 reached its fixed point (xs): the block starts are the exact float trajectory's
-    if (drift && xs) drift[j] = (float)((double)S.b[j].gmu - gd);
+    // (a study's first call, which reads no drift, always writes one: 0 when stage 0 stopped short,
+    // so a later call never starts from another batch's or an unset value -- ADVICE r4)
+    if (drift && (xs || !drift_in)) drift[j] = xs ? (float)((double)S.b[j].gmu - gd) : 0.0f;
     if (tid == 0) {
         ch.mu = S.mu;
         ch.conv = itk_conv(S.mu, S.sig, n);

@@ -1233,7 +1233,10 @@ void vh_launch_n4_study(vh_batch *b, const vh_n4_params &prm) {
     a.tcap = b->t_cap;
     a.pcdrift = nullptr;
     if (PC_DRIFT) {
-        if (!b->d_pcdrift) HIP_TRY(hipMalloc(&b->d_pcdrift, sizeof(float) * ST_TPB * b->nb));
+        if (!b->d_pcdrift) {
+            HIP_TRY(hipMalloc(&b->d_pcdrift, sizeof(float) * ST_TPB * b->nb));
+            HIP_TRY(hipMemsetAsync(b->d_pcdrift, 0, sizeof(float) * ST_TPB * b->nb, b->stream));
+        }
         a.pcdrift = b->d_pcdrift;
     }
     vh_set_max_lds((const void *)k_n4_study, ST_MAX_LDS);

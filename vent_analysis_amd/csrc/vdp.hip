@@ -1370,6 +1370,59 @@ __global__ void __launch_bounds__(KM_TPB) k_km_tiles(const uint32_t *__restrict_
     if ((threadIdx.x & 63) == 0) tile_scratch[b * (max_ktiles + 1) + tt] = ts;
 }
 
+// The centre update of one Lloyd step (one thread; oracle/vdp_oracle.py kmeans_1d_sorted): every
+// non-empty cluster's mean; a cluster left empty takes the value farthest from its own cluster's
+// (old) centre among clusters of >= 2 values -- a sorted cluster's farthest values are its two
+// ends, ties to the lowest index, never a value at distance 0 -- which leaves its donor's sum
+// (scikit-learn's empty-cluster relocation with a fixed tie order); then the centres are sorted.
+// Only degenerate data (equal initial centres: two or three distinct values) has empty clusters.
+__device__ void km_update(const uint32_t *k, const int64_t *cut, const double *sum, double *c) {
+    double old[KM_K], nc[KM_K], sums[KM_K];
+    int64_t cnt[KM_K], wa[KM_K], we[KM_K];
+    for (int j = 0; j < KM_K; ++j) {
+        old[j] = nc[j] = c[j];
+        wa[j] = cut[j];
+        we[j] = cut[j + 1];
+        cnt[j] = we[j] - wa[j];
+        sums[j] = cnt[j] > 0 ? sum[j] : 0.0;
+    }
+    for (int j = 0; j < KM_K; ++j) {
+        if (cut[j + 1] > cut[j]) continue;
+        double best = 0.0, bx = 0.0;
+        int64_t bi = -1;
+        int bq = -1;
+        for (int q = 0; q < KM_K; ++q) {
+            if (we[q] - wa[q] < 2) continue;
+            for (int e = 0; e < 2; ++e) {
+                const int64_t i = e ? we[q] - 1 : wa[q];
+                const double x = (double)key2f(k[i]);
+                const double dd = fabs(x - old[q]);
+                if (dd > best || (dd == best && dd > 0.0 && i < bi)) {
+                    best = dd;
+                    bi = i;
+                    bq = q;
+                    bx = x;
+                }
+            }
+        }
+        if (bi >= 0) {
+            nc[j] = bx;
+            sums[bq] -= bx;
+            cnt[bq] -= 1;
+            if (bi == wa[bq]) ++wa[bq]; else --we[bq];
+        }
+    }
+    for (int j = 0; j < KM_K; ++j)
+        if (cut[j + 1] > cut[j]) nc[j] = sums[j] / (double)cnt[j];
+    for (int j = 1; j < KM_K; ++j) {   // insertion sort
+        const double v = nc[j];
+        int i = j - 1;
+        while (i >= 0 && nc[i] > v) { nc[i + 1] = nc[i]; --i; }
+        nc[i + 1] = v;
+    }
+    for (int j = 0; j < KM_K; ++j) c[j] = nc[j];
+}
+
 // One block (16 waves) per volume.  Cluster sums: head partial tile + whole tiles (a difference of
 // the exclusive prefix of the tile sums, in LDS or -- large volumes, tile sums from k_km_tiles -- in
 // global memory) + tail partial tile (deterministic: fixed orders throughout).
@@ -1379,7 +1432,7 @@ __global__ void __launch_bounds__(KM_TPB) k_kmeans(const uint32_t *__restrict__ 
     __shared__ double s_tiles[KM_LDS_TILES + 1];   // tile sums -> exclusive prefix of them
     __shared__ double s_wtot[KM_TPB / 64];
     __shared__ float s_samp[KM_SAMPLES];
-    __shared__ double s_c[KM_K];
+    __shared__ double s_c[KM_K], s_sum[KM_K];
     __shared__ int64_t s_cut[KM_K + 1], s_new[KM_K + 1];
     __shared__ int s_done;
     const int64_t b = blockIdx.x;
@@ -1442,7 +1495,13 @@ __global__ void __launch_bounds__(KM_TPB) k_kmeans(const uint32_t *__restrict__ 
     int it = 0;
     for (it = 1; it <= 300; ++it) {
         if (w < KM_K - 1) {
-            const int64_t c = km_boundary(k, n, s_c[w], s_c[w + 1], s_samp, ns, stride);
+            // the boundary against the next LARGER centre value (centres are kept sorted; a centre
+            // equal to its predecessor gets no values: ties go to the lowest index).  Wave-uniform.
+            double chi = 0.0;
+            bool up = false;
+            for (int m = w + 1; m < KM_K; ++m)
+                if (!up && s_c[m] > s_c[w]) { chi = s_c[m]; up = true; }
+            const int64_t c = up ? km_boundary(k, n, s_c[w], chi, s_samp, ns, stride) : n;
             if (lane == 0) s_new[w + 1] = c;
         }
         __syncthreads();
@@ -1468,14 +1527,19 @@ __global__ void __launch_bounds__(KM_TPB) k_kmeans(const uint32_t *__restrict__ 
                     double sum = head;
                     if (te > ta + 1) sum += in_lds ? s_tiles[te] - s_tiles[ta + 1] : gt[te] - gt[ta + 1];
                     if (te != ta) sum += tail;
-                    s_c[w] = sum / (double)(e - a);
+                    s_sum[w] = sum;
                 }
             }
         }
         __syncthreads();
+        if (t == 0) km_update(k, s_cut, s_sum, s_c);   // means, empty-cluster relocation, sort
+        __syncthreads();
     }
-    if (t == 0) {
-        sc[b].n_km0 = s_cut[1] - s_cut[0];
+    if (t == 0) {   // VDP_km: the lowest non-empty cluster
+        int64_t low = 0;
+        for (int j = KM_K - 1; j >= 0; --j)
+            if (s_cut[j + 1] > s_cut[j]) low = s_cut[j + 1] - s_cut[j];
+        sc[b].n_km0 = low;
         sc[b].km_iters = it;
         for (int j = 0; j < KM_K; ++j) sc[b].km_c[j] = s_c[j];
     }

@@ -300,6 +300,7 @@ vh_ci_table *vh_ci_table_build(vh_ctx *ctx, int64_t R, int64_t C, const int16_t 
                                int64_t rows, const int32_t *bounds, const double *radii, int64_t nbs);
 void vh_ci_table_free(vh_ci_table *t);
 void vh_ci_run(vh_batch *b, const vh_ci_table *t, double minvox, double *d_ci, VolScalars *h_sc = nullptr);
+void vh_ci_debug_check();   // VH_DEBUG_BOUNDS builds: raise the CI kernels' first bounds violation
 void vh_ensure_n4_workspace(vh_batch *b, const vh_n4_params &prm);
 
 // ---- shared host helpers ----------------------------------------------------------------------

@@ -77,7 +77,8 @@ def radii_indices(table: np.ndarray) -> np.ndarray:
 class SphereTable:
     """Device-ready view of a sphere table for one array shape."""
 
-    def __init__(self, offsets, bounds, radii, dup):
+    def __init__(self, offsets, bounds, radii, dup, key=None):
+        self.key = key           # content key (vox, Rmax, R, C) when built by compact_table_for
         self.offsets = offsets   # int16 [rows, 3]  (dx, dy, dz)
         self.bounds = bounds     # int32 [nb]      prefix lengths tested in order (CI.py:94)
         self.radii = radii       # float64 [nb]    r[b-1] for each bound (CI.py:105)
@@ -90,7 +91,9 @@ class SphereTable:
 
 @functools.lru_cache(maxsize=16)
 def _compact_cached(vox_key: tuple, radius: int, shape: tuple) -> SphereTable:
-    return compact_table(_sphere_pix_cached(vox_key, radius), shape)
+    t = compact_table(_sphere_pix_cached(vox_key, radius), shape)
+    t.key = (vox_key, radius, shape[0], shape[1])   # the table depends on (vox, Rmax, R, C) only
+    return t
 
 
 def compact_table_for(vox, radius, shape) -> SphereTable:
