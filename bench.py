@@ -159,20 +159,41 @@ def algorithmic_bytes(name, hp, mk, res, R, C, Z, study=True, conv_mode=0):
     return 0.0
 
 
+def lib_digest(path=None):
+    """sha256 of the libventhip.so this process runs (vent_analysis_amd/_lib.LIB_PATH)."""
+    import hashlib
+    if path is None:
+        from vent_analysis_amd import _lib
+        path = _lib.LIB_PATH
+    try:
+        return hashlib.sha256(open(path, "rb").read()).hexdigest()
+    except OSError:
+        return None
+
+
 def pmc_traffic(kernel):
     """Per-launch HBM-side bytes of ``kernel`` from the newest committed PMC summary
-    (profiles/r*_pmc_traffic.json, written by scripts/pmc_summary.py), or None."""
+    (profiles/r*_pmc_traffic.json, written by scripts/pmc_summary.py from separate rocprofv3
+    --pmc passes).  The bench cannot collect PMC counters itself (rocprofv3 wraps the process), so
+    the value is only used when the summary was made with the very library this process runs (its
+    sha256 recorded by pmc_summary.py); otherwise (None, source, "stale ...")."""
     import glob
     def run_order(f):   # r<round><tag>: tags run a..z, then aa..az, ... (r4z before r4av)
         m = re.match(r"r(\d+)([a-z]*)", os.path.basename(f))
         return (int(m.group(1)), len(m.group(2)), m.group(2)) if m else (-1, 0, "")
     files = sorted(glob.glob(os.path.join(HERE, "profiles", "r*_pmc_traffic.json")), key=run_order)
     if not files:
-        return None, None
-    k = json.load(open(files[-1]))["kernels"].get(kernel)
+        return None, None, "no committed PMC summary"
+    src = os.path.relpath(files[-1], HERE)
+    d = json.load(open(files[-1]))
+    k = d["kernels"].get(kernel)
     if not k:
-        return None, None
-    return k["traffic_bytes_per_launch"], os.path.relpath(files[-1], HERE)
+        return None, src, f"{kernel} not in the summary"
+    mine = lib_digest()
+    if d.get("lib_sha256") != mine:
+        return None, src, (f"stale: the summary's library sha256 {str(d.get('lib_sha256'))[:12]} "
+                           f"is not this run's {str(mine)[:12]}")
+    return k["traffic_bytes_per_launch"], src, "same library (sha256 match)"
 
 
 # ------------------------------------------------------------------------------------------------
@@ -507,6 +528,9 @@ def main():
     ap.add_argument("--h2h-keep-batch", action="store_true",
                     help="A/B: keep the device-resident batch (and its stream) open during the "
                          "host-to-host measurement (round-3 behaviour)")
+    ap.add_argument("--iso-runs", type=int, default=5,
+                    help="runs of batch 0 alone after the timed region (batch latency and the "
+                         "isolated kernel durations the roofline uses)")
     ap.add_argument("--workload", default="vdp", choices=["vdp", "ci"],
                     help="vdp: the BASELINE metric (default); ci: the cluster-index line")
     ap.add_argument("--dry-run", action="store_true",
@@ -665,54 +689,63 @@ def main():
                                                study=used_study, conv_mode=args.conv_mode) * runs
             if tot_n:
                 kernels[name] = {"ms_total": tot_ms, "launches": tot_n, "alg_bytes": tot_b}
-    roof = None
-    if kernels:
-        dom = max(kernels, key=lambda k: kernels[k]["ms_total"])
-        k = kernels[dom]
-        avg_ms = k["ms_total"] / k["launches"]
-        bpl = k["alg_bytes"] / k["launches"]
-        ach = bpl / (avg_ms * 1e-3) / 1e9 if avg_ms > 0 else 0.0
-        traffic, tsrc = pmc_traffic(dom)
-        roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
-                "traffic": round(traffic) if traffic else None, "traffic_source": tsrc,
-                "avg_launch_us": round(avg_ms * 1e3, 2), "alg_bytes_per_launch": bpl,
-                "kernel_ms_per_step": {n: round(v["ms_total"] / args.steps, 3)
-                                       for n, v in sorted(kernels.items(),
-                                                          key=lambda kv: -kv[1]["ms_total"])},
-                "kernel_us_per_launch": {n: round(v["ms_total"] / v["launches"] * 1e3, 2)
-                                         for n, v in kernels.items()}}
     batch_latency_ms = None
     iso_kernels = {}
-    if ninf > 1:   # one batch alone (untimed above): the latency a single batch sees, and its
-        # kernels' launch durations without another batch's workgroups on the CUs
+    if ninf > 1 or not args.no_profile:
+        # batch 0 alone, args.iso_runs times (untimed above): the latency one batch sees, and every
+        # kernel class's launch duration with no other batch's workgroups on the CUs -- what a
+        # kernel-trace of one batch at a time reports (rocprofv3 --kernel-trace --stats of
+        # bench.py --inflight 1), so the roofline fraction is reproducible from profiles/
         Bt.reset_timers()
-        t1 = time.perf_counter()
-        step(opts, 0)
-        sync_all()
-        batch_latency_ms = round((time.perf_counter() - t1) * 1e3, 3)
+        lat = []
+        for _ in range(max(1, args.iso_runs)):
+            t1 = time.perf_counter()
+            step(opts, 0)
+            sync_all()
+            lat.append(time.perf_counter() - t1)
+        batch_latency_ms = round(sorted(lat)[len(lat) // 2] * 1e3, 3)
         if not args.no_profile:
             for name in _lib.lib().vh_batch_kernel_names().decode().split(";"):
                 ms, n, _ = Bt.kernel_time(name)
                 if n:
                     iso_kernels[name] = ms / n
-
-    if roof and iso_kernels.get(roof["kernel"]):
-        # the same launch class alone on the GPU: its duration without the other batch's workgroups
-        iso_us = iso_kernels[roof["kernel"]] * 1e3
-        b0 = algorithmic_bytes(roof["kernel"], hp, mk, res, R, C, Z, study=used_study,
-                               conv_mode=args.conv_mode)   # batch 0's bytes per launch
-        ach_iso = b0 / (iso_us * 1e-6) / 1e9
-        roof["isolated"] = {"avg_launch_us": round(iso_us, 2), "achieved": round(ach_iso, 1),
-                            "frac": round(ach_iso / HBM_PEAK_GBS, 4),
-                            "note": "one batch alone (batch_latency run): no other batch's "
-                                    "workgroups on the CUs",
-                            # every class's launch time alone (the overlapped kernel_ms_per_step
-                            # above includes waiting for CUs the other batch's studies hold)
-                            "kernel_us_per_launch": {n: round(v * 1e3, 2) for n, v in
-                                                     sorted(iso_kernels.items(), key=lambda kv: -kv[1])},
-                            "non_n4_us_per_step": round(sum(v for n, v in iso_kernels.items()
-                                                            if not n.startswith("n4_")) * 1e3, 2)}
+    roof = None
+    if kernels and iso_kernels:
+        dom = max(iso_kernels, key=lambda k: iso_kernels[k])   # the longest launch class alone
+        iso_us = iso_kernels[dom] * 1e3
+        bpl = algorithmic_bytes(dom, hp, mk, res, R, C, Z, study=used_study,
+                                conv_mode=args.conv_mode)   # batch 0's bytes per launch
+        ach = bpl / (iso_us * 1e-6) / 1e9
+        traffic, tsrc, tnote = pmc_traffic(dom)
+        k = kernels.get(dom, {"ms_total": 0.0, "launches": 0, "alg_bytes": 0.0})
+        roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                "traffic": round(traffic) if traffic else None,
+                "traffic_source": f"from committed profile {tsrc}" if tsrc else None,
+                "traffic_note": tnote,
+                "traffic_over_alg": round(traffic / bpl, 3) if traffic else None,
+                "avg_launch_us": round(iso_us, 2), "alg_bytes_per_launch": bpl,
+                "timing": f"HIP events around each launch of batch 0 alone, mean of "
+                          f"{max(1, args.iso_runs)} runs (no other batch on the CUs)",
+                "limiter": ("latency, below the HBM roof: the serial S7 recurrence evaluated by "
+                            "guess-and-verify rounds and the latency-bound fit / eval walks of "
+                            "one workgroup per study (DESIGN.md section 5)"
+                            if dom == "n4_study" else None),
+                "kernel_us_per_launch": {n: round(v * 1e3, 2) for n, v in
+                                         sorted(iso_kernels.items(), key=lambda kv: -kv[1])},
+                "non_n4_us_per_step": round(sum(v for n, v in iso_kernels.items()
+                                                if not n.startswith("n4_")) * 1e3, 2)}
+        if ninf > 1 and k["launches"]:
+            # the timed region's own launches: batches in flight overlap, so a launch's duration
+            # includes waiting for CUs another batch's studies hold -- not a kernel cost
+            avg_ms = k["ms_total"] / k["launches"]
+            roof["overlapped"] = {
+                "note": "batches in flight: includes CU wait",
+                "avg_launch_us": round(avg_ms * 1e3, 2),
+                "frac": round(k["alg_bytes"] / k["launches"] / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                "kernel_ms_per_step": {n: round(v["ms_total"] / args.steps, 3)
+                                       for n, v in sorted(kernels.items(),
+                                                          key=lambda kv: -kv[1]["ms_total"])}}
     its = np.array([list(r.n4_iters[:4]) for r in res])
     if not args.h2h_keep_batch:
         # the device-resident batches (their streams, 1.5 GB of HBM each) are done: the pipe's slot

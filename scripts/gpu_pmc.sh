@@ -14,7 +14,7 @@ i=0
 for PASS in "${LIST[@]}"; do
   i=$((i+1))
   timeout -k 10 300 rocprofv3 --pmc $PASS --kernel-include-regex "$REGEX" --output-format csv \
-      -d gpurun_out/${TAG}_p$i -o pmc -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-profile --no-h2h \
+      -d gpurun_out/${TAG}_p$i -o pmc -- python3 bench.py --steps 2 --warmup 1 --inflight 1 --iso-runs 1 --no-cpu-baseline --no-profile --no-h2h \
       > gpurun_out/${TAG}_p$i.log 2>&1
   rc=$?; echo "pass $i ($PASS) rc=$rc"; [ $rc -eq 0 ] || exit $rc
   dirs+=(gpurun_out/${TAG}_p$i)

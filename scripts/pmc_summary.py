@@ -44,8 +44,14 @@ def main():
         fetch, write = v["FETCH_SIZE"] / nf, v["WRITE_SIZE"] / nw
         res[c] = {"traffic_bytes_per_launch": 2.0 * fetch + write,
                   "fetch_size_bytes": fetch, "write_size_bytes": write, "launches": nf}
+    import hashlib
+    import os
+    here = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.environ.get("VH_LIB_PATH") or os.path.join(here, "vent_analysis_amd", "libventhip.so")
+    # the library the passes ran: bench.py uses this summary's traffic only for the same build
+    sha = hashlib.sha256(open(lib, "rb").read()).hexdigest() if os.path.exists(lib) else None
     json.dump({"note": "traffic = 2*FETCH_SIZE + WRITE_SIZE per launch (gfx950 FETCH_SIZE halving)",
-               "kernels": res}, open(out, "w"), indent=1)
+               "lib_sha256": sha, "kernels": res}, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
 
