@@ -1,9 +1,16 @@
 #!/bin/bash
-# GPU-box: A/B benchmark of library variants under scratch_libs/ (VH_LIB_PATH), one bench each.
+# GPU-box: alternated A/B of library variants (VH_LIB_PATH; "base" = the in-tree libventhip.so),
+# REPS rounds over VARIANTS, one short bench each: the isolated k_n4_study launch (mean of 5 runs of
+# one batch alone) and the device-resident rate.  usage: VARIANTS="base apx3" REPS=2 scripts/gpu_ab.sh TAG
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-for v in ${VARIANTS:-$(cd scratch_libs && ls *.so | sed 's/\.so$//')}; do
-  VH_LIB_PATH=$PWD/scratch_libs/$v.so timeout -k 10 300 python bench.py --no-cpu-baseline ${BENCH_ARGS} > gpurun_out/ab_$v.json 2> gpurun_out/ab_$v.err
-  rc=$?; echo "variant $v rc=$rc"; [ $rc -eq 0 ] || exit $rc
-  python3 -c "import json;d=json.load(open('gpurun_out/ab_$v.json'));print('$v', d['value'], d['roofline']['kernel_ms_per_step'])"
+TAG=${1:-ab}
+for r in $(seq 1 ${REPS:-2}); do
+  for v in ${VARIANTS:-base}; do
+    lib=$PWD/vent_analysis_amd/libventhip.so; [ "$v" = base ] || lib=$PWD/scratch_libs/$v.so
+    VH_LIB_PATH=$lib timeout -k 10 200 python bench.py --steps 6 --warmup 1 --no-cpu-baseline --no-h2h ${BENCH_ARGS} \
+        > gpurun_out/${TAG}_${v}_$r.json 2> gpurun_out/${TAG}_${v}_$r.err
+    rc=$?; [ $rc -eq 0 ] || { echo "variant $v rc=$rc"; tail -3 gpurun_out/${TAG}_${v}_$r.err; exit $rc; }
+    python3 -c "import json;d=json.loads(open('gpurun_out/${TAG}_${v}_$r.json').read().splitlines()[-1]);r=d['roofline'];print('$v', $r, d['value'], r['avg_launch_us'], r['kernel'], d['n4_study_times'])"
+  done
 done
