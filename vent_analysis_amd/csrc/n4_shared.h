@@ -1138,11 +1138,8 @@ __device__ __forceinline__ void pc_kf2(pc_f2 k, pc_f2 p, PcKf &qa, PcKf &qb) {
 }
 // one phase-A step; returns false when the mu step is not certified (the state is then approximate)
 // e0 >= r0 2^-40 + 2^-44 >= 2^-22 |mu rl| + 2^-46 |mu| for mu < 4 (one bound per block: r0 <= 1/k0)
-#ifndef PC_VBAD
-#define PC_VBAD 0
-#endif
 template <bool SIG = true>
-__device__ __forceinline__ uint32_t pc_apx_step(const PcKf &q, float e0, float p, bool first, float &mu, float &sig) {
+__device__ __forceinline__ bool pc_apx_step(const PcKf &q, float e0, float p, bool first, float &mu, float &sig) {
     if (!SIG && !first) {   // mu alone: sig carries sum (p - mu)^2 along the block (PCX's binade estimate)
         const float dq = p - mu;
         sig = fmaf(dq, dq, sig);
@@ -1160,14 +1157,9 @@ __device__ __forceinline__ uint32_t pc_apx_step(const PcKf &q, float e0, float p
     const float t = fmaf(-mu, q.rl, t1);
     const float E = fmaf(fabsf(t), 0x1p-21f, e0);
     const pc_f2 y2 = (pc_f2)mu + ((pc_f2)t + (pc_f2){-E, E});   // both ends in two packed adds
-    mu = y2.x;   // = RN(mu + t) whenever the ends agree
-#if PC_VBAD
-    // the ends' bit difference, OR-ed by the caller over the group in a VGPR: no per-step compare
-    // into VCC and SALU mask merge on the step chain (the ends are never NaN for finite p)
-    return __float_as_uint(y2.x) ^ __float_as_uint(y2.y);
-#else
-    return y2.x == y2.y ? 0u : 1u;
-#endif
+    const bool ok = y2.x == y2.y;
+    mu = y2.x;   // = RN(mu + t) whenever ok
+    return ok;
 }
 // a lane's block in phase A: groups of 8 steps without guards; a group with an uncertified step is
 // redone with the exact steps (rare: the wave branches only when one of its lanes needs it)
@@ -1190,11 +1182,11 @@ __device__ __forceinline__ void pc_apx_group(const float (&c)[8], float kf, floa
         pc_kf2(kk, (pc_f2){c[i], c[i + 1]}, q[i], q[i + 1]);
     }
     const float mu0 = mu, sig0 = sig;
-    uint32_t bad = !PART || cnt > 0 ? pc_apx_step<SIG>(q[0], e0, c[0], kf == 1.0f, mu, sig) : 0u;
+    bool ok = !PART || cnt > 0 ? pc_apx_step<SIG>(q[0], e0, c[0], kf == 1.0f, mu, sig) : true;
 #pragma unroll
     for (int i = 1; i < 8; ++i)
-        if (!PART || i < cnt) bad |= pc_apx_step<SIG>(q[i], e0, c[i], false, mu, sig);
-    if (bad) {   // redo the group exactly
+        if (!PART || i < cnt) ok &= pc_apx_step<SIG>(q[i], e0, c[i], false, mu, sig);
+    if (!ok) {   // redo the group exactly
         mu = mu0;
         sig = sig0;
         double kd = (double)kf;
@@ -1209,9 +1201,6 @@ __device__ __forceinline__ void pc_apx_group(const float (&c)[8], float kf, floa
 // P is read through a buffer resource of np floats (np = (L + 1) nl, the block layout's extent): the
 // step rows are loaded unguarded with the row offset in an SGPR (soffset), and rows past a block's
 // end (or past np) cost nothing but a load whose value is never used (0 beyond np)
-#ifndef PC_APX3
-#define PC_APX3 0   // phase-A blocks with loads two groups ahead (pc_block_apx_t)
-#endif
 template <bool SIG, bool CLAMP>
 __device__ __forceinline__ void pc_block_apx_t(const __amdgpu_buffer_rsrc_t rs, int voff, int rstride,
                                                uint32_t len, uint32_t k0, float &mu, float &sig) {
@@ -1231,46 +1220,6 @@ __device__ __forceinline__ void pc_block_apx_t(const __amdgpu_buffer_rsrc_t rs, 
     float kf = CLAMP ? fminf((float)k0, (float)ITK_NMAX) : (float)k0;
     const float e0 = fmaf(__builtin_amdgcn_rcpf(kf), 0x1p-39f, 0x1p-44f);   // covers every step's r0
     uint32_t s0 = 0;
-#if PC_APX3
-    // three groups in rotation: each group's loads are issued two groups ahead of their use (the
-    // rounds re-read p from L2 / the Infinity Cache, whose latency one group's work did not cover)
-    float c[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) b[i] = ld(8u + (uint32_t)i);
-    for (; s0 + 24 <= len; s0 += 24) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) c[i] = ld(s0 + 16 + (uint32_t)i);
-        pc_apx_group<SIG, CLAMP>(a, kf, e0, mu, sig);
-        kf = adv(kf);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) a[i] = ld(s0 + 24 + (uint32_t)i);
-        pc_apx_group<SIG, CLAMP>(b, kf, e0, mu, sig);
-        kf = adv(kf);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) b[i] = ld(s0 + 32 + (uint32_t)i);
-        pc_apx_group<SIG, CLAMP>(c, kf, e0, mu, sig);
-        kf = adv(kf);
-    }
-    // a = rows s0 .., b = rows s0 + 8 .. are loaded; fewer than 24 steps remain
-    if (s0 + 8 <= len) {
-        pc_apx_group<SIG, CLAMP>(a, kf, e0, mu, sig);
-        kf = adv(kf);
-        s0 += 8;
-#pragma unroll
-        for (int i = 0; i < 8; ++i) a[i] = b[i];
-        if (s0 + 8 <= len) {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) b[i] = ldv(s0 + 8 + (uint32_t)i);
-            pc_apx_group<SIG, CLAMP>(a, kf, e0, mu, sig);
-            kf = adv(kf);
-            s0 += 8;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) a[i] = b[i];
-        }
-    }
-    if (s0 < len) pc_apx_group<SIG, CLAMP, true>(a, kf, e0, mu, sig, (int)(len - s0));   // the tail
-    return;
-#endif
     for (; s0 + 16 <= len; s0 += 16) {
 #pragma unroll
         for (int i = 0; i < 8; ++i) b[i] = ld(s0 + 8 + (uint32_t)i);
