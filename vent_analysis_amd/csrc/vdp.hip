@@ -1259,6 +1259,16 @@ void vh_launch_border(vh_batch *b, const uint8_t *d_in, uint8_t *d_out) {
 #define KM_SAMPLES 4096   // LDS sample of the sorted values for the boundary searches
 #define KM_TPB 1024
 
+// key i of [lo, hi) as a float, 0 outside: the load is unconditional (index clamped into the range,
+// hi > lo), so a group of such loads stays in flight together -- a guarded load compiles to an
+// exec-masked branch whose s_waitcnt vmcnt(0) serialises the group
+template <typename I>
+__device__ __forceinline__ float km_key_in(const uint32_t *k, I i, I lo, I hi) {
+    const I c = i < lo ? lo : (i >= hi ? hi - 1 : i);
+    const float v = key2f(k[c]);
+    return (i >= lo && i < hi) ? v : 0.0f;
+}
+
 // wave-cooperative sum of sorted values k[i], i in tile t intersected with [a, e): lane l adds
 // elements t*1024 + j*64 + l for j = 0..15 in order, then a fixed shuffle tree (deterministic)
 __device__ __forceinline__ double km_tile_sum(const uint32_t *k, int64_t t, int64_t a, int64_t e) {
@@ -1268,7 +1278,7 @@ __device__ __forceinline__ double km_tile_sum(const uint32_t *k, int64_t t, int6
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         const int64_t i = t * KM_TILE + j * 64 + lane;
-        v[j] = (i >= a && i < e) ? key2f(k[i]) : 0.0f;
+        v[j] = km_key_in(k, i, a, e);
     }
 #pragma unroll
     for (int j = 0; j < 16; ++j) acc += (double)v[j];
@@ -1285,8 +1295,8 @@ __device__ __forceinline__ void km_tile_sum2(const uint32_t *k, int64_t t0, int6
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
         const int64_t i0 = t0 * KM_TILE + j * 64 + lane, i1 = t1 * KM_TILE + j * 64 + lane;
-        v0[j] = (i0 >= a && i0 < e) ? key2f(k[i0]) : 0.0f;
-        v1[j] = (i1 >= a && i1 < e) ? key2f(k[i1]) : 0.0f;
+        v0[j] = km_key_in(k, i0, a, e);
+        v1[j] = km_key_in(k, i1, a, e);
     }
     double acc0 = 0.0, acc1 = 0.0;
 #pragma unroll
@@ -1307,30 +1317,34 @@ __device__ __forceinline__ bool km_closer(double x, double clo, double chi) {
     return fabs(x - chi) < fabs(x - clo);
 }
 
-__device__ __forceinline__ int64_t km_boundary(const uint32_t *k, int64_t n, double clo, double chi,
-                                               const float *samp, int64_t ns, int64_t stride) {
+// first sample index js in [0, ns] with the predicate true (ns if none): 64-ary over the LDS sample
+__device__ __forceinline__ int64_t km_sample_search(const float *samp, int64_t ns64, double clo, double chi) {
     const int lane = threadIdx.x & 63;
-    // sample: first sample index js with the predicate true (ns if none)
-    int64_t slo = 0, shi = ns;   // answer in [slo, shi]
+    const int ns = (int)ns64;   // <= KM_SAMPLES: 32-bit index arithmetic (a constant divisor is a mul-hi)
+    int slo = 0, shi = ns;      // answer in [slo, shi]
     while (shi - slo > 64) {
-        const int64_t span = shi - slo;
-        const int64_t p = slo + (span * (lane + 1)) / 65;
+        const int span = shi - slo;
+        const int p = slo + (span * (lane + 1)) / 65;
         const uint64_t m = __ballot(km_closer((double)samp[p], clo, chi));
         if (m == 0ull) {
             slo = slo + (span * 64) / 65 + 1;
         } else {
             const int f = __ffsll((long long)m) - 1;
-            const int64_t pf = slo + (span * (f + 1)) / 65;
-            const int64_t pprev = f == 0 ? slo - 1 : slo + (span * f) / 65;
+            const int pf = slo + (span * (f + 1)) / 65;
+            const int pprev = f == 0 ? slo - 1 : slo + (span * f) / 65;
             slo = pprev + 1;
             shi = pf;
         }
     }
-    {
-        const int64_t p = slo + lane;
-        const bool pr = p < shi ? km_closer((double)samp[p], clo, chi) : true;
-        slo = slo + (__ffsll((long long)__ballot(pr)) - 1);
-    }
+    const int p = slo + lane;
+    const bool pr = p < shi ? km_closer((double)samp[p], clo, chi) : true;
+    return slo + (__ffsll((long long)__ballot(pr)) - 1);
+}
+
+__device__ __forceinline__ int64_t km_boundary(const uint32_t *k, int64_t n, double clo, double chi,
+                                               const float *samp, int64_t ns, int64_t stride) {
+    const int lane = threadIdx.x & 63;
+    const int64_t slo = km_sample_search(samp, ns, clo, chi);
     // global: sample js - 1 is false (or none), sample js is true (or none)
     int64_t lo = slo == 0 ? 0 : (slo - 1) * stride + 1;
     int64_t hi = slo >= ns ? n : slo * stride;   // answer in [lo, hi]
@@ -1376,50 +1390,101 @@ __global__ void __launch_bounds__(KM_TPB) k_km_tiles(const uint32_t *__restrict_
 // ends, ties to the lowest index, never a value at distance 0 -- which leaves its donor's sum
 // (scikit-learn's empty-cluster relocation with a fixed tie order); then the centres are sorted.
 // Only degenerate data (equal initial centres: two or three distinct values) has empty clusters.
-__device__ void km_update(const uint32_t *k, const int64_t *cut, const double *sum, double *c) {
+__device__ __forceinline__ double readlane_d(double v, int l) {   // l wave-uniform
+    const unsigned long long x = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)x, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(x >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+__device__ __forceinline__ void km_cswap(double &a, double &b, bool do_swap) {
+    const double x = a;
+    a = do_swap ? b : a;
+    b = do_swap ? x : b;
+}
+// (fully unrolled, register-only: the out-of-line form with indexed local arrays was a call with
+// 54 scratch accesses on every Lloyd iteration)
+// WAVE: called by a whole wave with wave-uniform arguments (k_kmeans_s): lane j computes mean j, so
+// the four IEEE divisions cost one division's latency; else by one thread (k_kmeans).
+template <bool WAVE, typename I>
+__device__ __forceinline__ void km_update(const uint32_t *k, const I *cut, const double *sum, double *c) {
     double old[KM_K], nc[KM_K], sums[KM_K];
-    int64_t cnt[KM_K], wa[KM_K], we[KM_K];
+    I wa[KM_K], we[KM_K];
+    bool empty[KM_K];
+    bool any_empty = false;
+#pragma unroll
     for (int j = 0; j < KM_K; ++j) {
         old[j] = nc[j] = c[j];
         wa[j] = cut[j];
         we[j] = cut[j + 1];
-        cnt[j] = we[j] - wa[j];
-        sums[j] = cnt[j] > 0 ? sum[j] : 0.0;
+        empty[j] = we[j] <= wa[j];
+        sums[j] = empty[j] ? 0.0 : sum[j];
+        any_empty = any_empty || empty[j];
     }
-    for (int j = 0; j < KM_K; ++j) {
-        if (cut[j + 1] > cut[j]) continue;
-        double best = 0.0, bx = 0.0;
-        int64_t bi = -1;
-        int bq = -1;
-        for (int q = 0; q < KM_K; ++q) {
-            if (we[q] - wa[q] < 2) continue;
-            for (int e = 0; e < 2; ++e) {
-                const int64_t i = e ? we[q] - 1 : wa[q];
-                const double x = (double)key2f(k[i]);
-                const double dd = fabs(x - old[q]);
-                if (dd > best || (dd == best && dd > 0.0 && i < bi)) {
-                    best = dd;
-                    bi = i;
-                    bq = q;
-                    bx = x;
+    if (any_empty) {   // degenerate data only
+#pragma unroll
+        for (int j = 0; j < KM_K; ++j) {
+            if (!empty[j]) continue;
+            double best = 0.0, bx = 0.0;
+            I bi = -1;
+            int bq = -1;
+#pragma unroll
+            for (int q = 0; q < KM_K; ++q) {
+                if (we[q] - wa[q] < 2) continue;
+#pragma unroll
+                for (int e = 0; e < 2; ++e) {
+                    const I i = e ? we[q] - 1 : wa[q];
+                    const double x = (double)key2f(k[i]);
+                    const double dd = fabs(x - old[q]);
+                    if (dd > best || (dd == best && dd > 0.0 && i < bi)) {
+                        best = dd;
+                        bi = i;
+                        bq = q;
+                        bx = x;
+                    }
                 }
             }
-        }
-        if (bi >= 0) {
-            nc[j] = bx;
-            sums[bq] -= bx;
-            cnt[bq] -= 1;
-            if (bi == wa[bq]) ++wa[bq]; else --we[bq];
+            if (bi >= 0) {
+                nc[j] = bx;
+#pragma unroll
+                for (int q = 0; q < KM_K; ++q)
+                    if (q == bq) {
+                        sums[q] -= bx;
+                        if (bi == wa[q]) ++wa[q]; else --we[q];
+                    }
+            }
         }
     }
-    for (int j = 0; j < KM_K; ++j)
-        if (cut[j + 1] > cut[j]) nc[j] = sums[j] / (double)cnt[j];
-    for (int j = 1; j < KM_K; ++j) {   // insertion sort
-        const double v = nc[j];
-        int i = j - 1;
-        while (i >= 0 && nc[i] > v) { nc[i + 1] = nc[i]; --i; }
-        nc[i + 1] = v;
+    if (WAVE) {
+        const int l = threadIdx.x & 3;
+        double sl = sums[0], cl = (double)(we[0] - wa[0]);
+#pragma unroll
+        for (int j = 1; j < KM_K; ++j)
+            if (l == j) { sl = sums[j]; cl = (double)(we[j] - wa[j]); }
+        const double ml = sl / cl;
+#pragma unroll
+        for (int j = 0; j < KM_K; ++j)
+            if (!empty[j]) nc[j] = readlane_d(ml, j);
+    } else {
+#pragma unroll
+        for (int j = 0; j < KM_K; ++j)
+            if (!empty[j]) nc[j] = sums[j] / (double)(we[j] - wa[j]);
     }
+    // insertion sort by adjacent swaps while strictly greater (KM_K = 4, unrolled)
+    static_assert(KM_K == 4, "km_update's sort is written for four centres");
+    km_cswap(nc[0], nc[1], nc[0] > nc[1]);
+    if (nc[1] > nc[2]) {
+        km_cswap(nc[1], nc[2], true);
+        km_cswap(nc[0], nc[1], nc[0] > nc[1]);
+    }
+    if (nc[2] > nc[3]) {
+        km_cswap(nc[2], nc[3], true);
+        if (nc[1] > nc[2]) {
+            km_cswap(nc[1], nc[2], true);
+            km_cswap(nc[0], nc[1], nc[0] > nc[1]);
+        }
+    }
+#pragma unroll
     for (int j = 0; j < KM_K; ++j) c[j] = nc[j];
 }
 
@@ -1532,7 +1597,7 @@ __global__ void __launch_bounds__(KM_TPB) k_kmeans(const uint32_t *__restrict__ 
             }
         }
         __syncthreads();
-        if (t == 0) km_update(k, s_cut, s_sum, s_c);   // means, empty-cluster relocation, sort
+        if (t == 0) km_update<false>(k, s_cut, s_sum, s_c);   // means, empty-cluster relocation, sort
         __syncthreads();
     }
     if (t == 0) {   // VDP_km: the lowest non-empty cluster
@@ -1542,6 +1607,278 @@ __global__ void __launch_bounds__(KM_TPB) k_kmeans(const uint32_t *__restrict__ 
         sc[b].n_km0 = low;
         sc[b].km_iters = it;
         for (int j = 0; j < KM_K; ++j) sc[b].km_c[j] = s_c[j];
+    }
+}
+
+// k-means for volumes of up to KMS_TILES * 64 keys (the 128x128x24 bench studies; larger volumes
+// take k_kmeans): the same Lloyd iteration over 64-key tiles.  All 16 waves sum the tiles (16 tiles
+// per wave at a time, one exchange reduction for the 16) into an exclusive prefix in LDS and take the
+// LDS sample from the same loads (the sample stride is a whole number of tiles).  Then ONE wave runs
+// the iterations, with no barrier: per boundary it checks whether the cut still lies in the previous
+// iteration's sample interval (two LDS reads; the 64-ary sample search only when it moved), loads
+// the 192-key window of sorted keys around that interval (three aligned tiles, holding the interval
+// and the tile the cut falls in; the three boundaries' loads in flight together), finds the cut and
+// its partial tile sums (below / above the cut inside its tile) in the same registers, and forms the
+// four cluster sums from the prefix.  k_kmeans takes two dependent global rounds, four barriers and
+// a one-thread update per iteration.
+#define KMS_TILES 8192
+#define KMS_WAVES (KM_TPB / 64)
+
+// Fixed-order wave sums of N values per lane (N a power of two, 2 <= N <= 64), by halving exchanges:
+// step s pairs lane l with l ^ (32 >> s), and the lane with that bit clear keeps the lower half of
+// its values (adding its partner's), the other the upper half; then butterflies over the remaining
+// lane bits.  Lane l ends with the total of value (l >> (6 - log2 N)); every lane holding a total
+// holds the same bits (a + b = b + a).  log2 N + 6 - log2 N = 6 exchanges of N - 1 + 6 - log2 N
+// values instead of 6 N.
+template <int H, int OFF, int N>
+__device__ __forceinline__ void wave_sums_halve(double (&v)[N], int lane) {
+    if constexpr (H >= 1) {
+        const bool up = (lane & OFF) != 0;
+#pragma unroll
+        for (int i = 0; i < H; ++i) {
+            const double keep = up ? v[H + i] : v[i], send = up ? v[i] : v[H + i];
+            v[i] = keep + __shfl_xor(send, OFF, 64);
+        }
+        wave_sums_halve<H / 2, OFF / 2>(v, lane);
+    }
+}
+template <int N>
+__device__ __forceinline__ double wave_sums_x(double (&v)[N]) {
+    static_assert(N >= 2 && N <= 64 && (N & (N - 1)) == 0, "N a power of two in [2, 64]");
+    const int lane = threadIdx.x & 63;
+    wave_sums_halve<N / 2, 32>(v, lane);
+#pragma unroll
+    for (int off = 32 / N; off >= 1; off >>= 1) v[0] += __shfl_xor(v[0], off, 64);
+    return v[0];
+}
+
+__device__ __forceinline__ double wave_sum_d(double v) {   // fixed shuffle tree, result in all lanes
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+__global__ void __launch_bounds__(KM_TPB) k_kmeans_s(const uint32_t *__restrict__ keys, int64_t V,
+                                                    VolScalars *sc) {
+    __shared__ double s_pre[KMS_TILES + 1];   // 64-key tile sums -> their exclusive prefix
+    __shared__ double s_wtot[KMS_WAVES];
+    __shared__ float s_samp[KM_SAMPLES];
+    const int64_t b = blockIdx.x;
+    const int64_t n64 = sc[b].n_mask;
+    if (n64 <= 0) return;
+    if (n64 > (int64_t)KMS_TILES * 64) {   // (the host launches k_kmeans for such volumes)
+        if (threadIdx.x == 0) sc[b].km_iters = -1;
+        return;
+    }
+#ifdef KM_PROF
+    const uint64_t kp0 = wall_clock64();
+#endif
+    const uint32_t *k = keys + b * V;
+    const int n = (int)n64;   // positions below fit 32 bits (n <= 2^19): half the index instructions
+    const int t = threadIdx.x, w = t >> 6, lane = t & 63;
+    const int nt = (n + 63) / 64;
+    const int tps_log = nt > KM_SAMPLES ? 1 : 0;   // tiles per sample: 1 or 2 (nt <= 2 KM_SAMPLES)
+    const int stride = 64 << tps_log;
+    const int ns = (n - 1) / stride + 1;   // samples at 0, stride, 2 stride, ... < n
+    // tile sums and the sample (key j * stride = the first key of tile j << tps_log)
+    for (int t0 = (int)w * 16; t0 < nt; t0 += KMS_WAVES * 16) {
+        float f[16];
+        double v[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) f[q] = km_key_in(k, (t0 + q) * 64 + lane, 0, n);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            v[q] = (double)f[q];
+            const int tq = t0 + q;
+            if (lane == 0 && tq < nt && (tq & ((1 << tps_log) - 1)) == 0) s_samp[tq >> tps_log] = f[q];
+        }
+        const double ts = wave_sums_x<16>(v);
+        const int tt = t0 + (lane >> 2);
+        if ((lane & 3) == 0 && tt < nt) s_pre[tt] = ts;
+    }
+    __syncthreads();
+    {   // exclusive prefix of the tile sums (fixed order: thread chunks, wave scan)
+        const int per = (int)((nt + KM_TPB - 1) / KM_TPB);
+        const int t0 = (int)t * per, t1 = t0 + per < nt ? t0 + per : nt;
+        double mine = 0.0;   // (each thread rewrites only its own chunk)
+        for (int tt = t0; tt < t1; ++tt) mine += s_pre[tt];
+        double inc = mine;
+        for (int off = 1; off < 64; off <<= 1) {
+            const double o = __shfl_up(inc, off, 64);
+            if (lane >= off) inc += o;
+        }
+        double run = __shfl_up(inc, 1, 64);
+        if (lane == 0) run = 0.0;
+        if (lane == 63) s_wtot[w] = inc;
+        __syncthreads();
+        for (int ww = 0; ww < w; ++ww) run += s_wtot[ww];
+        for (int tt = t0; tt < t1; ++tt) { const double v = s_pre[tt]; s_pre[tt] = run; run += v; }
+        if (t1 == nt && t0 < t1) s_pre[nt] = run;
+    }
+    __syncthreads();
+    if (w != 0) return;   // one wave iterates; every value below is wave-uniform
+    double c[KM_K];
+#pragma unroll
+    for (int j = 0; j < KM_K; ++j) c[j] = (double)key2f(k[(int)(((int64_t)n * (2 * j + 1)) / (2 * KM_K))]);
+    // the fixed cuts 0 and n: cut 0 has Σ[0, min(64, n)) above it; cut n has Σ[64 floor(n / 64), n)
+    // below it
+    const int wbn = ((n - 1) / 64) * 64;
+    double plo_n;
+    {
+        const int tn = (n / 64) * 64;
+        double lo = 0.0;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            const int i = wbn + 64 * q + lane;
+            const float x = km_key_in(k, i, (decltype(i))0, (decltype(i))n);
+            lo += i >= tn && i < n ? (double)x : 0.0;
+        }
+        plo_n = wave_sum_d(lo);
+    }
+    const double phi_0 = s_pre[1] - s_pre[0];
+    int cut[KM_K + 1];
+    double plo[KM_K + 1], phi[KM_K + 1];
+#pragma unroll
+    for (int j = 0; j <= KM_K; ++j) { cut[j] = -1; plo[j] = 0.0; phi[j] = 0.0; }
+    int jsp[KM_K - 1], wbp[KM_K - 1];
+    float wv[KM_K - 1][3];
+#pragma unroll
+    for (int j = 0; j < KM_K - 1; ++j) {
+        jsp[j] = -1;
+        wbp[j] = -1;
+#pragma unroll
+        for (int q = 0; q < 3; ++q) wv[j][q] = 0.0f;
+    }
+#ifdef KM_PROF
+    const uint64_t kp1 = wall_clock64();
+    int nsearch = 0;
+#endif
+    int it = 0;
+    for (it = 1; it <= 300; ++it) {
+        // sample intervals of the three boundaries (LDS only); a boundary is taken against the next
+        // LARGER centre (centres are kept sorted; one equal to its predecessor gets no values)
+        bool up[KM_K - 1];
+        double clo[KM_K - 1], chi[KM_K - 1];
+        int lo[KM_K - 1], hi[KM_K - 1], wb[KM_K - 1];
+#pragma unroll
+        for (int j = 0; j < KM_K - 1; ++j) {
+            up[j] = false;
+            chi[j] = 0.0;
+#pragma unroll
+            for (int m = j + 1; m < KM_K; ++m)
+                if (!up[j] && c[m] > c[j]) { chi[j] = c[m]; up[j] = true; }
+            clo[j] = c[j];
+            lo[j] = hi[j] = n;
+            wb[j] = wbn;
+            if (up[j]) {
+                int js = jsp[j];
+                bool still = js >= 0;
+                if (still) {   // sample js true (or js = ns) and sample js - 1 false (or js = 0)
+                    const bool tr = js < ns ? km_closer((double)s_samp[js], clo[j], chi[j]) : true;
+                    const bool fa = js == 0 ? true : !km_closer((double)s_samp[js - 1], clo[j], chi[j]);
+                    still = tr && fa;
+                }
+                if (!still) {
+                    js = km_sample_search(s_samp, ns, clo[j], chi[j]);
+#ifdef KM_PROF
+                    ++nsearch;
+#endif
+                }
+                jsp[j] = js;
+                lo[j] = js == 0 ? 0 : (js - 1) * stride + 1;   // the cut is in [lo, hi]
+                hi[j] = js >= ns ? n : js * stride;
+                wb[j] = (lo[j] / 64) * 64;   // hi - lo < stride <= 128: [wb, wb + 192) holds [lo, hi]
+            }                                // and the whole tile of any cut in it
+        }
+#pragma unroll
+        for (int j = 0; j < KM_K - 1; ++j)
+            if (wb[j] != wbp[j]) {   // (a boundary whose interval stayed keeps its window)
+                wbp[j] = wb[j];
+#pragma unroll
+                for (int q = 0; q < 3; ++q) wv[j][q] = km_key_in(k, wb[j] + 64 * q + lane, 0, n);
+            }
+        int nc[KM_K + 1];
+        double pv[8];
+        nc[0] = 0;
+        nc[KM_K] = n;
+#pragma unroll
+        for (int j = 0; j < KM_K - 1; ++j) {
+            int cj = n;
+            if (up[j]) {
+                uint64_t any = 0ull;
+                int first = 192;
+#pragma unroll
+                for (int q = 0; q < 3; ++q) {
+                    const int i = wb[j] + 64 * q + lane;
+                    const bool pr = i >= lo[j] && i < hi[j] && km_closer((double)wv[j][q], clo[j], chi[j]);
+                    const uint64_t m = __ballot(pr);
+                    if (!any && m) first = 64 * q + __ffsll((long long)m) - 1;
+                    any |= m;
+                }
+                cj = any ? wb[j] + first : hi[j];
+            }
+            nc[j + 1] = cj;
+            const int tc = (cj / 64) * 64;   // the cut's tile (inside the window)
+            double a = 0.0, e = 0.0;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) {
+                const int i = wb[j] + 64 * q + lane;
+                const bool in = i >= tc && i < tc + 64 && i < n;
+                a += in && i < cj ? (double)wv[j][q] : 0.0;
+                e += in && i >= cj ? (double)wv[j][q] : 0.0;
+            }
+            pv[2 * j] = a;
+            pv[2 * j + 1] = e;
+        }
+        pv[6] = pv[7] = 0.0;
+        const double red = wave_sums_x<8>(pv);   // value q's total in lanes 8q .. 8q + 7
+        double nlo[KM_K + 1], nhi[KM_K + 1];
+        nlo[0] = 0.0;
+        nhi[0] = phi_0;
+        nlo[KM_K] = plo_n;
+        nhi[KM_K] = 0.0;
+#pragma unroll
+        for (int j = 0; j < KM_K - 1; ++j) {
+            nlo[j + 1] = readlane_d(red, 16 * j);
+            nhi[j + 1] = readlane_d(red, 16 * j + 8);
+        }
+#pragma unroll
+        for (int j = 2; j < KM_K; ++j)
+            if (nc[j] < nc[j - 1]) {   // (as k_kmeans; sorted centres give ordered cuts)
+                nc[j] = nc[j - 1];
+                nlo[j] = nlo[j - 1];
+                nhi[j] = nhi[j - 1];
+            }
+        bool same = true;
+#pragma unroll
+        for (int j = 0; j <= KM_K; ++j) same = same && nc[j] == cut[j];
+        if (same) break;
+        double sum[KM_K];
+#pragma unroll
+        for (int j = 0; j <= KM_K; ++j) { cut[j] = nc[j]; plo[j] = nlo[j]; phi[j] = nhi[j]; }
+#pragma unroll
+        for (int j = 0; j < KM_K; ++j) {   // head partial + whole tiles (prefix) + tail partial
+            const int a = cut[j], e = cut[j + 1];
+            const int ta = a / 64, te = e / 64;
+            sum[j] = e <= a ? 0.0
+                            : (ta == te ? phi[j] - phi[j + 1] : phi[j] + (s_pre[te] - s_pre[ta + 1]) + plo[j + 1]);
+        }
+        km_update<true>(k, cut, sum, c);   // means, empty-cluster relocation, sort
+    }
+    if (lane == 0) {   // VDP_km: the lowest non-empty cluster
+        int low = 0;
+#pragma unroll
+        for (int j = KM_K - 1; j >= 0; --j)
+            if (cut[j + 1] > cut[j]) low = cut[j + 1] - cut[j];
+        sc[b].n_km0 = low;
+        sc[b].km_iters = it;
+#pragma unroll
+        for (int j = 0; j < KM_K; ++j) sc[b].km_c[j] = c[j];
+#ifdef KM_PROF
+        const uint64_t kp2 = wall_clock64();
+        if (b < 4)
+            printf("KMPROF b=%d n=%d it=%d init=%lu loop=%lu searches=%d\n", (int)b, n, it,
+                   (unsigned long)(kp1 - kp0), (unsigned long)(kp2 - kp1), nsearch);
+#endif
     }
 }
 
@@ -1799,7 +2136,10 @@ void vh_launch_vdp_chain(vh_batch *b, const float *d_n4, const vh_run_opts &o) {
                          KM_TPB, 0, st>>>(b->d_keys0, b->V, scratch, max_ktiles, b->d_sc);
             VH_CHECK_LAUNCH();
         }
-        k_kmeans<<<(unsigned)b->nb, KM_TPB, 0, st>>>(b->d_keys0, b->V, scratch, max_ktiles, b->d_sc);
+        if (b->V <= (int64_t)KMS_TILES * 64 && !(getenv("VH_KM_OLD") && atoi(getenv("VH_KM_OLD"))))
+            k_kmeans_s<<<(unsigned)b->nb, KM_TPB, 0, st>>>(b->d_keys0, b->V, b->d_sc);
+        else
+            k_kmeans<<<(unsigned)b->nb, KM_TPB, 0, st>>>(b->d_keys0, b->V, scratch, max_ktiles, b->d_sc);
         VH_CHECK_LAUNCH();
     }
     if (o.do_snr) vh_launch_snr(b);
