@@ -1081,12 +1081,17 @@ __global__ void __launch_bounds__(ST_TPB, 4) k_n4_study(StudyArgs a) {
 // cost) first, ties by index: the dispatcher starts workgroups in order, so when the CUs are
 // shared with another batch's launch (batches in flight) the long studies start first and the
 // launch's tail is its short studies.  One workgroup, rank by counting (nb <= 4096).
+// The counts are staged in LDS first (each thread reading all nb counts from global memory, one
+// load after another, took 26 us).
 __global__ void __launch_bounds__(1024) k_study_order(const VolScalars *sc, int64_t nb, int32_t *order) {
+    __shared__ int64_t s_n[4096];
+    for (int64_t i = threadIdx.x; i < nb; i += blockDim.x) s_n[i] = sc[i].n_mask1;
+    __syncthreads();
     for (int64_t i = threadIdx.x; i < nb; i += blockDim.x) {
-        const int64_t ni = sc[i].n_mask1;
+        const int64_t ni = s_n[i];
         int32_t r = 0;
         for (int64_t j = 0; j < nb; ++j) {
-            const int64_t nj = sc[j].n_mask1;
+            const int64_t nj = s_n[j];
             r += (nj > ni) || (nj == ni && j < i);
         }
         order[r] = (int32_t)i;

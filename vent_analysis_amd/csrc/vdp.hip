@@ -144,9 +144,18 @@ __global__ void __launch_bounds__(VH_TPB) k_mask_finish(const int32_t *colcount,
     s_part[t] = acc;
     if (t == 0) { s_cmin = INT_MAX; s_cmax = 0; s_rowe = 0; s_slie = 0; s_rlo = INT_MAX; s_rhi = -1; }
     __syncthreads();
-    if (t == 0) {
-        int64_t run = 0;
-        for (int i = 0; i < VH_TPB; ++i) { int64_t v = s_part[i]; s_part[i] = run; run += v; }
+    if (t < 64) {   // exclusive scan of the VH_TPB partials by one wave (integers: exact in any order)
+        int64_t v[VH_TPB / 64], tot = 0;
+#pragma unroll
+        for (int q = 0; q < VH_TPB / 64; ++q) { v[q] = s_part[t * (VH_TPB / 64) + q]; tot += v[q]; }
+        int64_t inc = tot;
+        for (int off = 1; off < 64; off <<= 1) {
+            const int64_t o = __shfl_up(inc, off, 64);
+            if (t >= off) inc += o;
+        }
+        int64_t run = inc - tot;
+#pragma unroll
+        for (int q = 0; q < VH_TPB / 64; ++q) { s_part[t * (VH_TPB / 64) + q] = run; run += v[q]; }
     }
     __syncthreads();
     int64_t run = s_part[t];
@@ -275,6 +284,14 @@ __global__ void __launch_bounds__(VS_TPB) k_sort_vol(uint32_t *__restrict__ k0,
     for (int i = t; i < 4 * 256; i += VS_TPB) (&s_hist[0][0])[i] = 0u;
     __syncthreads();
     uint32_t *kin = k0 + b * V, *kout = k1 + b * V;
+#ifdef VS_PROF
+    uint64_t vp[7] = {0, 0, 0, 0, 0, 0, 0}, vrank[4] = {0, 0, 0, 0};
+    uint32_t vor = 0u, vfirst = n > 0 ? k0[b * V] : 0u;
+    uint64_t vq = wall_clock64();
+#define VS_STAMP(k) do { if (t == 0) { const uint64_t x_ = wall_clock64(); vp[k] += x_ - vq; vq = x_; } } while (0)
+#else
+#define VS_STAMP(k) do { } while (0)
+#endif
     // ---- the four digit histograms (one add per row when a row shares its digit); each wave
     // loads VS_KPT rows of 64 keys at a time, so one memory round trip covers 8 rows ----
     for (int64_t i0 = (int64_t)w * (VS_KPT * 64); i0 < n; i0 += (int64_t)VS_TPB * VS_KPT) {
@@ -287,6 +304,9 @@ __global__ void __launch_bounds__(VS_TPB) k_sort_vol(uint32_t *__restrict__ k0,
 #pragma unroll
         for (int r = 0; r < VS_KPT; ++r) {
             const bool valid = i0 + r * 64 + lane < n;
+#ifdef VS_PROF
+            if (valid) vor |= kr[r] ^ vfirst;
+#endif
             const uint64_t vmask = __ballot(valid);   // outside the lane-0 branch
 #pragma unroll
             for (int p = 0; p < 4; ++p) {
@@ -301,6 +321,7 @@ __global__ void __launch_bounds__(VS_TPB) k_sort_vol(uint32_t *__restrict__ k0,
         }
     }
     __syncthreads();
+    VS_STAMP(0);
     if (t < 4) {   // exclusive scan per digit position
         uint32_t run = 0;
         for (int d = 0; d < 256; ++d) { const uint32_t v = s_hist[t][d]; s_hist[t][d] = run; run += v; }
@@ -320,6 +341,10 @@ __global__ void __launch_bounds__(VS_TPB) k_sort_vol(uint32_t *__restrict__ k0,
                 const int64_t idx = c0 + (int64_t)w * (VS_KPT * 64) + r * 64 + lane;
                 key[r] = idx < n ? kin[idx] : 0u;
             }
+#ifdef VS_PROF
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            VS_STAMP(6);
+#endif
 #pragma unroll
             for (int r = 0; r < VS_KPT; ++r) {   // wave w owns keys [c0 + 64 VS_KPT w, c0 + 64 VS_KPT (w + 1))
                 const int64_t idx = c0 + (int64_t)w * (VS_KPT * 64) + r * 64 + lane;
@@ -341,6 +366,10 @@ __global__ void __launch_bounds__(VS_TPB) k_sort_vol(uint32_t *__restrict__ k0,
                 rank[r] = valid ? base + below : 0xffffffffu;
             }
             __syncthreads();
+#ifdef VS_PROF
+            if (t == 0) { const uint64_t x_ = wall_clock64(); vrank[p] += x_ - vq; }
+#endif
+            VS_STAMP(1);
             if (t < 256) {   // digit t: chunk-local wave prefixes and chunk total, then a scan of
                              // the totals over digits (wave shuffles + wave sums)
                 uint32_t tot = 0;
@@ -359,12 +388,14 @@ __global__ void __launch_bounds__(VS_TPB) k_sort_vol(uint32_t *__restrict__ k0,
                 s_cst[t] = inc - tot;   // exclusive within this wave of digits
             }
             __syncthreads();
+            VS_STAMP(2);
             if (t < 256) {
                 uint32_t pre = 0;
                 for (int ww = 0; ww < w; ++ww) pre += s_wsum[ww];
                 s_cst[t] += pre;        // chunk-local start of digit t
             }
             __syncthreads();
+            VS_STAMP(3);
 #pragma unroll
             for (int r = 0; r < VS_KPT; ++r) {   // stage at the chunk-local sorted position
                 if (rank[r] == 0xffffffffu) continue;
@@ -372,6 +403,7 @@ __global__ void __launch_bounds__(VS_TPB) k_sort_vol(uint32_t *__restrict__ k0,
                 s_stage[s_cst[d] + s_wc[w][d] + rank[r]] = key[r];
             }
             __syncthreads();
+            VS_STAMP(4);
             // write out in staged order: equal digits are consecutive, so are their targets
             const int cn = (int)(n - c0 < VS_CHUNK ? n - c0 : VS_CHUNK);
             for (int q = t; q < cn; q += VS_TPB) {
@@ -380,11 +412,20 @@ __global__ void __launch_bounds__(VS_TPB) k_sort_vol(uint32_t *__restrict__ k0,
                 kout[s_hist[p][d] + s_run[d] + ((uint32_t)q - s_cst[d])] = kk;
             }
             __syncthreads();
+            VS_STAMP(5);
             if (t < 256) s_run[t] += s_tot[t];
         }
         uint32_t *tmp = kin; kin = kout; kout = tmp;
         __syncthreads();   // this pass's stores before the next pass's loads (same workgroup)
     }
+#ifdef VS_PROF
+    if (t == 0 && b < 4)
+        printf("VSPROF b=%d n=%ld hist=%lu load=%lu rank=%lu scan=%lu pre=%lu stage=%lu write=%lu rank/pass %lu %lu %lu %lu varbits(t0) %08x\n", (int)b,
+               (long)n, (unsigned long)vp[0], (unsigned long)vp[6], (unsigned long)vp[1], (unsigned long)vp[2],
+               (unsigned long)vp[3], (unsigned long)vp[4], (unsigned long)vp[5], (unsigned long)vrank[0],
+               (unsigned long)vrank[1], (unsigned long)vrank[2], (unsigned long)vrank[3], vor);
+#endif
+#undef VS_STAMP
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1902,10 +1943,12 @@ __device__ __forceinline__ int cohort_g(uint32_t key, float p99) {
     return nv < 0.0f ? -1 : VH_COHORT_BINS;
 }
 
-__global__ void __launch_bounds__(VH_TPB) k_cohort_search(const uint32_t *__restrict__ keys,
+#define CO_TPB 1024
+#define CO_SAMPLES 4096   // LDS sample: the global part of an edge's search spans <= n / 4096 + 1 keys
+__global__ void __launch_bounds__(CO_TPB) k_cohort_search(const uint32_t *__restrict__ keys,
                                                          const VolScalars *sc, int64_t V,
                                                          uint32_t *rows) {
-    __shared__ int s_g[VH_COHORT_BINS];
+    __shared__ int s_g[CO_SAMPLES];
     __shared__ int64_t s_first[VH_COHORT_BINS + 1];
     const int64_t b = blockIdx.x;
     const int64_t n = sc[b].n_mask;
@@ -1913,10 +1956,10 @@ __global__ void __launch_bounds__(VH_TPB) k_cohort_search(const uint32_t *__rest
     const uint32_t *k = keys + b * V;
     const int t = threadIdx.x;
     if (n <= 0 || !(p99 > 0.0f) || isinf(p99)) {   // scan path (k_cohort_vol)
-        __shared__ uint32_t h[VH_COHORT_BINS];
-        for (int i = t; i < VH_COHORT_BINS; i += VH_TPB) h[i] = 0u;
+        uint32_t *h = reinterpret_cast<uint32_t *>(s_g);
+        for (int i = t; i < VH_COHORT_BINS; i += CO_TPB) h[i] = 0u;
         __syncthreads();
-        const int64_t per = (n + VH_TPB - 1) / VH_TPB;
+        const int64_t per = (n + CO_TPB - 1) / CO_TPB;
         const int64_t cs = t * per < n ? t * per : n, ce = cs + per < n ? cs + per : n;
         for (int64_t i = cs; i < ce; ++i) {
             const float nv = key2f(k[i]) / p99;
@@ -1926,13 +1969,25 @@ __global__ void __launch_bounds__(VH_TPB) k_cohort_search(const uint32_t *__rest
             }
         }
         __syncthreads();
-        for (int i = t; i < VH_COHORT_BINS; i += VH_TPB) rows[b * VH_COHORT_BINS + i] = h[i];
+        for (int i = t; i < VH_COHORT_BINS; i += CO_TPB) rows[b * VH_COHORT_BINS + i] = h[i];
         return;
     }
-    const int S = n < VH_COHORT_BINS ? (int)n : VH_COHORT_BINS;
-    for (int j = t; j < S; j += VH_TPB) s_g[j] = cohort_g(k[(j * n) / S], p99);
+    const int S = n < CO_SAMPLES ? (int)n : CO_SAMPLES;
+    {   // the sample's loads all in flight (unconditional, index clamped: a guarded load waits)
+        uint32_t kv[CO_SAMPLES / CO_TPB];
+#pragma unroll
+        for (int q = 0; q < CO_SAMPLES / CO_TPB; ++q) {
+            const int j = t + q * CO_TPB;
+            kv[q] = k[j < S ? ((int64_t)j * n) / S : 0];
+        }
+#pragma unroll
+        for (int q = 0; q < CO_SAMPLES / CO_TPB; ++q) {
+            const int j = t + q * CO_TPB;
+            if (j < S) s_g[j] = cohort_g(kv[q], p99);
+        }
+    }
     __syncthreads();
-    for (int e = t; e <= VH_COHORT_BINS; e += VH_TPB) {
+    for (int e = t; e <= VH_COHORT_BINS; e += CO_TPB) {
         // last sample j with g < e (sample positions are increasing, g non-decreasing)
         int lo = -1, hi = S;   // s_g[lo] < e <= s_g[hi] (virtual ends)
         while (hi - lo > 1) {
@@ -1940,7 +1995,7 @@ __global__ void __launch_bounds__(VH_TPB) k_cohort_search(const uint32_t *__rest
             if (s_g[mid] < e) lo = mid; else hi = mid;
         }
         // first index i with g(i) >= e lies in (pos(lo), pos(hi)]
-        int64_t a = lo < 0 ? -1 : (lo * n) / S, z = hi >= S ? n : (hi * n) / S;
+        int64_t a = lo < 0 ? -1 : ((int64_t)lo * n) / S, z = hi >= S ? n : ((int64_t)hi * n) / S;
         while (z - a > 1) {
             const int64_t mid = (a + z) >> 1;
             if (cohort_g(k[mid], p99) < e) a = mid; else z = mid;
@@ -1948,16 +2003,37 @@ __global__ void __launch_bounds__(VH_TPB) k_cohort_search(const uint32_t *__rest
         s_first[e] = z;
     }
     __syncthreads();
-    for (int i = t; i < VH_COHORT_BINS; i += VH_TPB)
+    for (int i = t; i < VH_COHORT_BINS; i += CO_TPB)
         rows[b * VH_COHORT_BINS + i] = (uint32_t)(s_first[i + 1] - s_first[i]);
 }
 
-__global__ void k_cohort_sum(const uint32_t *rows, int64_t nb, uint64_t *cohort) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= VH_COHORT_BINS) return;
+// the cohort: per bin the sum of the volumes' rows (integers: any order gives the same sum).
+// Block = 64 bins x 16 volume groups; a thread sums every 16th volume with its loads in flight
+// together, then the 16 groups are added in LDS (one thread per bin summing 256 rows in a loop
+// waited on its loads: ~0.03 ms of the cohort's 0.09 ms).
+#define CS_BINS 64
+#define CS_GROUPS 16
+__global__ void __launch_bounds__(CS_BINS * CS_GROUPS) k_cohort_sum(const uint32_t *rows, int64_t nb,
+                                                                   uint64_t *cohort) {
+    __shared__ uint64_t s_part[CS_GROUPS][CS_BINS];
+    const int bin = blockIdx.x * CS_BINS + (threadIdx.x % CS_BINS), g = threadIdx.x / CS_BINS;
     uint64_t s = 0;
-    for (int64_t b = 0; b < nb; ++b) s += rows[b * VH_COHORT_BINS + i];
-    cohort[i] = s;
+    int64_t v = g;
+    for (; v + 7 * CS_GROUPS < nb; v += 8 * CS_GROUPS) {
+        uint32_t r[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) r[q] = rows[(v + q * CS_GROUPS) * VH_COHORT_BINS + bin];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) s += r[q];
+    }
+    for (; v < nb; v += CS_GROUPS) s += rows[v * VH_COHORT_BINS + bin];
+    s_part[g][threadIdx.x % CS_BINS] = s;
+    __syncthreads();
+    if (g == 0) {
+        uint64_t tot = 0;
+        for (int q = 0; q < CS_GROUPS; ++q) tot += s_part[q][threadIdx.x];
+        cohort[bin] = tot;
+    }
 }
 
 // =============================================================================================
@@ -2006,12 +2082,18 @@ __global__ void __launch_bounds__(VH_TPB) k_snr(const float *__restrict__ hp,
     snr_block_write(acc, s_red, sb.part + (b * sb.nparts + blockIdx.x) * 4);
 }
 
+// One wave per volume: lane l sums parts l, l + 64, ... in order, then a fixed shuffle tree (one
+// thread per volume walking its parts one load after another took 13 us).
 __global__ void k_snr_finish(const double *part, int64_t nparts, int64_t nb, VolScalars *sc) {
-    const int64_t b = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    const int64_t b = blockIdx.x * (int64_t)(blockDim.x / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
     if (b >= nb) return;
     double a[4] = {0, 0, 0, 0};
-    for (int64_t p = 0; p < nparts; ++p)
+    for (int64_t p = lane; p < nparts; p += 64)
         for (int q = 0; q < 4; ++q) a[q] += part[(b * nparts + p) * 4 + q];
+    for (int q = 0; q < 4; ++q)
+        for (int off = 32; off > 0; off >>= 1) a[q] += __shfl_xor(a[q], off, 64);
+    if (lane != 0) return;
     const double nsig = (double)sc[b].n_mask;
     if (!sc[b].snr_ok || a[3] <= 0.0 || nsig <= 0.0) {
         sc[b].snr = __longlong_as_double(0x7ff8000000000000ll);
@@ -2034,8 +2116,7 @@ void vh_launch_snr(vh_batch *b) {
                                                b->V, b->part_blocks, sb);
         VH_CHECK_LAUNCH();
     }
-    k_snr_finish<<<(unsigned)((b->nb + 63) / 64), 64, 0, st>>>(b->d_snrpart, b->slab_blocks, b->nb,
-                                                              b->d_sc);
+    k_snr_finish<<<(unsigned)((b->nb + 3) / 4), 256, 0, st>>>(b->d_snrpart, b->slab_blocks, b->nb, b->d_sc);
     VH_CHECK_LAUNCH();
 }
 
@@ -2121,9 +2202,9 @@ void vh_launch_vdp_chain(vh_batch *b, const float *d_n4, const vh_run_opts &o) {
     if (o.do_cohort) {
         ScopedKTimer tm(b, "cohort", 0.0);
         uint32_t *rows = b->d_tilecnt;   // free after the sort: nb*256*max_tiles >= nb*1024 u32
-        k_cohort_search<<<(unsigned)b->nb, VH_TPB, 0, st>>>(b->d_keys0, b->d_sc, b->V, rows);
+        k_cohort_search<<<(unsigned)b->nb, CO_TPB, 0, st>>>(b->d_keys0, b->d_sc, b->V, rows);
         VH_CHECK_LAUNCH();
-        k_cohort_sum<<<VH_COHORT_BINS / 256, 256, 0, st>>>(rows, b->nb, b->d_cohort);
+        k_cohort_sum<<<VH_COHORT_BINS / CS_BINS, CS_BINS * CS_GROUPS, 0, st>>>(rows, b->nb, b->d_cohort);
         VH_CHECK_LAUNCH();
     }
     if (o.do_kmeans) {
