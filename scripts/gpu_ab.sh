@@ -11,6 +11,6 @@ for r in $(seq 1 ${REPS:-2}); do
     VH_LIB_PATH=$lib timeout -k 10 200 python bench.py --steps 6 --warmup 1 --no-cpu-baseline --no-h2h ${BENCH_ARGS} \
         > gpurun_out/${TAG}_${v}_$r.json 2> gpurun_out/${TAG}_${v}_$r.err
     rc=$?; [ $rc -eq 0 ] || { echo "variant $v rc=$rc"; tail -3 gpurun_out/${TAG}_${v}_$r.err; exit $rc; }
-    python3 -c "import json;d=json.loads(open('gpurun_out/${TAG}_${v}_$r.json').read().splitlines()[-1]);r=d['roofline'];k=r['kernel_us_per_launch'];print('$v', $r, d['value'], r['avg_launch_us'], r['kernel'], d['n4_study_times'], {n: k[n] for n in k if not n.startswith('n4_')}, 'non_n4', r.get('non_n4_us_per_step'))"
+    python3 -c "import json;d=json.loads(open('gpurun_out/${TAG}_${v}_$r.json').read().splitlines()[-1]);r=d['roofline'];k=r['kernel_us_per_launch'];print('$v', $r, d['value'], r['avg_launch_us'], r['kernel'], d['n4_study_times'], {n: k[n] for n in k if n != 'n4_study'}, 'non_n4', r.get('non_n4_us_per_step'))"
   done
 done

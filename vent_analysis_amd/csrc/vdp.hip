@@ -638,12 +638,16 @@ __device__ float pw_tree_sum(const uint32_t *a, int m, PwTree &T) {
         const int ln = has ? T.n[node] : 0;
         const uint32_t *p = a + (has ? T.s[node] : 0);
         const int lim = ln - ln % 8;
-        float v[16];
+        // every load unconditional at a clamped index (p[0] is a key of the chunk): guarded loads
+        // compile to exec-masked branches that wait for each load in turn
+        float v[16], tl[7];
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
             const int i = 8 * q + j;
-            v[q] = i < lim ? key2f(p[i]) : 0.0f;
+            v[q] = key2f(p[i < lim ? i : 0]);
         }
+#pragma unroll
+        for (int q = 0; q < 7; ++q) tl[q] = key2f(p[lim + q < ln ? lim + q : 0]);   // the n % 8 tail
         float r = v[0];
 #pragma unroll
         for (int q = 1; q < 16; ++q)
@@ -653,7 +657,9 @@ __device__ float pw_tree_sum(const uint32_t *a, int m, PwTree &T) {
         r = r + __shfl_xor(r, 4, 64);
         if (has && j == 0) {
             float res = ln < 8 ? 0.0f : r;
-            for (int i = lim; i < ln; ++i) res = res + key2f(p[i]);
+#pragma unroll
+            for (int q = 0; q < 7; ++q)
+                if (lim + q < ln) res = res + tl[q];
             T.sum[node] = res;
         }
     }
@@ -690,15 +696,19 @@ __global__ void __launch_bounds__(VH_TPB) k_chunk_sums(const uint32_t *__restric
     // full chunk: 64 leaves of 128, 8 at a time: lane = (leaf, accumulator j) -- pw_leaf's 8
     // stride-8 accumulators run on 8 lanes (loads of a leaf row are 8 consecutive keys), then its
     // fixed combine tree by xor shuffles (a + b == b + a bitwise)
+    float v[8][16];   // all 8 groups' loads in flight together (one memory round trip, not 8)
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+        const uint32_t *p = a + 128 * (g * 8 + (lane >> 3));
+#pragma unroll
+        for (int q = 0; q < 16; ++q) v[g][q] = key2f(p[8 * q + (lane & 7)]);
+    }
+#pragma unroll
     for (int g = 0; g < 8; ++g) {
         const int leaf = g * 8 + (lane >> 3), j = lane & 7;
-        const uint32_t *p = a + 128 * leaf;
-        float v[16];
+        float r = v[g][0];
 #pragma unroll
-        for (int q = 0; q < 16; ++q) v[q] = key2f(p[8 * q + j]);
-        float r = v[0];
-#pragma unroll
-        for (int q = 1; q < 16; ++q) r = r + v[q];
+        for (int q = 1; q < 16; ++q) r = r + v[g][q];
         r = r + __shfl_xor(r, 1, 64);
         r = r + __shfl_xor(r, 2, 64);
         r = r + __shfl_xor(r, 4, 64);
