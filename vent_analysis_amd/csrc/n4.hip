@@ -383,6 +383,26 @@ __global__ void __launch_bounds__(64) k_n4_rowcount(const uint32_t *colbits, int
     }
 }
 
+// exclusive scan of VH_TPB partials in LDS by one wave (integers: exact in any order)
+__device__ __forceinline__ void excl_scan_parts(int64_t *s_part) {
+    const int t = threadIdx.x;
+    if (t < 64) {
+        int64_t v[VH_TPB / 64], tot = 0;
+#pragma unroll
+        for (int q = 0; q < VH_TPB / 64; ++q) { v[q] = s_part[t * (VH_TPB / 64) + q]; tot += v[q]; }
+        int64_t inc = tot;
+        for (int off = 1; off < 64; off <<= 1) {
+            const int64_t o = __shfl_up(inc, off, 64);
+            if (t >= off) inc += o;
+        }
+        int64_t run = inc - tot;
+#pragma unroll
+        for (int q = 0; q < VH_TPB / 64; ++q) { s_part[t * (VH_TPB / 64) + q] = run; run += v[q]; }
+    }
+}
+#define RSB 16   // loads per batch, all in flight (unconditional, clamped index): a loop of guarded
+                 // loads waits for each one in turn (k_n4_rowscan + k_n4_rrank took 0.1 ms per batch)
+
 // pass 2: exclusive scan over (tile, row) in tile-major order, one block per volume
 __global__ void __launch_bounds__(VH_TPB) k_n4_rowscan(int32_t *rs, int64_t n) {
     __shared__ int64_t s_part[VH_TPB];
@@ -392,16 +412,26 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_rowscan(int32_t *rs, int64_t n) {
     const int64_t per = (n + VH_TPB - 1) / VH_TPB;
     const int64_t s0 = t * per < n ? t * per : n, e0 = s0 + per < n ? s0 + per : n;
     int64_t acc = 0;
-    for (int64_t i = s0; i < e0; ++i) acc += a[i];
+    for (int64_t i0 = s0; i0 < e0; i0 += RSB) {
+        int32_t v[RSB];
+#pragma unroll
+        for (int q = 0; q < RSB; ++q) v[q] = a[i0 + q < e0 ? i0 + q : s0];
+#pragma unroll
+        for (int q = 0; q < RSB; ++q) acc += i0 + q < e0 ? v[q] : 0;
+    }
     s_part[t] = acc;
     __syncthreads();
-    if (t == 0) {
-        int64_t run = 0;
-        for (int i = 0; i < VH_TPB; ++i) { const int64_t v = s_part[i]; s_part[i] = run; run += v; }
-    }
+    excl_scan_parts(s_part);
     __syncthreads();
     int64_t run = s_part[t];
-    for (int64_t i = s0; i < e0; ++i) { const int32_t v = a[i]; a[i] = (int32_t)run; run += v; }
+    for (int64_t i0 = s0; i0 < e0; i0 += RSB) {
+        int32_t v[RSB];
+#pragma unroll
+        for (int q = 0; q < RSB; ++q) v[q] = a[i0 + q < e0 ? i0 + q : s0];
+#pragma unroll
+        for (int q = 0; q < RSB; ++q)
+            if (i0 + q < e0) { a[i0 + q] = (int32_t)run; run += v[q]; }
+    }
 }
 
 // ---- the same two scans for large volumes, over the whole GPU (config 5: the one-workgroup forms
@@ -534,15 +564,18 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_rrank(const uint64_t *rowmask, co
                                                     int64_t R, int64_t ntiles, int64_t VS,
                                                     int32_t *rrank, int32_t *perm) {
     extern __shared__ int32_t s_rowtot[];   // [R]
-    __shared__ int32_t s_part[VH_TPB];
+    __shared__ int64_t s_part[VH_TPB];
     const int64_t b = blockIdx.x;
     const uint64_t *rm = rowmask + b * ntiles * R;
     int32_t *rr = rrank + b * ntiles * R;
-    for (int64_t x = threadIdx.x; x < R; x += VH_TPB) {
+    for (int64_t x = threadIdx.x; x < R; x += VH_TPB) {   // row totals
         int32_t run = 0;
-        for (int64_t t = 0; t < ntiles; ++t) {
-            rr[t * R + x] = run;
-            run += __popcll(rm[t * R + x]);
+        for (int64_t t0 = 0; t0 < ntiles; t0 += RSB) {
+            uint64_t m[RSB];
+#pragma unroll
+            for (int q = 0; q < RSB; ++q) m[q] = rm[(t0 + q < ntiles ? t0 + q : 0) * R + x];
+#pragma unroll
+            for (int q = 0; q < RSB; ++q) run += t0 + q < ntiles ? __popcll(m[q]) : 0;
         }
         s_rowtot[x] = run;
     }
@@ -550,24 +583,29 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_rrank(const uint64_t *rowmask, co
     const int t = threadIdx.x;
     const int64_t per = (R + VH_TPB - 1) / VH_TPB;
     const int64_t s0 = t * per < R ? t * per : R, e0 = s0 + per < R ? s0 + per : R;
-    int32_t acc = 0;
+    int64_t acc = 0;
     for (int64_t i = s0; i < e0; ++i) acc += s_rowtot[i];
     s_part[t] = acc;
     __syncthreads();
-    if (t == 0) {
-        int32_t run = 0;
-        for (int i = 0; i < VH_TPB; ++i) { const int32_t v = s_part[i]; s_part[i] = run; run += v; }
-    }
+    excl_scan_parts(s_part);
     __syncthreads();
-    int32_t run = s_part[t];
+    int32_t run = (int32_t)s_part[t];
     for (int64_t i = s0; i < e0; ++i) { const int32_t v = s_rowtot[i]; s_rowtot[i] = run; run += v; }
     __syncthreads();
-    // raster rank of each (tile, row)'s first masked voxel; perm (raster rank -> compact index,
-    // the sweep driver's convergence walk) is scattered by k_n4_perm over the whole GPU (one
-    // workgroup here took 22 ms at 512^3)
+    // raster rank of each (tile, row)'s first masked voxel = masked voxels of the rows before x
+    // plus those of row x in the tiles before; perm (raster rank -> compact index, the sweep
+    // driver's convergence walk) is scattered by k_n4_perm over the whole GPU (one workgroup here
+    // took 22 ms at 512^3)
     for (int64_t x = threadIdx.x; x < R; x += VH_TPB) {
-        const int32_t base = s_rowtot[x];
-        for (int64_t tt = 0; tt < ntiles; ++tt) rr[tt * R + x] += base;
+        int32_t r = s_rowtot[x];
+        for (int64_t t0 = 0; t0 < ntiles; t0 += RSB) {
+            uint64_t m[RSB];
+#pragma unroll
+            for (int q = 0; q < RSB; ++q) m[q] = rm[(t0 + q < ntiles ? t0 + q : 0) * R + x];
+#pragma unroll
+            for (int q = 0; q < RSB; ++q)
+                if (t0 + q < ntiles) { rr[(t0 + q) * R + x] = r; r += __popcll(m[q]); }
+        }
     }
 }
 

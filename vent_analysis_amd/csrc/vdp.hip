@@ -275,7 +275,8 @@ __global__ void __launch_bounds__(VS_TPB) k_sort_vol(uint32_t *__restrict__ k0,
     __shared__ uint32_t s_wc[VS_WAVES][256]; // per-wave digit counts -> per-wave digit offsets
     __shared__ uint32_t s_run[256];          // keys of each digit placed by earlier chunks
     __shared__ uint32_t s_tot[256], s_cst[256], s_wsum[4];   // chunk digit totals / starts
-    __shared__ uint32_t s_stage[VS_CHUNK];   // the chunk in digit order
+    __shared__ uint32_t s_stage[VS_CHUNK + 1];   // the chunk in digit order (+ a slot for invalid keys)
+    __shared__ uint32_t s_off[256];              // digit d's output position minus its chunk-local start
     const int64_t b = blockIdx.x;
     const int64_t n = sc[b].n_mask;
     if (n <= 1) return;
@@ -393,23 +394,26 @@ __global__ void __launch_bounds__(VS_TPB) k_sort_vol(uint32_t *__restrict__ k0,
                 uint32_t pre = 0;
                 for (int ww = 0; ww < w; ++ww) pre += s_wsum[ww];
                 s_cst[t] += pre;        // chunk-local start of digit t
+                s_off[t] = s_hist[p][t] + s_run[t] - s_cst[t];
             }
             __syncthreads();
             VS_STAMP(3);
+            // stage at the chunk-local sorted position; branch-free (an invalid key goes to the spare
+            // slot), so the rows' LDS reads issue together instead of one row's after another's
 #pragma unroll
-            for (int r = 0; r < VS_KPT; ++r) {   // stage at the chunk-local sorted position
-                if (rank[r] == 0xffffffffu) continue;
+            for (int r = 0; r < VS_KPT; ++r) {
                 const uint32_t d = (key[r] >> shift) & 255u;
-                s_stage[s_cst[d] + s_wc[w][d] + rank[r]] = key[r];
+                rank[r] = rank[r] == 0xffffffffu ? (uint32_t)VS_CHUNK : s_cst[d] + s_wc[w][d] + rank[r];
             }
+#pragma unroll
+            for (int r = 0; r < VS_KPT; ++r) s_stage[rank[r]] = key[r];
             __syncthreads();
             VS_STAMP(4);
             // write out in staged order: equal digits are consecutive, so are their targets
             const int cn = (int)(n - c0 < VS_CHUNK ? n - c0 : VS_CHUNK);
             for (int q = t; q < cn; q += VS_TPB) {
                 const uint32_t kk = s_stage[q];
-                const uint32_t d = (kk >> shift) & 255u;
-                kout[s_hist[p][d] + s_run[d] + ((uint32_t)q - s_cst[d])] = kk;
+                kout[s_off[(kk >> shift) & 255u] + (uint32_t)q] = kk;
             }
             __syncthreads();
             VS_STAMP(5);
