@@ -30,7 +30,9 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_status_strings():
     L = _lib.lib()
-    assert L.vh_abi_version() == 8
+    assert L.vh_abi_version() == 8 == _lib.ABI_VERSION
+    hdr = open(os.path.join(os.path.dirname(__file__), "..", "include", "vent_hip.h")).read()
+    assert "#define VH_ABI_VERSION %d" % _lib.ABI_VERSION in hdr   # shim, header and library agree
     assert L.vh_status_string(0) == b"ok"
     assert b"maximum radius" in L.vh_status_string(_lib.VH_ERR_MAXRADIUS)
 

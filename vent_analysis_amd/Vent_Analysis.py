@@ -249,7 +249,12 @@ class Vent_Analysis:
         Returns float32 like sitk.GetArrayFromImage."""
         m = np.asarray(mask).astype(np.float32)
         m = ((m >= 1) & (m < 2)).astype(np.uint8)   # sitk.Cast(..., UInt8) == label 1 (:323-327)
-        if not m.any():   # empty label set: ITK's N4 leaves the image unchanged (calculate_VDP)
+        if not m.any():
+            # Empty label set (e.g. a 0/255 mask): no voxel to fit.  Returned as the image unchanged,
+            # which is what ITK's N4 computes when its fit has no points (an all-zero field).
+            # PARITY UNPINNED: SimpleITK is absent, so neither that output nor ITK's iteration
+            # counts on an empty label set are checked against the reference.  n4_iterations is
+            # the sentinel [0, 0, 0, 0] = "N4 not run", not a claim about ITK's counts.
             self.n4_iterations = [0, 0, 0, 0]
             return np.asarray(HPvent, dtype=np.float32).copy()
         out, its, _ = _lib.n4(np.asarray(HPvent, dtype=np.float32), m, device=self.device)

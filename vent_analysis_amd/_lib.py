@@ -104,6 +104,7 @@ _SIGS = {
     "vh_comm_destroy": ([_P], ct.c_int),
 }
 EXPORTED = tuple(_SIGS)
+ABI_VERSION = 8   # include/vent_hip.h VH_ABI_VERSION
 
 _lib = None
 _lock = threading.RLock()
@@ -123,6 +124,10 @@ def lib():
                     f = getattr(L, name)
                     f.argtypes = args
                     f.restype = res
+                v = L.vh_abi_version()
+                if v != ABI_VERSION:   # a stale build: its structs and signatures differ
+                    raise ImportError(f"{LIB_PATH} has ABI version {v}, this shim needs "
+                                      f"{ABI_VERSION}: rebuild it (`python __graft_entry__.py build`)")
                 _lib = L
     return _lib
 
