@@ -962,9 +962,13 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_hred(const uint64_t *hpart, const
 __global__ void __launch_bounds__(VH_TPB) k_n4_emap(const uint64_t *hpart, const int32_t *cp,
                                                    const double2 *tw, int bins, float fwhm,
                                                    float noise, const N4State *st, float *Eout,
-                                                   int64_t vol0, const uint64_t *hred) {
+                                                   int64_t vol0, const uint64_t *hred,
+                                                   const int32_t *nactive, int32_t *hflag) {
     __shared__ double2 V[VH_FFT_P], F[VH_FFT_P], U[VH_FFT_P], NUM[VH_FFT_P], DEN[VH_FFT_P],
         TMP[VH_FFT_P], TMP2[VH_FFT_P], TW[VH_FFT_P / 2];
+    // the iteration's active count (k_n4_ctrl's atomic sum) into the host's page-locked flag: the
+    // host reads it after the event behind this launch (a 4-byte D2H ran as a 10 us blit kernel)
+    if (blockIdx.x == 0 && threadIdx.x == 0) *hflag = *nactive;
     const int64_t b = vol0 + blockIdx.x;
     if (!st[b].active) return;
     const int P = VH_FFT_P, off = (P - bins) / 2;
@@ -1143,17 +1147,21 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_fit_clear(unsigned long long *num
     if (e < 2 * nlat) numfix[2 * b * lat_cap + e] = 0ull;
 }
 
-// MODE 1: den = fixed-point sum; MODE 0: phi = num / den (0 where den == 0), lattice += phi (S5)
+// MODE 1: den = fixed-point sum; MODE 0: phi = num / den (0 where den == 0), lattice += phi (S5).
+// The fixed-point accumulators are zeroed once read, so the next fit starts from zero without a
+// clearing launch (k_n4_fit_clear runs once per level, before the denominators' fit).
 template <int MODE>
-__global__ void __launch_bounds__(VH_TPB) k_n4_latupd(const unsigned long long *numfix, float *lat,
+__global__ void __launch_bounds__(VH_TPB) k_n4_latupd(unsigned long long *numfix, float *lat,
                                                      double *den, int64_t lat_cap, int64_t nlat,
                                                      const N4State *st, int64_t vol0) {
     const int64_t b = vol0 + blockIdx.x;
     if (MODE == 0 && !st[b].active) return;
     const int64_t e = blockIdx.y * (int64_t)VH_TPB + threadIdx.x;
     if (e >= nlat) return;
-    const unsigned long long *nf = numfix + 2 * (b * lat_cap + e);
+    unsigned long long *nf = numfix + 2 * (b * lat_cap + e);
     const double v = fix128_get(nf, nf + 1);
+    nf[0] = 0ull;
+    nf[1] = 0ull;
     if (MODE == 1) {
         den[b * lat_cap + e] = v;
     } else {
@@ -1194,17 +1202,21 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_T(const double *P1, int64_t q2_ca
                                                 float *T, int64_t tbuf, int64_t tcap, int64_t vol0) {
     const int64_t b = vol0 + blockIdx.y;
     if (!st[b].active) return;
+    // one thread per (column, control row): a thread walking its column's ncx rows waited for
+    // each row's loads in turn (18 us per launch at config 2)
     const int64_t CZ = C * Z;
-    const int64_t col = blockIdx.x * (int64_t)VH_TPB + threadIdx.x;
-    if (col >= CZ) return;
+    const int ncx = lv.ax[0].ncp;
+    const int64_t e = blockIdx.x * (int64_t)VH_TPB + threadIdx.x;
+    if (e >= CZ * ncx) return;
+    const int64_t col = e / ncx;
+    const int i = (int)(e - col * ncx);
     const int64_t y = col / Z, z = col % Z;
     const int ncy = lv.ax[1].ncp;
     const int by = lv.ax[1].base[y];
     const float4 wy = *reinterpret_cast<const float4 *>(lv.ax[1].w + 4 * y);
     const double *p1 = P1 + b * q2_cap;
-    const int ncx = lv.ax[0].ncp;
-    float *t = T + (st[b].tlast ^ 1) * tbuf + b * tcap + col * ncx;   // [col][ncx]: one 16-B load per voxel
-    for (int i = 0; i < ncx; ++i) t[i] = (float)col_T(p1, i, ncy, Z, by, wy, z);
+    float *t = T + (st[b].tlast ^ 1) * tbuf + b * tcap;   // [col][ncx]: one 16-B load per voxel
+    t[e] = (float)col_T(p1, i, ncy, Z, by, wy, z);
 }
 
 // Evaluate the new field at masked voxels: B_new and U = L0 - B_new (compact), the convergence
@@ -2173,7 +2185,6 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
     hipStream_t st = b->stream;
     const int64_t ntiles = b->n4_tiles;
     const int32_t ch0 = hcp[vol0], nch = hcp[vol0 + ns] - hcp[vol0];
-    const dim3 cg((unsigned)((b->CZ + VH_TPB - 1) / VH_TPB), (unsigned)ns);
     const int rsh = b->rsh;
     const int bins = prm.n_bins;
     const int cm = prm.conv_mode;
@@ -2185,7 +2196,9 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
     std::vector<hipEvent_t> evs;
     std::vector<int> ev_slot;   // iteration slot (d_nactive / h_flags index) behind each event
     if (!b->h_flags) HIP_TRY(hipHostMalloc((void **)&b->h_flags, sizeof(int32_t) * 1024));
-    int32_t *hflag = b->h_flags;
+    volatile int32_t *hflag = b->h_flags;   // written by k_n4_emap through its device mapping
+    int32_t *dflag = nullptr;
+    HIP_TRY(hipHostGetDevicePointer((void **)&dflag, b->h_flags, 0));
     // studies with many chunks: their chunk histograms are summed in slices first (k_n4_hred)
     int32_t max_ch = 0;
     for (int64_t v = vol0; v < vol0 + ns; ++v) max_ch = std::max(max_ch, hcp[v + 1] - hcp[v]);
@@ -2290,13 +2303,6 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
                     b->d_st, b->d_cpart, b->d_cp, b->d_sc, cm, L, it, prm.conv_threshold, bins, vol0,
                     b->d_nactive + gi, U, b->d_colbits, b->d_rowstart, b->R, b->CZ, b->VS, ntiles);
                 VH_CHECK_LAUNCH();
-                HIP_TRY(hipMemcpyAsync(hflag + (gi % 1024), b->d_nactive + gi, sizeof(int32_t),
-                                       hipMemcpyDeviceToHost, st));
-                hipEvent_t ev;
-                HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-                evs.push_back(ev);
-                ev_slot.push_back(gi);
-                HIP_TRY(hipEventRecord(ev, st));
                 if (nch > 0) {
                     ScopedKTimer tm(b, "n4_hist", 0.0);
                     k_n4_hist<<<(unsigned)nch, VH_TPB, 0, st>>>(U, b->d_cp, b->d_cvol, b->d_sc, b->VS,
@@ -2310,12 +2316,18 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
                 }
                 k_n4_emap<<<(unsigned)ns, VH_TPB, 0, st>>>(b->d_hpart, b->d_cp, b->d_twiddle, bins,
                                                            prm.fwhm, prm.wiener_noise, b->d_st,
-                                                           b->d_E, vol0, hred);
+                                                           b->d_E, vol0, hred, b->d_nactive + gi,
+                                                           dflag + (gi % 1024));
                 VH_CHECK_LAUNCH();
                 {
+                    hipEvent_t ev;
+                    HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+                    evs.push_back(ev);
+                    ev_slot.push_back(gi);
+                    HIP_TRY(hipEventRecord(ev, st));
+                }
+                {
                     ScopedKTimer tm(b, "n4_fit", 0.0);
-                    k_n4_fit_clear<0><<<zg, VH_TPB, 0, st>>>(b->d_numfix, b->lat_cap, nlat, b->d_st, vol0);
-                    VH_CHECK_LAUNCH();
                     k_n4_fit_items<0><<<fg, FIT_WAVES * 64, fit_lds, st>>>(
                         U, b->d_rowstart, b->d_rowmask, b->d_sc, (int)b->R, (int)b->C, (int)b->Z,
                         b->VS, (int)ntiles, nslots, bins, b->d_st, b->d_E, lv, rowcap, FIT_NB,
@@ -2330,7 +2342,7 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
                     k_n4_P1<<<pg, VH_TPB, 0, st>>>(b->d_lat, b->lat_cap, b->d_P1, b->q2_cap, b->Z,
                                                    b->d_st, lv, vol0);
                     VH_CHECK_LAUNCH();
-                    k_n4_T<<<cg, VH_TPB, 0, st>>>(b->d_P1, b->q2_cap, b->C, b->Z, lv, b->d_st,
+                    k_n4_T<<<dim3((unsigned)((b->CZ * ncx + VH_TPB - 1) / VH_TPB), (unsigned)ns), VH_TPB, 0, st>>>(b->d_P1, b->q2_cap, b->C, b->Z, lv, b->d_st,
                                                   b->d_T, b->nb * b->t_cap, b->t_cap, vol0);
                     VH_CHECK_LAUNCH();
                 }
