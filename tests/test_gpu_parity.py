@@ -584,6 +584,30 @@ def test_kmeans_global_tile_prefix_vs_oracle():
     assert np.float32(res[0].p99) == s[int(len(s) * 0.99)]
 
 
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 63, 64, 65, 127, 129, 4095, 4097, 262143, 262144, 262145,
+                               300000])
+def test_kmeans_one_wave_kernel_sizes(n, monkeypatch):
+    """k_kmeans_s (volumes of up to 2^19 voxels) at masked counts around its 64-key tiles, its
+    192-key windows and its sample stride (one sample per tile up to 2^18 keys, per two tiles above):
+    the partition and the centres against the oracle's Lloyd run, and against the multi-wave
+    k_kmeans on the same data (VH_KM_OLD=1)."""
+    R, C, Z = 128, 128, 32   # V = 2^19
+    rng = np.random.default_rng(1000 + n)
+    X = (rng.gamma(4.0, 50.0, size=(R, C, Z)) + 1.0).astype(np.float32)
+    M = np.zeros(R * C * Z, np.uint8)
+    M[rng.choice(R * C * Z, n, replace=False)] = 1
+    M = M.reshape(R, C, Z)
+    vox = (1.5, 1.5, 10.0)
+    res = _lib.vdp(X, M, vox)[3]
+    counts, centres, _ = O.kmeans_1d_sorted(np.sort(X[M > 0]))
+    assert int(res[0].n_km0) == O.kmeans_low_count(counts)
+    assert np.allclose(list(res[0].km_centres), centres, rtol=1e-12)
+    monkeypatch.setenv("VH_KM_OLD", "1")
+    old = _lib.vdp(X, M, vox)[3]
+    assert int(old[0].n_km0) == int(res[0].n_km0)
+    assert np.allclose(list(old[0].km_centres), list(res[0].km_centres), rtol=1e-12)
+
+
 def test_empty_mask_volume_in_batch():
     """A study with an empty mask must not disturb its neighbours; the class raises IndexError
     like the reference's sorted-list indexing (Vent_Analysis.py:255)."""
