@@ -983,6 +983,35 @@ def test_sorted_statistics_adversarial(kind):
     assert np.array_equal(h, exp_h)
 
 
+def test_cohort_rows_around_the_sample_size():
+    """k_cohort_search's rows for masked counts below, at and above its 4096-key LDS sample (one
+    sample per key below it) and a count large enough that each bin edge's search spans several
+    keys, in one batch; summed by k_cohort_sum against numpy's histogram of p99-normalised values."""
+    sizes = [1, 100, 4095, 4096, 4097, 50000]
+    R, C, Z = 64, 64, 16
+    rng = np.random.default_rng(31)
+    hp = (rng.gamma(3.0, 40.0, size=(len(sizes), R, C, Z)) + 0.5).astype(np.float32)
+    mk = np.zeros((len(sizes), R * C * Z), np.uint8)
+    for b, n in enumerate(sizes):
+        mk[b, rng.choice(R * C * Z, n, replace=False)] = 1
+    mk = mk.reshape(len(sizes), R, C, Z)
+    B = _lib.Batch(R, C, Z, len(sizes))
+    B.upload(hp, mk)
+    B.run(B.options(do_n4=False, vox=(1.5, 1.5, 10.0), do_cohort=True))
+    res = B.download()[4]
+    h = B.cohort_hist()
+    B.close()
+    exp_h = np.zeros(_lib.COHORT_BINS, np.uint64)
+    for b in range(len(sizes)):
+        s = np.sort(hp[b][mk[b] > 0])
+        assert np.float32(res[b].p99) == s[int(len(s) * 0.99)]
+        nv = (hp[b] / np.float32(res[b].p99)).astype(np.float32)[mk[b] > 0]
+        sel = (nv >= 0) & (nv < np.float32(1.5))
+        bi = np.minimum((nv[sel] * np.float32(_lib.COHORT_BINS / 1.5)).astype(np.int64), 1023)
+        exp_h += np.bincount(bi, minlength=_lib.COHORT_BINS).astype(np.uint64)
+    assert np.array_equal(h, exp_h)
+
+
 # ---- rendering after the hot path (SURVEY section 8f rank 3; oracle parity unpinned) -----------
 def _render_case(R, C, Z, seed):
     rng = np.random.default_rng(seed)
