@@ -503,6 +503,75 @@ void n4o_pc_sig_bound(const float *d, int64_t n, int nb, double *lo, float *sig_
     *mu_out = mu;
 }
 
+/* The early certified decision (n4_shared.h pcw_run, PC_PRE): the same bound from the exact running
+ * mean, block by block as the GPU forms it (nb blocks, float reciprocals, the same margins).  Returns
+ * lo (a lower bound of ITK's float sig), muhi (an upper bound of its float mean) and ok (every p in
+ * (0.5, 1.9), where the bound holds); *dmax_out = max over k of |mu_k - m_k| / D_k, the float mean's
+ * observed distance from the exact one over the bound D_k = 2^-24 (k + 3) (1 + 2^-20) (must be <= 1).
+ * Also ITK's float (mu, sig) for the check.  Test infrastructure (tests/test_n4_oracle.py). */
+void n4o_pc_pre_bound(const float *d, int64_t n, int nb, double *lo_out, float *muhi_out, int *ok_out,
+                      double *dmax_out, float *sig_out, float *mu_out)
+{
+    const int64_t L = n / nb, rem = n % nb;
+    float *p = (float *)malloc(sizeof(float) * (size_t)(n > 0 ? n : 1));
+    int ok = 1;
+    float pmax = 0.0f;
+    for (int64_t k = 0; k < n; ++k) {
+        p[k] = expf_cr(d[k]);
+        if (!(p[k] < 1.9f && p[k] > 0.5f)) ok = 0;
+        if (p[k] > pmax) pmax = p[k];
+    }
+    const double Mx = (double)pmax * (1.0 + 0x1p-24 * ((double)n + 3.0)) * (1.0 + 0x1p-20);
+    const double cD = 0x1p-25 * Mx * (1.0 + 0x1p-20);
+    /* ITK's float recurrence and the observed drift from the exact running mean */
+    float mu = 0.0f, sig = 0.0f, N = 0.0f;
+    double P = 0.0, dmax = 0.0;
+    for (int64_t k = 1; k <= n; ++k) {
+        const float pk = p[k - 1];
+        N = (float)((double)N + 1.0);
+        const double Nd = (double)N;
+        if (Nd > 1.0) {
+            const float q = pk - mu;
+            sig = (float)((double)sig + ((double)(q * q) * (Nd - 1.0)) / Nd);
+        }
+        mu = (float)((double)mu * (1.0 - 1.0 / Nd) + (double)(pk / N));
+        P += (double)pk - 1.0;
+        const double mk = 1.0 + P / (double)k;
+        const double r = fabs((double)mu - mk) / (cD * ((double)k + 3.0));
+        if (r > dmax) dmax = r;
+    }
+    /* the GPU's bound: blocks of L (+1) steps, exact prefix of (p - 1), float reciprocals */
+    double tot = 0.0, Pk = 0.0;
+    int64_t k = 1;
+    for (int j = 0; j < nb; ++j) {
+        const int64_t len = L + (j < rem ? 1 : 0), k0 = k;
+        double acc = 0.0;
+        for (int64_t s = 0; s < len; ++s, ++k) {
+            const double pd = (double)p[k - 1];
+            if (k >= 2) {
+                const double r = (double)(1.0f / (float)(k - 1));
+                const double m = fma(Pk, r, 1.0);
+                const double eps = fabs(m - 1.0) * 0x1p-21 + 0x1p-50;
+                const double a = fabs(pd - m) - cD * (double)(k + 2) - eps;
+                if (a > 0.0) acc = fma(a, a, acc);
+            }
+            Pk += pd - 1.0;
+        }
+        tot += acc * (1.0 - 1.0 / fmax((double)k0, 2.0));
+    }
+    *lo_out = tot * (1.0 - ((double)n + 8.0) * 0x1p-24 - 0x1p-40);
+    const double mn = 1.0 + Pk / (double)n;
+    const double hi = mn + cD * ((double)n + 3.0) + fabs(mn - 1.0) * 0x1p-50 + 0x1p-50;
+    float f = (float)hi;
+    if ((double)f < hi) f = nextafterf(f, INFINITY);
+    *muhi_out = f;
+    *ok_out = ok;
+    *dmax_out = dmax;
+    *sig_out = sig;
+    *mu_out = mu;
+    free(p);
+}
+
 /* S7x (conv_mode 1): the coefficient of variation ITK intends, evaluated exactly enough that
  * order does not matter: d' = expm1c(d), CoV from sum d', sum d'^2 in double */
 static double conv_exact(const float *d, int64_t n)

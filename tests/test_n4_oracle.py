@@ -132,6 +132,48 @@ def _conv(mu, sig, n):
     return np.float32(sd / np.float32(mu))
 
 
+@pytest.mark.parametrize("shape,seed,nb,vary", [((64, 64, 16), 0, 1024, False),
+                                                ((128, 128, 24), 17, 1024, True),
+                                                ((40, 36, 9), 5, 64, False)])
+def test_pc_early_decision_bound(tmp_path, monkeypatch, shape, seed, nb, vary):
+    """PC's early certified decision (n4_shared.h pcw_run, PC_PRE), restated by
+    oracle/n4_oracle.c n4o_pc_pre_bound: on every iteration's d sequence of an oracle N4 run the
+    float mean stays within D_k of the exact running mean (the drift bound the decision rests on),
+    the bound lo never exceeds ITK's float sig, muhi is at or above its float mean, so the measure
+    at (RD(lo), muhi) never exceeds the true one; and it decides some iterations at the default
+    threshold (those well above it)."""
+    import ctypes as ct
+    dump = tmp_path / "d.bin"
+    monkeypatch.setenv("N4_DUMP_D", str(dump))
+    X, M = synth_volume(*shape, seed, vary=vary)
+    native.n4(X, M)
+    raw = dump.read_bytes()
+    L = native.lib()
+    L.n4o_pc_pre_bound.restype = None
+    off = its = decided = 0
+    while off < len(raw):
+        n = int(np.frombuffer(raw, np.int64, 1, off)[0])
+        d = np.frombuffer(raw, np.float32, n, off + 8).copy()
+        off += 8 + 4 * n
+        lo, muhi, ok, dmax = ct.c_double(), ct.c_float(), ct.c_int(), ct.c_double()
+        sig, mu = ct.c_float(), ct.c_float()
+        L.n4o_pc_pre_bound(d.ctypes.data_as(ct.POINTER(ct.c_float)), ct.c_int64(n), ct.c_int(nb),
+                           ct.byref(lo), ct.byref(muhi), ct.byref(ok), ct.byref(dmax), ct.byref(sig),
+                           ct.byref(mu))
+        assert ok.value == 1
+        assert dmax.value <= 1.0, (its, dmax.value)          # |mu_k - m_k| <= D_k at every step
+        assert lo.value <= sig.value, (its, lo.value, sig.value)
+        assert muhi.value >= mu.value
+        sl = np.float32(lo.value)
+        if np.float64(sl) > lo.value:
+            sl = np.nextafter(sl, np.float32(0))
+        if lo.value > 0.0:
+            assert _conv(muhi.value, sl, n) <= _conv(mu.value, sig.value, n)
+            decided += _conv(muhi.value, sl, n) > np.float32(0.001)
+        its += 1
+    assert its >= 4 and decided >= 1
+
+
 @pytest.mark.parametrize("shape,seed,nb", [((64, 64, 16), 0, 1024), ((96, 80, 12), 3, 1024),
                                            ((40, 36, 9), 5, 64)])
 def test_pc_sig_lower_bound(tmp_path, monkeypatch, shape, seed, nb):

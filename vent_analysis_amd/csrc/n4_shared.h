@@ -1693,6 +1693,9 @@ static_assert(PC_APASS >= 1 && PC_APASS <= 2, "PC_APASS: 1 or 2 phase-A stages (
 #ifndef PC_S12F
 #define PC_S12F 1   // the guesses' block sums in float (r4ar: 18.87 vs 18.93 ms per isolated launch)
 #endif
+#ifndef PC_PRE
+#define PC_PRE 1    // early certified decision from the exact running mean (pcw_run, round 5)
+#endif
 template <int NL>
 __host__ __device__ constexpr size_t pcw_lds_bytes() {
     return sizeof(PcShared<NL>) > sizeof(float) * PC_G0 * (NL + 8) ? sizeof(PcShared<NL>)
@@ -1702,7 +1705,7 @@ template <int NL, bool PEXP = false, class LoadD>
 __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n, PcShared<NL> &S,
                                                   ChainState &ch, int req, double *tbuf, int tcap,
                                                   float skip_thresh = 0.0f, float *drift = nullptr,
-                                                  bool drift_in = false) {
+                                                  bool drift_in = false, bool try_pre = false) {
     const int tid = threadIdx.x;
     const PcMap m = pc_map(n, NL);
     const uint32_t j = (uint32_t)tid, len = pc_len(m, j), k0 = pc_k0(m, j);
@@ -1723,10 +1726,13 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
     static_assert(sizeof(float) * G0 * TS <= pcw_lds_bytes<NL>(), "pass-0 transpose buffer");
     float *const T0 = reinterpret_cast<float *>(&S);
     const uint32_t lmax = m.L + (m.rem ? 1u : 0u);
+    // s1 = sum of (p - 1) in double: exact (every p - 1 is a multiple of 2^-24 below 2^-4 in size
+    // wherever the early decision uses it, so any order of the sums is exact); s2 seeds the guesses
+    double s1 = 0.0;
 #if PC_S12F   // the guesses' block sums: they only seed the rounds (the result is exact either way)
-    float s1 = 0.0f, s2 = 0.0f;
+    float s2 = 0.0f;
 #else
-    double s1 = 0.0, s2 = 0.0;
+    double s2 = 0.0;
 #endif
     // certified-frozen start intervals: the block's p range; the bound N h is taken at the block's
     // first step, where N is smallest (N = min(k, NMAX) never decreases), so [max p - N0 h,
@@ -1767,13 +1773,12 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
                 const float p = PEXP ? T0[i * TS + j] : PC_EXPS ? expf_crs(T0[i * TS + j]) : expf_cr(T0[i * TS + j]);
 #endif
                 P[(size_t)(g0 + i) * NL + j] = p;
+                s1 += (double)p - 1.0;
 #if PC_S12F
                 const float e = p - 1.0f;
-                s1 += e;
                 s2 = fmaf(e, e, s2);
 #else
                 const double e = (double)p - 1.0;
-                s1 += e;
                 s2 = fma(e, e, s2);
 #endif
                 pmax = fmaxf(pmax, p);
@@ -1794,6 +1799,7 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
         S.xdone = 0;
         S.nfrz = 0;
         S.nfr = 0;
+        S.xslots = 0;   // (the early decision's max p before PCX takes the field over)
     }
 #ifdef PC_PROF
     if (tid < 32) S.pchg[tid] = S.pwav[tid] = 0;
@@ -1810,8 +1816,78 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
                               ok && fa2 <= fb2 ? f_up(fa2) : inf, ok && fa2 <= fb2 ? f_dn(fb2) : -inf);
     }
     __syncthreads();
-    double gd;
-    pcw_guess<NL>(S, m, gd, dr);
+    bool pre = false;   // decided from the exact running mean: no rounds at all (below)
+#if PC_PRE
+    if (try_pre && skip_thresh > 0.0f && n > 1 && n < ((int64_t)1 << 24)) {
+        // Early certified decision (round 5).  The float mean's distance from the exact running mean
+        // m_k is bounded without running the recurrence: a step's rounding errors (float division p/N,
+        // the double products, the final float rounding) are at most 2^-24 (|mu_k| + |p_k| / k)(1 +
+        // 2^-26), and the recurrence damps older errors by (1 - 1/k), so |mu_k - m_k| <= sum_i
+        // |delta_i| i / k <= D_k = 2^-25 M (k + 3)(1 + 2^-20) with M >= |mu_i|, |p_i| for every i
+        // (below; every p in (0.5, 1.9), which also keeps the sums of p - 1 exact).  Then |q_k| >= (|p_k - m_(k-1)| - D_(k-1))(1 - 2^-24), and
+        // with the bounds of the certified decision below (t_k >= q^2 (1 - 1/N)(1 - 2^-24)(1 -
+        // 2^-52)^2, S >= (1 - n 2^-24) sum t_k) lo = sum over blocks of (1 - 1/max(k0, 2)) sum_k
+        // max(0, |p_k - m_(k-1)| - D_(k-1) - eps_k)^2 (1 - (n + 8) 2^-24) bounds ITK's float sig
+        // from below, and mu_n <= m_n + D_n.  ITK's measure is monotone in both, so a measure above
+        // the threshold at (RD(lo), RU(m_n + D_n)) proves the iteration goes on.  It decides the
+        // iterations whose measure is well above the threshold (about a quarter on the bench
+        // studies), without a single round; the caller tries it only where the previous measure
+        // was (try_pre).  m_(k-1) = 1 + P_(k-1) / (k - 1) from the exact prefix P of (p - 1), the
+        // quotient by a float reciprocal: eps_k = |m - 1| 2^-21 + 2^-50 covers its error.
+        double dmx, nbad;
+        const bool okb = len == 0u || (pmax < 1.9f && pmin > 0.5f);
+        if (len > 0u) atomicMax(&S.xslots, __float_as_int(pmax));   // positive floats order as ints
+        pcw_scan<NL>(S, 1.0, S.s1(j), okb ? 0.0 : 1.0, dmx, nbad);   // exact prefix of (p - 1); its
+        // barrier also completes the max: M = max p (the exact mean and, within D, the float mean
+        // never exceed it)
+        // (|mu_i| <= max p + D_i: M = max p / (1 - 2^-25 (n + 3)(1 + 2^-20)) <= max p (1 + 2^-24 (n + 3)))
+        const double Mx = (double)__int_as_float(S.xslots) * (1.0 + 0x1p-24 * ((double)n + 3.0)) * (1.0 + 0x1p-20);
+        double Pk = dmx, acc = 0.0;
+        const double cD = 0x1p-25 * Mx * (1.0 + 0x1p-20);   // D_k = cD (k + 3)
+        for (uint32_t s0 = 0; s0 < len; s0 += 8) {   // 8 loads in flight (unconditional, clamped)
+            float pv[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) pv[q] = P[(size_t)(s0 + q < len ? s0 + q : len - 1u) * NL + j];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const uint32_t k = k0 + s0 + (uint32_t)q;   // 1-based step index of this value
+                const double p = (double)pv[q];
+                const bool in = s0 + (uint32_t)q < len;
+                if (in && k >= 2u) {
+                    const double r = (double)__frcp_rn((float)(k - 1u));
+                    const double mk = fma(Pk, r, 1.0);
+                    const double eps = fabs(mk - 1.0) * 0x1p-21 + 0x1p-50;
+                    const double a = fabs(p - mk) - cD * (double)(k + 2u) - eps;
+                    acc = a > 0.0 ? fma(a, a, acc) : acc;
+                }
+                Pk += in ? p - 1.0 : 0.0;
+            }
+        }
+        const double wown = acc * (1.0 - 1.0 / fmax((double)k0, 2.0));
+        double wpre, unused;
+        pcw_scan<NL>(S, 1.0, wown, 0.0, wpre, unused);
+        if (tid == NL - 1) {
+            const double f = 1.0 - ((double)n + 8.0) * 0x1p-24 - 0x1p-40;
+            const double lo = (wpre + wown) * f;
+            const bool allok = nbad + (okb ? 0.0 : 1.0) == 0.0;   // every block's p in (0.5, 1.9)
+            float sl = (float)lo;
+            if ((double)sl > lo && sl > 0.0f) sl = __uint_as_float(__float_as_uint(sl) - 1u);
+            const double Pn = dmx + s1;                     // exact sum of (p - 1) over all n steps
+            const double mn = 1.0 + Pn / (double)n;         // m_n (one double division)
+            const float muh = f_up(mn + cD * ((double)n + 3.0) + fabs(mn - 1.0) * 0x1p-50 + 0x1p-50);
+            if (allok && f > 0.5 && lo > 0.0 && itk_conv(muh, sl, n) > skip_thresh) {
+                S.mu = muh;
+                S.sig = sl;
+                S.rounds = 0;
+                S.xdone = 4 * req + 1;
+            }
+        }
+        __syncthreads();
+        pre = S.xdone == 4 * req + 1;
+    }
+#endif
+    double gd = 0.0;
+    if (!pre) pcw_guess<NL>(S, m, gd, dr);
     __syncthreads();
 #ifdef PC_PROF
     c1 = clock64();
@@ -1824,8 +1900,8 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
     unsigned long long cblk = 0, cst[2] = {0, 0}, cbs[2] = {0, 0};
     int rst[2] = {0, 0};
 #endif
-    bool xs = false;   // sig finished exactly by PCX: no stage 1, no exact rounds
-    for (int pass = 0; pass < PC_APASS; ++pass) {
+    bool xs = pre;   // sig finished exactly by PCX (or decided early): no stage 1, no exact rounds
+    for (int pass = 0; pass < PC_APASS && !pre; ++pass) {
         if (pass == 1 && PC_XSIG && S.done == 4 * req) {   // stage 0 reached its fixed point
 #ifdef PC_PROF
             const unsigned long long cx0 = clock64();
@@ -1997,7 +2073,8 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
     // stage 0 reached its fixed point (xs): the block starts are the exact float trajectory's
     // (a study's first call, which reads no drift, always writes one: 0 when stage 0 stopped short,
     // so a later call never starts from another batch's or an unset value -- ADVICE r4)
-    if (drift && (xs || !drift_in)) drift[j] = xs ? (float)((double)S.b[j].gmu - gd) : 0.0f;
+    if (drift && !pre && (xs || !drift_in)) drift[j] = xs ? (float)((double)S.b[j].gmu - gd) : 0.0f;
+    if (drift && pre && !drift_in) drift[j] = 0.0f;   // (an early decision finds no block starts)
     if (tid == 0) {
         ch.mu = S.mu;
         ch.conv = itk_conv(S.mu, S.sig, n);

@@ -121,6 +121,7 @@ struct StudyMisc {
     ChainState ch;             // PC's result (conv of the last iteration)
     int32_t itn, uin;          // iterations of the level, U buffer of the last field
     int32_t pc_rounds, pc_fb;  // S7 by PC: rounds and serial fallbacks over all iterations
+    int32_t pc_pre;            // the last call decided early (PC_PRE): try again on the next one
 };
 
 // One level's axis tables staged in LDS.
@@ -641,6 +642,7 @@ __global__ void __launch_bounds__(ST_TPB, 4) k_n4_study(StudyArgs a) {
         M.uin = 0;
         M.pc_rounds = 0;
         M.pc_fb = 0;
+        M.pc_pre = 0;
     }
     if (wv == 0) find_first(a, b, fm, M);
     {   // item schedule: items by row count, largest first (ties by index), so the dynamic item
@@ -988,8 +990,10 @@ __global__ void __launch_bounds__(ST_TPB, 4) k_n4_study(StudyArgs a) {
                     pcw_run<ST_TPB, ST_EVAL_EXP>([=](int64_t r) { return Dr[r]; }, a.D + a.half + b * a.VS, n, PW, M.ch, itk,
                             reinterpret_cast<double *>(a.D + b * a.VS), (int)(a.VS / 2),
                             itk < a.lvs->max_iters[L] ? a.thresh : 0.0f,
-                            a.pcdrift ? a.pcdrift + (size_t)b * ST_TPB : nullptr, !(L == 0 && itk == 1));
+                            a.pcdrift ? a.pcdrift + (size_t)b * ST_TPB : nullptr, !(L == 0 && itk == 1),
+                            itk == 1 || M.pc_pre != 0);   // early decision: a level's first call, then while it decides
                     if (t == 0) {
+                        M.pc_pre = PW.xdone == 4 * itk + 1;
                         M.conv = (double)M.ch.conv;
                         M.pc_rounds += PW.rounds;
                         // serial fallbacks of the exact rounds (units), frozen-serial stage-0 closes (thousands)
