@@ -1392,9 +1392,14 @@ __global__ void __launch_bounds__(PC_TPB) k_n4_pcw(const float *D, const int32_t
     const int32_t *const pb = perm + b * VS;
     // D[b] (compact d) is free once pass 0 has read it: PCX's stored increments.  skip_thresh:
     // the certified "above the threshold" decision of pcw_run (0 at the level's last iteration)
+    // early decision (PC_PRE): a level's first call, then as long as it keeps deciding
     pcw_run<PC_TPB>([=](int64_t r) { return Db[pb[r]]; }, Pbuf + b * VS, sc[b].n_mask1, S, ch, 1,
-            reinterpret_cast<double *>(const_cast<float *>(Db)), (int)(VS / 2), skip_thresh);
-    if (threadIdx.x == 0) st[b].conv_w = ch.conv;
+            reinterpret_cast<double *>(const_cast<float *>(Db)), (int)(VS / 2), skip_thresh, nullptr,
+            false, st[b].iters == 1 || st[b].pc_pre != 0);
+    if (threadIdx.x == 0) {
+        st[b].conv_w = ch.conv;
+        st[b].pc_pre = S.xdone == 4 * 1 + 1;
+    }
 }
 
 // S7 by guess and verify over the whole GPU, for one large study (the sweep driver with a single

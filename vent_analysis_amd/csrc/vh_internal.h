@@ -106,6 +106,7 @@ struct N4State {
     uint64_t t_start, t_end;   // k_n4_study: device wall clock (wall_clock64) at the workgroup's start / end
     uint32_t hw_id, xcc_id;    // k_n4_study: where the workgroup ran (HW_REG_HW_ID / HW_REG_XCC_ID)
     int32_t pc_rounds, pc_fallbacks;   // k_n4_study: S7 guess-and-verify rounds / serial fallbacks, all iterations
+    int32_t pc_pre;            // k_n4_pcw: the last call decided early (PC_PRE): try again on the next one
 };
 
 // Per-axis, per-level B-spline tables (host-built, identical to oracle/n4_oracle.c).
