@@ -229,13 +229,19 @@ __global__ void __launch_bounds__(VH_TPB) k_gather(const float *__restrict__ n4,
     int64_t pos = b * V + colstart[b * CZ + col];
     const float *p = n4 + b * V + col;
     const uint8_t *m = mask + b * V + col;
-    for (int64_t x0 = lo; x0 <= hi; x0 += 8) {   // 8 rows of loads in flight
+    for (int64_t x0 = lo; x0 <= hi; x0 += 8) {   // 8 rows of mask and value loads in flight
         uint8_t mk[8];
         float v[8];
+        // unconditional loads at a clamped row (a guarded load compiles to a branch that waits for
+        // it: the mask-then-value chain took 0.55 ms per batch)
 #pragma unroll
-        for (int k = 0; k < 8; ++k) mk[k] = x0 + k <= hi ? m[(x0 + k) * CZ] : 0;
+        for (int k = 0; k < 8; ++k) {
+            const int64_t x = x0 + k <= hi ? x0 + k : hi;
+            mk[k] = m[x * CZ];
+            v[k] = p[x * CZ];
+        }
 #pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = mk[k] ? p[(x0 + k) * CZ] : 0.0f;
+        for (int k = 0; k < 8; ++k) mk[k] = x0 + k <= hi ? mk[k] : 0;
 #pragma unroll
         for (int k = 0; k < 8; ++k)
             if (mk[k]) keys[pos++] = f2key(v[k]);
@@ -2082,9 +2088,12 @@ __global__ void __launch_bounds__(VH_TPB) k_snr(const float *__restrict__ hp,
         const float *a = hp + b * V + x0 * CZ + col;
         for (int i0 = 0; i0 < nr; i0 += 8) {   // 8 rows of loads in flight
             float v[8];
+            // unconditional loads at a clamped row, then the selection (a guarded load compiles to
+            // a branch that waits for it; nearly every row is signal or noise anyway)
 #pragma unroll
-            for (int k = 0; k < 8; ++k)
-                v[k] = (i0 + k < nr && ((need >> (i0 + k)) & 1u)) ? a[(int64_t)(i0 + k) * CZ] : 0.0f;
+            for (int k = 0; k < 8; ++k) v[k] = a[(int64_t)(i0 + k < nr ? i0 + k : nr - 1) * CZ];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = (i0 + k < nr && ((need >> (i0 + k)) & 1u)) ? v[k] : 0.0f;
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 const int i = i0 + k;
