@@ -1529,10 +1529,11 @@ __global__ void __launch_bounds__(PC_TPB) k_n4_pcg(PcgArgs A) {
     for (uint32_t s0 = 0; s0 < len; s0 += 8) {
         int32_t pi[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) pi[i] = s0 + i < len ? A.perm[k0 - 1u + s0 + i] : 0;
+        for (int i = 0; i < 8; ++i)   // clamped, unconditional: the loads stay in flight together
+            pi[i] = A.perm[k0 - 1u + (s0 + i < len ? s0 + i : len - 1u)];
         float v[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = s0 + i < len ? Db[pi[i]] : 0.0f;
+        for (int i = 0; i < 8; ++i) v[i] = Db[pi[i]];
 #pragma unroll
         for (int i = 0; i < 8; ++i)
             if (s0 + i < len) {
@@ -1826,10 +1827,11 @@ __global__ void __launch_bounds__(PC_TPB) k_n4_pcg2(Pcg2Args A) {
     for (uint32_t s0 = 0; s0 < len; s0 += 8) {
         int32_t pi[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) pi[i] = s0 + i < len ? A.perm[k0 - 1u + s0 + i] : 0;
+        for (int i = 0; i < 8; ++i)   // clamped, unconditional: the loads stay in flight together
+            pi[i] = A.perm[k0 - 1u + (s0 + i < len ? s0 + i : len - 1u)];
         float v[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = s0 + i < len ? A.D[pi[i]] : 0.0f;
+        for (int i = 0; i < 8; ++i) v[i] = A.D[pi[i]];
 #pragma unroll
         for (int i = 0; i < 8; ++i)
             if (s0 + i < len) {
