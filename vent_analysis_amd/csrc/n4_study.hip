@@ -437,6 +437,9 @@ __device__ void eval_item(const Item &it, int item, int Z, int CZ, const TabV &T
 // strided passes below hit distinct LDS banks.  Only wave-local ordering is needed.
 // ---------------------------------------------------------------------------------------------
 #define ST_FFT_N (VH_FFT_P + VH_FFT_P / 8)   // padded slots of one transform
+#ifndef ST_WPAR
+#define ST_WPAR 1   // E-map: Wiener filter on all threads before the one-wave inverse (0: inside it)
+#endif
 __device__ __forceinline__ int fpad(int i) { return i + (i >> 3); }
 
 struct FftId {
@@ -864,6 +867,19 @@ __global__ void __launch_bounds__(ST_TPB, 4) k_n4_study(StudyArgs a) {
                     if (g.w < 2) wave_fft_lds(g.w ? F : V, TW, false, FftId(), FftId());
                     gsync(g, M);
                     ST_MARK(12);
+#if ST_WPAR
+                    // Wiener filter on every thread (the divisions would otherwise run 8 deep on
+                    // one wave); the same per-point arithmetic as the gather-side form below
+                    for (int i = g.t; i < P; i += g.n) {
+                        const double2 f = F[fpad(i)], v = V[fpad(i)];
+                        const double fa = f.x, fb = f.y;
+                        const double gg = fa / ((fa * fa - (-fb) * fb) + (double)a.noise);
+                        V[fpad(i)] = make_double2(v.x * gg, v.y * gg);
+                    }
+                    gsync(g, M);
+                    if (g.w == 0) {   // inverse, clamp and the moment series (last pass)
+                        wave_fft_lds(V, TW, true, FftId(),
+#else
                     if (g.w == 0) {   // Wiener filter (first pass), inverse, clamp and the moment series (last pass)
                         const double noise = (double)a.noise;
                         wave_fft_lds(V, TW, true,
@@ -873,6 +889,7 @@ __global__ void __launch_bounds__(ST_TPB, 4) k_n4_study(StudyArgs a) {
                                 const double gg = fa / ((fa * fa - (-fb) * fb) + noise);
                                 return make_double2(v.x * gg, v.y * gg);
                             },
+#endif
                             [=](int i, double2 v) {
                                 const double ur = v.x > 0.0 ? v.x : 0.0;
                                 const float c = bmin + ((float)i - (float)off) * slope;
