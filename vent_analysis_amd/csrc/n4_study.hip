@@ -438,7 +438,11 @@ __device__ void eval_item(const Item &it, int item, int Z, int CZ, const TabV &T
 // ---------------------------------------------------------------------------------------------
 #define ST_FFT_N (VH_FFT_P + VH_FFT_P / 8)   // padded slots of one transform
 #ifndef ST_WPAR
-#define ST_WPAR 1   // E-map: Wiener filter on all threads before the one-wave inverse (0: inside it)
+// E-map: the pointwise steps between the FFTs run on all threads, as passes of their own (3: the
+// Wiener filter, the clamp / moment series and the kernel product; 2: not the product; 1: only the
+// filter; 0: all inside the one- or two-wave FFTs' first / last passes, round 4).  Bit-identical
+// arithmetic; 3 is 5 % faster on the study kernel (DESIGN_LOG.md round 5).
+#define ST_WPAR 3
 #endif
 __device__ __forceinline__ int fpad(int i) { return i + (i >> 3); }
 
@@ -687,7 +691,7 @@ __global__ void __launch_bounds__(ST_TPB, 4) k_n4_study(StudyArgs a) {
         for (int e = t; e < nl0; e += ST_TPB) lat[e] = 0.0f;
     }
 #ifdef ST_PROF
-    unsigned long long st_prof[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_t0 = clock64();
+    unsigned long long st_prof[18] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_t0 = clock64();
     if (t == 0) M.fprof[0] = M.fprof[1] = M.fprof[2] = M.fprof[3] = 0ull;
     if (t == 0) M.sprof[0] = M.sprof[1] = M.sprof[2] = M.sprof[3] = 0ull;
 #endif
@@ -867,6 +871,12 @@ __global__ void __launch_bounds__(ST_TPB, 4) k_n4_study(StudyArgs a) {
                     if (g.w < 2) wave_fft_lds(g.w ? F : V, TW, false, FftId(), FftId());
                     gsync(g, M);
                     ST_MARK(12);
+                    const auto wpost = [=](int i, double2 v) {   // clamp; the moment series' points
+                        const double ur = v.x > 0.0 ? v.x : 0.0;
+                        const float c = bmin + ((float)i - (float)off) * slope;
+                        DEN[fpad(i)] = make_double2(ur, 0.0);
+                        return make_double2((double)c * ur, 0.0);
+                    };
 #if ST_WPAR
                     // Wiener filter on every thread (the divisions would otherwise run 8 deep on
                     // one wave); the same per-point arithmetic as the gather-side form below
@@ -877,8 +887,16 @@ __global__ void __launch_bounds__(ST_TPB, 4) k_n4_study(StudyArgs a) {
                         V[fpad(i)] = make_double2(v.x * gg, v.y * gg);
                     }
                     gsync(g, M);
-                    if (g.w == 0) {   // inverse, clamp and the moment series (last pass)
-                        wave_fft_lds(V, TW, true, FftId(),
+                    ST_MARK(16);
+#if ST_WPAR >= 2
+                    if (g.w == 0) wave_fft_lds(V, TW, true, FftId(), FftId());   // inverse
+                    ST_MARK(17);
+                    gsync(g, M);
+                    for (int i = g.t; i < P; i += g.n) V[fpad(i)] = wpost(i, V[fpad(i)]);
+#else
+                    if (g.w == 0) wave_fft_lds(V, TW, true, FftId(), wpost);   // inverse, clamp, series
+                    ST_MARK(17);
+#endif
 #else
                     if (g.w == 0) {   // Wiener filter (first pass), inverse, clamp and the moment series (last pass)
                         const double noise = (double)a.noise;
@@ -888,26 +906,34 @@ __global__ void __launch_bounds__(ST_TPB, 4) k_n4_study(StudyArgs a) {
                                 const double fa = f.x, fb = f.y;
                                 const double gg = fa / ((fa * fa - (-fb) * fb) + noise);
                                 return make_double2(v.x * gg, v.y * gg);
-                            },
-#endif
-                            [=](int i, double2 v) {
-                                const double ur = v.x > 0.0 ? v.x : 0.0;
-                                const float c = bmin + ((float)i - (float)off) * slope;
-                                DEN[fpad(i)] = make_double2(ur, 0.0);
-                                return make_double2((double)c * ur, 0.0);
-                            });
+                            }, wpost);
                     }
+#endif
                     gsync(g, M);
                     ST_MARK(13);
+                    const auto kmul = [=](int i, double2 v) {   // times the kernel's transform
+                        const double2 f = F[fpad(i)];
+                        const double fa = f.x, fb = f.y;
+                        return make_double2(v.x * fa - v.y * fb, v.x * fb + v.y * fa);
+                    };
+#if ST_WPAR >= 3
+                    // each series: forward; the product on every thread; inverse
+                    if (g.w < 2) wave_fft_lds(g.w ? DEN : V, TW, false, FftId(), FftId());
+                    gsync(g, M);
+                    for (int e = g.t; e < 2 * P; e += g.n) {
+                        double2 *const x = e < P ? V : DEN;
+                        const int i = e < P ? e : e - P;
+                        x[fpad(i)] = kmul(i, x[fpad(i)]);
+                    }
+                    gsync(g, M);
+                    if (g.w < 2) wave_fft_lds(g.w ? DEN : V, TW, true, FftId(), FftId());
+#else
                     if (g.w < 2) {   // each series: forward, times the kernel's transform (last pass), inverse
                         double2 *x = g.w ? DEN : V;
-                        wave_fft_lds(x, TW, false, FftId(), [=](int i, double2 v) {
-                            const double2 f = F[fpad(i)];
-                            const double fa = f.x, fb = f.y;
-                            return make_double2(v.x * fa - v.y * fb, v.x * fb + v.y * fa);
-                        });
+                        wave_fft_lds(x, TW, false, FftId(), kmul);
                         wave_fft_lds(x, TW, true, FftId(), FftId());
                     }
+#endif
                     gsync(g, M);
                     ST_MARK(14);
                     for (int i = g.t; i < bins; i += g.n) {
@@ -1068,11 +1094,13 @@ __global__ void __launch_bounds__(ST_TPB, 4) k_n4_study(StudyArgs a) {
         int its = 0;   // (st_pt is thread 0, the writer of iters_level)
         for (int q = 0; q < a.nlev; ++q) its += stb->iters_level[q];
         printf("ST_PROF b %d n %lld its %d den %llu ctrl %llu hist %llu emap %llu fit %llu latP1 %llu eval %llu "
-               "wait %llu level %llu exact %llu top %llu | emap: series %llu fwd %llu filter %llu conv %llu div %llu\n",
+               "wait %llu level %llu exact %llu top %llu | emap: series %llu fwd %llu filter %llu conv %llu div %llu"
+               " (filter: wiener %llu fft %llu sync %llu)\n",
                ST_PROF_B, (long long)n, its, st_prof[0], st_prof[1], st_prof[2],
                st_prof[3] + st_prof[11] + st_prof[12] + st_prof[13] + st_prof[14],
                st_prof[4], st_prof[5], st_prof[6], st_prof[7], st_prof[8], st_prof[9], st_prof[10],
-               st_prof[11], st_prof[12], st_prof[13], st_prof[14], st_prof[3]);
+               st_prof[11], st_prof[12], st_prof[13] + st_prof[16] + st_prof[17], st_prof[14], st_prof[3],
+               st_prof[16], st_prof[17], st_prof[13]);
         printf("ST_PROF fit: rows %llu push %llu contract %llu items %llu | series thread 300: total %llu "
                "hist %llu kernel-exp %llu; thread 200 twiddle %llu\n", M.fprof[0], M.fprof[1],
                M.fprof[2], M.fprof[3], M.sprof[0], M.sprof[1], M.sprof[2], M.sprof[3]);
