@@ -172,11 +172,11 @@ def lib_digest(path=None):
 
 
 def pmc_traffic(kernel):
-    """Per-launch HBM-side bytes of ``kernel`` from the newest committed PMC summary
-    (profiles/r*_pmc_traffic.json, written by scripts/pmc_summary.py from separate rocprofv3
+    """Per-launch HBM-side bytes of ``kernel`` from the newest committed PMC summary of this
+    library (profiles/r*_pmc_traffic.json, written by scripts/pmc_summary.py from separate rocprofv3
     --pmc passes).  The bench cannot collect PMC counters itself (rocprofv3 wraps the process), so
-    the value is only used when the summary was made with the very library this process runs (its
-    sha256 recorded by pmc_summary.py); otherwise (None, source, "stale ...")."""
+    the value is only used from a summary made with the very library this process runs (its
+    sha256 recorded by pmc_summary.py); with none, (None, newest source, "stale ...")."""
     import glob
     def run_order(f):   # r<round><tag>: tags run a..z, then aa..az, ... (r4z before r4av)
         m = re.match(r"r(\d+)([a-z]*)", os.path.basename(f))
@@ -184,16 +184,19 @@ def pmc_traffic(kernel):
     files = sorted(glob.glob(os.path.join(HERE, "profiles", "r*_pmc_traffic.json")), key=run_order)
     if not files:
         return None, None, "no committed PMC summary"
+    mine = lib_digest()
+    for f in reversed(files):   # the newest summary of this very library
+        d = json.load(open(f))
+        if d.get("lib_sha256") == mine:
+            src = os.path.relpath(f, HERE)
+            k = d["kernels"].get(kernel)
+            if not k:
+                return None, src, f"{kernel} not in the summary"
+            return k["traffic_bytes_per_launch"], src, "same library (sha256 match)"
     src = os.path.relpath(files[-1], HERE)
     d = json.load(open(files[-1]))
-    k = d["kernels"].get(kernel)
-    if not k:
-        return None, src, f"{kernel} not in the summary"
-    mine = lib_digest()
-    if d.get("lib_sha256") != mine:
-        return None, src, (f"stale: the summary's library sha256 {str(d.get('lib_sha256'))[:12]} "
-                           f"is not this run's {str(mine)[:12]}")
-    return k["traffic_bytes_per_launch"], src, "same library (sha256 match)"
+    return None, src, (f"stale: no summary of this run's library {str(mine)[:12]} (newest: "
+                       f"{str(d.get('lib_sha256'))[:12]})")
 
 
 # ------------------------------------------------------------------------------------------------
