@@ -164,19 +164,31 @@ def lib_digest(path=None):
     import hashlib
     if path is None:
         from vent_analysis_amd import _lib
-        path = _lib.LIB_PATH
+        path = getattr(_lib, "LIB_PATH", None)
     try:
         return hashlib.sha256(open(path, "rb").read()).hexdigest()
-    except OSError:
+    except (OSError, TypeError):
         return None
 
 
-def pmc_traffic(kernel):
-    """Per-launch HBM-side bytes of ``kernel`` from the newest committed PMC summary of this
-    library (profiles/r*_pmc_traffic.json, written by scripts/pmc_summary.py from separate rocprofv3
-    --pmc passes).  The bench cannot collect PMC counters itself (rocprofv3 wraps the process), so
-    the value is only used from a summary made with the very library this process runs (its
-    sha256 recorded by pmc_summary.py); with none, (None, newest source, "stale ...")."""
+DEFAULT_WORKLOAD = None   # filled lazily: workload_key of the default command line
+
+
+def summary_workload(d):
+    """The workload a PMC summary was measured on.  Summaries from before round 6 carry none: they
+    were all made by scripts/gpu_pmc.sh on the default bench command line."""
+    global DEFAULT_WORKLOAD
+    if DEFAULT_WORKLOAD is None:
+        DEFAULT_WORKLOAD = workload_key(make_parser().parse_args([]))
+    return d.get("workload") or DEFAULT_WORKLOAD
+
+
+def pmc_traffic(kernel, workload, digest=None):
+    """Per-launch HBM-side bytes of ``kernel`` from the newest committed PMC summary
+    (profiles/r*_pmc_traffic.json, written by scripts/pmc_summary.py from separate rocprofv3 --pmc
+    passes) of this very library (its sha256) AND this very workload (workload_key: shape, batch,
+    driver and N4 options).  The bench cannot collect PMC counters itself (rocprofv3 wraps the
+    process).  Returns (bytes or None, source file or None, why)."""
     import glob
     def run_order(f):   # r<round><tag>: tags run a..z, then aa..az, ... (r4z before r4av)
         m = re.match(r"r(\d+)([a-z]*)", os.path.basename(f))
@@ -184,19 +196,36 @@ def pmc_traffic(kernel):
     files = sorted(glob.glob(os.path.join(HERE, "profiles", "r*_pmc_traffic.json")), key=run_order)
     if not files:
         return None, None, "no committed PMC summary"
-    mine = lib_digest()
-    for f in reversed(files):   # the newest summary of this very library
+    mine = digest if digest is not None else lib_digest()
+    same_lib = None
+    for f in reversed(files):   # the newest summary of this library and workload
         d = json.load(open(f))
-        if d.get("lib_sha256") == mine:
-            src = os.path.relpath(f, HERE)
-            k = d["kernels"].get(kernel)
-            if not k:
-                return None, src, f"{kernel} not in the summary"
-            return k["traffic_bytes_per_launch"], src, "same library (sha256 match)"
+        if d.get("lib_sha256") != mine:
+            continue
+        same_lib = same_lib or f
+        if summary_workload(d) != workload:
+            continue
+        src = os.path.relpath(f, HERE)
+        k = d["kernels"].get(kernel)
+        if not k:
+            return None, src, f"{kernel} not in the summary of this library and workload"
+        return k["traffic_bytes_per_launch"], src, "same library (sha256) and workload"
+    if same_lib:
+        return None, os.path.relpath(same_lib, HERE), ("refused: the summaries of this library were "
+                                                       "measured on another workload")
     src = os.path.relpath(files[-1], HERE)
     d = json.load(open(files[-1]))
     return None, src, (f"stale: no summary of this run's library {str(mine)[:12]} (newest: "
                        f"{str(d.get('lib_sha256'))[:12]})")
+
+
+def dominant_class(iso_ms_total, iso_launches, runs):
+    """The kernel class with the most time per step when batch 0 runs alone: each class's summed
+    launch time over ``runs`` isolated runs, divided by the runs (launch time x launches per step).
+    Returns (class, mean launch ms, launches per step)."""
+    per_step = {k: iso_ms_total[k] / runs for k in iso_ms_total if iso_launches.get(k)}
+    dom = max(per_step, key=lambda k: per_step[k])
+    return dom, iso_ms_total[dom] / iso_launches[dom], iso_launches[dom] / runs
 
 
 # ------------------------------------------------------------------------------------------------
@@ -257,7 +286,7 @@ class stdout_to_stderr:
         os.close(self.saved)
 
 
-def host_to_host(R, C, Z, nb, args, device, opts, seed, aligned=True):
+def host_to_host(R, C, Z, nb, args, device, opts, seed, aligned=True, _lib=None):
     """Volumes/s from host memory to host memory: args.h2h_batches x nb studies streamed through
     vh_pipe in sub-batches of args.h2h_sub studies on args.h2h_slots slots (pinned staging, one
     stream each: the H2D, compute and D2H of different sub-batches overlap, and the studies of
@@ -265,7 +294,8 @@ def host_to_host(R, C, Z, nb, args, device, opts, seed, aligned=True):
     every output the class returns out (N4HPvent, defectArray, defectBorder, defectArrayLB,
     scalars).  The slowest rank's time is what the caller's aggregate uses (ranks run
     independently)."""
-    from vent_analysis_amd import _lib
+    if _lib is None:
+        from vent_analysis_amd import _lib
     from vent_analysis_amd.synth import synth_batch
     slots, sub = args.h2h_slots, min(args.h2h_sub, nb)
     hb = args.h2h_batches or (12 if int(os.environ.get("WORLD_SIZE", "1")) == 1 else 6)
@@ -288,10 +318,13 @@ def host_to_host(R, C, Z, nb, args, device, opts, seed, aligned=True):
         runs.append(time.perf_counter() - t)
     pinned_peak, staged = P.stats()
     P.close()
+    budget = pin_budget()
+    if pinned_peak > budget:
+        raise RuntimeError(f"vh_pipe pinned {pinned_peak} B in place, past this rank's budget {budget} B")
     dt = sorted(runs)[1]
-    return {"volumes": n, "seconds": round(dt, 4), "runs_seconds": [round(r, 4) for r in runs],
+    return {"volumes": n, "seconds": round(dt, 6), "runs_seconds": [round(r, 6) for r in runs],
             "statistic": "median of 3 passes", "sub_batch": sub, "slots": slots,
-            "pinned_peak_bytes": pinned_peak, "staged_spans": staged,
+            "pinned_peak_bytes": pinned_peak, "pin_budget_bytes": budget, "staged_spans": staged,
             "includes": "H2D of HPvent f32 + mask u8, the full pipeline, D2H of N4HPvent f32 + "
                         "defect / border / LB u8 + per-study scalars, host staging memcpys; over "
                         "PCIe the mask travels as bits and the three maps as one packed byte "
@@ -300,11 +333,21 @@ def host_to_host(R, C, Z, nb, args, device, opts, seed, aligned=True):
             "pcie_bytes_per_volume": int(R * C * Z * (4 + 0.125 + 4 + 1))}
 
 
-def link_probe(device, mb=256):
+def pin_budget():
+    """This rank's vh_pipe_run page-locking budget, by the library's rule (api.hip, vh_pipe_create):
+    VH_PIPE_PIN_CAP bytes, else 32 GiB per node divided by LOCAL_WORLD_SIZE (the ranks sharing
+    the host's memory)."""
+    if os.environ.get("VH_PIPE_PIN_CAP"):
+        return int(os.environ["VH_PIPE_PIN_CAP"])
+    return (32 << 30) // max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1") or 1))
+
+
+def link_probe(device, mb=256, _lib=None):
     """This box's PCIe link with pinned host memory: H2D alone, D2H alone and both at once on two
     streams (as the pipe's overlapped chunks use it), best of 3 each (vh_link_probe).  The
     host-to-host line can not beat link rate / PCIe bytes per volume, whatever the device rate."""
-    from vent_analysis_amd import _lib
+    if _lib is None:
+        from vent_analysis_amd import _lib
     r = _lib.context(device).link_probe(mb << 20)
     r["bytes_each_way"] = mb << 20
     return r
@@ -432,69 +475,7 @@ def launch_ranks(args, argv):
     return rc
 
 
-def main_dry(args, rank, world, dist):
-    """--dry-run (CPU, gloo): the multi-rank skeleton of the GPU line without libventhip -- shard
-    seeds, the unique-id broadcast, the barrier-bracketed max-over-ranks timing and the cohort
-    histogram sum -- with a numpy stand-in for the step (tests/test_dist_gloo.py)."""
-    import torch
-    from vent_analysis_amd.synth import synth_batch
-    R, C, Z = args.shape
-    hp, mk = synth_batch(R, C, Z, args.batch, base_seed=shard_seed(rank), unique=BENCH_UNIQUE, vary=True)
-    uid = broadcast_uid(bytes(range(128)) if rank == 0 else None, dist)
-    if os.environ.get("VH_DRY_FAIL_RANK") == str(rank):   # tests: a failing rank fails the job
-        raise SystemExit(3)
-
-    def local_rows():   # per-rank cohort rows (numpy stand-in for k_cohort_*)
-        h = np.zeros(1024, np.int64)
-        for x, m in zip(hp, mk):
-            s = np.sort(x[m > 0])
-            nv = (x / np.float32(s[int(len(s) * 0.99)])).astype(np.float32)[m > 0]
-            nv = nv[(nv >= 0) & (nv < np.float32(1.5))]
-            h += np.bincount(np.minimum((nv * np.float32(1024 / 1.5)).astype(np.int64), 1023),
-                             minlength=1024)
-        return h
-
-    def step():   # the stand-in communicator's all-reduce (RCCL's on the GPU)
-        t = torch.from_numpy(local_rows())
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-        return t.numpy()
-
-    for _ in range(args.warmup):
-        step()
-    dist.barrier()
-    t0 = time.perf_counter()
-    t_local = None
-    for _ in range(args.steps):
-        hist = step()
-    t_local = time.perf_counter() - t0
-    dist.barrier()
-    dt = max_over_ranks(time.perf_counter() - t0, dist)
-    # the GPU line's self-check with the stand-in communicator: local rows, the communicator's sum,
-    # the gloo sum of the per-rank rows
-    loc = local_rows()
-    if os.environ.get("VH_DRY_BAD_SUM") == str(rank):   # tests: a wrong all-reduce is caught
-        loc = loc + 1
-    ok, total_rows = check_cohort(loc, hist, dist)
-    rates = per_rank(args.batch * args.steps / t_local, dist)
-    line = {"metric": METRIC, "value": round(world * args.batch * args.steps / dt, 2),
-            "unit": "volumes/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": "dry run (CPU, no GPU work)", "volumes_per_gpu": args.batch,
-                       "shape": [R, C, Z], "parallelism": f"dp{world}"},
-            "comm": {"kind": "gloo stand-in (dry run)", "rccl_ranks": dist.get_world_size(),
-                     "allreduce_ok": ok, "cohort_total": total_rows},
-            "per_rank_vol_s": [round(r, 2) for r in rates],
-            "dry_run": {"uid_ok": uid == bytes(range(128)), "cohort_hist": hist.tolist(),
-                        "rank_seeds": [shard_seed(r) for r in range(world)]}}
-    if rank == 0:
-        print(json.dumps(line), flush=True)
-    dist.destroy_process_group()
-    if not ok:
-        sys.exit("bench.py: the cohort all-reduce differs from the sum of the per-rank histograms")
-
-
-def main():
+def make_parser():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
@@ -537,12 +518,37 @@ def main():
     ap.add_argument("--workload", default="vdp", choices=["vdp", "ci"],
                     help="vdp: the BASELINE metric (default); ci: the cluster-index line")
     ap.add_argument("--dry-run", action="store_true",
-                    help="multi-rank skeleton on the CPU (gloo, no GPU): launcher, uid broadcast, "
-                         "timing and cohort sum (tests)")
+                    help="tests only: this main() on the CPU over gloo with tests/standin_lib.py in "
+                         "place of libventhip (every host step of the N > 1 line runs; the stand-in's "
+                         "cohort all-reduce is a gloo all-reduce); the line says so and measures nothing")
     ap.add_argument("--conv-threshold", type=float, default=0.001,
                     help="N4 convergence threshold (SimpleITK default 0.001; 0 = fixed 4x50 "
                          "iterations, for kernel A/B runs at constant work)")
-    args = ap.parse_args()
+    return ap
+
+
+def workload_key(args):
+    """What a PMC summary must have been measured on to price this line's traffic: the shape, the
+    batch and every option that changes which kernels run or how much work they do."""
+    return {"shape": [int(v) for v in args.shape], "batch": int(args.batch),
+            "n4_mode": args.n4_mode, "morph3d": bool(args.morph3d), "conv_mode": int(args.conv_mode),
+            "conv_threshold": float(args.conv_threshold), "no_n4": bool(args.no_n4),
+            "subbatch": int(args.subbatch)}
+
+
+def load_lib(dry_run):
+    """libventhip's ctypes shim, or under --dry-run (tests only) the CPU stand-in with the same
+    surface (tests/standin_lib.py)."""
+    if dry_run:
+        sys.path.insert(0, os.path.join(HERE, "tests"))
+        import standin_lib
+        return standin_lib
+    from vent_analysis_amd import _lib
+    return _lib
+
+
+def main():
+    args = make_parser().parse_args()
     if args.workload == "ci":
         return main_ci(args)
 
@@ -566,10 +572,7 @@ def main():
         import torch.distributed as dist
         with stdout_to_stderr():   # gloo prints its connection banner on fd 1
             dist.init_process_group("gloo", rank=rank, world_size=world)
-    if args.dry_run:
-        return main_dry(args, rank, world, dist)
-
-    from vent_analysis_amd import _lib
+    _lib = load_lib(args.dry_run)
     from vent_analysis_amd.synth import synth_batch
 
     # --inflight I: I device batches (distinct studies) whose steps are enqueued back to back on
@@ -596,7 +599,8 @@ def main():
             _lib.comm_init(1, 0, _lib.comm_unique_id(), device=local)
         if use_comm:   # what RCCL itself reports (ncclCommCount / ncclCommUserRank)
             n_rccl, r_rccl = _lib.comm_info(device=local)
-            comm = {"kind": "rccl", "rccl_ranks": n_rccl, "rccl_rank": r_rccl}
+            comm = {"kind": getattr(_lib, "COMM_KIND", "rccl"), "rccl_ranks": n_rccl,
+                    "rccl_rank": r_rccl}
             if n_rccl != world or r_rccl != rank:
                 sys.exit(f"bench.py: RCCL reports rank {r_rccl} of {n_rccl}, expected {rank} of {world}")
     vox = (1.5, 1.5, 10.0)
@@ -622,7 +626,7 @@ def main():
 
     try:
         import torch
-        if torch.cuda.is_available():   # this rank's GPU (torch's current device is 0 otherwise)
+        if not args.dry_run and torch.cuda.is_available():   # this rank's GPU (torch's current device is 0 otherwise)
             torch.cuda.set_device(local)
             sync_dev = torch.cuda.synchronize
         else:
@@ -693,7 +697,7 @@ def main():
             if tot_n:
                 kernels[name] = {"ms_total": tot_ms, "launches": tot_n, "alg_bytes": tot_b}
     batch_latency_ms = None
-    iso_kernels = {}
+    iso_kernels = {}   # class -> (summed ms, launches) over the isolated runs of batch 0
     if ninf > 1 or not args.no_profile:
         # batch 0 alone, args.iso_runs times (untimed above): the latency one batch sees, and every
         # kernel class's launch duration with no other batch's workgroups on the CUs -- what a
@@ -711,16 +715,28 @@ def main():
             for name in _lib.lib().vh_batch_kernel_names().decode().split(";"):
                 ms, n, _ = Bt.kernel_time(name)
                 if n:
-                    iso_kernels[name] = ms / n
+                    iso_kernels[name] = (ms, n)
     roof = None
     if kernels and iso_kernels:
-        dom = max(iso_kernels, key=lambda k: iso_kernels[k])   # the longest launch class alone
-        iso_us = iso_kernels[dom] * 1e3
+        runs = max(1, args.iso_runs)
+        # the dominant class is the one with the most time per step (launch time x launches), not
+        # the longest single launch: config 5's ~170 grid-PC launches outweigh its one sort launch
+        dom, iso_ms, per_step = dominant_class({n: v[0] for n, v in iso_kernels.items()},
+                                               {n: v[1] for n, v in iso_kernels.items()}, runs)
+        iso_us = iso_ms * 1e3
+        # algorithmic_bytes is the class's total over one step: per launch = / launches per step
         bpl = algorithmic_bytes(dom, hp, mk, res, R, C, Z, study=used_study,
-                                conv_mode=args.conv_mode)   # batch 0's bytes per launch
+                                conv_mode=args.conv_mode) / per_step
         ach = bpl / (iso_us * 1e-6) / 1e9
-        traffic, tsrc, tnote = pmc_traffic(dom)
+        traffic, tsrc, tnote = pmc_traffic(dom, workload_key(args), digest=lib_digest(
+            getattr(_lib, "LIB_PATH", None)))
         k = kernels.get(dom, {"ms_total": 0.0, "launches": 0, "alg_bytes": 0.0})
+        lim = {"n4_study": "latency, below the HBM roof: the serial S7 recurrence evaluated by "
+                           "guess-and-verify rounds and the latency-bound fit / eval walks of one "
+                           "workgroup per study (DESIGN.md section 5)",
+               "n4_pcg": "latency, below the HBM roof: the serial S7 recurrence of one large study "
+                         "by guess-and-verify rounds over a cooperative grid, one grid barrier per "
+                         "round (DESIGN.md section 4.2)"}
         roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
                 "traffic": round(traffic) if traffic else None,
@@ -728,16 +744,17 @@ def main():
                 "traffic_note": tnote,
                 "traffic_over_alg": round(traffic / bpl, 3) if traffic else None,
                 "avg_launch_us": round(iso_us, 2), "alg_bytes_per_launch": bpl,
+                "launches_per_step": round(per_step, 3),
+                "dominant_by": "time per step of batch 0 alone (mean launch x launches per step)",
                 "timing": f"HIP events around each launch of batch 0 alone, mean of "
-                          f"{max(1, args.iso_runs)} runs (no other batch on the CUs)",
-                "limiter": ("latency, below the HBM roof: the serial S7 recurrence evaluated by "
-                            "guess-and-verify rounds and the latency-bound fit / eval walks of "
-                            "one workgroup per study (DESIGN.md section 5)"
-                            if dom == "n4_study" else None),
-                "kernel_us_per_launch": {n: round(v * 1e3, 2) for n, v in
-                                         sorted(iso_kernels.items(), key=lambda kv: -kv[1])},
-                "non_n4_us_per_step": round(sum(v for n, v in iso_kernels.items()
-                                                if not n.startswith("n4_")) * 1e3, 2)}
+                          f"{runs} runs (no other batch on the CUs)",
+                "limiter": lim.get(dom),
+                "kernel_us_per_launch": {n: round(v[0] / v[1] * 1e3, 2) for n, v in
+                                         sorted(iso_kernels.items(), key=lambda kv: -kv[1][0])},
+                "kernel_us_per_step": {n: round(v[0] / runs * 1e3, 2) for n, v in
+                                       sorted(iso_kernels.items(), key=lambda kv: -kv[1][0])},
+                "non_n4_us_per_step": round(sum(v[0] for n, v in iso_kernels.items()
+                                                if not n.startswith("n4_")) / runs * 1e3, 2)}
         if ninf > 1 and k["launches"]:
             # the timed region's own launches: batches in flight overlap, so a launch's duration
             # includes waiting for CUs another batch's studies hold -- not a kernel cost
@@ -759,12 +776,12 @@ def main():
     if not args.no_h2h:
         if dist:   # every rank streams at once (host memory and PCIe shared as in a cohort run)
             dist.barrier()
-        h2h = host_to_host(R, C, Z, nb, args, local, warm, shard_seed(rank) + 500)
-        h2h["link"] = link_probe(local)
+        h2h = host_to_host(R, C, Z, nb, args, local, warm, shard_seed(rank) + 500, _lib=_lib)
+        h2h["link"] = link_probe(local, _lib=_lib)
         h2h["link"]["bound_vol_s"] = round(link_bound(h2h["link"], R, C, Z), 1)
         h2h["link"]["h2h_of_bound"] = round(h2h["volumes"] / h2h["seconds"] / h2h["link"]["bound_vol_s"], 3)
         if dist:   # the aggregate uses the slowest rank's time
-            h2h["seconds"] = round(max_over_ranks(h2h["seconds"], dist), 4)
+            h2h["seconds"] = round(max_over_ranks(h2h["seconds"], dist), 6)
             h2h["seconds_statistic"] = "max over ranks of each rank's median"
     total = world * nb * args.steps
     line = {
@@ -779,7 +796,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic",
+        "data": "synthetic" if not args.dry_run else
+                "DRY RUN: tests/standin_lib.py in place of libventhip (CPU, gloo); nothing measured",
         "config": {"workload": f"batch of {nb} synthetic {R}x{C}x{Z} Xe volumes per GPU, "
                                "end-to-end calculate_VDP: N4 (SimpleITK defaults 4x50 it) + "
                                "mean-anchored + linear-binning + k-means VDP + defect border + "

@@ -507,7 +507,8 @@ void n4o_pc_sig_bound(const float *d, int64_t n, int nb, double *lo, float *sig_
  * mean, block by block as the GPU forms it (nb blocks, float reciprocals, the same margins).  Returns
  * lo (a lower bound of ITK's float sig), muhi (an upper bound of its float mean) and ok (every p in
  * (0.5, 1.9), where the bound holds); *dmax_out = max over k of |mu_k - m_k| / D_k, the float mean's
- * observed distance from the exact one over the bound D_k = 2^-24 (k + 3) (1 + 2^-20) (must be <= 1).
+ * observed distance from the exact one over the bound D_k = 2^-25 M (k + 3) (1 + 2^-20) (must be
+ * <= 1), M = max p (1 + 2^-24 (n + 3)) (1 + 2^-20) >= every |mu_i|, |p_i| (the code's cD (k + 3)).
  * Also ITK's float (mu, sig) for the check.  Test infrastructure (tests/test_n4_oracle.py). */
 void n4o_pc_pre_bound(const float *d, int64_t n, int nb, double *lo_out, float *muhi_out, int *ok_out,
                       double *dmax_out, float *sig_out, float *mu_out)

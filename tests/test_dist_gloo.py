@@ -82,29 +82,47 @@ def _bench(cmd, env=None, timeout=300):
 
 
 DRY = ["--dry-run", "--steps", "2", "--warmup", "1", "--batch", str(PER_RANK), "--shape",
-       *map(str, SHAPE), "--no-h2h"]
+       *map(str, SHAPE), "--inflight", "2", "--iso-runs", "2", "--h2h-batches", "2", "--h2h-sub", "2",
+       "--h2h-slots", "2"]
 
 
-def _check_dry_line(out, world):
+def _check_dry_line(out, world, pin_cap=None):
+    """bench.main()'s own N > 1 line, produced with tests/standin_lib.py in place of libventhip
+    (VERDICT r5 item 1): everything but the device work and RCCL itself ran as on the GPU boxes."""
     import json
     lines = [ln for ln in out.splitlines() if ln.strip()]
     assert len(lines) == 1, out          # rank 0's one JSON line, nothing else on stdout
     line = json.loads(lines[0])
     assert line["n_gpus"] == world and line["config"]["parallelism"] == f"dp{world}"
-    assert line["dry_run"]["uid_ok"]
+    assert line["data"].startswith("DRY RUN")
+    assert line["value"] > 0 and line["steps"] == 2 and line["cpu_baseline"] is None
     X, M = [], []
-    for r in range(world):
+    for r in range(world):   # each rank's batch 0 (checked after the timed region)
         x, m = synth_batch(*SHAPE, PER_RANK, base_seed=bench.shard_seed(r), vary=True)
         X.append(x)
         M.append(m)
     whole = cohort_hist(np.concatenate(X), np.concatenate(M))
-    assert np.array_equal(np.array(line["dry_run"]["cohort_hist"]), whole)
-    # the self-check fields the GPU line carries: the communicator's rank
-    # count, the all-reduce checked against the gloo sum of per-rank rows, a rate per rank
-    assert line["comm"]["rccl_ranks"] == world
-    assert line["comm"]["allreduce_ok"] is True
-    assert line["comm"]["cohort_total"] == int(whole.sum())
+    # the communicator as main() checked it: ranks as the stand-in reported them, the all-reduce
+    # checked against the gloo sum of every rank's rows (check_cohort), the cohort's total
+    c = line["comm"]
+    assert c["kind"].startswith("gloo stand-in")
+    assert c["rccl_ranks"] == world and c["rccl_rank"] == 0
+    assert c["allreduce_ok"] is True
+    assert c["cohort_total"] == int(whole.sum())
     assert len(line["per_rank_vol_s"]) == world and min(line["per_rank_vol_s"]) > 0
+    # the roofline block: the dominant class by time per step (10 x 1 ms of n4_pcg beat one 5 ms
+    # sort launch), bytes per launch = the class's bytes per step / launches per step
+    r = line["roofline"]
+    assert r["kernel"] == "n4_pcg" and r["launches_per_step"] == 10.0
+    assert r["avg_launch_us"] == 1000.0
+    assert r["traffic"] is None and "stale" in r["traffic_note"]
+    # the host-to-host leg: slowest rank's median, this rank's page-locking budget
+    h = line["host_to_host"]
+    assert h["seconds_statistic"] == "max over ranks of each rank's median"
+    budget = pin_cap if pin_cap is not None else (32 << 30) // world
+    assert h["pin_budget_bytes"] == budget and h["pinned_peak_bytes"] <= budget
+    if pin_cap is not None:
+        assert h["staged_spans"] > 0
     return line
 
 
@@ -126,6 +144,13 @@ def test_bench_under_torchrun():
     _check_dry_line(r.stdout, 2)
 
 
+def test_bench_pin_budget_per_rank():
+    """A per-rank page-locking cap past which the pipe stages (VH_PIPE_PIN_CAP) reaches every rank."""
+    r = _bench(["bench.py", "--gpus", "2"] + DRY, env={"VH_PIPE_PIN_CAP": str(1 << 16)})
+    assert r.returncode == 0, r.stderr[-2000:]
+    _check_dry_line(r.stdout, 2, pin_cap=1 << 16)
+
+
 def test_bench_rank_failure_and_world_mismatch():
     r = _bench(["bench.py", "--gpus", "2"] + DRY, env={"VH_DRY_FAIL_RANK": "1"})
     assert r.returncode != 0
@@ -134,8 +159,17 @@ def test_bench_rank_failure_and_world_mismatch():
     assert r.returncode != 0 and "WORLD_SIZE 1 but --gpus 2" in r.stderr
 
 
-def test_bench_cohort_mismatch_fails():
-    """A rank whose all-reduced histogram differs from the per-rank sum fails the whole job."""
-    r = _bench(["bench.py", "--gpus", "2"] + DRY, env={"VH_DRY_BAD_SUM": "1"})
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_cohort_mismatch_fails(world):
+    """A rank whose communicator returns a wrong sum fails the whole job (main()'s check_cohort)."""
+    r = _bench(["bench.py", "--gpus", str(world)] + DRY, env={"VH_DRY_BAD_SUM": str(world - 1)})
     assert r.returncode != 0
     assert "differs from the sum" in r.stderr
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_communicator_rank_count_checked(world):
+    """A communicator that reports the wrong rank count stops the job before the timed region."""
+    r = _bench(["bench.py", "--gpus", str(world)] + DRY, env={"VH_DRY_BAD_RANKS": "1"})
+    assert r.returncode != 0
+    assert "RCCL reports rank 1 of" in r.stderr

@@ -1399,6 +1399,7 @@ __global__ void __launch_bounds__(PC_TPB) k_n4_pcw(const float *D, const int32_t
     if (threadIdx.x == 0) {
         st[b].conv_w = ch.conv;
         st[b].pc_pre = S.xdone == 4 * 1 + 1;
+        st[b].conv_bound = S.xdone == 4 * 1 + 1 || S.xdone == 4 * 1 + 3;   // decided on bounds
     }
 }
 
@@ -1904,7 +1905,10 @@ __global__ void __launch_bounds__(PC_TPB) k_n4_pcg2(Pcg2Args A) {
         const float mue = L.mue;
         const float muh = __uint_as_float(__float_as_uint(mue) + 1u);
         if (f > 0.5 && lo > 0.0 && mue > 0.0f && itk_conv(muh, sl, n) > A.skip_thresh) {
-            if (j == 0) A.st[A.b].conv_w = itk_conv(muh, sl, n);
+            if (j == 0) {
+                A.st[A.b].conv_w = itk_conv(muh, sl, n);
+                A.st[A.b].conv_bound = 1;   // a bound, not ITK's float measure (threshold test only)
+            }
 #ifdef PCG_PROF
             if (j == 0) printf("PCG2 n %lld G %d L %u stage0 %d decided\n", (long long)n, (int)gridDim.x, m.L, round + 1);
 #endif
@@ -1966,7 +1970,10 @@ __global__ void __launch_bounds__(PC_TPB) k_n4_pcg2(Pcg2Args A) {
             parity ^= 1;
             if (first == NB) {
                 if (phase == 0) break;   // stage 1's fixed point (sig steps uncertified): verify it exactly
-                if (j == (uint32_t)(nbe - 1)) A.st[A.b].conv_w = itk_conv(le, les, n);
+                if (j == (uint32_t)(nbe - 1)) {
+                    A.st[A.b].conv_w = itk_conv(le, les, n);
+                    A.st[A.b].conv_bound = 0;
+                }
                 done = true;
                 break;
             }
@@ -1994,6 +2001,7 @@ __global__ void __launch_bounds__(PC_TPB) k_n4_pcg2(Pcg2Args A) {
                 for (uint32_t s = 0; s < l; ++s, kd += 1.0) pc_step(kd, A.P[(size_t)s * NB + jb], mu, sig);
             }
             A.st[A.b].conv_w = itk_conv(mu, sig, n);
+            A.st[A.b].conv_bound = 0;
         }
     }
 }
@@ -2181,8 +2189,9 @@ static void n4_trace(vh_batch *b, int64_t vol0, int L, int it) {
         return x;
     };
     const uint64_t hu = fnv(b->d_U), hd = fnv(b->d_D);
-    fprintf(stderr, "N4TRACE L%d it%d active %d U %016llx D %016llx conv_w %.9g\n", L, it, s.active,
-            (unsigned long long)hu, (unsigned long long)hd, s.conv_w);
+    fprintf(stderr, "N4TRACE L%d it%d active %d U %016llx D %016llx conv_w %.9g%s\n", L, it, s.active,
+            (unsigned long long)hu, (unsigned long long)hd, s.conv_w,
+            s.conv_bound ? " (certified bound: decided above the threshold, not ITK's value)" : "");
 }
 
 // One sub-batch [vol0, vol0 + ns): the whole multi-level loop.  Flat sweeps run over the chunk
@@ -2267,7 +2276,11 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
                 int dev = 0, ncu = 0, per = 0;
                 HIP_TRY(hipGetDevice(&dev));
                 HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-                HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)k_n4_pcg, PC_TPB, 0));
+                // the occupancy of the kernel actually launched (k_n4_pcg2 unless VH_PCG_V=1: other
+                // LDS and register use); a cooperative launch larger than fits would fail
+                HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                    &per, pcg_v1 ? (const void *)k_n4_pcg : (const void *)k_n4_pcg2, PC_TPB, 0));
+                if (per < 1) throw VhError{VH_ERR_ARG, "N4 grid PC: no workgroup fits on a CU"};
                 // ~1/4 of V masked, VH_PCG_STEPS (default 16) steps per chain block (config 2: 64 -> 16
                 // steps: n4_pcg 14.4 -> 10.3 ms per study; config 5 is at one workgroup per CU anyway)
                 const int64_t spb = getenv("VH_PCG_STEPS") ? std::max(1, atoi(getenv("VH_PCG_STEPS"))) : 16;

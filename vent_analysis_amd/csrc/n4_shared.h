@@ -1278,6 +1278,9 @@ __device__ __forceinline__ void aff_step(double &A, double &B, double &Bs) {
     A = A * ya;
     Bs = ys + Bs;
 }
+// Exclusive affine scan over the workgroup's NL threads.  One barrier in the middle (the wave
+// aggregates published by lane 63), none at the end: two calls back to back need a __syncthreads()
+// between them, or a fast wave's second-call aggregate store races a slow wave's first-call read.
 template <int NL>
 __device__ __forceinline__ void pcw_scan(PcShared<NL> &S, double a, double b, double bs, double &dm,
                                          double &ds) {
@@ -1726,8 +1729,10 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
     static_assert(sizeof(float) * G0 * TS <= pcw_lds_bytes<NL>(), "pass-0 transpose buffer");
     float *const T0 = reinterpret_cast<float *>(&S);
     const uint32_t lmax = m.L + (m.rem ? 1u : 0u);
-    // s1 = sum of (p - 1) in double: exact (every p - 1 is a multiple of 2^-24 below 2^-4 in size
-    // wherever the early decision uses it, so any order of the sums is exact); s2 seeds the guesses
+    // s1 = sum of (p - 1) in double: exact wherever the early decision uses it (it requires every p
+    // in (0.5, 1.9): then p - 1 is a multiple of 2^-24 with |p - 1| < 0.9, so it and every partial
+    // sum of n < 2^24 of them are integers times 2^-24 below 2^24 in size -- at most 48 significant
+    // bits, within a double's 53, so any order of the sums is exact); s2 seeds the guesses
     double s1 = 0.0;
 #if PC_S12F   // the guesses' block sums: they only seed the rounds (the result is exact either way)
     float s2 = 0.0f;
@@ -1865,6 +1870,9 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
         }
         const double wown = acc * (1.0 - 1.0 / fmax((double)k0, 2.0));
         double wpre, unused;
+        // the first scan's wave aggregates may still be being read by a slower wave (pcw_scan ends
+        // without a barrier): the second scan's lane-63 stores must wait for every wave
+        __syncthreads();
         pcw_scan<NL>(S, 1.0, wown, 0.0, wpre, unused);
         if (tid == NL - 1) {
             const double f = 1.0 - ((double)n + 8.0) * 0x1p-24 - 0x1p-40;

@@ -107,6 +107,10 @@ struct N4State {
     uint32_t hw_id, xcc_id;    // k_n4_study: where the workgroup ran (HW_REG_HW_ID / HW_REG_XCC_ID)
     int32_t pc_rounds, pc_fallbacks;   // k_n4_study: S7 guess-and-verify rounds / serial fallbacks, all iterations
     int32_t pc_pre;            // k_n4_pcw: the last call decided early (PC_PRE): try again on the next one
+    // 1 when conv_w of the last S7 call is a certified bound (an early / stage-0 decision: mu's upper
+    // and sig's lower bound, enough for the threshold test only), 0 when it is ITK's float measure.
+    // A level's last call is never decided early, so conv_level[] is always the exact measure.
+    int32_t conv_bound;
 };
 
 // Per-axis, per-level B-spline tables (host-built, identical to oracle/n4_oracle.c).
