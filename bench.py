@@ -485,10 +485,12 @@ def make_parser():
     ap.add_argument("--no-n4", action="store_true", help="VDP chain only (N4 := identity)")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-profile", action="store_true", help="no HIP events in the timed region")
+    ap.add_argument("--no-profile", action="store_true",
+                    help="no HIP events in the isolated runs (no roofline); the timed region never has any")
     ap.add_argument("--subbatch", type=int, default=0, help="volumes per N4 sub-batch (0: all)")
-    ap.add_argument("--n4-mode", default="auto", choices=["auto", "sweep", "study"],
-                    help="N4 driver: per-iteration sweeps or one workgroup per study")
+    ap.add_argument("--n4-mode", default="auto", choices=["auto", "sweep", "study", "grid"],
+                    help="N4 driver: per-iteration sweeps, one workgroup per study, or one study "
+                         "over a cooperative grid of workgroups")
     ap.add_argument("--morph3d", action="store_true",
                     help="build-defined 3-D median / border (BASELINE config 5)")
     ap.add_argument("--conv-mode", type=int, default=0, choices=[0, 1],
@@ -643,8 +645,8 @@ def main():
         dist.barrier()
     sync_dev()
     t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(opts, i)
+    for i in range(args.steps):   # no HIP events in the timed region (they cost a one-study step
+        step(warm, i)             # of ~500 short launches half its time): the isolated runs below time kernels
     sync_all()
     sync_dev()
     t_local = time.perf_counter() - t0
@@ -678,24 +680,6 @@ def main():
         tail = {"min_us": round(float(st_us.min()), 1), "mean_us": round(float(st_us.mean()), 1),
                 "max_us": round(float(st_us.max()), 1),
                 "max_over_mean": round(float(st_us.max() / st_us.mean()), 4)}
-    used_study = args.n4_mode == "study" or (args.n4_mode == "auto" and nb >= 16)
-    kernels = {}
-    if not args.no_profile:
-        # (a batch the timed steps never reached -- steps < batches in flight -- has no results)
-        results = [res] + [b_.download(n4=False, maps=False)[4] if i < args.steps else None
-                           for i, b_ in enumerate(batches[1:], 1)]
-        for name in _lib.lib().vh_batch_kernel_names().decode().split(";"):
-            tot_ms, tot_n, tot_b = 0.0, 0, 0.0
-            for i, b_ in enumerate(batches):
-                ms, n, _ = b_.kernel_time(name)
-                runs = len(range(i, args.steps, ninf))   # timed steps batch i ran
-                tot_ms += ms
-                tot_n += n
-                if n:
-                    tot_b += algorithmic_bytes(name, data[i][0], data[i][1], results[i], R, C, Z,
-                                               study=used_study, conv_mode=args.conv_mode) * runs
-            if tot_n:
-                kernels[name] = {"ms_total": tot_ms, "launches": tot_n, "alg_bytes": tot_b}
     batch_latency_ms = None
     iso_kernels = {}   # class -> (summed ms, launches) over the isolated runs of batch 0
     if ninf > 1 or not args.no_profile:
@@ -717,7 +701,10 @@ def main():
                 if n:
                     iso_kernels[name] = (ms, n)
     roof = None
-    if kernels and iso_kernels:
+    # the volume-resident kernels (one workgroup per study, or the grid form for one study) ran when
+    # their timer class did: n4_init then counts only the row scans (algorithmic_bytes)
+    used_study = "n4_study" in iso_kernels
+    if iso_kernels:
         runs = max(1, args.iso_runs)
         # the dominant class is the one with the most time per step (launch time x launches), not
         # the longest single launch: config 5's ~170 grid-PC launches outweigh its one sort launch
@@ -730,7 +717,6 @@ def main():
         ach = bpl / (iso_us * 1e-6) / 1e9
         traffic, tsrc, tnote = pmc_traffic(dom, workload_key(args), digest=lib_digest(
             getattr(_lib, "LIB_PATH", None)))
-        k = kernels.get(dom, {"ms_total": 0.0, "launches": 0, "alg_bytes": 0.0})
         lim = {"n4_study": "latency, below the HBM roof: the serial S7 recurrence evaluated by "
                            "guess-and-verify rounds and the latency-bound fit / eval walks of one "
                            "workgroup per study (DESIGN.md section 5)",
@@ -755,17 +741,6 @@ def main():
                                        sorted(iso_kernels.items(), key=lambda kv: -kv[1][0])},
                 "non_n4_us_per_step": round(sum(v[0] for n, v in iso_kernels.items()
                                                 if not n.startswith("n4_")) / runs * 1e3, 2)}
-        if ninf > 1 and k["launches"]:
-            # the timed region's own launches: batches in flight overlap, so a launch's duration
-            # includes waiting for CUs another batch's studies hold -- not a kernel cost
-            avg_ms = k["ms_total"] / k["launches"]
-            roof["overlapped"] = {
-                "note": "batches in flight: includes CU wait",
-                "avg_launch_us": round(avg_ms * 1e3, 2),
-                "frac": round(k["alg_bytes"] / k["launches"] / (avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                "kernel_ms_per_step": {n: round(v["ms_total"] / args.steps, 3)
-                                       for n, v in sorted(kernels.items(),
-                                                          key=lambda kv: -kv[1]["ms_total"])}}
     its = np.array([list(r.n4_iters[:4]) for r in res])
     if not args.h2h_keep_batch:
         # the device-resident batches (their streams, 1.5 GB of HBM each) are done: the pipe's slot

@@ -106,7 +106,9 @@ typedef struct {
                                 axes, instead of the reference's per-slice medfilt2d / 2-D border */
     int32_t n4_mode;         /* N4 driver: 0 auto, 1 per-iteration sweeps over the batch (any size),
                                 2 volume-resident (one workgroup per study, the whole iteration
-                                loop in one launch; studies whose N4 state fits in LDS) */
+                                loop in one launch; studies whose N4 state fits in LDS),
+                                3 grid form (each study over G cooperating workgroups, one
+                                launch per study; auto picks it for a batch of one study) */
 } vh_run_opts;
 
 #define VH_COHORT_BINS 1024

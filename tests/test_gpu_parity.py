@@ -503,7 +503,7 @@ RAGGED = [((37, 45, 7), 11), ((12, 70, 9), 12), ((12, 70, 9), 13), ((130, 20, 3)
 
 
 @pytest.mark.parametrize("conv_mode", [0, 1])
-@pytest.mark.parametrize("driver", ["sweep", "study"])
+@pytest.mark.parametrize("driver", ["sweep", "study", "grid"])
 @pytest.mark.parametrize("shape,seed", RAGGED, ids=lambda v: "x".join(map(str, v)) if isinstance(v, tuple) else str(v))
 def test_n4_ragged_shapes_vs_oracle(shape, seed, driver, conv_mode):
     """Rows past one 64-row slot, columns not a multiple of the 64-column tile, 2- and 3-slice
@@ -517,7 +517,7 @@ def test_n4_ragged_shapes_vs_oracle(shape, seed, driver, conv_mode):
     try:
         n4, d, _, lb, res = _run_batch(X[None], M.astype(np.uint8)[None], driver, conv_mode=conv_mode)
     except ValueError as e:   # the study driver holds a study's state in LDS: not every shape fits
-        if driver == "study" and "LDS budget" in str(e):
+        if driver in ("study", "grid") and "LDS budget" in str(e):
             pytest.skip(str(e))
         raise
     assert_n4_matches(n4[0], res[0].n4_iters[:4], res[0].n4_conv[:4], ref, its_ref, conv_ref,
@@ -1077,3 +1077,55 @@ def test_export_class_methods(tmp_path):
     assert png.shape == img.shape and (png != img).any()
     diff = (png != img).any(axis=2)
     assert (png[diff] >= img[diff]).all()
+
+
+# ---- grid form: one study over G cooperating workgroups (k_n4_studyg) ------------------------------
+def _run_one(X, M, mode, **kw):
+    return _run_batch(X[None], M.astype(np.uint8)[None], mode, **kw)
+
+
+@pytest.mark.parametrize("conv_mode", [0, 1])
+@pytest.mark.parametrize("shape,seed", [((256, 256, 24), 7), ((128, 128, 24), 0), ((96, 112, 20), 5),
+                                        ((64, 64, 64), 6)])
+def test_n4_grid_vs_oracle_and_sweeps(shape, seed, conv_mode):
+    """n4_mode=3 (k_n4_studyg, the default for a batch of one study) against the C oracle, and
+    against the per-iteration sweep driver bit for bit (the same S1-S9 operations): N4HPvent,
+    iteration counts and convergence values identical, the VDP maps identical."""
+    X, M = synth_volume(*shape, seed)
+    ref, its_ref, conv_ref = native.n4(X, M, conv_mode=conv_mode)
+    g = _run_one(X, M, "grid", conv_mode=conv_mode)
+    assert_n4_matches(g[0][0], g[4][0].n4_iters[:4], g[4][0].n4_conv[:4], ref, its_ref, conv_ref,
+                      conv_mode, (shape, seed, "grid"))
+    s = _run_one(X, M, "sweep", conv_mode=conv_mode)
+    assert np.array_equal(g[0], s[0]) and np.array_equal(g[1], s[1]) and np.array_equal(g[3], s[3])
+    assert list(g[4][0].n4_iters[:4]) == list(s[4][0].n4_iters[:4])
+    assert g[4][0].n4_conv[:4] == s[4][0].n4_conv[:4]
+
+
+@pytest.mark.parametrize("G", ["1", "2", "5", "13", "40"])
+def test_n4_grid_any_workgroup_count(G, monkeypatch):
+    """The grid form's cross-workgroup sums (histogram counts and o-weights, 128-bit lattice
+    numerators, range records, the grid PC) are order-free integers: any workgroup count gives the
+    same field bit for bit, run after run (VH_STG_G)."""
+    X, M = synth_volume(128, 128, 24, 3)
+    monkeypatch.delenv("VH_STG_G", raising=False)
+    base = _run_one(X, M, "grid")
+    monkeypatch.setenv("VH_STG_G", G)
+    for _ in range(2):
+        o = _run_one(X, M, "grid")
+        assert np.array_equal(o[0], base[0]) and np.array_equal(o[1], base[1])
+        assert list(o[4][0].n4_iters[:4]) == list(base[4][0].n4_iters[:4])
+        assert o[4][0].n4_conv[:4] == base[4][0].n4_conv[:4]
+
+
+def test_n4_grid_empty_and_tiny_masks():
+    """A study with no mask voxel (n < 2: the field stays zero, N4HPvent = HPvent) and one with a
+    handful, on the grid form."""
+    X, M = synth_volume(64, 64, 16, 7)
+    e = _run_one(X, np.zeros_like(M), "grid")
+    assert e[4][0].n_mask == 0 and np.array_equal(e[0][0], X)
+    M2 = np.zeros_like(M)
+    M2[30:33, 30:32, 5:7] = 1
+    ref, its, conv = native.n4(X, M2)
+    t = _run_one(X, M2, "grid")
+    assert_n4_matches(t[0][0], t[4][0].n4_iters[:4], t[4][0].n4_conv[:4], ref, its, conv, 0, "tiny")

@@ -542,7 +542,7 @@ class Batch:
             o.vox[i] = float(vox[i])
         o.n4_subbatch = int(n4_subbatch)
         o.morph3d = int(bool(morph3d))
-        o.n4_mode = {"auto": 0, "sweep": 1, "study": 2}.get(n4_mode, n4_mode)
+        o.n4_mode = {"auto": 0, "sweep": 1, "study": 2, "grid": 3}.get(n4_mode, n4_mode)
         return o
 
     def run(self, opts: RunOpts):

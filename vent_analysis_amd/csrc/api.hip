@@ -114,7 +114,7 @@ static void batch_free(vh_batch *b) {
     dfree(b->d_cohort);
     dfree(b->d_L0); dfree(b->d_lat); dfree(b->d_E);
     dfree(b->d_numfix); dfree(b->d_rowstart); dfree(b->d_rowmask); dfree(b->d_rrank); dfree(b->d_iscan); dfree(b->d_D); dfree(b->d_perm); dfree(b->d_P1); dfree(b->d_den); dfree(b->d_T); dfree(b->d_pcdrift);
-    dfree(b->d_U); dfree(b->d_ridx); dfree(b->d_cp); dfree(b->d_cvol); dfree(b->d_hpart); dfree(b->d_hred); dfree(b->d_cpart); dfree(b->d_st); dfree(b->d_nactive); dfree(b->d_tabs); dfree(b->d_twiddle); dfree(b->d_study_lv); dfree(b->d_study_order); dfree(b->d_pcg); dfree(b->d_sortg); dfree(b->d_study_latg);
+    dfree(b->d_U); dfree(b->d_ridx); dfree(b->d_cp); dfree(b->d_cvol); dfree(b->d_hpart); dfree(b->d_hred); dfree(b->d_cpart); dfree(b->d_st); dfree(b->d_nactive); dfree(b->d_tabs); dfree(b->d_twiddle); dfree(b->d_study_lv); dfree(b->d_study_order); dfree(b->d_pcg); dfree(b->d_stg); dfree(b->d_sortg); dfree(b->d_study_latg);
     dfree(b->d_bitmap); dfree(b->d_ci_list); dfree(b->d_ci_shell); dfree(b->d_ci_hist);
     dfree(b->d_ci_status);
     dfree(b->d_ci_count); dfree(b->d_ci_map);

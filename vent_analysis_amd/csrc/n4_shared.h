@@ -7,6 +7,7 @@
 #include "vh_internal.h"
 #include "expf_small.h"
 #include <cfloat>
+#include <hip/hip_cooperative_groups.h>
 
 struct DevAxis {
     const int32_t *base;
@@ -42,6 +43,8 @@ DevLevel vh_dev_level(const vh_batch *b, const vh_n4_params &prm, int L);
 // N4 driver selection (vh_run_opts.n4_mode)
 bool vh_n4_study_eligible(const vh_batch *b, const vh_n4_params &prm, size_t *lds_bytes);
 void vh_launch_n4_study(vh_batch *b, const vh_n4_params &prm);
+bool vh_n4_studyg_eligible(const vh_batch *b, const vh_n4_params &prm, size_t *lds_bytes);
+void vh_launch_n4_studyg(vh_batch *b, const vh_n4_params &prm);
 
 // ---- small device helpers ----------------------------------------------------------------------
 __device__ __forceinline__ int lanes_below(uint64_t m) {
@@ -2157,3 +2160,366 @@ __device__ void chain_wave_sig(int64_t n, ChainSlot *slots, ChainState *cs) {
         cs->conv = itk_conv(cs->mu, sig, n);
     }
 }
+
+// ---- grid PC, one grid barrier per round (round 5) ----------------------------------------------
+// k_n4_pcg2: the study kernel's stage structure (pcw_run) over a cooperative grid.
+//   stage 0: certified float rounds on mu alone to their fixed point (mu never reads sig), each
+//            block also summing (p - mu)^2 along its trajectory;
+//   decision: below the level's iteration cap, the measure is only compared with the threshold:
+//            with mu exact, the weighted stage-0 sums bound ITK's float sig from below (pcw_run's
+//            certified decision), and a bound above the threshold ends the call -- most iterations;
+//   stage 1 + phase B: otherwise certified rounds on (mu, sig) from the exact mu starts and the
+//            stage-0 prefix as sig guesses, then exact rounds (the verification), as k_n4_pcg.
+// One grid barrier per round instead of two: a block's map T_j(x) = a_j x + b_j needs b_j =
+// e_j - g_{j+1}, and g_{j+1} of a workgroup's last block lives in the next workgroup.  So each
+// workgroup composes its maps with its last block's b left out and publishes, before the barrier,
+// that aggregate, its first block's guesses and its last block's ends; after the barrier every
+// workgroup adds the boundary terms itself (b = e_last(v) - g_first(v + 1)) while composing the
+// aggregates before it, finds the first mismatch (local ones and boundaries) and sets its own blocks'
+// next guesses g_j + delta_j -- no second barrier to publish guesses.  The records are double
+// buffered by round parity: a workgroup writes round r + 2's record only after every workgroup
+// passed barrier r + 1, i.e. finished reading round r's.
+struct PcgWg {
+    double A, B, S;         // the workgroup's composed maps (last block's b left out) / sig-channel sum
+    float gfirst, gsfirst;  // its first block's guesses this round
+    float elast, eslast;    // its last block's ends this round
+    int F;                  // first local mismatch (global block index), NB when none
+    float enbe;             // the end of block nbe - 1 when this workgroup holds it
+};
+struct Pcg2Args {
+    const float *D;
+    const int32_t *perm;
+    float *P;
+    const VolScalars *sc;
+    N4State *st;
+    int64_t b;
+    PcgWg *wg;              // [2][G]
+    float *E;               // [2][NB] every block's ends (the serial fallback)
+    float skip_thresh;      // > 0: the measure is only compared with it (certified decision allowed)
+};
+struct Pcg2Lds {
+    double wA[PC_TPB / 64], wB[PC_TPB / 64], wS[PC_TPB / 64];
+    int wF[PC_TPB / 64];
+    float gg[PC_TPB], gsg[PC_TPB];   // this round's guesses of the workgroup's blocks
+    float elast, eslast, enbe;
+    double pB, pS, tot;     // the workgroups before this one applied to 0; the grid's S total
+    float mue;              // the end of the last non-empty block
+    int first;
+};
+// The round's scan (one grid barrier).  Per thread: the map (a, b) and sig channel bs of its block
+// (b, bs of a workgroup's last block are ignored: its boundary terms are added after the barrier),
+// its mismatch flag (likewise), its guesses g, gs and ends e, es.  sum_mode: the S channel is a plain
+// sum (stage 0: the decision sums), no boundary term.  Out: dm, ds = the exclusive compositions at
+// this block applied to 0; first = the grid's first mismatching transition (NB when none).
+__device__ void pcg2_scan(const Pcg2Args &A, Pcg2Lds &L, cooperative_groups::grid_group &grid, int parity,
+                          int nbe, double a, double b, double bs, bool mm, float g, float gs, float e, float es,
+                          bool sum_mode, double &dm, double &ds, int &first) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, G = gridDim.x;
+    const int NB = G * PC_TPB;
+    const bool last = t == PC_TPB - 1;
+    if (t == 0) L.enbe = 0.0f;
+    __syncthreads();
+    if ((int)(blockIdx.x * PC_TPB + t) == nbe - 1) L.enbe = e;
+    if (last) {
+        b = 0.0;
+        if (!sum_mode) bs = 0.0;
+        mm = false;
+        L.elast = e;
+        L.eslast = es;
+    }
+    double Aw = a, Bw = b, Sw = bs;
+    aff_step<0x111, 0xf>(Aw, Bw, Sw);
+    aff_step<0x112, 0xf>(Aw, Bw, Sw);
+    aff_step<0x114, 0xf>(Aw, Bw, Sw);
+    aff_step<0x118, 0xf>(Aw, Bw, Sw);
+    aff_step<0x142, 0xa>(Aw, Bw, Sw);
+    aff_step<0x143, 0xc>(Aw, Bw, Sw);
+    const uint64_t bal = __ballot(mm);
+    if (lane == 63) {
+        L.wA[w] = Aw;
+        L.wB[w] = Bw;
+        L.wS[w] = Sw;
+    }
+    if (lane == 0) L.wF[w] = bal ? (int)(blockIdx.x * PC_TPB + w * 64 + __ffsll((unsigned long long)bal) - 1) : NB;
+    const double ea = dpp_d<0x138, 0xf>(Aw, 1.0), eb = dpp_d<0x138, 0xf>(Bw, 0.0), es_ = dpp_d<0x138, 0xf>(Sw, 0.0);
+    __syncthreads();
+    PcgWg *const rec = A.wg + (size_t)parity * G;
+    if (t == 0) {
+        double At = 1.0, Bt = 0.0, St = 0.0;
+        int f = NB;
+        for (int v = 0; v < PC_TPB / 64; ++v) {
+            Bt = L.wA[v] * Bt + L.wB[v];
+            At = At * L.wA[v];
+            St = St + L.wS[v];
+            f = min(f, L.wF[v]);
+        }
+        PcgWg r;
+        r.A = At;
+        r.B = Bt;
+        r.S = St;
+        r.F = f;
+        r.enbe = L.enbe;
+        r.gfirst = g;
+        r.gsfirst = gs;
+        r.elast = L.elast;
+        r.eslast = L.eslast;
+        rec[blockIdx.x] = r;
+    }
+    grid.sync();
+    if (w == 0) {   // lane l folds workgroups [per l, per l + per) in order: those before this one
+        // into the prefix (with their boundary terms), all of them into the S total and the first
+        // mismatch
+        double Al = 1.0, Bl = 0.0, Sl = 0.0, Tl = 0.0;
+        int f = NB;
+        float mue = 0.0f;
+        const int per = (G + 63) / 64;
+        for (int i = 0; i < per; ++i) {
+            const int u = per * lane + i;
+            if (u < G) {
+                const PcgWg r = rec[u];
+                const int jl = (u + 1) * PC_TPB - 1;   // the boundary transition jl -> jl + 1
+                double bb = 0.0, bs2 = 0.0;
+                if (jl < nbe - 1) {
+                    const PcgWg rn = rec[u + 1];
+                    bb = (double)r.elast - (double)rn.gfirst;
+                    if (!sum_mode) bs2 = (double)r.eslast - (double)rn.gsfirst;
+                    const bool bm = __float_as_uint(r.elast) != __float_as_uint(rn.gfirst) ||
+                                    (!sum_mode && __float_as_uint(r.eslast) != __float_as_uint(rn.gsfirst));
+                    if (bm) f = min(f, jl);
+                }
+                if (jl >= nbe - 1 && jl - PC_TPB < nbe - 1) mue = r.enbe;   // holds block nbe - 1
+                f = min(f, r.F);
+                Tl += r.S + bs2;
+                if (u < (int)blockIdx.x) {
+                    Bl = r.A * Bl + (r.B + bb);
+                    Al = Al * r.A;
+                    Sl = Sl + (r.S + bs2);
+                }
+            }
+        }
+        for (int off = 1; off < 64; off <<= 1) {
+            const double ya = __shfl_up(Al, off, 64), yb = __shfl_up(Bl, off, 64), ys = __shfl_up(Sl, off, 64);
+            if (lane >= off) {
+                Bl = Al * yb + Bl;
+                Al = Al * ya;
+                Sl = ys + Sl;
+            }
+            f = min(f, __shfl_xor(f, off, 64));
+        }
+        for (int off = 32; off > 0; off >>= 1) Tl += __shfl_down(Tl, off, 64);   // fixed tree
+        const uint64_t hm = __ballot(mue != 0.0f);
+        const float me = hm ? __shfl(mue, __ffsll((unsigned long long)hm) - 1, 64) : 0.0f;
+        if (lane == 63) {
+            L.pB = Bl;
+            L.pS = Sl;
+            L.first = f;
+        }
+        if (lane == 0) {
+            L.tot = Tl;
+            L.mue = me;
+        }
+    }
+    __syncthreads();
+    double x = L.pB, xs = L.pS;
+    for (int v = 0; v < w; ++v) {
+        x = L.wA[v] * x + L.wB[v];
+        xs = xs + L.wS[v];
+    }
+    dm = ea * x + eb;
+    ds = xs + es_;
+    first = L.first;
+}
+
+// The grid PC's whole call over the launch's grid (every workgroup of it, PC_TPB threads each):
+// pass 0 reads d through ld(raster rank) (k_n4_pcg2: the raster -> compact permutation; the grid
+// study kernel: d stored in raster order); the result goes to A.st[A.b].conv_w / conv_bound, written
+// by one thread -- the caller's next grid barrier publishes it.
+template <class LoadD>
+__device__ void pcg2_body(const Pcg2Args &A, Pcg2Lds &L, cooperative_groups::grid_group &grid, LoadD ld) {
+    const int64_t n = A.sc[A.b].n_mask1;
+    const int NB = gridDim.x * PC_TPB;
+    const PcMap m = pc_map(n, NB);
+    const int t = threadIdx.x;
+    const uint32_t j = blockIdx.x * PC_TPB + t, len = pc_len(m, j), k0 = pc_k0(m, j);
+    const int nbe = m.L ? NB : (int)m.rem;
+    const uint32_t np = (m.L + 1u) * (uint32_t)NB;
+    // pass 0: p = exp(d) in block layout, block sums (they seed the mu guesses)
+    double s1 = 0.0, s2 = 0.0;
+    for (uint32_t s0 = 0; s0 < len; s0 += 8) {
+        float v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)   // clamped, unconditional: the loads stay in flight together
+            v[i] = ld((int64_t)(k0 - 1u + (s0 + i < len ? s0 + i : len - 1u)));
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            if (s0 + i < len) {
+                const float p = expf_crs(v[i]);
+                A.P[(size_t)(s0 + i) * NB + j] = p;
+                const double e = (double)p - 1.0;
+                s1 += e;
+                s2 = fma(e, e, s2);
+            }
+    }
+    int parity = 0, first = NB;
+    double dm, ds;
+    // the guesses: exclusive sums of s1 (dm) through the same scan in sum mode (no maps: a = 1, b = 0)
+    pcg2_scan(A, L, grid, parity, nbe, 1.0, 0.0, s1, false, 0.0f, 0.0f, 0.0f, 0.0f, true, dm, ds, first);
+    parity ^= 1;
+    float g = 0.0f, gs = 0.0f;
+    {
+        const double K = (double)(k0 - 1u);
+        if (K > 0.0) g = (float)(1.0 + ds / K);   // ds = the sum of p - 1 over the steps before the block
+    }
+    // stage 0: mu alone
+    float lg = __int_as_float(0x7fc00000), le = 0.0f, lsum = 0.0f, go = 0.0f, eo = 0.0f;
+    bool have_o = false, s0done = false;
+    int round = 0;
+    for (int r = 0; r < PC_AMAX; ++r, ++round) {
+        L.gg[t] = g;
+        const bool same = __float_as_uint(g) == __float_as_uint(lg);
+        if (__ballot(!same) != 0ull && !same) {
+            float mu = g, sq = 0.0f;
+            pc_block_apx<0, false>(A.P, j, len, k0, mu, sq, (uint32_t)NB, np);
+            lg = g;
+            le = mu;
+            lsum = sq;
+        }
+        __syncthreads();
+        double a = 1.0, bm = 0.0;
+        bool mm = false;
+        if ((int)j < nbe - 1 && t < PC_TPB - 1) {
+            const float gn = L.gg[t + 1];
+            mm = __float_as_uint(le) != __float_as_uint(gn);
+            bm = (double)le - (double)gn;
+        }
+        if ((int)j < nbe - 1) {
+            const uint32_t k1 = k0 + len - 1u;
+            float af = (float)(k0 - 1u) * __builtin_amdgcn_rcpf((float)k1);
+            if (have_o && g != go) {
+                const float sl = (le - eo) * __builtin_amdgcn_rcpf(g - go);
+                if (sl >= 0.0f && sl <= 1.0f) af = sl;
+            }
+            a = (double)af;
+        }
+        go = g;
+        eo = le;
+        have_o = true;
+        // the decision sums: the block's stage-0 sum weighted by the smallest (N - 1) / N of the block
+        const double wown = ((int)j < nbe && k0 > 1u) ? (double)lsum * (1.0 - 1.0 / fmin((double)k0, ITK_NMAX)) : 0.0;
+        pcg2_scan(A, L, grid, parity, nbe, a, bm, wown, mm, g, 0.0f, le, 0.0f, true, dm, ds, first);
+        parity ^= 1;
+        if (first == NB) {
+            s0done = true;
+            break;
+        }
+        g = dm == 0.0 ? g : (float)((double)g + dm);
+    }
+    if (s0done && A.skip_thresh > 0.0f) {   // certified decision (pcw_run; uniform over the grid)
+        const double f = 1.0 - ((double)n + (double)m.L + 8.0) * 0x1p-24;
+        const double lo = L.tot * f;
+        float sl = (float)lo;
+        if ((double)sl > lo && sl > 0.0f) sl = __uint_as_float(__float_as_uint(sl) - 1u);
+        const float mue = L.mue;
+        const float muh = __uint_as_float(__float_as_uint(mue) + 1u);
+        if (f > 0.5 && lo > 0.0 && mue > 0.0f && itk_conv(muh, sl, n) > A.skip_thresh) {
+            if (j == 0) {
+                A.st[A.b].conv_w = itk_conv(muh, sl, n);
+                A.st[A.b].conv_bound = 1;   // a bound, not ITK's float measure (threshold test only)
+            }
+#ifdef PCG_PROF
+            if (j == 0) printf("PCG2 n %lld G %d L %u stage0 %d decided\n", (long long)n, (int)gridDim.x, m.L, round + 1);
+#endif
+            return;
+        }
+    }
+    // stage 1 (mu, sig) from the stage-0 guesses (exact mu starts when stage 0 converged) and the
+    // prefix of the stage-0 sums as sig guesses, then exact rounds
+    gs = (float)(ds > 0.0 ? ds : 0.0);
+    if (!s0done) gs = 0.0f;
+    float ls = __int_as_float(0x7fc00000), les = 0.0f;
+    lg = __int_as_float(0x7fc00000);
+    have_o = false;
+    bool done = false;
+    const int rs1 = round;
+    (void)rs1;
+    for (int phase = 0; phase < 2 && !done; ++phase) {
+        const int cap = phase == 0 ? PC_AMAX : PC_RMAX;
+        for (int r = 0; r < cap; ++r, ++round) {
+            L.gg[t] = g;
+            L.gsg[t] = gs;
+            float mu = g, sig = gs;
+            if (phase == 1) {
+                pc_block<0>(A.P, j, len, k0, mu, sig, NB);
+                le = mu;
+                les = sig;
+            } else {
+                const bool same = __float_as_uint(g) == __float_as_uint(lg) && __float_as_uint(gs) == __float_as_uint(ls);
+                if (__ballot(!same) != 0ull && !same) {
+                    pc_block_apx<0>(A.P, j, len, k0, mu, sig, (uint32_t)NB, np);
+                    lg = g;
+                    ls = gs;
+                    le = mu;
+                    les = sig;
+                }
+            }
+            __syncthreads();
+            double a = 1.0, bm = 0.0, bsv = 0.0;
+            bool mm = false;
+            if ((int)j < nbe - 1 && t < PC_TPB - 1) {
+                const float gn = L.gg[t + 1], gsn = L.gsg[t + 1];
+                mm = __float_as_uint(le) != __float_as_uint(gn) || __float_as_uint(les) != __float_as_uint(gsn);
+                bm = (double)le - (double)gn;
+                bsv = (double)les - (double)gsn;
+            }
+            if ((int)j < nbe - 1) {
+                const uint32_t k1 = k0 + len - 1u;
+                float af = (float)(k0 - 1u) * __builtin_amdgcn_rcpf((float)k1);
+                if (have_o && g != go) {
+                    const float sl = (le - eo) * __builtin_amdgcn_rcpf(g - go);
+                    if (sl >= 0.0f && sl <= 1.0f) af = sl;
+                }
+                a = (double)af;
+            }
+            go = g;
+            eo = le;
+            have_o = true;
+            pcg2_scan(A, L, grid, parity, nbe, a, bm, bsv, mm, g, gs, le, les, false, dm, ds, first);
+            parity ^= 1;
+            if (first == NB) {
+                if (phase == 0) break;   // stage 1's fixed point (sig steps uncertified): verify it exactly
+                if (j == (uint32_t)(nbe - 1)) {
+                    A.st[A.b].conv_w = itk_conv(le, les, n);
+                    A.st[A.b].conv_bound = 0;
+                }
+                done = true;
+                break;
+            }
+            if (r == cap - 1) break;
+            g = dm == 0.0 ? g : (float)((double)g + dm);
+            gs = ds == 0.0 ? gs : (float)((double)gs + ds);
+        }
+    }
+#ifdef PCG_PROF
+    if (j == 0) printf("PCG2 n %lld G %d L %u stage0 %d stage1+B %d done %d\n", (long long)n, (int)gridDim.x, m.L,
+                       rs1 + 1, round - rs1, (int)done);
+#endif
+    if (!done) {   // round cap: serial from the first failing transition (ends exact up to it); its
+        // predecessors' ends are in the published records only at workgroup edges, so the grid
+        // publishes every end first
+        float *const E = A.E;
+        E[j] = le;
+        E[(size_t)NB + j] = les;
+        grid.sync();
+        if (j == 0) {
+            float mu = E[first], sig = E[(size_t)NB + first];
+            for (int jb = first + 1; jb < nbe; ++jb) {
+                const uint32_t l = pc_len(m, jb);
+                double kd = (double)pc_k0(m, jb);
+                for (uint32_t s = 0; s < l; ++s, kd += 1.0) pc_step(kd, A.P[(size_t)s * NB + jb], mu, sig);
+            }
+            A.st[A.b].conv_w = itk_conv(mu, sig, n);
+            A.st[A.b].conv_bound = 0;
+        }
+    }
+}
+

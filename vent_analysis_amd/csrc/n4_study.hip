@@ -1126,6 +1126,525 @@ __global__ void __launch_bounds__(ST_TPB, 4) k_n4_study(StudyArgs a) {
     }
 }
 
+// =============================================================================================
+// Grid form (round 6): ONE study over G cooperating workgroups (k_n4_studyg, a cooperative launch)
+// =============================================================================================
+// The per-iteration sweep launches of the sweep driver (~10 per iteration, plus the host's flag
+// reads) carried one large study (config 2, 256x256x24; the class's one-study calls): its kernels
+// were short and the launches, gaps and host round trips set the time.  Here the whole multi-level
+// loop of one study runs in one launch, as k_n4_study does for a batch, with the study's items
+// dealt over G workgroups.  Every workgroup keeps its own copy of the small state in LDS (tables,
+// lattice, E map, P1) and computes it redundantly from the same integer sums, so the copies stay
+// identical; only order-free integer sums cross workgroups:
+//   hist  each workgroup's packed LDS histogram of its slice of compact U, unpacked into counts and
+//         o-weight sums and added to the global sums of this iteration's parity (integer atomics)
+//   fit   each workgroup's 128-bit fixed-point LDS numerators added to the global numerators of
+//         this iteration's parity (carry-correct 64-bit atomics, fix128_flush)
+//   range each workgroup's Range3 of its items (a plain record per workgroup; merging is order-free)
+//   S7    the grid PC (n4_shared.h pcg2_body) over all G x 1024 threads, d read in raster order
+// with a grid barrier after hist, fit, eval and S7 (and the PC's own rounds).  A buffer of one
+// parity is zeroed (each workgroup its slice) two barriers after its last read, so no pass needs a
+// clearing launch.  Results are bit-identical to k_n4_study / the oracle: the same per-item code,
+// the same item-order reductions (the exact CoV sums go through global memory in item order).
+struct StudyGrid {
+    unsigned long long *hsum;  // [2 parity][2][VH_MAX_BINS]: bin counts, then o-weight sums
+    unsigned long long *nsum;  // [3][2 * lat_cap]: fixed-point numerators by parity; [2]: denominators
+    float4 *rrec;              // [ST_NB][G]: each workgroup's Range3 of U buffer u
+    double *ipart;             // [nitems][2]: exact-CoV item sums (conv_mode 1)
+    Pcg2Args pc;               // the grid PC: P, wg, E (this study's scratch), sc, st, b
+};
+
+// 128-bit fixed-point partial (l, h) added to a global accumulator (fix128_add's carry rule)
+__device__ __forceinline__ void fix128_flush(unsigned long long *glo, unsigned long long *ghi,
+                                             unsigned long long l, unsigned long long h) {
+    if (l == 0ull && h == 0ull) return;
+    const unsigned long long old = atomicAdd(glo, l);
+    const unsigned long long carry = old + l < old ? 1ull : 0ull;
+    atomicAdd(ghi, h + carry);
+}
+
+// The c-th item of workgroup r in the largest-first order: items dealt in snake order (round q
+// forward when q is even, backward when odd), so every workgroup's share has about the same rows
+__device__ __forceinline__ int owned_item(int c, int r, int G, int nitems) {
+    const int pos = (c & 1) ? G - 1 - r : r;
+    const int k = c * G + pos;
+    return k < nitems ? k : -1;
+}
+__device__ __forceinline__ int next_item_g(StudyMisc &M, const int32_t *ordr, int nitems, int r, int G) {
+    int c = 0;
+    if ((threadIdx.x & 63) == 0) c = atomicAdd(&M.item_ctr, 1);
+    c = uni(__shfl(c, 0, 64));
+    const int k = owned_item(c, r, G, nitems);
+    return k < 0 ? -1 : uni(ordr[k]);
+}
+
+// wave 0: this workgroup's items' Range3 merged, as record rrec[u][r]
+__device__ void publish_range(const StudyGrid &g, const float4 *rp, const int32_t *ordr, int nitems, int u,
+                              int r, int G) {
+    if (threadIdx.x >= 64) return;
+    const int lane = threadIdx.x;
+    Range3 rg;
+    r3_init(rg);
+    for (int c = lane;; c += 64) {
+        const int k = owned_item(c, r, G, nitems);
+        if (k < 0) break;
+        const float4 p = rp[ordr[k]];
+        Range3 o;
+        o.mx = p.x; o.m1 = p.y; o.m2 = p.z; o.m3 = p.w;
+        r3_merge(rg, o);
+    }
+    rg = r3_wave(rg);
+    if (lane == 0) g.rrec[(size_t)u * G + r] = make_float4(rg.mx, rg.m1, rg.m2, rg.m3);
+}
+
+__global__ void __launch_bounds__(ST_TPB, 4) k_n4_studyg(StudyArgs a, StudyGrid gd) {
+    namespace cg = cooperative_groups;
+    cg::grid_group grid = cg::this_grid();
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    __shared__ Pcg2Lds PL;
+    const int64_t b = a.vol0;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int r = blockIdx.x, G = gridDim.x;
+    StudyMisc &M = *reinterpret_cast<StudyMisc *>(smem + a.o_misc);
+    float *sE = reinterpret_cast<float *>(smem + a.o_E);
+    float *lat = reinterpret_cast<float *>(smem + a.o_lat);
+    float4 *const rpart0 = reinterpret_cast<float4 *>(smem + a.o_rpart);   // [2][nitems] (own items)
+    int32_t *ordr = reinterpret_cast<int32_t *>(smem + a.o_order);
+    char *scr = smem + a.o_scr;
+
+    const int64_t n = a.sc[b].n_mask1;
+    N4State *stb = a.st + b;
+    if (r == 0 && t == 0) {
+        stb->t_start = wall_clock64();
+        stb->hw_id = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+        stb->xcc_id = __builtin_amdgcn_s_getreg((15 << 11) | 20);
+    }
+    const DevLevel &lvl = a.lvs->lv[a.nlev - 1];
+    const int p1last = lvl.ax[0].ncp * lvl.ax[1].ncp * a.Z;
+    if (n < 2) {   // no fit: zero field, no iterations (uniform over the grid)
+        if (r == 0) {
+            for (int e = t; e < p1last; e += ST_TPB) a.P1out[b * a.q2cap + e] = 0.0;
+            if (t < VH_MAX_LEVELS) {
+                stb->iters_level[t] = 0;
+                stb->conv_level[t] = 0.0f;
+            }
+            if (t == 0) stb->t_end = wall_clock64();
+        }
+        return;
+    }
+    Grp g;
+    g.w = wv;
+    g.nw = ST_WAVES;
+    g.t = t;
+    g.n = ST_TPB;
+    float *Lb = a.L0 + b * a.VS;
+    const int64_t fm = a.sc[b].first_masked;
+    unsigned long long *numfix = reinterpret_cast<unsigned long long *>(scr);
+    double *const P1 = reinterpret_cast<double *>(scr);
+    float *const Tg0 = a.Tg + (size_t)b * 2 * a.tcap;
+    FitRing ring;
+    ring.q = reinterpret_cast<double *>(scr + a.o_wave) + (size_t)g.w * a.nb_ring * a.s_cap;
+    ring.sx = nullptr;
+    ring.rowcap = a.s_cap;
+    ring.nr = 0;
+    double *const Wk3 = reinterpret_cast<double *>(smem + a.o_wk);
+    double2 *V = reinterpret_cast<double2 *>(scr), *F = V + ST_FFT_N, *DEN = F + ST_FFT_N;
+    double2 *TW = DEN + ST_FFT_N;
+    unsigned long long *Hc = reinterpret_cast<unsigned long long *>(DEN);
+    const PcMap pm = pc_map(n, 256);
+    const int bins = a.bins;
+    unsigned long long *const NSd = gd.nsum + (size_t)2 * 2 * a.lat_cap;   // denominators
+
+    if (t == 0) {
+        M.item_ctr = 0;
+        M.uin = 0;
+    }
+    if (wv == 0) find_first(a, b, fm, M);
+    {   // the largest-first item order (every workgroup computes the same one)
+        int32_t *isz = reinterpret_cast<int32_t *>(scr);
+        for (int item = wv; item < a.nitems; item += ST_WAVES) {
+            Item it;
+            const bool any = study_item(it, a, b, item);
+            if (lane == 0) isz[item] = any ? it.xe - it.xs + 1 : 0;
+        }
+        __syncthreads();
+        for (int i = t; i < a.nitems; i += ST_TPB) {
+            const int si = isz[i];
+            int rank = 0;
+            for (int j = 0; j < a.nitems; ++j) {
+                const int sj = isz[j];
+                rank += (sj > si || (sj == si && j < i)) ? 1 : 0;
+            }
+            ordr[rank] = i;
+        }
+    }
+    __syncthreads();
+    for (;;) {   // L0, U = L0 (U buffer 0) and its range, this workgroup's items
+        const int item = next_item_g(M, ordr, a.nitems, r, G);
+        if (item < 0) break;
+        Item it;
+        if (!study_item(it, a, b, item)) {
+            if (lane == 0) rpart0[item] = make_float4(-FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX);
+            continue;
+        }
+        init_item(a, b, it, item, Lb, a.U + b * a.VS, n, rpart0);
+    }
+    __syncthreads();
+    publish_range(gd, rpart0, ordr, a.nitems, 0, r, G);
+    {
+        const DevLevel &l0 = a.lvs->lv[0];
+        const int nl0 = l0.ax[0].ncp * l0.ax[1].ncp * l0.ax[2].ncp;
+        for (int e = t; e < nl0; e += ST_TPB) lat[e] = 0.0f;
+    }
+    int tpar = 0;   // Tg buffer of the last computed field's T windows
+    int gi = 0;     // iterations computed so far (all levels): the parity of the global sums
+    for (int L = 0; L < a.nlev; ++L) {
+        const DevLevel &lv = a.lvs->lv[L];
+        char *tabp = smem + a.o_tab;
+        load_tables(tab_w(tabp, a.R, a.C, a.Z, a.kcap), lv, a.R, a.C, a.Z);
+        const TabV T = tab_view(tabp, a.R, a.C, a.Z, a.kcap);
+        const int ncx = lv.ax[0].ncp, ncy = lv.ax[1].ncp, ncz = lv.ax[2].ncp;
+        const int nlat = ncx * ncy * ncz;
+        double *const Wk2 = Wk3 + (size_t)ncz * a.Z;
+        for (int e = t; e < ncz * a.Z; e += ST_TPB) {
+            Wk3[e] = lv.wk3[e];
+            Wk2[e] = lv.wk2[e];
+        }
+        double2 *const Wx3 = reinterpret_cast<double2 *>(smem + a.o_wx), *const Wx2 = Wx3 + 2 * a.R;
+        for (int x = t; x < a.R; x += ST_TPB) {
+            const double2 *w3 = reinterpret_cast<const double2 *>(lv.ax[0].w3i + 4 * x);
+            const double2 *w2 = reinterpret_cast<const double2 *>(lv.ax[0].w2 + 4 * x);
+            Wx3[2 * x] = w3[0];
+            Wx3[2 * x + 1] = w3[1];
+            Wx2[2 * x] = w2[0];
+            Wx2[2 * x + 1] = w2[1];
+        }
+        // ---- denominators of this level: the previous level's are read by nobody any more (every
+        // workgroup passed the last iteration's barriers); level 0's were zeroed by the host ----
+        if (L > 0) {
+            for (int e = r * ST_TPB + t; e < 2 * nlat; e += G * ST_TPB) NSd[e] = 0ull;
+            grid.sync();
+        }
+        for (int e = t; e < 2 * nlat; e += ST_TPB) numfix[e] = 0ull;
+        if (t == 0) M.item_ctr = 0;
+        __syncthreads();
+        {
+            float *const Ub = a.U + M.uin * a.half + b * a.VS;
+            for (;;) {
+                const int item = next_item_g(M, ordr, a.nitems, r, G);
+                if (item < 0) break;
+                Item it;
+                if (!study_item(it, a, b, item)) continue;
+                fit_item<1, true>(it, T, Wk2, Wx2, ncy, ncz, a.Z, bins, Ub, n, sE, 0.0f, 1.0, ring,
+                                  a.nb_ring, numfix);
+            }
+        }
+        __syncthreads();
+        for (int e = t; e < nlat; e += ST_TPB) fix128_flush(NSd + 2 * e, NSd + 2 * e + 1, numfix[2 * e], numfix[2 * e + 1]);
+        grid.sync();
+        {
+            int itn = 0;
+            int uin = M.uin;
+            for (;;) {
+                float *const Ub = a.U + uin * a.half + b * a.VS;
+                const int p = gi & 1;
+                unsigned long long *const HS = gd.hsum + (size_t)p * 2 * VH_MAX_BINS;
+                unsigned long long *const HSo = gd.hsum + (size_t)(p ^ 1) * 2 * VH_MAX_BINS;
+                unsigned long long *const NS = gd.nsum + (size_t)p * 2 * a.lat_cap;
+                unsigned long long *const NSo = gd.nsum + (size_t)(p ^ 1) * 2 * a.lat_cap;
+                if (g.w == 0) {   // ctrl (every workgroup, the same decision): the grid's records
+                    Range3 rr;
+                    r3_init(rr);
+                    for (int i = lane; i < G; i += 64) {
+                        const float4 q = gd.rrec[(size_t)uin * G + i];
+                        Range3 o;
+                        o.mx = q.x; o.m1 = q.y; o.m2 = q.z; o.m3 = q.w;
+                        r3_merge(rr, o);
+                    }
+                    rr = r3_wave(rr);
+                    if (lane < M.nfirst) M.fu[lane] = Ub[M.foff[lane]];
+                    double sd = 0.0, sd2 = 0.0;   // S7x: the item sums in item order (k_n4_study's order)
+                    if (a.conv_mode == 1 && itn > 0) {
+                        for (int i = lane; i < a.nitems; i += 64) {
+                            sd += gd.ipart[2 * i];
+                            sd2 += gd.ipart[2 * i + 1];
+                        }
+                        for (int off = 32; off > 0; off >>= 1) {
+                            sd += __shfl_down(sd, off, 64);
+                            sd2 += __shfl_down(sd2, off, 64);
+                        }
+                    }
+                    wave_lds_order();
+                    if (lane == 0) {
+                        M.stop = 0;
+                        M.exact = 0;
+                        if (itn > 0) {
+                            M.conv = a.conv_mode == 1 ? conv_of(sd, sd2, (double)n) : (double)stb->conv_w;
+                            if (!(M.conv > (double)a.thresh) || itn >= a.lvs->max_iters[L]) M.stop = 1;
+                        }
+                        if (!M.stop) {
+                            float bmin;
+                            M.bmax = rr.mx;
+                            if (r3_bin_min(rr, M.fu, M.nfirst, bmin)) {
+                                M.bin_min = bmin;
+                                M.slope = (rr.mx - bmin) / (float)(bins - 1);
+                            } else {
+                                M.exact = 1;
+                            }
+                        }
+                    }
+                }
+                __syncthreads();
+                if (M.stop) break;
+                if (M.exact) {   // rare: every workgroup scans the study itself
+                    float *s_cmax = reinterpret_cast<float *>(scr);
+                    const float m = exact_min_study(a, b, Ub, s_cmax, s_cmax + g.n, g, M);
+                    if (g.t == 0) {
+                        M.bin_min = m;
+                        M.slope = (M.bmax - m) / (float)(bins - 1);
+                    }
+                    __syncthreads();
+                }
+                const int itk = itn + 1;
+                const float bmin = M.bin_min, slope = M.slope;
+                const double rinv = 1.0 / (double)slope;
+                // ---- hist (S3): this workgroup's slice of compact U, then the grid's integer sums ----
+                for (int i = g.t; i < ST_HC * VH_MAX_BINS; i += g.n) Hc[i] = 0ull;
+                __syncthreads();
+                {
+                    unsigned long long *H = Hc + (lane & (ST_HC - 1)) * VH_MAX_BINS;
+                    const int64_t hchunk = ((n + G - 1) / G + 15) / 16 * 16;   // (16-aligned slices)
+                    const int64_t h0 = (int64_t)r * hchunk, h1 = min(n, h0 + hchunk);
+                    for (int64_t j0 = h0 + (int64_t)g.t * 16; j0 < h1; j0 += (int64_t)g.n * 16) {
+                        float u[16];
+                        if (j0 + 16 <= h1) {
+#pragma unroll
+                            for (int q = 0; q < 4; ++q) {
+                                const float4 v = reinterpret_cast<const float4 *>(Ub + j0)[q];
+                                u[4 * q] = v.x; u[4 * q + 1] = v.y; u[4 * q + 2] = v.z; u[4 * q + 3] = v.w;
+                            }
+                        } else {
+#pragma unroll
+                            for (int k = 0; k < 16; ++k) u[k] = j0 + k < h1 ? Ub[j0 + k] : __int_as_float(0x7fc00000);
+                        }
+#pragma unroll
+                        for (int k = 0; k < 16; ++k) {
+                            int idx;
+                            const unsigned long long w = hist_pack(u[k], bmin, rinv, bins, idx);
+                            atomicAdd(&H[idx], w);
+                        }
+                    }
+                }
+                __syncthreads();
+                for (int h = t; h < bins; h += ST_TPB) {
+                    unsigned long long cs = 0ull, os = 0ull;
+#pragma unroll
+                    for (int q = 0; q < ST_HC; ++q) {
+                        const unsigned long long w = Hc[q * VH_MAX_BINS + h];
+                        cs += hist_count(w);
+                        os += hist_osum(w);
+                    }
+                    if (cs) atomicAdd(HS + h, cs);
+                    if (os) atomicAdd(HS + VH_MAX_BINS + h, os);
+                }
+                grid.sync();
+                // the other parity's sums were last read by the previous iteration's E map
+                for (int e = r * ST_TPB + t; e < 2 * VH_MAX_BINS; e += G * ST_TPB) HSo[e] = 0ull;
+                // ---- emap (k_n4_study's arithmetic on the grid's sums) ----
+                {
+                    const int P = VH_FFT_P, off = (P - bins) / 2;
+                    const float sFWHM = a.fwhm / slope;
+                    const float ef = (float)(4.0 * LN2 / (double)(sFWHM * sFWHM));
+                    const float sf = (float)(2.0 * sqrt(LN2 / PI_D) / (double)sFWHM);
+                    const double2 twv = g.t < P / 2 ? a.tw[g.t] : make_double2(0.0, 0.0);
+                    for (int i = g.t; i < P; i += g.n) {
+                        const int h = i - off;
+                        unsigned long long s = 0ull;
+                        if (h >= 0 && h < bins) {
+                            s = (HS[h] << 24) - HS[VH_MAX_BINS + h];
+                            if (h > 0) s += HS[VH_MAX_BINS + h - 1];
+                        }
+                        V[fpad(i)] = make_double2((double)s * (1.0 / 16777216.0), 0.0);
+                        double fx;
+                        if (i == 0) {
+                            fx = (double)sf;
+                        } else if (i == P / 2) {
+                            fx = (double)sf * exp(-0.25 * (double)((float)P * (float)P) * (double)ef);
+                        } else {
+                            const float nf = (float)(i < P / 2 ? i : P - i);
+                            fx = (double)(sf * expf_cr_tail(-(nf * nf) * ef));
+                        }
+                        F[fpad(i)] = make_double2(fx, 0.0);
+                    }
+                    if (g.t < P / 2) TW[g.t] = twv;
+                    __syncthreads();
+                    if (g.w < 2) wave_fft_lds(g.w ? F : V, TW, false, FftId(), FftId());
+                    __syncthreads();
+                    for (int i = g.t; i < P; i += g.n) {
+                        const double2 f = F[fpad(i)], v = V[fpad(i)];
+                        const double fa = f.x, fb = f.y;
+                        const double gg = fa / ((fa * fa - (-fb) * fb) + (double)a.noise);
+                        V[fpad(i)] = make_double2(v.x * gg, v.y * gg);
+                    }
+                    __syncthreads();
+                    if (g.w == 0) wave_fft_lds(V, TW, true, FftId(), FftId());
+                    __syncthreads();
+                    for (int i = g.t; i < P; i += g.n) {
+                        const double ur = V[fpad(i)].x > 0.0 ? V[fpad(i)].x : 0.0;
+                        const float c = bmin + ((float)i - (float)off) * slope;
+                        DEN[fpad(i)] = make_double2(ur, 0.0);
+                        V[fpad(i)] = make_double2((double)c * ur, 0.0);
+                    }
+                    __syncthreads();
+                    if (g.w < 2) wave_fft_lds(g.w ? DEN : V, TW, false, FftId(), FftId());
+                    __syncthreads();
+                    for (int e = g.t; e < 2 * P; e += g.n) {
+                        double2 *const x = e < P ? V : DEN;
+                        const int i = e < P ? e : e - P;
+                        const double2 f = F[fpad(i)], v = x[fpad(i)];
+                        x[fpad(i)] = make_double2(v.x * f.x - v.y * f.y, v.x * f.y + v.y * f.x);
+                    }
+                    __syncthreads();
+                    if (g.w < 2) wave_fft_lds(g.w ? DEN : V, TW, true, FftId(), FftId());
+                    __syncthreads();
+                    for (int i = g.t; i < bins; i += g.n) {
+                        const double d = DEN[fpad(i + off)].x;
+                        sE[i] = d != 0.0 ? (float)(V[fpad(i + off)].x / d) : 0.0f;
+                    }
+                    __syncthreads();
+                }
+                // ---- fit: this workgroup's items into LDS, then into the grid's numerators ----
+                for (int e = g.t; e < 2 * nlat; e += g.n) numfix[e] = 0ull;
+                if (g.t == 0) M.item_ctr = 0;
+                __syncthreads();
+                for (;;) {
+                    const int item = next_item_g(M, ordr, a.nitems, r, G);
+                    if (item < 0) break;
+                    Item it;
+                    if (!study_item(it, a, b, item)) continue;
+                    fit_item<0, true>(it, T, Wk3, Wx3, ncy, ncz, a.Z, bins, Ub, n, sE, bmin, rinv, ring,
+                                      a.nb_ring, numfix);
+                }
+                __syncthreads();
+                for (int e = t; e < nlat; e += ST_TPB)
+                    fix128_flush(NS + 2 * e, NS + 2 * e + 1, numfix[2 * e], numfix[2 * e + 1]);
+                grid.sync();
+                // ---- lattice update and P1 (each workgroup its own copy, from the grid's sums) ----
+                for (int e = g.t; e < nlat; e += g.n) {
+                    const double d = fix128_get(NSd + 2 * e, NSd + 2 * e + 1);
+                    const double num = fix128_get(NS + 2 * e, NS + 2 * e + 1);
+                    const float phi = d != 0.0 ? (float)(num / d) : 0.0f;
+                    lat[e] += phi;
+                }
+                // the other parity's numerators were last read by the previous iteration's update
+                for (int e = r * ST_TPB + t; e < 2 * nlat; e += G * ST_TPB) NSo[e] = 0ull;
+                __syncthreads();
+                for (int e = g.t; e < ncx * ncy * a.Z; e += g.n) {
+                    const int ij = e / a.Z, z = e % a.Z;
+                    const float4 w = T.wz[z];
+                    const float *l = lat + ij * ncz + T.bz[z];
+                    P1[e] = (double)w.x * (double)l[0] + (double)w.y * (double)l[1] +
+                            (double)w.z * (double)l[2] + (double)w.w * (double)l[3];
+                }
+                if (g.t == 0) M.item_ctr = 0;
+                __syncthreads();
+                // ---- eval: this workgroup's items; U into the other buffer, d in raster order ----
+                const int uo = (uin + 1) % ST_NB;
+                {
+                    float *const Uo = a.U + uo * a.half + b * a.VS;
+                    float *const Dw = a.D + b * a.VS;
+                    float4 *const rp_out = rpart0 + uo * a.nitems;
+                    const bool first_of_level = itk == 1;
+                    const bool bo_mode = !(L == 0 && first_of_level);
+                    const bool same = !(first_of_level && L > 0);
+                    TabV To = T;
+                    int ncxo = ncx;
+                    if (!same) {
+                        const DevLevel &lo = a.lvs->lv[L - 1];
+                        To.wx = reinterpret_cast<const float4 *>(lo.ax[0].w);
+                        To.bx = lo.ax[0].base;
+                        ncxo = lo.ax[0].ncp;
+                    }
+                    float *const Tgn = Tg0 + (size_t)(tpar ^ 1) * a.tcap;
+                    const float *const Tgo = Tg0 + (size_t)tpar * a.tcap;
+                    for (;;) {
+                        const int item = next_item_g(M, ordr, a.nitems, r, G);
+                        if (item < 0) break;
+                        Item it;
+                        if (!study_item(it, a, b, item)) {
+                            if (lane == 0) {
+                                gd.ipart[2 * item] = 0.0;
+                                gd.ipart[2 * item + 1] = 0.0;
+                                rp_out[item] = make_float4(-FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX);
+                            }
+                            continue;
+                        }
+#define STG_EVAL(S, CM) eval_item<S, CM>(it, item, a.Z, a.CZ, T, To, ncx, ncy, ncxo, P1, Tgn, Tgo, bo_mode, \
+                                         Lb, Uo, Dw, n, gd.ipart, rp_out, pm)
+                        if (a.conv_mode == 0) {
+                            if (same) STG_EVAL(true, 0);
+                            else STG_EVAL(false, 0);
+                        } else {
+                            if (same) STG_EVAL(true, 1);
+                            else STG_EVAL(false, 1);
+                        }
+#undef STG_EVAL
+                    }
+                    __syncthreads();
+                    publish_range(gd, rpart0 + uo * a.nitems, ordr, a.nitems, uo, r, G);
+                }
+                grid.sync();
+                if (a.conv_mode == 0) {   // S7: the grid PC over every workgroup, d in raster order
+                    Pcg2Args A = gd.pc;
+                    A.skip_thresh = itk < a.lvs->max_iters[L] ? a.thresh : 0.0f;
+                    const float *const Dr = a.D + b * a.VS;
+                    pcg2_body(A, PL, grid, [=](int64_t q) { return Dr[q]; });
+                    grid.sync();   // conv_w (one thread's store) to every workgroup
+                }
+                tpar ^= 1;
+                uin = uo;
+                itn = itk;
+                ++gi;
+            }
+            if (g.t == 0) {
+                M.itn = itn;
+                M.uin = uin;
+            }
+        }
+        __syncthreads();
+        if (r == 0 && t == 0) {
+            stb->iters_level[L] = M.itn;
+            stb->conv_level[L] = (float)M.conv;
+        }
+        if (L < a.nlev - 1) {   // exact subdivision of the lattice for the next level (every copy)
+            const int nl_max = lvl.ax[0].ncp * lvl.ax[1].ncp * lvl.ax[2].ncp;
+            float *T1 = reinterpret_cast<float *>(scr), *T2 = T1 + nl_max;
+            refine_axis_st(lat, T1, ncx, ncy, ncz, 0);
+            __syncthreads();
+            refine_axis_st(T1, T2, 2 * ncx - 3, ncy, ncz, 1);
+            __syncthreads();
+            refine_axis_st(T2, lat, 2 * ncx - 3, 2 * ncy - 3, ncz, 2);
+            __syncthreads();
+        }
+    }
+    if (r == 0) {   // final field's P1 for k_n4_final
+        const TabV T = tab_view(smem + a.o_tab, a.R, a.C, a.Z, a.kcap);
+        const int ncz = lvl.ax[2].ncp;
+        for (int e = t; e < p1last; e += ST_TPB) {
+            const int ij = e / a.Z, z = e % a.Z;
+            const float4 w = T.wz[z];
+            const float *l = lat + ij * ncz + T.bz[z];
+            a.P1out[b * a.q2cap + e] = (double)w.x * (double)l[0] + (double)w.y * (double)l[1] +
+                                       (double)w.z * (double)l[2] + (double)w.w * (double)l[3];
+        }
+        if (t == 0) {
+            stb->conv = M.conv;
+            stb->active = 0;
+            stb->t_end = wall_clock64();
+        }
+    }
+}
+
 // Workgroup -> study, the largest study (most mask == 1 voxels, the best a-priori proxy of its
 // cost) first, ties by index: the dispatcher starts workgroups in order, so when the CUs are
 // shared with another batch's launch (batches in flight) the long studies start first and the
@@ -1155,7 +1674,11 @@ struct StudyLayout {
     StudyArgs a;
 };
 
-static bool study_layout(const vh_batch *b, const vh_n4_params &prm, StudyLayout &out) {
+// grid = true: the grid form's per-workgroup layout (k_n4_studyg): no item partials of the exact CoV
+// in LDS (they go to global memory), no PC area (the grid PC's LDS is static), the budget less that
+// static area, and the packed-histogram bound per workgroup (<= V / G values) instead of per study.
+static bool study_layout(const vh_batch *b, const vh_n4_params &prm, StudyLayout &out, bool grid = false,
+                         int G = 1) {
     StudyArgs &a = out.a;
     std::memset(&a, 0, sizeof(a));
     const int R = (int)b->R, C = (int)b->C, Z = (int)b->Z;
@@ -1188,7 +1711,7 @@ static bool study_layout(const vh_batch *b, const vh_n4_params &prm, StudyLayout
     const size_t fit_num = 2 * sizeof(unsigned long long) * (size_t)nlat_max;
     const size_t fit = ((fit_num + 15) & ~(size_t)15) + sizeof(double) * fit_waves * nb_ring * (size_t)s_cap;
     const size_t exact = sizeof(float) * 2 * ST_TPB;
-    const size_t pcs = prm.conv_mode == 0 ? pcw_lds_bytes<ST_TPB>() : 0;
+    const size_t pcs = prm.conv_mode == 0 && !grid ? pcw_lds_bytes<ST_TPB>() : 0;
     const size_t p1 = sizeof(double) * (size_t)p1_max;   // the new field's P1, lattice update to eval
     const size_t scr = std::max({refine, emap, fit, exact, pcs, p1});
     auto A = [](size_t v) { return (v + 15) & ~(size_t)15; };
@@ -1199,7 +1722,7 @@ static bool study_layout(const vh_batch *b, const vh_n4_params &prm, StudyLayout
     a.o_lat = (int32_t)o; o += A(sizeof(float) * nlat_max);
     const int64_t nslots = (b->R + SLOT_R - 1) / SLOT_R;
     const int64_t nitems = b->n4_tiles * nslots;
-    a.o_ipart = (int32_t)o; o += A(sizeof(double) * 2 * (size_t)nitems);
+    a.o_ipart = (int32_t)o; o += grid ? 0 : A(sizeof(double) * 2 * (size_t)nitems);
     a.o_rpart = (int32_t)o; o += A(sizeof(float4) * ST_NB * (size_t)nitems);
     a.o_order = (int32_t)o; o += A(sizeof(int32_t) * (size_t)nitems);
     a.o_misc = (int32_t)o; o += A(sizeof(StudyMisc));
@@ -1213,7 +1736,10 @@ static bool study_layout(const vh_batch *b, const vh_n4_params &prm, StudyLayout
     a.nslots = (int32_t)nslots;
     a.nitems = (int32_t)nitems;
     out.bytes = o;
-    // packed histogram bins stay exact below 2^20 values per study (hist_pack)
+    // packed histogram bins stay exact below 2^20 values per workgroup (hist_pack)
+    if (grid)
+        return geom_ok && o + sizeof(Pcg2Lds) <= ST_MAX_LDS && prm.n_levels <= VH_MAX_LEVELS &&
+               (b->V + G - 1) / G + 16 < ((int64_t)1 << 20);
     return geom_ok && o <= ST_MAX_LDS && prm.n_levels <= VH_MAX_LEVELS && b->V < ((int64_t)1 << 20);
 }
 
@@ -1309,5 +1835,134 @@ void vh_launch_n4_study(vh_batch *b, const vh_n4_params &prm) {
     if (b->st_n4) {
         HIP_TRY(hipEventRecord(b->ev_n4_post, b->st_n4));
         HIP_TRY(hipStreamWaitEvent(b->stream, b->ev_n4_post, 0));
+    }
+}
+
+// ---- grid form (k_n4_studyg): one study per cooperative launch of G workgroups ----
+// G: about one item per wave (items / 16 workgroups), at most one workgroup per CU (the cooperative
+// launch needs the whole grid resident), at least V / 2^20 (the per-workgroup packed histogram).
+// VH_STG_G overrides (A/B runs).
+static int studyg_workgroups(const vh_batch *b, int nitems) {
+    int dev = 0, ncu = 0, per = 0;
+    HIP_TRY(hipGetDevice(&dev));
+    HIP_TRY(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)k_n4_studyg, ST_TPB, 0));
+    int G = (nitems + ST_WAVES - 1) / ST_WAVES;
+    if (const char *e = getenv("VH_STG_G")) G = atoi(e);
+    G = std::max<int>(G, (int)((b->V >> 20) + 1));
+    // one workgroup per CU at most whatever the occupancy query says (it can report one too many,
+    // and a cooperative grid that does not fit would never pass its first barrier)
+    G = std::min(G, ncu * std::min(std::max(per, 1), 1));
+    return std::max(G, 1);
+}
+
+bool vh_n4_studyg_eligible(const vh_batch *b, const vh_n4_params &prm, size_t *lds_bytes) {
+    if (b->n4_tiles == 0) return false;
+    StudyLayout L0;
+    study_layout(b, prm, L0);   // (item count)
+    const int G = studyg_workgroups(b, L0.a.nitems);
+    StudyLayout L;
+    const bool ok = study_layout(b, prm, L, true, G);
+    if (lds_bytes) *lds_bytes = L.bytes;
+    return ok;
+}
+
+void vh_launch_n4_studyg(vh_batch *b, const vh_n4_params &prm) {
+    StudyLayout L0;
+    study_layout(b, prm, L0);
+    const int G = studyg_workgroups(b, L0.a.nitems);
+    StudyLayout Ly;
+    if (!study_layout(b, prm, Ly, true, G)) throw VhError{VH_ERR_ARG, "N4 grid study kernel: LDS budget exceeded"};
+    StudyArgs a = Ly.a;
+    a.I = b->d_hp;
+    a.V = b->V;
+    a.L0 = b->d_L0;
+    a.U = b->d_U;
+    a.D = b->d_D;
+    a.half = b->nb * b->VS;
+    a.rs = b->d_rowstart;
+    a.rmask = b->d_rowmask;
+    a.rrs = b->d_rrank;
+    a.sc = b->d_sc;
+    a.st = b->d_st;
+    a.P1out = b->d_P1;
+    a.q2cap = b->q2_cap;
+    a.tw = b->d_twiddle;
+    a.VS = b->VS;
+    a.R = (int32_t)b->R;
+    a.C = (int32_t)b->C;
+    a.Z = (int32_t)b->Z;
+    a.CZ = (int32_t)b->CZ;
+    a.ntiles = (int32_t)b->n4_tiles;
+    a.nlev = prm.n_levels;
+    a.bins = prm.n_bins;
+    a.conv_mode = prm.conv_mode;
+    a.thresh = prm.conv_threshold;
+    a.fwhm = prm.fwhm;
+    a.noise = prm.wiener_noise;
+    StudyLevels h{};
+    for (int L = 0; L < prm.n_levels; ++L) {
+        h.max_iters[L] = prm.max_iters[L];
+        h.lv[L] = vh_dev_level(b, prm, L);
+    }
+    if (!b->d_study_lv) HIP_TRY(hipMalloc(&b->d_study_lv, sizeof(StudyLevels)));
+    HIP_TRY(hipMemcpyAsync(b->d_study_lv, &h, sizeof(StudyLevels), hipMemcpyHostToDevice, b->stream));
+    a.lvs = (const StudyLevels *)b->d_study_lv;
+    a.order = nullptr;
+    {
+        const int Lf = prm.n_levels - 1;
+        const int64_t cx = vh_level_ncp(prm, Lf, 0);
+        const int64_t nl = cx * vh_level_ncp(prm, Lf, 1) * vh_level_ncp(prm, Lf, 2);
+        if (!b->d_den || !b->d_T || b->lat_cap < nl || b->t_cap < cx * b->CZ)
+            throw VhError{VH_ERR_ARG, "N4 grid study kernel: workspace not prepared"};
+    }
+    a.den = b->d_den;
+    a.lat_cap = b->lat_cap;
+    a.Tg = b->d_T;
+    a.tcap = b->t_cap;
+    a.pcdrift = nullptr;
+    // per-launch global state: the sums of both parities and the denominators (zeroed here), the
+    // range records, the exact-CoV item sums, the grid PC's records / ends / p values
+    const int64_t NB = (int64_t)G * PC_TPB;
+    auto A256 = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    const size_t b_h = A256(sizeof(unsigned long long) * 2 * 2 * VH_MAX_BINS);
+    const size_t b_n = A256(sizeof(unsigned long long) * 3 * 2 * (size_t)b->lat_cap);
+    const size_t b_r = A256(sizeof(float4) * ST_NB * (size_t)G);
+    const size_t b_i = A256(sizeof(double) * 2 * (size_t)std::max<int32_t>(a.nitems, 1));
+    const size_t b_w = A256(sizeof(PcgWg) * 2 * (size_t)G);
+    const size_t b_e = A256(sizeof(float) * 2 * (size_t)NB);
+    const size_t b_p = A256(sizeof(float) * ((size_t)b->VS + (size_t)NB));   // (L + 1) NB <= n + NB
+    const size_t need = b_h + b_n + b_r + b_i + b_w + b_e + b_p;
+    if ((int64_t)need > b->stg_cap) {
+        if (b->d_stg) HIP_TRY(hipFree(b->d_stg));
+        b->d_stg = nullptr;
+        b->stg_cap = 0;
+        HIP_TRY(hipMalloc(&b->d_stg, need));
+        b->stg_cap = (int64_t)need;
+    }
+    vh_set_max_lds((const void *)k_n4_studyg, (int)(ST_MAX_LDS - sizeof(Pcg2Lds)));
+    ScopedKTimer tm(b, "n4_study", 0.0);
+    for (int64_t v = 0; v < b->nb; ++v) {   // one study per launch (the class and configs 2 / 5: one)
+        char *w = (char *)b->d_stg;
+        StudyGrid gd{};
+        gd.hsum = (unsigned long long *)w; w += b_h;
+        gd.nsum = (unsigned long long *)w; w += b_n;
+        gd.rrec = (float4 *)w; w += b_r;
+        gd.ipart = (double *)w; w += b_i;
+        gd.pc.wg = (PcgWg *)w; w += b_w;
+        gd.pc.E = (float *)w; w += b_e;
+        gd.pc.P = (float *)w;
+        gd.pc.D = nullptr;
+        gd.pc.perm = nullptr;
+        gd.pc.sc = b->d_sc;
+        gd.pc.st = b->d_st;
+        gd.pc.b = v;
+        gd.pc.skip_thresh = 0.0f;
+        HIP_TRY(hipMemsetAsync(b->d_stg, 0, b_h + b_n, b->stream));
+        StudyArgs av = a;
+        av.vol0 = v;
+        void *args[] = {&av, &gd};
+        HIP_TRY(hipLaunchCooperativeKernel((const void *)k_n4_studyg, dim3((unsigned)G), dim3(ST_TPB), args,
+                                           Ly.bytes, b->stream));
     }
 }

@@ -254,6 +254,8 @@ struct vh_batch {
     void *d_study_latg = nullptr;    // n4_study.hip depth 2: the lattice before the last two updates
     size_t study_latg_cap = 0;
     int64_t pcg_cap = 0;             // bytes of d_pcg
+    void *d_stg = nullptr;           // n4_study.hip grid form: global sums, records, grid-PC scratch
+    int64_t stg_cap = 0;             // bytes of d_stg
     void *d_sortg = nullptr;         // vdp.hip grid sort: per-chunk digit counts / offsets
     int64_t sortg_cap = 0;           // entries of d_sortg
     // CI workspace
