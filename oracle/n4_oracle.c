@@ -470,10 +470,15 @@ static float conv_welford(const float *d, int64_t n)
 /* S7 alone (tests/test_n4_oracle.py) */
 float n4o_conv_welford(const float *d, int64_t n) { return conv_welford(d, n); }
 
+/* (1 - 2^-24)^m rounded down by 2^-40 (n4_shared.h pc_accum_factor, the same expression) */
+static double pc_accum_factor(double m) { return exp(m * log1p(-0x1p-24)) * (1.0 - 0x1p-40); }
+
 /* The lower bound of the float sig that PC's certified decision uses (vent_analysis_amd/csrc/
  * n4_shared.h pcw_run, after stage 0): nb blocks of consecutive steps, block j's float sum
  * B_j = fma(q, q, B_j) of q = (float)(p - mu) along the exact mu trajectory, weighted by
- * 1 - 1/min(k0_j, 2^24), summed in double in block order, times 1 - (n + L + 8) 2^-24.  Returns the
+ * 1 - 1/min(k0_j, 2^24), summed in double in block order, times (1 - 2^-24)^(n + L + 8)
+ * (pc_accum_factor: the float accumulation of n positive terms keeps at least that fraction of
+ * their exact sum; round 6, before: the linear 1 - (n + L + 8) 2^-24, negative past 2^24).  Returns the
  * true float sig of the recurrence in *sig and the bound in *lo (tests/test_n4_oracle.py checks
  * lo <= sig on oracle d sequences). */
 void n4o_pc_sig_bound(const float *d, int64_t n, int nb, double *lo, float *sig_out, float *mu_out)
@@ -498,7 +503,7 @@ void n4o_pc_sig_bound(const float *d, int64_t n, int nb, double *lo, float *sig_
         }
         if (k0 > 1) tot += (double)B * (1.0 - 1.0 / fmin((double)k0, 16777216.0));
     }
-    *lo = tot * (1.0 - ((double)n + (double)L + 8.0) * 0x1p-24);
+    *lo = tot * pc_accum_factor((double)n + (double)L + 8.0);
     *sig_out = sig;
     *mu_out = mu;
 }
@@ -560,7 +565,7 @@ void n4o_pc_pre_bound(const float *d, int64_t n, int nb, double *lo_out, float *
         }
         tot += acc * (1.0 - 1.0 / fmax((double)k0, 2.0));
     }
-    *lo_out = tot * (1.0 - ((double)n + 8.0) * 0x1p-24 - 0x1p-40);
+    *lo_out = tot * pc_accum_factor((double)n + 8.0);
     const double mn = 1.0 + Pk / (double)n;
     const double hi = mn + cD * ((double)n + 3.0) + fabs(mn - 1.0) * 0x1p-50 + 0x1p-50;
     float f = (float)hi;

@@ -205,3 +205,33 @@ def test_pc_sig_lower_bound(tmp_path, monkeypatch, shape, seed, nb):
         assert lo.value > 0.95 * sig.value          # tight enough to decide most iterations
         its += 1
     assert its >= 4
+
+
+def test_pc_sig_lower_bound_past_2_24_steps():
+    """The certified decision's accumulation factor (1 - 2^-24)^(n + L + 8) (round 6, pc_accum_factor)
+    stays a lower bound past 2^24 steps, where the float counter N freezes and the float sum of the
+    sig increments swamps: on a config-5-sized sequence (2^25 + 12345 steps, d ~ N(0, 0.02), the grid
+    PC's 262144 blocks) the bound is positive and below ITK's float sig (the linear factor it
+    replaces, 1 - (n + L + 8) 2^-24, is negative there: no decision was possible)."""
+    import ctypes as ct
+    n = (1 << 25) + 12345
+    rng = np.random.default_rng(5)
+    d = (rng.standard_normal(n) * 0.02).astype(np.float32)
+    L = native.lib()
+    L.n4o_pc_sig_bound.restype = None
+    lo, sig, mu = ct.c_double(), ct.c_float(), ct.c_float()
+    nb = 262144
+    L.n4o_pc_sig_bound(d.ctypes.data_as(ct.POINTER(ct.c_float)), ct.c_int64(n), ct.c_int(nb),
+                       ct.byref(lo), ct.byref(sig), ct.byref(mu))
+    assert 1.0 - (n + n // nb + 8.0) * 2.0 ** -24 < 0.0      # the old factor: no bound at all
+    assert 0.0 < lo.value <= sig.value, (lo.value, sig.value)
+    f = np.exp((n + n // nb + 8.0) * np.log1p(-2.0 ** -24))
+    assert 0.1 < f < 0.2                                       # (1 - 2^-24)^n ~ e^-2
+
+
+@pytest.mark.parametrize("m", [1.0, 1e3, 1e6, 2.0 ** 23, 2.0 ** 24, 3e7])
+def test_pc_accum_factor_dominates_linear(m):
+    """(1 - u)^m >= 1 - m u (Bernoulli): the decisions only get stronger, and the factor is positive."""
+    u = 2.0 ** -24
+    f = np.exp(m * np.log1p(-u)) * (1.0 - 2.0 ** -40)
+    assert f > 0.0 and f >= 1.0 - m * u - 2.0 ** -39

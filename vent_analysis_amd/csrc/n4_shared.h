@@ -554,6 +554,15 @@ __device__ __forceinline__ bool r3_bin_min(const Range3 &r, const float *u, int 
 //     exact: 24 x 24 bits), then the 64 steps sig <- (float)(sig + t), systolic.
 // ---------------------------------------------------------------------------------------------
 #define ITK_NMAX 16777216.0   // 2^24: float N += 1.0 stops growing there (2^24 + 1 rounds to 2^24)
+// The certified decisions' accumulation factor (round 6): a float running sum of m positive terms,
+// each step rounded once (relative error <= 2^-24 of that step's sum), keeps at least (1 - 2^-24)^m
+// of their exact sum -- s_m = sum_k t_k prod_{j >= k} (1 + delta_j) >= (1 - 2^-24)^m sum_k t_k --
+// rounded down here by a 2^-40 margin (exp / log1p are within a few double ulps).  By Bernoulli it
+// is >= the linear form 1 - m 2^-24 the decisions used before, and unlike that form it stays
+// positive for m > 2^24 (config 5's 28 M-voxel iterations, where the linear form was < 0).
+__host__ __device__ inline double pc_accum_factor(double m) {
+    return exp(m * log1p(-0x1p-24)) * (1.0 - 0x1p-40);
+}
 __device__ __forceinline__ double itk_Nd(double k) { return fmin(k, ITK_NMAX); }
 // the measure from the final state after n steps
 __device__ __forceinline__ float itk_conv(float mu, float sig, int64_t n) {
@@ -1834,8 +1843,8 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
         // |delta_i| i / k <= D_k = 2^-25 M (k + 3)(1 + 2^-20) with M >= |mu_i|, |p_i| for every i
         // (below; every p in (0.5, 1.9), which also keeps the sums of p - 1 exact).  Then |q_k| >= (|p_k - m_(k-1)| - D_(k-1))(1 - 2^-24), and
         // with the bounds of the certified decision below (t_k >= q^2 (1 - 1/N)(1 - 2^-24)(1 -
-        // 2^-52)^2, S >= (1 - n 2^-24) sum t_k) lo = sum over blocks of (1 - 1/max(k0, 2)) sum_k
-        // max(0, |p_k - m_(k-1)| - D_(k-1) - eps_k)^2 (1 - (n + 8) 2^-24) bounds ITK's float sig
+        // 2^-52)^2, S >= (1 - 2^-24)^n sum t_k) lo = sum over blocks of (1 - 1/max(k0, 2)) sum_k
+        // max(0, |p_k - m_(k-1)| - D_(k-1) - eps_k)^2 (1 - 2^-24)^(n + 8) bounds ITK's float sig
         // from below, and mu_n <= m_n + D_n.  ITK's measure is monotone in both, so a measure above
         // the threshold at (RD(lo), RU(m_n + D_n)) proves the iteration goes on.  It decides the
         // iterations whose measure is well above the threshold (about a quarter on the bench
@@ -1878,7 +1887,7 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
         __syncthreads();
         pcw_scan<NL>(S, 1.0, wown, 0.0, wpre, unused);
         if (tid == NL - 1) {
-            const double f = 1.0 - ((double)n + 8.0) * 0x1p-24 - 0x1p-40;
+            const double f = pc_accum_factor((double)n + 8.0);
             const double lo = (wpre + wown) * f;
             const bool allok = nbad + (okb ? 0.0 : 1.0) == 0.0;   // every block's p in (0.5, 1.9)
             float sl = (float)lo;
@@ -1886,7 +1895,7 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
             const double Pn = dmx + s1;                     // exact sum of (p - 1) over all n steps
             const double mn = 1.0 + Pn / (double)n;         // m_n (one double division)
             const float muh = f_up(mn + cD * ((double)n + 3.0) + fabs(mn - 1.0) * 0x1p-50 + 0x1p-50);
-            if (allok && f > 0.5 && lo > 0.0 && itk_conv(muh, sl, n) > skip_thresh) {
+            if (allok && lo > 0.0 && itk_conv(muh, sl, n) > skip_thresh) {
                 S.mu = muh;
                 S.sig = sl;
                 S.rounds = 0;
@@ -1927,22 +1936,22 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
             // Certified decision (skip_thresh > 0: this iteration's measure is only compared with the
             // threshold, never reported): with mu exact after stage 0, every float sig step is
             // t_k = RN(RN(RN_f(q q) (N - 1)) / N) >= q^2 (1 - 1/N)(1 - 2^-24)(1 - 2^-52)^2, the float
-            // accumulation keeps S >= (1 - n 2^-24) sum t_k, and a block's stage-0 float sum B of
-            // fma(q, q, .) over its <= L + 1 steps has sum q^2 >= B (1 - (L + 1) 2^-24).  So
-            // S >= lo = (sum of the weighted B) (1 - (n + L + 8) 2^-24), and since ITK's measure
+            // accumulation keeps S >= (1 - 2^-24)^n sum t_k, and a block's stage-0 float sum B of
+            // fma(q, q, .) over its <= L + 1 steps has sum q^2 >= B (1 - 2^-24)^(L + 1).  So
+            // S >= lo = (sum of the weighted B) (1 - 2^-24)^(n + L + 8) (pc_accum_factor), and since ITK's measure
             // sqrt(S / (N - 1)) / mu is monotone in S under round-to-nearest, a measure above the
             // threshold at sig = RD(lo) proves the true one is above it too: the iteration goes on
             // and the exact sig (PCX below) is not needed.  Otherwise, or when the measure is the
             // level's reported one (skip_thresh = 0), PCX computes it exactly.
             if (tid == NL - 1 && skip_thresh > 0.0f) {
-                const double f = 1.0 - ((double)n + (double)m.L + 8.0) * 0x1p-24;
+                const double f = pc_accum_factor((double)n + (double)m.L + 8.0);
                 const double lo = (wpre + wown) * f;
                 float sl = (float)lo;
                 if ((double)sl > lo && sl > 0.0f) sl = __uint_as_float(__float_as_uint(sl) - 1u);
                 const int nbe = m.L ? NL : (int)m.rem;
                 const float mue = S.b[nbe - 1].emu;   // (one float up: a margin that costs nothing)
                 const float muh = __uint_as_float(__float_as_uint(mue) + 1u);
-                if (f > 0.5 && lo > 0.0 && mue > 0.0f && itk_conv(muh, sl, n) > skip_thresh) {
+                if (lo > 0.0 && mue > 0.0f && itk_conv(muh, sl, n) > skip_thresh) {
                     S.mu = mue;
                     S.sig = sl;
                     S.rounds = round + 1;
@@ -2196,7 +2205,51 @@ struct Pcg2Args {
     PcgWg *wg;              // [2][G]
     float *E;               // [2][NB] every block's ends (the serial fallback)
     float skip_thresh;      // > 0: the measure is only compared with it (certified decision allowed)
+    // the grid study form: the round records as tagged granules [2][G][PCG_GW] (no grid barrier per
+    // round; zeroed before the launch), and the tag base of this call (tags base + scan + 1); null:
+    // records through A.wg and a grid barrier (k_n4_pcg2)
+    unsigned long long *gran;
+    uint32_t tag0;
 };
+// A round record as PCG_GW tagged granules (cdna_hip_programming.md Guideline 16, R2: the data is the
+// flag): each 32-bit word of the record in an 8-byte {tag, word} granule written by ONE relaxed
+// agent-scope atomic store (sc1) and read by sc1 loads until every tag is the round's.  A workgroup
+// publishes round r + 1 only after reading every round-r record, so the parity double buffer is
+// never overwritten under a reader (as with the barrier form).
+#define PCG_GW 12
+__device__ __forceinline__ void pcg_publish(unsigned long long *g, const PcgWg &r, uint32_t tag) {
+    const uint64_t a = (uint64_t)__double_as_longlong(r.A), bb = (uint64_t)__double_as_longlong(r.B),
+                   s = (uint64_t)__double_as_longlong(r.S);
+    const uint32_t v[PCG_GW] = {(uint32_t)a, (uint32_t)(a >> 32), (uint32_t)bb, (uint32_t)(bb >> 32),
+                                (uint32_t)s, (uint32_t)(s >> 32), __float_as_uint(r.gfirst),
+                                __float_as_uint(r.gsfirst), __float_as_uint(r.elast),
+                                __float_as_uint(r.eslast), (uint32_t)r.F, __float_as_uint(r.enbe)};
+#pragma unroll
+    for (int k = 0; k < PCG_GW; ++k)
+        __hip_atomic_store(g + k, ((unsigned long long)tag << 32) | v[k], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+// true when every granule of the record carries the tag; the record in r
+__device__ __forceinline__ bool pcg_fetch(const unsigned long long *g, uint32_t tag, PcgWg &r) {
+    uint32_t v[PCG_GW];
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < PCG_GW; ++k) {
+        const unsigned long long x = __hip_atomic_load(g + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok &= (uint32_t)(x >> 32) == tag;
+        v[k] = (uint32_t)x;
+    }
+    r.A = __longlong_as_double((long long)(((uint64_t)v[1] << 32) | v[0]));
+    r.B = __longlong_as_double((long long)(((uint64_t)v[3] << 32) | v[2]));
+    r.S = __longlong_as_double((long long)(((uint64_t)v[5] << 32) | v[4]));
+    r.gfirst = __uint_as_float(v[6]);
+    r.gsfirst = __uint_as_float(v[7]);
+    r.elast = __uint_as_float(v[8]);
+    r.eslast = __uint_as_float(v[9]);
+    r.F = (int)v[10];
+    r.enbe = __uint_as_float(v[11]);
+    return ok;
+}
 struct Pcg2Lds {
     double wA[PC_TPB / 64], wB[PC_TPB / 64], wS[PC_TPB / 64];
     int wF[PC_TPB / 64];
@@ -2213,7 +2266,7 @@ struct Pcg2Lds {
 // this block applied to 0; first = the grid's first mismatching transition (NB when none).
 __device__ void pcg2_scan(const Pcg2Args &A, Pcg2Lds &L, cooperative_groups::grid_group &grid, int parity,
                           int nbe, double a, double b, double bs, bool mm, float g, float gs, float e, float es,
-                          bool sum_mode, double &dm, double &ds, int &first) {
+                          bool sum_mode, double &dm, double &ds, int &first, uint32_t tag = 0u) {
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, G = gridDim.x;
     const int NB = G * PC_TPB;
     const bool last = t == PC_TPB - 1;
@@ -2263,9 +2316,32 @@ __device__ void pcg2_scan(const Pcg2Args &A, Pcg2Lds &L, cooperative_groups::gri
         r.gsfirst = gs;
         r.elast = L.elast;
         r.eslast = L.eslast;
-        rec[blockIdx.x] = r;
+        if (A.gran) pcg_publish(A.gran + ((size_t)parity * G + blockIdx.x) * PCG_GW, r, tag);
+        else rec[blockIdx.x] = r;
     }
-    grid.sync();
+    unsigned long long *const gr = A.gran ? A.gran + (size_t)parity * G * PCG_GW : nullptr;
+    if (!A.gran) grid.sync();
+    if (w == 0 && gr) {   // wait until every record this lane reads carries the round's tag (bounded:
+        // a missing record would be a bug; the rounds' result is then unusable but nothing hangs)
+        const int per = (G + 63) / 64;
+        for (uint32_t spin = 0;; ++spin) {
+            bool ok = true;
+            for (int i = 0; i < per; ++i) {
+                const int u = per * lane + i;
+                PcgWg q;
+                if (u < G) ok &= pcg_fetch(gr + (size_t)u * PCG_GW, tag, q);
+                if ((u + 1) * PC_TPB < nbe) ok &= pcg_fetch(gr + (size_t)(u + 1) * PCG_GW, tag, q);
+            }
+            if (__all(ok) || spin > (1u << 24)) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    auto recv = [&](int u) {
+        PcgWg q;
+        if (gr) pcg_fetch(gr + (size_t)u * PCG_GW, tag, q);
+        else q = rec[u];
+        return q;
+    };
     if (w == 0) {   // lane l folds workgroups [per l, per l + per) in order: those before this one
         // into the prefix (with their boundary terms), all of them into the S total and the first
         // mismatch
@@ -2276,11 +2352,11 @@ __device__ void pcg2_scan(const Pcg2Args &A, Pcg2Lds &L, cooperative_groups::gri
         for (int i = 0; i < per; ++i) {
             const int u = per * lane + i;
             if (u < G) {
-                const PcgWg r = rec[u];
+                const PcgWg r = recv(u);
                 const int jl = (u + 1) * PC_TPB - 1;   // the boundary transition jl -> jl + 1
                 double bb = 0.0, bs2 = 0.0;
                 if (jl < nbe - 1) {
-                    const PcgWg rn = rec[u + 1];
+                    const PcgWg rn = recv(u + 1);
                     bb = (double)r.elast - (double)rn.gfirst;
                     if (!sum_mode) bs2 = (double)r.eslast - (double)rn.gsfirst;
                     const bool bm = __float_as_uint(r.elast) != __float_as_uint(rn.gfirst) ||
@@ -2363,7 +2439,9 @@ __device__ void pcg2_body(const Pcg2Args &A, Pcg2Lds &L, cooperative_groups::gri
     int parity = 0, first = NB;
     double dm, ds;
     // the guesses: exclusive sums of s1 (dm) through the same scan in sum mode (no maps: a = 1, b = 0)
-    pcg2_scan(A, L, grid, parity, nbe, 1.0, 0.0, s1, false, 0.0f, 0.0f, 0.0f, 0.0f, true, dm, ds, first);
+    uint32_t nscan = 0;   // the grid form's record tags: A.tag0 + the scan's index (1-based)
+    pcg2_scan(A, L, grid, parity, nbe, 1.0, 0.0, s1, false, 0.0f, 0.0f, 0.0f, 0.0f, true, dm, ds, first,
+              A.gran ? A.tag0 + (++nscan) : 0u);
     parity ^= 1;
     float g = 0.0f, gs = 0.0f;
     {
@@ -2406,7 +2484,8 @@ __device__ void pcg2_body(const Pcg2Args &A, Pcg2Lds &L, cooperative_groups::gri
         have_o = true;
         // the decision sums: the block's stage-0 sum weighted by the smallest (N - 1) / N of the block
         const double wown = ((int)j < nbe && k0 > 1u) ? (double)lsum * (1.0 - 1.0 / fmin((double)k0, ITK_NMAX)) : 0.0;
-        pcg2_scan(A, L, grid, parity, nbe, a, bm, wown, mm, g, 0.0f, le, 0.0f, true, dm, ds, first);
+        pcg2_scan(A, L, grid, parity, nbe, a, bm, wown, mm, g, 0.0f, le, 0.0f, true, dm, ds, first,
+                  A.gran ? A.tag0 + (++nscan) : 0u);
         parity ^= 1;
         if (first == NB) {
             s0done = true;
@@ -2415,13 +2494,13 @@ __device__ void pcg2_body(const Pcg2Args &A, Pcg2Lds &L, cooperative_groups::gri
         g = dm == 0.0 ? g : (float)((double)g + dm);
     }
     if (s0done && A.skip_thresh > 0.0f) {   // certified decision (pcw_run; uniform over the grid)
-        const double f = 1.0 - ((double)n + (double)m.L + 8.0) * 0x1p-24;
+        const double f = pc_accum_factor((double)n + (double)m.L + 8.0);
         const double lo = L.tot * f;
         float sl = (float)lo;
         if ((double)sl > lo && sl > 0.0f) sl = __uint_as_float(__float_as_uint(sl) - 1u);
         const float mue = L.mue;
         const float muh = __uint_as_float(__float_as_uint(mue) + 1u);
-        if (f > 0.5 && lo > 0.0 && mue > 0.0f && itk_conv(muh, sl, n) > A.skip_thresh) {
+        if (lo > 0.0 && mue > 0.0f && itk_conv(muh, sl, n) > A.skip_thresh) {
             if (j == 0) {
                 A.st[A.b].conv_w = itk_conv(muh, sl, n);
                 A.st[A.b].conv_bound = 1;   // a bound, not ITK's float measure (threshold test only)
@@ -2483,7 +2562,8 @@ __device__ void pcg2_body(const Pcg2Args &A, Pcg2Lds &L, cooperative_groups::gri
             go = g;
             eo = le;
             have_o = true;
-            pcg2_scan(A, L, grid, parity, nbe, a, bm, bsv, mm, g, gs, le, les, false, dm, ds, first);
+            pcg2_scan(A, L, grid, parity, nbe, a, bm, bsv, mm, g, gs, le, les, false, dm, ds, first,
+                      A.gran ? A.tag0 + (++nscan) : 0u);
             parity ^= 1;
             if (first == NB) {
                 if (phase == 0) break;   // stage 1's fixed point (sig steps uncertified): verify it exactly

@@ -1197,6 +1197,12 @@ __device__ void publish_range(const StudyGrid &g, const float4 *rp, const int32_
     if (lane == 0) g.rrec[(size_t)u * G + r] = make_float4(rg.mx, rg.m1, rg.m2, rg.m3);
 }
 
+// STG_PROF builds: workgroup 0 prints the device wall-clock ticks (100 MHz) spent per phase
+#ifdef STG_PROF
+#define STG_MARK(k) do { if (r == 0 && t == 0) { const uint64_t _c = wall_clock64(); stg_p[k] += _c - stg_t0; stg_t0 = _c; } } while (0)
+#else
+#define STG_MARK(k) do { } while (0)
+#endif
 __global__ void __launch_bounds__(ST_TPB, 4) k_n4_studyg(StudyArgs a, StudyGrid gd) {
     namespace cg = cooperative_groups;
     cg::grid_group grid = cg::this_grid();
@@ -1298,6 +1304,9 @@ __global__ void __launch_bounds__(ST_TPB, 4) k_n4_studyg(StudyArgs a, StudyGrid 
     }
     int tpar = 0;   // Tg buffer of the last computed field's T windows
     int gi = 0;     // iterations computed so far (all levels): the parity of the global sums
+#ifdef STG_PROF
+    uint64_t stg_p[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, stg_t0 = wall_clock64();
+#endif
     for (int L = 0; L < a.nlev; ++L) {
         const DevLevel &lv = a.lvs->lv[L];
         char *tabp = smem + a.o_tab;
@@ -1342,6 +1351,7 @@ __global__ void __launch_bounds__(ST_TPB, 4) k_n4_studyg(StudyArgs a, StudyGrid 
         __syncthreads();
         for (int e = t; e < nlat; e += ST_TPB) fix128_flush(NSd + 2 * e, NSd + 2 * e + 1, numfix[2 * e], numfix[2 * e + 1]);
         grid.sync();
+        STG_MARK(7);
         {
             int itn = 0;
             int uin = M.uin;
@@ -1395,6 +1405,7 @@ __global__ void __launch_bounds__(ST_TPB, 4) k_n4_studyg(StudyArgs a, StudyGrid 
                     }
                 }
                 __syncthreads();
+                STG_MARK(0);
                 if (M.stop) break;
                 if (M.exact) {   // rare: every workgroup scans the study itself
                     float *s_cmax = reinterpret_cast<float *>(scr);
@@ -1447,7 +1458,9 @@ __global__ void __launch_bounds__(ST_TPB, 4) k_n4_studyg(StudyArgs a, StudyGrid 
                     if (cs) atomicAdd(HS + h, cs);
                     if (os) atomicAdd(HS + VH_MAX_BINS + h, os);
                 }
+                STG_MARK(1);
                 grid.sync();
+                STG_MARK(8);
                 // the other parity's sums were last read by the previous iteration's E map
                 for (int e = r * ST_TPB + t; e < 2 * VH_MAX_BINS; e += G * ST_TPB) HSo[e] = 0ull;
                 // ---- emap (k_n4_study's arithmetic on the grid's sums) ----
@@ -1513,6 +1526,7 @@ __global__ void __launch_bounds__(ST_TPB, 4) k_n4_studyg(StudyArgs a, StudyGrid 
                     }
                     __syncthreads();
                 }
+                STG_MARK(2);
                 // ---- fit: this workgroup's items into LDS, then into the grid's numerators ----
                 for (int e = g.t; e < 2 * nlat; e += g.n) numfix[e] = 0ull;
                 if (g.t == 0) M.item_ctr = 0;
@@ -1528,7 +1542,9 @@ __global__ void __launch_bounds__(ST_TPB, 4) k_n4_studyg(StudyArgs a, StudyGrid 
                 __syncthreads();
                 for (int e = t; e < nlat; e += ST_TPB)
                     fix128_flush(NS + 2 * e, NS + 2 * e + 1, numfix[2 * e], numfix[2 * e + 1]);
+                STG_MARK(3);
                 grid.sync();
+                STG_MARK(8);
                 // ---- lattice update and P1 (each workgroup its own copy, from the grid's sums) ----
                 for (int e = g.t; e < nlat; e += g.n) {
                     const double d = fix128_get(NSd + 2 * e, NSd + 2 * e + 1);
@@ -1548,6 +1564,7 @@ __global__ void __launch_bounds__(ST_TPB, 4) k_n4_studyg(StudyArgs a, StudyGrid 
                 }
                 if (g.t == 0) M.item_ctr = 0;
                 __syncthreads();
+                STG_MARK(4);
                 // ---- eval: this workgroup's items; U into the other buffer, d in raster order ----
                 const int uo = (uin + 1) % ST_NB;
                 {
@@ -1593,14 +1610,18 @@ __global__ void __launch_bounds__(ST_TPB, 4) k_n4_studyg(StudyArgs a, StudyGrid 
                     __syncthreads();
                     publish_range(gd, rpart0 + uo * a.nitems, ordr, a.nitems, uo, r, G);
                 }
+                STG_MARK(5);
                 grid.sync();
+                STG_MARK(8);
                 if (a.conv_mode == 0) {   // S7: the grid PC over every workgroup, d in raster order
                     Pcg2Args A = gd.pc;
                     A.skip_thresh = itk < a.lvs->max_iters[L] ? a.thresh : 0.0f;
+                    A.tag0 = (uint32_t)gi << 12;   // < 4096 scans per call (stage caps 40 + 40 + 48 rounds)
                     const float *const Dr = a.D + b * a.VS;
                     pcg2_body(A, PL, grid, [=](int64_t q) { return Dr[q]; });
                     grid.sync();   // conv_w (one thread's store) to every workgroup
                 }
+                STG_MARK(6);
                 tpar ^= 1;
                 uin = uo;
                 itn = itk;
@@ -1627,6 +1648,15 @@ __global__ void __launch_bounds__(ST_TPB, 4) k_n4_studyg(StudyArgs a, StudyGrid 
             __syncthreads();
         }
     }
+#ifdef STG_PROF
+    STG_MARK(7);
+    if (r == 0 && t == 0)
+        printf("STG_PROF G %d n %lld its %d ticks(10ns): ctrl %llu hist %llu emap %llu fit %llu lat %llu eval %llu "
+               "pc %llu level %llu barriers(hist/fit/eval) %llu\n", G, (long long)n, gi,
+               (unsigned long long)stg_p[0], (unsigned long long)stg_p[1], (unsigned long long)stg_p[2],
+               (unsigned long long)stg_p[3], (unsigned long long)stg_p[4], (unsigned long long)stg_p[5],
+               (unsigned long long)stg_p[6], (unsigned long long)stg_p[7], (unsigned long long)stg_p[8]);
+#endif
     if (r == 0) {   // final field's P1 for k_n4_final
         const TabV T = tab_view(smem + a.o_tab, a.R, a.C, a.Z, a.kcap);
         const int ncz = lvl.ax[2].ncp;
@@ -1930,9 +1960,10 @@ void vh_launch_n4_studyg(vh_batch *b, const vh_n4_params &prm) {
     const size_t b_r = A256(sizeof(float4) * ST_NB * (size_t)G);
     const size_t b_i = A256(sizeof(double) * 2 * (size_t)std::max<int32_t>(a.nitems, 1));
     const size_t b_w = A256(sizeof(PcgWg) * 2 * (size_t)G);
+    const size_t b_g = A256(sizeof(unsigned long long) * 2 * PCG_GW * (size_t)G);   // (zeroed)
     const size_t b_e = A256(sizeof(float) * 2 * (size_t)NB);
     const size_t b_p = A256(sizeof(float) * ((size_t)b->VS + (size_t)NB));   // (L + 1) NB <= n + NB
-    const size_t need = b_h + b_n + b_r + b_i + b_w + b_e + b_p;
+    const size_t need = b_h + b_n + b_g + b_r + b_i + b_w + b_e + b_p;
     if ((int64_t)need > b->stg_cap) {
         if (b->d_stg) HIP_TRY(hipFree(b->d_stg));
         b->d_stg = nullptr;
@@ -1947,6 +1978,11 @@ void vh_launch_n4_studyg(vh_batch *b, const vh_n4_params &prm) {
         StudyGrid gd{};
         gd.hsum = (unsigned long long *)w; w += b_h;
         gd.nsum = (unsigned long long *)w; w += b_n;
+        // VH_STG_BARRIER_PC=1: the rounds' records through a grid barrier instead (A/B runs)
+        gd.pc.gran = (getenv("VH_STG_BARRIER_PC") && atoi(getenv("VH_STG_BARRIER_PC")) == 1)
+                         ? nullptr : (unsigned long long *)w;
+        w += b_g;
+        gd.pc.tag0 = 0u;
         gd.rrec = (float4 *)w; w += b_r;
         gd.ipart = (double *)w; w += b_i;
         gd.pc.wg = (PcgWg *)w; w += b_w;
@@ -1958,7 +1994,7 @@ void vh_launch_n4_studyg(vh_batch *b, const vh_n4_params &prm) {
         gd.pc.st = b->d_st;
         gd.pc.b = v;
         gd.pc.skip_thresh = 0.0f;
-        HIP_TRY(hipMemsetAsync(b->d_stg, 0, b_h + b_n, b->stream));
+        HIP_TRY(hipMemsetAsync(b->d_stg, 0, b_h + b_n + b_g, b->stream));
         StudyArgs av = a;
         av.vol0 = v;
         void *args[] = {&av, &gd};
