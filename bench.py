@@ -434,6 +434,43 @@ def main_ci(args):
     print(json.dumps(line))
 
 
+def main_class(args):
+    """One-study latency line: Vent_Analysis.calculate_VDP -- the GUI's call --
+    on one synthetic study of --shape, host arrays in and out (H2D, N4 on the grid form, the VDP
+    chain, D2H of N4HPvent and the three maps, the class's numpy bookkeeping), args.steps calls
+    after args.warmup, the median call reported.  The study's own device batch is pooled
+    (_lib.pooled_batch), as in an interactive session that analyses study after study."""
+    import contextlib
+    import io
+    from vent_analysis_amd import Vent_Analysis
+    from vent_analysis_amd.synth import synth_volume
+    R, C, Z = args.shape
+    X, M = synth_volume(R, C, Z, 0, True)
+    vox = (1.5, 1.5, 10.0)
+    ts = []
+    sink = io.StringIO()   # the class prints the reference's status lines; stdout carries the JSON
+    for i in range(args.warmup + args.steps):
+        v = Vent_Analysis(xenon_array=X, mask_array=M, vox=vox)
+        t = time.perf_counter()
+        with contextlib.redirect_stdout(sink):
+            v.calculate_VDP()
+        if i >= args.warmup:
+            ts.append(time.perf_counter() - t)
+    med = sorted(ts)[len(ts) // 2]
+    line = {"metric": f"calculate_VDP latency, one {R}x{C}x{Z} study (host to host)",
+            "value": round(1.0 / med, 2), "unit": "volumes/s", "n_gpus": 1, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(med * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": "Vent_Analysis(xenon_array, mask_array).calculate_VDP(): N4 + "
+                                   "mean-anchored + linear-binning + k-means VDP + border + SNR, one "
+                                   "study, host arrays in and out", "shape": [R, C, Z],
+                       "n4_iterations": [int(i) for i in v.n4_iterations]},
+            "latency_ms": {"median": round(med * 1e3, 3), "min": round(min(ts) * 1e3, 3),
+                           "max": round(max(ts) * 1e3, 3)},
+            "roofline": None, "cpu_baseline": None}
+    print(json.dumps(line))
+
+
 def free_port():
     import socket
     with socket.socket() as so:
@@ -517,8 +554,9 @@ def make_parser():
     ap.add_argument("--iso-runs", type=int, default=5,
                     help="runs of batch 0 alone after the timed region (batch latency and the "
                          "isolated kernel durations the roofline uses)")
-    ap.add_argument("--workload", default="vdp", choices=["vdp", "ci"],
-                    help="vdp: the BASELINE metric (default); ci: the cluster-index line")
+    ap.add_argument("--workload", default="vdp", choices=["vdp", "ci", "class"],
+                    help="vdp: the BASELINE metric (default); ci: the cluster-index line; class: "
+                         "one study's Vent_Analysis.calculate_VDP latency, host to host")
     ap.add_argument("--dry-run", action="store_true",
                     help="tests only: this main() on the CPU over gloo with tests/standin_lib.py in "
                          "place of libventhip (every host step of the N > 1 line runs; the stand-in's "
@@ -553,6 +591,8 @@ def main():
     args = make_parser().parse_args()
     if args.workload == "ci":
         return main_ci(args)
+    if args.workload == "class":
+        return main_class(args)
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:   # python bench.py --gpus N: N ranks
         sys.exit(launch_ranks(args, sys.argv[1:]))

@@ -1129,3 +1129,17 @@ def test_n4_grid_empty_and_tiny_masks():
     ref, its, conv = native.n4(X, M2)
     t = _run_one(X, M2, "grid")
     assert_n4_matches(t[0][0], t[4][0].n4_iters[:4], t[4][0].n4_conv[:4], ref, its, conv, 0, "tiny")
+
+
+def test_class_pooled_batch_reuse_across_studies():
+    """calculate_VDP reuses one pooled device batch per shape (_lib.pooled_batch): study after study
+    through the class gives what a fresh batch gives for each, N4 field and maps bit for bit."""
+    from vent_analysis_amd import Vent_Analysis
+    vox = (1.5, 1.5, 10.0)
+    for seed in (4, 5, 4):
+        X, M = synth_volume(96, 80, 16, seed)
+        v = Vent_Analysis(xenon_array=X, mask_array=M, vox=vox)
+        v.calculate_VDP()
+        n4, d, bo, lb, res = _run_batch(X[None], M.astype(np.uint8)[None], "auto")
+        assert np.array_equal(v.N4HPvent, n4[0]) and np.array_equal(v.defectArray, d[0])
+        assert list(v.n4_iterations) == list(res[0].n4_iters[:4])

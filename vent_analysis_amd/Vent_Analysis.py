@@ -200,13 +200,10 @@ class Vent_Analysis:
                                       device=self.device)
         else:
             do_n4 = _n4_label(v)
-            B = _lib.Batch(*hp.shape, 1, device=self.device)
-            try:
+            with _lib.pooled_batch(*hp.shape, 1, device=self.device) as B:   # reused across calls
                 B.upload(hp.astype(np.float32)[None], mask_u8[None])
                 B.run(B.options(do_n4=do_n4, thresh=thresh, vox=vox))
                 n4, d, bo, lb, res = B.download(n4=True)
-            finally:
-                B.close()
             if res[0].n_mask == 0:   # sorted([])[int(0 * 0.99)] in the reference (:245, :255)
                 raise IndexError("calculate_VDP: empty mask (list index out of range)")
             self.N4HPvent = n4[0]

@@ -285,6 +285,7 @@ def _shutdown():
     vh_destroy ran in no defined order, possibly after C-level exit handlers had started taking the
     runtime and rocprofv3 down (SIGSEGV in exit() after profiled cooperative launches)."""
     with _lock:
+        _batch_pool.clear()
         for o in list(_live):   # batches and pipes first: they hold their context
             try:
                 o.close()
@@ -585,6 +586,41 @@ class Batch:
                                                    ct.byref(n), ct.byref(by)),
                        "vh_batch_kernel_time")
         return ms.value, n.value, by.value
+
+
+_batch_pool = {}   # (device, R, C, Z, n) -> idle Batch objects (pooled_batch)
+_BATCH_POOL_KEEP = 2
+
+
+class pooled_batch:
+    """A device-resident batch of this shape for the length of a ``with`` block, reused across calls
+    (the class's one-study calculate_VDP: creating a batch allocates its device workspace, which cost
+    more than the pipeline itself on a 128x128x24 study).  Exclusive while held, so host threads never
+    share one; at most _BATCH_POOL_KEEP idle batches per shape stay allocated (the rest are closed)."""
+
+    def __init__(self, R, C, Z, n=1, device=0):
+        self.key = (int(device), int(R), int(C), int(Z), int(n))
+
+    def __enter__(self):
+        with _lock:
+            idle = _batch_pool.get(self.key)
+            self.b = idle.pop() if idle else None
+        if self.b is None or self.b.h is None:
+            self.b = Batch(*self.key[1:], device=self.key[0])
+        return self.b
+
+    def __exit__(self, exc_type, exc, tb):
+        b = self.b
+        if exc_type is not None:   # a failed call may have left the batch in any state
+            b.close()
+            return False
+        with _lock:
+            idle = _batch_pool.setdefault(self.key, [])
+            if len(idle) < _BATCH_POOL_KEEP:
+                idle.append(b)
+                return False
+        b.close()
+        return False
 
 
 class Pipe:

@@ -1978,9 +1978,10 @@ void vh_launch_n4_studyg(vh_batch *b, const vh_n4_params &prm) {
         StudyGrid gd{};
         gd.hsum = (unsigned long long *)w; w += b_h;
         gd.nsum = (unsigned long long *)w; w += b_n;
-        // VH_STG_BARRIER_PC=1: the rounds' records through a grid barrier instead (A/B runs)
-        gd.pc.gran = (getenv("VH_STG_BARRIER_PC") && atoi(getenv("VH_STG_BARRIER_PC")) == 1)
-                         ? nullptr : (unsigned long long *)w;
+        // VH_STG_GRAN=1: the rounds' records as tagged granules instead of through a grid barrier
+        // (measured slower, r6e: S7 4.22 vs 3.87 ms per config-2 study; kept for A/B runs)
+        gd.pc.gran = (getenv("VH_STG_GRAN") && atoi(getenv("VH_STG_GRAN")) == 1)
+                         ? (unsigned long long *)w : nullptr;
         w += b_g;
         gd.pc.tag0 = 0u;
         gd.rrec = (float4 *)w; w += b_r;
