@@ -1647,10 +1647,12 @@ __global__ void __launch_bounds__(PC_TPB) k_n4_pcg2(Pcg2Args A) {
     cg::grid_group grid = cg::this_grid();
     if (!A.st[A.b].active) return;   // uniform over the grid
     __shared__ Pcg2Lds L;
+    __shared__ float T0[PCG_G0 * (PC_TPB + 8)];   // pass 0's transpose (pcg2_body)
     // pass 0's loads: the perm loads of a group issued together, then the d loads they address
     const float *const D = A.D;
     const int32_t *const perm = A.perm;
-    pcg2_body(A, L, grid, [=](int64_t r) { return D[perm[r]]; });
+    pcg2_body(A, L, grid, [=](int64_t r) { return D[perm[r]]; },
+              A.t0 ? T0 : nullptr);
 }
 
 // Exact cubic B-spline subdivision (spans doubled on every axis), axis by axis, one block/volume.
@@ -1963,6 +1965,8 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
                 pcg2_args.wg = (PcgWg *)w; w += 2 * (size_t)pcg_grid * sizeof(PcgWg);
                 pcg2_args.E = (float *)w;
                 pcg2_args.sc = b->d_sc;
+                // VH_PCG_T0=0: pass 0 reads each thread's own block (the round-5 form, A/B runs)
+                pcg2_args.t0 = !(getenv("VH_PCG_T0") && atoi(getenv("VH_PCG_T0")) == 0);
                 pcg2_args.st = b->d_st;
             }
             for (int it = 0; it < prm.max_iters[L]; ++it, ++gi) {

@@ -2210,6 +2210,7 @@ struct Pcg2Args {
     // records through A.wg and a grid barrier (k_n4_pcg2)
     unsigned long long *gran;
     uint32_t tag0;
+    int32_t t0;             // k_n4_pcg2: pass 0 through the LDS transpose (pcg2_body's T0)
 };
 // A round record as PCG_GW tagged granules (cdna_hip_programming.md Guideline 16, R2: the data is the
 // flag): each 32-bit word of the record in an 8-byte {tag, word} granule written by ONE relaxed
@@ -2410,8 +2411,15 @@ __device__ void pcg2_scan(const Pcg2Args &A, Pcg2Lds &L, cooperative_groups::gri
 // pass 0 reads d through ld(raster rank) (k_n4_pcg2: the raster -> compact permutation; the grid
 // study kernel: d stored in raster order); the result goes to A.st[A.b].conv_w / conv_bound, written
 // by one thread -- the caller's next grid barrier publishes it.
+// Pass 0's loads transposed through LDS (T0: PCG_G0 x (PC_TPB + 8) floats, or null): a thread's block
+// is ~n / NB consecutive raster steps, so one thread reading its own block made every wave-wide
+// load touch 64 lines (config 5: 107 steps per block, two such gathers per step through the
+// permutation); instead the workgroup loads each group of PCG_G0 steps of all its blocks together
+// (PCG_G0 lanes per block: 32-byte runs) and transposes it through LDS, as pcw_run's pass 0 does.
+#define PCG_G0 8
 template <class LoadD>
-__device__ void pcg2_body(const Pcg2Args &A, Pcg2Lds &L, cooperative_groups::grid_group &grid, LoadD ld) {
+__device__ void pcg2_body(const Pcg2Args &A, Pcg2Lds &L, cooperative_groups::grid_group &grid, LoadD ld,
+                          float *T0 = nullptr) {
     const int64_t n = A.sc[A.b].n_mask1;
     const int NB = gridDim.x * PC_TPB;
     const PcMap m = pc_map(n, NB);
@@ -2421,7 +2429,40 @@ __device__ void pcg2_body(const Pcg2Args &A, Pcg2Lds &L, cooperative_groups::gri
     const uint32_t np = (m.L + 1u) * (uint32_t)NB;
     // pass 0: p = exp(d) in block layout, block sums (they seed the mu guesses)
     double s1 = 0.0, s2 = 0.0;
-    for (uint32_t s0 = 0; s0 < len; s0 += 8) {
+    if (T0) {
+        constexpr int G0 = PCG_G0, TS = PC_TPB + 8;
+        const uint32_t lmax = m.L + (m.rem ? 1u : 0u);
+        float v[G0];
+        // thread t loads step t % G0 of the workgroup's blocks t / G0 + (PC_TPB / G0) q, at a clamped
+        // index (unconditional: the group's loads stay in flight together)
+        auto fetch = [&](uint32_t g0) {
+#pragma unroll
+            for (int q = 0; q < G0; ++q) {
+                const uint32_t jb = blockIdx.x * PC_TPB + (uint32_t)t / G0 + (uint32_t)(PC_TPB / G0) * q;
+                const uint32_t lb = pc_len(m, jb), i = g0 + (uint32_t)t % G0;
+                const int64_t r = lb ? (int64_t)(pc_k0(m, jb) - 1u + (i < lb ? i : lb - 1u)) : 0;
+                v[q] = ld(r < n ? r : (n > 0 ? n - 1 : 0));
+            }
+        };
+        if (lmax) fetch(0);
+        for (uint32_t g0 = 0; g0 < lmax; g0 += G0) {
+#pragma unroll
+            for (int q = 0; q < G0; ++q) T0[(t % G0) * TS + t / G0 + (PC_TPB / G0) * q] = v[q];
+            __syncthreads();
+            if (g0 + G0 < lmax) fetch(g0 + G0);   // the next group's loads in flight during this one's exp
+#pragma unroll
+            for (int i = 0; i < G0; ++i)
+                if (g0 + i < len) {
+                    const float p = expf_crs(T0[i * TS + t]);
+                    A.P[(size_t)(g0 + i) * NB + j] = p;
+                    const double e = (double)p - 1.0;
+                    s1 += e;
+                    s2 = fma(e, e, s2);
+                }
+            __syncthreads();
+        }
+    }
+    for (uint32_t s0 = 0; !T0 && s0 < len; s0 += 8) {
         float v[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i)   // clamped, unconditional: the loads stay in flight together
