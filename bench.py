@@ -450,9 +450,9 @@ def main_class(args):
     ts = []
     sink = io.StringIO()   # the class prints the reference's status lines; stdout carries the JSON
     for i in range(args.warmup + args.steps):
-        v = Vent_Analysis(xenon_array=X, mask_array=M, vox=vox)
-        t = time.perf_counter()
         with contextlib.redirect_stdout(sink):
+            v = Vent_Analysis(xenon_array=X, mask_array=M, vox=vox)
+            t = time.perf_counter()
             v.calculate_VDP()
         if i >= args.warmup:
             ts.append(time.perf_counter() - t)
