@@ -30,6 +30,12 @@
 #define N4_VPT (N4_CH / VH_TPB)
 #define HIST_COPIES 8   // LDS histogram copies (neighbouring lanes share bins)
 #define FIT_WAVES 4     // fit items per block (one per wave)
+#ifndef FIT_GS
+#define FIT_GS FIT_G    // the sweep fit's rows per load group (fit_item FG)
+#endif
+#ifndef FIT_WPE
+#define FIT_WPE 1       // the sweep fit's minimum waves per SIMD (launch bound; 1: no register cap)
+#endif
 
 // ---------------------------------------------------------------------------------------------
 // host: per-level axis tables (identical expressions to oracle/n4_oracle.c axis_tables)
@@ -1086,7 +1092,7 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_emap(const uint64_t *hpart, const
 // stage-1 output buffer, then E.
 // ---------------------------------------------------------------------------------------------
 template <int MODE>
-__global__ void __launch_bounds__(FIT_WAVES * 64) k_n4_fit_items(
+__global__ void __launch_bounds__(FIT_WAVES * 64, FIT_WPE) k_n4_fit_items(
     const float *__restrict__ U, const int32_t *rs, const uint64_t *rmask, const VolScalars *sc,
     int R, int C, int Z, int64_t VS, int ntiles, int nslots, int bins, const N4State *st,
     const float *E, DevLevel lv, int rowcap, int nbmax, unsigned long long *numfix,
@@ -1129,10 +1135,10 @@ __global__ void __launch_bounds__(FIT_WAVES * 64) k_n4_fit_items(
     if (MODE == 0) {
         const float bmin = st[b].bin_min;
         const double rinv = 1.0 / (double)st[b].slope;
-        fit_item<0, false>(it, T, lv.wk3, reinterpret_cast<const double2 *>(lv.ax[0].w3i), ncy, ncz, Z,
+        fit_item<0, false, FIT_GS>(it, T, lv.wk3, reinterpret_cast<const double2 *>(lv.ax[0].w3i), ncy, ncz, Z,
                     bins, U + b * VS, n, sE, bmin, rinv, rg, nbmax, nf);
     } else {
-        fit_item<1, false>(it, T, lv.wk2, reinterpret_cast<const double2 *>(lv.ax[0].w2), ncy, ncz, Z,
+        fit_item<1, false, FIT_GS>(it, T, lv.wk2, reinterpret_cast<const double2 *>(lv.ax[0].w2), ncy, ncz, Z,
                     bins, U + b * VS, n, sE, 0.0f, 1.0, rg, nbmax, nf);
     }
 }

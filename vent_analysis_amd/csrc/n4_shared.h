@@ -374,7 +374,7 @@ __device__ __forceinline__ void fit_ring_begin(FitRing &rg, const Item &it, cons
 // [2x], [2x+1]), p = (double)(u - sharpen(u)) * (1/sum wy^2 * 1/sum wz^2); MODE 1: denominator,
 // Wx = wx^2, p = 1.  Each control row's column partial is an fma chain over the item's rows in
 // row order: acc_a = fma(Wx(x, a), p(x), acc_a) for the window's four control rows.
-template <int MODE, bool INPLACE>
+template <int MODE, bool INPLACE, int FG = FIT_G>
 __device__ void fit_item(const Item &it, const TabV &T, const double *Wk, const double2 *Wx,
                          int ncy, int ncz, int Z, int bins, const float *Ub, int64_t n,
                          const float *sE, float bmin, double rinv, FitRing &rg, int nb_ring,
@@ -402,13 +402,13 @@ __device__ void fit_item(const Item &it, const TabV &T, const double *Wk, const 
     for (;;) {
         if (x <= it.xe) {   // rows of control span wb: the window does not move
             const int rb = uni(min(it.xe, T.xst[wb + 1] - 1));
-            // groups of FIT_G rows, two per trip: the next group's U loads are in flight while this
+            // groups of FG rows, two per trip: the next group's U loads are in flight while this
             // group's rows are added (the chains still take the rows in order)
-            uint32_t oA[FIT_G], oB[FIT_G];
-            float uA[FIT_G], uB[FIT_G];
-            auto issue = [&](int xb, uint32_t (&o)[FIT_G], float (&u)[FIT_G]) {
+            uint32_t oA[FG], oB[FG];
+            float uA[FG], uB[FG];
+            auto issue = [&](int xb, uint32_t (&o)[FG], float (&u)[FG]) {
 #pragma unroll
-                for (int g = 0; g < FIT_G; ++g) {
+                for (int g = 0; g < FG; ++g) {
                     const int xg = xb + g;
                     o[g] = item_off(it, xg <= rb ? xg : rb, xg <= rb);
 #ifdef AB_FIT_NOLOAD   // A/B builds only (fixed iteration counts): the fit without its U loads
@@ -418,9 +418,9 @@ __device__ void fit_item(const Item &it, const TabV &T, const double *Wk, const 
 #endif
                 }
             };
-            auto run = [&](int xb, const uint32_t (&o)[FIT_G], const float (&u)[FIT_G]) {
+            auto run = [&](int xb, const uint32_t (&o)[FG], const float (&u)[FG]) {
 #pragma unroll
-                for (int g = 0; g < FIT_G; ++g) {
+                for (int g = 0; g < FG; ++g) {
                     // branch-free: a masked-out lane / row past the span adds exact zeros (its U load
                     // returned 0, so every operand is finite) -- see eval_item for why
                     const bool on = o[g] != VH_OOB;
@@ -444,15 +444,15 @@ __device__ void fit_item(const Item &it, const TabV &T, const double *Wk, const 
             if (x <= rb) {
                 issue(x, oA, uA);
 #pragma unroll 1
-                for (int xb = x;; xb += 2 * FIT_G) {
+                for (int xb = x;; xb += 2 * FG) {
                     // the next group is issued unconditionally (rows past rb load nothing): a branch
                     // round the issue makes its loads maybe-pending at the join
-                    issue(xb + FIT_G, oB, uB);
+                    issue(xb + FG, oB, uB);
                     run(xb, oA, uA);
-                    if (xb + FIT_G > rb) break;
-                    issue(xb + 2 * FIT_G, oA, uA);
-                    run(xb + FIT_G, oB, uB);
-                    if (xb + 2 * FIT_G > rb) break;
+                    if (xb + FG > rb) break;
+                    issue(xb + 2 * FG, oA, uA);
+                    run(xb + FG, oB, uB);
+                    if (xb + 2 * FG > rb) break;
                 }
             }
             x = rb + 1 > x ? rb + 1 : x;
