@@ -12,7 +12,7 @@ import json
 import sys
 
 # timer class -> kernel names rocprofv3 reports for it (the first one present is used)
-NAMES = {"n4_study": ["k_n4_study"], "n4_pcg": ["k_n4_pcg2", "k_n4_pcg"], "n4_pcw": ["k_n4_pcw"],
+NAMES = {"n4_study": ["k_n4_study", "k_n4_studyg"], "n4_pcg": ["k_n4_pcg2", "k_n4_pcg"], "n4_pcw": ["k_n4_pcw"],
          "n4_fit": ["void k_n4_fit_items<0>"], "n4_eval": ["k_n4_eval"], "n4_hist": ["k_n4_hist"],
          "sort": ["k_sort_vol"], "kmeans": ["k_kmeans_s", "k_kmeans"], "n4_final": ["k_n4_final"],
          "ci_walk": ["k_ci_walk"], "classify": ["void k_plane<0, true>", "void k_plane<1, true>"]}

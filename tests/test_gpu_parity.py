@@ -1143,3 +1143,16 @@ def test_class_pooled_batch_reuse_across_studies():
         n4, d, bo, lb, res = _run_batch(X[None], M.astype(np.uint8)[None], "auto")
         assert np.array_equal(v.N4HPvent, n4[0]) and np.array_equal(v.defectArray, d[0])
         assert list(v.n4_iterations) == list(res[0].n4_iters[:4])
+
+
+def test_n4_grid_several_studies_one_launch_each():
+    """n4_mode=3 on a batch of three studies (one cooperative launch per study, vol0 = v, the same
+    per-launch global state reused): each study equals the oracle and the sweeps."""
+    hp, mk = synth_batch(96, 112, 20, 3, base_seed=40)
+    g = _run_batch(hp, mk, "grid")
+    s = _run_batch(hp, mk, "sweep")
+    assert np.array_equal(g[0], s[0]) and np.array_equal(g[1], s[1])
+    for b in range(3):
+        ref, its_ref, conv_ref = native.n4(hp[b], mk[b])
+        assert_n4_matches(g[0][b], g[4][b].n4_iters[:4], g[4][b].n4_conv[:4], ref, its_ref, conv_ref, 0,
+                          ("grid batch", b))
