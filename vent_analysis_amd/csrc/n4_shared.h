@@ -1711,13 +1711,31 @@ static_assert(PC_APASS >= 1 && PC_APASS <= 2, "PC_APASS: 1 or 2 phase-A stages (
 #ifndef PC_PRE
 #define PC_PRE 1    // early certified decision from the exact running mean (pcw_run, round 5)
 #endif
+#ifndef PC_P0CLAMP
+#define PC_P0CLAMP 1   // pass 0's loads unconditional at clamped indices (round 6)
+#endif
+#ifndef PC_INLINE
+#define PC_INLINE 0    // 1: pcw_run inlined (LDS through ds_* instead of flat; A/B builds)
+#endif
 template <int NL>
 __host__ __device__ constexpr size_t pcw_lds_bytes() {
     return sizeof(PcShared<NL>) > sizeof(float) * PC_G0 * (NL + 8) ? sizeof(PcShared<NL>)
                                                                     : sizeof(float) * PC_G0 * (NL + 8);
 }
+// LDS through an address_space(3) pointer: pcw_run is not inlined, so its LDS pointers are generic
+// and every access compiled to a flat_load / flat_store, which counts in vmcnt: waiting for one
+// waited for every global load in flight too (pass 0's prefetch).  A C-style cast to address space
+// 3 gives ds_read / ds_write (lgkmcnt only).
+typedef __attribute__((address_space(3))) float lds_f32;
+__device__ __forceinline__ float lds_ld(const float *p) { return *(const lds_f32 *)p; }
+__device__ __forceinline__ void lds_st(float *p, float v) { *(lds_f32 *)p = v; }
+#if PC_INLINE
+#define PCW_INL __forceinline__
+#else
+#define PCW_INL __attribute__((noinline))
+#endif
 template <int NL, bool PEXP = false, class LoadD>
-__device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n, PcShared<NL> &S,
+__device__ PCW_INL void pcw_run(LoadD ld, float *P, int64_t n, PcShared<NL> &S,
                                                   ChainState &ch, int req, double *tbuf, int tcap,
                                                   float skip_thresh = 0.0f, float *drift = nullptr,
                                                   bool drift_in = false, bool try_pre = false) {
@@ -1760,11 +1778,25 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
     // loads are in flight while this group's exp runs
     float v[G0];
     auto fetch = [&](uint32_t g0) {
+#if PC_P0CLAMP
+        // unconditional loads at a clamped index, the select after them (round 6): the guarded form
+        // `in ? ld(...) : 0` compiled to an exec-masked branch per load whose s_waitcnt vmcnt(0)
+        // waited for each load before the next issued -- the group's 8 loads one round trip at a
+        // time (scripts/dev/isa_serial_loads.py)
+#pragma unroll
+        for (int q = 0; q < G0; ++q) {   // (the value of a step past the block's end: never read)
+            const uint32_t jb = (uint32_t)tid / G0 + (uint32_t)(NL / G0) * q, i = (uint32_t)tid % G0;
+            const uint32_t lb = pc_len(m, jb), ii = g0 + i;
+            const int64_t r = lb ? (int64_t)(pc_k0(m, jb) - 1u + (ii < lb ? ii : lb - 1u)) : 0;
+            v[q] = ld(r < n ? r : (n > 0 ? n - 1 : 0));
+        }
+#else
 #pragma unroll
         for (int q = 0; q < G0; ++q) {
             const uint32_t jb = (uint32_t)tid / G0 + (uint32_t)(NL / G0) * q, i = (uint32_t)tid % G0;
             v[q] = g0 + i < pc_len(m, jb) ? ld((int64_t)(pc_k0(m, jb) - 1u + g0 + i)) : 0.0f;
         }
+#endif
     };
     fetch(0);
 #ifdef PC_PROF
@@ -1776,18 +1808,21 @@ __device__ __attribute__((noinline)) void pcw_run(LoadD ld, float *P, int64_t n,
     for (uint32_t g0 = 0; g0 < lmax; g0 += G0) {
 #pragma unroll
         for (int q = 0; q < G0; ++q)
-            T0[(tid % G0) * TS + tid / G0 + (NL / G0) * q] = v[q];
+            lds_st(T0 + (tid % G0) * TS + tid / G0 + (NL / G0) * q, v[q]);
         P0M(0);   // (profiling) the group's loads arrived and went to LDS
         __syncthreads();
         P0M(1);   // first barrier
         if (g0 + G0 < lmax) fetch(g0 + G0);
+        float tv[G0];   // this group's steps of this thread's block, from LDS (ds_read: lgkmcnt only)
+#pragma unroll
+        for (int i = 0; i < G0; ++i) tv[i] = lds_ld(T0 + i * TS + j);
 #pragma unroll
         for (int i = 0; i < G0; ++i)
             if (g0 + i < len) {
 #ifdef AB_P0_FASTEXP   // A/B probe only (results not the spec's): pass 0 without the double exp
-                const float p = PEXP ? T0[i * TS + j] : __expf(T0[i * TS + j]);
+                const float p = PEXP ? tv[i] : __expf(tv[i]);
 #else
-                const float p = PEXP ? T0[i * TS + j] : PC_EXPS ? expf_crs(T0[i * TS + j]) : expf_cr(T0[i * TS + j]);
+                const float p = PEXP ? tv[i] : PC_EXPS ? expf_crs(tv[i]) : expf_cr(tv[i]);
 #endif
                 P[(size_t)(g0 + i) * NL + j] = p;
                 s1 += (double)p - 1.0;
