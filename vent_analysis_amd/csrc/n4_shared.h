@@ -831,13 +831,16 @@ template <int NL>
 __device__ __forceinline__ void pc_block(const float *P, uint32_t j, uint32_t len, uint32_t k0,
                                          float &mu, float &sig, uint32_t nl = NL) {
     float cur[8], nxt[8];
+    // unconditional loads at clamped steps (a guarded load waited for itself before the next issued);
+    // the values past the block's end are never used
+    const uint32_t lc = len ? len - 1u : 0u;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) cur[i] = (uint32_t)i < len ? P[(size_t)i * nl + j] : 0.0f;
+    for (int i = 0; i < 8; ++i) cur[i] = P[(size_t)((uint32_t)i < len ? (uint32_t)i : lc) * nl + j];
     double kd = (double)k0;
     uint32_t s0 = 0;
     for (; s0 + 8 <= len; s0 += 8) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) nxt[i] = s0 + 8 + i < len ? P[(size_t)(s0 + 8 + i) * nl + j] : 0.0f;
+        for (int i = 0; i < 8; ++i) nxt[i] = P[(size_t)(s0 + 8 + i < len ? s0 + 8 + i : lc) * nl + j];
         PcK q[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) q[i] = pc_consts(kd + (double)i, cur[i]);
@@ -866,6 +869,29 @@ struct alignas(16) PcBlk {
     float gmu_o, emu_o;  // the previous round's guess and end (secant of the mu map)
     float sp0, sp1;      // pass 0 only: (s1, s2) below
 };
+// LDS through an address_space(3) pointer: pcw_run is not inlined, so its LDS pointers are generic
+// and every access compiled to a flat_load / flat_store, which counts in vmcnt: waiting for one
+// waited for every global load in flight too (pass 0's prefetch).  A C-style cast to address space
+// 3 gives ds_read / ds_write (lgkmcnt only).
+typedef __attribute__((address_space(3))) float lds_f32;
+__device__ __forceinline__ float lds_ld(const float *p) { return *(const lds_f32 *)p; }
+__device__ __forceinline__ void lds_st(float *p, float v) { *(lds_f32 *)p = v; }
+// any object in LDS (PcShared fields) read / written through an address-space-3 pointer
+// (the host compilation pass of these device functions has no address spaces: plain accesses there)
+template <class T> __device__ __forceinline__ T lget(const T &r) {
+#if __HIP_DEVICE_COMPILE__
+    return *(const __attribute__((address_space(3))) T *)&r;
+#else
+    return r;
+#endif
+}
+template <class T> __device__ __forceinline__ void lset(T &r, const T &v) {
+#if __HIP_DEVICE_COMPILE__
+    *(__attribute__((address_space(3))) T *)&r = v;
+#else
+    r = v;
+#endif
+}
 template <int NL>
 struct PcShared {
     PcBlk b[NL];
@@ -1307,9 +1333,9 @@ __device__ __forceinline__ void pcw_scan(PcShared<NL> &S, double a, double b, do
     aff_step<0x142, 0xa>(A, B, Bs);   // row_bcast:15 -> rows 1, 3
     aff_step<0x143, 0xc>(A, B, Bs);   // row_bcast:31 -> rows 2, 3
     if (lane == 63) {
-        S.agA[w] = A;
-        S.agB[w] = B;
-        S.agS[w] = Bs;
+        lset(S.agA[w], A);
+        lset(S.agB[w], B);
+        lset(S.agS[w], Bs);
     }
     const double ea = dpp_d<0x138, 0xf>(A, 1.0), eb = dpp_d<0x138, 0xf>(B, 0.0),   // wave_shr:1
                  es = dpp_d<0x138, 0xf>(Bs, 0.0);
@@ -1319,9 +1345,9 @@ __device__ __forceinline__ void pcw_scan(PcShared<NL> &S, double a, double b, do
     static_assert(NL / 64 <= 16, "one DPP row of wave aggregates");
     double gA = 1.0, gB = 0.0, gS = 0.0;
     if (lane < w) {
-        gA = S.agA[lane];
-        gB = S.agB[lane];
-        gS = S.agS[lane];
+        gA = lget(S.agA[lane]);
+        gB = lget(S.agB[lane]);
+        gS = lget(S.agS[lane]);
     }
     aff_step<0x111, 0xf>(gA, gB, gS);
     aff_step<0x112, 0xf>(gA, gB, gS);
@@ -1353,8 +1379,8 @@ __device__ void pcw_guess(PcShared<NL> &S, const PcMap &m, double &gd, float dr 
         const double v = ds - dm * (dm / K);
         gs = (float)(v > 0.0 ? v : 0.0);
     }
-    S.b[j].gmu = g;
-    S.b[j].gsig = gs;
+    lset(S.b[j].gmu, g);
+    lset(S.b[j].gsig, gs);
 }
 
 // Check and update after a round (all threads).  S.done = req when every block end matched (S.mu /
@@ -1369,8 +1395,8 @@ __device__ void pcw_update(PcShared<NL> &S, const PcMap &m, int round, int req, 
     float em = 0.0f, es = 0.0f;
     bool mm = false;
     if (j < nbe - 1) {
-        const PcBlk B = S.b[j];
-        const float gn = S.b[j + 1].gmu, gsn = S.b[j + 1].gsig;
+        const PcBlk B = lget(S.b[j]);
+        const float gn = lget(S.b[j + 1].gmu), gsn = lget(S.b[j + 1].gsig);
         em = B.emu;
         es = B.esig;
         mm = __float_as_uint(B.emu) != __float_as_uint(gn) ||
@@ -1385,15 +1411,15 @@ __device__ void pcw_update(PcShared<NL> &S, const PcMap &m, int round, int req, 
             if (sl >= 0.0f && sl <= 1.0f) af = sl;
         }
         a = (double)af;
-        S.b[j].gmu_o = B.gmu;
-        S.b[j].emu_o = B.emu;
+        lset(S.b[j].gmu_o, B.gmu);
+        lset(S.b[j].emu_o, B.emu);
     }
     const uint64_t bal = __ballot(mm);
-    if (lane == 0) S.agFirst[w] = bal ? w * 64 + __ffsll((unsigned long long)bal) - 1 : NL;
+    if (lane == 0) lset(S.agFirst[w], bal ? w * 64 + __ffsll((unsigned long long)bal) - 1 : NL);
     double dm, ds;
     pcw_scan<NL>(S, a, bm, bs, dm, ds);   // its barrier also publishes agFirst
     int first = NL;
-    for (int v = 0; v < NL / 64; ++v) first = min(first, S.agFirst[v]);
+    for (int v = 0; v < NL / 64; ++v) first = min(first, lget(S.agFirst[v]));
     if (first == NL) {
         if (j == 0) {
             S.mu = S.b[nbe - 1].emu;
@@ -1412,8 +1438,8 @@ __device__ void pcw_update(PcShared<NL> &S, const PcMap &m, int round, int req, 
         return;
     }
     if (j < nbe - 1) {
-        S.b[j + 1].gmu = dm == 0.0 ? em : (float)((double)em + a * dm);
-        if (use_sig) S.b[j + 1].gsig = ds == 0.0 ? es : (float)((double)es + ds);
+        lset(S.b[j + 1].gmu, dm == 0.0 ? em : (float)((double)em + a * dm));
+        if (use_sig) lset(S.b[j + 1].gsig, ds == 0.0 ? es : (float)((double)es + ds));
     }
 }
 
@@ -1502,7 +1528,7 @@ __device__ void pcx_tpass(PcShared<NL> &S, const PcMap &m, const float *P, uint3
     for (uint32_t s0 = 0; s0 < len; s0 += 8) {
         float pv[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) pv[i] = s0 + i < len ? P[(size_t)(s0 + i) * NL + j] : 1.0f;
+        for (int i = 0; i < 8; ++i) pv[i] = P[(size_t)(s0 + i < len ? s0 + i : len - 1u) * NL + j];   // (clamped: unused past len)
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
             if (s0 + i >= len) break;
@@ -1722,13 +1748,6 @@ __host__ __device__ constexpr size_t pcw_lds_bytes() {
     return sizeof(PcShared<NL>) > sizeof(float) * PC_G0 * (NL + 8) ? sizeof(PcShared<NL>)
                                                                     : sizeof(float) * PC_G0 * (NL + 8);
 }
-// LDS through an address_space(3) pointer: pcw_run is not inlined, so its LDS pointers are generic
-// and every access compiled to a flat_load / flat_store, which counts in vmcnt: waiting for one
-// waited for every global load in flight too (pass 0's prefetch).  A C-style cast to address space
-// 3 gives ds_read / ds_write (lgkmcnt only).
-typedef __attribute__((address_space(3))) float lds_f32;
-__device__ __forceinline__ float lds_ld(const float *p) { return *(const lds_f32 *)p; }
-__device__ __forceinline__ void lds_st(float *p, float v) { *(lds_f32 *)p = v; }
 #if PC_INLINE
 #define PCW_INL __forceinline__
 #else
@@ -2052,7 +2071,7 @@ __device__ PCW_INL void pcw_run(LoadD ld, float *P, int64_t n, PcShared<NL> &S,
 #ifdef PC_PROF
             const unsigned long long cq = clock64();
 #endif
-            const float g = S.b[j].gmu, gs = S.b[j].gsig;
+            const float g = lget(S.b[j].gmu), gs = lget(S.b[j].gsig);
             const bool same = __float_as_uint(g) == __float_as_uint(lg) && __float_as_uint(gs) == __float_as_uint(ls);
 #ifdef PC_PROF
             if (pass == 0 && ra0 < 32 && (tid & 63) == 0) {
@@ -2070,8 +2089,8 @@ __device__ PCW_INL void pcw_run(LoadD ld, float *P, int64_t n, PcShared<NL> &S,
                 le = mu;
                 les = sig;
             }
-            S.b[j].emu = le;
-            S.b[j].esig = les;
+            lset(S.b[j].emu, le);
+            lset(S.b[j].esig, les);
             __syncthreads();
 #ifdef PC_PROF
             cblk += clock64() - cq;
@@ -2306,15 +2325,15 @@ __device__ void pcg2_scan(const Pcg2Args &A, Pcg2Lds &L, cooperative_groups::gri
     const int t = threadIdx.x, lane = t & 63, w = t >> 6, G = gridDim.x;
     const int NB = G * PC_TPB;
     const bool last = t == PC_TPB - 1;
-    if (t == 0) L.enbe = 0.0f;
+    if (t == 0) lset(L.enbe, 0.0f);
     __syncthreads();
-    if ((int)(blockIdx.x * PC_TPB + t) == nbe - 1) L.enbe = e;
+    if ((int)(blockIdx.x * PC_TPB + t) == nbe - 1) lset(L.enbe, e);
     if (last) {
         b = 0.0;
         if (!sum_mode) bs = 0.0;
         mm = false;
-        L.elast = e;
-        L.eslast = es;
+        lset(L.elast, e);
+        lset(L.eslast, es);
     }
     double Aw = a, Bw = b, Sw = bs;
     aff_step<0x111, 0xf>(Aw, Bw, Sw);
@@ -2325,11 +2344,11 @@ __device__ void pcg2_scan(const Pcg2Args &A, Pcg2Lds &L, cooperative_groups::gri
     aff_step<0x143, 0xc>(Aw, Bw, Sw);
     const uint64_t bal = __ballot(mm);
     if (lane == 63) {
-        L.wA[w] = Aw;
-        L.wB[w] = Bw;
-        L.wS[w] = Sw;
+        lset(L.wA[w], Aw);
+        lset(L.wB[w], Bw);
+        lset(L.wS[w], Sw);
     }
-    if (lane == 0) L.wF[w] = bal ? (int)(blockIdx.x * PC_TPB + w * 64 + __ffsll((unsigned long long)bal) - 1) : NB;
+    if (lane == 0) lset(L.wF[w], bal ? (int)(blockIdx.x * PC_TPB + w * 64 + __ffsll((unsigned long long)bal) - 1) : NB);
     const double ea = dpp_d<0x138, 0xf>(Aw, 1.0), eb = dpp_d<0x138, 0xf>(Bw, 0.0), es_ = dpp_d<0x138, 0xf>(Sw, 0.0);
     __syncthreads();
     PcgWg *const rec = A.wg + (size_t)parity * G;
@@ -2337,21 +2356,21 @@ __device__ void pcg2_scan(const Pcg2Args &A, Pcg2Lds &L, cooperative_groups::gri
         double At = 1.0, Bt = 0.0, St = 0.0;
         int f = NB;
         for (int v = 0; v < PC_TPB / 64; ++v) {
-            Bt = L.wA[v] * Bt + L.wB[v];
-            At = At * L.wA[v];
-            St = St + L.wS[v];
-            f = min(f, L.wF[v]);
+            Bt = lget(L.wA[v]) * Bt + lget(L.wB[v]);
+            At = At * lget(L.wA[v]);
+            St = St + lget(L.wS[v]);
+            f = min(f, lget(L.wF[v]));
         }
         PcgWg r;
         r.A = At;
         r.B = Bt;
         r.S = St;
         r.F = f;
-        r.enbe = L.enbe;
+        r.enbe = lget(L.enbe);
         r.gfirst = g;
         r.gsfirst = gs;
-        r.elast = L.elast;
-        r.eslast = L.eslast;
+        r.elast = lget(L.elast);
+        r.eslast = lget(L.eslast);
         if (A.gran) pcg_publish(A.gran + ((size_t)parity * G + blockIdx.x) * PCG_GW, r, tag);
         else rec[blockIdx.x] = r;
     }
@@ -2422,24 +2441,24 @@ __device__ void pcg2_scan(const Pcg2Args &A, Pcg2Lds &L, cooperative_groups::gri
         const uint64_t hm = __ballot(mue != 0.0f);
         const float me = hm ? __shfl(mue, __ffsll((unsigned long long)hm) - 1, 64) : 0.0f;
         if (lane == 63) {
-            L.pB = Bl;
-            L.pS = Sl;
-            L.first = f;
+            lset(L.pB, Bl);
+            lset(L.pS, Sl);
+            lset(L.first, f);
         }
         if (lane == 0) {
-            L.tot = Tl;
-            L.mue = me;
+            lset(L.tot, Tl);
+            lset(L.mue, me);
         }
     }
     __syncthreads();
-    double x = L.pB, xs = L.pS;
+    double x = lget(L.pB), xs = lget(L.pS);
     for (int v = 0; v < w; ++v) {
-        x = L.wA[v] * x + L.wB[v];
-        xs = xs + L.wS[v];
+        x = lget(L.wA[v]) * x + lget(L.wB[v]);
+        xs = xs + lget(L.wS[v]);
     }
     dm = ea * x + eb;
     ds = xs + es_;
-    first = L.first;
+    first = lget(L.first);
 }
 
 // The grid PC's whole call over the launch's grid (every workgroup of it, PC_TPB threads each):
@@ -2529,7 +2548,7 @@ __device__ void pcg2_body(const Pcg2Args &A, Pcg2Lds &L, cooperative_groups::gri
     bool have_o = false, s0done = false;
     int round = 0;
     for (int r = 0; r < PC_AMAX; ++r, ++round) {
-        L.gg[t] = g;
+        lset(L.gg[t], g);
         const bool same = __float_as_uint(g) == __float_as_uint(lg);
         if (__ballot(!same) != 0ull && !same) {
             float mu = g, sq = 0.0f;
@@ -2542,7 +2561,7 @@ __device__ void pcg2_body(const Pcg2Args &A, Pcg2Lds &L, cooperative_groups::gri
         double a = 1.0, bm = 0.0;
         bool mm = false;
         if ((int)j < nbe - 1 && t < PC_TPB - 1) {
-            const float gn = L.gg[t + 1];
+            const float gn = lget(L.gg[t + 1]);
             mm = __float_as_uint(le) != __float_as_uint(gn);
             bm = (double)le - (double)gn;
         }
@@ -2571,10 +2590,10 @@ __device__ void pcg2_body(const Pcg2Args &A, Pcg2Lds &L, cooperative_groups::gri
     }
     if (s0done && A.skip_thresh > 0.0f) {   // certified decision (pcw_run; uniform over the grid)
         const double f = pc_accum_factor((double)n + (double)m.L + 8.0);
-        const double lo = L.tot * f;
+        const double lo = lget(L.tot) * f;
         float sl = (float)lo;
         if ((double)sl > lo && sl > 0.0f) sl = __uint_as_float(__float_as_uint(sl) - 1u);
-        const float mue = L.mue;
+        const float mue = lget(L.mue);
         const float muh = __uint_as_float(__float_as_uint(mue) + 1u);
         if (lo > 0.0 && mue > 0.0f && itk_conv(muh, sl, n) > A.skip_thresh) {
             if (j == 0) {
@@ -2600,8 +2619,8 @@ __device__ void pcg2_body(const Pcg2Args &A, Pcg2Lds &L, cooperative_groups::gri
     for (int phase = 0; phase < 2 && !done; ++phase) {
         const int cap = phase == 0 ? PC_AMAX : PC_RMAX;
         for (int r = 0; r < cap; ++r, ++round) {
-            L.gg[t] = g;
-            L.gsg[t] = gs;
+            lset(L.gg[t], g);
+            lset(L.gsg[t], gs);
             float mu = g, sig = gs;
             if (phase == 1) {
                 pc_block<0>(A.P, j, len, k0, mu, sig, NB);
@@ -2621,7 +2640,7 @@ __device__ void pcg2_body(const Pcg2Args &A, Pcg2Lds &L, cooperative_groups::gri
             double a = 1.0, bm = 0.0, bsv = 0.0;
             bool mm = false;
             if ((int)j < nbe - 1 && t < PC_TPB - 1) {
-                const float gn = L.gg[t + 1], gsn = L.gsg[t + 1];
+                const float gn = lget(L.gg[t + 1]), gsn = lget(L.gsg[t + 1]);
                 mm = __float_as_uint(le) != __float_as_uint(gn) || __float_as_uint(les) != __float_as_uint(gsn);
                 bm = (double)le - (double)gn;
                 bsv = (double)les - (double)gsn;
