@@ -833,14 +833,16 @@ __device__ __forceinline__ void pc_block(const float *P, uint32_t j, uint32_t le
     float cur[8], nxt[8];
     // unconditional loads at clamped steps (a guarded load waited for itself before the next issued);
     // the values past the block's end are never used
-    const uint32_t lc = len ? len - 1u : 0u;
+    // (an empty block reads P[0], which every non-empty call has written: past a tiny study's block
+    // layout P[j] could lie beyond the buffer)
+    const uint32_t lc = len ? len - 1u : 0u, jc = len ? j : 0u;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) cur[i] = P[(size_t)((uint32_t)i < len ? (uint32_t)i : lc) * nl + j];
+    for (int i = 0; i < 8; ++i) cur[i] = P[(size_t)((uint32_t)i < len ? (uint32_t)i : lc) * nl + jc];
     double kd = (double)k0;
     uint32_t s0 = 0;
     for (; s0 + 8 <= len; s0 += 8) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) nxt[i] = P[(size_t)(s0 + 8 + i < len ? s0 + 8 + i : lc) * nl + j];
+        for (int i = 0; i < 8; ++i) nxt[i] = P[(size_t)(s0 + 8 + i < len ? s0 + 8 + i : lc) * nl + jc];
         PcK q[8];
 #pragma unroll
         for (int i = 0; i < 8; ++i) q[i] = pc_consts(kd + (double)i, cur[i]);
@@ -1817,7 +1819,9 @@ __device__ PCW_INL void pcw_run(LoadD ld, float *P, int64_t n, PcShared<NL> &S,
         }
 #endif
     };
-    fetch(0);
+    // (n == 0: no load at all -- the clamped index 0 would read a permutation entry of an empty
+    // study, r6y's illegal address)
+    if (lmax) fetch(0);
 #ifdef PC_PROF
     unsigned long long p0t[4] = {0, 0, 0, 0}, p0c = clock64();
 #define P0M(k) do { const unsigned long long _c = clock64(); p0t[k] += _c - p0c; p0c = _c; } while (0)
