@@ -1156,3 +1156,19 @@ def test_n4_grid_several_studies_one_launch_each():
         ref, its_ref, conv_ref = native.n4(hp[b], mk[b])
         assert_n4_matches(g[0][b], g[4][b].n4_iters[:4], g[4][b].n4_conv[:4], ref, its_ref, conv_ref, 0,
                           ("grid batch", b))
+
+
+@pytest.mark.parametrize("driver", ["sweep", "grid"])
+@pytest.mark.parametrize("nb", [1, 2])
+def test_n4_studies_smaller_than_the_pc_block_count(driver, nb):
+    """Studies of fewer voxels than PC's 1024 blocks (the block layout P of a tiny study is shorter
+    than one row of blocks: empty blocks must not read past it), one with an empty mask beside it."""
+    hp, mk = synth_batch(8, 10, 6, nb, base_seed=50)
+    mk[:, 2:6, 3:8, 1:5] = 1
+    if nb == 2:
+        mk[1] = 0
+    n4, d, _, _, res = _run_batch(hp, mk, driver)
+    ref, its, conv = native.n4(hp[0], mk[0])
+    assert_n4_matches(n4[0], res[0].n4_iters[:4], res[0].n4_conv[:4], ref, its, conv, 0, ("tiny", driver))
+    if nb == 2:
+        assert np.array_equal(n4[1], hp[1])
