@@ -2317,6 +2317,7 @@ struct Pcg2Lds {
     double pB, pS, tot;     // the workgroups before this one applied to 0; the grid's S total
     float mue;              // the end of the last non-empty block
     int first;
+    double xA[PC_TPB / 64], xB[PC_TPB / 64], xS[PC_TPB / 64];   // waves before wave w composed
 };
 // The round's scan (one grid barrier).  Per thread: the map (a, b) and sig channel bs of its block
 // (b, bs of a workgroup's last block are ignored: its boundary terms are added after the barrier),
@@ -2356,15 +2357,37 @@ __device__ void pcg2_scan(const Pcg2Args &A, Pcg2Lds &L, cooperative_groups::gri
     const double ea = dpp_d<0x138, 0xf>(Aw, 1.0), eb = dpp_d<0x138, 0xf>(Bw, 0.0), es_ = dpp_d<0x138, 0xf>(Sw, 0.0);
     __syncthreads();
     PcgWg *const rec = A.wg + (size_t)parity * G;
-    if (t == 0) {
-        double At = 1.0, Bt = 0.0, St = 0.0;
-        int f = NB;
-        for (int v = 0; v < PC_TPB / 64; ++v) {
-            Bt = lget(L.wA[v]) * Bt + lget(L.wB[v]);
-            At = At * lget(L.wA[v]);
-            St = St + lget(L.wS[v]);
-            f = min(f, lget(L.wF[v]));
+    constexpr int NW = PC_TPB / 64;
+    static_assert(NW <= 16, "the wave aggregates in one DPP row");
+    if (w == 0) {   // the wave aggregates scanned on lanes 0..NW-1 (one DPP row, 4 steps instead of a
+        // 16-step serial loop on thread 0 and up to 15 steps on every thread): lane v holds waves
+        // 0..v composed -- the workgroup's aggregate on lane NW-1, wave v+1's prefix on lane v
+        double A2 = 1.0, B2 = 0.0, S2 = 0.0;
+        int f2 = NB;
+        if (lane < NW) {
+            A2 = lget(L.wA[lane]);
+            B2 = lget(L.wB[lane]);
+            S2 = lget(L.wS[lane]);
+            f2 = lget(L.wF[lane]);
         }
+        aff_step<0x111, 0xf>(A2, B2, S2);   // row_shr:1
+        aff_step<0x112, 0xf>(A2, B2, S2);   // row_shr:2
+        aff_step<0x114, 0xf>(A2, B2, S2);   // row_shr:4
+        aff_step<0x118, 0xf>(A2, B2, S2);   // row_shr:8
+        if (lane < NW - 1) {
+            lset(L.xA[lane + 1], A2);
+            lset(L.xB[lane + 1], B2);
+            lset(L.xS[lane + 1], S2);
+        }
+        if (lane == 0) {
+            lset(L.xA[0], 1.0);
+            lset(L.xB[0], 0.0);
+            lset(L.xS[0], 0.0);
+        }
+        for (int off = 1; off < NW; off <<= 1) f2 = min(f2, __shfl_xor(f2, off, 64));
+        const double At = __shfl(A2, NW - 1, 64), Bt = __shfl(B2, NW - 1, 64), St = __shfl(S2, NW - 1, 64);
+        const int f = __shfl(f2, 0, 64);
+        if (lane == 0) {
         PcgWg r;
         r.A = At;
         r.B = Bt;
@@ -2377,6 +2400,7 @@ __device__ void pcg2_scan(const Pcg2Args &A, Pcg2Lds &L, cooperative_groups::gri
         r.eslast = lget(L.eslast);
         if (A.gran) pcg_publish(A.gran + ((size_t)parity * G + blockIdx.x) * PCG_GW, r, tag);
         else rec[blockIdx.x] = r;
+        }
     }
     unsigned long long *const gr = A.gran ? A.gran + (size_t)parity * G * PCG_GW : nullptr;
     if (!A.gran) grid.sync();
@@ -2455,11 +2479,9 @@ __device__ void pcg2_scan(const Pcg2Args &A, Pcg2Lds &L, cooperative_groups::gri
         }
     }
     __syncthreads();
-    double x = lget(L.pB), xs = lget(L.pS);
-    for (int v = 0; v < w; ++v) {
-        x = lget(L.wA[v]) * x + lget(L.wB[v]);
-        xs = xs + lget(L.wS[v]);
-    }
+    // the waves before this one applied to the workgroups before this one (the guesses only steer the
+    // rounds: the composed form rounds differently from the serial fold, the result is exact either way)
+    const double x = lget(L.xA[w]) * lget(L.pB) + lget(L.xB[w]), xs = lget(L.pS) + lget(L.xS[w]);
     dm = ea * x + eb;
     ds = xs + es_;
     first = lget(L.first);

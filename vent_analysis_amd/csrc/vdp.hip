@@ -23,73 +23,98 @@ __global__ void k_init_scalars(VolScalars *sc, int64_t nb) {
 
 // One pass over the mask in 32-row slabs (one bitmap word) x 4 columns per lane (a 32-bit load
 // per row: 256 B per wave).  Writes the slab's bitmap words of mask == 1 (N4 label) and mask != 0
-// (VDP / SNR mask), the row / col / slice "any" flags, and per volume the masked counts and the
-// first mask == 1 voxel (atomics on integers: order-free).  k_mask_cols then derives each
-// column's masked row range and count from the mask != 0 words.
-template <bool VEC>
+// (VDP / SNR mask), the row "any" flags, and per volume the masked counts and the first mask == 1
+// voxel (atomics on integers: order-free).  The four bytes of a row word are tested together (SWAR:
+// bit 7 of each byte) and gathered 8 rows at a time before they are spread into the column words.
+// k_mask_cols then derives each column's masked row range and count from the mask != 0 words;
+// the column / slice flags come from those counts in k_mask_finish (one byte store per masked column
+// and slab into a volume's one or two flag lines made this kernel 3x slower than its loads).
+template <int CPL, bool VEC>
 __global__ void __launch_bounds__(VH_TPB) k_mask_stats(const uint8_t *__restrict__ mask, int64_t R,
-                                                      int64_t C, int64_t Z, int64_t V, int64_t ncb4,
+                                                      int64_t C, int64_t Z, int64_t V, int64_t ncb,
                                                       uint32_t *colbits, uint32_t *colbnz,
-                                                      uint8_t *rowany, uint8_t *colany,
-                                                      uint8_t *sliceany, VolScalars *sc) {
+                                                      uint8_t *rowany, VolScalars *sc) {
+    constexpr int NW4 = CPL / 4;   // 32-bit words of a lane's row (VEC: one 4- or 16-byte load)
     __shared__ uint32_t s_row;
     __shared__ unsigned long long s_n, s_n1, s_first;
     const int64_t b = blockIdx.y;
     const int64_t CZ = C * Z;
-    const int64_t sl = blockIdx.x / ncb4;
-    const int64_t c0 = ((blockIdx.x % ncb4) * VH_TPB + threadIdx.x) * 4;
+    const int64_t sl = blockIdx.x / ncb;
+    const int64_t c0 = ((blockIdx.x % ncb) * VH_TPB + threadIdx.x) * CPL;
     const int64_t x0 = sl * VH_SLAB;
     const int nr = (int)(R - x0 < VH_SLAB ? R - x0 : VH_SLAB);
     if (threadIdx.x == 0) { s_row = 0u; s_n = 0; s_n1 = 0; s_first = ULLONG_MAX; }
     __syncthreads();
-    uint32_t w1[4] = {0u, 0u, 0u, 0u}, wn[4] = {0u, 0u, 0u, 0u};
-    const int nc = c0 < CZ ? (int)(CZ - c0 < 4 ? CZ - c0 : 4) : 0;
+    uint32_t w1[CPL], wn[CPL];
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) { w1[q] = 0u; wn[q] = 0u; }
+    const int nc = c0 < CZ ? (int)(CZ - c0 < CPL ? CZ - c0 : CPL) : 0;
     if (nc) {
         const uint8_t *m = mask + b * V + x0 * CZ + c0;
-        uint32_t mv[VH_SLAB];   // the slab's 32 row loads all in flight
+        uint32_t mv[VH_SLAB][NW4];   // the slab's 32 row loads all in flight
 #pragma unroll
         for (int k = 0; k < VH_SLAB; ++k) {
-            mv[k] = 0u;
+#pragma unroll
+            for (int j = 0; j < NW4; ++j) mv[k][j] = 0u;
             if (k < nr) {
                 const uint8_t *p = m + (int64_t)k * CZ;
-                if (VEC) mv[k] = *reinterpret_cast<const uint32_t *>(p);
-                else
-                    for (int q = 0; q < nc; ++q) mv[k] |= (uint32_t)p[q] << (8 * q);
+                if (VEC) {
+                    if (NW4 == 4) {
+                        const uint4 u = *reinterpret_cast<const uint4 *>(p);
+                        mv[k][0] = u.x; mv[k][NW4 > 1 ? 1 : 0] = u.y;
+                        mv[k][NW4 > 2 ? 2 : 0] = u.z; mv[k][NW4 > 3 ? 3 : 0] = u.w;
+                    } else {
+                        mv[k][0] = *reinterpret_cast<const uint32_t *>(p);
+                    }
+                } else {
+                    for (int q = 0; q < nc; ++q) mv[k][0] |= (uint32_t)p[q] << (8 * q);
+                }
             }
         }
 #pragma unroll
-        for (int k = 0; k < VH_SLAB; ++k) {
+        for (int j = 0; j < NW4; ++j) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint32_t v = (mv[k] >> (8 * q)) & 0xFFu;
-                w1[q] |= (uint32_t)(v == 1u) << k;
-                wn[q] |= (uint32_t)(v != 0u) << k;
+            for (int g = 0; g < VH_SLAB / 8; ++g) {
+                uint32_t a1 = 0u, an = 0u;   // byte q, bit r: row 8g + r of column 4j + q
+#pragma unroll
+                for (int r = 0; r < 8; ++r) {
+                    uint32_t x = mv[8 * g + r][j];
+                    asm volatile("" : "+v"(x));   // keeps the word a word (else the byte tests become i8 vectors: 14x the code, scratch)
+                    const uint32_t y = x ^ 0x01010101u;
+                    const uint32_t nz = (((x & 0x7f7f7f7fu) + 0x7f7f7f7fu) | x) & 0x80808080u;
+                    const uint32_t ne1 = (((y & 0x7f7f7f7fu) + 0x7f7f7f7fu) | y) & 0x80808080u;
+                    an |= (nz >> 7) << r;
+                    a1 |= ((ne1 ^ 0x80808080u) >> 7) << r;
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    wn[4 * j + q] |= ((an >> (8 * q)) & 0xFFu) << (8 * g);
+                    w1[4 * j + q] |= ((a1 >> (8 * q)) & 0xFFu) << (8 * g);
+                }
             }
         }
         const int64_t nw = (R + 31) >> 5;
         uint32_t *cb = colbits + (b * nw + sl) * CZ + c0, *cn = colbnz + (b * nw + sl) * CZ + c0;
         if (VEC) {
-            *reinterpret_cast<uint4 *>(cb) = make_uint4(w1[0], w1[1], w1[2], w1[3]);
-            *reinterpret_cast<uint4 *>(cn) = make_uint4(wn[0], wn[1], wn[2], wn[3]);
+#pragma unroll
+            for (int j = 0; j < NW4; ++j) {
+                *reinterpret_cast<uint4 *>(cb + 4 * j) = make_uint4(w1[4 * j], w1[4 * j + 1], w1[4 * j + 2], w1[4 * j + 3]);
+                *reinterpret_cast<uint4 *>(cn + 4 * j) = make_uint4(wn[4 * j], wn[4 * j + 1], wn[4 * j + 2], wn[4 * j + 3]);
+            }
         } else {
             for (int q = 0; q < nc; ++q) { cb[q] = w1[q]; cn[q] = wn[q]; }
         }
     }
     unsigned long long n = 0, n1 = 0, first = ULLONG_MAX;
     uint32_t rows = 0u;
-    for (int q = 0; q < nc; ++q) {
+#pragma unroll
+    for (int q = 0; q < CPL; ++q) {   // words past nc are 0
         n += (unsigned)__popc(wn[q]);
         n1 += (unsigned)__popc(w1[q]);
         rows |= wn[q];
-        const int64_t col = c0 + q;
-        if (wn[q]) {   // 32-bit division (CZ < 2^31, check_dims)
-            const uint32_t y = (uint32_t)col / (uint32_t)Z;
-            colany[b * C + y] = 1;
-            sliceany[b * Z + ((uint32_t)col - y * (uint32_t)Z)] = 1;
-        }
         if (w1[q]) {
             const unsigned long long idx =
-                (unsigned long long)((x0 + __builtin_ctz(w1[q])) * CZ + col);
+                (unsigned long long)((x0 + __builtin_ctz(w1[q])) * CZ + c0 + q);
             if (idx < first) first = idx;
         }
     }
@@ -106,7 +131,8 @@ __global__ void __launch_bounds__(VH_TPB) k_mask_stats(const uint8_t *__restrict
     }
 }
 
-// each column's masked (mask != 0) row range [lo, hi] (lo = R, hi = -1 when empty) and count
+// each column's masked (mask != 0) row range [lo, hi] (lo = R, hi = -1 when empty) and count; the
+// column's bitmap words load 8 at a time (clamped index: all in flight)
 __global__ void __launch_bounds__(VH_TPB) k_mask_cols(const uint32_t *colbnz, int64_t R, int64_t CZ,
                                                      int32_t *colrange, int32_t *colcount) {
     const int64_t b = blockIdx.y;
@@ -114,57 +140,129 @@ __global__ void __launch_bounds__(VH_TPB) k_mask_cols(const uint32_t *colbnz, in
     if (col >= CZ) return;
     const int64_t nw = (R + 31) >> 5;
     int32_t lo = (int32_t)R, hi = -1, n = 0;
-    for (int64_t w = 0; w < nw; ++w) {
-        const uint32_t v = colbnz[(b * nw + w) * CZ + col];
-        if (!v) continue;
-        n += __popc(v);
-        if (lo == (int32_t)R) lo = (int32_t)(w * 32 + __builtin_ctz(v));
-        hi = (int32_t)(w * 32 + 31 - __builtin_clz(v));
+    for (int64_t w0 = 0; w0 < nw; w0 += 8) {
+        uint32_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] = colbnz[(b * nw + (w0 + k < nw ? w0 + k : nw - 1)) * CZ + col];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t x = w0 + k < nw ? v[k] : 0u;
+            if (!x) continue;
+            n += __popc(x);
+            if (lo == (int32_t)R) lo = (int32_t)((w0 + k) * 32 + __builtin_ctz(x));
+            hi = (int32_t)((w0 + k) * 32 + 31 - __builtin_clz(x));
+        }
     }
     colrange[(b * CZ + col) * 2] = lo;
     colrange[(b * CZ + col) * 2 + 1] = hi;
     colcount[b * CZ + col] = n;
 }
 
-// exclusive prefix of the per-column masked counts (compaction offsets for the sort keys) and
-// the SNR box parameters.  One block per volume.
+// exclusive prefix of the per-column masked counts (compaction offsets for the sort keys), the
+// column / slice flags from the counts and the SNR box parameters.  One block per volume; the
+// counts stream through LDS in tiles of MF_TILE (coalesced loads, all in flight; each thread scans
+// 16 consecutive counts; coalesced colstart stores).  Flags go to LDS bitmaps when C, Z <= 32768,
+// else straight to the global flag arrays.
+#define MF_TILE (VH_TPB * 16)
+#define MF_FLAGW 1024
+__device__ __forceinline__ int64_t mf_block_excl(int64_t v, int64_t *s_w, int64_t &total) {
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    int64_t inc = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int64_t o = __shfl_up(inc, off, 64);
+        if (lane >= off) inc += o;
+    }
+    if (lane == 63) s_w[w] = inc;
+    __syncthreads();
+    int64_t pre = 0;
+    total = 0;
+#pragma unroll
+    for (int q = 0; q < VH_TPB / 64; ++q) {
+        const int64_t x = s_w[q];
+        if (q < w) pre += x;
+        total += x;
+    }
+    __syncthreads();
+    return pre + inc - v;
+}
+
 __global__ void __launch_bounds__(VH_TPB) k_mask_finish(const int32_t *colcount, int64_t *colstart,
-                                                       const uint8_t *rowany, const uint8_t *colany,
-                                                       const uint8_t *sliceany, int64_t R,
+                                                       const uint8_t *rowany, uint8_t *colany,
+                                                       uint8_t *sliceany, int64_t R,
                                                        int64_t C, int64_t Z, VolScalars *sc) {
-    __shared__ int64_t s_part[VH_TPB];
+    __shared__ int32_t s_cnt[MF_TILE];
+    __shared__ int64_t s_ex[MF_TILE];
+    __shared__ int64_t s_w[VH_TPB / 64];
+    __shared__ uint32_t s_cf[MF_FLAGW], s_sf[MF_FLAGW];
     __shared__ int32_t s_cmin, s_cmax, s_rowe, s_slie, s_rlo, s_rhi;
     const int64_t b = blockIdx.x;
     const int64_t CZ = C * Z;
     const int t = threadIdx.x;
-    const int64_t per = (CZ + VH_TPB - 1) / VH_TPB;
-    const int64_t s = t * per, e = s + per < CZ ? s + per : CZ;
-    int64_t acc = 0;
-    for (int64_t i = s; i < e; ++i) acc += colcount[b * CZ + i];
-    s_part[t] = acc;
+    const bool lf = C <= 32 * MF_FLAGW && Z <= 32 * MF_FLAGW;
+    for (int i = t; i < MF_FLAGW; i += VH_TPB) { s_cf[i] = 0u; s_sf[i] = 0u; }
     if (t == 0) { s_cmin = INT_MAX; s_cmax = 0; s_rowe = 0; s_slie = 0; s_rlo = INT_MAX; s_rhi = -1; }
     __syncthreads();
-    if (t < 64) {   // exclusive scan of the VH_TPB partials by one wave (integers: exact in any order)
-        int64_t v[VH_TPB / 64], tot = 0;
+    const int32_t *cc = colcount + b * CZ;
+    int64_t base = 0;
+    for (int64_t c0 = 0; c0 < CZ; c0 += MF_TILE) {
+        int32_t v[16];
 #pragma unroll
-        for (int q = 0; q < VH_TPB / 64; ++q) { v[q] = s_part[t * (VH_TPB / 64) + q]; tot += v[q]; }
-        int64_t inc = tot;
-        for (int off = 1; off < 64; off <<= 1) {
-            const int64_t o = __shfl_up(inc, off, 64);
-            if (t >= off) inc += o;
+        for (int k = 0; k < 16; ++k) {
+            const int64_t i = c0 + k * VH_TPB + t;
+            v[k] = cc[i < CZ ? i : CZ - 1];
         }
-        int64_t run = inc - tot;
 #pragma unroll
-        for (int q = 0; q < VH_TPB / 64; ++q) { s_part[t * (VH_TPB / 64) + q] = run; run += v[q]; }
+        for (int k = 0; k < 16; ++k) {
+            const int64_t i = c0 + k * VH_TPB + t;
+            const int32_t x = i < CZ ? v[k] : 0;
+            s_cnt[k * VH_TPB + t] = x;
+            if (x) {   // 32-bit division (CZ < 2^31, check_dims)
+                const uint32_t y = (uint32_t)i / (uint32_t)Z, z = (uint32_t)i - y * (uint32_t)Z;
+                if (lf) {
+                    atomicOr(&s_cf[y >> 5], 1u << (y & 31));
+                    atomicOr(&s_sf[z >> 5], 1u << (z & 31));
+                } else {
+                    colany[b * C + y] = 1;
+                    sliceany[b * Z + z] = 1;
+                }
+            }
+        }
+        __syncthreads();
+        int32_t own[16];
+        int64_t acc = 0;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) { own[q] = s_cnt[16 * t + q]; acc += own[q]; }
+        int64_t tot;
+        int64_t run = base + mf_block_excl(acc, s_w, tot);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) { s_ex[16 * t + q] = run; run += own[q]; }
+        __syncthreads();
+        const int64_t cn = CZ - c0 < MF_TILE ? CZ - c0 : MF_TILE;
+        for (int k = t; k < cn; k += VH_TPB) colstart[b * CZ + c0 + k] = s_ex[k];
+        base += tot;
+        __syncthreads();
     }
-    __syncthreads();
-    int64_t run = s_part[t];
-    for (int64_t i = s; i < e; ++i) { colstart[b * CZ + i] = run; run += colcount[b * CZ + i]; }
-    for (int64_t c = t; c < C; c += VH_TPB)
-        if (colany[b * C + c]) {
-            if (c > 0) atomicMin(&s_cmin, (int32_t)c);
-            atomicMax(&s_cmax, (int32_t)c);
+    if (lf) {
+        for (int64_t wi = t; wi < (C + 31) / 32; wi += VH_TPB) {
+            const uint32_t x = s_cf[wi], xm = wi == 0 ? x & ~1u : x;   // column 0 counts for cmax only
+            if (xm) atomicMin(&s_cmin, (int32_t)(wi * 32 + __builtin_ctz(xm)));
+            if (x) atomicMax(&s_cmax, (int32_t)(wi * 32 + 31 - __builtin_clz(x)));
         }
+        for (int64_t z = t; z < Z; z += VH_TPB) {
+            const uint8_t f = (uint8_t)((s_sf[z >> 5] >> (z & 31)) & 1u);
+            sliceany[b * Z + z] = f;
+            if (!f) s_slie = 1;
+        }
+    } else {
+        for (int64_t c = t; c < C; c += VH_TPB)
+            if (colany[b * C + c]) {
+                if (c > 0) atomicMin(&s_cmin, (int32_t)c);
+                atomicMax(&s_cmax, (int32_t)c);
+            }
+        for (int64_t z = t; z < Z; z += VH_TPB)
+            if (!sliceany[b * Z + z]) s_slie = 1;
+    }
     for (int64_t r = t; r < R; r += VH_TPB) {
         if (!rowany[b * R + r]) s_rowe = 1;
         else {
@@ -172,8 +270,6 @@ __global__ void __launch_bounds__(VH_TPB) k_mask_finish(const int32_t *colcount,
             atomicMax(&s_rhi, (int32_t)r);
         }
     }
-    for (int64_t z = t; z < Z; z += VH_TPB)
-        if (!sliceany[b * Z + z]) s_slie = 1;
     __syncthreads();
     if (t == 0) {
         sc[b].cmin = s_cmin;
@@ -196,11 +292,13 @@ void vh_launch_mask_stats(vh_batch *b) {
     VH_CHECK_LAUNCH();
     {
         ScopedKTimer tm(b, "mask_stats", (double)b->V);
-        const int64_t ncb4 = (b->CZ + 4 * VH_TPB - 1) / (4 * VH_TPB);
-        const dim3 grid((unsigned)(ncb4 * ((b->R + VH_SLAB - 1) / VH_SLAB)), (unsigned)b->nb);
-        auto fn = (b->CZ & 3) == 0 ? k_mask_stats<true> : k_mask_stats<false>;
-        fn<<<grid, VH_TPB, 0, st>>>(b->d_mask, b->R, b->C, b->Z, b->V, ncb4, b->d_colbits,
-                                    b->d_colbnz, b->d_rowany, b->d_colany, b->d_sliceany, b->d_sc);
+        // 16 columns per lane (16-byte row loads) when CZ % 16 == 0, else 4 (4-byte or byte loads)
+        const int cpl = (b->CZ & 15) == 0 ? 16 : 4;
+        const int64_t ncb = (b->CZ + cpl * VH_TPB - 1) / (cpl * VH_TPB);
+        const dim3 grid((unsigned)(ncb * ((b->R + VH_SLAB - 1) / VH_SLAB)), (unsigned)b->nb);
+        auto fn = cpl == 16 ? k_mask_stats<16, true> : (b->CZ & 3) == 0 ? k_mask_stats<4, true> : k_mask_stats<4, false>;
+        fn<<<grid, VH_TPB, 0, st>>>(b->d_mask, b->R, b->C, b->Z, b->V, ncb, b->d_colbits,
+                                    b->d_colbnz, b->d_rowany, b->d_sc);
         VH_CHECK_LAUNCH();
         k_mask_cols<<<col_grid(b), VH_TPB, 0, st>>>(b->d_colbnz, b->R, b->CZ, b->d_colrange,
                                                    b->d_colcount);
@@ -274,6 +372,30 @@ __device__ __forceinline__ uint64_t vs_peers(uint32_t d, bool valid) {
     return peers;
 }
 
+#ifndef VS_MATCH_LDS
+#define VS_MATCH_LDS 1
+#endif
+// the same set through a per-wave LDS table of 64-bit lane sets (3 LDS instructions instead of 8
+// ballots and their 64-bit merges): every lane ORs its bit into its digit's entry, reads the entry
+// back and clears it.  A wave's LDS instructions execute in order, so the read sees the whole row's
+// ORs and the next row's ORs see the clear; invalid lanes use the spare entry 256.
+__device__ __forceinline__ uint64_t vs_peers_lds(unsigned long long *m, uint32_t d, bool valid, int lane) {
+    unsigned long long *e = m + (valid ? d : 256u);
+    __hip_atomic_fetch_or(e, 1ull << lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    const uint64_t p = __hip_atomic_load(e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    __hip_atomic_store(e, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    return valid ? p : 0ull;
+}
+#if VS_MATCH_LDS
+#define VS_PEERS(d, valid) vs_peers_lds(&s_match[w][0], d, valid, lane)
+#define VS_MATCH_DECL __shared__ unsigned long long s_match[VS_WAVES][257]
+#define VS_MATCH_INIT for (int i_ = lane; i_ < 257; i_ += 64) s_match[w][i_] = 0ull
+#else
+#define VS_PEERS(d, valid) vs_peers(d, valid)
+#define VS_MATCH_DECL
+#define VS_MATCH_INIT
+#endif
+
 __global__ void __launch_bounds__(VS_TPB) k_sort_vol(uint32_t *__restrict__ k0,
                                                     uint32_t *__restrict__ k1,
                                                     const VolScalars *sc, int64_t V) {
@@ -283,12 +405,14 @@ __global__ void __launch_bounds__(VS_TPB) k_sort_vol(uint32_t *__restrict__ k0,
     __shared__ uint32_t s_tot[256], s_cst[256], s_wsum[4];   // chunk digit totals / starts
     __shared__ uint32_t s_stage[VS_CHUNK + 1];   // the chunk in digit order (+ a slot for invalid keys)
     __shared__ uint32_t s_off[256];              // digit d's output position minus its chunk-local start
+    VS_MATCH_DECL;
     const int64_t b = blockIdx.x;
     const int64_t n = sc[b].n_mask;
     if (n <= 1) return;
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     const uint64_t lt = (1ull << lane) - 1ull;
     for (int i = t; i < 4 * 256; i += VS_TPB) (&s_hist[0][0])[i] = 0u;
+    VS_MATCH_INIT;
     __syncthreads();
     uint32_t *kin = k0 + b * V, *kout = k1 + b * V;
 #ifdef VS_PROF
@@ -360,7 +484,7 @@ __global__ void __launch_bounds__(VS_TPB) k_sort_vol(uint32_t *__restrict__ k0,
                 const uint32_t d = (kk >> shift) & 255u;
                 // a row that shares one digit (typical of high digits) needs no match ballots
                 const uint32_t d0 = (uint32_t)__shfl((int)d, 0, 64);
-                const uint64_t peers = __all(!valid || d == d0) ? __ballot(valid) : vs_peers(d, valid);
+                const uint64_t peers = __all(!valid || d == d0) ? __ballot(valid) : VS_PEERS(d, valid);
                 const uint32_t below = (uint32_t)__popcll(peers & lt);
                 // the digit group's leader reserves its slots with a returning LDS add (a wave's
                 // LDS atomics complete in issue order, so rows stay ordered) and hands the base
@@ -510,6 +634,7 @@ __global__ void __launch_bounds__(VS_TPB) k_sortg_scatter(const uint32_t *__rest
     __shared__ uint32_t s_wc[VS_WAVES][256];
     __shared__ uint32_t s_tot[256], s_cst[256], s_wsum[4], s_off[256];
     __shared__ uint32_t s_stage[VS_CHUNK];
+    VS_MATCH_DECL;
     const int64_t n = sc[b].n_mask;
     const int64_t c0 = (int64_t)blockIdx.x * VS_CHUNK;
     if (n <= 1 || c0 >= n) return;
@@ -517,6 +642,7 @@ __global__ void __launch_bounds__(VS_TPB) k_sortg_scatter(const uint32_t *__rest
     const uint64_t lt = (1ull << lane) - 1ull;
     for (int d = lane; d < 256; d += 64) s_wc[w][d] = 0u;
     if (t < 256) s_off[t] = off[(int64_t)blockIdx.x * 256 + t];
+    VS_MATCH_INIT;
     __syncthreads();
     uint32_t key[VS_KPT], rank[VS_KPT];
 #pragma unroll
@@ -531,7 +657,7 @@ __global__ void __launch_bounds__(VS_TPB) k_sortg_scatter(const uint32_t *__rest
         const uint32_t kk = key[r];
         const uint32_t d = (kk >> shift) & 255u;
         const uint32_t d0 = (uint32_t)__shfl((int)d, 0, 64);
-        const uint64_t peers = __all(!valid || d == d0) ? __ballot(valid) : vs_peers(d, valid);
+        const uint64_t peers = __all(!valid || d == d0) ? __ballot(valid) : VS_PEERS(d, valid);
         const uint32_t below = (uint32_t)__popcll(peers & lt);
         uint32_t base = 0u;
         if (valid && below == 0) base = atomicAdd(&s_wc[w][d], (uint32_t)__popcll(peers));
