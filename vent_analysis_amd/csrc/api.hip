@@ -21,10 +21,29 @@
 // ---------------------------------------------------------------------------------------------
 // timing
 // ---------------------------------------------------------------------------------------------
-ScopedKTimer::ScopedKTimer(vh_batch *bb, const char *name, double bytes) : b(bb), t(nullptr) {
+static void kst_reset(vh_batch *b) {
+    HIP_TRY(hipMemsetAsync(b->d_kst, 0xFF, sizeof(unsigned long long) * VH_KST_CAP, b->stream));
+    HIP_TRY(hipMemsetAsync(b->d_kst + VH_KST_CAP, 0, sizeof(unsigned long long) * VH_KST_CAP, b->stream));
+    b->kst_n = 0;
+}
+
+ScopedKTimer::ScopedKTimer(vh_batch *bb, const char *name, double bytes, bool stamped)
+    : b(bb), t(nullptr) {
     if (!b->profile) return;
     t = &b->timers[name];
     if (bytes > 0) t->bytes_per_launch = bytes;
+    if (stamped) {
+        if (!b->d_kst) {
+            HIP_TRY(hipMalloc((void **)&b->d_kst, sizeof(unsigned long long) * 2 * VH_KST_CAP));
+            kst_reset(b);
+        }
+        if (b->kst_n < VH_KST_CAP) {
+            const int s = b->kst_n++;
+            t->slots.push_back(s);
+            ks = b->d_kst + s;
+            return;
+        }   // (every slot taken until the next resolve: events)
+    }
     hipEvent_t e0;
     HIP_TRY(hipEventCreate(&e0));
     HIP_TRY(hipEventCreate(&e1));
@@ -32,7 +51,7 @@ ScopedKTimer::ScopedKTimer(vh_batch *bb, const char *name, double bytes) : b(bb)
     t->ev.push_back(e0);
 }
 ScopedKTimer::~ScopedKTimer() {
-    if (!t) return;
+    if (!t || ks) return;
     (void)hipEventRecord(e1, b->stream);
     t->ev.push_back(e1);
 }
@@ -41,9 +60,21 @@ static void clear_timers(vh_batch *b) {
     for (auto &kv : b->timers)
         for (auto e : kv.second.ev) (void)hipEventDestroy(e);
     b->timers.clear();
+    if (b->d_kst && b->kst_n) kst_reset(b);
 }
 
 static void resolve_timers(vh_batch *b) {
+    std::vector<unsigned long long> ks;
+    double ticks_per_ms = 0.0;
+    if (b->d_kst && b->kst_n) {   // the stamped launches' spans (wall clock ticks; the rate in kHz)
+        HIP_TRY(hipStreamSynchronize(b->stream));
+        ks.resize(2 * VH_KST_CAP);
+        HIP_TRY(hipMemcpy(ks.data(), b->d_kst, sizeof(unsigned long long) * 2 * VH_KST_CAP,
+                          hipMemcpyDeviceToHost));
+        int khz = 0;
+        HIP_TRY(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, b->ctx->device));
+        ticks_per_ms = (double)khz;
+    }
     for (auto &kv : b->timers) {
         KTimer &t = kv.second;
         for (size_t i = 0; i + 1 < t.ev.size(); i += 2) {
@@ -56,7 +87,14 @@ static void resolve_timers(vh_batch *b) {
             (void)hipEventDestroy(t.ev[i + 1]);
         }
         t.ev.clear();
+        for (int s : t.slots) {
+            const unsigned long long s0 = ks[s], s1 = ks[VH_KST_CAP + s];
+            if (s1 >= s0 && ticks_per_ms > 0.0) t.total_ms += (double)(s1 - s0) / ticks_per_ms;
+            t.launches += 1;
+        }
+        t.slots.clear();
     }
+    if (!ks.empty()) kst_reset(b);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -106,6 +144,7 @@ static void check_dims(int64_t R, int64_t C, int64_t Z, int64_t batch) {
 static void batch_free(vh_batch *b) {
     if (!b) return;
     clear_timers(b);
+    dfree(b->d_kst);
     dfree(b->d_hp); dfree(b->d_mask); dfree(b->d_n4);
     dfree(b->d_defect); dfree(b->d_border); dfree(b->d_lb);
     dfree(b->d_colrange); dfree(b->d_colcount); dfree(b->d_colstart); dfree(b->d_colbits); dfree(b->d_colbnz); dfree(b->d_snrpart);

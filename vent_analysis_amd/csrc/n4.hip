@@ -1651,14 +1651,17 @@ __global__ void __launch_bounds__(PC_TPB) k_n4_pcg(PcgArgs A) {
 __global__ void __launch_bounds__(PC_TPB) k_n4_pcg2(Pcg2Args A) {
     namespace cg = cooperative_groups;
     cg::grid_group grid = cg::this_grid();
-    if (!A.st[A.b].active) return;   // uniform over the grid
     __shared__ Pcg2Lds L;
     __shared__ float T0[PCG_G0 * (PC_TPB + 8)];   // pass 0's transpose (pcg2_body)
-    // pass 0's loads: the perm loads of a group issued together, then the d loads they address
-    const float *const D = A.D;
-    const int32_t *const perm = A.perm;
-    pcg2_body(A, L, grid, [=](int64_t r) { return D[perm[r]]; },
-              A.t0 ? T0 : nullptr);
+    kst_begin(A.kst);   // profiling: this launch's span (stamped timer)
+    if (A.st[A.b].active) {   // uniform over the grid
+        // pass 0's loads: the perm loads of a group issued together, then the d loads they address
+        const float *const D = A.D;
+        const int32_t *const perm = A.perm;
+        pcg2_body(A, L, grid, [=](int64_t r) { return D[perm[r]]; },
+                  A.t0 ? T0 : nullptr);
+    }
+    kst_end(A.kst);
 }
 
 // Exact cubic B-spline subdivision (spans doubled on every axis), axis by axis, one block/volume.
@@ -2039,8 +2042,9 @@ static void n4_subbatch(vh_batch *b, const vh_n4_params &prm, int64_t vol0, int6
                                                                b->d_st, vol0);
                     VH_CHECK_LAUNCH();
                 } else if (cm == 0 && pcg_grid > 0 && !pcg_v1) {   // one large study: PC over the GPU
-                    ScopedKTimer tm(b, "n4_pcg", 0.0);
+                    ScopedKTimer tm(b, "n4_pcg", 0.0, true);   // stamped: a cooperative launch
                     Pcg2Args A = pcg2_args;
+                    A.kst = tm.stamp();
                     A.b = vol0;
                     A.D = b->d_D + vol0 * b->VS;
                     A.perm = b->d_perm + vol0 * b->VS;

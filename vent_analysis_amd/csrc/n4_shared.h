@@ -2269,6 +2269,7 @@ struct Pcg2Args {
     unsigned long long *gran;
     uint32_t tag0;
     int32_t t0;             // k_n4_pcg2: pass 0 through the LDS transpose (pcg2_body's T0)
+    unsigned long long *kst;   // profiling: the launch's stamped-timer slot (kst_begin / kst_end), or null
 };
 // A round record as PCG_GW tagged granules (cdna_hip_programming.md Guideline 16, R2: the data is the
 // flag): each 32-bit word of the record in an 8-byte {tag, word} granule written by ONE relaxed

@@ -55,7 +55,9 @@
 #ifndef ST_EVAL_EXP
 #define ST_EVAL_EXP 0   // 1: eval stores p = expf_cr(d) for PC (its pass 0 then skips the exp)
 #endif
-static_assert(ST_TPB == 1024 || ST_TPB == 512, "pcw_run takes the whole workgroup (one block per thread)");
+// 1024 only: the round-4 512-thread build (two studies per CU) no longer
+// converges since the round-5/6 PC changes (r6t: every level runs 50 iterations) and is not kept up
+static_assert(ST_TPB == 1024, "pcw_run takes the whole workgroup (one block per thread)");
 constexpr int ST_NB = 2;   // U buffers: the last computed field's and the one being computed
 
 // ST_PROF builds (scripts/dev/phase_ab.sh): block 0 prints shader cycles per phase at the end
@@ -1220,6 +1222,7 @@ __global__ void __launch_bounds__(ST_TPB, 4) k_n4_studyg(StudyArgs a, StudyGrid 
 
     const int64_t n = a.sc[b].n_mask1;
     N4State *stb = a.st + b;
+    kst_begin(gd.pc.kst);   // profiling: this launch's span (stamped timer)
     if (r == 0 && t == 0) {
         stb->t_start = wall_clock64();
         stb->hw_id = __builtin_amdgcn_s_getreg((31 << 11) | 4);
@@ -1236,6 +1239,7 @@ __global__ void __launch_bounds__(ST_TPB, 4) k_n4_studyg(StudyArgs a, StudyGrid 
             }
             if (t == 0) stb->t_end = wall_clock64();
         }
+        kst_end(gd.pc.kst);
         return;
     }
     Grp g;
@@ -1673,6 +1677,7 @@ __global__ void __launch_bounds__(ST_TPB, 4) k_n4_studyg(StudyArgs a, StudyGrid 
             stb->t_end = wall_clock64();
         }
     }
+    kst_end(gd.pc.kst);
 }
 
 // Workgroup -> study, the largest study (most mask == 1 voxels, the best a-priori proxy of its
@@ -1972,8 +1977,8 @@ void vh_launch_n4_studyg(vh_batch *b, const vh_n4_params &prm) {
         b->stg_cap = (int64_t)need;
     }
     vh_set_max_lds((const void *)k_n4_studyg, (int)(ST_MAX_LDS - sizeof(Pcg2Lds)));
-    ScopedKTimer tm(b, "n4_study", 0.0);
     for (int64_t v = 0; v < b->nb; ++v) {   // one study per launch (the class and configs 2 / 5: one)
+        ScopedKTimer tm(b, "n4_study", 0.0, true);   // stamped: a cooperative launch
         char *w = (char *)b->d_stg;
         StudyGrid gd{};
         gd.hsum = (unsigned long long *)w; w += b_h;
@@ -1995,6 +2000,7 @@ void vh_launch_n4_studyg(vh_batch *b, const vh_n4_params &prm) {
         gd.pc.st = b->d_st;
         gd.pc.b = v;
         gd.pc.skip_thresh = 0.0f;
+        gd.pc.kst = tm.stamp();
         HIP_TRY(hipMemsetAsync(b->d_stg, 0, b_h + b_n + b_g, b->stream));
         StudyArgs av = a;
         av.vol0 = v;

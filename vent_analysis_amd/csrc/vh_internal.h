@@ -123,6 +123,7 @@ struct AxisTab {
 
 struct KTimer {
     std::vector<hipEvent_t> ev;   // pairs (start, stop)
+    std::vector<int> slots;       // stamped launches: slots of vh_batch::d_kst
     double bytes_per_launch = 0;
     double total_ms = 0;
     int64_t launches = 0;
@@ -273,6 +274,10 @@ struct vh_batch {
     // timing
     bool profile = false;
     std::map<std::string, KTimer> timers;
+    // stamped timers (cooperative launches): [VH_KST_CAP] first-workgroup starts, then
+    // [VH_KST_CAP] last-workgroup ends, device wall clock; kst_n slots handed out since the reset
+    unsigned long long *d_kst = nullptr;
+    int kst_n = 0;
     // last run options
     vh_run_opts opts{};
     bool have_result = false;
@@ -288,13 +293,28 @@ struct vh_ci_table {
 };
 
 // ---- timing helper ----------------------------------------------------------------------------
+// stamped (profiling a cooperative launch): no events; the kernel stamps its own span through
+// stamp() (kst_begin / kst_end), because HIP events around hipLaunchCooperativeKernel also time the
+// runtime's cooperative handshake (config 5 k_n4_pcg2: 677 us per launch by events against 542 us in
+// rocprofv3's trace, whose gaps round the launch are ~13 us each, r6q)
 struct ScopedKTimer {
     vh_batch *b;
     KTimer *t;
     hipEvent_t e1 = nullptr;
-    ScopedKTimer(vh_batch *bb, const char *name, double bytes);
+    unsigned long long *ks = nullptr;
+    ScopedKTimer(vh_batch *bb, const char *name, double bytes, bool stamped = false);
     ~ScopedKTimer();
+    unsigned long long *stamp() const { return ks; }   // null unless stamped and profiling
 };
+#define VH_KST_CAP 4096
+// a stamped launch's span: thread 0 of every workgroup at its start / end (vector atomics)
+__device__ __forceinline__ void kst_begin(unsigned long long *s) {
+    if (s && threadIdx.x == 0) atomicMin(s, (unsigned long long)wall_clock64());
+}
+__device__ __forceinline__ void kst_end(unsigned long long *s) {
+    __syncthreads();
+    if (s && threadIdx.x == 0) atomicMax(s + VH_KST_CAP, (unsigned long long)wall_clock64());
+}
 
 // ---- launchers (defined in vdp.hip / n4.hip / ci.hip) ---------------------------------------
 void vh_launch_mask_stats(vh_batch *b);
