@@ -159,10 +159,14 @@ def algorithmic_bytes(name, hp, mk, res, R, C, Z, study=True, conv_mode=0):
     return 0.0
 
 
-def lib_digest(path=None):
-    """sha256 of the libventhip.so this process runs (vent_analysis_amd/_lib.LIB_PATH)."""
+_OWN_LIB = object()
+
+
+def lib_digest(path=_OWN_LIB):
+    """sha256 of the libventhip.so this process runs (vent_analysis_amd/_lib.LIB_PATH), or of
+    ``path``; None for a surface with no shared object (the dry run's stand-in: LIB_PATH None)."""
     import hashlib
-    if path is None:
+    if path is _OWN_LIB:
         from vent_analysis_amd import _lib
         path = getattr(_lib, "LIB_PATH", None)
     try:
@@ -183,7 +187,7 @@ def summary_workload(d):
     return d.get("workload") or DEFAULT_WORKLOAD
 
 
-def pmc_traffic(kernel, workload, digest=None):
+def pmc_traffic(kernel, workload, digest=_OWN_LIB):
     """Per-launch HBM-side bytes of ``kernel`` from the newest committed PMC summary
     (profiles/r*_pmc_traffic.json, written by scripts/pmc_summary.py from separate rocprofv3 --pmc
     passes) of this very library (its sha256) AND this very workload (workload_key: shape, batch,
@@ -196,7 +200,9 @@ def pmc_traffic(kernel, workload, digest=None):
     files = sorted(glob.glob(os.path.join(HERE, "profiles", "r*_pmc_traffic.json")), key=run_order)
     if not files:
         return None, None, "no committed PMC summary"
-    mine = digest if digest is not None else lib_digest()
+    mine = lib_digest() if digest is _OWN_LIB else digest
+    if mine is None:   # no shared object to match (the dry run's stand-in)
+        return None, None, "stale: no library digest, no summary can match"
     same_lib = None
     for f in reversed(files):   # the newest summary of this library and workload
         d = json.load(open(f))
