@@ -634,6 +634,118 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_rrank(const uint64_t *rowmask, co
     }
 }
 
+// One stage of a 32 x 32 bit-matrix transpose (element (i, j) = bit j of A[i]): rows k and k + J
+// (k with bit J clear) swap the J-bit blocks above / below the diagonal.
+template <int J>
+__device__ __forceinline__ void bit_swap_stage(uint32_t (&A)[32], uint32_t m) {
+#pragma unroll
+    for (int k0 = 0; k0 < 32; k0 += 2 * J)
+#pragma unroll
+        for (int k = k0; k < k0 + J; ++k) {
+            const uint32_t tt = ((A[k] >> J) ^ A[k + J]) & m;
+            A[k] ^= tt << J;
+            A[k + J] ^= tt;
+        }
+}
+
+// k_n4_rowcount + k_n4_rowscan + k_n4_rrank in one workgroup of 1024 threads per volume, for
+// volumes with nrs = tiles x R <= RP_MAX_NRS.  Each thread takes 16 columns of one bitmap word
+// (32 rows) and transposes them into 32 16-bit row pieces (a bit-matrix transpose: ~400 bit
+// operations instead of 32 ballots and their 64-bit selects per word): the quarter (c % 64) / 16 of
+// the (tile, row) lane masks, stored as 16-bit pieces of the u64 rowmask, and their popcounts added
+// into the (tile, row) counts in LDS.  Then from that LDS copy: raster ranks (row totals, their scan,
+// each row's running count over the tiles) and the compact offsets (the exclusive scan in tile-major
+// order).  Integers only: the same values as the three kernels.
+#define RP_MAX_NRS 16384
+#define RP_MAX_R 4096
+#define RP_TPB 1024
+__global__ void __launch_bounds__(RP_TPB) k_n4_rowprep(const uint32_t *colbits, int64_t R, int64_t CZ,
+                                                      int64_t ntiles, int32_t *rs, uint64_t *rowmask,
+                                                      int32_t *rrank) {
+    extern __shared__ int32_t s_dyn[];   // [nrs] counts, then [R] row totals -> row bases
+    __shared__ int64_t s_part[RP_TPB];
+    const int64_t b = blockIdx.x, nrs = ntiles * R;
+    const int64_t nw = (R + 31) >> 5;
+    int32_t *s_cnt = s_dyn, *s_row = s_dyn + nrs;
+    const int t = threadIdx.x;
+    for (int64_t i = t; i < nrs; i += RP_TPB) s_cnt[i] = 0;
+    __syncthreads();
+    const int64_t nq = ntiles * 4;   // 16-column groups, the last tile's past CZ included (zeros)
+    uint16_t *rm16 = reinterpret_cast<uint16_t *>(rowmask + b * nrs);
+    for (int64_t item = t; item < nw * nq; item += RP_TPB) {
+        const int64_t w = item / nq, g = item - w * nq, c0 = g * 16;
+        const uint32_t *src = colbits + (b * nw + w) * CZ;
+        uint32_t A[32];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {   // unconditional at a clamped column: the 16 loads in flight
+            const int64_t c = c0 + i;
+            const uint32_t v = src[c < CZ ? c : CZ - 1];
+            const uint32_t x = c < CZ ? v : 0u;
+            A[i] = x & 0xFFFFu;
+            A[i + 16] = x >> 16;
+        }
+        bit_swap_stage<8>(A, 0x00FF00FFu);   // (the first stage, J = 16, was the split above)
+        bit_swap_stage<4>(A, 0x0F0F0F0Fu);
+        bit_swap_stage<2>(A, 0x33333333u);
+        bit_swap_stage<1>(A, 0x55555555u);
+        // A[k] bit i: column c0 + i at row 32 w + k
+        const int64_t tile = g >> 2, x0 = w * 32;
+        uint16_t *dst = rm16 + (tile * R + x0) * 4 + (g & 3);
+        int32_t *cnt = s_cnt + tile * R + x0;
+#pragma unroll
+        for (int k = 0; k < 32; ++k)
+            if (x0 + k < R) {
+                dst[4 * k] = (uint16_t)A[k];
+                if (A[k]) atomicAdd(&cnt[k], __popc(A[k]));
+            }
+    }
+    __syncthreads();
+    for (int64_t x = t; x < R; x += RP_TPB) {   // row totals over the tiles
+        int32_t run = 0;
+        for (int64_t tt = 0; tt < ntiles; ++tt) run += s_cnt[tt * R + x];
+        s_row[x] = run;
+    }
+    __syncthreads();
+    auto block_excl = [&](int32_t *a, int64_t n, int32_t *out_g) {
+        // exclusive scan of a[0, n) in place (thread chunks, then one wave over the partials); with
+        // out_g the scanned values go to global memory instead (a keeps the counts)
+        const int64_t per = (n + RP_TPB - 1) / RP_TPB;
+        const int64_t s0 = t * per < n ? t * per : n, e0 = s0 + per < n ? s0 + per : n;
+        int64_t acc = 0;
+        for (int64_t i = s0; i < e0; ++i) acc += a[i];
+        s_part[t] = acc;
+        __syncthreads();
+        if (t < 64) {
+            int64_t v[RP_TPB / 64], tot = 0;
+#pragma unroll
+            for (int q = 0; q < RP_TPB / 64; ++q) { v[q] = s_part[t * (RP_TPB / 64) + q]; tot += v[q]; }
+            int64_t inc = tot;
+            for (int off = 1; off < 64; off <<= 1) {
+                const int64_t o = __shfl_up(inc, off, 64);
+                if (t >= off) inc += o;
+            }
+            int64_t run = inc - tot;
+#pragma unroll
+            for (int q = 0; q < RP_TPB / 64; ++q) { s_part[t * (RP_TPB / 64) + q] = run; run += v[q]; }
+        }
+        __syncthreads();
+        int32_t run = (int32_t)s_part[t];
+        for (int64_t i = s0; i < e0; ++i) {
+            const int32_t v = a[i];
+            if (out_g) out_g[i] = run; else a[i] = run;
+            run += v;
+        }
+        __syncthreads();
+    };
+    block_excl(s_row, R, nullptr);   // row bases: masked voxels of the rows before
+    int32_t *rr = rrank + b * nrs;
+    for (int64_t x = t; x < R; x += RP_TPB) {   // raster rank of each (tile, row)'s first masked voxel
+        int32_t r = s_row[x];
+        for (int64_t tt = 0; tt < ntiles; ++tt) { rr[tt * R + x] = r; r += s_cnt[tt * R + x]; }
+    }
+    block_excl(s_cnt, nrs, rs + b * nrs);   // compact offsets, tile-major
+}
+
 // perm[raster rank] = compact index: one wave per (tile, row), one lane per column of the tile
 __global__ void __launch_bounds__(VH_TPB) k_n4_perm(const uint64_t *rowmask, const int32_t *rowstart,
                                                    const int32_t *rrank, int64_t R, int64_t ntiles,
@@ -2122,11 +2234,19 @@ void vh_launch_n4(vh_batch *b, const vh_n4_params &prm) {
     b->n4_used_study = mode == 2 || (mode == 0 && fits && b->nb >= 16) || use_grid;
     {
         ScopedKTimer tm(b, "n4_init", 0.0);
-        k_n4_rowcount<<<dim3((unsigned)ntiles, (unsigned)b->nb), 64, 0, st>>>(
-            b->d_colbits, b->R, b->CZ, ntiles, b->d_rowstart, b->d_rowmask);
-        VH_CHECK_LAUNCH();
         const int64_t nrs = ntiles * b->R;
-        if (nrs <= ((int64_t)1 << 16)) {   // small volumes (the bench): one workgroup per volume
+        const bool prep = nrs <= RP_MAX_NRS && b->R <= RP_MAX_R && !getenv("VH_ROWPREP_OLD");
+        if (prep) {   // masks, counts, raster ranks and offsets in one launch per volume
+            k_n4_rowprep<<<(unsigned)b->nb, RP_TPB, sizeof(int32_t) * (size_t)(nrs + b->R), st>>>(
+                b->d_colbits, b->R, b->CZ, ntiles, b->d_rowstart, b->d_rowmask, b->d_rrank);
+            VH_CHECK_LAUNCH();
+        } else {
+            k_n4_rowcount<<<dim3((unsigned)ntiles, (unsigned)b->nb), 64, 0, st>>>(
+                b->d_colbits, b->R, b->CZ, ntiles, b->d_rowstart, b->d_rowmask);
+            VH_CHECK_LAUNCH();
+        }
+        if (prep) {
+        } else if (nrs <= ((int64_t)1 << 16)) {   // small volumes (the bench): one workgroup per volume
             k_n4_rowscan<<<(unsigned)b->nb, VH_TPB, 0, st>>>(b->d_rowstart, nrs);
             VH_CHECK_LAUNCH();
             if (b->R > 16384) throw VhError{VH_ERR_ARG, "N4: more than 16384 rows"};

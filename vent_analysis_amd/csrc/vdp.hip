@@ -438,16 +438,30 @@ __global__ void __launch_bounds__(VS_TPB) k_sort_vol(uint32_t *__restrict__ k0,
 #ifdef VS_PROF
             if (valid) vor |= kr[r] ^ vfirst;
 #endif
-            const uint64_t vmask = __ballot(valid);   // outside the lane-0 branch
-#pragma unroll
-            for (int p = 0; p < 4; ++p) {
-                const uint32_t d = (kr[r] >> (8 * p)) & 255u;
-                const uint32_t d0 = (uint32_t)__shfl((int)d, 0, 64);
-                if (__all(!valid || d == d0)) {   // one digit in the row (typical of high digits)
-                    if (lane == 0 && vmask) atomicAdd(&s_hist[p][d0], (uint32_t)__popcll(vmask));
-                } else if (valid) {                 // spread digits: plain adds, few collisions
-                    atomicAdd(&s_hist[p][d], 1u);
-                }
+            // valid lanes are a prefix of the row, so lane 0's key stands for the row when any is
+            // valid.  Digits 0 and 1 nearly always differ inside a row: plain adds, no test.  Digit
+            // 3 nearly always agrees: one row test and one add of the row's count; digit 2 takes
+            // the same test and either path.  (Round 6: four shuffle-and-vote tests per row, one
+            // per digit, made this pass the sort's costliest after the ranking.)
+            const uint32_t kk = kr[r];
+            const uint64_t vmask = __ballot(valid);
+            const uint32_t k0r = (uint32_t)__builtin_amdgcn_readfirstlane((int)kk);
+            const uint32_t cnt = (uint32_t)__popcll(vmask);
+            if (valid) {
+                atomicAdd(&s_hist[0][kk & 255u], 1u);
+                atomicAdd(&s_hist[1][(kk >> 8) & 255u], 1u);
+            }
+            const bool same3 = __ballot(valid && (kk >> 24) != (k0r >> 24)) == 0ull;
+            const bool same2 = __ballot(valid && ((kk >> 16) & 255u) != ((k0r >> 16) & 255u)) == 0ull;
+            if (same3) {
+                if (lane == 0 && cnt) atomicAdd(&s_hist[3][k0r >> 24], cnt);
+            } else if (valid) {
+                atomicAdd(&s_hist[3][kk >> 24], 1u);
+            }
+            if (same2) {
+                if (lane == 0 && cnt) atomicAdd(&s_hist[2][(k0r >> 16) & 255u], cnt);
+            } else if (valid) {
+                atomicAdd(&s_hist[2][(kk >> 16) & 255u], 1u);
             }
         }
     }
@@ -482,8 +496,9 @@ __global__ void __launch_bounds__(VS_TPB) k_sort_vol(uint32_t *__restrict__ k0,
                 const bool valid = idx < n;
                 const uint32_t kk = key[r];
                 const uint32_t d = (kk >> shift) & 255u;
-                // a row that shares one digit (typical of high digits) needs no match ballots
-                const uint32_t d0 = (uint32_t)__shfl((int)d, 0, 64);
+                // a row that shares one digit (typical of high digits) needs no match ballots (lane
+                // 0 is valid whenever any lane is: valid lanes are a prefix of the row)
+                const uint32_t d0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)d);
                 const uint64_t peers = __all(!valid || d == d0) ? __ballot(valid) : VS_PEERS(d, valid);
                 const uint32_t below = (uint32_t)__popcll(peers & lt);
                 // the digit group's leader reserves its slots with a returning LDS add (a wave's
@@ -656,7 +671,7 @@ __global__ void __launch_bounds__(VS_TPB) k_sortg_scatter(const uint32_t *__rest
         const bool valid = idx < n;
         const uint32_t kk = key[r];
         const uint32_t d = (kk >> shift) & 255u;
-        const uint32_t d0 = (uint32_t)__shfl((int)d, 0, 64);
+        const uint32_t d0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)d);   // (valid lanes: a prefix)
         const uint64_t peers = __all(!valid || d == d0) ? __ballot(valid) : VS_PEERS(d, valid);
         const uint32_t below = (uint32_t)__popcll(peers & lt);
         uint32_t base = 0u;
