@@ -1843,14 +1843,15 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_final(const float *__restrict__ I
     __syncthreads();
     const bool act = col < CZ;
     const int64_t nw = (R + 31) >> 5;
-    const bool emit = keys != nullptr && s.n_mask == s.n_mask1;   // block-uniform
-    // keys: the wave's 64 columns own one contiguous run of k_gather's column compaction, slab by
-    // slab; the sort needs the values only, so they are stored row by row across the wave
+    const bool emit = keys != nullptr;   // block-uniform
+    // keys of the mask != 0 voxels (k_gather's set; for a binary mask the N4 label's): the wave's 64
+    // columns own one contiguous run of k_gather's column compaction, slab by slab; the sort needs
+    // the values only, so they are stored row by row across the wave
     int64_t kpos = 0;
     if (emit) {
         int before = 0;   // this column's keys in the earlier slabs
         if (act)
-            for (int64_t w = 0; w < sl; ++w) before += __popc(colbits[(b * nw + w) * CZ + col]);
+            for (int64_t w = 0; w < sl; ++w) before += __popc(colbnz[(b * nw + w) * CZ + col]);
         for (int off = 32; off > 0; off >>= 1) before += __shfl_xor(before, off, 64);
         if (act) kpos = b * V + colstart[b * CZ + (col & ~(int64_t)63)] + before;
     }
@@ -1861,7 +1862,6 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_final(const float *__restrict__ I
         const int by = lv.ax[1].base[y];
         const float4 wy = *reinterpret_cast<const float4 *>(lv.ax[1].w + 4 * y);
         const double *p1 = P1 + b * q2_cap;
-        const uint32_t word = colbits[(b * nw + sl) * CZ + col];
         const uint32_t sig = colbnz[(b * nw + sl) * CZ + col];
         const uint32_t noise = snr_col_noise(sb, s, b, Z, col, s_rows);
         snr_count(acc, noise);
@@ -1908,7 +1908,7 @@ __global__ void __launch_bounds__(VH_TPB) k_n4_final(const float *__restrict__ I
                     dst[(int64_t)i * CZ] = o;
                     snr_add(acc, x, (sig >> i) & 1u, (noise >> i) & 1u);
                     if (emit) {
-                        const bool on = (word >> i) & 1u;
+                        const bool on = (sig >> i) & 1u;
                         const uint64_t bal = __ballot(on);
                         if (on) keys[kpos + lanes_below(bal)] = f2key(o);
                         kpos += __popcll(bal);
@@ -2322,7 +2322,7 @@ void vh_launch_n4(vh_batch *b, const vh_n4_params &prm) {
                                                     b->part_blocks, b->q2_cap, b->d_P1, lv,
                                                     b->d_colbits, b->d_colbnz, b->d_colstart,
                                                     b->d_sc, b->d_keys0, sbox);
-        b->keys_fused = true;   // the VDP chain's gather skips volumes with binary masks
+        b->keys_fused = true;   // the VDP chain's gather is not needed
         b->snr_fused = true;    // and the SNR partials of the input image are done
         VH_CHECK_LAUNCH();
     }
