@@ -2290,11 +2290,10 @@ void vh_launch_snr(vh_batch *b) {
 void vh_launch_vdp_chain(vh_batch *b, const float *d_n4, const vh_run_opts &o) {
     hipStream_t st = b->stream;
     const int64_t CZ = b->CZ;
-    {
+    if (!(o.do_n4 && b->keys_fused)) {   // (after N4, k_n4_final emitted every volume's keys)
         ScopedKTimer tm(b, "gather", 5.0 * (double)b->V);
         k_gather<<<col_grid(b), VH_TPB, 0, st>>>(d_n4, b->d_mask, b->d_colrange, b->d_colstart,
-                                                 CZ, b->V, b->d_sc,
-                                                 (o.do_n4 && b->keys_fused) ? 1 : 0, b->d_keys0);
+                                                 CZ, b->V, b->d_sc, 0, b->d_keys0);
         VH_CHECK_LAUNCH();
     }
     {
