@@ -14,6 +14,6 @@ for round in 1 2; do
     env "${E[@]}" timeout -k 10 300 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-h2h \
         > gpurun_out/${TAG}_${i}_$round.json 2> gpurun_out/${TAG}_${i}_$round.err
     rc=$?; [ $rc -eq 0 ] || { echo "$set rc=$rc"; tail -3 gpurun_out/${TAG}_${i}_$round.err; exit $rc; }
-    python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().splitlines()[-1]); r=d['roofline']; print(sys.argv[2], d['value'], d['ms_per_step'], 'non_n4', r.get('non_n4_us_per_step'), {k: v for k, v in r['kernel_us_per_step'].items() if k != 'n4_study'})" gpurun_out/${TAG}_${i}_$round.json "$set"
+    python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().splitlines()[-1]); r=d['roofline']; print(sys.argv[2], d['value'], d['ms_per_step'], 'lat', d.get('batch_latency_ms'), 'non_n4', r.get('non_n4_us_per_step'), 'wall', r.get('non_n4_wall_us_per_step'), {k: v for k, v in r['kernel_us_per_step'].items() if k != 'n4_study'})" gpurun_out/${TAG}_${i}_$round.json "$set"
   done
 done

@@ -27,8 +27,8 @@ static void kst_reset(vh_batch *b) {
     b->kst_n = 0;
 }
 
-ScopedKTimer::ScopedKTimer(vh_batch *bb, const char *name, double bytes, bool stamped)
-    : b(bb), t(nullptr) {
+ScopedKTimer::ScopedKTimer(vh_batch *bb, const char *name, double bytes, bool stamped, hipStream_t on)
+    : b(bb), t(nullptr), s(on ? on : bb->stream) {
     if (!b->profile) return;
     t = &b->timers[name];
     if (bytes > 0) t->bytes_per_launch = bytes;
@@ -47,12 +47,12 @@ ScopedKTimer::ScopedKTimer(vh_batch *bb, const char *name, double bytes, bool st
     hipEvent_t e0;
     HIP_TRY(hipEventCreate(&e0));
     HIP_TRY(hipEventCreate(&e1));
-    HIP_TRY(hipEventRecord(e0, b->stream));
+    HIP_TRY(hipEventRecord(e0, s));
     t->ev.push_back(e0);
 }
 ScopedKTimer::~ScopedKTimer() {
     if (!t || ks) return;
-    (void)hipEventRecord(e1, b->stream);
+    (void)hipEventRecord(e1, s);
     t->ev.push_back(e1);
 }
 
@@ -746,7 +746,7 @@ int vh_batch_cohort_hist(vh_batch *b, uint64_t *hist) {
 
 const char *vh_batch_kernel_names(void) {
     return "mask_stats;gather;sort;mean;classify;cohort;kmeans;snr;border;n4_init;n4_den;n4_hist;"
-           "n4_fit;n4_contract;n4_eval;n4_welford;n4_pcw;n4_pcg;n4_final;n4_study;ci_walk";
+           "n4_fit;n4_contract;n4_eval;n4_welford;n4_pcw;n4_pcg;n4_final;n4_study;ci_walk;vdp_chain";
 }
 
 int vh_batch_reset_timers(vh_batch *b) {

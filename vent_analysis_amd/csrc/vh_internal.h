@@ -302,7 +302,9 @@ struct ScopedKTimer {
     KTimer *t;
     hipEvent_t e1 = nullptr;
     unsigned long long *ks = nullptr;
-    ScopedKTimer(vh_batch *bb, const char *name, double bytes, bool stamped = false);
+    hipStream_t s = nullptr;   // the stream the timed launches go to (the batch's by default)
+    ScopedKTimer(vh_batch *bb, const char *name, double bytes, bool stamped = false,
+                 hipStream_t on = nullptr);
     ~ScopedKTimer();
     unsigned long long *stamp() const { return ks; }   // null unless stamped and profiling
 };
