@@ -357,7 +357,8 @@ __global__ void __launch_bounds__(VH_TPB) k_gather(const float *__restrict__ n4,
 #define VS_TPB 1024
 #define VS_WAVES (VS_TPB / 64)
 #ifndef VS_KPT
-#define VS_KPT 16   // keys per lane per chunk (8: 0.51 ms per bench step, 16: 0.47, r4c)
+#define VS_KPT 12   // keys per lane per chunk (8: 0.51 ms per bench step, 16: 0.47, r4c; with the LDS lane-set
+                    // ranking 12: 0.320-0.322 against 16: 0.331-0.335 ms and no VGPR spills, r6an)
 #endif
 #define VS_CHUNK (VS_TPB * VS_KPT)
 
