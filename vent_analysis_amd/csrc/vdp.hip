@@ -580,31 +580,35 @@ __global__ void __launch_bounds__(VS_TPB) k_sort_vol(uint32_t *__restrict__ k0,
 
 // ---------------------------------------------------------------------------------------------
 // The same stable LSD sort over the whole GPU for ONE large volume (config 5: ~28 M keys, where the
-// one-workgroup sort took 118 ms).  Per 8-bit pass: k_sortg_count (one workgroup per VS_CHUNK-key chunk:
+// one-workgroup sort took 118 ms).  Per 8-bit pass: k_sortg_count (one workgroup per VSG_CHUNK-key chunk:
 // the chunk's digit counts), k_sortg_offsets (one workgroup: per digit, the exclusive prefix over
 // chunks in chunk order plus the digit's base), k_sortg_scatter (one workgroup per chunk: the
 // chunk ranked exactly as k_sort_vol ranks it, written at its chunk's digit offsets).  Chunk c of
-// every pass holds keys [VS_CHUNK c, VS_CHUNK (c + 1)), so the order of equal digits is the input order:
+// every pass holds keys [VSG_CHUNK c, VSG_CHUNK (c + 1)), so the order of equal digits is the input order:
 // stable, and the result is the same array k_sort_vol produces.
 // ---------------------------------------------------------------------------------------------
+// the grid sort keeps 16 keys per lane per chunk: with k_sort_vol's 12 its per-digit chunk offsets
+// (k_sortg_offsets, one workgroup, serial over the chunks) took config 5's sort 1.18 -> 1.38 ms (r6ao)
+#define VSG_KPT 16
+#define VSG_CHUNK (VS_TPB * VSG_KPT)
 __global__ void __launch_bounds__(VS_TPB) k_sortg_count(const uint32_t *__restrict__ kin,
                                                        const VolScalars *sc, int64_t b, int shift,
                                                        uint32_t *cnt) {
     __shared__ uint32_t s_c[256];
     const int64_t n = sc[b].n_mask;
-    const int64_t c0 = (int64_t)blockIdx.x * VS_CHUNK;
+    const int64_t c0 = (int64_t)blockIdx.x * VSG_CHUNK;
     if (n <= 1 || c0 >= n) return;
     const int t = threadIdx.x;
     if (t < 256) s_c[t] = 0u;
     __syncthreads();
-    uint32_t kr[VS_KPT];
+    uint32_t kr[VSG_KPT];
 #pragma unroll
-    for (int r = 0; r < VS_KPT; ++r) {
+    for (int r = 0; r < VSG_KPT; ++r) {
         const int64_t i = c0 + (int64_t)r * VS_TPB + t;
         kr[r] = i < n ? kin[i] : 0u;
     }
 #pragma unroll
-    for (int r = 0; r < VS_KPT; ++r)
+    for (int r = 0; r < VSG_KPT; ++r)
         if (c0 + (int64_t)r * VS_TPB + t < n) atomicAdd(&s_c[(kr[r] >> shift) & 255u], 1u);
     __syncthreads();
     if (t < 256) cnt[(int64_t)blockIdx.x * 256 + t] = s_c[t];
@@ -617,7 +621,7 @@ __global__ void __launch_bounds__(VS_TPB) k_sortg_offsets(uint32_t *cnt, const V
     __shared__ uint32_t s_base[256];
     const int64_t n = sc[b].n_mask;
     if (n <= 1) return;
-    const int64_t nch = (n + VS_CHUNK - 1) / VS_CHUNK;
+    const int64_t nch = (n + VSG_CHUNK - 1) / VSG_CHUNK;
     const int t = threadIdx.x, d = t & 255, q = t >> 8;
     const int64_t per = (nch + 3) / 4, lo = min(nch, q * per), hi = min(nch, lo + per);
     uint32_t sum = 0;
@@ -649,10 +653,10 @@ __global__ void __launch_bounds__(VS_TPB) k_sortg_scatter(const uint32_t *__rest
                                                          int64_t b, int shift) {
     __shared__ uint32_t s_wc[VS_WAVES][256];
     __shared__ uint32_t s_tot[256], s_cst[256], s_wsum[4], s_off[256];
-    __shared__ uint32_t s_stage[VS_CHUNK];
+    __shared__ uint32_t s_stage[VSG_CHUNK];
     VS_MATCH_DECL;
     const int64_t n = sc[b].n_mask;
-    const int64_t c0 = (int64_t)blockIdx.x * VS_CHUNK;
+    const int64_t c0 = (int64_t)blockIdx.x * VSG_CHUNK;
     if (n <= 1 || c0 >= n) return;
     const int t = threadIdx.x, w = t >> 6, lane = t & 63;
     const uint64_t lt = (1ull << lane) - 1ull;
@@ -660,15 +664,15 @@ __global__ void __launch_bounds__(VS_TPB) k_sortg_scatter(const uint32_t *__rest
     if (t < 256) s_off[t] = off[(int64_t)blockIdx.x * 256 + t];
     VS_MATCH_INIT;
     __syncthreads();
-    uint32_t key[VS_KPT], rank[VS_KPT];
+    uint32_t key[VSG_KPT], rank[VSG_KPT];
 #pragma unroll
-    for (int r = 0; r < VS_KPT; ++r) {
-        const int64_t idx = c0 + (int64_t)w * (VS_KPT * 64) + r * 64 + lane;
+    for (int r = 0; r < VSG_KPT; ++r) {
+        const int64_t idx = c0 + (int64_t)w * (VSG_KPT * 64) + r * 64 + lane;
         key[r] = idx < n ? kin[idx] : 0u;
     }
 #pragma unroll
-    for (int r = 0; r < VS_KPT; ++r) {   // as k_sort_vol: wave w owns keys [c0 + 64 VS_KPT w, c0 + 64 VS_KPT (w + 1))
-        const int64_t idx = c0 + (int64_t)w * (VS_KPT * 64) + r * 64 + lane;
+    for (int r = 0; r < VSG_KPT; ++r) {   // as k_sort_vol: wave w owns keys [c0 + 64 VSG_KPT w, c0 + 64 VSG_KPT (w + 1))
+        const int64_t idx = c0 + (int64_t)w * (VSG_KPT * 64) + r * 64 + lane;
         const bool valid = idx < n;
         const uint32_t kk = key[r];
         const uint32_t d = (kk >> shift) & 255u;
@@ -706,13 +710,13 @@ __global__ void __launch_bounds__(VS_TPB) k_sortg_scatter(const uint32_t *__rest
     }
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < VS_KPT; ++r) {
+    for (int r = 0; r < VSG_KPT; ++r) {
         if (rank[r] == 0xffffffffu) continue;
         const uint32_t d = (key[r] >> shift) & 255u;
         s_stage[s_cst[d] + s_wc[w][d] + rank[r]] = key[r];
     }
     __syncthreads();
-    const int cn = (int)(n - c0 < VS_CHUNK ? n - c0 : VS_CHUNK);
+    const int cn = (int)(n - c0 < VSG_CHUNK ? n - c0 : VSG_CHUNK);
     for (int q = t; q < cn; q += VS_TPB) {
         const uint32_t kk = s_stage[q];
         const uint32_t d = (kk >> shift) & 255u;
@@ -2321,7 +2325,7 @@ void vh_launch_vdp_chain(vh_batch *b, const float *d_n4, const vh_run_opts &o) {
     {
         ScopedKTimer tm(b, "sort", 0.0);
         if (b->nb == 1 && b->V >= ((int64_t)1 << 20)) {   // one large volume: the grid sort
-            const int64_t nchunk = (b->V + VS_CHUNK - 1) / VS_CHUNK;
+            const int64_t nchunk = (b->V + VSG_CHUNK - 1) / VSG_CHUNK;
             if (b->sortg_cap < nchunk * 256) {
                 if (b->d_sortg) HIP_TRY(hipFree(b->d_sortg));
                 b->d_sortg = nullptr;
